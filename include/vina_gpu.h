@@ -1,0 +1,115 @@
+/* vina_gpu.h — C-ABI of the MI355X-native VINA-SLAM per-scan LIO hot path.
+ *
+ * The reference (SheepYang666/VINA-SLAM) has no plugin/FFI layer: its hot path
+ * is a plain C++ API called from the odometry thread. Each entry point below
+ * replaces one of those calls (reference file:line cited); a C++ caller shaped
+ * like src/pipeline/local_mapping.cpp binds them directly.
+ *
+ * Conventions
+ *  - Every function returns int: 0 = ok, < 0 = error (VG_E_*); vg_last_error()
+ *    gives text. Nothing calls exit() (the reference does: octree.cpp:407,
+ *    optimizers.cpp:70).
+ *  - Pointers without a _dev suffix are caller-owned HOST buffers; *_dev entry
+ *    points take device pointers already resident in HBM.
+ *  - Calls are synchronous with respect to the host unless stated; work inside
+ *    is ordered on the context's HIP stream.
+ *  - State vector (250 doubles), the reference's IMUST (types.hpp:43-113):
+ *      [0] t, [1..9] R row-major, [10..12] p, [13..15] v, [16..18] bg,
+ *      [19..21] ba, [22..24] g, [25..249] cov 15x15 row-major.
+ *  - IMU samples: m rows of 7 doubles [t, gx, gy, gz, ax, ay, az]
+ *    (sensor_msgs::Imu subset, m/s^2 and rad/s).
+ */
+#ifndef VINA_GPU_H
+#define VINA_GPU_H
+#include <stdint.h>
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VG_OK 0
+#define VG_E_ARG (-1)
+#define VG_E_HIP (-2)
+#define VG_E_CAPACITY (-3)
+#define VG_E_RANGE (-4)
+#define VG_E_STATE (-5)
+
+#define VG_STATE_LEN 250
+
+/* Hot-path parameters: the reference's ROS 2 keys (node.cpp:52-291). */
+typedef struct vg_config {
+  double voxel_size;                /* Odometry.voxel_size (node.cpp:192) */
+  double down_size;                 /* Odometry.down_size (node.cpp:183) */
+  double min_eigen_value;           /* Odometry.min_eigen_value (node.cpp:198) */
+  double plane_eigen_value_thre[4]; /* LocalBA.plane_eigen_value_thre as written in YAML; inverted internally (node.cpp:256-259) */
+  double min_point[4];              /* {20,20,15,10} (node.cpp:219) */
+  double dept_err, beam_err;        /* Odometry.dept_err / beam_err (node.cpp:186-190) */
+  double imu_coef;                  /* LocalBA.imu_coef (node.cpp:247) */
+  double ba_cov_gyr, ba_cov_acc, ba_rdw_gyr, ba_rdw_acc;     /* LocalBA.* -> noiseMeas/noiseWalk (node.cpp:262-265) */
+  double odo_cov_gyr, odo_cov_acc, odo_rdw_gyr, odo_rdw_acc; /* Odometry.* -> IMUEKF (node.cpp:211-214) */
+  double ext_R[9], ext_t[3];        /* General.extrinsic_rota / extrinsic_tran (node.cpp:78-82, 217-218) */
+  int max_layer;                    /* LocalBA.max_layer */
+  int max_points;                   /* octree.cpp:70 (100) */
+  int win_size;                     /* LocalBA.win_size */
+  int thread_num;                   /* LocalBA.thread_num: only its semantic quirks (voxel_map.cpp:96-97, local_mapping.cpp:27,93) */
+  int if_BA;                        /* General.if_BA (default 0, node.cpp:96) */
+  int reserved0, reserved1, reserved2;
+} vg_config;
+
+/* Capacities of the device-resident map (HBM). Zero fields take defaults. */
+typedef struct vg_capacity {
+  int max_points_per_scan;   /* raw points per scan (default 2,000,000) */
+  int max_nodes;             /* octree nodes (default 4,000,000) */
+  int max_fix_points;        /* point_fix arena, points (default 16,000,000) */
+  int hash_log2;             /* root voxel hash slots = 2^hash_log2 (default 23) */
+} vg_capacity;
+
+/* Per-scan counters (SURVEY §8(d) byte model inputs). */
+typedef struct vg_stats {
+  int n_raw, n_ds, iekf_iters, iekf_matches[4];
+  int roots_new, n_slide, n_factors, ba_iters, degenerate;
+  int nodes_used, fix_used, pad0, pad1;
+} vg_stats;
+
+typedef struct vg_ctx vg_ctx;
+
+/* Context lifecycle. Replaces the VINA_SLAM members surf_map, surf_map_slide,
+ * sws, x_buf, pvec_buf, imu_pre_buf (node.hpp:34-70). device = HIP ordinal. */
+int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx** out);
+int vg_destroy(vg_ctx* ctx);
+const char* vg_last_error(const vg_ctx* ctx);
+/* Drop the map and window; replaces VINA_SLAM::system_reset (node.cpp:368-408). */
+int vg_reset(vg_ctx* ctx);
+
+/* A1 — down_sampling_voxel (include/vina_slam/core/point_utils.hpp:7-44).
+ * xyz: n x 3 floats (AoS), intensity: n floats (may be NULL).
+ * out_xyzic: n x 5 floats [x, y, z, intensity(first point), count] in
+ * ascending voxel-key order (the reference emits unordered_map order; the SET
+ * is identical, bit-for-bit). Returns the voxel count in *n_out. */
+int vg_downsample(vg_ctx* ctx, const float* xyz, const float* intensity, int n, double voxel_size,
+                  float* out_xyzic, int* n_out);
+
+/* Per-scan pipeline — the steady-state branch of
+ * VINA_SLAM::thd_odometry_localmapping (local_mapping.cpp:389-547):
+ * IMU propagation (imu_ekf.cpp:28-94) -> downsample (+ /2 fallback) ->
+ * var_init -> IEKF (odometry.cpp:64-255) -> pvec_update -> cut_voxel_multi ->
+ * multi_recut + tras_opt -> [win full] LI_BA damping_iter -> multi_margi -> slide.
+ * vg_seed sets x_curr (the output of initialisation). */
+int vg_seed(vg_ctx* ctx, const double* state);
+int vg_step(vg_ctx* ctx, const float* xyz, const float* intensity, int n, double pcl_beg_time,
+            double pcl_end_time, const double* imu, int m);
+/* Same, with the scan already in HBM as SoA x/y/z/intensity device arrays. */
+int vg_step_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, const float* d_intensity, int n,
+                double pcl_beg_time, double pcl_end_time, const double* imu, int m);
+int vg_get_state(vg_ctx* ctx, double* state);
+int vg_get_stats(vg_ctx* ctx, vg_stats* out);
+/* Window states x_buf (win_count x 250 doubles); returns win_count via *n. */
+int vg_window_states(vg_ctx* ctx, double* out, int* n);
+
+/* HIP stream the context enqueues on (hipStream_t as void*). */
+void* vg_stream(vg_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VINA_GPU_H */

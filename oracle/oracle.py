@@ -1,0 +1,160 @@
+"""ORACLE — test infrastructure only.
+
+ctypes binding of the CPU restatement (liboracle.so). Importable only from
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg; the product
+path (vina-slam_amd/) never imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+STATE_LEN = 250
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("n_raw", ctypes.c_int), ("n_ds", ctypes.c_int), ("iekf_iters", ctypes.c_int),
+                ("iekf_matches", ctypes.c_int * 4), ("roots_new", ctypes.c_int), ("n_slide", ctypes.c_int),
+                ("n_factors", ctypes.c_int), ("ba_iters", ctypes.c_int), ("degenerate", ctypes.c_int)]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        P = ctypes.c_void_p
+        dp = ctypes.POINTER(ctypes.c_double)
+        fp = ctypes.POINTER(ctypes.c_float)
+        ip = ctypes.POINTER(ctypes.c_int)
+        lp = ctypes.POINTER(ctypes.c_int64)
+        L.orc_voxel_key_d.argtypes = [dp, ctypes.c_int, ctypes.c_double, lp]
+        L.orc_voxel_hash.argtypes = [ctypes.c_int64] * 3
+        L.orc_voxel_hash.restype = ctypes.c_size_t
+        L.orc_downsample.argtypes = [fp, fp, ctypes.c_int, ctypes.c_double, fp, ip]
+        L.orc_calc_body_var.argtypes = [dp, ctypes.c_double, ctypes.c_double, dp, dp]
+        L.orc_eig3.argtypes = [dp, dp, dp]
+        L.orc_inverse15.argtypes = [dp, dp]
+        L.orc_ldlt_solve.argtypes = [dp, dp, ctypes.c_int, dp]
+        L.orc_so3.argtypes = [dp, dp, dp, dp, dp]
+        L.orc_create.argtypes = [P]
+        L.orc_create.restype = P
+        L.orc_destroy.argtypes = [P]
+        L.orc_seed.argtypes = [P, dp]
+        L.orc_get_state.argtypes = [P, dp]
+        L.orc_step.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int, dp]
+        L.orc_get_stats.argtypes = [P, ctypes.POINTER(Stats)]
+        L.orc_traj_len.argtypes = [P]
+        L.orc_get_traj.argtypes = [P, dp]
+        L.orc_window_states.argtypes = [P, dp]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _f(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def voxel_keys(xyz, size):
+    xyz = np.ascontiguousarray(xyz, dtype=np.float64)
+    out = np.zeros((xyz.shape[0], 3), dtype=np.int64)
+    lib().orc_voxel_key_d(_d(xyz), xyz.shape[0], size, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+    return out
+
+
+def downsample(xyz, inten, size):
+    """Reference down_sampling_voxel; returns (n,5) [x,y,z,intensity,count] in unordered_map order."""
+    xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+    inten = np.ascontiguousarray(inten, dtype=np.float32)
+    out = np.zeros((xyz.shape[0], 5), dtype=np.float32)
+    n = ctypes.c_int(0)
+    lib().orc_downsample(_f(xyz), _f(inten), xyz.shape[0], size, _f(out), ctypes.byref(n))
+    return out[: n.value]
+
+
+def eig3(A):
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    w = np.zeros(3)
+    V = np.zeros((3, 3))
+    lib().orc_eig3(_d(A), _d(w), _d(V))
+    return w, V
+
+
+def inverse15(A):
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    o = np.zeros((15, 15))
+    lib().orc_inverse15(_d(A), _d(o))
+    return o
+
+
+def ldlt_solve(A, b):
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(b.shape[0])
+    lib().orc_ldlt_solve(_d(A), _d(b), b.shape[0], _d(x))
+    return x
+
+
+class Pipeline:
+    """The reference's per-scan steady-state loop (CPU restatement)."""
+
+    def __init__(self, cconfig):
+        self._cfg = cconfig
+        self.h = lib().orc_create(ctypes.byref(cconfig))
+
+    def close(self):
+        if self.h:
+            lib().orc_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def seed(self, state):
+        s = np.ascontiguousarray(state, dtype=np.float64)
+        lib().orc_seed(self.h, _d(s))
+
+    def step(self, xyz, inten, beg, end, imu):
+        xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+        inten = np.ascontiguousarray(inten, dtype=np.float32)
+        imu = np.ascontiguousarray(imu, dtype=np.float64).reshape(-1, 7)
+        timing = np.zeros(8)
+        r = lib().orc_step(self.h, _f(xyz), _f(inten), xyz.shape[0], beg, end, _d(imu), imu.shape[0], _d(timing))
+        if r != 0:
+            raise RuntimeError("orc_step failed: %d" % r)
+        return timing
+
+    def state(self):
+        s = np.zeros(STATE_LEN)
+        lib().orc_get_state(self.h, _d(s))
+        return s
+
+    def stats(self):
+        s = Stats()
+        lib().orc_get_stats(self.h, ctypes.byref(s))
+        return {k: (list(getattr(s, k)) if k == "iekf_matches" else getattr(s, k)) for k, _ in Stats._fields_}
+
+    def trajectory(self):
+        n = lib().orc_traj_len(self.h)
+        out = np.zeros((n, 13))
+        lib().orc_get_traj(self.h, _d(out))
+        return out
+
+    def window_states(self):
+        out = np.zeros((64, STATE_LEN))
+        n = lib().orc_window_states(self.h, _d(out))
+        return out[:n]

@@ -1,0 +1,64 @@
+/* ORACLE — test infrastructure only. C API of the CPU restatement of the
+ * VINA-SLAM per-scan hot path, loaded by tests/ (ctypes), smoke() and the
+ * bench.py cpu_baseline leg. The product library never includes this file.
+ *
+ * State vector layout used by orc_seed/orc_get_state (250 doubles):
+ *   [0] t, [1..9] R row-major, [10..12] p, [13..15] v, [16..18] bg,
+ *   [19..21] ba, [22..24] g, [25..249] cov 15x15 row-major
+ * (the reference's IMUST, include/vina_slam/core/types.hpp:43-113). */
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_config {
+  double voxel_size;              /* Odometry.voxel_size        node.cpp:192 */
+  double down_size;               /* Odometry.down_size         node.cpp:183 */
+  double min_eigen_value;         /* Odometry.min_eigen_value   node.cpp:198 */
+  double plane_eigen_value_thre[4]; /* LocalBA.plane_eigen_value_thre, as in YAML (inverted internally) */
+  double min_point[4];            /* hard-coded {20,20,15,10}   node.cpp:219 */
+  double dept_err, beam_err;      /* Odometry.dept_err/beam_err node.cpp:186-190 */
+  double imu_coef;                /* LocalBA.imu_coef           node.cpp:247 */
+  double ba_cov_gyr, ba_cov_acc, ba_rdw_gyr, ba_rdw_acc; /* LocalBA.* node.cpp:228-238 */
+  double odo_cov_gyr, odo_cov_acc, odo_rdw_gyr, odo_rdw_acc; /* Odometry.* node.cpp:171-181 */
+  double ext_R[9], ext_t[3];      /* General.extrinsic_rota/tran node.cpp:78-82 */
+  int max_layer;                  /* LocalBA.max_layer */
+  int max_points;                 /* octree.cpp:70 (100) */
+  int win_size;                   /* LocalBA.win_size */
+  int thread_num;                 /* LocalBA.thread_num (semantic: partition/quirks) */
+  int if_BA;                      /* General.if_BA (default 0) */
+  int use_threads;                /* oracle only: spawn real std::threads */
+  int vnc_prep;                   /* oracle only: run the dead VNC prep (cost fidelity) */
+  int pad;
+} orc_config;
+
+typedef struct orc_stats {
+  int n_raw, n_ds, iekf_iters, iekf_matches[4];
+  int roots_new, n_slide, n_factors, ba_iters, degenerate;
+} orc_stats;
+
+void orc_voxel_key_d(const double* xyz, int n, double size, int64_t* out);
+size_t orc_voxel_hash(int64_t x, int64_t y, int64_t z);
+int orc_downsample(const float* xyz, const float* inten, int n, double size, float* out_xyzic, int* n_out);
+void orc_calc_body_var(const double* p, double range_inc, double degree_inc, double* pnt_out, double* var_out);
+void orc_eig3(const double* A, double* w, double* V);
+void orc_inverse15(const double* A, double* out);
+void orc_ldlt_solve(const double* A, const double* b, int n, double* x);
+void orc_so3(const double* w, double* R_out, double* log_out, double* jr_out, double* jrinv_out);
+
+void* orc_create(const orc_config* c);
+void orc_destroy(void* h);
+void orc_seed(void* h, const double* state);
+void orc_get_state(void* h, double* state);
+int orc_step(void* h, const float* xyz, const float* inten, int n, double beg, double end, const double* imu, int m,
+             double* timing);
+void orc_get_stats(void* h, orc_stats* s);
+int orc_traj_len(void* h);
+void orc_get_traj(void* h, double* out);
+int orc_window_states(void* h, double* out);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,73 @@
+"""A1 parity: the HIP downsample (vg_downsample) against the oracle's
+down_sampling_voxel (point_utils.hpp:7-44). Bit-exact as a set: keys, float
+means, first-point intensity, counts."""
+import numpy as np
+import pytest
+
+import oracle
+import synth
+import vgconfig
+import vgpu
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = vgpu.Context(vgconfig.to_c(vgconfig.load("mid360")), max_points=400_000)
+    yield c
+    c.close()
+
+
+def _canon(a):
+    a = np.asarray(a, dtype=np.float32)
+    order = np.lexsort(tuple(a[:, j] for j in range(4, -1, -1)))
+    return a[order]
+
+
+def _check(ctx, xyz, inten, size):
+    g = ctx.downsample(xyz, inten, size)
+    o = oracle.downsample(xyz, inten, size)
+    assert g.shape == o.shape
+    # GPU emits ascending key order; compare as sets, bit for bit
+    assert np.array_equal(_canon(g).view(np.uint32), _canon(o).view(np.uint32))
+    return g
+
+
+@pytest.mark.parametrize("lidar,size", [("tiny", 0.1), ("64line", 0.1), ("64line", 0.05), ("128line", 0.1)])
+def test_downsample_synthetic_bit_exact(ctx, oracle_lib, lidar, size):
+    seq = synth.Sequence(lidar, seq_id=3, blind=1.0)
+    xyz, inten, _, _ = seq.scan(5)
+    g = _check(ctx, xyz, inten, size)
+    assert g.shape[0] > 1000
+
+
+def test_downsample_edge_cases(ctx, oracle_lib):
+    rng = np.random.default_rng(5)
+    # exact negative multiples, zeros, duplicates, huge clusters in one voxel
+    xyz = np.array([[-0.5, -0.5, -0.5], [0, 0, 0], [0, 0, 0], [-0.1, 0.1, -1e-9], [0.1, -0.1, 1e-9]], np.float32)
+    _check(ctx, xyz, np.arange(5, dtype=np.float32), 0.1)
+    blob = (rng.normal(0, 0.01, (5000, 3)) + 3.05).astype(np.float32)
+    g = _check(ctx, blob, np.zeros(5000, np.float32), 0.1)
+    assert g[:, 4].sum() == 5000
+    one = np.array([[1.0, 2.0, 3.0]], np.float32)
+    _check(ctx, one, np.ones(1, np.float32), 0.1)
+
+
+def test_downsample_empty_and_noop(ctx):
+    assert ctx.downsample(np.zeros((0, 3), np.float32), np.zeros(0, np.float32), 0.1).shape[0] == 0
+    xyz = np.ones((4, 3), np.float32)
+    assert ctx.downsample(xyz, np.zeros(4, np.float32), 0.0005).shape[0] == 4
+
+
+def test_downsample_range_error(ctx):
+    xyz = np.array([[1e6, 0, 0]], np.float32)  # key 1e7 > 2^20: reported, not wrapped
+    with pytest.raises(vgpu.VgError):
+        ctx.downsample(xyz, np.zeros(1, np.float32), 0.1)
+
+
+def test_downsample_golden(ctx):
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "downsample_tiny.npz"))
+    g = ctx.downsample(d["xyz"], d["inten"], float(d["size"]))
+    assert np.array_equal(_canon(g).view(np.uint32), _canon(d["out"]).view(np.uint32))

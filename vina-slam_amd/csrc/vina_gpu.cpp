@@ -1,0 +1,178 @@
+// vina_gpu.cpp — C-ABI entry points (include/vina_gpu.h) and context lifecycle.
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include "vg_internal.h"
+
+using namespace vg;
+
+static void fill_capacity(vg_capacity& c) {
+  if (c.max_points_per_scan <= 0) c.max_points_per_scan = 2000000;
+  if (c.max_nodes <= 0) c.max_nodes = 4000000;
+  if (c.max_fix_points <= 0) c.max_fix_points = 16000000;
+  if (c.hash_log2 <= 0) c.hash_log2 = 23;
+}
+
+extern "C" {
+
+int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx** out) {
+  if (!cfg || !out) return VG_E_ARG;
+  *out = nullptr;
+  vg_ctx* ctx = new (std::nothrow) vg_ctx();
+  if (!ctx) return VG_E_CAPACITY;
+  ctx->cfg = *cfg;
+  memset(&ctx->cap, 0, sizeof(ctx->cap));
+  if (cap) ctx->cap = *cap;
+  fill_capacity(ctx->cap);
+  ctx->device = device;
+  memset(&ctx->stats, 0, sizeof(ctx->stats));
+  auto fail = [&](int code) {
+    fprintf(stderr, "vg_create: %s\n", ctx->err.c_str());
+    vg_destroy(ctx);
+    return code;
+  };
+  if (cfg->win_size <= 0 || cfg->win_size > 32 || cfg->max_layer < 0 || cfg->max_layer > 3 ||
+      cfg->voxel_size <= 0) {
+    ctx->err = "invalid config (win_size in [1,32], max_layer in [0,3], voxel_size > 0)";
+    return fail(VG_E_ARG);
+  }
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    ctx->err = std::string("hipSetDevice: ") + hipGetErrorString(e);
+    return fail(VG_E_HIP);
+  }
+  if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) {
+    ctx->err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
+    return fail(VG_E_HIP);
+  }
+  if ((e = hipHostMalloc((void**)&ctx->h_pinned, 4096, hipHostMallocDefault)) != hipSuccess) {
+    ctx->err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
+    return fail(VG_E_HIP);
+  }
+  const size_t n = (size_t)ctx->cap.max_points_per_scan;
+  size_t need = n * 120 + (64ull << 20);
+  if ((e = hipMalloc((void**)&ctx->arena.base, need)) != hipSuccess) {
+    ctx->err = std::string("hipMalloc arena: ") + hipGetErrorString(e);
+    return fail(VG_E_HIP);
+  }
+  ctx->arena.size = need;
+  ctx->d_x = ctx->arena.take<float>(n);
+  ctx->d_y = ctx->arena.take<float>(n);
+  ctx->d_z = ctx->arena.take<float>(n);
+  ctx->d_i = ctx->arena.take<float>(n);
+  int r = ds_alloc(ctx);
+  if (r != VG_OK) return fail(r);
+  *out = ctx;
+  return VG_OK;
+}
+
+int vg_destroy(vg_ctx* ctx) {
+  if (!ctx) return VG_OK;
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->arena.base) (void)hipFree(ctx->arena.base);
+  if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return VG_OK;
+}
+
+const char* vg_last_error(const vg_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void* vg_stream(vg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int vg_reset(vg_ctx* ctx) {
+  if (!ctx) return VG_E_ARG;
+  return VG_OK;
+}
+
+static int upload_aos(vg_ctx* ctx, const float* xyz, const float* inten, int n) {
+  std::vector<float> soa((size_t)n * 4);
+  for (int i = 0; i < n; i++) {
+    soa[i] = xyz[3 * i];
+    soa[(size_t)n + i] = xyz[3 * i + 1];
+    soa[2 * (size_t)n + i] = xyz[3 * i + 2];
+    soa[3 * (size_t)n + i] = inten ? inten[i] : 0.0f;
+  }
+  hipStream_t s = ctx->stream;
+  VG_HIP(hipMemcpyAsync(ctx->d_x, soa.data(), n * sizeof(float), hipMemcpyHostToDevice, s));
+  VG_HIP(hipMemcpyAsync(ctx->d_y, soa.data() + n, n * sizeof(float), hipMemcpyHostToDevice, s));
+  VG_HIP(hipMemcpyAsync(ctx->d_z, soa.data() + 2 * (size_t)n, n * sizeof(float), hipMemcpyHostToDevice, s));
+  VG_HIP(hipMemcpyAsync(ctx->d_i, soa.data() + 3 * (size_t)n, n * sizeof(float), hipMemcpyHostToDevice, s));
+  VG_HIP(hipStreamSynchronize(s));
+  return VG_OK;
+}
+
+int vg_downsample(vg_ctx* ctx, const float* xyz, const float* intensity, int n, double voxel_size,
+                  float* out_xyzic, int* n_out) {
+  if (!ctx || (!xyz && n > 0) || !out_xyzic || !n_out || n < 0) return VG_E_ARG;
+  if (n > ctx->cap.max_points_per_scan) {
+    ctx->err = "scan larger than max_points_per_scan";
+    return VG_E_CAPACITY;
+  }
+  *n_out = 0;
+  if (voxel_size < 0.001) {  // point_utils.hpp:9-10: no-op
+    for (int i = 0; i < n; i++) {
+      out_xyzic[5 * i] = xyz[3 * i];
+      out_xyzic[5 * i + 1] = xyz[3 * i + 1];
+      out_xyzic[5 * i + 2] = xyz[3 * i + 2];
+      out_xyzic[5 * i + 3] = intensity ? intensity[i] : 0.0f;
+      out_xyzic[5 * i + 4] = 0.0f;
+    }
+    *n_out = n;
+    return VG_OK;
+  }
+  if (n == 0) return VG_OK;
+  VG_TRY(upload_aos(ctx, xyz, intensity, n));
+  int m = 0;
+  VG_TRY(ds_run(ctx, ctx->d_x, ctx->d_y, ctx->d_z, ctx->d_i, n, voxel_size, &m));
+  std::vector<float> buf((size_t)m * 5);
+  hipStream_t s = ctx->stream;
+  const DownsampleBufs& d = ctx->ds;
+  float* cols[5] = {d.ox, d.oy, d.oz, d.oi, d.oc};
+  for (int c = 0; c < 5; c++)
+    VG_HIP(hipMemcpyAsync(buf.data() + (size_t)c * m, cols[c], m * sizeof(float), hipMemcpyDeviceToHost, s));
+  VG_HIP(hipStreamSynchronize(s));
+  for (int v = 0; v < m; v++)
+    for (int c = 0; c < 5; c++) out_xyzic[5 * v + c] = buf[(size_t)c * m + v];
+  *n_out = m;
+  return VG_OK;
+}
+
+int vg_seed(vg_ctx* ctx, const double* state) {
+  if (!ctx || !state) return VG_E_ARG;
+  ctx->err = "vg_seed: not implemented yet";
+  return VG_E_STATE;
+}
+
+int vg_step(vg_ctx* ctx, const float*, const float*, int, double, double, const double*, int) {
+  if (!ctx) return VG_E_ARG;
+  ctx->err = "vg_step: not implemented yet";
+  return VG_E_STATE;
+}
+
+int vg_step_dev(vg_ctx* ctx, const float*, const float*, const float*, const float*, int, double, double,
+                const double*, int) {
+  if (!ctx) return VG_E_ARG;
+  ctx->err = "vg_step_dev: not implemented yet";
+  return VG_E_STATE;
+}
+
+int vg_get_state(vg_ctx* ctx, double*) {
+  if (!ctx) return VG_E_ARG;
+  ctx->err = "vg_get_state: not implemented yet";
+  return VG_E_STATE;
+}
+
+int vg_get_stats(vg_ctx* ctx, vg_stats* out) {
+  if (!ctx || !out) return VG_E_ARG;
+  *out = ctx->stats;
+  return VG_OK;
+}
+
+int vg_window_states(vg_ctx* ctx, double*, int* n) {
+  if (!ctx || !n) return VG_E_ARG;
+  *n = 0;
+  return VG_OK;
+}
+
+}  // extern "C"

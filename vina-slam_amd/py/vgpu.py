@@ -1,0 +1,157 @@
+"""ctypes binding of the product C-ABI (include/vina_gpu.h, lib/libvina_gpu.so).
+
+This is the Python face of the drop-in boundary used by tests/ and bench.py. It
+loads ONLY the in-tree HIP library; there is no CPU fallback — if the library
+or a GPU is missing every call raises.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+
+from vgconfig import CConfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+REPO = os.path.dirname(PKG)
+LIB = os.path.join(PKG, "lib", "libvina_gpu.so")
+HEADER = os.path.join(REPO, "include", "vina_gpu.h")
+STATE_LEN = 250
+
+
+class Capacity(ctypes.Structure):
+    _fields_ = [("max_points_per_scan", ctypes.c_int), ("max_nodes", ctypes.c_int),
+                ("max_fix_points", ctypes.c_int), ("hash_log2", ctypes.c_int)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("n_raw", ctypes.c_int), ("n_ds", ctypes.c_int), ("iekf_iters", ctypes.c_int),
+                ("iekf_matches", ctypes.c_int * 4), ("roots_new", ctypes.c_int), ("n_slide", ctypes.c_int),
+                ("n_factors", ctypes.c_int), ("ba_iters", ctypes.c_int), ("degenerate", ctypes.c_int),
+                ("nodes_used", ctypes.c_int), ("fix_used", ctypes.c_int), ("pad0", ctypes.c_int),
+                ("pad1", ctypes.c_int)]
+
+
+def build(jobs=8):
+    subprocess.check_call(["make", "-s", "-j%d" % jobs, "-C", PKG])
+
+
+def header_symbols():
+    """Every function the C-ABI header declares."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void\*|const char\*)\s+(vg_\w+)\s*\(", txt, re.M)))
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError("libvina_gpu.so not built: run `make -C vina-slam_amd` (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB)
+        P = ctypes.c_void_p
+        dp = ctypes.POINTER(ctypes.c_double)
+        fp = ctypes.POINTER(ctypes.c_float)
+        ip = ctypes.POINTER(ctypes.c_int)
+        L.vg_create.argtypes = [ctypes.POINTER(CConfig), ctypes.POINTER(Capacity), ctypes.c_int, ctypes.POINTER(P)]
+        L.vg_destroy.argtypes = [P]
+        L.vg_last_error.argtypes = [P]
+        L.vg_last_error.restype = ctypes.c_char_p
+        L.vg_reset.argtypes = [P]
+        L.vg_downsample.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, fp, ip]
+        L.vg_seed.argtypes = [P, dp]
+        L.vg_step.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
+        L.vg_step_dev.argtypes = [P, P, P, P, P, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
+        L.vg_get_state.argtypes = [P, dp]
+        L.vg_get_stats.argtypes = [P, ctypes.POINTER(Stats)]
+        L.vg_window_states.argtypes = [P, dp, ip]
+        L.vg_stream.argtypes = [P]
+        L.vg_stream.restype = P
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _f(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+class VgError(RuntimeError):
+    pass
+
+
+class Context:
+    """One device-resident LIO sequence (vg_ctx)."""
+
+    def __init__(self, cconfig, device=0, max_points=2_000_000, max_nodes=0, max_fix_points=0, hash_log2=0):
+        self.h = ctypes.c_void_p()
+        cap = Capacity(max_points, max_nodes, max_fix_points, hash_log2)
+        r = lib().vg_create(ctypes.byref(cconfig), ctypes.byref(cap), device, ctypes.byref(self.h))
+        if r != 0:
+            raise VgError("vg_create failed (%d)" % r)
+
+    def _chk(self, r, what):
+        if r != 0:
+            raise VgError("%s failed (%d): %s" % (what, r, lib().vg_last_error(self.h).decode()))
+
+    def close(self):
+        if self.h:
+            lib().vg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def downsample(self, xyz, inten, size):
+        xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+        inten = np.ascontiguousarray(inten, dtype=np.float32)
+        out = np.zeros((max(xyz.shape[0], 1), 5), dtype=np.float32)
+        n = ctypes.c_int(0)
+        self._chk(lib().vg_downsample(self.h, _f(xyz), _f(inten), xyz.shape[0], size, _f(out), ctypes.byref(n)),
+                  "vg_downsample")
+        return out[: n.value]
+
+    def seed(self, state):
+        s = np.ascontiguousarray(state, dtype=np.float64)
+        self._chk(lib().vg_seed(self.h, _d(s)), "vg_seed")
+
+    def step(self, xyz, inten, beg, end, imu):
+        xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+        inten = np.ascontiguousarray(inten, dtype=np.float32)
+        imu = np.ascontiguousarray(imu, dtype=np.float64).reshape(-1, 7)
+        self._chk(lib().vg_step(self.h, _f(xyz), _f(inten), xyz.shape[0], beg, end, _d(imu), imu.shape[0]),
+                  "vg_step")
+
+    def step_dev(self, dx, dy, dz, di, n, beg, end, imu):
+        imu = np.ascontiguousarray(imu, dtype=np.float64).reshape(-1, 7)
+        self._chk(lib().vg_step_dev(self.h, ctypes.c_void_p(dx), ctypes.c_void_p(dy), ctypes.c_void_p(dz),
+                                    ctypes.c_void_p(di), n, beg, end, _d(imu), imu.shape[0]), "vg_step_dev")
+
+    def state(self):
+        s = np.zeros(STATE_LEN)
+        self._chk(lib().vg_get_state(self.h, _d(s)), "vg_get_state")
+        return s
+
+    def stats(self):
+        s = Stats()
+        self._chk(lib().vg_get_stats(self.h, ctypes.byref(s)), "vg_get_stats")
+        return {k: (list(getattr(s, k)) if k == "iekf_matches" else getattr(s, k)) for k, _ in Stats._fields_}
+
+    def window_states(self):
+        out = np.zeros((64, STATE_LEN))
+        n = ctypes.c_int(0)
+        self._chk(lib().vg_window_states(self.h, _d(out), ctypes.byref(n)), "vg_window_states")
+        return out[: n.value]
+
+    def stream(self):
+        return lib().vg_stream(self.h)
