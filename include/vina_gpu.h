@@ -106,6 +106,11 @@ int vg_get_stats(vg_ctx* ctx, vg_stats* out);
 /* Window states x_buf (win_count x 250 doubles); returns win_count via *n. */
 int vg_window_states(vg_ctx* ctx, double* out, int* n);
 
+/* Per-scan poses published after the IEKF (pub_localtraj / save_pose_tum,
+ * local_mapping.cpp:427-430): n rows of 13 doubles [t, R row-major 9, p 3].
+ * Copies min(n, cap) rows; *n = total rows. out may be NULL to query. */
+int vg_trajectory(vg_ctx* ctx, double* out, int cap, int* n);
+
 /* HIP stream the context enqueues on (hipStream_t as void*). */
 void* vg_stream(vg_ctx* ctx);
 

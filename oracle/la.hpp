@@ -213,6 +213,11 @@ struct MatX {
 inline std::vector<double> ldlt_solve(const MatX& Ain, const std::vector<double>& b) {
   const int n = Ain.n;
   MatX A = Ain;
+  // Eigen::LDLT<MatrixXd> (UpLo = Lower) reads only the lower triangle; the
+  // LiDAR Hessian's diagonal 6x6 blocks are not exactly symmetric
+  // (factors.cpp:90-91 adds -0.5*hat(jjt)), so mirror lower -> upper first.
+  for (int i = 0; i < n; i++)
+    for (int j = i + 1; j < n; j++) A(i, j) = A(j, i);
   std::vector<int> perm(n);
   for (int i = 0; i < n; i++) perm[i] = i;
   // in-place: A becomes L (strict lower) and D (diag)

@@ -1,0 +1,1204 @@
+// map.hip — the device-resident adaptive voxel map and the IEKF hot loop.
+//
+// SURVEY §8(a) rows:
+//   A3  var_init / pvec_update           point_utils.cpp:3-65        (fused)
+//   A4  cut_voxel_multi -> allocate/push voxel_map.cpp:47-135, octree.cpp:151-228
+//   A5  multi_recut -> OctoTree::recut    local_mapping.cpp:144-201, octree.cpp:257-393
+//   A6  tras_opt (factor extraction)      octree.cpp:498-521
+//   A7  match / OctoTree::match / inside  voxel_map.cpp:241-266, octree.cpp:551-595, 732-737
+//   A9  LioStateEstimation point loop     odometry.cpp:111-148
+//   A10 multi_margi -> OctoTree::margi    local_mapping.cpp:17-84, octree.cpp:302-333, 395-495
+//
+// Layout in HBM (vg_internal.h DevMap): a root-voxel open-addressing hash
+// (packed 63-bit key -> node id), a node pool of fixed records (NodeHdr 96 B for
+// descent, PlaneRec 224 B for the gate, clusters/cov_add/eigen as separate
+// arrays), SlideWindow clusters inline per node (W x 80 B), per-physical-slot
+// window point arrays (body pnt, world var, owning leaf) and a point_fix arena.
+// The reference's pointer-chasing recursion becomes level-synchronous
+// worklists; per-leaf accumulation keeps the reference's point order by
+// sorting (leaf, order) keys and walking each leaf's segment sequentially, so
+// sums are deterministic and order-faithful.
+#include <hipcub/hipcub.hpp>
+#include "vg_dev.h"
+
+namespace vg {
+
+// ------------------------------------------------------------------ alloc
+int map_alloc(vg_ctx* ctx) {
+  DevMap& m = ctx->map;
+  const int W = ctx->cfg.win_size;
+  m.W = W;
+  m.cap_nodes = ctx->cap.max_nodes;
+  m.cap_fix = ctx->cap.max_fix_points;
+  m.hash_mask = (1 << ctx->cap.hash_log2) - 1;
+  m.cap_wp = ctx->cap.max_points_per_scan;
+  const size_t cn = m.cap_nodes, hs = (size_t)m.hash_mask + 1, cw = (size_t)m.cap_wp;
+  auto ok = [&](void* p) { return p != nullptr; };
+  bool good = true;
+  good &= ok(m.hdr = ctx->arena.take<NodeHdr>(cn));
+  good &= ok(m.pl = ctx->arena.take<PlaneRec>(cn));
+  good &= ok(m.pcr_add = ctx->arena.take<Clu>(cn));
+  good &= ok(m.pcr_fix = ctx->arena.take<Clu>(cn));
+  good &= ok(m.cov_add = ctx->arena.take<double>(cn * kCovN));
+  good &= ok(m.eig = ctx->arena.take<double>(cn * 12));
+  good &= ok(m.jour = ctx->arena.take<double>(cn));
+  good &= ok(m.pcrs = ctx->arena.take<Clu>(cn * W));
+  good &= ok(m.nscr = ctx->arena.take<int>(cn * 4));
+  good &= ok(m.cfirst = ctx->arena.take<int>(cn * 8));
+  good &= ok(m.hkey = ctx->arena.take<uint64_t>(hs));
+  good &= ok(m.hval = ctx->arena.take<int>(hs));
+  good &= ok(m.hfirst = ctx->arena.take<int>(hs));
+  good &= ok(m.slide = ctx->arena.take<int>(cn));
+  good &= ok(m.in_slide = ctx->arena.take<uint8_t>(cn));
+  good &= ok(m.fix_pnt = ctx->arena.take<double>((size_t)m.cap_fix * 3));
+  good &= ok(m.fix_var = ctx->arena.take<double>((size_t)m.cap_fix * 9));
+  good &= ok(m.wp_pnt = ctx->arena.take<double>(cw * W * 3));
+  good &= ok(m.wp_var = ctx->arena.take<double>(cw * W * 9));
+  good &= ok(m.wp_leaf = ctx->arena.take<int>(cw * W));
+  good &= ok(m.counters = ctx->arena.take<int>(kCntN));
+  Work& w = ctx->wk;
+  w.cap = (int)(cw * (W + 1));
+  good &= ok(w.k0 = ctx->arena.take<uint64_t>(w.cap));
+  good &= ok(w.k1 = ctx->arena.take<uint64_t>(w.cap));
+  good &= ok(w.v0 = ctx->arena.take<uint32_t>(w.cap));
+  good &= ok(w.v1 = ctx->arena.take<uint32_t>(w.cap));
+  good &= ok(w.u0 = ctx->arena.take<uint32_t>(w.cap));
+  good &= ok(w.u1 = ctx->arena.take<uint32_t>(w.cap));
+  good &= ok(w.evsrc = ctx->arena.take<uint32_t>(w.cap));
+  good &= ok(w.ac_cnt = ctx->arena.take<uint32_t>(cn));
+  good &= ok(w.ac_off = ctx->arena.take<uint32_t>(cn));
+  good &= ok(w.cand = ctx->arena.take<int>(cn));
+  good &= ok(w.list0 = ctx->arena.take<int>(cn));
+  good &= ok(w.list1 = ctx->arena.take<int>(cn));
+  good &= ok(w.list2 = ctx->arena.take<int>(cn));
+  good &= ok(w.leaf = ctx->arena.take<int>(cw));
+  good &= ok(w.pw = ctx->arena.take<double>(cw * 3));
+  good &= ok(w.iekf_cache = ctx->arena.take<int>(cw));
+  w.nparts = 1024;
+  good &= ok(w.partials = ctx->arena.take<double>((size_t)w.nparts * 40));
+  if (!good) {
+    ctx->err = "arena exhausted (map)";
+    return VG_E_CAPACITY;
+  }
+  size_t b1 = 0, b2 = 0;
+  VG_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, b1, w.k0, w.k1, w.cap, 0, 64, ctx->stream));
+  VG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, w.v0, w.v1, w.cap, ctx->stream));
+  w.tmp_bytes = (b1 > b2 ? b1 : b2) + 256;
+  w.tmp = ctx->arena.take<char>(w.tmp_bytes);
+  if (!w.tmp) {
+    ctx->err = "arena exhausted (sort workspace)";
+    return VG_E_CAPACITY;
+  }
+  return VG_OK;
+}
+
+int map_reset(vg_ctx* ctx) {
+  DevMap& m = ctx->map;
+  hipStream_t s = ctx->stream;
+  const size_t hs = (size_t)m.hash_mask + 1;
+  VG_HIP(hipMemsetAsync(m.hkey, 0xff, hs * sizeof(uint64_t), s));
+  VG_HIP(hipMemsetAsync(m.hval, 0xff, hs * sizeof(int), s));
+  VG_HIP(hipMemsetAsync(m.hfirst, 0x7f, hs * sizeof(int), s));
+  VG_HIP(hipMemsetAsync(m.counters, 0, kCntN * sizeof(int), s));
+  VG_HIP(hipMemsetAsync(m.in_slide, 0, m.cap_nodes, s));
+  VG_HIP(hipMemsetAsync(m.cfirst, 0x7f, (size_t)m.cap_nodes * 8 * sizeof(int), s));
+  VG_HIP(hipMemsetAsync(m.nscr, 0xff, (size_t)m.cap_nodes * 4 * sizeof(int), s));
+  VG_HIP(hipStreamSynchronize(s));
+  return VG_OK;
+}
+
+// Node records of freshly allocated nodes must be zero: the pool is zeroed
+// lazily per allocation range.
+__global__ void k_zero_nodes(int first, const int* __restrict__ cnt_after, int W, PlaneRec* pl, Clu* pcr_add,
+                             Clu* pcr_fix, double* cov, double* eig, double* jour, Clu* pcrs) {
+  const int last = cnt_after[0];
+  for (int id = first + blockIdx.x * blockDim.x + threadIdx.x; id < last; id += gridDim.x * blockDim.x) {
+    PlaneRec& p = pl[id];
+    for (int j = 0; j < 27; j++) (&p.center[0])[j] = 0.0;
+    p.radius = 0;
+    p.pad = 0;
+    clu_zero(pcr_add[id]);
+    clu_zero(pcr_fix[id]);
+    for (int j = 0; j < kCovN; j++) cov[(size_t)id * kCovN + j] = 0.0;
+    for (int j = 0; j < 12; j++) eig[(size_t)id * 12 + j] = 0.0;
+    jour[id] = 0.0;
+    for (int j = 0; j < W; j++) clu_zero(pcrs[(size_t)id * W + j]);
+  }
+}
+
+// ------------------------------------------------------------------ IEKF
+// One IEKF iteration's point loop (odometry.cpp:111-148): world covariance,
+// association (cached-leaf fast path or root hash + octree descent), the
+// probabilistic point-to-plane gate (octree.cpp:557-579), the Jacobian and the
+// weighted normal-equation accumulation. Each block writes 34 partial sums:
+// HTH (upper 21), HTz (6), nnt (upper 6), match count (1). fp64 throughout.
+__device__ __forceinline__ int descend(const NodeHdr* __restrict__ hdr, int node, const V3& w) {
+  for (int d = 0; d < 8 && node >= 0; d++) {
+    const NodeHdr& h = hdr[node];
+    if (h.octo == 0) return node;
+    node = h.child[octant(w, h.center)];
+  }
+  return -1;
+}
+
+// OctoTree::match at a leaf; returns 1 and sigma on success
+__device__ __forceinline__ int match_leaf(const NodeHdr& h, const PlaneRec& P, const V3& wld, const M3& var_wld,
+                                          double& sigma) {
+  if (!h.is_plane) return 0;
+  V3 c = ld_v3(P.center), n = ld_v3(P.normal);
+  V3 d = sub(wld, c);
+  float dis_to_plane = fabs(dot3(n, d));
+  V3 cw = sub(c, wld);
+  float dis_to_center = cw[0] * cw[0] + cw[1] * cw[1] + cw[2] * cw[2];
+  float range_dis = (dis_to_center - dis_to_plane * dis_to_plane);
+  if (!(range_dis <= 3 * 3 * P.radius)) return 0;
+  double J[6] = {d[0], d[1], d[2], -n[0], -n[1], -n[2]};
+  double t[6];
+  for (int j = 0; j < 6; j++) {
+    double s = J[0] * P.var[sym_idx(6, 0, j)];
+    for (int k = 1; k < 6; k++) s += J[k] * P.var[sym_idx(6, k, j)];
+    t[j] = s;
+  }
+  double sl = t[0] * J[0];
+  for (int j = 1; j < 6; j++) sl += t[j] * J[j];
+  V3 vn = mul(var_wld, n);
+  sl += dot3(n, vn);
+  if (dis_to_plane < 3 * sqrt(sl)) {
+    sigma = sl;
+    return 1;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ bool inside(const NodeHdr& h, const V3& w) {
+  double hl = h.qlen * 2;
+  return (w[0] >= h.center[0] - hl && w[0] <= h.center[0] + hl && w[1] >= h.center[1] - hl &&
+          w[1] <= h.center[1] + hl && w[2] >= h.center[2] - hl && w[2] <= h.center[2] + hl);
+}
+
+constexpr int kIekfVals = 34;
+
+__global__ void __launch_bounds__(256) k_iekf(int n, const float* __restrict__ x, const float* __restrict__ y,
+                                              const float* __restrict__ z, MP mp, IekfPose ps, DevMap m,
+                                              int* __restrict__ cache, double* __restrict__ partials) {
+  double acc[kIekfVals];
+  for (int j = 0; j < kIekfVals; j++) acc[j] = 0.0;
+  const M3 R = ld_m3(ps.R), rot_var = ld_m3(ps.rot_var), tsl_var = ld_m3(ps.tsl_var);
+  const V3 p = ld_v3(ps.p);
+  const M3 Rt = tr(R);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    V3 pnt;
+    M3 var;
+    var_init_pt(mp, x[i], y[i], z[i], pnt, var);
+    M3 var_world = world_var(R, var, pnt, rot_var, tsl_var);
+    V3 wld = rigid(R, pnt, p);
+    int leaf = cache[i];
+    int flag = 0;
+    double sigma = 0;
+    if (leaf >= 0 && inside(m.hdr[leaf], wld)) {
+      flag = match_leaf(m.hdr[leaf], m.pl[leaf], wld, var_world, sigma);
+    } else {
+      uint64_t key;
+      if (pack_key(wld, mp.vs, key)) {
+        int root = hash_find(m.hkey, m.hval, m.hash_mask, key);
+        int lf = root >= 0 ? descend(m.hdr, root, wld) : -1;
+        if (lf >= 0) {
+          flag = match_leaf(m.hdr[lf], m.pl[lf], wld, var_world, sigma);
+          if (flag) leaf = lf;
+        }
+      }
+    }
+    if (flag) {
+      cache[i] = leaf;
+      const PlaneRec& P = m.pl[leaf];
+      V3 nn = ld_v3(P.normal), c = ld_v3(P.center);
+      double R_inv = 1.0 / (0.0005 + sigma);
+      double resi = dot3(nn, sub(wld, c));
+      V3 j3 = mul(mul(hat(pnt), Rt), nn);
+      double jac[6] = {j3[0], j3[1], j3[2], nn[0], nn[1], nn[2]};
+      int k = 0;
+      for (int r = 0; r < 6; r++) {
+        double jr_ = jac[r] * R_inv;
+        for (int c2 = r; c2 < 6; c2++, k++) acc[k] += jr_ * jac[c2];
+      }
+      for (int r = 0; r < 6; r++) acc[21 + r] -= jac[r] * (R_inv * resi);
+      acc[27] += nn[0] * nn[0];
+      acc[28] += nn[0] * nn[1];
+      acc[29] += nn[0] * nn[2];
+      acc[30] += nn[1] * nn[1];
+      acc[31] += nn[1] * nn[2];
+      acc[32] += nn[2] * nn[2];
+      acc[33] += 1.0;
+    }
+  }
+  // block reduction: wave shuffles then LDS across the 4 waves (fixed tree)
+  __shared__ double red[4][kIekfVals];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int j = 0; j < kIekfVals; j++) {
+    double v = acc[j];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) red[wv][j] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kIekfVals) {
+    int j = threadIdx.x;
+    partials[(size_t)blockIdx.x * kIekfVals + j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+  }
+}
+
+__global__ void k_iekf_final(int nb, const double* __restrict__ partials, double* __restrict__ out) {
+  int j = threadIdx.x;
+  if (j < kIekfVals) {
+    double s = 0;
+    for (int b = 0; b < nb; b++) s += partials[(size_t)b * kIekfVals + j];
+    out[j] = s;
+  }
+}
+
+int iekf_reset_cache(vg_ctx* ctx, int n) {
+  VG_HIP(hipMemsetAsync(ctx->wk.iekf_cache, 0xff, (size_t)n * sizeof(int), ctx->stream));
+  return VG_OK;
+}
+
+int iekf_iter(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n,
+              const IekfPose& pose, double* out34) {
+  Work& w = ctx->wk;
+  hipStream_t s = ctx->stream;
+  int nb = grid_for(n, 256, 512);
+  k_iekf<<<nb, 256, 0, s>>>(n, x, y, z, mp, pose, ctx->map, w.iekf_cache, w.partials);
+  k_iekf_final<<<1, 64, 0, s>>>(nb, w.partials, w.partials + (size_t)w.nparts * 38);
+  VG_HIP(hipGetLastError());
+  VG_HIP(hipMemcpyAsync(ctx->h_pinned_d, w.partials + (size_t)w.nparts * 38, kIekfVals * sizeof(double),
+                        hipMemcpyDeviceToHost, s));
+  VG_HIP(hipStreamSynchronize(s));
+  for (int j = 0; j < kIekfVals; j++) out34[j] = ctx->h_pinned_d[j];
+  return VG_OK;
+}
+
+// ------------------------------------------------------------------ insert (A3/A4)
+// per downsampled point: var_init + pvec_update (world var), world point, root
+// key insert-or-find, first-occurrence marking of brand-new keys
+__global__ void k_ins_prep(int n, const float* __restrict__ ox, const float* __restrict__ oy,
+                           const float* __restrict__ oz, MP mp, InsPose ps, int slot, DevMap m,
+                           double* __restrict__ pw, uint32_t* __restrict__ hslot) {
+  const M3 R = ld_m3(ps.R), rot_var = ld_m3(ps.rot_var), tsl_var = ld_m3(ps.tsl_var);
+  const V3 p = ld_v3(ps.p);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    V3 pnt;
+    M3 var;
+    var_init_pt(mp, ox[i], oy[i], oz[i], pnt, var);
+    M3 vw = world_var(R, var, pnt, rot_var, tsl_var);
+    V3 w = rigid(R, pnt, p);
+    size_t base = (size_t)slot * m.cap_wp + i;
+    for (int j = 0; j < 3; j++) m.wp_pnt[base * 3 + j] = pnt[j];
+    for (int j = 0; j < 9; j++) m.wp_var[base * 9 + j] = vw[j];
+    m.wp_leaf[base] = -1;
+    for (int j = 0; j < 3; j++) pw[(size_t)i * 3 + j] = w[j];
+    uint64_t key;
+    if (!pack_key(w, mp.vs, key)) {
+      atomicOr(&m.counters[kCntErr], 1);
+      hslot[i] = 0xffffffffu;
+      continue;
+    }
+    bool fresh;
+    int s = hash_insert(m.hkey, m.hash_mask, key, fresh);
+    if (s < 0) {
+      atomicOr(&m.counters[kCntErr], 2);
+      hslot[i] = 0xffffffffu;
+      continue;
+    }
+    hslot[i] = (uint32_t)s;
+    if (m.hval[s] < 0) atomicMin(&m.hfirst[s], i);
+  }
+}
+
+__global__ void k_ins_newflag(int n, const uint32_t* __restrict__ hslot, const int* __restrict__ hval,
+                              const int* __restrict__ hfirst, uint32_t* __restrict__ flag) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    uint32_t s = hslot[i];
+    flag[i] = (s != 0xffffffffu && hval[s] < 0 && hfirst[s] == i) ? 1u : 0u;
+  }
+}
+
+// allocate new roots in first-occurrence order (deterministic ids); new roots
+// join surf_map_slide (voxel_map.cpp:77-83)
+__global__ void k_ins_newalloc(int n, const uint32_t* __restrict__ hslot, const uint32_t* __restrict__ flag,
+                               const uint32_t* __restrict__ rank, MP mp, DevMap m) {
+  const int base = m.counters[kCntNodes];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (!flag[i]) continue;
+    uint32_t s = hslot[i];
+    int id = base + (int)rank[i];
+    if (id >= m.cap_nodes) {
+      atomicOr(&m.counters[kCntErr], 4);
+      continue;
+    }
+    uint64_t key = m.hkey[s];
+    double c[3];
+    int64_t k[3] = {unpack_axis(key, 42), unpack_axis(key, 21), unpack_axis(key, 0)};
+    for (int j = 0; j < 3; j++) c[j] = (0.5 + k[j]) * mp.vs;
+    init_node(m.hdr[id], c, (float)(mp.vs / 4.0), 0, -1);
+    m.hval[s] = id;
+    m.hfirst[s] = 0x7f7f7f7f;
+    m.in_slide[id] = 1;
+    int pos = atomicAdd(&m.counters[kCntSlide], 1);
+    m.slide[pos] = id;
+  }
+}
+
+__global__ void k_add_counter(int* counters, int idx, const uint32_t* __restrict__ flag,
+                              const uint32_t* __restrict__ rank, int n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0 && n > 0) counters[idx] += (int)(rank[n - 1] + flag[n - 1]);
+}
+
+// distinct roots touched by the scan (the thread_num quirk, voxel_map.cpp:94-97),
+// isexist on existing roots (voxel_map.cpp:70), surf_map_slide registration
+__global__ void k_ins_touch(int n, const uint32_t* __restrict__ hslot, int epoch, int first_new, DevMap m,
+                           int* __restrict__ root_of) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    uint32_t s = hslot[i];
+    int root = s != 0xffffffffu ? m.hval[s] : -1;
+    root_of[i] = root;
+    if (root < 0) continue;
+    if (atomicExch(&m.nscr[(size_t)root * 4 + 3], epoch) != epoch) {
+      atomicAdd(&m.counters[kCntTouched], 1);
+      if (root < first_new) {
+        m.hdr[root].isexist = 1;
+        if (!m.in_slide[root]) {
+          m.in_slide[root] = 1;
+          int pos = atomicAdd(&m.counters[kCntSlide], 1);
+          m.slide[pos] = root;
+        }
+      }
+    }
+  }
+}
+
+// descend to a leaf; a missing child becomes a creation request (parent, octant)
+__global__ void k_ins_descend(int n, const double* __restrict__ pw, DevMap m, int* __restrict__ leaf,
+                              int* __restrict__ reqlist) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int node = leaf[i];
+    if (node < 0) continue;
+    V3 w = v3(pw[3 * i], pw[3 * i + 1], pw[3 * i + 2]);
+    for (int d = 0; d < 8; d++) {
+      const NodeHdr& h = m.hdr[node];
+      if (h.octo == 0) break;
+      int o = octant(w, h.center);
+      int c = h.child[o];
+      if (c < 0) {
+        // request (parent, octant); the first requester of a parent registers it
+        if (atomicCAS(&m.cfirst[(size_t)node * 8 + o], 0x7f7f7f7f, -5) == 0x7f7f7f7f) {
+          if (atomicExch(&m.nscr[(size_t)node * 4 + 1], -7) != -7) {
+            int pos = atomicAdd(&m.counters[kCntCreate], 1);
+            reqlist[pos] = node;
+          }
+        }
+        node = -2 - (node * 8 + o);
+        break;
+      }
+      node = c;
+    }
+    leaf[i] = node;
+  }
+}
+
+// children for a sorted list of parents: ids = base + prefix(popcount(mask))
+__global__ void k_child_count(int np, const int* __restrict__ parents, DevMap m, uint32_t* __restrict__ cnt) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < np; q += gridDim.x * blockDim.x) {
+    int p = parents[q];
+    int c = 0;
+    for (int o = 0; o < 8; o++) c += (m.cfirst[(size_t)p * 8 + o] == -5) ? 1 : 0;
+    cnt[q] = (uint32_t)c;
+  }
+}
+
+__global__ void k_child_alloc(int np, const int* __restrict__ parents, const uint32_t* __restrict__ off, DevMap m,
+                              int* __restrict__ next, int next_base) {
+  const int base = m.counters[kCntNodes];
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < np; q += gridDim.x * blockDim.x) {
+    int p = parents[q];
+    NodeHdr& ph = m.hdr[p];
+    int k = 0;
+    for (int o = 0; o < 8; o++) {
+      if (m.cfirst[(size_t)p * 8 + o] != -5) continue;
+      int id = base + (int)off[q] + k;
+      k++;
+      m.cfirst[(size_t)p * 8 + o] = 0x7f7f7f7f;
+      if (id >= m.cap_nodes) {
+        atomicOr(&m.counters[kCntErr], 4);
+        continue;
+      }
+      int xyz[3] = {(o >> 2) & 1, (o >> 1) & 1, o & 1};
+      double c[3];
+      for (int j = 0; j < 3; j++) c[j] = ph.center[j] + (float)((2 * xyz[j] - 1) * ph.qlen);
+      init_node(m.hdr[id], c, ph.qlen / 2, ph.layer + 1, p);
+      ph.child[o] = id;
+      if (next) next[next_base + (int)off[q] + k - 1] = id;
+    }
+    m.nscr[(size_t)p * 4 + 1] = -1;
+  }
+}
+
+__global__ void k_ins_resolve(int n, const double* __restrict__ pw, DevMap m, int* __restrict__ leaf) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int node = leaf[i];
+    if (node >= -1) continue;
+    int code = -2 - node;
+    leaf[i] = m.hdr[code >> 3].child[code & 7];
+  }
+}
+
+// sort key: (leaf << 27) | order
+__global__ void k_ins_keys(int n, const int* __restrict__ leaf, uint64_t* __restrict__ keys) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int l = leaf[i];
+    keys[i] = l >= 0 ? (((uint64_t)l << 27) | (uint64_t)i) : ~0ull;
+  }
+}
+
+// OctoTree::push (octree.cpp:151-177) for every point of a leaf segment, in order
+__global__ void k_push_window(int n, const uint64_t* __restrict__ keys, MP mp, int slot, DevMap m,
+                              const double* __restrict__ pw) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    uint64_t k = keys[j];
+    if (k == ~0ull) continue;
+    int leaf = (int)(k >> 27);
+    if (j > 0 && (int)(keys[j - 1] >> 27) == leaf && keys[j - 1] != ~0ull) continue;
+    NodeHdr& h = m.hdr[leaf];
+    h.has_sw = 1;
+    h.isexist = 1;
+    const bool listed = h.layer < mp.max_layer;
+    Clu loc = m.pcrs[(size_t)leaf * mp.W + slot];
+    Clu add_ = m.pcr_add[leaf];
+    double cov[kCovN];
+    for (int t = 0; t < kCovN; t++) cov[t] = m.cov_add[(size_t)leaf * kCovN + t];
+    for (int jj = j; jj < n; jj++) {
+      uint64_t kk = keys[jj];
+      if (kk == ~0ull || (int)(kk >> 27) != leaf) break;
+      int i = (int)(kk & ((1u << 27) - 1));
+      size_t b = (size_t)slot * m.cap_wp + i;
+      V3 pnt = ld_v3(&m.wp_pnt[b * 3]);
+      M3 var = ld_m3(&m.wp_var[b * 9]);
+      V3 w = v3(pw[3 * i], pw[3 * i + 1], pw[3 * i + 2]);
+      if (listed) m.wp_leaf[b] = leaf;
+      clu_push(loc, pnt);
+      clu_push(add_, w);
+      bf_var_acc(cov, var, w);
+    }
+    m.pcrs[(size_t)leaf * mp.W + slot] = loc;
+    m.pcr_add[leaf] = add_;
+    for (int t = 0; t < kCovN; t++) m.cov_add[(size_t)leaf * kCovN + t] = cov[t];
+  }
+}
+
+static int read_counters(vg_ctx* ctx) {
+  VG_HIP(hipMemcpyAsync(ctx->h_pinned, ctx->map.counters, kCntN * sizeof(int), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  VG_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->h_pinned[kCntErr]) {
+    int e = ctx->h_pinned[kCntErr];
+    ctx->err = std::string("device map error flags=") + std::to_string(e) +
+               ((e & 4) ? " (node pool full)" : "") + ((e & 8) ? " (point_fix arena full)" : "") +
+               ((e & 1) ? " (voxel key out of packed range)" : "") + ((e & 2) ? " (root hash full)" : "");
+    return (e & 1) ? VG_E_RANGE : VG_E_CAPACITY;
+  }
+  return VG_OK;
+}
+
+static int sort_keys(vg_ctx* ctx, const uint64_t* in, uint64_t* out, int n, int end_bit) {
+  size_t tb = ctx->wk.tmp_bytes;
+  if (n <= 0) return VG_OK;
+  VG_HIP(hipcub::DeviceRadixSort::SortKeys(ctx->wk.tmp, tb, in, out, n, 0, end_bit, ctx->stream));
+  return VG_OK;
+}
+static int excl_scan(vg_ctx* ctx, const uint32_t* in, uint32_t* out, int n) {
+  size_t tb = ctx->wk.tmp_bytes;
+  if (n <= 0) return VG_OK;
+  VG_HIP(hipcub::DeviceScan::ExclusiveSum(ctx->wk.tmp, tb, in, out, n, ctx->stream));
+  return VG_OK;
+}
+static int bits_for(long v) {
+  int b = 1;
+  while ((1L << b) <= v) b++;
+  return b;
+}
+
+// sort an int list of n node ids in place (deterministic creation order)
+__global__ void k_i2k(int n, const int* __restrict__ a, uint64_t* __restrict__ k) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) k[i] = (uint64_t)a[i];
+}
+__global__ void k_k2i(int n, const uint64_t* __restrict__ k, int* __restrict__ a) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) a[i] = (int)k[i];
+}
+static int sort_ids(vg_ctx* ctx, int* a, int n) {
+  if (n <= 1) return VG_OK;
+  Work& w = ctx->wk;
+  k_i2k<<<grid_for(n), kBlock, 0, ctx->stream>>>(n, a, w.k0);
+  VG_TRY(sort_keys(ctx, w.k0, w.k1, n, 32));
+  k_k2i<<<grid_for(n), kBlock, 0, ctx->stream>>>(n, w.k1, a);
+  return VG_OK;
+}
+
+// allocate children for the parents in plist (sorted), ids deterministic
+static int alloc_children(vg_ctx* ctx, int* plist, int np, int* next, int next_base, bool sorted, int* n_created) {
+  Work& w = ctx->wk;
+  hipStream_t s = ctx->stream;
+  *n_created = 0;
+  if (np <= 0) return VG_OK;
+  if (!sorted) VG_TRY(sort_ids(ctx, plist, np));
+  VG_TRY(read_counters(ctx));
+  int first = ctx->h_pinned[kCntNodes];
+  k_child_count<<<grid_for(np), kBlock, 0, s>>>(np, plist, ctx->map, w.ac_cnt);
+  VG_TRY(excl_scan(ctx, w.ac_cnt, w.ac_off, np));
+  k_child_alloc<<<grid_for(np), kBlock, 0, s>>>(np, plist, w.ac_off, ctx->map, next, next_base);
+  k_add_counter<<<1, 64, 0, s>>>(ctx->map.counters, kCntNodes, w.ac_cnt, w.ac_off, np);
+  k_zero_nodes<<<grid_for(1 << 16), kBlock, 0, s>>>(first, ctx->map.counters + kCntNodes, ctx->map.W, ctx->map.pl,
+                                                  ctx->map.pcr_add, ctx->map.pcr_fix, ctx->map.cov_add, ctx->map.eig,
+                                                  ctx->map.jour, ctx->map.pcrs);
+  VG_HIP(hipGetLastError());
+  VG_TRY(read_counters(ctx));
+  *n_created = ctx->h_pinned[kCntNodes] - first;
+  return VG_OK;
+}
+
+// cut_voxel_multi (voxel_map.cpp:47-135) + pvec_update (point_utils.cpp:54-65)
+int map_insert(vg_ctx* ctx, const MP& mp, int slot, const InsPose& pose, int n, int epoch, int thread_num,
+               int* roots_new, int* touched) {
+  DevMap& m = ctx->map;
+  Work& w = ctx->wk;
+  hipStream_t s = ctx->stream;
+  *roots_new = 0;
+  *touched = 0;
+  if (n <= 0) return VG_OK;
+  VG_TRY(read_counters(ctx));
+  const int first_new = ctx->h_pinned[kCntNodes];
+  int g = grid_for(n);
+  k_ins_prep<<<g, kBlock, 0, s>>>(n, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, mp, pose, slot, m, w.pw, w.u0);
+  k_ins_newflag<<<g, kBlock, 0, s>>>(n, w.u0, m.hval, m.hfirst, w.v0);
+  VG_TRY(excl_scan(ctx, w.v0, w.v1, n));
+  k_ins_newalloc<<<g, kBlock, 0, s>>>(n, w.u0, w.v0, w.v1, mp, m);
+  k_add_counter<<<1, 64, 0, s>>>(m.counters, kCntNodes, w.v0, w.v1, n);
+  k_zero_nodes<<<grid_for(1 << 16), kBlock, 0, s>>>(first_new, m.counters + kCntNodes, m.W, m.pl, m.pcr_add,
+                                                  m.pcr_fix, m.cov_add, m.eig, m.jour, m.pcrs);
+  VG_HIP(hipMemsetAsync(m.counters + kCntTouched, 0, sizeof(int), s));
+  k_ins_touch<<<g, kBlock, 0, s>>>(n, w.u0, epoch, first_new, m, w.leaf);
+  VG_HIP(hipGetLastError());
+  VG_TRY(read_counters(ctx));
+  *roots_new = ctx->h_pinned[kCntNodes] - first_new;
+  *touched = ctx->h_pinned[kCntTouched];
+  if (*touched < thread_num) return VG_OK;  // voxel_map.cpp:96-97: no allocation at all
+  VG_HIP(hipMemsetAsync(m.counters + kCntCreate, 0, sizeof(int), s));
+  k_ins_descend<<<g, kBlock, 0, s>>>(n, w.pw, m, w.leaf, w.list2);
+  VG_TRY(read_counters(ctx));
+  int np = ctx->h_pinned[kCntCreate], created = 0;
+  if (np > 0) {
+    VG_TRY(alloc_children(ctx, w.list2, np, nullptr, 0, false, &created));
+    k_ins_resolve<<<g, kBlock, 0, s>>>(n, w.pw, m, w.leaf);
+  }
+  k_ins_keys<<<g, kBlock, 0, s>>>(n, w.leaf, w.k0);
+  VG_TRY(sort_keys(ctx, w.k0, w.k1, n, 27 + bits_for(ctx->h_pinned[kCntNodes])));
+  k_push_window<<<g, kBlock, 0, s>>>(n, w.k1, mp, slot, m, w.pw);
+  VG_HIP(hipGetLastError());
+  return read_counters(ctx);
+}
+
+// ------------------------------------------------------------------ recut (A5/A6)
+// One level of OctoTree::recut (octree.cpp:335-393) over a worklist: internal
+// nodes forward their children, leaves run the plane test; failing leaves below
+// max_layer are marked for subdivision; planar leaves that pass tras_opt's
+// filter (octree.cpp:502-505) become factor candidates.
+__global__ void k_recut_visit(int nw, const int* __restrict__ work, MP mp, DevMap m, int* __restrict__ next,
+                              int* __restrict__ sub, int* __restrict__ cand) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) {
+    int node = work[q];
+    NodeHdr& h = m.hdr[node];
+    if (h.octo == 1) {
+      for (int o = 0; o < 8; o++)
+        if (h.child[o] >= 0) next[atomicAdd(&m.counters[kCntNext], 1)] = h.child[o];
+      continue;
+    }
+    h.opt_state = -1;
+    const Clu& a = m.pcr_add[node];
+    if (a.N <= mp.minpt[h.layer]) {
+      h.is_plane = 0;
+      continue;
+    }
+    if (!h.isexist || !h.has_sw) continue;
+    V3 ev;
+    M3 U;
+    eig3(clu_cov(a), ev, U);
+    double* e = &m.eig[(size_t)node * 12];
+    for (int j = 0; j < 3; j++) e[j] = ev[j];
+    for (int j = 0; j < 9; j++) e[3 + j] = U[j];
+    h.is_plane = (ev[0] < mp.min_eig && (ev[0] / ev[2]) < mp.thre[h.layer]) ? 1 : 0;
+    if (h.is_plane) {
+      if (!(ev[0] / ev[1] > 0.12)) cand[atomicAdd(&m.counters[kCntFactors], 1)] = node;
+      continue;
+    }
+    if (h.layer >= mp.max_layer) continue;
+    m.nscr[(size_t)node * 4 + 2] = 1;  // subdividing
+    sub[atomicAdd(&m.counters[kCntSub], 1)] = node;
+  }
+}
+
+// subdivision events: point_fix entries (fix_divide, octree.cpp:257-277) and
+// window points of every frame (subdivide, octree.cpp:279-300)
+__global__ void k_sub_fix_events(int ns, const int* __restrict__ sub, DevMap m, uint64_t* __restrict__ ev, int cap) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ns; q += gridDim.x * blockDim.x) {
+    int p = sub[q];
+    const NodeHdr& h = m.hdr[p];
+    for (int j = 0; j < h.fix_cnt; j++) {
+      size_t f = (size_t)h.fix_off + j;
+      V3 pt = ld_v3(&m.fix_pnt[f * 3]);
+      int o = octant(pt, h.center);
+      m.cfirst[(size_t)p * 8 + o] = -5;
+      int pos = atomicAdd(&m.counters[kCntEvents], 1);
+      // parent, octant, phase 0 (fix), index
+      if (pos < cap) ev[pos] = ((uint64_t)p << 27) | ((uint64_t)o << 24) | (uint64_t)j;
+    }
+  }
+}
+
+__global__ void k_sub_win_events(int total, int cap_wp, const int* __restrict__ nper, const int* __restrict__ slot_of,
+                                 WinD* __restrict__ win, DevMap m, uint64_t* __restrict__ ev,
+                                 uint32_t* __restrict__ evsrc, int cap) {
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += gridDim.x * blockDim.x) {
+    int ord = 0, i = g;
+    while (ord < win->win_count && i >= nper[ord]) {
+      i -= nper[ord];
+      ord++;
+    }
+    if (ord >= win->win_count) continue;
+    int slot = slot_of[ord];
+    size_t b = (size_t)slot * cap_wp + i;
+    int leaf = m.wp_leaf[b];
+    if (leaf < 0 || m.nscr[(size_t)leaf * 4 + 2] != 1) continue;
+    const NodeHdr& h = m.hdr[leaf];
+    V3 pw = rigid(ld_m3(win->R[ord]), ld_v3(&m.wp_pnt[b * 3]), ld_v3(win->p[ord]));
+    int o = octant(pw, h.center);
+    m.cfirst[(size_t)leaf * 8 + o] = -5;
+    int pos = atomicAdd(&m.counters[kCntEvents], 1);
+    if (pos < cap) {
+      ev[pos] = ((uint64_t)leaf << 27) | ((uint64_t)o << 24) | (uint64_t)(1 + ord);
+      evsrc[pos] = (uint32_t)i;
+    }
+  }
+}
+
+// rewrite events as (child << 27 | phase << 21 | idx) sort keys
+__global__ void k_sub_keys(int ne, const uint64_t* __restrict__ ev, const uint32_t* __restrict__ evsrc,
+                           DevMap m, uint64_t* __restrict__ keys, int nfix) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x) {
+    uint64_t v = ev[e];
+    int p = (int)(v >> 27);
+    int o = (int)((v >> 24) & 7);
+    int lo = (int)(v & 0xffffff);
+    int child = m.hdr[p].child[o];
+    uint64_t phase, idx;
+    if (e < nfix) {
+      phase = 0;
+      idx = (uint64_t)lo;
+    } else {
+      phase = (uint64_t)lo;  // 1 + ord
+      idx = evsrc[e];
+    }
+    keys[e] = ((uint64_t)child << 27) | (phase << 21) | idx;
+  }
+}
+
+// apply the sorted subdivision pushes to each child, in the reference's order:
+// fix points first (push_fix, octree.cpp:179-188), then window points frame by
+// frame (push, octree.cpp:151-177)
+__global__ void k_push_events(int ne, const uint64_t* __restrict__ keys, MP mp, WinD* __restrict__ win, DevMap m) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < ne; j += gridDim.x * blockDim.x) {
+    int child = (int)(keys[j] >> 27);
+    if (j > 0 && (int)(keys[j - 1] >> 27) == child) continue;
+    NodeHdr& h = m.hdr[child];
+    const int parent = h.parent;
+    const NodeHdr& ph = m.hdr[parent];
+    const bool listed = h.layer < mp.max_layer;
+    int jend = j;
+    int nfix = 0;
+    while (jend < ne && (int)(keys[jend] >> 27) == child) {
+      if (((keys[jend] >> 21) & 63) == 0) nfix++;
+      jend++;
+    }
+    if (nfix > 0 && listed) {
+      int off = atomicAdd(&m.counters[kCntFix], nfix);
+      if (off + nfix > m.cap_fix) {
+        atomicOr(&m.counters[kCntErr], 8);
+        continue;
+      }
+      h.fix_off = off;
+      h.fix_cap = nfix;
+      h.fix_cnt = 0;
+    }
+    Clu add_ = m.pcr_add[child];
+    Clu fix_ = m.pcr_fix[child];
+    double cov[kCovN];
+    for (int t = 0; t < kCovN; t++) cov[t] = m.cov_add[(size_t)child * kCovN + t];
+    int cur_slot = -1;
+    Clu loc;
+    clu_zero(loc);
+    for (int jj = j; jj < jend; jj++) {
+      uint64_t k = keys[jj];
+      int phase = (int)((k >> 21) & 63);
+      int idx = (int)(k & ((1u << 21) - 1));
+      if (phase == 0) {
+        size_t f = (size_t)ph.fix_off + idx;
+        V3 pt = ld_v3(&m.fix_pnt[f * 3]);
+        M3 var = ld_m3(&m.fix_var[f * 9]);
+        if (listed) {
+          size_t d = (size_t)h.fix_off + h.fix_cnt;
+          for (int t = 0; t < 3; t++) m.fix_pnt[d * 3 + t] = pt[t];
+          for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = var[t];
+          h.fix_cnt++;
+        }
+        clu_push(fix_, pt);
+        clu_push(add_, pt);
+        bf_var_acc(cov, var, pt);
+      } else {
+        int ord = phase - 1;
+        int slot = win->mp[ord];
+        if (slot != cur_slot) {
+          if (cur_slot >= 0) m.pcrs[(size_t)child * mp.W + cur_slot] = loc;
+          cur_slot = slot;
+          loc = m.pcrs[(size_t)child * mp.W + slot];
+        }
+        size_t b = (size_t)slot * m.cap_wp + idx;
+        V3 pnt = ld_v3(&m.wp_pnt[b * 3]);
+        M3 var = ld_m3(&m.wp_var[b * 9]);
+        V3 pw = rigid(ld_m3(win->R[ord]), pnt, ld_v3(win->p[ord]));
+        h.has_sw = 1;
+        h.isexist = 1;
+        m.wp_leaf[b] = listed ? child : -1;
+        clu_push(loc, pnt);
+        clu_push(add_, pw);
+        bf_var_acc(cov, var, pw);
+      }
+    }
+    if (cur_slot >= 0) m.pcrs[(size_t)child * mp.W + cur_slot] = loc;
+    m.pcr_add[child] = add_;
+    m.pcr_fix[child] = fix_;
+    for (int t = 0; t < kCovN; t++) m.cov_add[(size_t)child * kCovN + t] = cov[t];
+  }
+}
+
+// finish a subdivided parent: release its SlideWindow, free point_fix,
+// octo_state = 1 (octree.cpp:375-387)
+__global__ void k_sub_finish(int ns, const int* __restrict__ sub, DevMap m) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ns; q += gridDim.x * blockDim.x) {
+    int p = sub[q];
+    NodeHdr& h = m.hdr[p];
+    h.has_sw = 0;
+    for (int j = 0; j < m.W; j++) clu_zero(m.pcrs[(size_t)p * m.W + j]);
+    h.fix_cnt = 0;
+    h.fix_cap = 0;
+    h.octo = 1;
+    m.nscr[(size_t)p * 4 + 2] = -1;
+  }
+}
+
+// tras_opt: factor list in node-id order; opt_state = factor index
+__global__ void k_factor_finish(int nf, const int* __restrict__ fac, DevMap m, int* __restrict__ fac_node,
+                                double* __restrict__ fac_eig, Clu* __restrict__ fac_pcr) {
+  for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < nf; a += gridDim.x * blockDim.x) {
+    int node = fac[a];
+    fac_node[a] = node;
+    m.hdr[node].opt_state = a;
+    for (int j = 0; j < 12; j++) fac_eig[(size_t)a * 12 + j] = m.eig[(size_t)node * 12 + j];
+    fac_pcr[a] = m.pcr_add[node];
+  }
+}
+
+// multi_recut (local_mapping.cpp:144-201): level-synchronous recursion over
+// surf_map_slide, then tras_opt. Returns the factor count.
+int map_recut(vg_ctx* ctx, const MP& mp, const WinD& win, const int* nper, int thread_num, int* n_factors) {
+  DevMap& m = ctx->map;
+  Work& w = ctx->wk;
+  hipStream_t s = ctx->stream;
+  *n_factors = 0;
+  VG_TRY(read_counters(ctx));
+  int nslide = ctx->h_pinned[kCntSlide];
+  if (nslide < thread_num) return VG_OK;  // local_mapping.cpp:150-154
+  // upload the window (poses, ring) and per-ord point counts
+  WinD* dwin = (WinD*)ctx->ba.xs;
+  int* dn = (int*)((char*)ctx->ba.xs + sizeof(WinD));
+  int* dslot = dn + 32;
+  int hn[64];
+  for (int i = 0; i < 32; i++) {
+    hn[i] = i < win.win_count ? nper[i] : 0;
+    hn[32 + i] = win.mp[i];
+  }
+  VG_HIP(hipMemcpyAsync(dwin, &win, sizeof(WinD), hipMemcpyHostToDevice, s));
+  VG_HIP(hipMemcpyAsync(dn, hn, sizeof(hn), hipMemcpyHostToDevice, s));
+  int total = 0;
+  for (int i = 0; i < win.win_count; i++) total += nper[i];
+  VG_HIP(hipMemcpyAsync(w.list0, m.slide, (size_t)nslide * sizeof(int), hipMemcpyDeviceToDevice, s));
+  int nwork = nslide;
+  int* work = w.list0;
+  int* next = w.list1;
+  int* cand = w.cand;
+  int* subl = w.list2;
+  VG_HIP(hipMemsetAsync(m.counters + kCntFactors, 0, sizeof(int), s));
+  for (int level = 0; level <= 8 && nwork > 0; level++) {
+    VG_HIP(hipMemsetAsync(m.counters + kCntNext, 0, 3 * sizeof(int), s));  // Next, Sub, Events
+    VG_HIP(hipMemsetAsync(m.counters + kCntSub, 0, 2 * sizeof(int), s));
+    k_recut_visit<<<grid_for(nwork), kBlock, 0, s>>>(nwork, work, mp, m, next, subl, cand);
+    VG_HIP(hipGetLastError());
+    VG_TRY(read_counters(ctx));
+    int nnext = ctx->h_pinned[kCntNext], nsub = ctx->h_pinned[kCntSub];
+    if (nsub > 0) {
+      VG_TRY(sort_ids(ctx, subl, nsub));
+      k_sub_fix_events<<<grid_for(nsub), kBlock, 0, s>>>(nsub, subl, m, w.k0, w.cap);
+      VG_TRY(read_counters(ctx));
+      int nfix = ctx->h_pinned[kCntEvents];
+      if (nfix > w.cap) {
+        ctx->err = "subdivision event buffer overflow";
+        return VG_E_CAPACITY;
+      }
+      if (total > 0)
+        k_sub_win_events<<<grid_for(total), kBlock, 0, s>>>(total, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc,
+                                                            w.cap);
+      VG_TRY(read_counters(ctx));
+      int ne = ctx->h_pinned[kCntEvents];
+      if (ne > w.cap) {
+        ctx->err = "subdivision event buffer overflow";
+        return VG_E_CAPACITY;
+      }
+      // fix events sit at [0, nfix); their evsrc is unused
+      int created = 0;
+      VG_TRY(alloc_children(ctx, subl, nsub, next, nnext, true, &created));
+      nnext += created;
+      k_sub_keys<<<grid_for(ne), kBlock, 0, s>>>(ne, w.k0, w.evsrc, m, w.k1, nfix);
+      VG_TRY(sort_keys(ctx, w.k1, w.k0, ne, 27 + bits_for(ctx->h_pinned[kCntNodes])));
+      k_push_events<<<grid_for(ne), kBlock, 0, s>>>(ne, w.k0, mp, dwin, m);
+      k_sub_finish<<<grid_for(nsub), kBlock, 0, s>>>(nsub, subl, m);
+      VG_HIP(hipGetLastError());
+      VG_TRY(read_counters(ctx));
+    }
+    int* t = work;
+    work = next;
+    next = t;
+    nwork = nnext;
+  }
+  VG_TRY(read_counters(ctx));
+  int nf = ctx->h_pinned[kCntFactors];
+  if (nf > ctx->ba.cap_f) {
+    ctx->err = "factor capacity exceeded";
+    return VG_E_CAPACITY;
+  }
+  if (nf > 0) {
+    VG_TRY(sort_ids(ctx, cand, nf));
+    k_factor_finish<<<grid_for(nf), kBlock, 0, s>>>(nf, cand, m, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr);
+    VG_HIP(hipGetLastError());
+  }
+  *n_factors = nf;
+  return VG_OK;
+}
+
+// ------------------------------------------------------------------ margi (A10)
+// collect every node under the slide roots, level by level (top-down)
+__global__ void k_collect_level(int nw, const int* __restrict__ work, DevMap m, int* __restrict__ next,
+                                int* __restrict__ leaves) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) {
+    int node = work[q];
+    const NodeHdr& h = m.hdr[node];
+    if (h.octo == 1) {
+      for (int o = 0; o < 8; o++)
+        if (h.child[o] >= 0) next[atomicAdd(&m.counters[kCntNext], 1)] = h.child[o];
+    } else {
+      leaves[atomicAdd(&m.counters[kCntLeaves], 1)] = node;
+    }
+  }
+}
+
+// oldest-slot point segments per leaf: seg start/count in nscr[.*4+0/1]
+__global__ void k_margi_keys(int n, int slot, DevMap m, uint64_t* __restrict__ keys) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int l = m.wp_leaf[(size_t)slot * m.cap_wp + i];
+    keys[i] = l >= 0 ? (((uint64_t)l << 27) | (uint64_t)i) : ~0ull;
+  }
+}
+__global__ void k_margi_segs(int n, const uint64_t* __restrict__ keys, DevMap m) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    uint64_t k = keys[j];
+    if (k == ~0ull) continue;
+    int l = (int)(k >> 27);
+    if (j > 0 && keys[j - 1] != ~0ull && (int)(keys[j - 1] >> 27) == l) continue;
+    int c = 0;
+    while (j + c < n && keys[j + c] != ~0ull && (int)(keys[j + c] >> 27) == l) c++;
+    m.nscr[(size_t)l * 4 + 0] = j;
+    m.nscr[(size_t)l * 4 + 1] = c;
+  }
+}
+
+__device__ void plane_update_dev(DevMap& m, int node, const Clu& pcr_add, const double* e) {
+  PlaneRec& P = m.pl[node];
+  V3 center = v3(pcr_add.v[0] / pcr_add.N, pcr_add.v[1] / pcr_add.N, pcr_add.v[2] / pcr_add.N);
+  V3 u[3];
+  for (int k = 0; k < 3; k++) u[k] = v3(e[3 + 0 * 3 + k], e[3 + 1 * 3 + k], e[3 + 2 * 3 + k]);
+  double nv = 1.0 / pcr_add.N;
+  M<3, 9> uc;
+  uc.zero();
+  const int l = 0;
+  for (int k = 1; k < 3; k++) {
+    M3 ukl = outer3(u[k], u[l]);
+    double f[9];
+    f[0] = ukl(0, 0);
+    f[1] = ukl(1, 0) + ukl(0, 1);
+    f[2] = ukl(2, 0) + ukl(0, 2);
+    f[3] = ukl(1, 1);
+    f[4] = ukl(1, 2) + ukl(2, 1);
+    f[5] = ukl(2, 2);
+    double a1 = dot3(u[k], center), a2 = dot3(u[l], center);
+    for (int j = 0; j < 3; j++) f[6 + j] = -(u[l][j] * a1 + u[k][j] * a2);
+    double sc = nv / (e[l] - e[k]);
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 9; c++) uc(r, c) += (u[k][r] * sc) * f[c];
+  }
+  M<9, 9> cov = unpack9(&m.cov_add[(size_t)node * kCovN]);
+  M<3, 9> Jc = mul(uc, cov);
+  M3 A = mul(Jc, tr(uc));
+  double pv[6][6];
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) {
+      pv[r][c] = A(r, c);
+      pv[r][3 + c] = Jc(r, 6 + c) * nv;
+      pv[3 + c][r] = pv[r][3 + c];
+      pv[3 + r][3 + c] = cov(6 + r, 6 + c) * (nv * nv);
+    }
+  for (int r = 0; r < 6; r++)
+    for (int c = r; c < 6; c++) P.var[sym_idx(6, r, c)] = pv[r][c];
+  for (int j = 0; j < 3; j++) {
+    P.center[j] = center[j];
+    P.normal[j] = u[0][j];
+  }
+  P.radius = (float)e[2];
+}
+
+// OctoTree::margi leaf branch (octree.cpp:397-484), mgsize = 1. keys = the
+// oldest slot's listed points sorted by (leaf, index): each leaf's segment is
+// its sw->points[mp[0]] list in push order.
+__global__ void k_margi_leaf(int nl, const int* __restrict__ leaves, const uint64_t* __restrict__ keys, MP mp,
+                             WinD* __restrict__ win, DevMap m, const double* __restrict__ fac_eig,
+                             const Clu* __restrict__ fac_pcr) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nl; q += gridDim.x * blockDim.x) {
+    int node = leaves[q];
+    NodeHdr& h = m.hdr[node];
+    int seg = m.nscr[(size_t)node * 4 + 0], segn = m.nscr[(size_t)node * 4 + 1];
+    m.nscr[(size_t)node * 4 + 0] = -1;
+    m.nscr[(size_t)node * 4 + 1] = -1;
+    if (!h.isexist || !h.has_sw) continue;
+    const int W = mp.W;
+    const int s0 = win->mp[0];
+    Clu* loc = &m.pcrs[(size_t)node * W];
+    const M3 R0 = ld_m3(win->R[0]);
+    const V3 p0 = ld_v3(win->p[0]);
+    Clu w0;
+    clu_zero(w0);
+    if (loc[s0].N != 0) w0 = clu_transform(loc[s0], R0, p0);
+    Clu add_;
+    double* e = &m.eig[(size_t)node * 12];
+    if (h.opt_state >= 0) {
+      add_ = fac_pcr[h.opt_state];
+      for (int j = 0; j < 12; j++) e[j] = fac_eig[(size_t)h.opt_state * 12 + j];
+      h.opt_state = -1;
+    } else {
+      add_ = m.pcr_fix[node];
+      for (int i = 0; i < win->win_count; i++) {
+        int si = win->mp[i];
+        if (loc[si].N != 0) {
+          Clu t = (i == 0) ? w0 : clu_transform(loc[si], ld_m3(win->R[i]), ld_v3(win->p[i]));
+          clu_add(add_, t);
+        }
+      }
+      if (h.is_plane) {
+        V3 ev;
+        M3 U;
+        eig3(clu_cov(add_), ev, U);
+        for (int j = 0; j < 3; j++) e[j] = ev[j];
+        for (int j = 0; j < 9; j++) e[3 + j] = U[j];
+      }
+    }
+    Clu fix_ = m.pcr_fix[node];
+    if (fix_.N < mp.max_points && h.is_plane)
+      if (add_.N - h.last_num >= 5 || h.last_num <= 10) {
+        plane_update_dev(m, node, add_, e);
+        h.last_num = add_.N;
+      }
+    if (fix_.N < mp.max_points) {
+      if (w0.N != 0) {
+        clu_add(fix_, w0);
+        if (seg >= 0 && segn > 0) {
+          int need = h.fix_cnt + segn;
+          if (need > h.fix_cap) {  // grow the point_fix block (old block is abandoned)
+            int cap = need * 2 < 128 ? 128 : need * 2;
+            int off = atomicAdd(&m.counters[kCntFix], cap);
+            if (off + cap > m.cap_fix) {
+              atomicOr(&m.counters[kCntErr], 8);
+              continue;
+            }
+            for (int j = 0; j < h.fix_cnt; j++) {
+              size_t a = (size_t)h.fix_off + j, b = (size_t)off + j;
+              for (int t = 0; t < 3; t++) m.fix_pnt[b * 3 + t] = m.fix_pnt[a * 3 + t];
+              for (int t = 0; t < 9; t++) m.fix_var[b * 9 + t] = m.fix_var[a * 9 + t];
+            }
+            h.fix_off = off;
+            h.fix_cap = cap;
+          }
+          for (int j = 0; j < segn; j++) {
+            int i = (int)(keys[seg + j] & ((1u << 27) - 1));
+            size_t b = (size_t)s0 * m.cap_wp + i;
+            V3 pt = rigid(R0, ld_v3(&m.wp_pnt[b * 3]), p0);
+            size_t d = (size_t)h.fix_off + h.fix_cnt;
+            for (int t = 0; t < 3; t++) m.fix_pnt[d * 3 + t] = pt[t];
+            for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = m.wp_var[b * 9 + t];
+            h.fix_cnt++;
+          }
+        }
+      }
+    } else {
+      if (w0.N != 0) clu_sub(add_, w0);
+      h.fix_cnt = 0;
+    }
+    clu_zero(loc[s0]);
+    m.pcr_fix[node] = fix_;
+    m.pcr_add[node] = add_;
+    h.isexist = (fix_.N >= add_.N) ? 0 : 1;
+  }
+}
+
+__global__ void k_margi_segs_clear(int n, const uint64_t* __restrict__ keys, DevMap m) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    uint64_t k = keys[j];
+    if (k == ~0ull) continue;
+    int l = (int)(k >> 27);
+    m.nscr[(size_t)l * 4 + 0] = -1;
+    m.nscr[(size_t)l * 4 + 1] = -1;
+  }
+}
+
+// internal nodes bottom-up: isexist = OR(children) (octree.cpp:485-494)
+__global__ void k_margi_internal(int nw, const int* __restrict__ work, DevMap m) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) {
+    int node = work[q];
+    NodeHdr& h = m.hdr[node];
+    if (h.octo != 1) continue;
+    int8_t e = 0;
+    for (int o = 0; o < 8; o++)
+      if (h.child[o] >= 0) e |= m.hdr[h.child[o]].isexist;
+    h.isexist = e ? 1 : 0;
+  }
+}
+
+// erase dead roots from surf_map_slide (local_mapping.cpp:67-78) with
+// clear_slwd over their subtrees (octree.cpp:739-756)
+__global__ void k_margi_erase_mark(int nw, const int* __restrict__ work, DevMap m, int level, double jour) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) {
+    int node = work[q];
+    NodeHdr& h = m.hdr[node];
+    int dead;
+    if (level == 0) {
+      dead = h.isexist ? 0 : 1;
+    } else {
+      dead = m.nscr[(size_t)h.parent * 4 + 2] == 7 ? 1 : 0;
+    }
+    if (dead) {
+      m.nscr[(size_t)node * 4 + 2] = 7;
+      h.has_sw = 0;
+      for (int j = 0; j < m.W; j++) clu_zero(m.pcrs[(size_t)node * m.W + j]);
+      if (level == 0) m.in_slide[node] = 0;
+    }
+  }
+}
+__global__ void k_clear_mark(int nw, const int* __restrict__ work, DevMap m) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x)
+    m.nscr[(size_t)work[q] * 4 + 2] = -1;
+}
+__global__ void k_slide_compact(int n, const int* __restrict__ old, DevMap m) {
+  // single block, order-preserving compaction of the slide list
+  __shared__ int base;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  for (int start = 0; start < n; start += blockDim.x) {
+    int q = start + threadIdx.x;
+    int keep = (q < n && m.in_slide[old[q]]) ? 1 : 0;
+    // block-wide exclusive scan of keep
+    __shared__ int sc[1024];
+    sc[threadIdx.x] = keep;
+    __syncthreads();
+    for (int off = 1; off < (int)blockDim.x; off <<= 1) {
+      int v = threadIdx.x >= (unsigned)off ? sc[threadIdx.x - off] : 0;
+      __syncthreads();
+      sc[threadIdx.x] += v;
+      __syncthreads();
+    }
+    if (keep) m.slide[base + sc[threadIdx.x] - 1] = old[q];
+    __syncthreads();
+    if (threadIdx.x == blockDim.x - 1) base += sc[threadIdx.x];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) m.counters[kCntSlide] = base;
+}
+__global__ void k_set_jour(int n, const int* __restrict__ slide, double* jour, double j) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) jour[slide[q]] = j;
+}
+
+int map_margi(vg_ctx* ctx, const MP& mp, const WinD& win, int n_oldest, int thread_num, double jour) {
+  DevMap& m = ctx->map;
+  Work& w = ctx->wk;
+  hipStream_t s = ctx->stream;
+  VG_TRY(read_counters(ctx));
+  const int nslide = ctx->h_pinned[kCntSlide];
+  if (nslide < thread_num) return VG_OK;  // local_mapping.cpp:26-28
+  WinD* dwin = (WinD*)ctx->ba.xs;
+  VG_HIP(hipMemcpyAsync(dwin, &win, sizeof(WinD), hipMemcpyHostToDevice, s));
+  k_set_jour<<<grid_for(nslide), kBlock, 0, s>>>(nslide, m.slide, m.jour, jour);
+  // level lists: store them back to back in list1 (offsets on host)
+  std::vector<int> lvl_off(1, 0), lvl_n;
+  VG_HIP(hipMemcpyAsync(w.list1, m.slide, (size_t)nslide * sizeof(int), hipMemcpyDeviceToDevice, s));
+  VG_HIP(hipMemsetAsync(m.counters + kCntLeaves, 0, sizeof(int), s));
+  int cur_off = 0, cur_n = nslide;
+  for (int level = 0; level < 8 && cur_n > 0; level++) {
+    lvl_n.push_back(cur_n);
+    VG_HIP(hipMemsetAsync(m.counters + kCntNext, 0, sizeof(int), s));
+    k_collect_level<<<grid_for(cur_n), kBlock, 0, s>>>(cur_n, w.list1 + cur_off, m, w.list1 + cur_off + cur_n,
+                                                      w.list0);
+    VG_TRY(read_counters(ctx));
+    cur_off += cur_n;
+    lvl_off.push_back(cur_off);
+    cur_n = ctx->h_pinned[kCntNext];
+    if (cur_off + cur_n > m.cap_nodes) {
+      ctx->err = "margi level list overflow";
+      return VG_E_CAPACITY;
+    }
+  }
+  const int nleaves = ctx->h_pinned[kCntLeaves];
+  // oldest slot segments by leaf
+  const int s0 = win.mp[0];
+  if (n_oldest > 0) {
+    k_margi_keys<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, s0, m, w.k0);
+    VG_TRY(sort_keys(ctx, w.k0, w.k1, n_oldest, 64));
+    k_margi_segs<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, w.k1, m);
+  }
+  if (nleaves > 0) {
+    k_margi_leaf<<<grid_for(nleaves), kBlock, 0, s>>>(nleaves, w.list0, w.k1, mp, dwin, m, ctx->ba.fac_eig,
+                                                    ctx->ba.fac_pcr);
+  }
+  if (n_oldest > 0) k_margi_segs_clear<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, w.k1, m);
+  // bottom-up isexist for internal nodes
+  for (int l = (int)lvl_n.size() - 1; l >= 0; l--)
+    k_margi_internal<<<grid_for(lvl_n[l]), kBlock, 0, s>>>(lvl_n[l], w.list1 + lvl_off[l], m);
+  // erase dead roots and clear their subtrees' SlideWindows
+  for (int l = 0; l < (int)lvl_n.size(); l++)
+    k_margi_erase_mark<<<grid_for(lvl_n[l]), kBlock, 0, s>>>(lvl_n[l], w.list1 + lvl_off[l], m, l, jour);
+  for (int l = 0; l < (int)lvl_n.size(); l++)
+    k_clear_mark<<<grid_for(lvl_n[l]), kBlock, 0, s>>>(lvl_n[l], w.list1 + lvl_off[l], m);
+  k_slide_compact<<<1, 1024, 0, s>>>(nslide, w.list1, m);
+  VG_HIP(hipGetLastError());
+  return read_counters(ctx);
+}
+
+}  // namespace vg

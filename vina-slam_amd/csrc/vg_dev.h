@@ -1,0 +1,172 @@
+// vg_dev.h — device-side helpers shared by the map, IEKF and BA kernels.
+#pragma once
+#include "vg_internal.h"
+
+namespace vg {
+
+__device__ __forceinline__ M3 ld_m3(const double* a) {
+  M3 m;
+  for (int i = 0; i < 9; i++) m[i] = a[i];
+  return m;
+}
+__device__ __forceinline__ V3 ld_v3(const double* a) { return v3(a[0], a[1], a[2]); }
+
+// voxel key rule for double coordinates (voxel_map.cpp:57-65, 246-253)
+__device__ __forceinline__ int64_t key_axis_d(double c, double size) {
+  float l = (float)(c / size);
+  if (l < 0) l -= 1;
+  return (int64_t)l;
+}
+__device__ __forceinline__ bool pack_key(const V3& w, double size, uint64_t& out) {
+  int64_t k[3];
+  bool ok = true;
+  for (int j = 0; j < 3; j++) {
+    k[j] = key_axis_d(w[j], size) + kKeyOff;
+    ok &= (k[j] >= 0) & (k[j] < 2 * kKeyOff);
+  }
+  out = ok ? (((uint64_t)k[0] << 42) | ((uint64_t)k[1] << 21) | (uint64_t)k[2]) : 0;
+  return ok;
+}
+__device__ __forceinline__ int64_t unpack_axis(uint64_t key, int sh) {
+  return (int64_t)((key >> sh) & ((1ull << 21) - 1)) - kKeyOff;
+}
+__device__ __forceinline__ uint32_t hash_slot(uint64_t k, int mask) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return (uint32_t)k & (uint32_t)mask;
+}
+// open-addressing lookup of a root voxel: node id or -1
+__device__ __forceinline__ int hash_find(const uint64_t* __restrict__ hkey, const int* __restrict__ hval, int mask,
+                                         uint64_t key) {
+  uint32_t s = hash_slot(key, mask);
+  for (int probe = 0; probe <= mask; probe++) {
+    uint64_t k = hkey[s];
+    if (k == key) return hval[s];
+    if (k == kKeyEmpty) return -1;
+    s = (s + 1) & (uint32_t)mask;
+  }
+  return -1;
+}
+// insert-or-find; returns the slot, sets fresh if this thread inserted the key
+__device__ __forceinline__ int hash_insert(uint64_t* hkey, int mask, uint64_t key, bool& fresh) {
+  uint32_t s = hash_slot(key, mask);
+  fresh = false;
+  for (int probe = 0; probe <= mask; probe++) {
+    unsigned long long prev = atomicCAS((unsigned long long*)&hkey[s], (unsigned long long)kKeyEmpty,
+                                        (unsigned long long)key);
+    if (prev == kKeyEmpty) {
+      fresh = true;
+      return (int)s;
+    }
+    if (prev == key) return (int)s;
+    s = (s + 1) & (uint32_t)mask;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ int octant(const V3& p, const double* c) {
+  return 4 * (p[0] > c[0] ? 1 : 0) + 2 * (p[1] > c[1] ? 1 : 0) + (p[2] > c[2] ? 1 : 0);
+}
+
+// calcBodyVar — point_utils.cpp:3-34 (modifies pb[2] when 0, like the reference)
+__device__ __forceinline__ M3 calc_body_var(V3& pb, float range_inc, float degree_inc) {
+  if (pb[2] == 0) pb[2] = 0.0001;
+  float range = sqrt(pb[0] * pb[0] + pb[1] * pb[1] + pb[2] * pb[2]);
+  float range_var = range_inc * range_inc;
+  double s = sin(degree_inc * M_PI / 180.0);
+  double dv = s * s;
+  double nb = norm3(pb);
+  V3 d = v3(pb[0] / nb, pb[1] / nb, pb[2] / nb);
+  M3 dhat = hat(d);
+  V3 b1 = v3(1, 1, -(d[0] + d[1]) / d[2]);
+  double n1 = norm3(b1);
+  b1 = v3(b1[0] / n1, b1[1] / n1, b1[2] / n1);
+  V3 b2 = cross3(b1, d);
+  double n2 = norm3(b2);
+  b2 = v3(b2[0] / n2, b2[1] / n2, b2[2] / n2);
+  M<3, 2> Nm;
+  Nm(0, 0) = b1[0]; Nm(0, 1) = b2[0];
+  Nm(1, 0) = b1[1]; Nm(1, 1) = b2[1];
+  Nm(2, 0) = b1[2]; Nm(2, 1) = b2[2];
+  M<3, 2> A = mul(scl(dhat, (double)range), Nm);
+  M<2, 2> D;
+  D.zero();
+  D(0, 0) = dv;
+  D(1, 1) = dv;
+  V3 dr = v3(d[0] * (double)range_var, d[1] * (double)range_var, d[2] * (double)range_var);
+  return add(outer3(dr, d), mul(mul(A, D), tr(A)));
+}
+
+// var_init (point_utils.cpp:36-52) for one raw point: body pnt (after the
+// extrinsic) and its covariance.
+__device__ __forceinline__ void var_init_pt(const MP& mp, float x, float y, float z, V3& pnt, M3& var) {
+  V3 pb = v3(x, y, z);
+  M3 vb = calc_body_var(pb, mp.dept, mp.beam);
+  M3 eR = ld_m3(mp.extR);
+  pnt = rigid(eR, pb, ld_v3(mp.extt));
+  var = mul(mul(eR, vb), tr(eR));
+}
+
+// pvec_update world covariance (point_utils.cpp:60): R v R^T + [p] S_R [p]^T + S_t
+__device__ __forceinline__ M3 world_var(const M3& R, const M3& var, const V3& pnt, const M3& rot_var,
+                                        const M3& tsl_var) {
+  M3 ph = hat(pnt);
+  return add(add(mul(mul(R, var), tr(R)), mul(mul(ph, rot_var), tr(ph))), tsl_var);
+}
+
+// cov_add += Bf_var(pv, vec) (octree.cpp:83-92) on packed upper 9x9
+__device__ __forceinline__ void bf_var_acc(double* __restrict__ cov, const M3& var, const V3& v) {
+  M<6, 3> Bi;
+  Bi.zero();
+  Bi(0, 0) = 2 * v[0];
+  Bi(1, 0) = v[1]; Bi(1, 1) = v[0];
+  Bi(2, 0) = v[2]; Bi(2, 2) = v[0];
+  Bi(3, 1) = 2 * v[1];
+  Bi(4, 1) = v[2]; Bi(4, 2) = v[1];
+  Bi(5, 2) = 2 * v[2];
+  M<6, 3> Bu = mul(Bi, var);
+  M6 B66 = mul(Bu, tr(Bi));
+  int k = 0;
+  for (int r = 0; r < 9; r++)
+    for (int c = r; c < 9; c++, k++) {
+      double val;
+      if (r < 6 && c < 6) val = B66(r, c);
+      else if (r < 6) val = Bu(r, c - 6);
+      else val = var(r - 6, c - 6);
+      cov[k] += val;
+    }
+}
+
+__device__ __forceinline__ M<9, 9> unpack9(const double* cov) {
+  M<9, 9> m;
+  int k = 0;
+  for (int r = 0; r < 9; r++)
+    for (int c = r; c < 9; c++, k++) {
+      m(r, c) = cov[k];
+      m(c, r) = cov[k];
+    }
+  return m;
+}
+
+__device__ __forceinline__ void init_node(NodeHdr& h, const double c[3], float qlen, int layer, int parent) {
+  for (int j = 0; j < 3; j++) h.center[j] = c[j];
+  for (int j = 0; j < 8; j++) h.child[j] = -1;
+  h.qlen = qlen;
+  h.layer = (int8_t)layer;
+  h.octo = 0;
+  h.isexist = 0;
+  h.is_plane = 0;
+  h.has_sw = 0;
+  h.pad0 = h.pad1 = h.pad2 = 0;
+  h.opt_state = -1;
+  h.last_num = 0;
+  h.fix_off = 0;
+  h.fix_cnt = 0;
+  h.fix_cap = 0;
+  h.parent = parent;
+}
+
+}  // namespace vg

@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 #include "../../include/vina_gpu.h"
+#include "vg_la.h"
 
 #define VG_HIP(call)                                                                    \
   do {                                                                                  \
@@ -39,12 +40,20 @@ inline int grid_for(long n, int block = kBlock, int cap = 8192) {
 }
 
 // Bump allocator over one hipMalloc'd slab (16-byte aligned carve-outs).
+// In measure mode (base == nullptr) take() only accumulates the size and hands
+// out placeholder addresses, so vg_create can size the slab exactly.
 struct Arena {
   char* base = nullptr;
   size_t size = 0, used = 0;
+  bool measure = false;
   template <class T>
   T* take(size_t n) {
     size_t b = (n * sizeof(T) + 255) & ~size_t(255);
+    if (measure) {
+      T* p = (T*)(uintptr_t)(4096 + used);
+      used += b;
+      return p;
+    }
     if (used + b > size) return nullptr;
     T* p = (T*)(base + used);
     used += b;
@@ -62,6 +71,87 @@ struct DownsampleBufs {
   size_t tmp_bytes = 0;
 };
 
+// ---- device-resident voxel map (replaces unordered_map<VOXEL_LOC, OctoTree*>
+// surf_map, octree.hpp:21-97, slide_window.hpp:6-20) ----
+struct NodeHdr {            // 96 B: everything the correspondence descent reads
+  double center[3];         // voxel_center
+  int child[8];             // leaves[8] (-1 = none)
+  float qlen;               // quater_length
+  int8_t layer, octo, isexist, is_plane;
+  int8_t has_sw, pad0, pad1, pad2;
+  int opt_state, last_num;
+  int fix_off, fix_cnt, fix_cap;
+  int parent;
+};
+struct PlaneRec {           // 224 B: Plane (plane.hpp:5-24) as read by OctoTree::match
+  double center[3], normal[3];
+  double var[21];           // plane_var, packed upper 6x6
+  float radius;
+  int pad;
+};
+constexpr int kCovN = 45;   // cov_add packed upper 9x9
+
+struct DevMap {
+  int cap_nodes = 0, cap_fix = 0, hash_mask = 0, W = 0, cap_wp = 0;
+  NodeHdr* hdr = nullptr;
+  PlaneRec* pl = nullptr;
+  Clu* pcr_add = nullptr;
+  Clu* pcr_fix = nullptr;
+  double* cov_add = nullptr;   // cap_nodes * 45
+  double* eig = nullptr;       // cap_nodes * 12 (eig_value 3, eig_vector 9 row-major)
+  double* jour = nullptr;
+  Clu* pcrs = nullptr;         // cap_nodes * W (SlideWindow::pcrs_local, physical slot)
+  int* nscr = nullptr;         // per-node scratch (cap_nodes * 4)
+  int* cfirst = nullptr;       // per-node per-octant first-event scratch (cap_nodes * 8)
+  uint64_t* hkey = nullptr;    // root hash
+  int* hval = nullptr;
+  int* hfirst = nullptr;
+  int* slide = nullptr;        // surf_map_slide (root ids)
+  uint8_t* in_slide = nullptr;
+  double* fix_pnt = nullptr;   // point_fix arena: pnt (world) 3, var 6
+  double* fix_var = nullptr;
+  double* wp_pnt = nullptr;    // window points per physical slot: body pnt
+  double* wp_var = nullptr;    // world var (after pvec_update), packed 6
+  int* wp_leaf = nullptr;      // leaf holding the point in its list, -1 = not listed
+  int* counters = nullptr;     // device counters (see kCnt*)
+};
+enum {
+  kCntNodes = 0, kCntFix = 1, kCntSlide = 2, kCntNew = 3, kCntTouched = 4, kCntWork = 5, kCntNext = 6,
+  kCntSub = 7, kCntEvents = 8, kCntFactors = 9, kCntCreate = 10, kCntErr = 11, kCntLeaves = 12, kCntMisc = 13,
+  kCntN = 16
+};
+
+// per-scan work buffers
+struct Work {
+  int cap = 0;                 // entries
+  uint64_t *k0 = nullptr, *k1 = nullptr;
+  uint32_t *v0 = nullptr, *v1 = nullptr;
+  uint32_t *u0 = nullptr, *u1 = nullptr;
+  uint32_t* evsrc = nullptr;   // subdivision event source index
+  uint32_t *ac_cnt = nullptr, *ac_off = nullptr;  // child allocation scratch
+  int *list0 = nullptr, *list1 = nullptr, *list2 = nullptr, *cand = nullptr;
+  int* leaf = nullptr;         // per ds point leaf / per event target
+  double* pw = nullptr;        // per ds point world coords
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  double* partials = nullptr;  // reduction partials
+  int* iekf_cache = nullptr;   // per raw point cached leaf
+  int nparts = 0;
+};
+
+// BA device buffers
+struct BaBufs {
+  int cap_f = 0;
+  int* fac_node = nullptr;
+  double* fac_eig = nullptr;   // trial eig values/vectors (12) per factor
+  Clu* fac_pcr = nullptr;      // trial merged cluster per factor
+  double* fac_comp = nullptr;  // per factor compressed Hessian inputs
+  double* hpart = nullptr;     // chunk partials
+  double* hout = nullptr;      // reduced 60x60 upper + 60 + 1
+  double* rpart = nullptr;
+  double* xs = nullptr;        // window poses (W x 12: R9 p3)
+};
+
 }  // namespace vg
 
 struct vg_ctx {
@@ -74,11 +164,44 @@ struct vg_ctx {
   // raw scan staging (SoA)
   float *d_x = nullptr, *d_y = nullptr, *d_z = nullptr, *d_i = nullptr;
   vg::DownsampleBufs ds;
+  vg::DevMap map;
+  vg::Work wk;
+  vg::BaBufs ba;
   int* h_pinned = nullptr;  // small pinned host scratch for counters
+  double* h_pinned_d = nullptr;
   vg_stats stats;
+  void* host = nullptr;     // host-side pipeline state (pipeline.cpp)
 };
 
 namespace vg {
+// Hot-path parameters in kernel-argument form (node.cpp:52-291 values).
+struct MP {
+  double vs;          // Odometry.voxel_size
+  double min_eig;     // Odometry.min_eigen_value
+  double thre[4];     // 1 / LocalBA.plane_eigen_value_thre (node.cpp:256-259)
+  double minpt[4];    // min_point (node.cpp:219)
+  double extR[9], extt[3];
+  float dept, beam;   // dept_err / beam_err as the float params of calcBodyVar
+  int max_layer, max_points, W, pad;
+};
+
+struct WinD {           // window poses x_buf (by ord) and the ring mp[] (octree.cpp:75)
+  double R[32][9];
+  double p[32][3];
+  int mp[32];
+  int win_count;
+  int pad;
+};
+
+struct IekfPose {
+  double R[9], p[3], rot_var[9], tsl_var[9];
+};
+
+struct InsPose {
+  double R[9], p[3], rot_var[9], tsl_var[9];
+};
+
+
 // downsample.hip
 int ds_alloc(vg_ctx* ctx);
 // Voxel-grid downsample of a device-resident SoA cloud; results land in
@@ -86,4 +209,30 @@ int ds_alloc(vg_ctx* ctx);
 // (returns n_out).
 int ds_run(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, int n, double voxel,
            int* n_out);
+// map.hip
+int map_alloc(vg_ctx* ctx);
+int map_reset(vg_ctx* ctx);
+int iekf_reset_cache(vg_ctx* ctx, int n);
+int iekf_iter(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n,
+              const IekfPose& pose, double* out34);
+int map_insert(vg_ctx* ctx, const MP& mp, int slot, const InsPose& pose, int n, int epoch, int thread_num,
+               int* roots_new, int* touched);
+int map_recut(vg_ctx* ctx, const MP& mp, const WinD& win, const int* nper, int thread_num, int* n_factors);
+int map_margi(vg_ctx* ctx, const MP& mp, const WinD& win, int n_oldest, int thread_num, double jour);
+// ba.hip
+constexpr int kBaX = 24;        // per-frame state: R 9, p 3, v 3, bg 3, ba 3, g 3
+constexpr int kBaImuRec = 64 + 225;
+int ba_alloc(vg_ctx* ctx);
+int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double* imurec, double* bias_io,
+           int* iters);
+// pipeline.cpp
+void host_init(vg_ctx* ctx);
+void host_free(vg_ctx* ctx);
+void host_reset(vg_ctx* ctx);
+void host_seed(vg_ctx* ctx, const double* s);
+void host_state(vg_ctx* ctx, double* s);
+int host_window(vg_ctx* ctx, double* out);
+int host_traj(vg_ctx* ctx, double* out, int cap);
+int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n, double beg,
+              double end, const double* imu, int m);
 }  // namespace vg

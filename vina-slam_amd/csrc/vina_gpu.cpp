@@ -49,19 +49,40 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     ctx->err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
-  const size_t n = (size_t)ctx->cap.max_points_per_scan;
-  size_t need = n * 120 + (64ull << 20);
+  // size the slab exactly (measure pass), then carve it for real
+  auto carve = [&]() -> int {
+    const size_t n = (size_t)ctx->cap.max_points_per_scan;
+    ctx->d_x = ctx->arena.take<float>(n);
+    ctx->d_y = ctx->arena.take<float>(n);
+    ctx->d_z = ctx->arena.take<float>(n);
+    ctx->d_i = ctx->arena.take<float>(n);
+    int r = ds_alloc(ctx);
+    if (r == VG_OK) r = map_alloc(ctx);
+    if (r == VG_OK) r = ba_alloc(ctx);
+    return r;
+  };
+  ctx->arena.measure = true;
+  int r = carve();
+  if (r != VG_OK) return fail(r);
+  size_t need = ctx->arena.used + (1 << 20);
+  ctx->arena = vg::Arena();
   if ((e = hipMalloc((void**)&ctx->arena.base, need)) != hipSuccess) {
-    ctx->err = std::string("hipMalloc arena: ") + hipGetErrorString(e);
+    ctx->err = std::string("hipMalloc arena (") + std::to_string(need >> 20) + " MiB): " + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
   ctx->arena.size = need;
-  ctx->d_x = ctx->arena.take<float>(n);
-  ctx->d_y = ctx->arena.take<float>(n);
-  ctx->d_z = ctx->arena.take<float>(n);
-  ctx->d_i = ctx->arena.take<float>(n);
-  int r = ds_alloc(ctx);
+  if ((e = hipMemsetAsync(ctx->arena.base, 0, need, ctx->stream)) != hipSuccess) {
+    ctx->err = std::string("hipMemset arena: ") + hipGetErrorString(e);
+    return fail(VG_E_HIP);
+  }
+  r = carve();
+  if (r == VG_OK) r = map_reset(ctx);
   if (r != VG_OK) return fail(r);
+  if ((e = hipHostMalloc((void**)&ctx->h_pinned_d, 4096, hipHostMallocDefault)) != hipSuccess) {
+    ctx->err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
+    return fail(VG_E_HIP);
+  }
+  host_init(ctx);
   *out = ctx;
   return VG_OK;
 }
@@ -71,6 +92,8 @@ int vg_destroy(vg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->arena.base) (void)hipFree(ctx->arena.base);
   if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+  if (ctx->h_pinned_d) (void)hipHostFree(ctx->h_pinned_d);
+  if (ctx->host) host_free(ctx);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return VG_OK;
@@ -82,6 +105,8 @@ void* vg_stream(vg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 int vg_reset(vg_ctx* ctx) {
   if (!ctx) return VG_E_ARG;
+  VG_TRY(map_reset(ctx));
+  host_reset(ctx);
   return VG_OK;
 }
 
@@ -140,27 +165,35 @@ int vg_downsample(vg_ctx* ctx, const float* xyz, const float* intensity, int n, 
 
 int vg_seed(vg_ctx* ctx, const double* state) {
   if (!ctx || !state) return VG_E_ARG;
-  ctx->err = "vg_seed: not implemented yet";
-  return VG_E_STATE;
+  host_seed(ctx, state);
+  return VG_OK;
 }
 
-int vg_step(vg_ctx* ctx, const float*, const float*, int, double, double, const double*, int) {
-  if (!ctx) return VG_E_ARG;
-  ctx->err = "vg_step: not implemented yet";
-  return VG_E_STATE;
+int vg_step(vg_ctx* ctx, const float* xyz, const float* intensity, int n, double pcl_beg_time,
+            double pcl_end_time, const double* imu, int m) {
+  if (!ctx || (!xyz && n > 0) || n < 0 || m < 0 || (m > 0 && !imu)) return VG_E_ARG;
+  if (n > ctx->cap.max_points_per_scan) {
+    ctx->err = "scan larger than max_points_per_scan";
+    return VG_E_CAPACITY;
+  }
+  if (n > 0) VG_TRY(upload_aos(ctx, xyz, intensity, n));
+  return host_step(ctx, ctx->d_x, ctx->d_y, ctx->d_z, ctx->d_i, n, pcl_beg_time, pcl_end_time, imu, m);
 }
 
-int vg_step_dev(vg_ctx* ctx, const float*, const float*, const float*, const float*, int, double, double,
-                const double*, int) {
-  if (!ctx) return VG_E_ARG;
-  ctx->err = "vg_step_dev: not implemented yet";
-  return VG_E_STATE;
+int vg_step_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, const float* d_intensity, int n,
+                double pcl_beg_time, double pcl_end_time, const double* imu, int m) {
+  if (!ctx || n < 0 || m < 0 || (m > 0 && !imu) || (n > 0 && (!d_x || !d_y || !d_z))) return VG_E_ARG;
+  if (n > ctx->cap.max_points_per_scan) {
+    ctx->err = "scan larger than max_points_per_scan";
+    return VG_E_CAPACITY;
+  }
+  return host_step(ctx, d_x, d_y, d_z, d_intensity, n, pcl_beg_time, pcl_end_time, imu, m);
 }
 
-int vg_get_state(vg_ctx* ctx, double*) {
-  if (!ctx) return VG_E_ARG;
-  ctx->err = "vg_get_state: not implemented yet";
-  return VG_E_STATE;
+int vg_get_state(vg_ctx* ctx, double* state) {
+  if (!ctx || !state) return VG_E_ARG;
+  host_state(ctx, state);
+  return VG_OK;
 }
 
 int vg_get_stats(vg_ctx* ctx, vg_stats* out) {
@@ -169,9 +202,15 @@ int vg_get_stats(vg_ctx* ctx, vg_stats* out) {
   return VG_OK;
 }
 
-int vg_window_states(vg_ctx* ctx, double*, int* n) {
+int vg_window_states(vg_ctx* ctx, double* out, int* n) {
+  if (!ctx || !n || !out) return VG_E_ARG;
+  *n = host_window(ctx, out);
+  return VG_OK;
+}
+
+int vg_trajectory(vg_ctx* ctx, double* out, int cap, int* n) {
   if (!ctx || !n) return VG_E_ARG;
-  *n = 0;
+  *n = host_traj(ctx, out, cap);
   return VG_OK;
 }
 

@@ -69,6 +69,7 @@ def lib():
         L.vg_get_state.argtypes = [P, dp]
         L.vg_get_stats.argtypes = [P, ctypes.POINTER(Stats)]
         L.vg_window_states.argtypes = [P, dp, ip]
+        L.vg_trajectory.argtypes = [P, dp, ctypes.c_int, ip]
         L.vg_stream.argtypes = [P]
         L.vg_stream.restype = P
         _lib = L
@@ -151,6 +152,13 @@ class Context:
         out = np.zeros((64, STATE_LEN))
         n = ctypes.c_int(0)
         self._chk(lib().vg_window_states(self.h, _d(out), ctypes.byref(n)), "vg_window_states")
+        return out[: n.value]
+
+    def trajectory(self):
+        n = ctypes.c_int(0)
+        self._chk(lib().vg_trajectory(self.h, None, 0, ctypes.byref(n)), "vg_trajectory")
+        out = np.zeros((max(n.value, 1), 13))
+        self._chk(lib().vg_trajectory(self.h, _d(out), n.value, ctypes.byref(n)), "vg_trajectory")
         return out[: n.value]
 
     def stream(self):
