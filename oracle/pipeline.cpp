@@ -372,7 +372,6 @@ struct Pipeline {
     auto t3 = clk::now();
     multi_recut();
     st.n_factors = (int)voxhess.plvec_voxels.size();
-    st.n_slide = (int)surf_map_slide.size();
     auto t4 = clk::now();
     auto t5 = t4, t6 = t4;
     if (win_count >= cfg.win_size) {
@@ -413,6 +412,7 @@ struct Pipeline {
       win_count -= mgsize;
     }
     first = false;
+    st.n_slide = (int)surf_map_slide.size();
     auto t7 = clk::now();
     if (timing) {
       auto d = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); };

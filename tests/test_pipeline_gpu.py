@@ -36,11 +36,15 @@ def run_pair(cfgname, lidar, nscan, seq_id=0, max_points=300_000):
 @pytest.mark.parametrize("cfgname,lidar,nscan", [("mid360", "16line", 16), ("HILTI", "16line", 12)])
 def test_pipeline_matches_oracle(oracle_lib, cfgname, lidar, nscan):
     seq, orc, gpu, so, sg = run_pair(cfgname, lidar, nscan)
+    to, tg = orc.trajectory(), gpu.trajectory()
+    for k, (a, b) in enumerate(zip(so, sg)):
+        print(k, "dpos %.3e" % np.linalg.norm(to[k, 10:13] - tg[k, 10:13]),
+              {key: (a[key], b[key]) for key in ("n_ds", "roots_new", "n_slide", "n_factors", "ba_iters", "iekf_iters")},
+              "matches", a["iekf_matches"], b["iekf_matches"])
     for k, (a, b) in enumerate(zip(so, sg)):
         assert a["n_raw"] == b["n_raw"] and a["n_ds"] == b["n_ds"], (k, a, b)
         assert a["roots_new"] == b["roots_new"], (k, a, b)
         assert a["n_slide"] == b["n_slide"], (k, a, b)
-    to, tg = orc.trajectory(), gpu.trajectory()
     assert to.shape == tg.shape
     err = synth.ate(to, tg)
     print("ATE gpu vs oracle: %.3e m" % err, "factors", [s["n_factors"] for s in sg], [s["n_factors"] for s in so])
