@@ -1,0 +1,162 @@
+"""Benchmark: scans/s of the full per-scan LIO hot path (downsample + voxel-map
+correspondence + IEKF + map maintenance + LM solve) on synthetic LiDAR-inertial
+sequences, MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--lidar 64line] [--config mid360]
+
+N > 1 is launched by torch.distributed.run: one process per GPU, each running an
+independent sequence (replica mode, "scaling": "weak" — the path has no
+cross-sequence exchange). Timed region: K scans after W warm-up scans (the
+window must fill before BA/margi run), bracketed by barrier + synchronize;
+max over ranks. Inputs are resident in HBM before timing starts.
+
+Rank 0 at N = 1 also times the CPU restatement (oracle, test infrastructure) on
+a bounded sample of the same sequence: the cpu_baseline object.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "vina-slam_amd", "py"))
+
+import numpy as np  # noqa: E402
+
+METRIC = "scans/sec (downsample+kNN+LM solve), 64-line LiDAR, 1/2/4/8 MI355X; ATE vs CPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=12)
+    ap.add_argument("--lidar", default="64line")
+    ap.add_argument("--config", default="mid360")
+    ap.add_argument("--cpu-scans", type=int, default=24, help="oracle sample: scans timed after its own warm-up")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--seq", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import synth
+    import vgconfig
+    import vgpu
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    p = vgconfig.load(args.config)
+    g = p["General"]
+    seq = synth.Sequence(args.lidar, args.seq + rank, blind=g["blind"], ext_R=g["extrinsic_rota"],
+                         ext_t=g["extrinsic_tran"])
+    total = args.warmup + args.steps
+    scans, imus = [], []
+    for k in range(total):
+        xyz, inten, b, e = seq.scan(k)
+        t = torch.from_numpy(np.ascontiguousarray(np.concatenate([xyz.T, inten[None]], 0))).to(dev)
+        scans.append((t, xyz.shape[0], b, e))
+        imus.append(seq.imu(k))
+    npts = int(np.mean([s[1] for s in scans]))
+    ctx = vgpu.Context(vgconfig.to_c(p), device=local, max_points=max(s[1] for s in scans) + 16)
+    ctx.seed(seq.gt_state(0))
+    torch.cuda.synchronize(dev)
+
+    def run(k):
+        t, n, b, e = scans[k]
+        ctx.step_dev(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), n, b, e, imus[k])
+
+    for k in range(args.warmup):
+        run(k)
+    ctx.profile(True)
+    stats = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.warmup, total):
+        run(k)
+        stats.append(ctx.stats())
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    prof = ctx.profile_read()
+    if world > 1:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    value = world * args.steps / dt
+
+    # roofline of the dominant kernel (IEKF point loop, k_iekf): algorithmic
+    # bytes per launch = 16 B per raw point (fp32 xyz + cached leaf id read)
+    # + 4 B per matched point (cached leaf write); plane/node records are
+    # cache-resident and not counted (lower bound)
+    iek = prof["iekf"]
+    n_launch = iek["launches"]
+    pts = sum(s["n_raw"] * s["iekf_iters"] for s in stats)
+    matched = sum(sum(s["iekf_matches"][: s["iekf_iters"]]) for s in stats)
+    bytes_tot = 16.0 * pts + 4.0 * matched
+    avg_s = iek["ms"] * 1e-3 / max(n_launch, 1)
+    achieved = (bytes_tot / max(n_launch, 1)) / avg_s / 1e9 if avg_s > 0 else 0.0
+    roof = {"kernel": "k_iekf", "bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0, "unit": "GB/s",
+            "frac": round(achieved / 8000.0, 5), "traffic": None, "avg_launch_us": round(avg_s * 1e6, 3),
+            "launches": n_launch, "stage_ms_per_scan": {k: round(v["ms"] / args.steps, 4) for k, v in prof.items()}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(args, p, seq)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "scans/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": "synthetic-%s@%s.yaml" % (args.lidar, args.config), "lidar": args.lidar,
+                       "points_per_scan": npts, "downsampled_per_scan": int(np.mean([s["n_ds"] for s in stats])),
+                       "factors_per_scan": int(np.mean([s["n_factors"] for s in stats])),
+                       "parallelism": "replica x%d" % world},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, p, seq):
+    """Time the CPU restatement (oracle) on a bounded sample of the same sequence."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # test infrastructure: the baseline leg only
+    import vgconfig
+
+    oracle.build()
+    pl = oracle.Pipeline(vgconfig.to_c(p, use_threads=1, vnc_prep=1))
+    pl.seed(seq.gt_state(0))
+    warm = min(args.warmup, 12)
+    times = []
+    for k in range(warm + args.cpu_scans):
+        xyz, it, b, e = seq.scan(k)
+        tm = pl.step(xyz, it, b, e, seq.imu(k))
+        if k >= warm:
+            times.append(tm[6])
+    tot = float(np.sum(times))
+    return {"value": round(len(times) / tot, 3), "unit": "scans/s", "cores": 5, "kind": "port",
+            "sample": "%d scans after %d warm-up scans of the same synthetic %s sequence, %s.yaml; "
+                      "IEKF single-threaded, map/BA 5 std::threads as the reference; median %.1f ms/scan"
+                      % (len(times), warm, args.lidar, args.config, 1e3 * float(np.median(times)))}
+
+
+if __name__ == "__main__":
+    main()

@@ -111,6 +111,13 @@ int vg_window_states(vg_ctx* ctx, double* out, int* n);
  * Copies min(n, cap) rows; *n = total rows. out may be NULL to query. */
 int vg_trajectory(vg_ctx* ctx, double* out, int cap, int* n);
 
+/* Stage timing with HIP events on the context stream (device time). stage:
+ * 0 downsample, 1 IEKF point-loop kernel (k_iekf), 2 map insert, 3 recut +
+ * factor extraction, 4 BA, 5 margi, 6 whole IEKF. vg_profile resets the
+ * accumulators; vg_profile_read returns total ms and the number of intervals. */
+int vg_profile(vg_ctx* ctx, int on);
+int vg_profile_read(vg_ctx* ctx, int stage, double* total_ms, int* count);
+
 /* HIP stream the context enqueues on (hipStream_t as void*). */
 void* vg_stream(vg_ctx* ctx);
 

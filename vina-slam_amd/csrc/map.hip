@@ -265,12 +265,15 @@ int iekf_iter(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const f
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
   int nb = grid_for(n, 256, 512);
+  prof_begin(ctx, kProfIekfKernel);
   k_iekf<<<nb, 256, 0, s>>>(n, x, y, z, mp, pose, ctx->map, w.iekf_cache, w.partials);
+  prof_end(ctx, kProfIekfKernel);
   k_iekf_final<<<1, 64, 0, s>>>(nb, w.partials, w.partials + (size_t)w.nparts * 38);
   VG_HIP(hipGetLastError());
   VG_HIP(hipMemcpyAsync(ctx->h_pinned_d, w.partials + (size_t)w.nparts * 38, kIekfVals * sizeof(double),
                         hipMemcpyDeviceToHost, s));
   VG_HIP(hipStreamSynchronize(s));
+  prof_collect(ctx);
   for (int j = 0; j < kIekfVals; j++) out34[j] = ctx->h_pinned_d[j];
   return VG_OK;
 }

@@ -342,13 +342,17 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   }
   // downsample with the /2 fallback (local_mapping.cpp:396-403)
   int n_ds = 0;
+  prof_begin(ctx, kProfDownsample);
   VG_TRY(ds_run(ctx, dx, dy, dz, di, n, c.down_size, &n_ds));
   if (n_ds < 2000) VG_TRY(ds_run(ctx, dx, dy, dz, di, n, c.down_size / 2, &n_ds));
+  prof_end(ctx, kProfDownsample);
   ctx->stats.n_raw = n;
   ctx->stats.n_ds = n_ds;
   // IEKF on the full deskewed cloud (local_mapping.cpp:408-413)
   int degenerate = 0;
+  prof_begin(ctx, kProfIekf);
   VG_TRY(lio_state_estimation(ctx, P, dx, dy, dz, n, &degenerate));
+  prof_end(ctx, kProfIekf);
   ctx->stats.degenerate = degenerate;
   // trajectory (pub_localtraj / save_pose_tum at local_mapping.cpp:427-430)
   P->traj.push_back(P->x_curr.t);
@@ -376,7 +380,9 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
     }
   P->epoch++;
   int roots_new = 0, touched = 0;
+  prof_begin(ctx, kProfInsert);
   VG_TRY(map_insert(ctx, P->mpd, slot, ip, n_ds, P->epoch, c.thread_num, &roots_new, &touched));
+  prof_end(ctx, kProfInsert);
   P->wp_n[slot] = n_ds;
   ctx->stats.roots_new = roots_new;
   // multi_recut + tras_opt (local_mapping.cpp:451)
@@ -384,7 +390,9 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   int nper[32];
   for (int i = 0; i < P->win_count; i++) nper[i] = P->wp_n[P->mp[i]];
   int nf = 0;
+  prof_begin(ctx, kProfRecut);
   VG_TRY(map_recut(ctx, P->mpd, win, nper, c.thread_num, &nf));
+  prof_end(ctx, kProfRecut);
   ctx->stats.n_factors = nf;
   if (P->win_count >= W) {
     if (c.if_BA == 1) {  // LI_BA_Optimizer::damping_iter (local_mapping.cpp:492-497)
@@ -404,7 +412,9 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
         memcpy(&bias[(size_t)j * 12], P->imu_pre[j].bias, 12 * sizeof(double));
       }
       int iters = 0;
+      prof_begin(ctx, kProfBA);
       VG_TRY(ba_run(ctx, nf, P->mp.data(), xs.data(), rec.data(), bias.data(), &iters));
+      prof_end(ctx, kProfBA);
       ctx->stats.ba_iters = iters;
       for (int j = 0; j < W; j++) {
         HX& h = P->x_buf[j];
@@ -421,7 +431,9 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
     P->x_curr.p = P->x_buf[P->win_count - 1].p;
     // multi_margi (local_mapping.cpp:507)
     WinD w2 = make_win(P);
+    prof_begin(ctx, kProfMargi);
     VG_TRY(map_margi(ctx, P->mpd, w2, P->wp_n[P->mp[0]], c.thread_num, P->jour));
+    prof_end(ctx, kProfMargi);
     const int mgsize = 1;
     if ((P->win_base + P->win_count) % 10 == 0) {
       double spat = norm3(sub(P->x_curr.p, P->last_pos));
@@ -443,6 +455,7 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   P->first = false;
   VG_HIP(hipMemcpyAsync(ctx->h_pinned, ctx->map.counters, kCntN * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   VG_HIP(hipStreamSynchronize(ctx->stream));
+  prof_collect(ctx);
   ctx->stats.n_slide = ctx->h_pinned[kCntSlide];
   ctx->stats.nodes_used = ctx->h_pinned[kCntNodes];
   ctx->stats.fix_used = ctx->h_pinned[kCntFix];

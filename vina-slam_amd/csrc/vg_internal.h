@@ -171,7 +171,39 @@ struct vg_ctx {
   double* h_pinned_d = nullptr;
   vg_stats stats;
   void* host = nullptr;     // host-side pipeline state (pipeline.cpp)
+  // stage timing with HIP events on the context stream (vg_profile)
+  bool prof_on = false;
+  hipEvent_t prof_ev[8][2] = {};
+  bool prof_pending[8] = {};
+  double prof_ms[8] = {};
+  int prof_n[8] = {};
 };
+
+namespace vg {
+enum { kProfDownsample = 0, kProfIekfKernel = 1, kProfInsert = 2, kProfRecut = 3, kProfBA = 4, kProfMargi = 5,
+       kProfIekf = 6, kProfN = 7 };
+inline void prof_begin(vg_ctx* c, int id) {
+  if (c->prof_on) (void)hipEventRecord(c->prof_ev[id][0], c->stream);
+}
+inline void prof_end(vg_ctx* c, int id) {
+  if (c->prof_on) {
+    (void)hipEventRecord(c->prof_ev[id][1], c->stream);
+    c->prof_pending[id] = true;
+  }
+}
+// call only after the stream has been synchronised past the recorded events
+inline void prof_collect(vg_ctx* c) {
+  for (int i = 0; i < kProfN; i++)
+    if (c->prof_pending[i]) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, c->prof_ev[i][0], c->prof_ev[i][1]) == hipSuccess) {
+        c->prof_ms[i] += ms;
+        c->prof_n[i] += 1;
+      }
+      c->prof_pending[i] = false;
+    }
+}
+}  // namespace vg
 
 namespace vg {
 // Hot-path parameters in kernel-argument form (node.cpp:52-291 values).

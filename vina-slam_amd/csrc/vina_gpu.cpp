@@ -82,6 +82,12 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     ctx->err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 2; j++)
+      if ((e = hipEventCreate(&ctx->prof_ev[i][j])) != hipSuccess) {
+        ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
+        return fail(VG_E_HIP);
+      }
   host_init(ctx);
   *out = ctx;
   return VG_OK;
@@ -94,6 +100,9 @@ int vg_destroy(vg_ctx* ctx) {
   if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
   if (ctx->h_pinned_d) (void)hipHostFree(ctx->h_pinned_d);
   if (ctx->host) host_free(ctx);
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 2; j++)
+      if (ctx->prof_ev[i][j]) (void)hipEventDestroy(ctx->prof_ev[i][j]);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return VG_OK;
@@ -211,6 +220,24 @@ int vg_window_states(vg_ctx* ctx, double* out, int* n) {
 int vg_trajectory(vg_ctx* ctx, double* out, int cap, int* n) {
   if (!ctx || !n) return VG_E_ARG;
   *n = host_traj(ctx, out, cap);
+  return VG_OK;
+}
+
+int vg_profile(vg_ctx* ctx, int on) {
+  if (!ctx) return VG_E_ARG;
+  ctx->prof_on = on != 0;
+  for (int i = 0; i < 8; i++) {
+    ctx->prof_ms[i] = 0;
+    ctx->prof_n[i] = 0;
+    ctx->prof_pending[i] = false;
+  }
+  return VG_OK;
+}
+
+int vg_profile_read(vg_ctx* ctx, int stage, double* total_ms, int* count) {
+  if (!ctx || stage < 0 || stage >= vg::kProfN || !total_ms || !count) return VG_E_ARG;
+  *total_ms = ctx->prof_ms[stage];
+  *count = ctx->prof_n[stage];
   return VG_OK;
 }
 

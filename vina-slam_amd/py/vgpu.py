@@ -70,6 +70,8 @@ def lib():
         L.vg_get_stats.argtypes = [P, ctypes.POINTER(Stats)]
         L.vg_window_states.argtypes = [P, dp, ip]
         L.vg_trajectory.argtypes = [P, dp, ctypes.c_int, ip]
+        L.vg_profile.argtypes = [P, ctypes.c_int]
+        L.vg_profile_read.argtypes = [P, ctypes.c_int, dp, ip]
         L.vg_stream.argtypes = [P]
         L.vg_stream.restype = P
         _lib = L
@@ -160,6 +162,20 @@ class Context:
         out = np.zeros((max(n.value, 1), 13))
         self._chk(lib().vg_trajectory(self.h, _d(out), n.value, ctypes.byref(n)), "vg_trajectory")
         return out[: n.value]
+
+    PROFILE_STAGES = ["downsample", "iekf", "insert", "recut", "ba", "margi", "iekf_total"]
+
+    def profile(self, on=True):
+        self._chk(lib().vg_profile(self.h, 1 if on else 0), "vg_profile")
+
+    def profile_read(self):
+        out = {}
+        for i, name in enumerate(self.PROFILE_STAGES):
+            ms = ctypes.c_double(0)
+            n = ctypes.c_int(0)
+            self._chk(lib().vg_profile_read(self.h, i, ctypes.byref(ms), ctypes.byref(n)), "vg_profile_read")
+            out[name] = {"ms": ms.value, "launches": n.value}
+        return out
 
     def stream(self):
         return lib().vg_stream(self.h)
