@@ -68,7 +68,7 @@ __device__ __forceinline__ void factor_basics(const double* e, const Clu& pcr, d
 }
 
 // acc_evaluate2 per (factor, frame) — factors.cpp:57-97
-__global__ void k_ba_comp(int nf, int W, const int* __restrict__ fac_node, const double* __restrict__ fac_eig,
+__global__ void __launch_bounds__(256) k_ba_comp(int nf, int W, const int* __restrict__ fac_node, const double* __restrict__ fac_eig,
                           const Clu* __restrict__ fac_pcr, const Clu* __restrict__ pcrs, const int* __restrict__ mpring,
                           const double* __restrict__ xs, double* __restrict__ comp, double* __restrict__ compf,
                           const BaState* __restrict__ st) {
@@ -209,14 +209,20 @@ __global__ void __launch_bounds__(256) k_ba_hred(int nf, int W, const double* __
   }
 }
 
-__global__ void k_ba_hfinal(int nchunk, int nout, const double* __restrict__ part, double* __restrict__ out,
-                            const BaState* __restrict__ st) {
+// ordered sum of the chunk partials: 8 lanes per output split the chunks
+// (stride 8), then a fixed 3-step shuffle tree (deterministic)
+__global__ void __launch_bounds__(256) k_ba_hfinal(int nchunk, int nout, const double* __restrict__ part,
+                                                   double* __restrict__ out, const BaState* __restrict__ st) {
   if (st->done || !st->calc_hess) return;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nout; e += gridDim.x * blockDim.x) {
-    double s = 0.0;
-    for (int b = 0; b < nchunk; b++) s += part[(size_t)b * nout + e];
-    out[e] = s;
-  }
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = gt >> 3, sub = gt & 7;
+  double s = 0.0;
+  if (e < nout)
+    for (int b = sub; b < nchunk; b += 8) s += part[(size_t)b * nout + e];
+  s += __shfl_down(s, 4, 8);
+  s += __shfl_down(s, 2, 8);
+  s += __shfl_down(s, 1, 8);
+  if (e < nout && sub == 0) out[e] = s;
 }
 
 // IMU record layout (doubles): R_delta 9, p_delta 3, v_delta 3, R_bg 9, p_bg 9,
@@ -324,7 +330,7 @@ __global__ void __launch_bounds__(256) k_ba_imu(int nimu, const double* __restri
 }
 
 // IMU residuals only (give_evaluate(..., false)) at the trial state
-__global__ void k_ba_imures(int nimu, const double* __restrict__ imurec, const double* __restrict__ bias,
+__global__ void __launch_bounds__(256) k_ba_imures(int nimu, const double* __restrict__ imurec, const double* __restrict__ bias,
                             const double* __restrict__ xt, double* __restrict__ res, const BaState* __restrict__ st) {
   if (st->done) return;
   int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -412,14 +418,18 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, double imu_c
   __syncthreads();
   for (int t = tid; t < n; t += nt) A[lo(t, t)] += u * D[t];
   __syncthreads();
-  // LDL^T with diagonal pivoting (largest remaining |d|), logical order via perm
+  // LDL^T with diagonal pivoting (largest remaining |d|, first index on ties,
+  // as Eigen::LDLT / the oracle): the pivot is swapped physically (symmetric
+  // row+column swap in the packed lower triangle), so every step updates the
+  // contiguous trailing triangle with a 32 x 32 lane tiling.
+  const int tr_ = tid >> 5, tc_ = tid & 31;
   for (int k = 0; k < n; k++) {
     if (tid < 64) {
       double best = -1.0;
-      int bi = k;
+      int bi = n;
       for (int i = k + tid; i < n; i += 64) {
-        double v = fabs(A[lo(perm[i], perm[i])]);
-        if (v > best || (v == best && i < bi)) {
+        double v = fabs(A[lo(i, i)]);
+        if (v > best) {
           best = v;
           bi = i;
         }
@@ -432,51 +442,70 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, double imu_c
           bi = oi;
         }
       }
-      if (tid == 0) {
-        piv = bi;
-        int tmp = perm[k];
-        perm[k] = perm[bi];
-        perm[bi] = tmp;
+      if (tid == 0) piv = bi;
+    }
+    __syncthreads();
+    const int p = piv;
+    if (p != k) {
+      for (int j = tid; j < n; j += nt) {
+        if (j < k) {
+          double t = A[lo(k, j)]; A[lo(k, j)] = A[lo(p, j)]; A[lo(p, j)] = t;
+        } else if (j == k) {
+          double t = A[lo(k, k)]; A[lo(k, k)] = A[lo(p, p)]; A[lo(p, p)] = t;
+          int q = perm[k]; perm[k] = perm[p]; perm[p] = q;
+        } else if (j < p) {
+          double t = A[lo(j, k)]; A[lo(j, k)] = A[lo(p, j)]; A[lo(p, j)] = t;
+        } else if (j > p) {
+          double t = A[lo(j, k)]; A[lo(j, k)] = A[lo(j, p)]; A[lo(j, p)] = t;
+        }
+      }
+      __syncthreads();
+    }
+    const double dk = A[lo(k, k)];
+    for (int i = k + 1 + tid; i < n; i += nt) col[i] = A[lo(i, k)];
+    __syncthreads();
+    for (int i = k + 1 + tr_; i < n; i += 32) {
+      const double lik = (dk != 0.0) ? col[i] / dk : 0.0;
+      const int base = i * (i + 1) / 2;
+      for (int j = k + 1 + tc_; j <= i; j += 32) A[base + j] -= lik * col[j];
+      if (tc_ == 0) A[base + k] = lik;
+    }
+    __syncthreads();
+  }
+  // triangular solves on one wave, y held in registers (lane owns rows lane + 64 r)
+  if (tid < 64) {
+    double yv[3];
+    for (int r = 0; r < 3; r++) {
+      int i = tid + 64 * r;
+      yv[r] = i < n ? -J[perm[i]] : 0.0;
+    }
+    for (int k = 0; k < n; k++) {  // L y = P(-J)
+      const double yk = __shfl(yv[k >> 6], k & 63, 64);
+      for (int r = 0; r < 3; r++) {
+        int i = tid + 64 * r;
+        if (i > k && i < n) yv[r] -= A[lo(i, k)] * yk;
       }
     }
-    __syncthreads();
-    const int pk = perm[k];
-    const double dk = A[lo(pk, pk)];
-    for (int i = k + 1 + tid; i < n; i += nt) col[i] = A[lo(perm[i], pk)];
-    __syncthreads();
-    const int m = n - k - 1;
-    const int npair = m * (m + 1) / 2;
-    for (int t = tid; t < npair; t += nt) {
-      int a = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-      while ((a + 1) * (a + 2) / 2 <= t) a++;
-      while (a * (a + 1) / 2 > t) a--;
-      int b = t - a * (a + 1) / 2;
-      int i = k + 1 + a, j = k + 1 + b;  // j <= i
-      double lik = (dk != 0.0) ? col[i] / dk : 0.0;
-      A[lo(perm[i], perm[j])] -= lik * col[j];
+    for (int r = 0; r < 3; r++) {
+      int i = tid + 64 * r;
+      if (i < n) {
+        double d = A[lo(i, i)];
+        yv[r] = (d != 0.0) ? yv[r] / d : 0.0;
+      }
     }
-    __syncthreads();
-    for (int i = k + 1 + tid; i < n; i += nt) A[lo(perm[i], pk)] = (dk != 0.0) ? col[i] / dk : 0.0;
-    __syncthreads();
-  }
-  // solve: L y = P(-J); y /= d; L^T x = y
-  for (int t = tid; t < n; t += nt) y[t] = -J[perm[t]];
-  __syncthreads();
-  for (int k = 0; k < n; k++) {
-    const double yk = y[k];
-    for (int i = k + 1 + tid; i < n; i += nt) y[i] -= A[lo(perm[i], perm[k])] * yk;
-    __syncthreads();
-  }
-  for (int t = tid; t < n; t += nt) {
-    double d = A[lo(perm[t], perm[t])];
-    y[t] = (d != 0.0) ? y[t] / d : 0.0;
+    for (int k = n - 1; k >= 0; k--) {  // L^T x = y
+      const double yk = __shfl(yv[k >> 6], k & 63, 64);
+      for (int r = 0; r < 3; r++) {
+        int i = tid + 64 * r;
+        if (i < k) yv[r] -= A[lo(k, i)] * yk;
+      }
+    }
+    for (int r = 0; r < 3; r++) {
+      int i = tid + 64 * r;
+      if (i < n) y[i] = yv[r];
+    }
   }
   __syncthreads();
-  for (int k = n - 1; k >= 0; k--) {
-    const double yk = y[k];
-    for (int i = tid; i < k; i += nt) y[i] -= A[lo(perm[k], perm[i])] * yk;
-    __syncthreads();
-  }
   for (int t = tid; t < n; t += nt) col[perm[t]] = y[t];
   __syncthreads();
   // trial states (optimizers.cpp:468-475) and IMU bias trial (477-478)
@@ -547,7 +576,7 @@ __global__ void __launch_bounds__(256) k_ba_resid(int nf, int W, const int* __re
 }
 
 // LM bookkeeping (optimizers.cpp:480-515)
-__global__ void k_ba_control(int W, int nimu, int nrb, double imu_coef, const double* __restrict__ hl, int nl,
+__global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, double imu_coef, const double* __restrict__ hl, int nl,
                              const double* __restrict__ imuout, const double* __restrict__ imures,
                              const double* __restrict__ rpart, double* __restrict__ xs,
                              const double* __restrict__ xt, double* __restrict__ bias, BaState* __restrict__ st) {
@@ -600,7 +629,7 @@ __global__ void k_ba_control(int W, int nimu, int nrb, double imu_coef, const do
   }
 }
 
-__global__ void k_ba_init(BaState* st) {
+__global__ void __launch_bounds__(256) k_ba_init(BaState* st) {
   st->u = 0.01;
   st->v = 2;
   st->res1 = st->res2 = st->q1 = 0.0;
@@ -722,7 +751,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double*
       k_ba_comp<<<grid_for((long)nf * W), kBlock, 0, s>>>(nf, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
                                                          ctx->map.pcrs, d.mpring, d.xs, d.comp, d.compf, d.st);
       k_ba_hred<<<nchunk, 256, hred_lds, s>>>(nf, W, d.comp, d.compf, d.part, d.st);
-      k_ba_hfinal<<<grid_for(nout), kBlock, 0, s>>>(nchunk, nout, d.part, d.hl, d.st);
+      k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nchunk, nout, d.part, d.hl, d.st);
     }
     if (nimu > 0) k_ba_imu<<<nimu, 256, 0, s>>>(nimu, d.imurec, d.bias, d.xs, d.imuout, d.st);
     k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.xs, d.xt,

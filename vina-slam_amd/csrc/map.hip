@@ -109,7 +109,7 @@ int map_reset(vg_ctx* ctx) {
 
 // Node records of freshly allocated nodes must be zero: the pool is zeroed
 // lazily per allocation range.
-__global__ void k_zero_nodes(int first, const int* __restrict__ cnt_after, int W, PlaneRec* pl, Clu* pcr_add,
+__global__ void __launch_bounds__(256) k_zero_nodes(int first, const int* __restrict__ cnt_after, int W, PlaneRec* pl, Clu* pcr_add,
                              Clu* pcr_fix, double* cov, double* eig, double* jour, Clu* pcrs) {
   const int last = cnt_after[0];
   for (int id = first + blockIdx.x * blockDim.x + threadIdx.x; id < last; id += gridDim.x * blockDim.x) {
@@ -246,13 +246,23 @@ __global__ void __launch_bounds__(256) k_iekf(int n, const float* __restrict__ x
   }
 }
 
-__global__ void k_iekf_final(int nb, const double* __restrict__ partials, double* __restrict__ out) {
-  int j = threadIdx.x;
-  if (j < kIekfVals) {
-    double s = 0;
-    for (int b = 0; b < nb; b++) s += partials[(size_t)b * kIekfVals + j];
-    out[j] = s;
+// ordered two-level sum of the block partials: lane t sums rows t, t+256, ...
+// for all 34 values, then a fixed LDS tree (deterministic)
+__global__ void __launch_bounds__(256) k_iekf_final(int nb, const double* __restrict__ partials,
+                                                    double* __restrict__ out) {
+  __shared__ double red[256][kIekfVals + 1];
+  double acc[kIekfVals];
+  for (int j = 0; j < kIekfVals; j++) acc[j] = 0.0;
+  for (int b = threadIdx.x; b < nb; b += 256)
+    for (int j = 0; j < kIekfVals; j++) acc[j] += partials[(size_t)b * kIekfVals + j];
+  for (int j = 0; j < kIekfVals; j++) red[threadIdx.x][j] = acc[j];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w)
+      for (int j = 0; j < kIekfVals; j++) red[threadIdx.x][j] += red[threadIdx.x + w][j];
+    __syncthreads();
   }
+  if (threadIdx.x < kIekfVals) out[threadIdx.x] = red[0][threadIdx.x];
 }
 
 int iekf_reset_cache(vg_ctx* ctx, int n) {
@@ -268,7 +278,7 @@ int iekf_iter(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const f
   prof_begin(ctx, kProfIekfKernel);
   k_iekf<<<nb, 256, 0, s>>>(n, x, y, z, mp, pose, ctx->map, w.iekf_cache, w.partials);
   prof_end(ctx, kProfIekfKernel);
-  k_iekf_final<<<1, 64, 0, s>>>(nb, w.partials, w.partials + (size_t)w.nparts * 38);
+  k_iekf_final<<<1, 256, 0, s>>>(nb, w.partials, w.partials + (size_t)w.nparts * 38);
   VG_HIP(hipGetLastError());
   VG_HIP(hipMemcpyAsync(ctx->h_pinned_d, w.partials + (size_t)w.nparts * 38, kIekfVals * sizeof(double),
                         hipMemcpyDeviceToHost, s));
@@ -281,7 +291,7 @@ int iekf_iter(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const f
 // ------------------------------------------------------------------ insert (A3/A4)
 // per downsampled point: var_init + pvec_update (world var), world point, root
 // key insert-or-find, first-occurrence marking of brand-new keys
-__global__ void k_ins_prep(int n, const float* __restrict__ ox, const float* __restrict__ oy,
+__global__ void __launch_bounds__(256) k_ins_prep(int n, const float* __restrict__ ox, const float* __restrict__ oy,
                            const float* __restrict__ oz, MP mp, InsPose ps, int slot, DevMap m,
                            double* __restrict__ pw, uint32_t* __restrict__ hslot) {
   const M3 R = ld_m3(ps.R), rot_var = ld_m3(ps.rot_var), tsl_var = ld_m3(ps.tsl_var);
@@ -315,7 +325,7 @@ __global__ void k_ins_prep(int n, const float* __restrict__ ox, const float* __r
   }
 }
 
-__global__ void k_ins_newflag(int n, const uint32_t* __restrict__ hslot, const int* __restrict__ hval,
+__global__ void __launch_bounds__(256) k_ins_newflag(int n, const uint32_t* __restrict__ hslot, const int* __restrict__ hval,
                               const int* __restrict__ hfirst, uint32_t* __restrict__ flag) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     uint32_t s = hslot[i];
@@ -325,7 +335,7 @@ __global__ void k_ins_newflag(int n, const uint32_t* __restrict__ hslot, const i
 
 // allocate new roots in first-occurrence order (deterministic ids); new roots
 // join surf_map_slide (voxel_map.cpp:77-83)
-__global__ void k_ins_newalloc(int n, const uint32_t* __restrict__ hslot, const uint32_t* __restrict__ flag,
+__global__ void __launch_bounds__(256) k_ins_newalloc(int n, const uint32_t* __restrict__ hslot, const uint32_t* __restrict__ flag,
                                const uint32_t* __restrict__ rank, MP mp, DevMap m) {
   const int base = m.counters[kCntNodes];
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -349,36 +359,41 @@ __global__ void k_ins_newalloc(int n, const uint32_t* __restrict__ hslot, const 
   }
 }
 
-__global__ void k_add_counter(int* counters, int idx, const uint32_t* __restrict__ flag,
+__global__ void __launch_bounds__(256) k_add_counter(int* counters, int idx, const uint32_t* __restrict__ flag,
                               const uint32_t* __restrict__ rank, int n) {
   if (threadIdx.x == 0 && blockIdx.x == 0 && n > 0) counters[idx] += (int)(rank[n - 1] + flag[n - 1]);
 }
 
 // distinct roots touched by the scan (the thread_num quirk, voxel_map.cpp:94-97),
 // isexist on existing roots (voxel_map.cpp:70), surf_map_slide registration
-__global__ void k_ins_touch(int n, const uint32_t* __restrict__ hslot, int epoch, int first_new, DevMap m,
+__global__ void __launch_bounds__(256) k_ins_touch(int n, const uint32_t* __restrict__ hslot, int epoch, int first_new, DevMap m,
                            int* __restrict__ root_of) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    uint32_t s = hslot[i];
-    int root = s != 0xffffffffu ? m.hval[s] : -1;
-    root_of[i] = root;
-    if (root < 0) continue;
-    if (atomicExch(&m.nscr[(size_t)root * 4 + 3], epoch) != epoch) {
-      atomicAdd(&m.counters[kCntTouched], 1);
-      if (root < first_new) {
-        m.hdr[root].isexist = 1;
-        if (!m.in_slide[root]) {
-          m.in_slide[root] = 1;
-          int pos = atomicAdd(&m.counters[kCntSlide], 1);
-          m.slide[pos] = root;
+  for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    const int i = base + threadIdx.x;
+    int first = 0, add_slide = 0, root = -1;
+    if (i < n) {
+      uint32_t s = hslot[i];
+      root = s != 0xffffffffu ? m.hval[s] : -1;
+      root_of[i] = root;
+      if (root >= 0 && atomicExch(&m.nscr[(size_t)root * 4 + 3], epoch) != epoch) {
+        first = 1;
+        if (root < first_new) {
+          m.hdr[root].isexist = 1;
+          if (!m.in_slide[root]) {
+            m.in_slide[root] = 1;
+            add_slide = 1;
+          }
         }
       }
     }
+    (void)wave_append(&m.counters[kCntTouched], first);
+    int pos = wave_append(&m.counters[kCntSlide], add_slide);
+    if (add_slide) m.slide[pos] = root;
   }
 }
 
 // descend to a leaf; a missing child becomes a creation request (parent, octant)
-__global__ void k_ins_descend(int n, const double* __restrict__ pw, DevMap m, int* __restrict__ leaf,
+__global__ void __launch_bounds__(256) k_ins_descend(int n, const double* __restrict__ pw, DevMap m, int* __restrict__ leaf,
                               int* __restrict__ reqlist) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int node = leaf[i];
@@ -407,7 +422,7 @@ __global__ void k_ins_descend(int n, const double* __restrict__ pw, DevMap m, in
 }
 
 // children for a sorted list of parents: ids = base + prefix(popcount(mask))
-__global__ void k_child_count(int np, const int* __restrict__ parents, DevMap m, uint32_t* __restrict__ cnt) {
+__global__ void __launch_bounds__(256) k_child_count(int np, const int* __restrict__ parents, DevMap m, uint32_t* __restrict__ cnt) {
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < np; q += gridDim.x * blockDim.x) {
     int p = parents[q];
     int c = 0;
@@ -416,7 +431,7 @@ __global__ void k_child_count(int np, const int* __restrict__ parents, DevMap m,
   }
 }
 
-__global__ void k_child_alloc(int np, const int* __restrict__ parents, const uint32_t* __restrict__ off, DevMap m,
+__global__ void __launch_bounds__(256) k_child_alloc(int np, const int* __restrict__ parents, const uint32_t* __restrict__ off, DevMap m,
                               int* __restrict__ next, int next_base) {
   const int base = m.counters[kCntNodes];
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < np; q += gridDim.x * blockDim.x) {
@@ -443,7 +458,7 @@ __global__ void k_child_alloc(int np, const int* __restrict__ parents, const uin
   }
 }
 
-__global__ void k_ins_resolve(int n, const double* __restrict__ pw, DevMap m, int* __restrict__ leaf) {
+__global__ void __launch_bounds__(256) k_ins_resolve(int n, const double* __restrict__ pw, DevMap m, int* __restrict__ leaf) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int node = leaf[i];
     if (node >= -1) continue;
@@ -453,7 +468,7 @@ __global__ void k_ins_resolve(int n, const double* __restrict__ pw, DevMap m, in
 }
 
 // sort key: (leaf << 27) | order
-__global__ void k_ins_keys(int n, const int* __restrict__ leaf, uint64_t* __restrict__ keys) {
+__global__ void __launch_bounds__(256) k_ins_keys(int n, const int* __restrict__ leaf, uint64_t* __restrict__ keys) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int l = leaf[i];
     keys[i] = l >= 0 ? (((uint64_t)l << 27) | (uint64_t)i) : ~0ull;
@@ -461,7 +476,7 @@ __global__ void k_ins_keys(int n, const int* __restrict__ leaf, uint64_t* __rest
 }
 
 // OctoTree::push (octree.cpp:151-177) for every point of a leaf segment, in order
-__global__ void k_push_window(int n, const uint64_t* __restrict__ keys, MP mp, int slot, DevMap m,
+__global__ void __launch_bounds__(256) k_push_window(int n, const uint64_t* __restrict__ keys, MP mp, int slot, DevMap m,
                               const double* __restrict__ pw) {
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
     uint64_t k = keys[j];
@@ -528,10 +543,10 @@ static int bits_for(long v) {
 }
 
 // sort an int list of n node ids in place (deterministic creation order)
-__global__ void k_i2k(int n, const int* __restrict__ a, uint64_t* __restrict__ k) {
+__global__ void __launch_bounds__(256) k_i2k(int n, const int* __restrict__ a, uint64_t* __restrict__ k) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) k[i] = (uint64_t)a[i];
 }
-__global__ void k_k2i(int n, const uint64_t* __restrict__ k, int* __restrict__ a) {
+__global__ void __launch_bounds__(256) k_k2i(int n, const uint64_t* __restrict__ k, int* __restrict__ a) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) a[i] = (int)k[i];
 }
 static int sort_ids(vg_ctx* ctx, int* a, int n) {
@@ -611,78 +626,95 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, const InsPose& pose, int n, 
 // nodes forward their children, leaves run the plane test; failing leaves below
 // max_layer are marked for subdivision; planar leaves that pass tras_opt's
 // filter (octree.cpp:502-505) become factor candidates.
-__global__ void k_recut_visit(int nw, const int* __restrict__ work, MP mp, DevMap m, int* __restrict__ next,
+__global__ void __launch_bounds__(256) k_recut_visit(int nw, const int* __restrict__ work, MP mp, DevMap m, int* __restrict__ next,
                               int* __restrict__ sub, int* __restrict__ cand) {
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) {
-    int node = work[q];
-    NodeHdr& h = m.hdr[node];
-    if (h.octo == 1) {
-      for (int o = 0; o < 8; o++)
-        if (h.child[o] >= 0) next[atomicAdd(&m.counters[kCntNext], 1)] = h.child[o];
-      continue;
+  for (int base = blockIdx.x * blockDim.x; base < nw; base += gridDim.x * blockDim.x) {
+    const int q = base + threadIdx.x;
+    int node = q < nw ? work[q] : -1;
+    int nchild = 0, is_cand = 0, is_sub = 0;
+    int kids[8];
+    if (node >= 0) {
+      NodeHdr& h = m.hdr[node];
+      if (h.octo == 1) {
+        for (int o = 0; o < 8; o++)
+          if (h.child[o] >= 0) kids[nchild++] = h.child[o];
+      } else {
+        h.opt_state = -1;
+        const Clu& a = m.pcr_add[node];
+        if (a.N <= mp.minpt[h.layer]) {
+          h.is_plane = 0;
+        } else if (h.isexist && h.has_sw) {
+          V3 ev;
+          M3 U;
+          eig3(clu_cov(a), ev, U);
+          double* e = &m.eig[(size_t)node * 12];
+          for (int j = 0; j < 3; j++) e[j] = ev[j];
+          for (int j = 0; j < 9; j++) e[3 + j] = U[j];
+          h.is_plane = (ev[0] < mp.min_eig && (ev[0] / ev[2]) < mp.thre[h.layer]) ? 1 : 0;
+          if (h.is_plane) {
+            is_cand = !(ev[0] / ev[1] > 0.12) ? 1 : 0;
+          } else if (h.layer < mp.max_layer) {
+            m.nscr[(size_t)node * 4 + 2] = 1;  // subdividing
+            is_sub = 1;
+          }
+        }
+      }
     }
-    h.opt_state = -1;
-    const Clu& a = m.pcr_add[node];
-    if (a.N <= mp.minpt[h.layer]) {
-      h.is_plane = 0;
-      continue;
-    }
-    if (!h.isexist || !h.has_sw) continue;
-    V3 ev;
-    M3 U;
-    eig3(clu_cov(a), ev, U);
-    double* e = &m.eig[(size_t)node * 12];
-    for (int j = 0; j < 3; j++) e[j] = ev[j];
-    for (int j = 0; j < 9; j++) e[3 + j] = U[j];
-    h.is_plane = (ev[0] < mp.min_eig && (ev[0] / ev[2]) < mp.thre[h.layer]) ? 1 : 0;
-    if (h.is_plane) {
-      if (!(ev[0] / ev[1] > 0.12)) cand[atomicAdd(&m.counters[kCntFactors], 1)] = node;
-      continue;
-    }
-    if (h.layer >= mp.max_layer) continue;
-    m.nscr[(size_t)node * 4 + 2] = 1;  // subdividing
-    sub[atomicAdd(&m.counters[kCntSub], 1)] = node;
+    int o1 = wave_append(&m.counters[kCntNext], nchild);
+    int o2 = wave_append(&m.counters[kCntFactors], is_cand);
+    int o3 = wave_append(&m.counters[kCntSub], is_sub);
+    for (int j = 0; j < nchild; j++) next[o1 + j] = kids[j];
+    if (is_cand) cand[o2] = node;
+    if (is_sub) sub[o3] = node;
   }
 }
 
 // subdivision events: point_fix entries (fix_divide, octree.cpp:257-277) and
 // window points of every frame (subdivide, octree.cpp:279-300)
-__global__ void k_sub_fix_events(int ns, const int* __restrict__ sub, DevMap m, uint64_t* __restrict__ ev, int cap) {
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ns; q += gridDim.x * blockDim.x) {
-    int p = sub[q];
+__global__ void __launch_bounds__(256) k_sub_fix_events(int ns, const int* __restrict__ sub, DevMap m, uint64_t* __restrict__ ev, int cap) {
+  for (int base = blockIdx.x * blockDim.x; base < ns; base += gridDim.x * blockDim.x) {
+    const int q = base + threadIdx.x;
+    const int p = q < ns ? sub[q] : -1;
+    const int cnt = p >= 0 ? m.hdr[p].fix_cnt : 0;
+    int pos = wave_append(&m.counters[kCntEvents], cnt);
+    if (p < 0) continue;
     const NodeHdr& h = m.hdr[p];
-    for (int j = 0; j < h.fix_cnt; j++) {
+    for (int j = 0; j < cnt; j++, pos++) {
       size_t f = (size_t)h.fix_off + j;
       V3 pt = ld_v3(&m.fix_pnt[f * 3]);
       int o = octant(pt, h.center);
       m.cfirst[(size_t)p * 8 + o] = -5;
-      int pos = atomicAdd(&m.counters[kCntEvents], 1);
       // parent, octant, phase 0 (fix), index
       if (pos < cap) ev[pos] = ((uint64_t)p << 27) | ((uint64_t)o << 24) | (uint64_t)j;
     }
   }
 }
 
-__global__ void k_sub_win_events(int total, int cap_wp, const int* __restrict__ nper, const int* __restrict__ slot_of,
+__global__ void __launch_bounds__(256) k_sub_win_events(int total, int cap_wp, const int* __restrict__ nper, const int* __restrict__ slot_of,
                                  WinD* __restrict__ win, DevMap m, uint64_t* __restrict__ ev,
                                  uint32_t* __restrict__ evsrc, int cap) {
-  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += gridDim.x * blockDim.x) {
-    int ord = 0, i = g;
-    while (ord < win->win_count && i >= nper[ord]) {
-      i -= nper[ord];
-      ord++;
+  for (int base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
+    const int g = base + threadIdx.x;
+    int ord = 0, i = g, leaf = -1, o = 0;
+    if (g < total) {
+      while (ord < win->win_count && i >= nper[ord]) {
+        i -= nper[ord];
+        ord++;
+      }
+      if (ord < win->win_count) {
+        size_t b = (size_t)slot_of[ord] * cap_wp + i;
+        int l = m.wp_leaf[b];
+        if (l >= 0 && m.nscr[(size_t)l * 4 + 2] == 1) {
+          leaf = l;
+          const NodeHdr& h = m.hdr[leaf];
+          V3 pw = rigid(ld_m3(win->R[ord]), ld_v3(&m.wp_pnt[b * 3]), ld_v3(win->p[ord]));
+          o = octant(pw, h.center);
+          m.cfirst[(size_t)leaf * 8 + o] = -5;
+        }
+      }
     }
-    if (ord >= win->win_count) continue;
-    int slot = slot_of[ord];
-    size_t b = (size_t)slot * cap_wp + i;
-    int leaf = m.wp_leaf[b];
-    if (leaf < 0 || m.nscr[(size_t)leaf * 4 + 2] != 1) continue;
-    const NodeHdr& h = m.hdr[leaf];
-    V3 pw = rigid(ld_m3(win->R[ord]), ld_v3(&m.wp_pnt[b * 3]), ld_v3(win->p[ord]));
-    int o = octant(pw, h.center);
-    m.cfirst[(size_t)leaf * 8 + o] = -5;
-    int pos = atomicAdd(&m.counters[kCntEvents], 1);
-    if (pos < cap) {
+    int pos = wave_append(&m.counters[kCntEvents], leaf >= 0 ? 1 : 0);
+    if (leaf >= 0 && pos < cap) {
       ev[pos] = ((uint64_t)leaf << 27) | ((uint64_t)o << 24) | (uint64_t)(1 + ord);
       evsrc[pos] = (uint32_t)i;
     }
@@ -690,7 +722,7 @@ __global__ void k_sub_win_events(int total, int cap_wp, const int* __restrict__ 
 }
 
 // rewrite events as (child << 27 | phase << 21 | idx) sort keys
-__global__ void k_sub_keys(int ne, const uint64_t* __restrict__ ev, const uint32_t* __restrict__ evsrc,
+__global__ void __launch_bounds__(256) k_sub_keys(int ne, const uint64_t* __restrict__ ev, const uint32_t* __restrict__ evsrc,
                            DevMap m, uint64_t* __restrict__ keys, int nfix) {
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x) {
     uint64_t v = ev[e];
@@ -713,7 +745,7 @@ __global__ void k_sub_keys(int ne, const uint64_t* __restrict__ ev, const uint32
 // apply the sorted subdivision pushes to each child, in the reference's order:
 // fix points first (push_fix, octree.cpp:179-188), then window points frame by
 // frame (push, octree.cpp:151-177)
-__global__ void k_push_events(int ne, const uint64_t* __restrict__ keys, MP mp, WinD* __restrict__ win, DevMap m) {
+__global__ void __launch_bounds__(256) k_push_events(int ne, const uint64_t* __restrict__ keys, MP mp, WinD* __restrict__ win, DevMap m) {
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < ne; j += gridDim.x * blockDim.x) {
     int child = (int)(keys[j] >> 27);
     if (j > 0 && (int)(keys[j - 1] >> 27) == child) continue;
@@ -790,7 +822,7 @@ __global__ void k_push_events(int ne, const uint64_t* __restrict__ keys, MP mp, 
 
 // finish a subdivided parent: release its SlideWindow, free point_fix,
 // octo_state = 1 (octree.cpp:375-387)
-__global__ void k_sub_finish(int ns, const int* __restrict__ sub, DevMap m) {
+__global__ void __launch_bounds__(256) k_sub_finish(int ns, const int* __restrict__ sub, DevMap m) {
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ns; q += gridDim.x * blockDim.x) {
     int p = sub[q];
     NodeHdr& h = m.hdr[p];
@@ -804,7 +836,7 @@ __global__ void k_sub_finish(int ns, const int* __restrict__ sub, DevMap m) {
 }
 
 // tras_opt: factor list in node-id order; opt_state = factor index
-__global__ void k_factor_finish(int nf, const int* __restrict__ fac, DevMap m, int* __restrict__ fac_node,
+__global__ void __launch_bounds__(256) k_factor_finish(int nf, const int* __restrict__ fac, DevMap m, int* __restrict__ fac_node,
                                 double* __restrict__ fac_eig, Clu* __restrict__ fac_pcr) {
   for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < nf; a += gridDim.x * blockDim.x) {
     int node = fac[a];
@@ -903,28 +935,37 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinD& win, const int* nper, int t
 
 // ------------------------------------------------------------------ margi (A10)
 // collect every node under the slide roots, level by level (top-down)
-__global__ void k_collect_level(int nw, const int* __restrict__ work, DevMap m, int* __restrict__ next,
+__global__ void __launch_bounds__(256) k_collect_level(int nw, const int* __restrict__ work, DevMap m, int* __restrict__ next,
                                 int* __restrict__ leaves) {
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) {
-    int node = work[q];
-    const NodeHdr& h = m.hdr[node];
-    if (h.octo == 1) {
-      for (int o = 0; o < 8; o++)
-        if (h.child[o] >= 0) next[atomicAdd(&m.counters[kCntNext], 1)] = h.child[o];
-    } else {
-      leaves[atomicAdd(&m.counters[kCntLeaves], 1)] = node;
+  for (int base = blockIdx.x * blockDim.x; base < nw; base += gridDim.x * blockDim.x) {
+    const int q = base + threadIdx.x;
+    const int node = q < nw ? work[q] : -1;
+    int nchild = 0, is_leaf = 0;
+    int kids[8];
+    if (node >= 0) {
+      const NodeHdr& h = m.hdr[node];
+      if (h.octo == 1) {
+        for (int o = 0; o < 8; o++)
+          if (h.child[o] >= 0) kids[nchild++] = h.child[o];
+      } else {
+        is_leaf = 1;
+      }
     }
+    int o1 = wave_append(&m.counters[kCntNext], nchild);
+    int o2 = wave_append(&m.counters[kCntLeaves], is_leaf);
+    for (int j = 0; j < nchild; j++) next[o1 + j] = kids[j];
+    if (is_leaf) leaves[o2] = node;
   }
 }
 
 // oldest-slot point segments per leaf: seg start/count in nscr[.*4+0/1]
-__global__ void k_margi_keys(int n, int slot, DevMap m, uint64_t* __restrict__ keys) {
+__global__ void __launch_bounds__(256) k_margi_keys(int n, int slot, DevMap m, uint64_t* __restrict__ keys) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int l = m.wp_leaf[(size_t)slot * m.cap_wp + i];
     keys[i] = l >= 0 ? (((uint64_t)l << 27) | (uint64_t)i) : ~0ull;
   }
 }
-__global__ void k_margi_segs(int n, const uint64_t* __restrict__ keys, DevMap m) {
+__global__ void __launch_bounds__(256) k_margi_segs(int n, const uint64_t* __restrict__ keys, DevMap m) {
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
     uint64_t k = keys[j];
     if (k == ~0ull) continue;
@@ -984,7 +1025,7 @@ __device__ void plane_update_dev(DevMap& m, int node, const Clu& pcr_add, const 
 // OctoTree::margi leaf branch (octree.cpp:397-484), mgsize = 1. keys = the
 // oldest slot's listed points sorted by (leaf, index): each leaf's segment is
 // its sw->points[mp[0]] list in push order.
-__global__ void k_margi_leaf(int nl, const int* __restrict__ leaves, const uint64_t* __restrict__ keys, MP mp,
+__global__ void __launch_bounds__(256) k_margi_leaf(int nl, const int* __restrict__ leaves, const uint64_t* __restrict__ keys, MP mp,
                              WinD* __restrict__ win, DevMap m, const double* __restrict__ fac_eig,
                              const Clu* __restrict__ fac_pcr) {
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nl; q += gridDim.x * blockDim.x) {
@@ -1073,7 +1114,7 @@ __global__ void k_margi_leaf(int nl, const int* __restrict__ leaves, const uint6
   }
 }
 
-__global__ void k_margi_segs_clear(int n, const uint64_t* __restrict__ keys, DevMap m) {
+__global__ void __launch_bounds__(256) k_margi_segs_clear(int n, const uint64_t* __restrict__ keys, DevMap m) {
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
     uint64_t k = keys[j];
     if (k == ~0ull) continue;
@@ -1084,7 +1125,7 @@ __global__ void k_margi_segs_clear(int n, const uint64_t* __restrict__ keys, Dev
 }
 
 // internal nodes bottom-up: isexist = OR(children) (octree.cpp:485-494)
-__global__ void k_margi_internal(int nw, const int* __restrict__ work, DevMap m) {
+__global__ void __launch_bounds__(256) k_margi_internal(int nw, const int* __restrict__ work, DevMap m) {
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) {
     int node = work[q];
     NodeHdr& h = m.hdr[node];
@@ -1098,7 +1139,7 @@ __global__ void k_margi_internal(int nw, const int* __restrict__ work, DevMap m)
 
 // erase dead roots from surf_map_slide (local_mapping.cpp:67-78) with
 // clear_slwd over their subtrees (octree.cpp:739-756)
-__global__ void k_margi_erase_mark(int nw, const int* __restrict__ work, DevMap m, int level, double jour) {
+__global__ void __launch_bounds__(256) k_margi_erase_mark(int nw, const int* __restrict__ work, DevMap m, int level, double jour) {
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) {
     int node = work[q];
     NodeHdr& h = m.hdr[node];
@@ -1116,7 +1157,7 @@ __global__ void k_margi_erase_mark(int nw, const int* __restrict__ work, DevMap 
     }
   }
 }
-__global__ void k_clear_mark(int nw, const int* __restrict__ work, DevMap m) {
+__global__ void __launch_bounds__(256) k_clear_mark(int nw, const int* __restrict__ work, DevMap m) {
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x)
     m.nscr[(size_t)work[q] * 4 + 2] = -1;
 }
@@ -1145,7 +1186,7 @@ __global__ void k_slide_compact(int n, const int* __restrict__ old, DevMap m) {
   }
   if (threadIdx.x == 0) m.counters[kCntSlide] = base;
 }
-__global__ void k_set_jour(int n, const int* __restrict__ slide, double* jour, double j) {
+__global__ void __launch_bounds__(256) k_set_jour(int n, const int* __restrict__ slide, double* jour, double j) {
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) jour[slide[q]] = j;
 }
 
