@@ -106,6 +106,36 @@ int vg_get_stats(vg_ctx* ctx, vg_stats* out);
 /* Window states x_buf (win_count x 250 doubles); returns win_count via *n. */
 int vg_window_states(vg_ctx* ctx, double* out, int* n);
 
+/* ---- Stage-level API ------------------------------------------------------
+ * The steps vg_step composes, one entry per reference call of the steady-state
+ * loop (local_mapping.cpp:389-547), for a caller that keeps the reference's
+ * loop shape. Order per scan:
+ *   vg_scan_load | vg_scan_bind_dev        deskewed scan -> HBM
+ *   vg_propagate                           IMUEKF::process state/cov part (imu_ekf.cpp:28-94)
+ *   vg_downsample_scan                     down_sampling_voxel + /2 fallback (point_utils.hpp:7-44; local_mapping.cpp:396-403)
+ *   vg_lio_state_estimation                VINA_SLAM::VNC_lio -> LioStateEstimation (odometry.cpp:64-255)
+ *   vg_window_push                         x_buf / pvec_buf / IMU_PRE push (local_mapping.cpp:434-441)
+ *   vg_cut_voxel_multi                     pvec_update + cut_voxel_multi (point_utils.cpp:54-65; voxel_map.cpp:47-135)
+ *   vg_multi_recut                         VINA_SLAM::multi_recut + tras_opt (local_mapping.cpp:144-201)
+ *   if win_count >= win_size:
+ *     vg_damping_iter   (if if_BA)         LI_BA_Optimizer::damping_iter (optimizers.cpp:430-517)
+ *     vg_multi_margi                       x_curr <- x_buf.back(), multi_margi, slide (local_mapping.cpp:499-546)
+ *   vg_step_end                            per-scan counters (vg_get_stats)
+ * Every call returns VG_E_STATE when issued out of order. */
+int vg_scan_load(vg_ctx* ctx, const float* xyz, const float* intensity, int n);
+int vg_scan_bind_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, const float* d_intensity,
+                     int n);
+int vg_propagate(vg_ctx* ctx, const double* imu, int m, double pcl_beg_time, double pcl_end_time);
+int vg_downsample_scan(vg_ctx* ctx, int* n_ds);
+int vg_lio_state_estimation(vg_ctx* ctx, int* degenerate);
+int vg_window_push(vg_ctx* ctx, const double* imu, int m);
+int vg_cut_voxel_multi(vg_ctx* ctx);
+int vg_multi_recut(vg_ctx* ctx, int* n_factors);
+int vg_damping_iter(vg_ctx* ctx, int* lm_iters);
+int vg_multi_margi(vg_ctx* ctx);
+int vg_step_end(vg_ctx* ctx);
+int vg_win_count(vg_ctx* ctx, int* n);
+
 /* Per-scan poses published after the IEKF (pub_localtraj / save_pose_tum,
  * local_mapping.cpp:427-430): n rows of 13 doubles [t, R row-major 9, p 3].
  * Copies min(n, cap) rows; *n = total rows. out may be NULL to query. */

@@ -1,0 +1,83 @@
+"""The stage-level C-ABI (reference call order) reproduces vg_step exactly,
+the C++ replay driver (include/vina_gpu.hpp) reproduces the Python path, and
+out-of-order calls fail with VG_E_STATE instead of exiting."""
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import oracle
+import synth
+import vgconfig
+import vgpu
+
+pytestmark = pytest.mark.gpu
+CAP = dict(max_points=120_000, max_nodes=600_000, max_fix_points=2_000_000, hash_log2=20)
+
+
+def _seq(p, lidar="16line", seq_id=4):
+    g = p["General"]
+    return synth.Sequence(lidar, seq_id, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
+
+
+def test_stage_api_equals_step():
+    p = vgconfig.load("mid360")
+    seq = _seq(p)
+    a = vgpu.Context(vgconfig.to_c(p), **CAP)
+    b = vgpu.Context(vgconfig.to_c(p), **CAP)
+    a.seed(seq.gt_state(0))
+    b.seed(seq.gt_state(0))
+    W = p["LocalBA"]["win_size"]
+    for k in range(13):
+        xyz, it, beg, end = seq.scan(k)
+        imu = seq.imu(k)
+        a.step(xyz, it, beg, end, imu)
+        b.scan_load(xyz, it)
+        b.propagate(imu, beg, end)
+        b.downsample_scan()
+        b.lio_state_estimation()
+        b.window_push(imu)
+        b.cut_voxel_multi()
+        nf = b.multi_recut()
+        if b.win_count() >= W:
+            b.damping_iter()
+            b.multi_margi()
+        b.step_end()
+        assert nf == a.stats()["n_factors"]
+    assert np.array_equal(a.trajectory(), b.trajectory())
+    assert np.array_equal(a.window_states(), b.window_states())
+
+
+def test_out_of_order_is_an_error():
+    p = vgconfig.load("mid360")
+    c = vgpu.Context(vgconfig.to_c(p), **CAP)
+    with pytest.raises(vgpu.VgError):
+        c.downsample_scan()  # no scan loaded
+    with pytest.raises(vgpu.VgError):
+        c.damping_iter()  # window not full
+    with pytest.raises(vgpu.VgError):
+        c.multi_margi()
+
+
+def test_cpp_replay_driver_matches(oracle_lib):
+    p = vgconfig.load("mid360")
+    seq = _seq(p, seq_id=5)
+    n = 14
+    binp = os.path.join(vgpu.PKG, "bin", "vg_replay")
+    assert os.path.exists(binp)
+    with tempfile.TemporaryDirectory() as d:
+        rp, tp = os.path.join(d, "r.bin"), os.path.join(d, "t.txt")
+        synth.write_replay(rp, seq, vgconfig.to_c(p), n)
+        subprocess.check_call([binp, rp, tp])
+        tum = synth.read_tum(tp)
+    assert tum.shape == (n, 8)
+    orc = oracle.Pipeline(vgconfig.to_c(p, use_threads=0, vnc_prep=0))
+    orc.seed(seq.gt_state(0))
+    for k in range(n):
+        xyz, it, b, e = seq.scan(k)
+        orc.step(xyz, it, b, e, seq.imu(k))
+    to = orc.trajectory()
+    assert np.allclose(tum[:, 0], to[:, 0])
+    assert np.abs(tum[:, 1:4] - to[:, 10:13]).max() < 1e-6

@@ -139,6 +139,7 @@ struct HostPipe {
   MP mpd;
   M6 noiseMeas = M6::Z(), noiseWalk = M6::Z();
   std::vector<double> traj;
+  int cur_nds = 0, n_factors = 0;
 };
 
 static HostPipe* hp(vg_ctx* ctx) { return (HostPipe*)ctx->host; }
@@ -319,13 +320,9 @@ static WinD make_win(const HostPipe* P) {
   return w;
 }
 
-int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n, double beg,
-              double end, const double* imu, int m) {
-  HostPipe* P = hp(ctx);
-  const vg_config& c = ctx->cfg;
-  const int W = c.win_size;
-  memset(&ctx->stats, 0, sizeof(ctx->stats));
-  (void)beg;
+// ---- stage entry points (one per reference call in local_mapping.cpp:389-547)
+
+static std::vector<Imu> to_imus(const double* imu, int m) {
   std::vector<Imu> imus(m > 0 ? m : 0);
   for (int i = 0; i < m; i++) {
     imus[i].t = imu[7 * i];
@@ -334,13 +331,27 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
       imus[i].acc[j] = imu[7 * i + 4 + j];
     }
   }
-  if (!P->first)
-    propagate(ctx, P, imus, end);
-  else {
+  return imus;
+}
+
+// odom_ekf.process -> motion_blur state/covariance part (local_mapping.cpp:389)
+int stage_propagate(vg_ctx* ctx, const double* imu, int m, double end) {
+  HostPipe* P = hp(ctx);
+  memset(&ctx->stats, 0, sizeof(ctx->stats));
+  if (!P->first) {
+    propagate(ctx, P, to_imus(imu, m), end);
+  } else {
     P->x_curr.t = end;
     P->last_pcl_end_time = end;
   }
-  // downsample with the /2 fallback (local_mapping.cpp:396-403)
+  return VG_OK;
+}
+
+// down_sampling_voxel(pl_down, down_size) + the /2 fallback (local_mapping.cpp:396-403)
+int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n,
+                     int* n_ds_out) {
+  HostPipe* P = hp(ctx);
+  const vg_config& c = ctx->cfg;
   int n_ds = 0;
   prof_begin(ctx, kProfDownsample);
   VG_TRY(ds_run(ctx, dx, dy, dz, di, n, c.down_size, &n_ds));
@@ -348,29 +359,52 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   prof_end(ctx, kProfDownsample);
   ctx->stats.n_raw = n;
   ctx->stats.n_ds = n_ds;
-  // IEKF on the full deskewed cloud (local_mapping.cpp:408-413)
+  P->cur_nds = n_ds;
+  if (n_ds_out) *n_ds_out = n_ds;
+  return VG_OK;
+}
+
+// VNC_lio(no_ds_pptr) on the full cloud (local_mapping.cpp:408-430)
+int stage_iekf(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, int n, int* degenerate_out) {
+  HostPipe* P = hp(ctx);
   int degenerate = 0;
   prof_begin(ctx, kProfIekf);
   VG_TRY(lio_state_estimation(ctx, P, dx, dy, dz, n, &degenerate));
   prof_end(ctx, kProfIekf);
   ctx->stats.degenerate = degenerate;
+  if (degenerate_out) *degenerate_out = degenerate;
   // trajectory (pub_localtraj / save_pose_tum at local_mapping.cpp:427-430)
   P->traj.push_back(P->x_curr.t);
   for (int i = 0; i < 9; i++) P->traj.push_back(P->x_curr.R[i]);
   for (int i = 0; i < 3; i++) P->traj.push_back(P->x_curr.p[i]);
-  // window push (local_mapping.cpp:434-441)
+  return VG_OK;
+}
+
+// x_buf / pvec_buf / imu_pre_buf push (local_mapping.cpp:434-441)
+int stage_window_push(vg_ctx* ctx, const double* imu, int m) {
+  HostPipe* P = hp(ctx);
   P->win_count++;
   P->x_buf.push_back(P->x_curr);
   if (P->win_count > 1) {
     const HX& xb = P->x_buf[P->win_count - 2];
     P->imu_pre.emplace_back(xb.bg, xb.ba);
-    P->imu_pre.back().push_imu(imus, P->noiseMeas, P->noiseWalk);
+    P->imu_pre.back().push_imu(to_imus(imu, m), P->noiseMeas, P->noiseWalk);
+  }
+  return VG_OK;
+}
+
+// pvec_update + cut_voxel_multi of the downsampled scan (local_mapping.cpp:425-448)
+int stage_insert(vg_ctx* ctx) {
+  HostPipe* P = hp(ctx);
+  const vg_config& c = ctx->cfg;
+  if (P->win_count <= 0) {
+    ctx->err = "vg_map_insert: window is empty (push the scan first)";
+    return VG_E_STATE;
   }
   const int ord = P->win_count - 1;
   const int slot = P->mp[ord];
-  // pvec_update + cut_voxel_multi (local_mapping.cpp:425-448)
+  const HX& xc = P->x_buf[ord];
   InsPose ip;
-  const HX& xc = P->x_curr;
   memcpy(ip.R, xc.R.a, 72);
   memcpy(ip.p, xc.p.a, 24);
   for (int r = 0; r < 3; r++)
@@ -381,11 +415,17 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   P->epoch++;
   int roots_new = 0, touched = 0;
   prof_begin(ctx, kProfInsert);
-  VG_TRY(map_insert(ctx, P->mpd, slot, ip, n_ds, P->epoch, c.thread_num, &roots_new, &touched));
+  VG_TRY(map_insert(ctx, P->mpd, slot, ip, P->cur_nds, P->epoch, c.thread_num, &roots_new, &touched));
   prof_end(ctx, kProfInsert);
-  P->wp_n[slot] = n_ds;
+  P->wp_n[slot] = P->cur_nds;
   ctx->stats.roots_new = roots_new;
-  // multi_recut + tras_opt (local_mapping.cpp:451)
+  return VG_OK;
+}
+
+// multi_recut + tras_opt (local_mapping.cpp:451)
+int stage_recut(vg_ctx* ctx, int* nf_out) {
+  HostPipe* P = hp(ctx);
+  const vg_config& c = ctx->cfg;
   WinD win = make_win(P);
   int nper[32];
   for (int i = 0; i < P->win_count; i++) nper[i] = P->wp_n[P->mp[i]];
@@ -394,64 +434,91 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   VG_TRY(map_recut(ctx, P->mpd, win, nper, c.thread_num, &nf));
   prof_end(ctx, kProfRecut);
   ctx->stats.n_factors = nf;
-  if (P->win_count >= W) {
-    if (c.if_BA == 1) {  // LI_BA_Optimizer::damping_iter (local_mapping.cpp:492-497)
-      std::vector<double> xs((size_t)W * kBaX), rec((size_t)(W - 1) * kBaImuRec), bias((size_t)(W - 1) * 12);
-      for (int j = 0; j < W; j++) {
-        const HX& h = P->x_buf[j];
-        double* o = &xs[(size_t)j * kBaX];
-        memcpy(o, h.R.a, 72);
-        memcpy(o + 9, h.p.a, 24);
-        memcpy(o + 12, h.v.a, 24);
-        memcpy(o + 15, h.bg.a, 24);
-        memcpy(o + 18, h.ba.a, 24);
-        memcpy(o + 21, h.g.a, 24);
-      }
-      for (int j = 0; j < W - 1; j++) {
-        P->imu_pre[j].record(&rec[(size_t)j * kBaImuRec]);
-        memcpy(&bias[(size_t)j * 12], P->imu_pre[j].bias, 12 * sizeof(double));
-      }
-      int iters = 0;
-      prof_begin(ctx, kProfBA);
-      VG_TRY(ba_run(ctx, nf, P->mp.data(), xs.data(), rec.data(), bias.data(), &iters));
-      prof_end(ctx, kProfBA);
-      ctx->stats.ba_iters = iters;
-      for (int j = 0; j < W; j++) {
-        HX& h = P->x_buf[j];
-        const double* o = &xs[(size_t)j * kBaX];
-        memcpy(h.R.a, o, 72);
-        memcpy(h.p.a, o + 9, 24);
-        memcpy(h.v.a, o + 12, 24);
-        memcpy(h.bg.a, o + 15, 24);
-        memcpy(h.ba.a, o + 18, 24);
-      }
-      for (int j = 0; j < W - 1; j++) memcpy(P->imu_pre[j].bias, &bias[(size_t)j * 12], 12 * sizeof(double));
-    }
-    P->x_curr.R = P->x_buf[P->win_count - 1].R;
-    P->x_curr.p = P->x_buf[P->win_count - 1].p;
-    // multi_margi (local_mapping.cpp:507)
-    WinD w2 = make_win(P);
-    prof_begin(ctx, kProfMargi);
-    VG_TRY(map_margi(ctx, P->mpd, w2, P->wp_n[P->mp[0]], c.thread_num, P->jour));
-    prof_end(ctx, kProfMargi);
-    const int mgsize = 1;
-    if ((P->win_base + P->win_count) % 10 == 0) {
-      double spat = norm3(sub(P->x_curr.p, P->last_pos));
-      if (spat > 0.5) {
-        P->jour += spat;
-        P->last_pos = P->x_curr.p;
-      }
-    }
-    for (int i = 0; i < W; i++) {
-      P->mp[i] += mgsize;
-      if (P->mp[i] >= W) P->mp[i] -= W;
-    }
-    for (int i = mgsize; i < P->win_count; i++) P->x_buf[i - mgsize] = P->x_buf[i];
-    P->x_buf.pop_back();
-    P->imu_pre.pop_front();
-    P->win_base += mgsize;
-    P->win_count -= mgsize;
+  P->n_factors = nf;
+  if (nf_out) *nf_out = nf;
+  return VG_OK;
+}
+
+// LI_BA_Optimizer::damping_iter (local_mapping.cpp:492-497); x_curr.R/p <- x_buf.back() (501-502)
+int stage_ba(vg_ctx* ctx, int* iters_out) {
+  HostPipe* P = hp(ctx);
+  const int W = ctx->cfg.win_size;
+  if (P->win_count < W) {
+    ctx->err = "vg_ba: window not full";
+    return VG_E_STATE;
   }
+  std::vector<double> xs((size_t)W * kBaX), rec((size_t)(W - 1) * kBaImuRec), bias((size_t)(W - 1) * 12);
+  for (int j = 0; j < W; j++) {
+    const HX& h = P->x_buf[j];
+    double* o = &xs[(size_t)j * kBaX];
+    memcpy(o, h.R.a, 72);
+    memcpy(o + 9, h.p.a, 24);
+    memcpy(o + 12, h.v.a, 24);
+    memcpy(o + 15, h.bg.a, 24);
+    memcpy(o + 18, h.ba.a, 24);
+    memcpy(o + 21, h.g.a, 24);
+  }
+  for (int j = 0; j < W - 1; j++) {
+    P->imu_pre[j].record(&rec[(size_t)j * kBaImuRec]);
+    memcpy(&bias[(size_t)j * 12], P->imu_pre[j].bias, 12 * sizeof(double));
+  }
+  int iters = 0;
+  prof_begin(ctx, kProfBA);
+  VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), xs.data(), rec.data(), bias.data(), &iters));
+  prof_end(ctx, kProfBA);
+  ctx->stats.ba_iters = iters;
+  for (int j = 0; j < W; j++) {
+    HX& h = P->x_buf[j];
+    const double* o = &xs[(size_t)j * kBaX];
+    memcpy(h.R.a, o, 72);
+    memcpy(h.p.a, o + 9, 24);
+    memcpy(h.v.a, o + 12, 24);
+    memcpy(h.bg.a, o + 15, 24);
+    memcpy(h.ba.a, o + 18, 24);
+  }
+  for (int j = 0; j < W - 1; j++) memcpy(P->imu_pre[j].bias, &bias[(size_t)j * 12], 12 * sizeof(double));
+  if (iters_out) *iters_out = iters;
+  return VG_OK;
+}
+
+// x_curr.R/p <- x_buf.back(), multi_margi, jour, mp[] rotation and buffer slide
+// (local_mapping.cpp:499-546)
+int stage_margi_slide(vg_ctx* ctx) {
+  HostPipe* P = hp(ctx);
+  const vg_config& c = ctx->cfg;
+  const int W = c.win_size;
+  if (P->win_count < W) {
+    ctx->err = "vg_margi: window not full";
+    return VG_E_STATE;
+  }
+  P->x_curr.R = P->x_buf[P->win_count - 1].R;
+  P->x_curr.p = P->x_buf[P->win_count - 1].p;
+  WinD w2 = make_win(P);
+  prof_begin(ctx, kProfMargi);
+  VG_TRY(map_margi(ctx, P->mpd, w2, P->wp_n[P->mp[0]], c.thread_num, P->jour));
+  prof_end(ctx, kProfMargi);
+  const int mgsize = 1;
+  if ((P->win_base + P->win_count) % 10 == 0) {
+    double spat = norm3(sub(P->x_curr.p, P->last_pos));
+    if (spat > 0.5) {
+      P->jour += spat;
+      P->last_pos = P->x_curr.p;
+    }
+  }
+  for (int i = 0; i < W; i++) {
+    P->mp[i] += mgsize;
+    if (P->mp[i] >= W) P->mp[i] -= W;
+  }
+  for (int i = mgsize; i < P->win_count; i++) P->x_buf[i - mgsize] = P->x_buf[i];
+  P->x_buf.pop_back();
+  P->imu_pre.pop_front();
+  P->win_base += mgsize;
+  P->win_count -= mgsize;
+  return VG_OK;
+}
+
+int stage_finish(vg_ctx* ctx) {
+  HostPipe* P = hp(ctx);
   P->first = false;
   VG_HIP(hipMemcpyAsync(ctx->h_pinned, ctx->map.counters, kCntN * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   VG_HIP(hipStreamSynchronize(ctx->stream));
@@ -460,6 +527,26 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   ctx->stats.nodes_used = ctx->h_pinned[kCntNodes];
   ctx->stats.fix_used = ctx->h_pinned[kCntFix];
   return VG_OK;
+}
+
+int host_win_count(vg_ctx* ctx) { return hp(ctx)->win_count; }
+
+// one scan of thd_odometry_localmapping's steady-state branch
+int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n, double beg,
+              double end, const double* imu, int m) {
+  (void)beg;
+  const vg_config& c = ctx->cfg;
+  VG_TRY(stage_propagate(ctx, imu, m, end));
+  VG_TRY(stage_downsample(ctx, dx, dy, dz, di, n, nullptr));
+  VG_TRY(stage_iekf(ctx, dx, dy, dz, n, nullptr));
+  VG_TRY(stage_window_push(ctx, imu, m));
+  VG_TRY(stage_insert(ctx));
+  VG_TRY(stage_recut(ctx, nullptr));
+  if (hp(ctx)->win_count >= c.win_size) {
+    if (c.if_BA == 1) VG_TRY(stage_ba(ctx, nullptr));
+    VG_TRY(stage_margi_slide(ctx));
+  }
+  return stage_finish(ctx);
 }
 
 void host_seed(vg_ctx* ctx, const double* s) {

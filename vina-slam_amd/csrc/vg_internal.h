@@ -163,6 +163,9 @@ struct vg_ctx {
   vg::Arena arena;
   // raw scan staging (SoA)
   float *d_x = nullptr, *d_y = nullptr, *d_z = nullptr, *d_i = nullptr;
+  // the scan the stage-level API works on (own staging or caller's HBM)
+  const float *cur_x = nullptr, *cur_y = nullptr, *cur_z = nullptr, *cur_i = nullptr;
+  int cur_n = -1;
   vg::DownsampleBufs ds;
   vg::DevMap map;
   vg::Work wk;
@@ -267,4 +270,15 @@ int host_window(vg_ctx* ctx, double* out);
 int host_traj(vg_ctx* ctx, double* out, int cap);
 int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n, double beg,
               double end, const double* imu, int m);
+int host_win_count(vg_ctx* ctx);
+int stage_propagate(vg_ctx* ctx, const double* imu, int m, double end);
+int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n,
+                     int* n_ds_out);
+int stage_iekf(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, int n, int* degenerate_out);
+int stage_window_push(vg_ctx* ctx, const double* imu, int m);
+int stage_insert(vg_ctx* ctx);
+int stage_recut(vg_ctx* ctx, int* nf_out);
+int stage_ba(vg_ctx* ctx, int* iters_out);
+int stage_margi_slide(vg_ctx* ctx);
+int stage_finish(vg_ctx* ctx);
 }  // namespace vg

@@ -223,6 +223,99 @@ int vg_trajectory(vg_ctx* ctx, double* out, int cap, int* n) {
   return VG_OK;
 }
 
+// ---- stage-level API (include/vina_gpu.h "Stage-level API") ----
+int vg_scan_load(vg_ctx* ctx, const float* xyz, const float* intensity, int n) {
+  if (!ctx || n < 0 || (n > 0 && !xyz)) return VG_E_ARG;
+  if (n > ctx->cap.max_points_per_scan) {
+    ctx->err = "scan larger than max_points_per_scan";
+    return VG_E_CAPACITY;
+  }
+  if (n > 0) VG_TRY(upload_aos(ctx, xyz, intensity, n));
+  ctx->cur_x = ctx->d_x;
+  ctx->cur_y = ctx->d_y;
+  ctx->cur_z = ctx->d_z;
+  ctx->cur_i = ctx->d_i;
+  ctx->cur_n = n;
+  return VG_OK;
+}
+
+int vg_scan_bind_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, const float* d_intensity,
+                     int n) {
+  if (!ctx || n < 0 || (n > 0 && (!d_x || !d_y || !d_z))) return VG_E_ARG;
+  if (n > ctx->cap.max_points_per_scan) {
+    ctx->err = "scan larger than max_points_per_scan";
+    return VG_E_CAPACITY;
+  }
+  ctx->cur_x = d_x;
+  ctx->cur_y = d_y;
+  ctx->cur_z = d_z;
+  ctx->cur_i = d_intensity;
+  ctx->cur_n = n;
+  return VG_OK;
+}
+
+static int need_scan(vg_ctx* ctx) {
+  if (ctx->cur_n < 0) {
+    ctx->err = "no scan loaded (vg_scan_load / vg_scan_bind_dev)";
+    return VG_E_STATE;
+  }
+  return VG_OK;
+}
+
+int vg_propagate(vg_ctx* ctx, const double* imu, int m, double pcl_beg_time, double pcl_end_time) {
+  if (!ctx || m < 0 || (m > 0 && !imu)) return VG_E_ARG;
+  (void)pcl_beg_time;
+  return stage_propagate(ctx, imu, m, pcl_end_time);
+}
+
+int vg_downsample_scan(vg_ctx* ctx, int* n_ds) {
+  if (!ctx) return VG_E_ARG;
+  VG_TRY(need_scan(ctx));
+  return stage_downsample(ctx, ctx->cur_x, ctx->cur_y, ctx->cur_z, ctx->cur_i, ctx->cur_n, n_ds);
+}
+
+int vg_lio_state_estimation(vg_ctx* ctx, int* degenerate) {
+  if (!ctx) return VG_E_ARG;
+  VG_TRY(need_scan(ctx));
+  return stage_iekf(ctx, ctx->cur_x, ctx->cur_y, ctx->cur_z, ctx->cur_n, degenerate);
+}
+
+int vg_window_push(vg_ctx* ctx, const double* imu, int m) {
+  if (!ctx || m < 0 || (m > 0 && !imu)) return VG_E_ARG;
+  return stage_window_push(ctx, imu, m);
+}
+
+int vg_cut_voxel_multi(vg_ctx* ctx) {
+  if (!ctx) return VG_E_ARG;
+  return stage_insert(ctx);
+}
+
+int vg_multi_recut(vg_ctx* ctx, int* n_factors) {
+  if (!ctx) return VG_E_ARG;
+  return stage_recut(ctx, n_factors);
+}
+
+int vg_damping_iter(vg_ctx* ctx, int* lm_iters) {
+  if (!ctx) return VG_E_ARG;
+  return stage_ba(ctx, lm_iters);
+}
+
+int vg_multi_margi(vg_ctx* ctx) {
+  if (!ctx) return VG_E_ARG;
+  return stage_margi_slide(ctx);
+}
+
+int vg_step_end(vg_ctx* ctx) {
+  if (!ctx) return VG_E_ARG;
+  return stage_finish(ctx);
+}
+
+int vg_win_count(vg_ctx* ctx, int* n) {
+  if (!ctx || !n) return VG_E_ARG;
+  *n = host_win_count(ctx);
+  return VG_OK;
+}
+
 int vg_profile(vg_ctx* ctx, int on) {
   if (!ctx) return VG_E_ARG;
   ctx->prof_on = on != 0;

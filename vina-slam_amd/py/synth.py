@@ -220,3 +220,28 @@ def ate(traj_a, traj_b):
     a = np.asarray(traj_a)[:, 10:13]
     b = np.asarray(traj_b)[:, 10:13]
     return float(np.sqrt(np.mean(np.sum((a - b) ** 2, axis=1))))
+
+
+def write_replay(path, seq, cconfig, nscan, seed_state=None):
+    """Flat replay file read by vina-slam_amd/examples/vg_replay.cpp."""
+    import ctypes
+    import struct
+    with open(path, "wb") as f:
+        f.write(b"VGRPLAY1")
+        f.write(struct.pack("<i", nscan))
+        f.write(bytes(cconfig))
+        st = seq.gt_state(0) if seed_state is None else seed_state
+        f.write(np.ascontiguousarray(st, dtype="<f8").tobytes())
+        for k in range(nscan):
+            xyz, inten, b, e = seq.scan(k)
+            imu = seq.imu(k)
+            f.write(struct.pack("<ddii", b, e, xyz.shape[0], imu.shape[0]))
+            xyzi = np.concatenate([xyz, inten[:, None]], 1).astype("<f4")
+            f.write(xyzi.tobytes())
+            f.write(np.ascontiguousarray(imu, dtype="<f8").tobytes())
+    _ = ctypes
+
+
+def read_tum(path):
+    """TUM pose file (io.cpp:67-77): t x y z qx qy qz qw -> (n, 8)."""
+    return np.loadtxt(path, ndmin=2)

@@ -70,6 +70,18 @@ def lib():
         L.vg_get_stats.argtypes = [P, ctypes.POINTER(Stats)]
         L.vg_window_states.argtypes = [P, dp, ip]
         L.vg_trajectory.argtypes = [P, dp, ctypes.c_int, ip]
+        L.vg_scan_load.argtypes = [P, fp, fp, ctypes.c_int]
+        L.vg_scan_bind_dev.argtypes = [P, P, P, P, P, ctypes.c_int]
+        L.vg_propagate.argtypes = [P, dp, ctypes.c_int, ctypes.c_double, ctypes.c_double]
+        L.vg_downsample_scan.argtypes = [P, ip]
+        L.vg_lio_state_estimation.argtypes = [P, ip]
+        L.vg_window_push.argtypes = [P, dp, ctypes.c_int]
+        L.vg_cut_voxel_multi.argtypes = [P]
+        L.vg_multi_recut.argtypes = [P, ip]
+        L.vg_damping_iter.argtypes = [P, ip]
+        L.vg_multi_margi.argtypes = [P]
+        L.vg_step_end.argtypes = [P]
+        L.vg_win_count.argtypes = [P, ip]
         L.vg_profile.argtypes = [P, ctypes.c_int]
         L.vg_profile_read.argtypes = [P, ctypes.c_int, dp, ip]
         L.vg_stream.argtypes = [P]
@@ -162,6 +174,49 @@ class Context:
         out = np.zeros((max(n.value, 1), 13))
         self._chk(lib().vg_trajectory(self.h, _d(out), n.value, ctypes.byref(n)), "vg_trajectory")
         return out[: n.value]
+
+    # ---- stage-level API (reference call order, include/vina_gpu.h) ----
+    def scan_load(self, xyz, inten):
+        self._xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+        self._inten = np.ascontiguousarray(inten, dtype=np.float32)
+        self._chk(lib().vg_scan_load(self.h, _f(self._xyz), _f(self._inten), self._xyz.shape[0]), "vg_scan_load")
+
+    def propagate(self, imu, beg, end):
+        imu = np.ascontiguousarray(imu, dtype=np.float64).reshape(-1, 7)
+        self._chk(lib().vg_propagate(self.h, _d(imu), imu.shape[0], beg, end), "vg_propagate")
+
+    def _int_call(self, fn, name):
+        v = ctypes.c_int(0)
+        self._chk(fn(self.h, ctypes.byref(v)), name)
+        return v.value
+
+    def downsample_scan(self):
+        return self._int_call(lib().vg_downsample_scan, "vg_downsample_scan")
+
+    def lio_state_estimation(self):
+        return self._int_call(lib().vg_lio_state_estimation, "vg_lio_state_estimation")
+
+    def window_push(self, imu):
+        imu = np.ascontiguousarray(imu, dtype=np.float64).reshape(-1, 7)
+        self._chk(lib().vg_window_push(self.h, _d(imu), imu.shape[0]), "vg_window_push")
+
+    def cut_voxel_multi(self):
+        self._chk(lib().vg_cut_voxel_multi(self.h), "vg_cut_voxel_multi")
+
+    def multi_recut(self):
+        return self._int_call(lib().vg_multi_recut, "vg_multi_recut")
+
+    def damping_iter(self):
+        return self._int_call(lib().vg_damping_iter, "vg_damping_iter")
+
+    def multi_margi(self):
+        self._chk(lib().vg_multi_margi(self.h), "vg_multi_margi")
+
+    def step_end(self):
+        self._chk(lib().vg_step_end(self.h), "vg_step_end")
+
+    def win_count(self):
+        return self._int_call(lib().vg_win_count, "vg_win_count")
 
     PROFILE_STAGES = ["downsample", "iekf", "insert", "recut", "ba", "margi", "iekf_total"]
 
