@@ -93,11 +93,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     prof = ctx.profile_read()
-    if world > 1:
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    value = world * args.steps / dt
+    value, dt = aggregate(dt, args.steps, world, dev)
 
     # roofline of the dominant kernel (IEKF point loop, k_iekf): algorithmic
     # bytes per launch = 16 B per raw point (fp32 xyz + cached leaf id read)
@@ -133,6 +129,18 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def aggregate(dt, steps, world, dev):
+    """Whole-job scans/s from per-rank wall times: max over ranks (RCCL on GPU,
+    gloo on CPU), every rank processed `steps` scans of its own sequence."""
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    return world * steps / dt, dt
 
 
 def cpu_baseline(args, p, seq):

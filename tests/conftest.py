@@ -7,6 +7,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "vina-slam_amd", "py"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, REPO)
 
 
 def pytest_configure(config):
