@@ -45,3 +45,10 @@ def test_hash_known_answers(oracle_lib):
         h = ((((z % M) * 1000033) % M % 100000000000 + (y % M)) % M * 1000033) % M % 100000000000
         h = (h + (x % M)) % M
         assert L.orc_voxel_hash(x, y, z) == h
+
+
+def test_keys_golden(oracle_lib):
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "voxel_keys.npz"))
+    for s in ("0.05", "0.1", "0.5", "1.0"):
+        assert np.array_equal(oracle.voxel_keys(d["pts"], float(s)), d["k" + s])
