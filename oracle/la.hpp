@@ -18,6 +18,7 @@
 #include <cstring>
 #include <vector>
 #include <algorithm>
+#include <limits>
 
 namespace orc {
 
@@ -207,56 +208,66 @@ struct MatX {
   void setZero() { std::fill(d.begin(), d.end(), 0.0); }
 };
 
-// LDL^T with symmetric diagonal pivoting (largest remaining |diagonal|), as
-// Eigen::LDLT does; solves A x = b for symmetric A. Replaces
-// (Hess + u*D).ldlt().solve(-JacT) at optimizers.cpp:466.
+// Eigen::LDLT<MatrixXd, Lower>::compute + solve restated (Eigen 3.x,
+// Cholesky/LDLT.h: ldlt_inplace<Lower>::unblocked and LDLT::_solve_impl);
+// replaces (Hess + u*D).ldlt().solve(-JacT) at optimizers.cpp:466.
+// The factorization is LEFT-looking: at step k only A(k,k) and column k below
+// it are brought up to date, so the pivot (largest |A(i,i)|, i >= k, first on
+// ties) is chosen among the *original* diagonal entries of the remaining rows,
+// not the Schur-complement diagonal. Only the lower triangle is read (the
+// LiDAR Hessian's diagonal 6x6 blocks are not exactly symmetric,
+// factors.cpp:90-91).
 inline std::vector<double> ldlt_solve(const MatX& Ain, const std::vector<double>& b) {
   const int n = Ain.n;
   MatX A = Ain;
-  // Eigen::LDLT<MatrixXd> (UpLo = Lower) reads only the lower triangle; the
-  // LiDAR Hessian's diagonal 6x6 blocks are not exactly symmetric
-  // (factors.cpp:90-91 adds -0.5*hat(jjt)), so mirror lower -> upper first.
-  for (int i = 0; i < n; i++)
-    for (int j = i + 1; j < n; j++) A(i, j) = A(j, i);
-  std::vector<int> perm(n);
-  for (int i = 0; i < n; i++) perm[i] = i;
-  // in-place: A becomes L (strict lower) and D (diag)
+  std::vector<int> tr(n);
+  std::vector<double> temp(n);
   for (int k = 0; k < n; k++) {
     int p = k;
     double best = std::fabs(A(k, k));
     for (int i = k + 1; i < n; i++)
       if (std::fabs(A(i, i)) > best) { best = std::fabs(A(i, i)); p = i; }
-    if (p != k) {  // symmetric swap of row/col k and p
-      std::swap(perm[k], perm[p]);
-      for (int j = 0; j < n; j++) std::swap(A(k, j), A(p, j));
-      for (int i = 0; i < n; i++) std::swap(A(i, k), A(i, p));
+    tr[k] = p;
+    if (p != k) {  // transposition on the lower triangle only
+      for (int j = 0; j < k; j++) std::swap(A(k, j), A(p, j));
+      for (int i = p + 1; i < n; i++) std::swap(A(i, k), A(i, p));
+      std::swap(A(k, k), A(p, p));
+      for (int i = k + 1; i < p; i++) std::swap(A(i, k), A(p, i));
     }
-    const double dk = A(k, k);
-    std::vector<double> c(n, 0.0);
-    for (int i = k + 1; i < n; i++) c[i] = A(i, k);
-    for (int i = k + 1; i < n; i++) {
-      const double lik = (dk != 0.0) ? c[i] / dk : 0.0;
-      for (int j = k + 1; j <= i; j++) A(i, j) -= lik * c[j];
-      A(i, k) = lik;
+    if (k > 0) {
+      for (int j = 0; j < k; j++) temp[j] = A(j, j) * A(k, j);
+      double s = 0.0;
+      for (int j = 0; j < k; j++) s += A(k, j) * temp[j];
+      A(k, k) -= s;
+      for (int i = k + 1; i < n; i++) {
+        double t = 0.0;
+        for (int j = 0; j < k; j++) t += A(i, j) * temp[j];
+        A(i, k) -= t;
+      }
     }
-    for (int i = k + 1; i < n; i++)
-      for (int j = i + 1; j < n; j++) A(i, j) = A(j, i);  // symmetric copy for later pivot swaps
+    const double akk = A(k, k);
+    if (k == 0 && akk == 0.0) {  // all-zero diagonal: Eigen stops, identity transpositions
+      for (int j = 0; j < n; j++) tr[j] = j;
+      break;
+    }
+    if (akk != 0.0)
+      for (int i = k + 1; i < n; i++) A(i, k) /= akk;
   }
-  std::vector<double> y(n);
-  for (int i = 0; i < n; i++) y[i] = b[perm[i]];
-  for (int i = 0; i < n; i++) {  // L y = Pb
-    double s = y[i];
-    for (int j = 0; j < i; j++) s -= A(i, j) * y[j];
-    y[i] = s;
+  std::vector<double> x(b);
+  for (int k = 0; k < n; k++) std::swap(x[k], x[tr[k]]);  // P b
+  for (int i = 0; i < n; i++) {                          // L^-1
+    double s = 0.0;
+    for (int j = 0; j < i; j++) s += A(i, j) * x[j];
+    x[i] -= s;
   }
-  for (int i = 0; i < n; i++) y[i] = (A(i, i) != 0.0) ? y[i] / A(i, i) : 0.0;
-  for (int i = n - 1; i >= 0; i--) {  // L^T x = y
-    double s = y[i];
-    for (int j = i + 1; j < n; j++) s -= A(j, i) * y[j];
-    y[i] = s;
+  for (int i = 0; i < n; i++)  // pseudo-inverse of D (Eigen bug 241)
+    x[i] = (std::fabs(A(i, i)) > std::numeric_limits<double>::min()) ? x[i] / A(i, i) : 0.0;
+  for (int i = n - 1; i >= 0; i--) {  // L^-T
+    double s = 0.0;
+    for (int j = i + 1; j < n; j++) s += A(j, i) * x[j];
+    x[i] -= s;
   }
-  std::vector<double> x(n);
-  for (int i = 0; i < n; i++) x[perm[i]] = y[i];
+  for (int k = n - 1; k >= 0; k--) std::swap(x[k], x[tr[k]]);  // P^T
   return x;
 }
 

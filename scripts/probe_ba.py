@@ -1,0 +1,54 @@
+"""Phase clocks of the probed kernels (instrumented build, `make -C vina-slam_amd probe`).
+
+    VINA_GPU_LIB=vina-slam_amd/lib_probe/libvina_gpu.so python scripts/probe_ba.py
+"""
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("VINA_GPU_LIB", os.path.join(REPO, "vina-slam_amd", "lib_probe", "libvina_gpu.so"))
+sys.path.insert(0, os.path.join(REPO, "vina-slam_amd", "py"))
+import numpy as np  # noqa: E402
+
+import synth  # noqa: E402
+import vgconfig  # noqa: E402
+import vgpu  # noqa: E402
+
+PHASES = {0: "assemble", 1: "diag/tables", 2: "rank", 3: "tile fill", 4: "panel diag tile", 5: "panel rows",
+          6: "trailing mfma", 7: "tri solves", 8: "trial/q1"}
+
+
+def main(nscan=40, lidar="64line"):
+    p = vgconfig.load("mid360")
+    g = p["General"]
+    seq = synth.Sequence(lidar, 0, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
+    ctx = vgpu.Context(vgconfig.to_c(p), device=0)
+    ctx.seed(seq.gt_state(0))
+    L = vgpu.lib()
+    buf = (ctypes.c_ulonglong * 64)()
+    for k in range(nscan):
+        xyz, it, b, e = seq.scan(k)
+        ctx.step(xyz, it, b, e, seq.imu(k))
+        if k == 11:
+            L.vg_probe_read(buf, 64)  # clear the warm-up
+            L.vg_probe_read_map(buf, 64)
+    L.vg_probe_read(buf, 64)
+    calls = max(buf[63], 1)
+    print("k_ba_solve real calls:", buf[63])
+    tot = 0.0
+    for k, name in PHASES.items():
+        us = buf[k] * 0.01 / calls
+        tot += us
+        print("  %-16s %8.2f us/call" % (name, us))
+    print("  %-16s %8.2f us/call" % ("total", tot))
+    L.vg_probe_read_map(buf, 64)
+    na = max(buf[62], 1)
+    print("k_rc_apply calls:", buf[62])
+    for k, name in {16: "sort subs+events", 17: "child alloc", 18: "keys", 19: "bitonic", 20: "push", 21: "finish"}.items():
+        print("  %-16s %8.2f us/call" % (name, buf[k] * 0.01 / na))
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -81,3 +81,25 @@ def test_cpp_replay_driver_matches(oracle_lib):
     to = orc.trajectory()
     assert np.allclose(tum[:, 0], to[:, 0])
     assert np.abs(tum[:, 1:4] - to[:, 10:13]).max() < 1e-6
+
+
+def test_recut_replay_path_equals_fast_path():
+    """The host-sized recut replay (taken when a level's subdivision exceeds the
+    single-workgroup apply's LDS capacity) gives bit-identical results."""
+    import ctypes
+    p = vgconfig.load("mid360")
+    seq = _seq(p, seq_id=6)
+    a = vgpu.Context(vgconfig.to_c(p), **CAP)
+    b = vgpu.Context(vgconfig.to_c(p), **CAP)
+    assert vgpu.lib().vgx_debug(b.h, 1, 0) == 0  # every level replays
+    a.seed(seq.gt_state(0))
+    b.seed(seq.gt_state(0))
+    for k in range(14):
+        xyz, it, beg, end = seq.scan(k)
+        imu = seq.imu(k)
+        a.step(xyz, it, beg, end, imu)
+        b.step(xyz, it, beg, end, imu)
+        sa, sb = a.stats(), b.stats()
+        assert sa == sb, (k, sa, sb)
+    assert np.array_equal(a.trajectory(), b.trajectory())
+    assert np.array_equal(a.window_states(), b.window_states())

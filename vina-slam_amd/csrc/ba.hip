@@ -7,40 +7,41 @@
 // (imu_preintegration.cpp:97-163, 239-246).
 //
 // Per LM iteration, all device-resident, no host round trip:
-//   k_ba_comp    one lane per (factor, frame): Auk (3x6), viRiTuk, the diagonal
-//                6x6 block and the gradient piece                (fp64 VALU)
-//   k_ba_hred    one workgroup per chunk of 16 factors staged in LDS: every
-//                lane owns output entries of the 60x60 lower triangle + 60 + 1
-//                and sums the chunk -> per-chunk partials (deterministic)
+//   k_ba_hess    one workgroup per chunk of 2 x (256/W) factors: one lane per
+//                (factor, frame) evaluates Auk, the diagonal 6x6 block and the
+//                gradient piece (fp64 VALU); the off-diagonal blocks, sums of
+//                rank-1 terms, are reduced as X^T S X on fp64 MFMA from LDS
+//                -> per-chunk partials (deterministic)
 //   k_ba_hfinal  ordered sum of the chunk partials
 //   k_ba_imu     one workgroup per IMU factor: residual, 15x30 Jacobian,
 //                J^T C J (30x30) and J^T C r
-//   k_ba_solve   one 1024-lane workgroup: assemble the 15W x 15W system
+//   k_ba_solve   one 256-lane workgroup: assemble the 15W x 15W system
 //                (IMU blocks x imu_coef + LiDAR 6x6 blocks), gauge frame 0,
-//                Marquardt damping, LDL^T with diagonal pivoting in LDS
-//                (lower triangle, 90 KB), the trial state and q1
+//                Marquardt damping, blocked LDL^T of the pivoted system in
+//                LDS (16x16 tiles, MFMA f64 trailing updates), the trial
+//                state and q1
 //   k_ba_resid   one lane per factor: merge clusters at the trial poses, 3x3
 //                eigen, write the trial eig/cluster (the side effect margi
 //                consumes), chunk residual partials
 //   k_ba_imures  IMU residuals at the trial state
 //   k_ba_control LM accept/reject, Nielsen damping update, bias restore,
 //                convergence flag (1 lane)
-// Kernels early-exit on the device-side `done` / `calc_hess` flags, so the
-// host enqueues all 10 iterations (optimizers.cpp:449) without syncing.
+// Kernels early-exit on the device-side `done` / `calc_hess` flags; the host
+// enqueues two iterations at a time and reads `done` in between.
 #include "vg_dev.h"
 
 namespace vg {
 
 constexpr int kMaxW = 16;
-constexpr int kComp = 49;     // per (factor, frame): Auk 18, viRiTuk 3, ni 1, Hb lower 21, jjt 6
 constexpr int kCompF = 24;    // per factor: umumT 9, ukukT 9, uk 3, NN, coe, lmbd0
-constexpr int kFC = 16;       // factors per reduction chunk
 constexpr int kImuRec = 64 + 225;  // preintegration record + cov_inv
 
 struct BaState {             // device-resident LM state
   double u, v, res1, res2, q1;
   int calc_hess, done, iters, pad;
 };
+
+typedef double v4d __attribute__((ext_vector_type(4)));
 
 // x state per frame: R 9, p 3, v 3, bg 3, ba 3, g 3 = 24 doubles
 constexpr int kX = 24;
@@ -67,145 +68,199 @@ __device__ __forceinline__ void factor_basics(const double* e, const Clu& pcr, d
   f[23] = e[0];
 }
 
-// acc_evaluate2 per (factor, frame) — factors.cpp:57-97
-__global__ void __launch_bounds__(256) k_ba_comp(int nf, int W, const int* __restrict__ fac_node, const double* __restrict__ fac_eig,
-                          const Clu* __restrict__ fac_pcr, const Clu* __restrict__ pcrs, const int* __restrict__ mpring,
-                          const double* __restrict__ xs, double* __restrict__ comp, double* __restrict__ compf,
-                          const BaState* __restrict__ st) {
-  if (st->done || !st->calc_hess) return;
-  const int total = nf * W;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-    const int a = t / W, i = t % W;
-    const double* e = &fac_eig[(size_t)a * 12];
-    const Clu pa = fac_pcr[a];
-    double f[kCompF];
-    factor_basics(e, pa, f);
-    if (i == 0)
-      for (int k = 0; k < kCompF; k++) compf[(size_t)a * kCompF + k] = f[k];
-    double* o = &comp[((size_t)a * W + i) * kComp];
-    const Clu s = pcrs[(size_t)fac_node[a] * W + mpring[i]];
-    if (s.N == 0) {
-      for (int k = 0; k < kComp; k++) o[k] = 0.0;
-      continue;
+// acc_evaluate2 per (factor, frame) — factors.cpp:57-97. Outputs the
+// diagonal 6x6 block Hb (lower, 21), the gradient piece jjt (6) and the three
+// 6-vectors whose outer products make every off-diagonal block:
+//   Auk_i^T umumT Auk_j = sum_{m=1,2} c_m (Auk_i^T u_m)(Auk_j^T u_m)^T,
+//       umumT = sum_m c_m u_m u_m^T, c_m = 2/(lambda_0 - lambda_m)
+//   the correction terms (factors.cpp:80-86) = -(2/NN^2) h_i h_j^T,
+//       h_i = [viRiTuk; n_i uk]
+__device__ __forceinline__ void factor_frame(const double* e, const Clu& pa, const Clu& s, const double* x,
+                                             double* hb, double* jjt_o, double* g1, double* g2, double* h) {
+  double f[kCompF];
+  factor_basics(e, pa, f);
+  const double NN = f[21];
+  M3 umumT, ukukT;
+  for (int k = 0; k < 9; k++) {
+    umumT[k] = f[k];
+    ukukT[k] = f[9 + k];
+  }
+  const V3 uk = v3(f[18], f[19], f[20]);
+  const V3 vBar = v3(pa.v[0] / NN, pa.v[1] / NN, pa.v[2] / NN);
+  const M3 Pi = clu_Pm(s);
+  const V3 vi = clu_v(s);
+  const M3 Ri = ld_m3(x);
+  const double ni = (double)s.N;
+  const M3 vihat = hat(vi);
+  const V3 RiTuk = mul(tr(Ri), uk);
+  const M3 RiTukhat = hat(RiTuk);
+  const V3 PiRiTuk = mul(Pi, RiTuk);
+  const V3 viRiTuk = mul(vihat, RiTuk);
+  const V3 ti_v = sub(ld_v3(x + 9), vBar);
+  const double ukTti_v = dot3(uk, ti_v);
+  const M3 combo1 = add(hat(PiRiTuk), scl(vihat, ukTti_v));
+  const V3 combo2 = add(mul(Ri, vi), scl(ti_v, ni));
+  M<3, 6> A;
+  M3 A1 = sub(mul(add(mul(Ri, Pi), outer3(ti_v, vi)), RiTukhat), mul(Ri, combo1));
+  M3 A2 = add(outer3(combo2, uk), scl(M3::I(), dot3(combo2, uk)));
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) {
+      A(r, c) = A1(r, c) / NN;
+      A(r, 3 + c) = A2(r, c) / NN;
     }
-    const double NN = f[21];
-    M3 umumT, ukukT;
-    for (int k = 0; k < 9; k++) {
-      umumT[k] = f[k];
-      ukukT[k] = f[9 + k];
+  V6 jjt = mul(tr(A), uk);
+  M3 HRt = scl(outer3(viRiTuk, uk), 2.0 / NN * (1.0 - ni / NN));
+  M6 Hb = mul(mul(tr(A), umumT), A);
+  M3 c00 = sub(sub(scl(mul(sub(combo1, mul(RiTukhat, Pi)), RiTukhat), 2.0 / NN),
+                   scl(outer3(viRiTuk, viRiTuk), 2.0 / NN / NN)),
+               scl(hat(v3(jjt[0], jjt[1], jjt[2])), 0.5));
+  M3 c11 = scl(ukukT, 2.0 / NN * (ni - ni * ni / NN));
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) {
+      Hb(r, c) += c00(r, c);
+      Hb(r, 3 + c) += HRt(r, c);
+      Hb(3 + r, c) += HRt(c, r);
+      Hb(3 + r, 3 + c) += c11(r, c);
     }
-    const V3 uk = v3(f[18], f[19], f[20]);
-    const V3 vBar = v3(pa.v[0] / NN, pa.v[1] / NN, pa.v[2] / NN);
-    const M3 Pi = clu_Pm(s);
-    const V3 vi = clu_v(s);
-    const M3 Ri = ld_m3(&xs[(size_t)i * kX]);
-    const double ni = (double)s.N;
-    const M3 vihat = hat(vi);
-    const V3 RiTuk = mul(tr(Ri), uk);
-    const M3 RiTukhat = hat(RiTuk);
-    const V3 PiRiTuk = mul(Pi, RiTuk);
-    const V3 viRiTuk = mul(vihat, RiTuk);
-    const V3 ti_v = sub(ld_v3(&xs[(size_t)i * kX + 9]), vBar);
-    const double ukTti_v = dot3(uk, ti_v);
-    const M3 combo1 = add(hat(PiRiTuk), scl(vihat, ukTti_v));
-    const V3 combo2 = add(mul(Ri, vi), scl(ti_v, ni));
-    M<3, 6> A;
-    M3 A1 = sub(mul(add(mul(Ri, Pi), outer3(ti_v, vi)), RiTukhat), mul(Ri, combo1));
-    M3 A2 = add(outer3(combo2, uk), scl(M3::I(), dot3(combo2, uk)));
-    for (int r = 0; r < 3; r++)
-      for (int c = 0; c < 3; c++) {
-        A(r, c) = A1(r, c) / NN;
-        A(r, 3 + c) = A2(r, c) / NN;
-      }
-    V6 jjt = mul(tr(A), uk);
-    M3 HRt = scl(outer3(viRiTuk, uk), 2.0 / NN * (1.0 - ni / NN));
-    M6 Hb = mul(mul(tr(A), umumT), A);
-    M3 c00 = sub(sub(scl(mul(sub(combo1, mul(RiTukhat, Pi)), RiTukhat), 2.0 / NN),
-                     scl(outer3(viRiTuk, viRiTuk), 2.0 / NN / NN)),
-                 scl(hat(v3(jjt[0], jjt[1], jjt[2])), 0.5));
-    M3 c11 = scl(ukukT, 2.0 / NN * (ni - ni * ni / NN));
-    for (int r = 0; r < 3; r++)
-      for (int c = 0; c < 3; c++) {
-        Hb(r, c) += c00(r, c);
-        Hb(r, 3 + c) += HRt(r, c);
-        Hb(3 + r, c) += HRt(c, r);
-        Hb(3 + r, 3 + c) += c11(r, c);
-      }
-    for (int k = 0; k < 18; k++) o[k] = A[k];
-    for (int k = 0; k < 3; k++) o[18 + k] = viRiTuk[k];
-    o[21] = ni;
-    int q = 22;
-    for (int r = 0; r < 6; r++)
-      for (int c = 0; c <= r; c++) o[q++] = Hb(r, c);  // lower triangle
-    for (int k = 0; k < 6; k++) o[43 + k] = jjt[k];
+  int q = 0;
+  for (int r = 0; r < 6; r++)
+    for (int c = 0; c <= r; c++) hb[q++] = Hb(r, c);
+  for (int k = 0; k < 6; k++) jjt_o[k] = jjt[k];
+  const V3 u1 = v3(e[3 + 0 * 3 + 1], e[3 + 1 * 3 + 1], e[3 + 2 * 3 + 1]);
+  const V3 u2 = v3(e[3 + 0 * 3 + 2], e[3 + 1 * 3 + 2], e[3 + 2 * 3 + 2]);
+  for (int k = 0; k < 6; k++) {
+    g1[k] = A(0, k) * u1[0] + A(1, k) * u1[1] + A(2, k) * u1[2];
+    g2[k] = A(0, k) * u2[0] + A(1, k) * u2[1] + A(2, k) * u2[2];
+  }
+  for (int k = 0; k < 3; k++) {
+    h[k] = viRiTuk[k];
+    h[3 + k] = ni * uk[k];
   }
 }
 
-// outputs: 1830 lower entries of the 6W x 6W LiDAR Hessian (row-major lower),
-// then 6W gradient, then the residual
+// outputs per chunk: 1830 lower entries of the 6W x 6W LiDAR Hessian
+// (row-major lower), then 6W gradient, then the residual
 __device__ __forceinline__ int lower_idx(int r, int c) { return r * (r + 1) / 2 + c; }
 
-__global__ void __launch_bounds__(256) k_ba_hred(int nf, int W, const double* __restrict__ comp,
-                                                 const double* __restrict__ compf, double* __restrict__ part,
-                                                 const BaState* __restrict__ st) {
+constexpr int kHessThreads = 256;
+__host__ __device__ constexpr int hess_fs(int W) { return kHessThreads / W < 64 ? kHessThreads / W : 64; }  // factors per sub-chunk
+__host__ __device__ constexpr int hess_ks(int W) { return (3 * hess_fs(W) + 3) / 4 * 4; }  // GEMM K per sub-chunk
+__host__ __device__ constexpr int hess_nt(int W) { return (6 * W + 15) / 16; }           // 16-wide output tiles
+__host__ __device__ constexpr int hess_xs(int W) { return hess_nt(W) * 16 + 16; }        // X row stride (+16: rows k, k+1 in opposite LDS halves)
+__host__ __device__ constexpr int hess_chunk(int W) { return 2 * hess_fs(W); }      // factors per workgroup
+
+// One workgroup per chunk of factors, no HBM intermediates: lane (f, i)
+// evaluates factor f of the sub-chunk at frame i, keeps the coe-weighted
+// diagonal block / gradient in registers and writes its three rank-1 rows to
+// X (LDS); the off-diagonal blocks are then X^T S X on v_mfma_f64_16x16x4
+// (one wave per lower 16x16 output tile, accumulators live across
+// sub-chunks). Chunk partials go to `part` (summed by k_ba_hfinal).
+__global__ void __launch_bounds__(kHessThreads) k_ba_hess(int nf, int W, const int* __restrict__ fac_node,
+                                                          const double* __restrict__ fac_eig,
+                                                          const Clu* __restrict__ fac_pcr, const Clu* __restrict__ pcrs,
+                                                          const int* __restrict__ mpring, const double* __restrict__ xs,
+                                                          double* __restrict__ part, const BaState* __restrict__ st) {
   if (st->done || !st->calc_hess) return;
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int a0 = blockIdx.x * kFC;
-  const int na = min(kFC, nf - a0);
-  const int per = W * kComp + kCompF;
-  for (int t = threadIdx.x; t < na * per; t += blockDim.x) {
-    int a = t / per, k = t % per;
-    sm[t] = (k < W * kComp) ? comp[((size_t)(a0 + a) * W) * kComp + k] : compf[(size_t)(a0 + a) * kCompF + (k - W * kComp)];
-  }
-  __syncthreads();
-  const int L = 6 * W;
-  const int nl = L * (L + 1) / 2;
-  const int nout = nl + L + 1;
-  for (int e = threadIdx.x; e < nout; e += blockDim.x) {
-    double acc = 0.0;
-    if (e < nl) {
-      int row = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-      while (lower_idx(row + 1, 0) <= e) row++;
-      while (lower_idx(row, 0) > e) row--;
-      int col = e - lower_idx(row, 0);
-      int bi = row / 6, r = row % 6, bj = col / 6, c = col % 6;
-      for (int a = 0; a < na; a++) {
-        const double* F = &sm[a * per + W * kComp];
-        const double coe = F[22];
-        if (bi == bj) {
-          const double* o = &sm[a * per + bi * kComp];
-          if (o[21] != 0.0) acc += coe * o[22 + lower_idx(r, c)];
-        } else {
-          // lower entry (6bi+r, 6bj+c) = upper block (i=bj, j=bi) entry (c, r)
-          const double* oi = &sm[a * per + bj * kComp];
-          const double* oj = &sm[a * per + bi * kComp];
-          const double ni = oi[21], nj = oj[21];
-          if (ni == 0.0 || nj == 0.0) continue;
-          const double NN = F[21];
-          // (Auk_i^T umumT Auk_j)(c, r)
-          double tmp[3];
-          for (int k = 0; k < 3; k++) tmp[k] = F[k * 3 + 0] * oj[0 * 6 + r] + F[k * 3 + 1] * oj[1 * 6 + r] + F[k * 3 + 2] * oj[2 * 6 + r];
-          double hb = oi[0 * 6 + c] * tmp[0] + oi[1 * 6 + c] * tmp[1] + oi[2 * 6 + c] * tmp[2];
-          const double* vi = &oi[18];
-          const double* vj = &oj[18];
-          const double* uk = &F[18];
-          if (c < 3 && r < 3) hb += -2.0 / NN / NN * (vi[c] * vj[r]);
-          else if (c < 3) hb += -2.0 * nj / NN / NN * (vi[c] * uk[r - 3]);
-          else if (r < 3) hb += -2.0 * ni / NN / NN * (uk[c - 3] * vj[r]);
-          else hb += -2.0 * ni * nj / NN / NN * (uk[c - 3] * uk[r - 3]);
-          acc += coe * hb;
+  extern __shared__ __attribute__((aligned(16))) double X[];
+  __shared__ double S[kHessThreads];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int FS = hess_fs(W), KS = hess_ks(W), NT = hess_nt(W), XS = hess_xs(W);
+  const int L = 6 * W, nl = L * (L + 1) / 2, nout = nl + L + 1;
+  const int f = tid / W, i = tid % W;
+  const bool active = f < FS;
+  const int a_begin = blockIdx.x * hess_chunk(W);
+  const int a_end = min(nf, a_begin + hess_chunk(W));
+  double hb[21], jj[6], res = 0.0;
+  for (int k = 0; k < 21; k++) hb[k] = 0.0;
+  for (int k = 0; k < 6; k++) jj[k] = 0.0;
+  const int ntl = NT * (NT + 1) / 2;
+  v4d acc[4];  // <= 15 lower tiles (W <= 11) over 4 waves
+  for (int s = 0; s < 4; s++) acc[s] = v4d{0.0, 0.0, 0.0, 0.0};
+  for (int sub = a_begin; sub < a_end; sub += FS) {
+    for (int t = tid; t < KS * XS; t += kHessThreads) X[t] = 0.0;
+    for (int t = tid; t < KS; t += kHessThreads) S[t] = 0.0;
+    __syncthreads();
+    const int a = sub + f;
+    if (active && a < a_end) {
+      const double* e = &fac_eig[(size_t)a * 12];
+      const Clu pa = fac_pcr[a];
+      const double coe = 1.0;  // octree.cpp:507
+      if (i == 0) {
+        res += coe * e[0];
+        const double NN = (double)pa.N;
+        S[3 * f + 0] = coe * (2.0 / (e[0] - e[1]));
+        S[3 * f + 1] = coe * (2.0 / (e[0] - e[2]));
+        S[3 * f + 2] = -coe * (2.0 / NN / NN);
+      }
+      const Clu sc = pcrs[(size_t)fac_node[a] * W + mpring[i]];
+      if (sc.N != 0) {
+        double hbi[21], jji[6], g1[6], g2[6], h[6];
+        factor_frame(e, pa, sc, &xs[(size_t)i * kX], hbi, jji, g1, g2, h);
+        for (int k = 0; k < 21; k++) hb[k] += coe * hbi[k];
+        for (int k = 0; k < 6; k++) jj[k] += coe * jji[k];
+        double* x0 = &X[(size_t)(3 * f) * XS + 6 * i];
+        for (int k = 0; k < 6; k++) {
+          x0[k] = g1[k];
+          x0[XS + k] = g2[k];
+          x0[2 * XS + k] = h[k];
         }
       }
-    } else if (e < nl + L) {
-      int g = e - nl, bi = g / 6, r = g % 6;
-      for (int a = 0; a < na; a++) {
-        const double* o = &sm[a * per + bi * kComp];
-        acc += sm[a * per + W * kComp + 22] * o[43 + r];
-      }
-    } else {
-      for (int a = 0; a < na; a++) acc += sm[a * per + W * kComp + 22] * sm[a * per + W * kComp + 23];
     }
-    part[(size_t)blockIdx.x * nout + e] = acc;
+    __syncthreads();
+    for (int q = wave, slot = 0; q < ntl; q += kHessThreads / 64, slot++) {
+      int TI = 0;
+      while ((TI + 1) * (TI + 2) / 2 <= q) TI++;
+      const int TJ = q - TI * (TI + 1) / 2;
+      const int cc = lane & 15, rq = lane >> 4;
+      v4d c = acc[slot];
+      for (int k0 = 0; k0 < KS; k0 += 4) {
+        const int k = k0 + rq;
+        const double av = S[k] * X[(size_t)k * XS + 16 * TI + cc];
+        const double bv = X[(size_t)k * XS + 16 * TJ + cc];
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c, 0, 0, 0);
+      }
+      acc[slot] = c;
+    }
+    __syncthreads();
+  }
+  double* out = &part[(size_t)blockIdx.x * nout];
+  // off-diagonal blocks from the MFMA tiles (diagonal 6x6 blocks come from Hb)
+  for (int q = wave, slot = 0; q < ntl; q += kHessThreads / 64, slot++) {
+    int TI = 0;
+    while ((TI + 1) * (TI + 2) / 2 <= q) TI++;
+    const int TJ = q - TI * (TI + 1) / 2;
+    const int cc = lane & 15, rq = lane >> 4;
+    for (int g = 0; g < 4; g++) {
+      const int row = 16 * TI + rq + 4 * g, colx = 16 * TJ + cc;
+      if (row < L && colx <= row && row / 6 != colx / 6) out[lower_idx(row, colx)] = acc[slot][g];
+    }
+  }
+  // per-frame diagonal blocks, gradient and residual: ordered sum over f
+  double* R = X;
+  if (active) {
+    for (int k = 0; k < 21; k++) R[tid * 28 + k] = hb[k];
+    for (int k = 0; k < 6; k++) R[tid * 28 + 21 + k] = jj[k];
+    R[tid * 28 + 27] = res;
+  }
+  __syncthreads();
+  for (int e = tid; e < W * 27 + 1; e += kHessThreads) {
+    if (e == W * 27) {
+      double sres = 0.0;
+      for (int ff = 0; ff < FS; ff++) sres += R[(ff * W) * 28 + 27];
+      out[nl + L] = sres;
+      continue;
+    }
+    const int fi = e / 27, k = e % 27;
+    double sv = 0.0;
+    for (int ff = 0; ff < FS; ff++) sv += R[(ff * W + fi) * 28 + k];
+    if (k < 21) {
+      int r = 0;
+      while ((r + 1) * (r + 2) / 2 <= k) r++;
+      const int c = k - r * (r + 1) / 2;
+      out[lower_idx(6 * fi + r, 6 * fi + c)] = sv;
+    } else {
+      out[nl + 6 * fi + (k - 21)] = sv;
+    }
   }
 }
 
@@ -349,164 +404,326 @@ __global__ void __launch_bounds__(256) k_ba_imures(int nimu, const double* __res
   res[k] = s;
 }
 
-// packed lower storage of the n x n system
+// packed lower storage of the n x n system (Hcalc)
 __device__ __forceinline__ int lo(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
 
-// assemble (or reload), gauge, damp, LDL^T-solve, trial state, IMU bias trial
-__global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, double imu_coef, const double* __restrict__ hl,
+// ---- LDS tile store of the permuted system: lower block triangle of 16x16
+// fp64 tiles, tile (I,J) (I >= J) at I(I+1)/2 + J, element (r,c) at
+// r*16 + (c ^ r): rows and columns of a tile both read conflict-free, which
+// the MFMA operand loads (16 rows of one column per lane group) need.
+constexpr int kTile = 16;
+constexpr int kMaxNB = 11;  // 15W <= 176
+__device__ __forceinline__ int tix(int I, int J) { return I * (I + 1) / 2 + J; }
+__device__ __forceinline__ int tel(int r, int c) { return r * 16 + (c ^ r); }
+
+__device__ __forceinline__ double bcast(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo32 = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const int hi32 = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi32 << 32) | (unsigned int)lo32);
+}
+
+// assemble (or reload), gauge, damp, LDL^T-solve, trial state, IMU bias trial.
+//
+// Eigen's LDLT (the oracle's ldlt_solve) is left-looking, so its pivot order
+// depends only on the damped diagonal: it is the descending order of |diag|.
+// The kernel takes that permutation up front (rank sort), loads P A P^T into
+// the tile store and factors it without further pivoting, 16 columns per
+// panel: wave 0 factors the diagonal tile in registers, one lane per row
+// solves the panel below it, and the trailing update A22 -= L21 D L21^T runs
+// on v_mfma_f64_16x16x4 (one wave per 16x16 tile). Triangular solves run
+// blocked on wave 0. Ties in |diag| may order differently from Eigen's
+// sequential scan; that changes rounding only.
+__global__ void __launch_bounds__(256) k_ba_solve(int W, int nimu, double imu_coef, const double* __restrict__ hl,
                                                    const double* __restrict__ imuout, double* __restrict__ Hcalc,
                                                    double* __restrict__ Jcalc, const double* __restrict__ xs,
                                                    double* __restrict__ xt, double* __restrict__ bias,
                                                    double* __restrict__ dxi_out, BaState* __restrict__ st) {
   if (st->done) return;
-  extern __shared__ __attribute__((aligned(16))) double A[];
+  extern __shared__ __attribute__((aligned(16))) double T[];
+  constexpr int kN = kMaxNB * kTile;
+  __shared__ double Jv[kN], Dv[kN], xv[kN], col[kN], tk[256], dK[16], rdK[16], tb[16];
+  __shared__ int ip[kN], cnt[kN];
+  __shared__ unsigned char tI[kMaxNB * (kMaxNB + 1) / 2], tJ[kMaxNB * (kMaxNB + 1) / 2];
   const int n = 15 * W;
   const int nn = n * (n + 1) / 2;
-  __shared__ double J[15 * kMaxW], D[15 * kMaxW], col[15 * kMaxW], y[15 * kMaxW];
-  __shared__ int perm[15 * kMaxW];
-  __shared__ int piv;
+  const int NB = (n + kTile - 1) / kTile, N = NB * kTile;
+  const int ntile = NB * (NB + 1) / 2;
   const int tid = threadIdx.x, nt = blockDim.x;
-  const bool calc = st->calc_hess != 0;
+  const int lane = tid & 63, wave = tid >> 6, nwave = nt >> 6;
   const double u = st->u;
-  if (calc) {
-    for (int t = tid; t < nn; t += nt) A[t] = 0.0;
-    for (int t = tid; t < n; t += nt) J[t] = 0.0;
-    __syncthreads();
-    // IMU blocks: rows/cols 15k .. 15k+29, accumulated in k order (divide_thread 215-222)
-    for (int k = 0; k < nimu; k++) {
-      const double* o = &imuout[(size_t)k * 931];
-      for (int t = tid; t < 900; t += nt) {
-        int r = t / 30, c = t % 30;
-        if (r >= c) A[lo(15 * k + r, 15 * k + c)] += o[t];
-      }
-      for (int t = tid; t < 30; t += nt) J[15 * k + t] += o[900 + t];
-      __syncthreads();
-    }
-    for (int t = tid; t < nn; t += nt) A[t] *= imu_coef;
-    for (int t = tid; t < n; t += nt) J[t] *= imu_coef;
-    __syncthreads();
-    // hess_plus (optimizers.cpp:171-179): LiDAR 6x6 blocks into the rot/pos sub-blocks
+  VG_PROBE_BEGIN();
+  if (st->calc_hess != 0) {
+    // every lower entry in one pass, in the accumulation order of the host
+    // loop (divide_thread 215-222: IMU factors k ascending, x imu_coef, then
+    // hess_plus 171-179 adds the LiDAR 6x6 blocks)
     const int L = 6 * W;
-    for (int t = tid; t < L * (L + 1) / 2; t += nt) {
-      int row = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-      while ((row + 1) * (row + 2) / 2 <= t) row++;
-      while (row * (row + 1) / 2 > t) row--;
-      int colx = t - row * (row + 1) / 2;
-      int R = (row / 6) * 15 + row % 6, C = (colx / 6) * 15 + colx % 6;
-      A[lo(R, C)] += hl[t];
+#pragma unroll 4
+    for (int t = tid; t < nn; t += nt) {
+      int R = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+      while ((R + 1) * (R + 2) / 2 <= t) R++;
+      while (R * (R + 1) / 2 > t) R--;
+      const int C = t - R * (R + 1) / 2;
+      const int bR = R / 15, bC = C / 15, rR = R % 15, rC = C % 15;
+      double v = 0.0;
+      for (int k = bR > 0 ? bR - 1 : 0; k <= bC && k < nimu; k++)
+        v += imuout[(size_t)k * 931 + (R - 15 * k) * 30 + (C - 15 * k)];
+      v *= imu_coef;
+      if (rR < 6 && rC < 6) {
+        const int lr = bR * 6 + rR, lc = bC * 6 + rC;
+        v += hl[lr * (lr + 1) / 2 + lc];
+      }
+      Hcalc[t] = v;
     }
-    for (int t = tid; t < L; t += nt) J[(t / 6) * 15 + t % 6] += hl[L * (L + 1) / 2 + t];
+    for (int t = tid; t < n; t += nt) {
+      const int b = t / 15, r = t % 15;
+      double v = 0.0;
+      if (b >= 1 && b - 1 < nimu) v += imuout[(size_t)(b - 1) * 931 + 900 + r + 15];
+      if (b < nimu) v += imuout[(size_t)b * 931 + 900 + r];
+      v *= imu_coef;
+      if (r < 6) v += hl[L * (L + 1) / 2 + b * 6 + r];
+      Jcalc[t] = v;
+    }
     __syncthreads();
-    for (int t = tid; t < nn; t += nt) Hcalc[t] = A[t];
-    for (int t = tid; t < n; t += nt) Jcalc[t] = J[t];
-  } else {
-    for (int t = tid; t < nn; t += nt) A[t] = Hcalc[t];
-    for (int t = tid; t < n; t += nt) J[t] = Jcalc[t];
+  }
+  VG_PROBE_MARK(0);
+  // gauge frame 0 (optimizers.cpp:460-463), D = diag(H), tile index tables
+  for (int t = tid; t < N; t += nt) {
+    Dv[t] = t < n ? (t < 15 ? 1.0 : Hcalc[lo(t, t)]) : 0.0;
+    Jv[t] = (t < n && t >= 15) ? Jcalc[t] : 0.0;
+    cnt[t] = 0;
+  }
+  if (tid < ntile) {
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= tid) I++;
+    tI[tid] = (unsigned char)I;
+    tJ[tid] = (unsigned char)(tid - I * (I + 1) / 2);
   }
   __syncthreads();
-  // gauge frame 0 (optimizers.cpp:460-463)
-  for (int t = tid; t < 15 * n; t += nt) {
-    int r = t / n, c = t % n;
-    A[lo(r, c)] = (r == c) ? 1.0 : 0.0;
+  VG_PROBE_MARK(1);
+  // pivot order: rank of |D + u D| descending, index ascending on ties
+  // (uint64 order of the non-negative doubles: a total order, so even NaN
+  // input yields a permutation)
+  {
+    const int G = nt / n;
+    const int g = tid / n, i = tid % n;
+    if (g < G) {
+      const unsigned long long ki = (unsigned long long)__double_as_longlong(fabs(Dv[i] + u * Dv[i]));
+      const int j0 = g * n / G, j1 = (g + 1) * n / G;
+      int c = 0;
+      for (int j = j0; j < j1; j++) {
+        const unsigned long long kj = (unsigned long long)__double_as_longlong(fabs(Dv[j] + u * Dv[j]));
+        c += (kj > ki) || (kj == ki && j < i);
+      }
+      atomicAdd(&cnt[i], c);
+    }
   }
   __syncthreads();
-  for (int t = tid; t < n; t += nt) {
-    if (t < 15) J[t] = 0.0;
-    D[t] = A[lo(t, t)];
-    perm[t] = t;
+  for (int i = tid; i < n; i += nt) ip[cnt[i]] = i;
+  __syncthreads();
+  VG_PROBE_MARK(2);
+  // P A P^T into the tiles (diagonal tiles filled symmetric), padding = identity
+#pragma unroll 4
+  for (int e = tid; e < ntile * 256; e += nt) {
+    const int q = e >> 8, w = e & 255, r = w >> 4, c = w & 15;
+    const int R = tI[q] * 16 + r, C = tJ[q] * 16 + c;
+    double v;
+    if (R >= n || C >= n) {
+      v = (R == C) ? 1.0 : 0.0;
+    } else {
+      const int pr = ip[R], pc = ip[C];
+      if (pr == pc) v = Dv[pr] + u * Dv[pr];
+      else if (pr < 15 || pc < 15) v = 0.0;
+      else v = Hcalc[lo(pr, pc)];
+    }
+    T[q * 256 + tel(r, c)] = v;
   }
+  for (int t = tid; t < N; t += nt) xv[t] = t < n ? -Jv[ip[t]] : 0.0;
   __syncthreads();
-  for (int t = tid; t < n; t += nt) A[lo(t, t)] += u * D[t];
-  __syncthreads();
-  // LDL^T with diagonal pivoting (largest remaining |d|, first index on ties,
-  // as Eigen::LDLT / the oracle): the pivot is swapped physically (symmetric
-  // row+column swap in the packed lower triangle), so every step updates the
-  // contiguous trailing triangle with a 32 x 32 lane tiling.
-  const int tr_ = tid >> 5, tc_ = tid & 31;
-  for (int k = 0; k < n; k++) {
-    if (tid < 64) {
-      double best = -1.0;
-      int bi = n;
-      for (int i = k + tid; i < n; i += 64) {
-        double v = fabs(A[lo(i, i)]);
-        if (v > best) {
-          best = v;
-          bi = i;
+  VG_PROBE_MARK(3);
+
+  for (int K = 0; K < NB; K++) {
+    double* Tkk = &T[tix(K, K) * 256];
+    // (1) diagonal tile on wave 0: lane (r = lane/4, q = lane%4) holds
+    //     a(r, q + 4s); column j: L(r,j) = a(r,j) / d_j, then
+    //     a(r,m) -= L(r,j) * (d_j L(m,j)) for j < m <= r. The vector
+    //     d_j L(:,j) goes through LDS (tb), laid out so that lane q reads its
+    //     four entries m = q + 4s contiguously.
+    if (wave == 0) {
+      const int r = lane >> 2, q = lane & 3;
+      double a[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; s4++) a[s4] = Tkk[tel(r, q + 4 * s4)];
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int qj = j & 3, sj = j >> 2;
+        const double dj = bcast(a[sj], 4 * j + qj);
+        const double rdj = (dj != 0.0) ? 1.0 / dj : 1.0;  // Eigen leaves a zero pivot's column undivided
+        double l = __shfl(a[sj] * rdj, (lane & ~3) | qj, 64);
+        if (r > j && q == qj) a[sj] = l;
+        const double t = dj * l;
+        if (q == 0) {
+          tb[(r & 3) * 4 + (r >> 2)] = t;
+          if (r > j) tk[r * 16 + j] = t;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double tv[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++) tv[s4] = tb[q * 4 + s4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; s4++) {
+          const int m = q + 4 * s4;
+          if (m > j && m <= r) a[s4] -= l * tv[s4];
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < 4; s4++) {
+        const int c = q + 4 * s4;
+        if (c <= r) Tkk[tel(r, c)] = a[s4];
+        if (c == r) {
+          dK[r] = a[s4];
+          rdK[r] = (a[s4] != 0.0) ? 1.0 / a[s4] : 1.0;
         }
       }
-      for (int off = 32; off > 0; off >>= 1) {
-        double ob = __shfl_down(best, off, 64);
-        int oi = __shfl_down(bi, off, 64);
-        if (ob > best || (ob == best && oi < bi)) {
-          best = ob;
-          bi = oi;
-        }
+    }
+    __syncthreads();
+    VG_PROBE_MARK(4);
+    // (2) panel below the diagonal tile: one lane per row,
+    //     L(i,j) = (a(i,j) - sum_{m<j} L(i,m) tk(j,m)) / d_j;
+    //     meanwhile the last wave inverts the unit-lower diagonal tile into
+    //     its unused upper half (Linv(r,c), r > c, stored at (c,r)) for the
+    //     triangular solves
+    const int nrow = (NB - K - 1) * 16;
+    if (tid < nrow) {  // nrow <= 160 <= blockDim
+      const int I = K + 1 + (tid >> 4), r = tid & 15;
+      double* Tik = &T[tix(I, K) * 256];
+      double a[16];
+#pragma unroll
+      for (int c = 0; c < 16; c++) a[c] = Tik[tel(r, c)];
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        double v = a[j];
+#pragma unroll
+        for (int m = 0; m < j; m++) v -= a[m] * tk[j * 16 + m];
+        a[j] = v * rdK[j];
       }
-      if (tid == 0) piv = bi;
-    }
-    __syncthreads();
-    const int p = piv;
-    if (p != k) {
-      for (int j = tid; j < n; j += nt) {
-        if (j < k) {
-          double t = A[lo(k, j)]; A[lo(k, j)] = A[lo(p, j)]; A[lo(p, j)] = t;
-        } else if (j == k) {
-          double t = A[lo(k, k)]; A[lo(k, k)] = A[lo(p, p)]; A[lo(p, p)] = t;
-          int q = perm[k]; perm[k] = perm[p]; perm[p] = q;
-        } else if (j < p) {
-          double t = A[lo(j, k)]; A[lo(j, k)] = A[lo(p, j)]; A[lo(p, j)] = t;
-        } else if (j > p) {
-          double t = A[lo(j, k)]; A[lo(j, k)] = A[lo(j, p)]; A[lo(j, p)] = t;
-        }
+#pragma unroll
+      for (int c = 0; c < 16; c++) Tik[tel(r, c)] = a[c];
+    } else if (wave == nwave - 1 && lane < 16) {
+      const int c = lane;  // column c of Linv: x = e_c, x_i = -sum_{c<=k<i} L(i,k) x_k
+      double x[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        double v = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < i; k++) v -= Tkk[tel(i, k)] * x[k];
+        x[i] = (i < c) ? 0.0 : v;
       }
-      __syncthreads();
-    }
-    const double dk = A[lo(k, k)];
-    for (int i = k + 1 + tid; i < n; i += nt) col[i] = A[lo(i, k)];
-    __syncthreads();
-    for (int i = k + 1 + tr_; i < n; i += 32) {
-      const double lik = (dk != 0.0) ? col[i] / dk : 0.0;
-      const int base = i * (i + 1) / 2;
-      for (int j = k + 1 + tc_; j <= i; j += 32) A[base + j] -= lik * col[j];
-      if (tc_ == 0) A[base + k] = lik;
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+        if (i > c) Tkk[tel(c, i)] = x[i];
     }
     __syncthreads();
+    VG_PROBE_MARK(5);
+    // (3) trailing update on MFMA: tile (I,J) -= L(I,K) diag(d) L(J,K)^T
+    const int Rm = NB - K - 1;
+    const int ntr = Rm * (Rm + 1) / 2;
+    for (int q = wave; q < ntr; q += nwave) {
+      const int I = K + 1 + tI[q], J = K + 1 + tJ[q];
+      double* Tij = &T[tix(I, J) * 256];
+      const double* Aik = &T[tix(I, K) * 256];
+      const double* Ajk = &T[tix(J, K) * 256];
+      const int cc = lane & 15, rq = lane >> 4;
+      v4d acc;
+#pragma unroll
+      for (int g = 0; g < 4; g++) acc[g] = Tij[tel(rq + 4 * g, cc)];
+#pragma unroll
+      for (int ks = 0; ks < 4; ks++) {
+        const int kk = 4 * ks + rq;
+        const double av = -(Aik[tel(cc, kk)] * dK[kk]);
+        const double bv = Ajk[tel(cc, kk)];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; g++) Tij[tel(rq + 4 * g, cc)] = acc[g];
+    }
+    __syncthreads();
+    VG_PROBE_MARK(6);
   }
-  // triangular solves on one wave, y held in registers (lane owns rows lane + 64 r)
-  if (tid < 64) {
-    double yv[3];
-    for (int r = 0; r < 3; r++) {
-      int i = tid + 64 * r;
-      yv[r] = i < n ? -J[perm[i]] : 0.0;
-    }
-    for (int k = 0; k < n; k++) {  // L y = P(-J)
-      const double yk = __shfl(yv[k >> 6], k & 63, 64);
-      for (int r = 0; r < 3; r++) {
-        int i = tid + 64 * r;
-        if (i > k && i < n) yv[r] -= A[lo(i, k)] * yk;
+
+  // triangular solves on wave 0, lane (r = lane & 15, qd = lane >> 4): the
+  // off-diagonal tiles and the diagonal tiles' inverses as 4-way split
+  // matrix-vector products (no sequential substitution chains)
+  if (wave == 0) {
+    const int r = lane & 15, qd = lane >> 4;
+    for (int I = 0; I < NB; I++) {  // y_I = Linv_II (b_I - sum_{J<I} L_IJ y_J)
+      double s = 0.0;
+      for (int J = 0; J < I; J++) {
+        const double* Tt = &T[tix(I, J) * 256];
+#pragma unroll
+        for (int c = qd; c < 16; c += 4) s += Tt[tel(r, c)] * xv[16 * J + c];
       }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const double z = xv[16 * I + r] - s;
+      if (qd == 0) tb[r] = z;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const double* Td = &T[tix(I, I) * 256];
+      double s2 = 0.0;
+#pragma unroll
+      for (int c = qd; c < 16; c += 4)
+        if (c < r) s2 += Td[tel(c, r)] * tb[c];
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (qd == 0) xv[16 * I + r] = z + s2;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    for (int r = 0; r < 3; r++) {
-      int i = tid + 64 * r;
-      if (i < n) {
-        double d = A[lo(i, i)];
-        yv[r] = (d != 0.0) ? yv[r] / d : 0.0;
+    // D^+ (Eigen: |d| > DBL_MIN divides, else 0)
+    for (int t = lane; t < N; t += 64) {
+      const int I = t >> 4, rr = t & 15;
+      const double d = T[tix(I, I) * 256 + tel(rr, rr)];
+      xv[t] = (fabs(d) > 2.2250738585072014e-308) ? xv[t] / d : 0.0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int I = NB - 1; I >= 0; I--) {  // x_I = Linv_II^T (y_I - sum_{J>I} L_JI^T x_J)
+      double s = 0.0;
+      for (int J = I + 1; J < NB; J++) {
+        const double* Tt = &T[tix(J, I) * 256];
+#pragma unroll
+        for (int c = qd; c < 16; c += 4) s += Tt[tel(c, r)] * xv[16 * J + c];
       }
-    }
-    for (int k = n - 1; k >= 0; k--) {  // L^T x = y
-      const double yk = __shfl(yv[k >> 6], k & 63, 64);
-      for (int r = 0; r < 3; r++) {
-        int i = tid + 64 * r;
-        if (i < k) yv[r] -= A[lo(k, i)] * yk;
-      }
-    }
-    for (int r = 0; r < 3; r++) {
-      int i = tid + 64 * r;
-      if (i < n) y[i] = yv[r];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const double z = xv[16 * I + r] - s;
+      if (qd == 0) tb[r] = z;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const double* Td = &T[tix(I, I) * 256];
+      double s2 = 0.0;
+#pragma unroll
+      for (int c = qd; c < 16; c += 4)
+        if (c > r) s2 += Td[tel(r, c)] * tb[c];
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (qd == 0) xv[16 * I + r] = z + s2;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
   __syncthreads();
-  for (int t = tid; t < n; t += nt) col[perm[t]] = y[t];
+  VG_PROBE_MARK(7);
+  for (int t = tid; t < n; t += nt) col[ip[t]] = xv[t];
   __syncthreads();
   // trial states (optimizers.cpp:468-475) and IMU bias trial (477-478)
   if (tid < W) {
@@ -535,9 +752,13 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, double imu_c
   for (int t = tid; t < n; t += nt) dxi_out[t] = col[t];
   if (tid == 0) {
     double q1 = 0.0;
-    for (int r = 0; r < n; r++) q1 += col[r] * (u * D[r] * col[r] - J[r]);
+    for (int r = 0; r < n; r++) q1 += col[r] * (u * Dv[r] * col[r] - Jv[r]);
     st->q1 = 0.5 * q1;
   }
+  VG_PROBE_MARK(8);
+#ifdef VG_PROBE
+  if (tid == 0) atomicAdd(&g_probe[63], 1ull);
+#endif
 }
 
 // evaluate_only_residual (factors.cpp:128-158) at the trial poses
@@ -639,8 +860,6 @@ __global__ void __launch_bounds__(256) k_ba_init(BaState* st) {
 }
 
 struct BaDev {
-  double* comp;
-  double* compf;
   double* part;
   double* hl;
   double* imurec;
@@ -658,6 +877,16 @@ struct BaDev {
 };
 static BaDev g_dummy;
 
+static size_t hess_lds_bytes(int W) {
+  const size_t gemm = (size_t)hess_ks(W) * hess_xs(W), red = (size_t)kHessThreads * 28;
+  return (gemm > red ? gemm : red) * sizeof(double);
+}
+
+static size_t solve_lds_bytes(int W) {
+  const int NB = (15 * W + kTile - 1) / kTile;
+  return (size_t)NB * (NB + 1) / 2 * 256 * sizeof(double);
+}
+
 int ba_alloc(vg_ctx* ctx) {
   BaBufs& b = ctx->ba;
   const int W = ctx->cfg.win_size;
@@ -667,8 +896,7 @@ int ba_alloc(vg_ctx* ctx) {
   good &= (b.fac_node = ctx->arena.take<int>(b.cap_f)) != nullptr;
   good &= (b.fac_eig = ctx->arena.take<double>((size_t)b.cap_f * 12)) != nullptr;
   good &= (b.fac_pcr = ctx->arena.take<Clu>(b.cap_f)) != nullptr;
-  good &= (b.fac_comp = ctx->arena.take<double>((size_t)b.cap_f * (W * kComp + kCompF))) != nullptr;
-  good &= (b.hpart = ctx->arena.take<double>((size_t)(b.cap_f / kFC + 1) * nout)) != nullptr;
+  good &= (b.hpart = ctx->arena.take<double>((size_t)(b.cap_f / hess_chunk(W) + 1) * nout)) != nullptr;
   good &= (b.hout = ctx->arena.take<double>(nout + 16)) != nullptr;
   good &= (b.rpart = ctx->arena.take<double>(b.cap_f / 256 + 16)) != nullptr;
   good &= (b.xs = ctx->arena.take<double>(1024 + 2 * n * (n + 1) / 2 + 4 * n + 2 * kMaxW * kX + kMaxW * kImuRec +
@@ -677,11 +905,14 @@ int ba_alloc(vg_ctx* ctx) {
     ctx->err = "arena exhausted (BA)";
     return VG_E_CAPACITY;
   }
-  const int Wc = W > 12 ? 12 : W;
+  if (W > kMaxW || 15 * W > kMaxNB * kTile) {
+    ctx->err = "win_size > 11 unsupported by the BA solve (LDS-resident 15W x 15W tile store)";
+    return VG_E_ARG;
+  }
   VG_HIP(hipFuncSetAttribute((const void*)k_ba_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (15 * Wc) * (15 * Wc + 1) / 2 * (int)sizeof(double)));
-  VG_HIP(hipFuncSetAttribute((const void*)k_ba_hred, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             kFC * (W * kComp + kCompF) * (int)sizeof(double)));
+                             (int)solve_lds_bytes(W)));
+  VG_HIP(hipFuncSetAttribute((const void*)k_ba_hess, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)hess_lds_bytes(W)));
   return VG_OK;
 }
 
@@ -715,8 +946,6 @@ static BaDev carve(vg_ctx* ctx) {
   p += 8;
   d.mpring = (int*)p;
   p += 16;
-  d.comp = b.fac_comp;
-  d.compf = b.fac_comp + (size_t)b.cap_f * W * kComp;
   d.part = b.hpart;
   d.hl = b.hout;
   d.rpart = b.rpart;
@@ -728,8 +957,8 @@ static BaDev carve(vg_ctx* ctx) {
 int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double* imurec, double* bias_io,
            int* iters) {
   const int W = ctx->cfg.win_size;
-  if (W > 12) {
-    ctx->err = "win_size > 12 unsupported by the BA kernels (LDS-resident 15W x 15W solve)";
+  if (15 * W > kMaxNB * kTile) {
+    ctx->err = "win_size > 11 unsupported by the BA solve (LDS-resident 15W x 15W tile store)";
     return VG_E_ARG;
   }
   hipStream_t s = ctx->stream;
@@ -742,19 +971,20 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double*
   VG_HIP(hipMemcpyAsync(d.mpring, mp_ring, W * sizeof(int), hipMemcpyHostToDevice, s));
   VG_HIP(hipMemsetAsync(d.hl, 0, nout * sizeof(double), s));
   k_ba_init<<<1, 1, 0, s>>>(d.st);
-  const int nchunk = (nf + kFC - 1) / kFC;
+  const int nchunk = (nf + hess_chunk(W) - 1) / hess_chunk(W);
   const int nrb = (nf + 255) / 256;
-  const size_t hred_lds = (size_t)kFC * (W * kComp + kCompF) * sizeof(double);
-  const size_t solve_lds = (size_t)(15 * W) * (15 * W + 1) / 2 * sizeof(double);
-  for (int it = 0; it < 10; it++) {
+  const size_t hess_lds = hess_lds_bytes(W);
+  const size_t solve_lds = solve_lds_bytes(W);
+  // one LM iteration (optimizers.cpp:449-516); kernels early-exit on the
+  // device-side flags once converged
+  auto iteration = [&]() {
     if (nf > 0) {
-      k_ba_comp<<<grid_for((long)nf * W), kBlock, 0, s>>>(nf, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
-                                                         ctx->map.pcrs, d.mpring, d.xs, d.comp, d.compf, d.st);
-      k_ba_hred<<<nchunk, 256, hred_lds, s>>>(nf, W, d.comp, d.compf, d.part, d.st);
+      k_ba_hess<<<nchunk, kHessThreads, hess_lds, s>>>(nf, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
+                                                       ctx->map.pcrs, d.mpring, d.xs, d.part, d.st);
       k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nchunk, nout, d.part, d.hl, d.st);
     }
     if (nimu > 0) k_ba_imu<<<nimu, 256, 0, s>>>(nimu, d.imurec, d.bias, d.xs, d.imuout, d.st);
-    k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.xs, d.xt,
+    k_ba_solve<<<1, 256, solve_lds, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.xs, d.xt,
                                           d.bias, d.dxi, d.st);
     if (nf > 0)
       k_ba_resid<<<nrb, 256, 0, s>>>(nf, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
@@ -762,16 +992,32 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double*
     if (nimu > 0) k_ba_imures<<<1, 64, 0, s>>>(nimu, d.imurec, d.bias, d.xt, d.imures, d.st);
     k_ba_control<<<1, 256, 0, s>>>(W, nimu, nf > 0 ? nrb : 0, ctx->cfg.imu_coef, d.hl, nl + L, d.imuout, d.imures,
                                    d.rpart, d.xs, d.xt, d.bias, d.st);
+  };
+  // iterations are enqueued two at a time with a flag check in between: an
+  // early-exited iteration still costs ~7 launches, and the LM usually
+  // converges in 2-3 (optimizers.cpp:449, at most 10)
+  BaState* hflag = reinterpret_cast<BaState*>(ctx->h_pinned_d + 256);
+  int enq = 0;
+  while (enq < 10) {
+    for (int g = 0; g < 2 && enq < 10; g++, enq++) iteration();
+    if (enq >= 10) break;
+    VG_HIP(hipMemcpyAsync(hflag, d.st, sizeof(BaState), hipMemcpyDeviceToHost, s));
+    VG_HIP(stream_wait(ctx));
+    if (hflag->done) break;
   }
   VG_HIP(hipGetLastError());
   BaState hs;
   VG_HIP(hipMemcpyAsync(xs_io, d.xs, (size_t)W * kX * sizeof(double), hipMemcpyDeviceToHost, s));
   VG_HIP(hipMemcpyAsync(bias_io, d.bias, (size_t)nimu * 12 * sizeof(double), hipMemcpyDeviceToHost, s));
   VG_HIP(hipMemcpyAsync(&hs, d.st, sizeof(BaState), hipMemcpyDeviceToHost, s));
-  VG_HIP(hipStreamSynchronize(s));
+  VG_HIP(stream_wait(ctx));
   *iters = hs.iters;
   (void)g_dummy;
   return VG_OK;
 }
 
 }  // namespace vg
+
+#ifdef VG_PROBE
+VG_PROBE_READER(vg_probe_read)
+#endif

@@ -140,7 +140,7 @@ int ds_run(vg_ctx* ctx, const float* x, const float* y, const float* z, const fl
                                            d.oc);
   VG_HIP(hipGetLastError());
   VG_HIP(hipMemcpyAsync(ctx->h_pinned, d.flags, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
-  VG_HIP(hipStreamSynchronize(s));
+  VG_HIP(stream_wait(ctx));
   if (ctx->h_pinned[0]) {
     ctx->err = "voxel key out of packed range (|key| >= 2^20)";
     return VG_E_RANGE;

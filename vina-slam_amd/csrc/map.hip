@@ -19,6 +19,7 @@
 // sorting (leaf, order) keys and walking each leaf's segment sequentially, so
 // sums are deterministic and order-faithful.
 #include <hipcub/hipcub.hpp>
+#include <cstdio>
 #include "vg_dev.h"
 
 namespace vg {
@@ -74,6 +75,7 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(w.leaf = ctx->arena.take<int>(cw));
   good &= ok(w.pw = ctx->arena.take<double>(cw * 3));
   good &= ok(w.iekf_cache = ctx->arena.take<int>(cw));
+  good &= ok(w.rc = ctx->arena.take<int>(64));
   w.nparts = 1024;
   good &= ok(w.partials = ctx->arena.take<double>((size_t)w.nparts * 40));
   if (!good) {
@@ -282,7 +284,7 @@ int iekf_iter(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const f
   VG_HIP(hipGetLastError());
   VG_HIP(hipMemcpyAsync(ctx->h_pinned_d, w.partials + (size_t)w.nparts * 38, kIekfVals * sizeof(double),
                         hipMemcpyDeviceToHost, s));
-  VG_HIP(hipStreamSynchronize(s));
+  VG_HIP(stream_wait(ctx));
   prof_collect(ctx);
   for (int j = 0; j < kIekfVals; j++) out34[j] = ctx->h_pinned_d[j];
   return VG_OK;
@@ -432,31 +434,7 @@ __global__ void __launch_bounds__(256) k_child_count(int np, const int* __restri
 }
 
 __global__ void __launch_bounds__(256) k_child_alloc(int np, const int* __restrict__ parents, const uint32_t* __restrict__ off, DevMap m,
-                              int* __restrict__ next, int next_base) {
-  const int base = m.counters[kCntNodes];
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < np; q += gridDim.x * blockDim.x) {
-    int p = parents[q];
-    NodeHdr& ph = m.hdr[p];
-    int k = 0;
-    for (int o = 0; o < 8; o++) {
-      if (m.cfirst[(size_t)p * 8 + o] != -5) continue;
-      int id = base + (int)off[q] + k;
-      k++;
-      m.cfirst[(size_t)p * 8 + o] = 0x7f7f7f7f;
-      if (id >= m.cap_nodes) {
-        atomicOr(&m.counters[kCntErr], 4);
-        continue;
-      }
-      int xyz[3] = {(o >> 2) & 1, (o >> 1) & 1, o & 1};
-      double c[3];
-      for (int j = 0; j < 3; j++) c[j] = ph.center[j] + (float)((2 * xyz[j] - 1) * ph.qlen);
-      init_node(m.hdr[id], c, ph.qlen / 2, ph.layer + 1, p);
-      ph.child[o] = id;
-      if (next) next[next_base + (int)off[q] + k - 1] = id;
-    }
-    m.nscr[(size_t)p * 4 + 1] = -1;
-  }
-}
+                              int* __restrict__ next, int next_base);
 
 __global__ void __launch_bounds__(256) k_ins_resolve(int n, const double* __restrict__ pw, DevMap m, int* __restrict__ leaf) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -513,12 +491,13 @@ __global__ void __launch_bounds__(256) k_push_window(int n, const uint64_t* __re
 static int read_counters(vg_ctx* ctx) {
   VG_HIP(hipMemcpyAsync(ctx->h_pinned, ctx->map.counters, kCntN * sizeof(int), hipMemcpyDeviceToHost,
                         ctx->stream));
-  VG_HIP(hipStreamSynchronize(ctx->stream));
+  VG_HIP(stream_wait(ctx));
   if (ctx->h_pinned[kCntErr]) {
     int e = ctx->h_pinned[kCntErr];
     ctx->err = std::string("device map error flags=") + std::to_string(e) +
                ((e & 4) ? " (node pool full)" : "") + ((e & 8) ? " (point_fix arena full)" : "") +
-               ((e & 1) ? " (voxel key out of packed range)" : "") + ((e & 2) ? " (root hash full)" : "");
+               ((e & 1) ? " (voxel key out of packed range)" : "") + ((e & 2) ? " (root hash full)" : "") +
+               ((e & 16) ? " (subdivision event buffer full)" : "");
     return (e & 1) ? VG_E_RANGE : VG_E_CAPACITY;
   }
   return VG_OK;
@@ -542,19 +521,21 @@ static int bits_for(long v) {
   return b;
 }
 
-// sort an int list of n node ids in place (deterministic creation order)
-__global__ void __launch_bounds__(256) k_i2k(int n, const int* __restrict__ a, uint64_t* __restrict__ k) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) k[i] = (uint64_t)a[i];
+// sort an int list of n node ids in place (deterministic creation order);
+// scratch: the 32-bit buffers u0/u1 (k0/k1 may hold live events)
+__global__ void __launch_bounds__(256) k_i2u(int n, const int* __restrict__ a, uint32_t* __restrict__ k) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) k[i] = (uint32_t)a[i];
 }
-__global__ void __launch_bounds__(256) k_k2i(int n, const uint64_t* __restrict__ k, int* __restrict__ a) {
+__global__ void __launch_bounds__(256) k_u2i(int n, const uint32_t* __restrict__ k, int* __restrict__ a) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) a[i] = (int)k[i];
 }
 static int sort_ids(vg_ctx* ctx, int* a, int n) {
   if (n <= 1) return VG_OK;
   Work& w = ctx->wk;
-  k_i2k<<<grid_for(n), kBlock, 0, ctx->stream>>>(n, a, w.k0);
-  VG_TRY(sort_keys(ctx, w.k0, w.k1, n, 32));
-  k_k2i<<<grid_for(n), kBlock, 0, ctx->stream>>>(n, w.k1, a);
+  k_i2u<<<grid_for(n), kBlock, 0, ctx->stream>>>(n, a, w.u0);
+  size_t tb = w.tmp_bytes;
+  VG_HIP(hipcub::DeviceRadixSort::SortKeys(w.tmp, tb, w.u0, w.u1, n, 0, 32, ctx->stream));
+  k_u2i<<<grid_for(n), kBlock, 0, ctx->stream>>>(n, w.u1, a);
   return VG_OK;
 }
 
@@ -605,6 +586,9 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, const InsPose& pose, int n, 
   VG_TRY(read_counters(ctx));
   *roots_new = ctx->h_pinned[kCntNodes] - first_new;
   *touched = ctx->h_pinned[kCntTouched];
+#ifdef VG_PROBE
+  fprintf(stderr, "PROBE insert n=%d roots_new=%d touched=%d nodes=%d\n", n, *roots_new, *touched, ctx->h_pinned[kCntNodes]);
+#endif
   if (*touched < thread_num) return VG_OK;  // voxel_map.cpp:96-97: no allocation at all
   VG_HIP(hipMemsetAsync(m.counters + kCntCreate, 0, sizeof(int), s));
   k_ins_descend<<<g, kBlock, 0, s>>>(n, w.pw, m, w.leaf, w.list2);
@@ -622,56 +606,410 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, const InsPose& pose, int n, 
 }
 
 // ------------------------------------------------------------------ recut (A5/A6)
-// One level of OctoTree::recut (octree.cpp:335-393) over a worklist: internal
-// nodes forward their children, leaves run the plane test; failing leaves below
-// max_layer are marked for subdivision; planar leaves that pass tras_opt's
-// filter (octree.cpp:502-505) become factor candidates.
-__global__ void __launch_bounds__(256) k_recut_visit(int nw, const int* __restrict__ work, MP mp, DevMap m, int* __restrict__ next,
-                              int* __restrict__ sub, int* __restrict__ cand) {
+// Level-synchronous OctoTree::recut (octree.cpp:335-393) with every count kept
+// on the device: per level, k_rc_visit (worklist -> children / subdividing
+// leaves / factor candidates), k_rc_win (window points of subdividing leaves)
+// and k_rc_apply (one workgroup: deterministic child allocation, event sort in
+// LDS, pushes in the reference's order). The host enqueues max_layer+1 levels
+// and synchronizes once. A level whose subdivision exceeds the LDS capacity of
+// k_rc_apply sets rc[kRcAbort]; the host then replays the rest of the recut
+// with the host-sized path (recut_slow_apply), which only happens while the
+// map is first built.
+enum { kRcLvl = 0, kRcSub = 16, kRcWin = 32, kRcAbort = 48, kRcN = 64 };
+constexpr int kApplyThreads = 256;
+constexpr int kApplyEv = 4096;   // events sorted in LDS
+constexpr int kApplySub = kApplyThreads;  // subdividing leaves per level (one lane each)
+
+// visit one worklist entry; returns children / candidate / subdivide flags
+__device__ __forceinline__ void recut_visit_node(int node, const MP& mp, DevMap& m, int* kids, int& nchild,
+                                                 int& is_cand, int& is_sub) {
+  nchild = 0;
+  is_cand = 0;
+  is_sub = 0;
+  if (node < 0) return;
+  NodeHdr& h = m.hdr[node];
+  if (h.octo == 1) {
+    for (int o = 0; o < 8; o++)
+      if (h.child[o] >= 0) kids[nchild++] = h.child[o];
+    return;
+  }
+  h.opt_state = -1;
+  const Clu& a = m.pcr_add[node];
+  if (a.N <= mp.minpt[h.layer]) {
+    h.is_plane = 0;
+  } else if (h.isexist && h.has_sw) {
+    V3 ev;
+    M3 U;
+    eig3(clu_cov(a), ev, U);
+    double* e = &m.eig[(size_t)node * 12];
+    for (int j = 0; j < 3; j++) e[j] = ev[j];
+    for (int j = 0; j < 9; j++) e[3 + j] = U[j];
+    h.is_plane = (ev[0] < mp.min_eig && (ev[0] / ev[2]) < mp.thre[h.layer]) ? 1 : 0;
+    if (h.is_plane) {
+      is_cand = !(ev[0] / ev[1] > 0.12) ? 1 : 0;  // tras_opt filter, octree.cpp:502-505
+    } else if (h.layer < mp.max_layer) {
+      m.nscr[(size_t)node * 4 + 2] = 1;  // subdividing
+      is_sub = 1;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rc_visit(int L, int thread_num, const int* __restrict__ work_in, MP mp,
+                                                  DevMap m, int* __restrict__ next, int* __restrict__ sub,
+                                                  int* __restrict__ cand, int* __restrict__ rc) {
+  if (rc[kRcAbort]) return;
+  const int nw = (L == 0) ? m.counters[kCntSlide] : rc[kRcLvl + L - 1];
+  if (L == 0 && nw < thread_num) return;  // local_mapping.cpp:150-154
+  const int* work = (L == 0) ? m.slide : work_in;
   for (int base = blockIdx.x * blockDim.x; base < nw; base += gridDim.x * blockDim.x) {
     const int q = base + threadIdx.x;
-    int node = q < nw ? work[q] : -1;
-    int nchild = 0, is_cand = 0, is_sub = 0;
-    int kids[8];
-    if (node >= 0) {
-      NodeHdr& h = m.hdr[node];
-      if (h.octo == 1) {
-        for (int o = 0; o < 8; o++)
-          if (h.child[o] >= 0) kids[nchild++] = h.child[o];
-      } else {
-        h.opt_state = -1;
-        const Clu& a = m.pcr_add[node];
-        if (a.N <= mp.minpt[h.layer]) {
-          h.is_plane = 0;
-        } else if (h.isexist && h.has_sw) {
-          V3 ev;
-          M3 U;
-          eig3(clu_cov(a), ev, U);
-          double* e = &m.eig[(size_t)node * 12];
-          for (int j = 0; j < 3; j++) e[j] = ev[j];
-          for (int j = 0; j < 9; j++) e[3 + j] = U[j];
-          h.is_plane = (ev[0] < mp.min_eig && (ev[0] / ev[2]) < mp.thre[h.layer]) ? 1 : 0;
-          if (h.is_plane) {
-            is_cand = !(ev[0] / ev[1] > 0.12) ? 1 : 0;
-          } else if (h.layer < mp.max_layer) {
-            m.nscr[(size_t)node * 4 + 2] = 1;  // subdividing
-            is_sub = 1;
-          }
-        }
-      }
-    }
-    int o1 = wave_append(&m.counters[kCntNext], nchild);
+    int kids[8], nchild, is_cand, is_sub;
+    recut_visit_node(q < nw ? work[q] : -1, mp, m, kids, nchild, is_cand, is_sub);
+    const int node = q < nw ? work[q] : -1;
+    int o1 = wave_append(&rc[kRcLvl + L], nchild);
     int o2 = wave_append(&m.counters[kCntFactors], is_cand);
-    int o3 = wave_append(&m.counters[kCntSub], is_sub);
+    int o3 = wave_append(&rc[kRcSub + L], is_sub);
     for (int j = 0; j < nchild; j++) next[o1 + j] = kids[j];
     if (is_cand) cand[o2] = node;
     if (is_sub) sub[o3] = node;
   }
 }
 
-// subdivision events: point_fix entries (fix_divide, octree.cpp:257-277) and
-// window points of every frame (subdivide, octree.cpp:279-300)
-__global__ void __launch_bounds__(256) k_sub_fix_events(int ns, const int* __restrict__ sub, DevMap m, uint64_t* __restrict__ ev, int cap) {
+// window points of every frame that sit in a subdividing leaf (subdivide,
+// octree.cpp:279-300): event (leaf, octant, 1 + ord) with source index
+__device__ __forceinline__ bool win_event(int g, int cap_wp, const int* nper, const int* slot_of, const WinD* win,
+                                          DevMap& m, int& leaf, int& o, int& ord, int& i) {
+  ord = 0;
+  i = g;
+  while (ord < win->win_count && i >= nper[ord]) {
+    i -= nper[ord];
+    ord++;
+  }
+  if (ord >= win->win_count) return false;
+  const size_t b = (size_t)slot_of[ord] * cap_wp + i;
+  const int l = m.wp_leaf[b];
+  if (l < 0 || m.nscr[(size_t)l * 4 + 2] != 1) return false;
+  leaf = l;
+  const NodeHdr& h = m.hdr[leaf];
+  V3 pw = rigid(ld_m3(win->R[ord]), ld_v3(&m.wp_pnt[b * 3]), ld_v3(win->p[ord]));
+  o = octant(pw, h.center);
+  m.cfirst[(size_t)leaf * 8 + o] = -5;
+  return true;
+}
+
+__global__ void __launch_bounds__(256) k_rc_win(int L, int total, int cap_wp, const int* __restrict__ nper,
+                                                const int* __restrict__ slot_of, const WinD* __restrict__ win,
+                                                DevMap m, uint64_t* __restrict__ ev, uint32_t* __restrict__ evsrc,
+                                                int cap, int* __restrict__ rc) {
+  if (rc[kRcAbort] || rc[kRcSub + L] == 0) return;
+  for (int base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
+    const int g = base + threadIdx.x;
+    int leaf = -1, o = 0, ord = 0, i = 0;
+    const bool hit = g < total && win_event(g, cap_wp, nper, slot_of, win, m, leaf, o, ord, i);
+    const int pos = wave_append(&rc[kRcWin + L], hit ? 1 : 0);
+    if (hit) {
+      if (pos < cap) {
+        ev[pos] = ((uint64_t)leaf << 27) | ((uint64_t)o << 24) | (uint64_t)(1 + ord);
+        evsrc[pos] = (uint32_t)i;
+      } else {
+        atomicOr(&m.counters[kCntErr], 16);
+      }
+    }
+  }
+}
+
+// zero a freshly allocated node's records (the pool is zeroed lazily)
+__device__ __forceinline__ void zero_node(DevMap& m, int id) {
+  PlaneRec& p = m.pl[id];
+  for (int j = 0; j < 27; j++) (&p.center[0])[j] = 0.0;
+  p.radius = 0;
+  p.pad = 0;
+  clu_zero(m.pcr_add[id]);
+  clu_zero(m.pcr_fix[id]);
+  for (int j = 0; j < kCovN; j++) m.cov_add[(size_t)id * kCovN + j] = 0.0;
+  for (int j = 0; j < 12; j++) m.eig[(size_t)id * 12 + j] = 0.0;
+  m.jour[id] = 0.0;
+  for (int j = 0; j < m.W; j++) clu_zero(m.pcrs[(size_t)id * m.W + j]);
+}
+
+// children of parent p in octant order, ids id0, id0+1, ...; appended to next
+__device__ __forceinline__ void alloc_parent(DevMap& m, int p, int id0, int* next, int next_pos, bool zero) {
+  NodeHdr& ph = m.hdr[p];
+  int k = 0;
+  for (int o = 0; o < 8; o++) {
+    if (m.cfirst[(size_t)p * 8 + o] != -5) continue;
+    const int id = id0 + k;
+    k++;
+    m.cfirst[(size_t)p * 8 + o] = 0x7f7f7f7f;
+    if (id >= m.cap_nodes) {
+      atomicOr(&m.counters[kCntErr], 4);
+      continue;
+    }
+    int xyz[3] = {(o >> 2) & 1, (o >> 1) & 1, o & 1};
+    double c[3];
+    for (int j = 0; j < 3; j++) c[j] = ph.center[j] + (float)((2 * xyz[j] - 1) * ph.qlen);
+    init_node(m.hdr[id], c, ph.qlen / 2, ph.layer + 1, p);
+    if (zero) zero_node(m, id);
+    ph.child[o] = id;
+    if (next) next[next_pos + k - 1] = id;
+  }
+  m.nscr[(size_t)p * 4 + 1] = -1;
+}
+
+__global__ void __launch_bounds__(256) k_child_alloc(int np, const int* __restrict__ parents, const uint32_t* __restrict__ off, DevMap m,
+                              int* __restrict__ next, int next_base) {
+  const int base = m.counters[kCntNodes];
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < np; q += gridDim.x * blockDim.x)
+    alloc_parent(m, parents[q], base + (int)off[q], next, next_base + (int)off[q], false);
+}
+
+// apply the sorted pushes of one child (keys[j, jend)), in the reference's
+// order: fix points first (push_fix, octree.cpp:179-188), then window points
+// frame by frame (push, octree.cpp:151-177)
+__device__ void push_child(const uint64_t* keys, int j, int jend, const MP& mp, const WinD* win, DevMap& m) {
+  const int child = (int)(keys[j] >> 27);
+  NodeHdr& h = m.hdr[child];
+  const NodeHdr& ph = m.hdr[h.parent];
+  const bool listed = h.layer < mp.max_layer;
+  int nfix = 0;
+  for (int jj = j; jj < jend; jj++)
+    if (((keys[jj] >> 21) & 63) == 0) nfix++;
+  if (nfix > 0 && listed) {
+    int off = atomicAdd(&m.counters[kCntFix], nfix);
+    if (off + nfix > m.cap_fix) {
+      atomicOr(&m.counters[kCntErr], 8);
+      return;
+    }
+    h.fix_off = off;
+    h.fix_cap = nfix;
+    h.fix_cnt = 0;
+  }
+  Clu add_ = m.pcr_add[child];
+  Clu fix_ = m.pcr_fix[child];
+  double cov[kCovN];
+  for (int t = 0; t < kCovN; t++) cov[t] = m.cov_add[(size_t)child * kCovN + t];
+  int cur_slot = -1;
+  Clu loc;
+  clu_zero(loc);
+  for (int jj = j; jj < jend; jj++) {
+    const uint64_t k = keys[jj];
+    const int phase = (int)((k >> 21) & 63);
+    const int idx = (int)(k & ((1u << 21) - 1));
+    if (phase == 0) {
+      const size_t f = (size_t)ph.fix_off + idx;
+      V3 pt = ld_v3(&m.fix_pnt[f * 3]);
+      M3 var = ld_m3(&m.fix_var[f * 9]);
+      if (listed) {
+        const size_t d = (size_t)h.fix_off + h.fix_cnt;
+        for (int t = 0; t < 3; t++) m.fix_pnt[d * 3 + t] = pt[t];
+        for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = var[t];
+        h.fix_cnt++;
+      }
+      clu_push(fix_, pt);
+      clu_push(add_, pt);
+      bf_var_acc(cov, var, pt);
+    } else {
+      const int ord = phase - 1;
+      const int slot = win->mp[ord];
+      if (slot != cur_slot) {
+        if (cur_slot >= 0) m.pcrs[(size_t)child * mp.W + cur_slot] = loc;
+        cur_slot = slot;
+        loc = m.pcrs[(size_t)child * mp.W + slot];
+      }
+      const size_t b = (size_t)slot * m.cap_wp + idx;
+      V3 pnt = ld_v3(&m.wp_pnt[b * 3]);
+      M3 var = ld_m3(&m.wp_var[b * 9]);
+      V3 pw = rigid(ld_m3(win->R[ord]), pnt, ld_v3(win->p[ord]));
+      h.has_sw = 1;
+      h.isexist = 1;
+      m.wp_leaf[b] = listed ? child : -1;
+      clu_push(loc, pnt);
+      clu_push(add_, pw);
+      bf_var_acc(cov, var, pw);
+    }
+  }
+  if (cur_slot >= 0) m.pcrs[(size_t)child * mp.W + cur_slot] = loc;
+  m.pcr_add[child] = add_;
+  m.pcr_fix[child] = fix_;
+  for (int t = 0; t < kCovN; t++) m.cov_add[(size_t)child * kCovN + t] = cov[t];
+}
+
+// finish a subdivided parent: release its SlideWindow, free point_fix,
+// octo_state = 1 (octree.cpp:375-387)
+__device__ __forceinline__ void sub_finish(DevMap& m, int p) {
+  NodeHdr& h = m.hdr[p];
+  h.has_sw = 0;
+  for (int j = 0; j < m.W; j++) clu_zero(m.pcrs[(size_t)p * m.W + j]);
+  h.fix_cnt = 0;
+  h.fix_cap = 0;
+  h.octo = 1;
+  m.nscr[(size_t)p * 4 + 2] = -1;
+}
+
+// exclusive prefix over one value per thread of a 1024-lane workgroup
+__device__ __forceinline__ int block_excl_scan(int v, int* s_wsum, int* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_wsum[wv] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); k++) {
+      int t = s_wsum[k];
+      s_wsum[k] = acc;
+      acc += t;
+    }
+    s_wsum[16] = acc;
+  }
+  __syncthreads();
+  const int r = s_wsum[wv] + x - v;
+  *total = s_wsum[16];
+  __syncthreads();
+  return r;
+}
+
+// ascending bitonic sort of n (power of two) keys in LDS by the whole workgroup
+template <typename T>
+__device__ void lds_bitonic(T* a, int n) {
+  for (int k = 2; k <= n; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int pj = i ^ j;
+        if (pj > i) {
+          const T x = a[i], y = a[pj];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            a[i] = y;
+            a[pj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int ev_cap, MP mp, const WinD* __restrict__ win,
+                                                            DevMap m, int* __restrict__ next, const int* __restrict__ sub,
+                                                            const uint64_t* __restrict__ wev,
+                                                            const uint32_t* __restrict__ wsrc, int* __restrict__ rc) {
+  __shared__ uint64_t s_ev[kApplyEv];
+  __shared__ int s_sub[kApplySub], s_foff[kApplySub], s_coff[kApplySub];
+  __shared__ int s_wsum[32];
+  __shared__ int s_meta[4];
+  const int tid = threadIdx.x;
+  if (rc[kRcAbort]) return;
+  const int nsub = rc[kRcSub + L];
+  if (nsub == 0) return;
+  VG_PROBE_BEGIN();
+  const int nwin = rc[kRcWin + L];
+  if (nsub > kApplySub) {
+    if (tid == 0) rc[kRcAbort] = L + 1;
+    return;
+  }
+  // sorted subdividing leaves (ascending id: deterministic child ids)
+  int myp = tid < nsub ? sub[tid] : 0x7fffffff;
+  {
+    int rank = 0;
+    if (tid < nsub)
+      for (int q = 0; q < nsub; q++) rank += sub[q] < myp ? 1 : 0;
+    if (tid < nsub) s_sub[rank] = myp;
+  }
+  __syncthreads();
+  const int p_t = tid < nsub ? s_sub[tid] : -1;
+  int nfix;
+  const int foff = block_excl_scan(p_t >= 0 ? m.hdr[p_t].fix_cnt : 0, s_wsum, &nfix);
+  if (tid < nsub) s_foff[tid] = foff;
+  if (nfix + nwin > ev_cap) {
+    if (tid == 0) rc[kRcAbort] = L + 1;  // uniform: every lane saw the same totals
+    return;
+  }
+  __syncthreads();
+  // fix events (fix_divide, octree.cpp:257-277): (parent, octant, j) at foff + j
+  for (int e = tid; e < nfix; e += blockDim.x) {
+    int lo = 0, hi = nsub - 1;  // last q with s_foff[q] <= e
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_foff[mid] <= e) lo = mid;
+      else hi = mid - 1;
+    }
+    const int p = s_sub[lo], j = e - s_foff[lo];
+    const NodeHdr& h = m.hdr[p];
+    V3 pt = ld_v3(&m.fix_pnt[((size_t)h.fix_off + j) * 3]);
+    const int o = octant(pt, h.center);
+    m.cfirst[(size_t)p * 8 + o] = -5;
+    s_ev[e] = ((uint64_t)p << 27) | ((uint64_t)o << 24) | (uint64_t)j;
+  }
+  for (int e = tid; e < nwin; e += blockDim.x) s_ev[nfix + e] = wev[e];
+  __syncthreads();
+  VG_PROBE_MARK(16);
+  // children: per parent the marked octants, ids base + prefix (k_child_count/alloc)
+  int cc = 0;
+  if (p_t >= 0)
+    for (int o = 0; o < 8; o++) cc += (m.cfirst[(size_t)p_t * 8 + o] == -5) ? 1 : 0;
+  int ntot;
+  const int coff = block_excl_scan(cc, s_wsum, &ntot);
+  if (tid < nsub) s_coff[tid] = coff;
+  const int base = m.counters[kCntNodes];
+  const int nnext = rc[kRcLvl + L];
+  __syncthreads();
+  if (p_t >= 0) alloc_parent(m, p_t, base + coff, next, nnext + coff, true);
+  __syncthreads();
+  if (tid == 0) {
+    m.counters[kCntNodes] = base + ntot;
+    rc[kRcLvl + L] = nnext + ntot;
+  }
+  VG_PROBE_MARK(17);
+  // sort keys (child << 27 | phase << 21 | idx)
+  const int ne = nfix + nwin;
+  int npad = 2;
+  while (npad < ne) npad <<= 1;
+  for (int e = tid; e < npad; e += blockDim.x) {
+    if (e >= ne) {
+      s_ev[e] = ~0ull;
+      continue;
+    }
+    const uint64_t v = s_ev[e];
+    const int p = (int)(v >> 27), o = (int)((v >> 24) & 7), lo = (int)(v & 0xffffff);
+    const int child = m.hdr[p].child[o];
+    uint64_t phase, idx;
+    if (e < nfix) {
+      phase = 0;
+      idx = (uint64_t)lo;
+    } else {
+      phase = (uint64_t)lo;  // 1 + ord
+      idx = wsrc[e - nfix];
+    }
+    s_ev[e] = ((uint64_t)child << 27) | (phase << 21) | idx;
+  }
+  __syncthreads();
+  VG_PROBE_MARK(18);
+  lds_bitonic(s_ev, npad);
+  VG_PROBE_MARK(19);
+  for (int e = tid; e < ne; e += blockDim.x) {
+    const int child = (int)(s_ev[e] >> 27);
+    if (e > 0 && (int)(s_ev[e - 1] >> 27) == child) continue;
+    int jend = e + 1;
+    while (jend < ne && (int)(s_ev[jend] >> 27) == child) jend++;
+    push_child(s_ev, e, jend, mp, win, m);
+  }
+  __syncthreads();
+  VG_PROBE_MARK(20);
+  if (p_t >= 0) sub_finish(m, p_t);
+  VG_PROBE_MARK(21);
+#ifdef VG_PROBE
+  if (tid == 0) atomicAdd(&g_probe[62], 1ull);
+#endif
+  (void)s_meta;
+}
+
+// ---- host-sized path (overflow replay) ----------------------------------
+__global__ void __launch_bounds__(256) k_sub_fix_events(int ns, const int* __restrict__ sub, DevMap m,
+                                                        uint64_t* __restrict__ ev, int cap) {
   for (int base = blockIdx.x * blockDim.x; base < ns; base += gridDim.x * blockDim.x) {
     const int q = base + threadIdx.x;
     const int p = q < ns ? sub[q] : -1;
@@ -684,46 +1022,15 @@ __global__ void __launch_bounds__(256) k_sub_fix_events(int ns, const int* __res
       V3 pt = ld_v3(&m.fix_pnt[f * 3]);
       int o = octant(pt, h.center);
       m.cfirst[(size_t)p * 8 + o] = -5;
-      // parent, octant, phase 0 (fix), index
       if (pos < cap) ev[pos] = ((uint64_t)p << 27) | ((uint64_t)o << 24) | (uint64_t)j;
     }
   }
 }
 
-__global__ void __launch_bounds__(256) k_sub_win_events(int total, int cap_wp, const int* __restrict__ nper, const int* __restrict__ slot_of,
-                                 WinD* __restrict__ win, DevMap m, uint64_t* __restrict__ ev,
-                                 uint32_t* __restrict__ evsrc, int cap) {
-  for (int base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
-    const int g = base + threadIdx.x;
-    int ord = 0, i = g, leaf = -1, o = 0;
-    if (g < total) {
-      while (ord < win->win_count && i >= nper[ord]) {
-        i -= nper[ord];
-        ord++;
-      }
-      if (ord < win->win_count) {
-        size_t b = (size_t)slot_of[ord] * cap_wp + i;
-        int l = m.wp_leaf[b];
-        if (l >= 0 && m.nscr[(size_t)l * 4 + 2] == 1) {
-          leaf = l;
-          const NodeHdr& h = m.hdr[leaf];
-          V3 pw = rigid(ld_m3(win->R[ord]), ld_v3(&m.wp_pnt[b * 3]), ld_v3(win->p[ord]));
-          o = octant(pw, h.center);
-          m.cfirst[(size_t)leaf * 8 + o] = -5;
-        }
-      }
-    }
-    int pos = wave_append(&m.counters[kCntEvents], leaf >= 0 ? 1 : 0);
-    if (leaf >= 0 && pos < cap) {
-      ev[pos] = ((uint64_t)leaf << 27) | ((uint64_t)o << 24) | (uint64_t)(1 + ord);
-      evsrc[pos] = (uint32_t)i;
-    }
-  }
-}
-
-// rewrite events as (child << 27 | phase << 21 | idx) sort keys
-__global__ void __launch_bounds__(256) k_sub_keys(int ne, const uint64_t* __restrict__ ev, const uint32_t* __restrict__ evsrc,
-                           DevMap m, uint64_t* __restrict__ keys, int nfix) {
+// events at [0, fix_begin) come from the window, [fix_begin, ne) from point_fix
+__global__ void __launch_bounds__(256) k_sub_keys(int ne, const uint64_t* __restrict__ ev,
+                                                  const uint32_t* __restrict__ evsrc, DevMap m,
+                                                  uint64_t* __restrict__ keys, int fix_begin) {
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x) {
     uint64_t v = ev[e];
     int p = (int)(v >> 27);
@@ -731,7 +1038,7 @@ __global__ void __launch_bounds__(256) k_sub_keys(int ne, const uint64_t* __rest
     int lo = (int)(v & 0xffffff);
     int child = m.hdr[p].child[o];
     uint64_t phase, idx;
-    if (e < nfix) {
+    if (e >= fix_begin) {
       phase = 0;
       idx = (uint64_t)lo;
     } else {
@@ -742,97 +1049,19 @@ __global__ void __launch_bounds__(256) k_sub_keys(int ne, const uint64_t* __rest
   }
 }
 
-// apply the sorted subdivision pushes to each child, in the reference's order:
-// fix points first (push_fix, octree.cpp:179-188), then window points frame by
-// frame (push, octree.cpp:151-177)
-__global__ void __launch_bounds__(256) k_push_events(int ne, const uint64_t* __restrict__ keys, MP mp, WinD* __restrict__ win, DevMap m) {
+__global__ void __launch_bounds__(256) k_push_events(int ne, const uint64_t* __restrict__ keys, MP mp,
+                                                     WinD* __restrict__ win, DevMap m) {
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < ne; j += gridDim.x * blockDim.x) {
     int child = (int)(keys[j] >> 27);
     if (j > 0 && (int)(keys[j - 1] >> 27) == child) continue;
-    NodeHdr& h = m.hdr[child];
-    const int parent = h.parent;
-    const NodeHdr& ph = m.hdr[parent];
-    const bool listed = h.layer < mp.max_layer;
-    int jend = j;
-    int nfix = 0;
-    while (jend < ne && (int)(keys[jend] >> 27) == child) {
-      if (((keys[jend] >> 21) & 63) == 0) nfix++;
-      jend++;
-    }
-    if (nfix > 0 && listed) {
-      int off = atomicAdd(&m.counters[kCntFix], nfix);
-      if (off + nfix > m.cap_fix) {
-        atomicOr(&m.counters[kCntErr], 8);
-        continue;
-      }
-      h.fix_off = off;
-      h.fix_cap = nfix;
-      h.fix_cnt = 0;
-    }
-    Clu add_ = m.pcr_add[child];
-    Clu fix_ = m.pcr_fix[child];
-    double cov[kCovN];
-    for (int t = 0; t < kCovN; t++) cov[t] = m.cov_add[(size_t)child * kCovN + t];
-    int cur_slot = -1;
-    Clu loc;
-    clu_zero(loc);
-    for (int jj = j; jj < jend; jj++) {
-      uint64_t k = keys[jj];
-      int phase = (int)((k >> 21) & 63);
-      int idx = (int)(k & ((1u << 21) - 1));
-      if (phase == 0) {
-        size_t f = (size_t)ph.fix_off + idx;
-        V3 pt = ld_v3(&m.fix_pnt[f * 3]);
-        M3 var = ld_m3(&m.fix_var[f * 9]);
-        if (listed) {
-          size_t d = (size_t)h.fix_off + h.fix_cnt;
-          for (int t = 0; t < 3; t++) m.fix_pnt[d * 3 + t] = pt[t];
-          for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = var[t];
-          h.fix_cnt++;
-        }
-        clu_push(fix_, pt);
-        clu_push(add_, pt);
-        bf_var_acc(cov, var, pt);
-      } else {
-        int ord = phase - 1;
-        int slot = win->mp[ord];
-        if (slot != cur_slot) {
-          if (cur_slot >= 0) m.pcrs[(size_t)child * mp.W + cur_slot] = loc;
-          cur_slot = slot;
-          loc = m.pcrs[(size_t)child * mp.W + slot];
-        }
-        size_t b = (size_t)slot * m.cap_wp + idx;
-        V3 pnt = ld_v3(&m.wp_pnt[b * 3]);
-        M3 var = ld_m3(&m.wp_var[b * 9]);
-        V3 pw = rigid(ld_m3(win->R[ord]), pnt, ld_v3(win->p[ord]));
-        h.has_sw = 1;
-        h.isexist = 1;
-        m.wp_leaf[b] = listed ? child : -1;
-        clu_push(loc, pnt);
-        clu_push(add_, pw);
-        bf_var_acc(cov, var, pw);
-      }
-    }
-    if (cur_slot >= 0) m.pcrs[(size_t)child * mp.W + cur_slot] = loc;
-    m.pcr_add[child] = add_;
-    m.pcr_fix[child] = fix_;
-    for (int t = 0; t < kCovN; t++) m.cov_add[(size_t)child * kCovN + t] = cov[t];
+    int jend = j + 1;
+    while (jend < ne && (int)(keys[jend] >> 27) == child) jend++;
+    push_child(keys, j, jend, mp, win, m);
   }
 }
 
-// finish a subdivided parent: release its SlideWindow, free point_fix,
-// octo_state = 1 (octree.cpp:375-387)
 __global__ void __launch_bounds__(256) k_sub_finish(int ns, const int* __restrict__ sub, DevMap m) {
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ns; q += gridDim.x * blockDim.x) {
-    int p = sub[q];
-    NodeHdr& h = m.hdr[p];
-    h.has_sw = 0;
-    for (int j = 0; j < m.W; j++) clu_zero(m.pcrs[(size_t)p * m.W + j]);
-    h.fix_cnt = 0;
-    h.fix_cap = 0;
-    h.octo = 1;
-    m.nscr[(size_t)p * 4 + 2] = -1;
-  }
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ns; q += gridDim.x * blockDim.x) sub_finish(m, sub[q]);
 }
 
 // tras_opt: factor list in node-id order; opt_state = factor index
@@ -847,16 +1076,48 @@ __global__ void __launch_bounds__(256) k_factor_finish(int nf, const int* __rest
   }
 }
 
-// multi_recut (local_mapping.cpp:144-201): level-synchronous recursion over
-// surf_map_slide, then tras_opt. Returns the factor count.
+static int read_rc(vg_ctx* ctx, int* h) {
+  VG_HIP(hipMemcpyAsync(h, ctx->wk.rc, kRcN * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  return read_counters(ctx);  // synchronizes
+}
+
+// host-sized apply of level L (visit and window events already ran)
+static int recut_slow_apply(vg_ctx* ctx, int L, const MP& mp, WinD* dwin, int* next, int* hrc) {
+  DevMap& m = ctx->map;
+  Work& w = ctx->wk;
+  hipStream_t s = ctx->stream;
+  const int nsub = hrc[kRcSub + L], nwin = hrc[kRcWin + L], nnext = hrc[kRcLvl + L];
+  if (nsub <= 0) return VG_OK;
+  if (nwin > w.cap) {
+    ctx->err = "subdivision event buffer overflow";
+    return VG_E_CAPACITY;
+  }
+  VG_TRY(sort_ids(ctx, w.list2, nsub));
+  VG_HIP(hipMemsetD32Async((hipDeviceptr_t)(m.counters + kCntEvents), nwin, 1, s));
+  k_sub_fix_events<<<grid_for(nsub), kBlock, 0, s>>>(nsub, w.list2, m, w.k0, w.cap);
+  VG_TRY(read_counters(ctx));
+  const int ne = ctx->h_pinned[kCntEvents];
+  if (ne > w.cap) {
+    ctx->err = "subdivision event buffer overflow";
+    return VG_E_CAPACITY;
+  }
+  int created = 0;
+  VG_TRY(alloc_children(ctx, w.list2, nsub, next, nnext, true, &created));
+  VG_HIP(hipMemsetD32Async((hipDeviceptr_t)(w.rc + kRcLvl + L), nnext + created, 1, s));
+  k_sub_keys<<<grid_for(ne), kBlock, 0, s>>>(ne, w.k0, w.evsrc, m, w.k1, nwin);
+  VG_TRY(sort_keys(ctx, w.k1, w.k0, ne, 27 + bits_for(ctx->h_pinned[kCntNodes])));
+  k_push_events<<<grid_for(ne), kBlock, 0, s>>>(ne, w.k0, mp, dwin, m);
+  k_sub_finish<<<grid_for(nsub), kBlock, 0, s>>>(nsub, w.list2, m);
+  VG_HIP(hipGetLastError());
+  return read_counters(ctx);
+}
+
+// multi_recut (local_mapping.cpp:144-201) then tras_opt. Returns the factor count.
 int map_recut(vg_ctx* ctx, const MP& mp, const WinD& win, const int* nper, int thread_num, int* n_factors) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
   *n_factors = 0;
-  VG_TRY(read_counters(ctx));
-  int nslide = ctx->h_pinned[kCntSlide];
-  if (nslide < thread_num) return VG_OK;  // local_mapping.cpp:150-154
   // upload the window (poses, ring) and per-ord point counts
   WinD* dwin = (WinD*)ctx->ba.xs;
   int* dn = (int*)((char*)ctx->ba.xs + sizeof(WinD));
@@ -870,63 +1131,49 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinD& win, const int* nper, int t
   VG_HIP(hipMemcpyAsync(dn, hn, sizeof(hn), hipMemcpyHostToDevice, s));
   int total = 0;
   for (int i = 0; i < win.win_count; i++) total += nper[i];
-  VG_HIP(hipMemcpyAsync(w.list0, m.slide, (size_t)nslide * sizeof(int), hipMemcpyDeviceToDevice, s));
-  int nwork = nslide;
-  int* work = w.list0;
-  int* next = w.list1;
-  int* cand = w.cand;
-  int* subl = w.list2;
+  VG_HIP(hipMemsetAsync(w.rc, 0, kRcN * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.counters + kCntFactors, 0, sizeof(int), s));
-  for (int level = 0; level <= 8 && nwork > 0; level++) {
-    VG_HIP(hipMemsetAsync(m.counters + kCntNext, 0, 3 * sizeof(int), s));  // Next, Sub, Events
-    VG_HIP(hipMemsetAsync(m.counters + kCntSub, 0, 2 * sizeof(int), s));
-    k_recut_visit<<<grid_for(nwork), kBlock, 0, s>>>(nwork, work, mp, m, next, subl, cand);
-    VG_HIP(hipGetLastError());
-    VG_TRY(read_counters(ctx));
-    int nnext = ctx->h_pinned[kCntNext], nsub = ctx->h_pinned[kCntSub];
-    if (nsub > 0) {
-      VG_TRY(sort_ids(ctx, subl, nsub));
-      k_sub_fix_events<<<grid_for(nsub), kBlock, 0, s>>>(nsub, subl, m, w.k0, w.cap);
-      VG_TRY(read_counters(ctx));
-      int nfix = ctx->h_pinned[kCntEvents];
-      if (nfix > w.cap) {
-        ctx->err = "subdivision event buffer overflow";
-        return VG_E_CAPACITY;
-      }
-      if (total > 0)
-        k_sub_win_events<<<grid_for(total), kBlock, 0, s>>>(total, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc,
-                                                            w.cap);
-      VG_TRY(read_counters(ctx));
-      int ne = ctx->h_pinned[kCntEvents];
-      if (ne > w.cap) {
-        ctx->err = "subdivision event buffer overflow";
-        return VG_E_CAPACITY;
-      }
-      // fix events sit at [0, nfix); their evsrc is unused
-      int created = 0;
-      VG_TRY(alloc_children(ctx, subl, nsub, next, nnext, true, &created));
-      nnext += created;
-      k_sub_keys<<<grid_for(ne), kBlock, 0, s>>>(ne, w.k0, w.evsrc, m, w.k1, nfix);
-      VG_TRY(sort_keys(ctx, w.k1, w.k0, ne, 27 + bits_for(ctx->h_pinned[kCntNodes])));
-      k_push_events<<<grid_for(ne), kBlock, 0, s>>>(ne, w.k0, mp, dwin, m);
-      k_sub_finish<<<grid_for(nsub), kBlock, 0, s>>>(nsub, subl, m);
-      VG_HIP(hipGetLastError());
-      VG_TRY(read_counters(ctx));
-    }
-    int* t = work;
-    work = next;
-    next = t;
-    nwork = nnext;
+  const int nlev = mp.max_layer + 1;  // children sit one layer down; leaves at max_layer do not subdivide
+  auto list_of = [&](int L) { return (L % 2 == 1) ? w.list0 : w.list1; };  // worklist of level L >= 1
+  const int gv = 256, gw = grid_for(total > 0 ? total : 1);
+  const int ev_cap = (ctx->dbg_apply_cap >= 0 && ctx->dbg_apply_cap < kApplyEv) ? ctx->dbg_apply_cap : kApplyEv;
+  auto enqueue_level = [&](int L) {
+    k_rc_visit<<<gv, kBlock, 0, s>>>(L, thread_num, L > 0 ? list_of(L) : nullptr, mp, m, list_of(L + 1), w.list2,
+                                     w.cand, w.rc);
+    if (total > 0)
+      k_rc_win<<<gw, kBlock, 0, s>>>(L, total, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc, w.cap, w.rc);
+  };
+  for (int L = 0; L < nlev; L++) {
+    enqueue_level(L);
+    k_rc_apply<<<1, kApplyThreads, 0, s>>>(L, ev_cap, mp, dwin, m, list_of(L + 1), w.list2, w.k0, w.evsrc, w.rc);
   }
-  VG_TRY(read_counters(ctx));
-  int nf = ctx->h_pinned[kCntFactors];
+  VG_HIP(hipGetLastError());
+  int* hrc = ctx->h_pinned + 64;
+  VG_TRY(read_rc(ctx, hrc));
+  if (hrc[kRcAbort]) {  // replay from the level that overflowed on the host-sized path
+    const int L0 = hrc[kRcAbort] - 1;
+#ifdef VG_PROBE
+    fprintf(stderr, "PROBE recut overflow replay from level %d (nsub=%d nwin=%d)\n", L0, hrc[kRcSub + L0],
+            hrc[kRcWin + L0]);
+#endif
+    VG_HIP(hipMemsetAsync(w.rc + kRcAbort, 0, sizeof(int), s));
+    VG_TRY(recut_slow_apply(ctx, L0, mp, dwin, list_of(L0 + 1), hrc));
+    for (int L = L0 + 1; L < nlev; L++) {
+      enqueue_level(L);
+      VG_TRY(read_rc(ctx, hrc));
+      VG_TRY(recut_slow_apply(ctx, L, mp, dwin, list_of(L + 1), hrc));
+    }
+    VG_TRY(read_counters(ctx));
+  }
+  const int nf = ctx->h_pinned[kCntFactors];
   if (nf > ctx->ba.cap_f) {
     ctx->err = "factor capacity exceeded";
     return VG_E_CAPACITY;
   }
   if (nf > 0) {
-    VG_TRY(sort_ids(ctx, cand, nf));
-    k_factor_finish<<<grid_for(nf), kBlock, 0, s>>>(nf, cand, m, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr);
+    VG_TRY(sort_ids(ctx, w.cand, nf));
+    k_factor_finish<<<grid_for(nf), kBlock, 0, s>>>(nf, w.cand, m, ctx->ba.fac_node, ctx->ba.fac_eig,
+                                                    ctx->ba.fac_pcr);
     VG_HIP(hipGetLastError());
   }
   *n_factors = nf;
@@ -1246,3 +1493,7 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinD& win, int n_oldest, int thre
 }
 
 }  // namespace vg
+
+#ifdef VG_PROBE
+VG_PROBE_READER(vg_probe_read_map)
+#endif

@@ -521,7 +521,7 @@ int stage_finish(vg_ctx* ctx) {
   HostPipe* P = hp(ctx);
   P->first = false;
   VG_HIP(hipMemcpyAsync(ctx->h_pinned, ctx->map.counters, kCntN * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  VG_HIP(hipStreamSynchronize(ctx->stream));
+  VG_HIP(stream_wait(ctx));
   prof_collect(ctx);
   ctx->stats.n_slide = ctx->h_pinned[kCntSlide];
   ctx->stats.nodes_used = ctx->h_pinned[kCntNodes];

@@ -136,6 +136,7 @@ struct Work {
   size_t tmp_bytes = 0;
   double* partials = nullptr;  // reduction partials
   int* iekf_cache = nullptr;   // per raw point cached leaf
+  int* rc = nullptr;           // device-side recut level counts (map.hip kRc*)
   int nparts = 0;
 };
 
@@ -145,7 +146,6 @@ struct BaBufs {
   int* fac_node = nullptr;
   double* fac_eig = nullptr;   // trial eig values/vectors (12) per factor
   Clu* fac_pcr = nullptr;      // trial merged cluster per factor
-  double* fac_comp = nullptr;  // per factor compressed Hessian inputs
   double* hpart = nullptr;     // chunk partials
   double* hout = nullptr;      // reduced 60x60 upper + 60 + 1
   double* rpart = nullptr;
@@ -177,6 +177,8 @@ struct vg_ctx {
   // stage timing with HIP events on the context stream (vg_profile)
   bool prof_on = false;
   hipEvent_t prof_ev[8][2] = {};
+  hipEvent_t sync_ev = nullptr;  // host-spin synchronisation (vg::stream_wait)
+  int dbg_apply_cap = -1;        // test knob (vgx_debug): recut apply event capacity
   bool prof_pending[8] = {};
   double prof_ms[8] = {};
   int prof_n[8] = {};
@@ -193,6 +195,19 @@ inline void prof_end(vg_ctx* c, int id) {
     (void)hipEventRecord(c->prof_ev[id][1], c->stream);
     c->prof_pending[id] = true;
   }
+}
+// Wait for the context stream by spinning on an event: a blocking
+// hipStreamSynchronize may sleep and costs up to ~100+ us of wake-up latency
+// per round trip, and the map stages make several per scan.
+inline hipError_t stream_wait(vg_ctx* c) {
+  hipError_t e = hipEventRecord(c->sync_ev, c->stream);
+  if (e != hipSuccess) return e;
+  while ((e = hipEventQuery(c->sync_ev)) == hipErrorNotReady) {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+  }
+  return e;
 }
 // call only after the stream has been synchronised past the recorded events
 inline void prof_collect(vg_ctx* c) {
@@ -282,3 +297,34 @@ int stage_ba(vg_ctx* ctx, int* iters_out);
 int stage_margi_slide(vg_ctx* ctx);
 int stage_finish(vg_ctx* ctx);
 }  // namespace vg
+
+// ---- phase probes (instrumented build only, make probe) -------------------
+#ifdef VG_PROBE
+// one probe array per translation unit (no relocatable device code); each
+// .hip exports its reader with VG_PROBE_READER(name)
+namespace vg {
+static __device__ unsigned long long g_probe[64];
+}
+#define VG_PROBE_READER(fn)                                                                        \
+  extern "C" int fn(unsigned long long* out, int n) {                                              \
+    if (n > 64) n = 64;                                                                            \
+    if (hipDeviceSynchronize() != hipSuccess) return -2;                                           \
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vg::g_probe), n * sizeof(unsigned long long)) != hipSuccess) \
+      return -2;                                                                                   \
+    unsigned long long z[64] = {0};                                                                \
+    if (hipMemcpyToSymbol(HIP_SYMBOL(vg::g_probe), z, sizeof(z)) != hipSuccess) return -2;         \
+    return 0;                                                                                      \
+  }
+#define VG_PROBE_BEGIN() unsigned long long vg_probe_t = wall_clock64()
+#define VG_PROBE_MARK(k)                                  \
+  do {                                                    \
+    if (threadIdx.x == 0) {                               \
+      const unsigned long long now_ = wall_clock64();     \
+      atomicAdd(&vg::g_probe[(k)], now_ - vg_probe_t);    \
+      vg_probe_t = now_;                                  \
+    }                                                     \
+  } while (0)
+#else
+#define VG_PROBE_BEGIN() (void)0
+#define VG_PROBE_MARK(k) (void)0
+#endif

@@ -88,6 +88,10 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
         ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
         return fail(VG_E_HIP);
       }
+  if ((e = hipEventCreateWithFlags(&ctx->sync_ev, hipEventDisableTiming)) != hipSuccess) {
+    ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
+    return fail(VG_E_HIP);
+  }
   host_init(ctx);
   *out = ctx;
   return VG_OK;
@@ -103,6 +107,7 @@ int vg_destroy(vg_ctx* ctx) {
   for (int i = 0; i < 8; i++)
     for (int j = 0; j < 2; j++)
       if (ctx->prof_ev[i][j]) (void)hipEventDestroy(ctx->prof_ev[i][j]);
+  if (ctx->sync_ev) (void)hipEventDestroy(ctx->sync_ev);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return VG_OK;
@@ -335,3 +340,14 @@ int vg_profile_read(vg_ctx* ctx, int stage, double* total_ms, int* count) {
 }
 
 }  // extern "C"
+
+// Test-only knobs (not part of include/vina_gpu.h): key 1 = event capacity of
+// the single-workgroup recut apply (0 forces the host-sized replay path).
+extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
+  if (!ctx) return VG_E_ARG;
+  if (key == 1) {
+    ctx->dbg_apply_cap = value;
+    return VG_OK;
+  }
+  return VG_E_ARG;
+}

@@ -16,7 +16,7 @@ from vgconfig import CConfig
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 REPO = os.path.dirname(PKG)
-LIB = os.path.join(PKG, "lib", "libvina_gpu.so")
+LIB = os.environ.get("VINA_GPU_LIB") or os.path.join(PKG, "lib", "libvina_gpu.so")
 HEADER = os.path.join(REPO, "include", "vina_gpu.h")
 STATE_LEN = 250
 
