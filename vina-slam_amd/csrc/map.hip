@@ -75,7 +75,8 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(w.leaf = ctx->arena.take<int>(cw));
   good &= ok(w.pw = ctx->arena.take<double>(cw * 3));
   good &= ok(w.iekf_cache = ctx->arena.take<int>(cw));
-  good &= ok(w.rc = ctx->arena.take<int>(64));
+  good &= ok(w.rc = ctx->arena.take<int>(128));
+  good &= ok(w.plan = ctx->arena.take<int>(cn * 8));
   w.nparts = 1024;
   good &= ok(w.partials = ctx->arena.take<double>((size_t)w.nparts * 40));
   if (!good) {
@@ -454,37 +455,73 @@ __global__ void __launch_bounds__(256) k_ins_keys(int n, const int* __restrict__
 }
 
 // OctoTree::push (octree.cpp:151-177) for every point of a leaf segment, in order
-__global__ void __launch_bounds__(256) k_push_window(int n, const uint64_t* __restrict__ keys, MP mp, int slot, DevMap m,
-                              const double* __restrict__ pw) {
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-    uint64_t k = keys[j];
-    if (k == ~0ull) continue;
-    int leaf = (int)(k >> 27);
-    if (j > 0 && (int)(keys[j - 1] >> 27) == leaf && keys[j - 1] != ~0ull) continue;
-    NodeHdr& h = m.hdr[leaf];
-    h.has_sw = 1;
-    h.isexist = 1;
-    const bool listed = h.layer < mp.max_layer;
-    Clu loc = m.pcrs[(size_t)leaf * mp.W + slot];
-    Clu add_ = m.pcr_add[leaf];
-    double cov[kCovN];
-    for (int t = 0; t < kCovN; t++) cov[t] = m.cov_add[(size_t)leaf * kCovN + t];
-    for (int jj = j; jj < n; jj++) {
-      uint64_t kk = keys[jj];
-      if (kk == ~0ull || (int)(kk >> 27) != leaf) break;
-      int i = (int)(kk & ((1u << 27) - 1));
-      size_t b = (size_t)slot * m.cap_wp + i;
-      V3 pnt = ld_v3(&m.wp_pnt[b * 3]);
-      M3 var = ld_m3(&m.wp_var[b * 9]);
-      V3 w = v3(pw[3 * i], pw[3 * i + 1], pw[3 * i + 2]);
-      if (listed) m.wp_leaf[b] = leaf;
-      clu_push(loc, pnt);
-      clu_push(add_, w);
-      bf_var_acc(cov, var, w);
+// segment heads of a sorted (leaf << 27 | order) key list -> compact list
+__global__ void __launch_bounds__(256) k_seg_heads(int n, const uint64_t* __restrict__ keys, int* __restrict__ heads,
+                                                   int* __restrict__ cnt) {
+  for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    const int j = base + threadIdx.x;
+    int head = 0;
+    if (j < n) {
+      const uint64_t k = keys[j];
+      head = k != ~0ull && (j == 0 || (keys[j - 1] >> 27) != (k >> 27)) ? 1 : 0;
     }
-    m.pcrs[(size_t)leaf * mp.W + slot] = loc;
-    m.pcr_add[leaf] = add_;
-    for (int t = 0; t < kCovN; t++) m.cov_add[(size_t)leaf * kCovN + t] = cov[t];
+    const int pos = wave_append(cnt, head);
+    if (head) heads[pos] = j;
+  }
+}
+
+// pvec_update into the leaves (voxel_map.cpp:104-131 / octree.cpp:151-177):
+// one wave per leaf segment of the sorted keys; lanes 0-8 own the frame
+// cluster, 9-17 the accumulated cluster, 18-62 cov_add (see role_inc)
+constexpr int kPushWaves = 4;
+__global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __restrict__ heads,
+                                                                 const int* __restrict__ nheads, int n,
+                                                                 const uint64_t* __restrict__ keys, MP mp, int slot,
+                                                                 DevMap m, const double* __restrict__ pw) {
+  __shared__ double E[kPushWaves][64][kErec];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int role = lane < 63 ? lane : -1;
+  RoleIdx ri = role < 9 ? role_clu(role < 0 ? 0 : role, kEq) : role < 18 ? role_clu(role - 9, kEp) : role_cov(role - 18);
+  const int nseg = *nheads;
+  for (int sg = blockIdx.x * kPushWaves + wv; sg < nseg; sg += gridDim.x * kPushWaves) {
+    const int j0 = heads[sg];
+    const int leaf = (int)(keys[j0] >> 27);
+    const bool listed = m.hdr[leaf].layer < mp.max_layer;
+    Clu* loc = &m.pcrs[(size_t)leaf * mp.W + slot];
+    Clu* add = &m.pcr_add[leaf];
+    double* acc_p = role < 0 ? nullptr
+                    : role < 9 ? (role < 6 ? &loc->P[role] : &loc->v[role - 6])
+                    : role < 18 ? (role < 15 ? &add->P[role - 9] : &add->v[role - 15])
+                                : &m.cov_add[(size_t)leaf * kCovN + role - 18];
+    double acc = acc_p ? *acc_p : 0.0;
+    int cnt = 0;
+    for (int base = j0;; base += 64) {
+      const int e = base + lane;
+      const uint64_t kk = e < n ? keys[e] : ~0ull;
+      const bool valid = kk != ~0ull && (int)(kk >> 27) == leaf;
+      if (valid) {
+        const int i = (int)(kk & ((1u << 27) - 1));
+        const size_t b = (size_t)slot * m.cap_wp + i;
+        fill_record(E[wv][lane], ld_v3(&m.wp_pnt[b * 3]), v3(pw[3 * i], pw[3 * i + 1], pw[3 * i + 2]),
+                    ld_m3(&m.wp_var[b * 9]));
+        if (listed) m.wp_leaf[b] = leaf;
+      }
+      const int nb = __popcll(__ballot(valid));
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int k = 0; k < nb; k++) acc += role_inc(E[wv][k], ri);
+      cnt += nb;
+      __builtin_amdgcn_wave_barrier();
+      if (nb < 64) break;
+    }
+    if (acc_p) *acc_p = acc;
+    if (lane == 0) {
+      loc->N += cnt;
+      add->N += cnt;
+      m.hdr[leaf].has_sw = 1;
+      m.hdr[leaf].isexist = 1;
+    }
   }
 }
 
@@ -600,7 +637,11 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, const InsPose& pose, int n, 
   }
   k_ins_keys<<<g, kBlock, 0, s>>>(n, w.leaf, w.k0);
   VG_TRY(sort_keys(ctx, w.k0, w.k1, n, 27 + bits_for(ctx->h_pinned[kCntNodes])));
-  k_push_window<<<g, kBlock, 0, s>>>(n, w.k1, mp, slot, m, w.pw);
+  VG_HIP(hipMemsetAsync(m.counters + kCntSeg, 0, sizeof(int), s));
+  k_seg_heads<<<g, kBlock, 0, s>>>(n, w.k1, w.list1, m.counters + kCntSeg);
+  // ~one wave per leaf segment (the count stays on the device)
+  const int gseg = (n + kPushWaves - 1) / kPushWaves < 2048 ? (n + kPushWaves - 1) / kPushWaves : 2048;
+  k_push_window<<<gseg, 64 * kPushWaves, 0, s>>>(w.list1, m.counters + kCntSeg, n, w.k1, mp, slot, m, w.pw);
   VG_HIP(hipGetLastError());
   return read_counters(ctx);
 }
@@ -615,8 +656,8 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, const InsPose& pose, int n, 
 // k_rc_apply sets rc[kRcAbort]; the host then replays the rest of the recut
 // with the host-sized path (recut_slow_apply), which only happens while the
 // map is first built.
-enum { kRcLvl = 0, kRcSub = 16, kRcWin = 32, kRcAbort = 48, kRcN = 64 };
-constexpr int kApplyThreads = 256;
+enum { kRcLvl = 0, kRcSub = 16, kRcWin = 32, kRcAbort = 48, kRcCh = 64, kRcChBase = 80, kRcN = 128 };
+constexpr int kApplyThreads = 1024;
 constexpr int kApplyEv = 4096;   // events sorted in LDS
 constexpr int kApplySub = kApplyThreads;  // subdividing leaves per level (one lane each)
 
@@ -896,7 +937,9 @@ __device__ void lds_bitonic(T* a, int n) {
 __global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int ev_cap, MP mp, const WinD* __restrict__ win,
                                                             DevMap m, int* __restrict__ next, const int* __restrict__ sub,
                                                             const uint64_t* __restrict__ wev,
-                                                            const uint32_t* __restrict__ wsrc, int* __restrict__ rc) {
+                                                            const uint32_t* __restrict__ wsrc,
+                                                            uint64_t* __restrict__ keys_out, int* __restrict__ cseg,
+                                                            int* __restrict__ rc) {
   __shared__ uint64_t s_ev[kApplyEv];
   __shared__ int s_sub[kApplySub], s_foff[kApplySub], s_coff[kApplySub];
   __shared__ int s_wsum[32];
@@ -990,12 +1033,17 @@ __global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int ev_cap, M
   VG_PROBE_MARK(18);
   lds_bitonic(s_ev, npad);
   VG_PROBE_MARK(19);
+  // sorted keys and the per-child segments [start, end) for k_rc_push
   for (int e = tid; e < ne; e += blockDim.x) {
-    const int child = (int)(s_ev[e] >> 27);
-    if (e > 0 && (int)(s_ev[e - 1] >> 27) == child) continue;
-    int jend = e + 1;
-    while (jend < ne && (int)(s_ev[jend] >> 27) == child) jend++;
-    push_child(s_ev, e, jend, mp, win, m);
+    const uint64_t k = s_ev[e];
+    const int c = (int)(k >> 27) - base;
+    keys_out[e] = k;
+    if (e == 0 || (int)(s_ev[e - 1] >> 27) != c + base) cseg[2 * c] = e;
+    if (e == ne - 1 || (int)(s_ev[e + 1] >> 27) != c + base) cseg[2 * c + 1] = e + 1;
+  }
+  if (tid == 0) {
+    rc[kRcCh + L] = ntot;
+    rc[kRcChBase + L] = base;
   }
   __syncthreads();
   VG_PROBE_MARK(20);
@@ -1005,6 +1053,142 @@ __global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int ev_cap, M
   if (tid == 0) atomicAdd(&g_probe[62], 1ull);
 #endif
   (void)s_meta;
+}
+
+// pushes of one level's children (push_fix then push per frame, octree.cpp:
+// 151-188), one wave per child; role layout: 0-8 accumulated cluster, 9-17
+// fixed cluster (point_fix events), 18-62 cov_add, 63-71 the frame cluster of
+// the current window slot (lanes 0-7 carry a second role)
+constexpr int kRcPushWaves = 4;
+__global__ void __launch_bounds__(64 * kRcPushWaves) k_rc_push(int L, const uint64_t* __restrict__ keys,
+                                                               const int* __restrict__ cseg, MP mp,
+                                                               const WinD* __restrict__ win, DevMap m,
+                                                               const int* __restrict__ rc) {
+  __shared__ double E[kRcPushWaves][64][kErec];
+  __shared__ int s_slot[kRcPushWaves][64];  // window slot of the event, -1 for point_fix
+  if (rc[kRcAbort]) return;
+  const int nch = rc[kRcCh + L], cbase = rc[kRcChBase + L];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  auto make = [](int r) -> RoleIdx {
+    if (r < 9) return role_clu(r, kEp);
+    if (r < 18) return role_clu(r - 9, kEp);
+    if (r < 63) return role_cov(r - 18);
+    return role_clu(r - 63, kEq);
+  };
+  const int r0 = lane, r1 = lane + 64;
+  const bool has1 = r1 < 72;
+  const RoleIdx ri0 = make(r0), ri1 = make(has1 ? r1 : 0);
+  for (int c = blockIdx.x * kRcPushWaves + wv; c < nch; c += gridDim.x * kRcPushWaves) {
+    const int child = cbase + c, j0 = cseg[2 * c], j1 = cseg[2 * c + 1];
+    NodeHdr& h = m.hdr[child];
+    const NodeHdr& ph = m.hdr[h.parent];
+    const bool listed = h.layer < mp.max_layer;
+    // leading point_fix events (phase 0 sorts first)
+    int nfix = 0;
+    for (int b0 = j0; b0 < j1; b0 += 64) {
+      const int e = b0 + lane;
+      const bool f = e < j1 && ((keys[e] >> 21) & 63) == 0;
+      const int k = __popcll(__ballot(f));
+      nfix += k;
+      if (k < 64) break;
+    }
+    int fix_off = 0;
+    if (nfix > 0 && listed) {
+      int off = 0;
+      if (lane == 0) {
+        off = atomicAdd(&m.counters[kCntFix], nfix);
+        if (off + nfix > m.cap_fix) {
+          atomicOr(&m.counters[kCntErr], 8);
+          off = -1;
+        } else {
+          h.fix_off = off;
+          h.fix_cap = nfix;
+          h.fix_cnt = nfix;
+        }
+      }
+      fix_off = __shfl(off, 0, 64);
+      if (fix_off < 0) continue;
+    }
+    auto acc_ptr = [&](int r, int slot) -> double* {
+      if (r < 9) return r < 6 ? &m.pcr_add[child].P[r] : &m.pcr_add[child].v[r - 6];
+      if (r < 18) return r < 15 ? &m.pcr_fix[child].P[r - 9] : &m.pcr_fix[child].v[r - 15];
+      if (r < 63) return &m.cov_add[(size_t)child * kCovN + r - 18];
+      Clu& lc = m.pcrs[(size_t)child * mp.W + slot];
+      return r < 69 ? &lc.P[r - 63] : &lc.v[r - 69];
+    };
+    double a0 = r0 < 63 ? *acc_ptr(r0, 0) : 0.0, a1 = 0.0;
+    int cur_slot = -1, loc_n = 0, nwin = 0;
+    for (int b0 = j0; b0 < j1; b0 += 64) {
+      const int e = b0 + lane;
+      if (e < j1) {
+        const uint64_t k = keys[e];
+        const int phase = (int)((k >> 21) & 63), idx = (int)(k & ((1u << 21) - 1));
+        if (phase == 0) {
+          const size_t f = (size_t)ph.fix_off + idx;
+          const V3 pt = ld_v3(&m.fix_pnt[f * 3]);
+          const M3 var = ld_m3(&m.fix_var[f * 9]);
+          fill_record(E[wv][lane], pt, pt, var);
+          s_slot[wv][lane] = -1;
+          if (listed) {
+            const size_t d = (size_t)fix_off + (e - j0);
+            for (int t = 0; t < 3; t++) m.fix_pnt[d * 3 + t] = pt[t];
+            for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = var[t];
+          }
+        } else {
+          const int ord = phase - 1, slot = win->mp[ord];
+          const size_t bb = (size_t)slot * m.cap_wp + idx;
+          const V3 pnt = ld_v3(&m.wp_pnt[bb * 3]);
+          fill_record(E[wv][lane], pnt, rigid(ld_m3(win->R[ord]), pnt, ld_v3(win->p[ord])),
+                      ld_m3(&m.wp_var[bb * 9]));
+          s_slot[wv][lane] = slot;
+          m.wp_leaf[bb] = listed ? child : -1;
+        }
+      }
+      const int nb = (j1 - b0) < 64 ? (j1 - b0) : 64;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int k = 0; k < nb; k++) {
+        const int slot = s_slot[wv][k];
+        const bool isfix = slot < 0;
+        if (!isfix && slot != cur_slot) {  // frame cluster switch (uniform)
+          if (cur_slot >= 0) {
+            if (r0 >= 63) *acc_ptr(r0, cur_slot) = a0;
+            if (has1) *acc_ptr(r1, cur_slot) = a1;
+            if (lane == 63) m.pcrs[(size_t)child * mp.W + cur_slot].N += loc_n;
+          }
+          cur_slot = slot;
+          if (r0 >= 63) a0 = *acc_ptr(r0, cur_slot);
+          if (has1) a1 = *acc_ptr(r1, cur_slot);
+          loc_n = 0;
+        }
+        const double* Ek = E[wv][k];
+        const bool use0 = r0 < 9 || (r0 >= 18 && r0 < 63) || (r0 < 18 ? isfix : !isfix);
+        const double i0 = role_inc(Ek, ri0);
+        if (use0) a0 += i0;
+        if (has1 && !isfix) a1 += role_inc(Ek, ri1);
+        if (!isfix) {
+          loc_n++;
+          nwin++;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (r0 < 63) *acc_ptr(r0, 0) = a0;
+    if (cur_slot >= 0) {
+      if (r0 >= 63) *acc_ptr(r0, cur_slot) = a0;
+      if (has1) *acc_ptr(r1, cur_slot) = a1;
+      if (lane == 63) m.pcrs[(size_t)child * mp.W + cur_slot].N += loc_n;
+    }
+    if (lane == 0) {
+      m.pcr_add[child].N += j1 - j0;
+      m.pcr_fix[child].N += nfix;
+      if (nwin > 0) {
+        h.has_sw = 1;
+        h.isexist = 1;
+      }
+    }
+  }
 }
 
 // ---- host-sized path (overflow replay) ----------------------------------
@@ -1145,10 +1329,12 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinD& win, const int* nper, int t
   };
   for (int L = 0; L < nlev; L++) {
     enqueue_level(L);
-    k_rc_apply<<<1, kApplyThreads, 0, s>>>(L, ev_cap, mp, dwin, m, list_of(L + 1), w.list2, w.k0, w.evsrc, w.rc);
+    k_rc_apply<<<1, kApplyThreads, 0, s>>>(L, ev_cap, mp, dwin, m, list_of(L + 1), w.list2, w.k0, w.evsrc, w.k1,
+                                           (int*)w.ac_off, w.rc);
+    k_rc_push<<<64, 64 * kRcPushWaves, 0, s>>>(L, w.k1, (const int*)w.ac_off, mp, dwin, m, w.rc);
   }
   VG_HIP(hipGetLastError());
-  int* hrc = ctx->h_pinned + 64;
+  int* hrc = ctx->h_pinned + 128;
   VG_TRY(read_rc(ctx, hrc));
   if (hrc[kRcAbort]) {  // replay from the level that overflowed on the host-sized path
     const int L0 = hrc[kRcAbort] - 1;
@@ -1182,8 +1368,28 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinD& win, const int* nper, int t
 
 // ------------------------------------------------------------------ margi (A10)
 // collect every node under the slide roots, level by level (top-down)
-__global__ void __launch_bounds__(256) k_collect_level(int nw, const int* __restrict__ work, DevMap m, int* __restrict__ next,
-                                int* __restrict__ leaves) {
+// level L of the surf_map_slide subtrees: level 0 is m.slide itself, levels
+// >= 1 sit back to back in `lists` (level L at the sum of the counts of levels
+// 1..L-1; the count of level L+1 is rc[L], appended by level L)
+__device__ __forceinline__ int margi_level(int L, const DevMap& m, const int* rc, int* lists, int** work) {
+  if (L == 0) {
+    *work = m.slide;
+    return m.counters[kCntSlide];
+  }
+  int off = 0;
+  for (int l = 1; l < L; l++) off += rc[l - 1];
+  *work = lists + off;
+  return rc[L - 1];
+}
+
+__global__ void __launch_bounds__(256) k_collect_level(int L, int thread_num, DevMap m, int* __restrict__ lists,
+                                                       int* __restrict__ leaves, int* __restrict__ rc) {
+  if (m.counters[kCntSlide] < thread_num) return;
+  int* work;
+  const int nw = margi_level(L, m, rc, lists, &work);
+  int* next;
+  (void)margi_level(L + 1, m, rc, lists, &next);  // its count is still being appended
+  const int next_off = (int)(next - lists);
   for (int base = blockIdx.x * blockDim.x; base < nw; base += gridDim.x * blockDim.x) {
     const int q = base + threadIdx.x;
     const int node = q < nw ? work[q] : -1;
@@ -1198,8 +1404,12 @@ __global__ void __launch_bounds__(256) k_collect_level(int nw, const int* __rest
         is_leaf = 1;
       }
     }
-    int o1 = wave_append(&m.counters[kCntNext], nchild);
+    int o1 = wave_append(&rc[L], nchild);
     int o2 = wave_append(&m.counters[kCntLeaves], is_leaf);
+    if (next_off + o1 + nchild > m.cap_nodes) {
+      atomicOr(&m.counters[kCntErr], 4);
+      continue;
+    }
     for (int j = 0; j < nchild; j++) next[o1 + j] = kids[j];
     if (is_leaf) leaves[o2] = node;
   }
@@ -1272,12 +1482,17 @@ __device__ void plane_update_dev(DevMap& m, int node, const Clu& pcr_add, const 
 // OctoTree::margi leaf branch (octree.cpp:397-484), mgsize = 1. keys = the
 // oldest slot's listed points sorted by (leaf, index): each leaf's segment is
 // its sw->points[mp[0]] list in push order.
-__global__ void __launch_bounds__(256) k_margi_leaf(int nl, const int* __restrict__ leaves, const uint64_t* __restrict__ keys, MP mp,
-                             WinD* __restrict__ win, DevMap m, const double* __restrict__ fac_eig,
-                             const Clu* __restrict__ fac_pcr) {
+__global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nleaves, const int* __restrict__ leaves,
+                                                    MP mp, WinD* __restrict__ win, DevMap m,
+                                                    const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
+                                                    int* __restrict__ plan) {
+  const int nl = *nleaves;
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nl; q += gridDim.x * blockDim.x) {
     int node = leaves[q];
     NodeHdr& h = m.hdr[node];
+    int* pq = &plan[(size_t)q * 8];
+    pq[0] = -1;  // no point_fix copies (k_margi_copy)
+    pq[4] = 0;
     int seg = m.nscr[(size_t)node * 4 + 0], segn = m.nscr[(size_t)node * 4 + 1];
     m.nscr[(size_t)node * 4 + 0] = -1;
     m.nscr[(size_t)node * 4 + 1] = -1;
@@ -1331,23 +1546,16 @@ __global__ void __launch_bounds__(256) k_margi_leaf(int nl, const int* __restric
               atomicOr(&m.counters[kCntErr], 8);
               continue;
             }
-            for (int j = 0; j < h.fix_cnt; j++) {
-              size_t a = (size_t)h.fix_off + j, b = (size_t)off + j;
-              for (int t = 0; t < 3; t++) m.fix_pnt[b * 3 + t] = m.fix_pnt[a * 3 + t];
-              for (int t = 0; t < 9; t++) m.fix_var[b * 9 + t] = m.fix_var[a * 9 + t];
-            }
+            pq[0] = h.fix_off;  // grow: move the live block first
+            pq[1] = h.fix_cnt;
+            pq[2] = off;
             h.fix_off = off;
             h.fix_cap = cap;
           }
-          for (int j = 0; j < segn; j++) {
-            int i = (int)(keys[seg + j] & ((1u << 27) - 1));
-            size_t b = (size_t)s0 * m.cap_wp + i;
-            V3 pt = rigid(R0, ld_v3(&m.wp_pnt[b * 3]), p0);
-            size_t d = (size_t)h.fix_off + h.fix_cnt;
-            for (int t = 0; t < 3; t++) m.fix_pnt[d * 3 + t] = pt[t];
-            for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = m.wp_var[b * 9 + t];
-            h.fix_cnt++;
-          }
+          pq[3] = seg;  // then append the oldest frame's points of this leaf
+          pq[4] = segn;
+          pq[5] = h.fix_off + h.fix_cnt;
+          h.fix_cnt += segn;
         }
       }
     } else {
@@ -1358,6 +1566,44 @@ __global__ void __launch_bounds__(256) k_margi_leaf(int nl, const int* __restric
     m.pcr_fix[node] = fix_;
     m.pcr_add[node] = add_;
     h.isexist = (fix_.N >= add_.N) ? 0 : 1;
+  }
+}
+
+// the point_fix copies planned by k_margi_leaf, one wave per leaf: the live
+// block moves when it grows, then the leaf's points of the oldest frame are
+// appended in push order (octree.cpp:450-458)
+constexpr int kCopyWaves = 4;
+__global__ void __launch_bounds__(64 * kCopyWaves) k_margi_copy(const int* __restrict__ nleaves,
+                                                                const int* __restrict__ plan,
+                                                                const uint64_t* __restrict__ keys,
+                                                                const WinD* __restrict__ win, DevMap m) {
+  const int lane = threadIdx.x & 63;
+  const int nl = *nleaves;
+  const int s0 = win->mp[0];
+  const M3 R0 = ld_m3(win->R[0]);
+  const V3 p0 = ld_v3(win->p[0]);
+  for (int q = blockIdx.x * kCopyWaves + (threadIdx.x >> 6); q < nl; q += gridDim.x * kCopyWaves) {
+    const int* pq = &plan[(size_t)q * 8];
+    const int src = pq[0], segn = pq[4];
+    if (src >= 0) {
+      const int nold = pq[1], dst = pq[2];
+      for (int j = lane; j < nold; j += 64) {
+        const size_t a = (size_t)src + j, b = (size_t)dst + j;
+        for (int t = 0; t < 3; t++) m.fix_pnt[b * 3 + t] = m.fix_pnt[a * 3 + t];
+        for (int t = 0; t < 9; t++) m.fix_var[b * 9 + t] = m.fix_var[a * 9 + t];
+      }
+    }
+    if (segn > 0) {
+      const int seg = pq[3], dst = pq[5];
+      for (int j = lane; j < segn; j += 64) {
+        const int i = (int)(keys[seg + j] & ((1u << 27) - 1));
+        const size_t b = (size_t)s0 * m.cap_wp + i;
+        const V3 pt = rigid(R0, ld_v3(&m.wp_pnt[b * 3]), p0);
+        const size_t d = (size_t)dst + j;
+        for (int t = 0; t < 3; t++) m.fix_pnt[d * 3 + t] = pt[t];
+        for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = m.wp_var[b * 9 + t];
+      }
+    }
   }
 }
 
@@ -1372,7 +1618,11 @@ __global__ void __launch_bounds__(256) k_margi_segs_clear(int n, const uint64_t*
 }
 
 // internal nodes bottom-up: isexist = OR(children) (octree.cpp:485-494)
-__global__ void __launch_bounds__(256) k_margi_internal(int nw, const int* __restrict__ work, DevMap m) {
+__global__ void __launch_bounds__(256) k_margi_internal(int L, int thread_num, DevMap m, int* __restrict__ lists,
+                                                        const int* __restrict__ rc) {
+  if (m.counters[kCntSlide] < thread_num) return;
+  int* work;
+  const int nw = margi_level(L, m, rc, lists, &work);
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) {
     int node = work[q];
     NodeHdr& h = m.hdr[node];
@@ -1386,12 +1636,16 @@ __global__ void __launch_bounds__(256) k_margi_internal(int nw, const int* __res
 
 // erase dead roots from surf_map_slide (local_mapping.cpp:67-78) with
 // clear_slwd over their subtrees (octree.cpp:739-756)
-__global__ void __launch_bounds__(256) k_margi_erase_mark(int nw, const int* __restrict__ work, DevMap m, int level, double jour) {
+__global__ void __launch_bounds__(256) k_margi_erase_mark(int L, int thread_num, DevMap m, int* __restrict__ lists,
+                                                          const int* __restrict__ rc) {
+  if (m.counters[kCntSlide] < thread_num) return;
+  int* work;
+  const int nw = margi_level(L, m, rc, lists, &work);
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) {
     int node = work[q];
     NodeHdr& h = m.hdr[node];
     int dead;
-    if (level == 0) {
+    if (L == 0) {
       dead = h.isexist ? 0 : 1;
     } else {
       dead = m.nscr[(size_t)h.parent * 4 + 2] == 7 ? 1 : 0;
@@ -1400,24 +1654,32 @@ __global__ void __launch_bounds__(256) k_margi_erase_mark(int nw, const int* __r
       m.nscr[(size_t)node * 4 + 2] = 7;
       h.has_sw = 0;
       for (int j = 0; j < m.W; j++) clu_zero(m.pcrs[(size_t)node * m.W + j]);
-      if (level == 0) m.in_slide[node] = 0;
+      if (L == 0) m.in_slide[node] = 0;
     }
   }
 }
-__global__ void __launch_bounds__(256) k_clear_mark(int nw, const int* __restrict__ work, DevMap m) {
+__global__ void __launch_bounds__(256) k_clear_mark(int L, int thread_num, DevMap m, int* __restrict__ lists,
+                                                    const int* __restrict__ rc) {
+  if (m.counters[kCntSlide] < thread_num) return;
+  int* work;
+  const int nw = margi_level(L, m, rc, lists, &work);
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x)
     m.nscr[(size_t)work[q] * 4 + 2] = -1;
 }
-__global__ void k_slide_compact(int n, const int* __restrict__ old, DevMap m) {
-  // single block, order-preserving compaction of the slide list
+// single block, order-preserving in-place compaction of the slide list (a
+// chunk is read completely before any of it is written; writes never pass
+// the read position)
+__global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m) {
   __shared__ int base;
+  __shared__ int sc[1024];
+  const int n = m.counters[kCntSlide];
+  if (n < thread_num) return;
   if (threadIdx.x == 0) base = 0;
   __syncthreads();
   for (int start = 0; start < n; start += blockDim.x) {
-    int q = start + threadIdx.x;
-    int keep = (q < n && m.in_slide[old[q]]) ? 1 : 0;
-    // block-wide exclusive scan of keep
-    __shared__ int sc[1024];
+    const int q = start + threadIdx.x;
+    const int node = q < n ? m.slide[q] : -1;
+    const int keep = (node >= 0 && m.in_slide[node]) ? 1 : 0;
     sc[threadIdx.x] = keep;
     __syncthreads();
     for (int off = 1; off < (int)blockDim.x; off <<= 1) {
@@ -1426,68 +1688,49 @@ __global__ void k_slide_compact(int n, const int* __restrict__ old, DevMap m) {
       sc[threadIdx.x] += v;
       __syncthreads();
     }
-    if (keep) m.slide[base + sc[threadIdx.x] - 1] = old[q];
+    if (keep) m.slide[base + sc[threadIdx.x] - 1] = node;
     __syncthreads();
     if (threadIdx.x == blockDim.x - 1) base += sc[threadIdx.x];
     __syncthreads();
   }
   if (threadIdx.x == 0) m.counters[kCntSlide] = base;
 }
-__global__ void __launch_bounds__(256) k_set_jour(int n, const int* __restrict__ slide, double* jour, double j) {
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) jour[slide[q]] = j;
+__global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, double j) {
+  const int n = m.counters[kCntSlide];
+  if (n < thread_num) return;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) m.jour[m.slide[q]] = j;
 }
 
+// multi_margi (local_mapping.cpp:21-78): every count stays on the device;
+// the host enqueues max_layer+1 levels (no level can be deeper) and
+// synchronises once at the end for the error flags.
 int map_margi(vg_ctx* ctx, const MP& mp, const WinD& win, int n_oldest, int thread_num, double jour) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
-  VG_TRY(read_counters(ctx));
-  const int nslide = ctx->h_pinned[kCntSlide];
-  if (nslide < thread_num) return VG_OK;  // local_mapping.cpp:26-28
+  const int nlev = mp.max_layer + 1;
   WinD* dwin = (WinD*)ctx->ba.xs;
   VG_HIP(hipMemcpyAsync(dwin, &win, sizeof(WinD), hipMemcpyHostToDevice, s));
-  k_set_jour<<<grid_for(nslide), kBlock, 0, s>>>(nslide, m.slide, m.jour, jour);
-  // level lists: store them back to back in list1 (offsets on host)
-  std::vector<int> lvl_off(1, 0), lvl_n;
-  VG_HIP(hipMemcpyAsync(w.list1, m.slide, (size_t)nslide * sizeof(int), hipMemcpyDeviceToDevice, s));
+  VG_HIP(hipMemsetAsync(w.rc, 0, kRcN * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.counters + kCntLeaves, 0, sizeof(int), s));
-  int cur_off = 0, cur_n = nslide;
-  for (int level = 0; level < 8 && cur_n > 0; level++) {
-    lvl_n.push_back(cur_n);
-    VG_HIP(hipMemsetAsync(m.counters + kCntNext, 0, sizeof(int), s));
-    k_collect_level<<<grid_for(cur_n), kBlock, 0, s>>>(cur_n, w.list1 + cur_off, m, w.list1 + cur_off + cur_n,
-                                                      w.list0);
-    VG_TRY(read_counters(ctx));
-    cur_off += cur_n;
-    lvl_off.push_back(cur_off);
-    cur_n = ctx->h_pinned[kCntNext];
-    if (cur_off + cur_n > m.cap_nodes) {
-      ctx->err = "margi level list overflow";
-      return VG_E_CAPACITY;
-    }
-  }
-  const int nleaves = ctx->h_pinned[kCntLeaves];
-  // oldest slot segments by leaf
+  const int gl = 64;  // grid-stride over device-side counts
+  k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour);
+  for (int L = 0; L < nlev; L++) k_collect_level<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.list0, w.rc);
+  // oldest slot segments by leaf (the slot's point count is known on the host)
   const int s0 = win.mp[0];
   if (n_oldest > 0) {
     k_margi_keys<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, s0, m, w.k0);
     VG_TRY(sort_keys(ctx, w.k0, w.k1, n_oldest, 64));
     k_margi_segs<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, w.k1, m);
   }
-  if (nleaves > 0) {
-    k_margi_leaf<<<grid_for(nleaves), kBlock, 0, s>>>(nleaves, w.list0, w.k1, mp, dwin, m, ctx->ba.fac_eig,
-                                                    ctx->ba.fac_pcr);
-  }
+  k_margi_leaf<<<gl, kBlock, 0, s>>>(m.counters + kCntLeaves, w.list0, mp, dwin, m, ctx->ba.fac_eig, ctx->ba.fac_pcr,
+                                     w.plan);
+  k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, w.k1, dwin, m);
   if (n_oldest > 0) k_margi_segs_clear<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, w.k1, m);
-  // bottom-up isexist for internal nodes
-  for (int l = (int)lvl_n.size() - 1; l >= 0; l--)
-    k_margi_internal<<<grid_for(lvl_n[l]), kBlock, 0, s>>>(lvl_n[l], w.list1 + lvl_off[l], m);
-  // erase dead roots and clear their subtrees' SlideWindows
-  for (int l = 0; l < (int)lvl_n.size(); l++)
-    k_margi_erase_mark<<<grid_for(lvl_n[l]), kBlock, 0, s>>>(lvl_n[l], w.list1 + lvl_off[l], m, l, jour);
-  for (int l = 0; l < (int)lvl_n.size(); l++)
-    k_clear_mark<<<grid_for(lvl_n[l]), kBlock, 0, s>>>(lvl_n[l], w.list1 + lvl_off[l], m);
-  k_slide_compact<<<1, 1024, 0, s>>>(nslide, w.list1, m);
+  for (int L = nlev - 1; L >= 0; L--) k_margi_internal<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc);
+  for (int L = 0; L < nlev; L++) k_margi_erase_mark<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc);
+  for (int L = 0; L < nlev; L++) k_clear_mark<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc);
+  k_slide_compact<<<1, 1024, 0, s>>>(thread_num, m);
   VG_HIP(hipGetLastError());
   return read_counters(ctx);
 }

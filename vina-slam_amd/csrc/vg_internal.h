@@ -117,7 +117,7 @@ struct DevMap {
 };
 enum {
   kCntNodes = 0, kCntFix = 1, kCntSlide = 2, kCntNew = 3, kCntTouched = 4, kCntWork = 5, kCntNext = 6,
-  kCntSub = 7, kCntEvents = 8, kCntFactors = 9, kCntCreate = 10, kCntErr = 11, kCntLeaves = 12, kCntMisc = 13,
+  kCntSub = 7, kCntEvents = 8, kCntFactors = 9, kCntCreate = 10, kCntErr = 11, kCntLeaves = 12, kCntMisc = 13, kCntSeg = 14,
   kCntN = 16
 };
 
@@ -136,7 +136,8 @@ struct Work {
   size_t tmp_bytes = 0;
   double* partials = nullptr;  // reduction partials
   int* iekf_cache = nullptr;   // per raw point cached leaf
-  int* rc = nullptr;           // device-side recut level counts (map.hip kRc*)
+  int* rc = nullptr;           // device-side level counts (recut / margi, map.hip kRc*)
+  int* plan = nullptr;         // per-leaf point_fix copy plan (margi)
   int nparts = 0;
 };
 
