@@ -15,8 +15,8 @@ import synth  # noqa: E402
 import vgconfig  # noqa: E402
 import vgpu  # noqa: E402
 
-PHASES = {0: "assemble", 1: "diag/tables", 2: "rank", 3: "tile fill", 4: "panel diag tile", 5: "panel rows",
-          6: "trailing mfma", 7: "tri solves", 8: "trial/q1"}
+PHASES = {3: "load tiles", 4: "diag+Linv+z", 5: "panel mfma", 6: "b-upd+trailing", 7: "backward solve",
+          8: "trial/q1"}
 
 
 def main(nscan=40, lidar="64line"):

@@ -423,75 +423,160 @@ __device__ __forceinline__ double bcast(double v, int lane) {
   return __longlong_as_double(((long long)hi32 << 32) | (unsigned int)lo32);
 }
 
-// assemble (or reload), gauge, damp, LDL^T-solve, trial state, IMU bias trial.
-//
-// Eigen's LDLT (the oracle's ldlt_solve) is left-looking, so its pivot order
-// depends only on the damped diagonal: it is the descending order of |diag|.
-// The kernel takes that permutation up front (rank sort), loads P A P^T into
-// the tile store and factors it without further pivoting, 16 columns per
-// panel: wave 0 factors the diagonal tile in registers, one lane per row
-// solves the panel below it, and the trailing update A22 -= L21 D L21^T runs
-// on v_mfma_f64_16x16x4 (one wave per 16x16 tile). Triangular solves run
-// blocked on wave 0. Ties in |diag| may order differently from Eigen's
-// sequential scan; that changes rounding only.
-__global__ void __launch_bounds__(256) k_ba_solve(int W, int nimu, double imu_coef, const double* __restrict__ hl,
-                                                   const double* __restrict__ imuout, double* __restrict__ Hcalc,
-                                                   double* __restrict__ Jcalc, const double* __restrict__ xs,
-                                                   double* __restrict__ xt, double* __restrict__ bias,
-                                                   double* __restrict__ dxi_out, BaState* __restrict__ st) {
+
+// broadcast lane qd of every quad (DPP quad_perm) — qd must fold to a constant
+template <int Q>
+__device__ __forceinline__ double quad_bcast_c(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo32 = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), Q * 0x55, 0xf, 0xf, false);
+  const int hi32 = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), Q * 0x55, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi32 << 32) | (unsigned int)lo32);
+}
+__device__ __forceinline__ double quad_bcast(double v, int qd) {
+  switch (qd) {
+    case 0: return quad_bcast_c<0>(v);
+    case 1: return quad_bcast_c<1>(v);
+    case 2: return quad_bcast_c<2>(v);
+    default: return quad_bcast_c<3>(v);
+  }
+}
+
+// one assembled lower entry (R >= C) of the 15W x 15W system in the host
+// loop's accumulation order (divide_thread 215-222: IMU factors k ascending,
+// x imu_coef, then hess_plus 171-179 adds the LiDAR 6x6 blocks)
+__device__ __forceinline__ double asm_entry(int R, int C, int nimu, double imu_coef, const double* hl,
+                                            const double* imuout, int L) {
+  const int bR = R / 15, bC = C / 15, rR = R % 15, rC = C % 15;
+  double v = 0.0;
+  for (int k = bR > 0 ? bR - 1 : 0; k <= bC && k < nimu; k++)
+    v += imuout[(size_t)k * 931 + (R - 15 * k) * 30 + (C - 15 * k)];
+  v *= imu_coef;
+  if (rR < 6 && rC < 6) {
+    const int lr = bR * 6 + rR, lc = bC * 6 + rC;
+    v += hl[lr * (lr + 1) / 2 + lc];
+  }
+  return v;
+}
+__device__ __forceinline__ double asm_grad(int t, int nimu, double imu_coef, const double* hl, const double* imuout,
+                                           int L) {
+  const int b = t / 15, r = t % 15;
+  double v = 0.0;
+  if (b >= 1 && b - 1 < nimu) v += imuout[(size_t)(b - 1) * 931 + 900 + r + 15];
+  if (b < nimu) v += imuout[(size_t)b * 931 + 900 + r];
+  v *= imu_coef;
+  if (r < 6) v += hl[L * (L + 1) / 2 + b * 6 + r];
+  return v;
+}
+
+// Wide preparation of the permuted, gauged, damped system: one block per
+// 16x16 tile of the lower block triangle. Every block ranks the damped
+// diagonal (Eigen's LDLT is left-looking, so its pivot order is the
+// descending order of |diag|, see the oracle's ldlt_solve) and writes its
+// tile of P A P^T to the tile image; on Hessian iterations it also stores
+// the assembled entries it visits (each lower entry exactly once) for the
+// damping-only retries. Block 0 writes the permuted right-hand side.
+__global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coef, const double* __restrict__ hl,
+                                                 const double* __restrict__ imuout, double* __restrict__ Hcalc,
+                                                 double* __restrict__ Jcalc, double* __restrict__ timg,
+                                                 double* __restrict__ bvec, double* __restrict__ dvec,
+                                                 double* __restrict__ jvec, int* __restrict__ ipg,
+                                                 const BaState* __restrict__ st) {
+  if (st->done) return;
+  constexpr int kN = kMaxNB * kTile;
+  __shared__ double Dv[kN], Jg[kN];
+  __shared__ int ip[kN];
+  const int n = 15 * W, L = 6 * W, NB = (n + kTile - 1) / kTile, N = NB * kTile;
+  const int tid = threadIdx.x, q = blockIdx.x;
+  const bool calc = st->calc_hess != 0;
+  const double u = st->u;
+  for (int t = tid; t < n; t += blockDim.x)
+    Dv[t] = t < 15 ? 1.0 : (calc ? asm_entry(t, t, nimu, imu_coef, hl, imuout, L) : Hcalc[lo(t, t)]);
+  __syncthreads();
+  for (int i = tid; i < n; i += blockDim.x) {  // rank of |D + u D| descending, index ascending on ties
+    const unsigned long long ki = (unsigned long long)__double_as_longlong(fabs(Dv[i] + u * Dv[i]));
+    int c = 0;
+    for (int j = 0; j < n; j++) {
+      const unsigned long long kj = (unsigned long long)__double_as_longlong(fabs(Dv[j] + u * Dv[j]));
+      c += (kj > ki) || (kj == ki && j < i);
+    }
+    ip[c] = i;
+  }
+  __syncthreads();
+  int TI = 0;
+  while ((TI + 1) * (TI + 2) / 2 <= q) TI++;
+  const int TJ = q - TI * (TI + 1) / 2;
+  for (int e = tid; e < 256; e += blockDim.x) {
+    const int r = e >> 4, c = e & 15, R = TI * 16 + r, C = TJ * 16 + c;
+    double v;
+    if (R >= n || C >= n) {
+      v = (R == C) ? 1.0 : 0.0;
+    } else {
+      const int pr = ip[R], pc = ip[C], a = pr > pc ? pr : pc, bb = pr > pc ? pc : pr;
+      const double raw = calc ? asm_entry(a, bb, nimu, imu_coef, hl, imuout, L) : Hcalc[lo(a, bb)];
+      if (calc && R >= C) Hcalc[lo(a, bb)] = raw;
+      if (pr == pc) v = Dv[pr] + u * Dv[pr];
+      else if (pr < 15 || pc < 15) v = 0.0;  // gauge frame 0 (optimizers.cpp:460-463)
+      else v = raw;
+    }
+    timg[(size_t)q * 256 + tel(r, c)] = v;
+  }
+  if (q == 0) {
+    for (int t = tid; t < n; t += blockDim.x) {
+      const double raw = calc ? asm_grad(t, nimu, imu_coef, hl, imuout, L) : Jcalc[t];
+      if (calc) Jcalc[t] = raw;
+      Jg[t] = t < 15 ? 0.0 : raw;
+      dvec[t] = Dv[t];
+      ipg[t] = ip[t];
+    }
+    __syncthreads();
+    for (int t = tid; t < N; t += blockDim.x) {
+      bvec[t] = t < n ? -Jg[ip[t]] : 0.0;
+      if (t < n) jvec[t] = Jg[t];
+    }
+  }
+}
+
+// LDL^T solve of the prepared system in one workgroup, trial state, IMU bias
+// trial. P A P^T is factored without further pivoting, 16 columns per panel:
+//   (1) wave 0 factors the diagonal tile in registers (4 lanes per row, the
+//       rank-1 vectors through LDS), inverts its unit-lower factor (stored in
+//       the tile's unused upper half) and forms M = L^-T D^-1 and the panel's
+//       share of z = D^+ L^-1 b (the right-hand side rides along as a
+//       bordered row, so the forward solve needs no separate pass);
+//   (2) the panel below, L_IK = A_IK M, one v_mfma_f64_16x16x4 wave per tile;
+//   (3) the trailing update A22 -= L21 D L21^T on MFMA and b -= L21 D z.
+// The backward solve runs blocked on wave 0. Rounding differs from Eigen's
+// sequential recurrences (tolerance-level; ties in |diag| may order
+// differently from its scan).
+__global__ void __launch_bounds__(512) k_ba_solve(int W, int nimu, const double* __restrict__ timg,
+                                                  const double* __restrict__ bvec, const double* __restrict__ dvec,
+                                                  const double* __restrict__ jvec, const int* __restrict__ ipg,
+                                                  const double* __restrict__ xs, double* __restrict__ xt,
+                                                  double* __restrict__ bias, double* __restrict__ dxi_out,
+                                                  BaState* __restrict__ st) {
   if (st->done) return;
   extern __shared__ __attribute__((aligned(16))) double T[];
   constexpr int kN = kMaxNB * kTile;
-  __shared__ double Jv[kN], Dv[kN], xv[kN], col[kN], tk[256], dK[16], rdK[16], tb[16];
-  __shared__ int ip[kN], cnt[kN];
+  __shared__ double Jv[kN], Dv[kN], xv[kN], col[kN], sM[256], dK[16], rdK[16], tb[16];
+  __shared__ int ip[kN];
   __shared__ unsigned char tI[kMaxNB * (kMaxNB + 1) / 2], tJ[kMaxNB * (kMaxNB + 1) / 2];
   const int n = 15 * W;
-  const int nn = n * (n + 1) / 2;
   const int NB = (n + kTile - 1) / kTile, N = NB * kTile;
   const int ntile = NB * (NB + 1) / 2;
   const int tid = threadIdx.x, nt = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nwave = nt >> 6;
   const double u = st->u;
   VG_PROBE_BEGIN();
-  if (st->calc_hess != 0) {
-    // every lower entry in one pass, in the accumulation order of the host
-    // loop (divide_thread 215-222: IMU factors k ascending, x imu_coef, then
-    // hess_plus 171-179 adds the LiDAR 6x6 blocks)
-    const int L = 6 * W;
-#pragma unroll 4
-    for (int t = tid; t < nn; t += nt) {
-      int R = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-      while ((R + 1) * (R + 2) / 2 <= t) R++;
-      while (R * (R + 1) / 2 > t) R--;
-      const int C = t - R * (R + 1) / 2;
-      const int bR = R / 15, bC = C / 15, rR = R % 15, rC = C % 15;
-      double v = 0.0;
-      for (int k = bR > 0 ? bR - 1 : 0; k <= bC && k < nimu; k++)
-        v += imuout[(size_t)k * 931 + (R - 15 * k) * 30 + (C - 15 * k)];
-      v *= imu_coef;
-      if (rR < 6 && rC < 6) {
-        const int lr = bR * 6 + rR, lc = bC * 6 + rC;
-        v += hl[lr * (lr + 1) / 2 + lc];
-      }
-      Hcalc[t] = v;
-    }
-    for (int t = tid; t < n; t += nt) {
-      const int b = t / 15, r = t % 15;
-      double v = 0.0;
-      if (b >= 1 && b - 1 < nimu) v += imuout[(size_t)(b - 1) * 931 + 900 + r + 15];
-      if (b < nimu) v += imuout[(size_t)b * 931 + 900 + r];
-      v *= imu_coef;
-      if (r < 6) v += hl[L * (L + 1) / 2 + b * 6 + r];
-      Jcalc[t] = v;
-    }
-    __syncthreads();
+  {
+    const double2* src = reinterpret_cast<const double2*>(timg);
+    double2* dst = reinterpret_cast<double2*>(T);
+    for (int t = tid; t < ntile * 128; t += nt) dst[t] = src[t];
   }
-  VG_PROBE_MARK(0);
-  // gauge frame 0 (optimizers.cpp:460-463), D = diag(H), tile index tables
-  for (int t = tid; t < N; t += nt) {
-    Dv[t] = t < n ? (t < 15 ? 1.0 : Hcalc[lo(t, t)]) : 0.0;
-    Jv[t] = (t < n && t >= 15) ? Jcalc[t] : 0.0;
-    cnt[t] = 0;
+  for (int t = tid; t < N; t += nt) xv[t] = bvec[t];
+  for (int t = tid; t < n; t += nt) {
+    Dv[t] = dvec[t];
+    Jv[t] = jvec[t];
+    ip[t] = ipg[t];
   }
   if (tid < ntile) {
     int I = 0;
@@ -500,210 +585,139 @@ __global__ void __launch_bounds__(256) k_ba_solve(int W, int nimu, double imu_co
     tJ[tid] = (unsigned char)(tid - I * (I + 1) / 2);
   }
   __syncthreads();
-  VG_PROBE_MARK(1);
-  // pivot order: rank of |D + u D| descending, index ascending on ties
-  // (uint64 order of the non-negative doubles: a total order, so even NaN
-  // input yields a permutation)
-  {
-    const int G = nt / n;
-    const int g = tid / n, i = tid % n;
-    if (g < G) {
-      const unsigned long long ki = (unsigned long long)__double_as_longlong(fabs(Dv[i] + u * Dv[i]));
-      const int j0 = g * n / G, j1 = (g + 1) * n / G;
-      int c = 0;
-      for (int j = j0; j < j1; j++) {
-        const unsigned long long kj = (unsigned long long)__double_as_longlong(fabs(Dv[j] + u * Dv[j]));
-        c += (kj > ki) || (kj == ki && j < i);
-      }
-      atomicAdd(&cnt[i], c);
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < n; i += nt) ip[cnt[i]] = i;
-  __syncthreads();
-  VG_PROBE_MARK(2);
-  // P A P^T into the tiles (diagonal tiles filled symmetric), padding = identity
-#pragma unroll 4
-  for (int e = tid; e < ntile * 256; e += nt) {
-    const int q = e >> 8, w = e & 255, r = w >> 4, c = w & 15;
-    const int R = tI[q] * 16 + r, C = tJ[q] * 16 + c;
-    double v;
-    if (R >= n || C >= n) {
-      v = (R == C) ? 1.0 : 0.0;
-    } else {
-      const int pr = ip[R], pc = ip[C];
-      if (pr == pc) v = Dv[pr] + u * Dv[pr];
-      else if (pr < 15 || pc < 15) v = 0.0;
-      else v = Hcalc[lo(pr, pc)];
-    }
-    T[q * 256 + tel(r, c)] = v;
-  }
-  for (int t = tid; t < N; t += nt) xv[t] = t < n ? -Jv[ip[t]] : 0.0;
-  __syncthreads();
   VG_PROBE_MARK(3);
 
   for (int K = 0; K < NB; K++) {
     double* Tkk = &T[tix(K, K) * 256];
-    // (1) diagonal tile on wave 0: lane (r = lane/4, q = lane%4) holds
-    //     a(r, q + 4s); column j: L(r,j) = a(r,j) / d_j, then
-    //     a(r,m) -= L(r,j) * (d_j L(m,j)) for j < m <= r. The vector
-    //     d_j L(:,j) goes through LDS (tb), laid out so that lane q reads its
-    //     four entries m = q + 4s contiguously.
     if (wave == 0) {
+      // (1) diagonal tile, lane (r = lane/4, q = lane%4) holds a(r, q + 4s)
+      //     and X(r, q + 4s) (X -> L^-1 by the same row operations):
+      //     column j: L(r,j) = a(r,j)/d_j; a(r,m) -= L(r,j) (d_j L(m,j));
+      //     X(r,:) -= L(r,j) X(j,:). Exchanges by DPP / ds_bpermute only.
       const int r = lane >> 2, q = lane & 3;
-      double a[4];
+      double a[4], X[4];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; s4++) a[s4] = Tkk[tel(r, q + 4 * s4)];
+      for (int s4 = 0; s4 < 4; s4++) {
+        a[s4] = Tkk[tel(r, q + 4 * s4)];
+        X[s4] = (q + 4 * s4 == r) ? 1.0 : 0.0;
+      }
 #pragma unroll
       for (int j = 0; j < 16; j++) {
         const int qj = j & 3, sj = j >> 2;
         const double dj = bcast(a[sj], 4 * j + qj);
         const double rdj = (dj != 0.0) ? 1.0 / dj : 1.0;  // Eigen leaves a zero pivot's column undivided
-        double l = __shfl(a[sj] * rdj, (lane & ~3) | qj, 64);
+        const double l = quad_bcast(a[sj] * rdj, qj);
         if (r > j && q == qj) a[sj] = l;
         const double t = dj * l;
-        if (q == 0) {
-          tb[(r & 3) * 4 + (r >> 2)] = t;
-          if (r > j) tk[r * 16 + j] = t;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        double tv[4];
+        double tv[4], xj[4];
 #pragma unroll
-        for (int s4 = 0; s4 < 4; s4++) tv[s4] = tb[q * 4 + s4];
+        for (int s4 = 0; s4 < 4; s4++) {
+          tv[s4] = __shfl(t, 4 * (q + 4 * s4), 64);
+          xj[s4] = __shfl(X[s4], 4 * j + q, 64);
+        }
 #pragma unroll
         for (int s4 = 0; s4 < 4; s4++) {
           const int m = q + 4 * s4;
           if (m > j && m <= r) a[s4] -= l * tv[s4];
+          if (r > j) X[s4] -= l * xj[s4];
         }
-        __builtin_amdgcn_wave_barrier();
       }
+      double myd = 0.0;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; s4++)
+        if (q + 4 * s4 == r) myd = a[s4];
+      myd = __shfl(myd, 4 * r + (r & 3), 64);
+      const double rd = (myd != 0.0) ? 1.0 / myd : 1.0;
+      // z_r = D^+ (X b_K)_r (Eigen: |d| > DBL_MIN divides, else 0)
+      double zp = 0.0;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; s4++) zp += X[s4] * xv[16 * K + q + 4 * s4];
+      zp += __shfl_xor(zp, 1, 64);
+      zp += __shfl_xor(zp, 2, 64);
+      const double zr = (fabs(myd) > 2.2250738585072014e-308) ? zp / myd : 0.0;
 #pragma unroll
       for (int s4 = 0; s4 < 4; s4++) {
         const int c = q + 4 * s4;
         if (c <= r) Tkk[tel(r, c)] = a[s4];
-        if (c == r) {
-          dK[r] = a[s4];
-          rdK[r] = (a[s4] != 0.0) ? 1.0 / a[s4] : 1.0;
-        }
+        if (c < r) Tkk[tel(c, r)] = X[s4];  // Linv(r, c) in the unused upper half
+        sM[c * 16 + r] = X[s4] * rd;       // M = L^-T D^-1
       }
+      if (q == 0) {
+        dK[r] = myd;
+        rdK[r] = rd;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (q == 0) xv[16 * K + r] = zr;
     }
     __syncthreads();
     VG_PROBE_MARK(4);
-    // (2) panel below the diagonal tile: one lane per row,
-    //     L(i,j) = (a(i,j) - sum_{m<j} L(i,m) tk(j,m)) / d_j;
-    //     meanwhile the last wave inverts the unit-lower diagonal tile into
-    //     its unused upper half (Linv(r,c), r > c, stored at (c,r)) for the
-    //     triangular solves
-    const int nrow = (NB - K - 1) * 16;
-    if (tid < nrow) {  // nrow <= 160 <= blockDim
-      const int I = K + 1 + (tid >> 4), r = tid & 15;
+    // (2) panel: L_IK = A_IK M (in place, one wave per tile)
+    for (int I = K + 1 + wave; I < NB; I += nwave) {
       double* Tik = &T[tix(I, K) * 256];
-      double a[16];
+      const int cc = lane & 15, rq = lane >> 4;
+      v4d acc = v4d{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int c = 0; c < 16; c++) a[c] = Tik[tel(r, c)];
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        double v = a[j];
-#pragma unroll
-        for (int m = 0; m < j; m++) v -= a[m] * tk[j * 16 + m];
-        a[j] = v * rdK[j];
+      for (int ks = 0; ks < 4; ks++) {
+        const int kk = 4 * ks + rq;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Tik[tel(cc, kk)], sM[kk * 16 + cc], acc, 0, 0, 0);
       }
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int c = 0; c < 16; c++) Tik[tel(r, c)] = a[c];
-    } else if (wave == nwave - 1 && lane < 16) {
-      const int c = lane;  // column c of Linv: x = e_c, x_i = -sum_{c<=k<i} L(i,k) x_k
-      double x[16];
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        double v = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < i; k++) v -= Tkk[tel(i, k)] * x[k];
-        x[i] = (i < c) ? 0.0 : v;
-      }
-#pragma unroll
-      for (int i = 0; i < 16; i++)
-        if (i > c) Tkk[tel(c, i)] = x[i];
+      for (int g = 0; g < 4; g++) Tik[tel(rq + 4 * g, cc)] = acc[g];
     }
     __syncthreads();
     VG_PROBE_MARK(5);
-    // (3) trailing update on MFMA: tile (I,J) -= L(I,K) diag(d) L(J,K)^T
+    // (3) trailing tiles A_IJ -= L_IK diag(d) L_JK^T and the bordered
+    //     right-hand side b_I -= L_IK diag(d) z_K (column 0 of an MFMA tile),
+    //     one wave per job
     const int Rm = NB - K - 1;
     const int ntr = Rm * (Rm + 1) / 2;
-    for (int q = wave; q < ntr; q += nwave) {
-      const int I = K + 1 + tI[q], J = K + 1 + tJ[q];
-      double* Tij = &T[tix(I, J) * 256];
+    for (int q = wave; q < ntr + Rm; q += nwave) {
+      const bool brow = q >= ntr;
+      const int I = brow ? K + 1 + (q - ntr) : K + 1 + tI[q], J = brow ? 0 : K + 1 + tJ[q];
       const double* Aik = &T[tix(I, K) * 256];
       const double* Ajk = &T[tix(J, K) * 256];
+      double* Tij = &T[tix(I, J) * 256];
       const int cc = lane & 15, rq = lane >> 4;
       v4d acc;
 #pragma unroll
-      for (int g = 0; g < 4; g++) acc[g] = Tij[tel(rq + 4 * g, cc)];
+      for (int g = 0; g < 4; g++) acc[g] = brow ? (cc == 0 ? xv[16 * I + rq + 4 * g] : 0.0) : Tij[tel(rq + 4 * g, cc)];
 #pragma unroll
       for (int ks = 0; ks < 4; ks++) {
         const int kk = 4 * ks + rq;
         const double av = -(Aik[tel(cc, kk)] * dK[kk]);
-        const double bv = Ajk[tel(cc, kk)];
+        const double bv = brow ? (cc == 0 ? xv[16 * K + kk] : 0.0) : Ajk[tel(cc, kk)];
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
+      if (brow) {
+        if (cc == 0)
 #pragma unroll
-      for (int g = 0; g < 4; g++) Tij[tel(rq + 4 * g, cc)] = acc[g];
+          for (int g = 0; g < 4; g++) xv[16 * I + rq + 4 * g] = acc[g];
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; g++) Tij[tel(rq + 4 * g, cc)] = acc[g];
+      }
     }
     __syncthreads();
     VG_PROBE_MARK(6);
   }
 
-  // triangular solves on wave 0, lane (r = lane & 15, qd = lane >> 4): the
-  // off-diagonal tiles and the diagonal tiles' inverses as 4-way split
-  // matrix-vector products (no sequential substitution chains)
+  // backward solve on wave 0, lane (r = lane & 15, qd = lane >> 4):
+  // x_I = Linv_II^T (z_I - sum_{J>I} L_JI^T x_J)
   if (wave == 0) {
     const int r = lane & 15, qd = lane >> 4;
-    for (int I = 0; I < NB; I++) {  // y_I = Linv_II (b_I - sum_{J<I} L_IJ y_J)
-      double s = 0.0;
-      for (int J = 0; J < I; J++) {
-        const double* Tt = &T[tix(I, J) * 256];
-#pragma unroll
-        for (int c = qd; c < 16; c += 4) s += Tt[tel(r, c)] * xv[16 * J + c];
-      }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      const double z = xv[16 * I + r] - s;
-      if (qd == 0) tb[r] = z;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const double* Td = &T[tix(I, I) * 256];
-      double s2 = 0.0;
-#pragma unroll
-      for (int c = qd; c < 16; c += 4)
-        if (c < r) s2 += Td[tel(c, r)] * tb[c];
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (qd == 0) xv[16 * I + r] = z + s2;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    // D^+ (Eigen: |d| > DBL_MIN divides, else 0)
-    for (int t = lane; t < N; t += 64) {
-      const int I = t >> 4, rr = t & 15;
-      const double d = T[tix(I, I) * 256 + tel(rr, rr)];
-      xv[t] = (fabs(d) > 2.2250738585072014e-308) ? xv[t] / d : 0.0;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int I = NB - 1; I >= 0; I--) {  // x_I = Linv_II^T (y_I - sum_{J>I} L_JI^T x_J)
-      double s = 0.0;
+    for (int I = NB - 1; I >= 0; I--) {
+      double sacc = 0.0;
       for (int J = I + 1; J < NB; J++) {
         const double* Tt = &T[tix(J, I) * 256];
 #pragma unroll
-        for (int c = qd; c < 16; c += 4) s += Tt[tel(c, r)] * xv[16 * J + c];
+        for (int c = qd; c < 16; c += 4) sacc += Tt[tel(c, r)] * xv[16 * J + c];
       }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      const double z = xv[16 * I + r] - s;
+      sacc += __shfl_xor(sacc, 16, 64);
+      sacc += __shfl_xor(sacc, 32, 64);
+      const double z = xv[16 * I + r] - sacc;
       if (qd == 0) tb[r] = z;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -867,6 +881,11 @@ struct BaDev {
   double* imuout;
   double* imures;
   double* Hcalc;
+  double* timg;
+  double* bvec;
+  double* dvec;
+  double* jvec;
+  int* ipg;
   double* Jcalc;
   double* xs;
   double* xt;
@@ -899,7 +918,7 @@ int ba_alloc(vg_ctx* ctx) {
   good &= (b.hpart = ctx->arena.take<double>((size_t)(b.cap_f / hess_chunk(W) + 1) * nout)) != nullptr;
   good &= (b.hout = ctx->arena.take<double>(nout + 16)) != nullptr;
   good &= (b.rpart = ctx->arena.take<double>(b.cap_f / 256 + 16)) != nullptr;
-  good &= (b.xs = ctx->arena.take<double>(1024 + 2 * n * (n + 1) / 2 + 4 * n + 2 * kMaxW * kX + kMaxW * kImuRec +
+  good &= (b.xs = ctx->arena.take<double>(1024 + 2 * n * (n + 1) / 2 + 4 * n + kMaxNB * (kMaxNB + 1) / 2 * 256 + 4 * kMaxNB * kTile + 2 * kMaxW * kX + kMaxW * kImuRec +
                                           kMaxW * 12 + kMaxW * 931 + kMaxW + 64)) != nullptr;
   if (!good) {
     ctx->err = "arena exhausted (BA)";
@@ -926,6 +945,16 @@ static BaDev carve(vg_ctx* ctx) {
   BaDev d;
   d.Hcalc = p;
   p += nn;
+  d.timg = p;
+  p += kMaxNB * (kMaxNB + 1) / 2 * 256;
+  d.bvec = p;
+  p += kMaxNB * kTile;
+  d.dvec = p;
+  p += kMaxNB * kTile;
+  d.jvec = p;
+  p += kMaxNB * kTile;
+  d.ipg = (int*)p;
+  p += kMaxNB * kTile;
   d.Jcalc = p;
   p += n;
   d.dxi = p;
@@ -975,6 +1004,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double*
   const int nrb = (nf + 255) / 256;
   const size_t hess_lds = hess_lds_bytes(W);
   const size_t solve_lds = solve_lds_bytes(W);
+  const int NBt = (15 * W + kTile - 1) / kTile, ntile = NBt * (NBt + 1) / 2;
   // one LM iteration (optimizers.cpp:449-516); kernels early-exit on the
   // device-side flags once converged
   auto iteration = [&]() {
@@ -984,8 +1014,10 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double*
       k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nchunk, nout, d.part, d.hl, d.st);
     }
     if (nimu > 0) k_ba_imu<<<nimu, 256, 0, s>>>(nimu, d.imurec, d.bias, d.xs, d.imuout, d.st);
-    k_ba_solve<<<1, 256, solve_lds, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.xs, d.xt,
-                                          d.bias, d.dxi, d.st);
+    k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
+                                    d.dvec, d.jvec, d.ipg, d.st);
+    k_ba_solve<<<1, 512, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
+                                         d.st);
     if (nf > 0)
       k_ba_resid<<<nrb, 256, 0, s>>>(nf, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
                                      ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st);
