@@ -68,6 +68,123 @@ __device__ __forceinline__ void factor_basics(const double* e, const Clu& pcr, d
   f[23] = e[0];
 }
 
+// IMU record layout (doubles): R_delta 9, p_delta 3, v_delta 3, R_bg 9, p_bg 9,
+// p_ba 9, v_bg 9, v_ba 9, dtime 1 (=61), pad to 64, cov_inv 225.
+// bias state per factor: dbg 3, dba 3, dbg_buf 3, dba_buf 3.
+__device__ void imu_residual(const double* rec, const double* bias, const double* x1, const double* x2, double* rr,
+                             double* joc /*15x30 or null*/) {
+  const M3 Rd = ld_m3(rec), Rbg = ld_m3(rec + 15), pbg = ld_m3(rec + 24), pba = ld_m3(rec + 33),
+           vbg = ld_m3(rec + 42), vba = ld_m3(rec + 51);
+  const V3 pd = ld_v3(rec + 9), vd = ld_v3(rec + 12);
+  const double dtime = rec[60];
+  const V3 dbg = ld_v3(bias), dba = ld_v3(bias + 3);
+  const M3 R1 = ld_m3(x1), R2 = ld_m3(x2);
+  const V3 p1 = ld_v3(x1 + 9), p2 = ld_v3(x2 + 9), v1 = ld_v3(x1 + 12), v2 = ld_v3(x2 + 12);
+  const V3 bg1 = ld_v3(x1 + 15), bg2 = ld_v3(x2 + 15), ba1 = ld_v3(x1 + 18), ba2 = ld_v3(x2 + 18);
+  const V3 g1 = ld_v3(x1 + 21);
+  M3 Rc = mul(Rd, Exp(mul(Rbg, dbg)));
+  V3 tc = add(add(pd, mul(pbg, dbg)), mul(pba, dba));
+  V3 vc = add(add(vd, mul(vbg, dbg)), mul(vba, dba));
+  M3 res_r = mul(mul(tr(Rc), tr(R1)), R2);
+  V3 exp_v = mul(tr(R1), sub(sub(v2, v1), scl(g1, dtime)));
+  V3 res_v = sub(exp_v, vc);
+  V3 exp_t = mul(tr(R1), sub(sub(sub(p2, p1), scl(v1, dtime)), scl(g1, 0.5 * dtime * dtime)));
+  V3 res_t = sub(exp_t, tc);
+  V3 lr = Log(res_r);
+  for (int k = 0; k < 3; k++) {
+    rr[k] = lr[k];
+    rr[3 + k] = res_t[k];
+    rr[6 + k] = res_v[k];
+    rr[9 + k] = bg2[k] - bg1[k];
+    rr[12 + k] = ba2[k] - ba1[k];
+  }
+  if (!joc) return;
+  for (int k = 0; k < 450; k++) joc[k] = 0.0;
+  auto put = [&](int r0, int c0, const M3& m) {
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) joc[(r0 + r) * 30 + c0 + c] = m(r, c);
+  };
+  const M3 JRi = jr_inv(res_r);
+  const M3 R1t = tr(R1);
+  put(0, 0, scl(mul(mul(JRi, tr(R2)), R1), -1.0));
+  put(0, 15, JRi);
+  put(0, 9, scl(mul(mul(mul(JRi, tr(res_r)), jr(mul(Rbg, dbg))), Rbg), -1.0));
+  put(3, 0, hat(exp_t));
+  put(3, 3, scl(R1t, -1.0));
+  put(3, 6, scl(R1t, -dtime));
+  put(3, 9, scl(pbg, -1.0));
+  put(3, 12, scl(pba, -1.0));
+  put(3, 18, R1t);
+  put(6, 0, hat(exp_v));
+  put(6, 6, scl(R1t, -1.0));
+  put(6, 9, scl(vbg, -1.0));
+  put(6, 12, scl(vba, -1.0));
+  put(6, 21, R1t);
+  put(9, 9, scl(M3::I(), -1.0));
+  put(12, 12, scl(M3::I(), -1.0));
+  put(9, 24, M3::I());
+  put(12, 27, M3::I());
+}
+
+// give_evaluate with jac_enable at the current state; out per factor: jtj 900, gg 30, res 1
+__device__ void imu_factor_block(int k, const double* __restrict__ imurec, const double* __restrict__ bias,
+                                 const double* __restrict__ xs, double* __restrict__ out) {
+  __shared__ double joc[450], rr[15], P[450], C[225];
+  const double* rec = &imurec[(size_t)k * kImuRec];
+  if (threadIdx.x == 0) imu_residual(rec, &bias[k * 12], &xs[(size_t)k * kX], &xs[(size_t)(k + 1) * kX], rr, joc);
+  for (int t = threadIdx.x; t < 225; t += blockDim.x) C[t] = rec[64 + t];
+  __syncthreads();
+  // P = joc^T C (30 x 15)
+  for (int t = threadIdx.x; t < 450; t += blockDim.x) {
+    int r = t / 15, l = t % 15;
+    double s = joc[0 * 30 + r] * C[0 * 15 + l];
+    for (int q = 1; q < 15; q++) s += joc[q * 30 + r] * C[q * 15 + l];
+    P[t] = s;
+  }
+  __syncthreads();
+  double* o = &out[(size_t)k * 931];
+  for (int t = threadIdx.x; t < 900; t += blockDim.x) {
+    int r = t / 30, c = t % 30;
+    double s = P[r * 15 + 0] * joc[0 * 30 + c];
+    for (int l = 1; l < 15; l++) s += P[r * 15 + l] * joc[l * 30 + c];
+    o[t] = s;
+  }
+  if (threadIdx.x < 30) {
+    int r = threadIdx.x;
+    double s = P[r * 15 + 0] * rr[0];
+    for (int l = 1; l < 15; l++) s += P[r * 15 + l] * rr[l];
+    o[900 + r] = s;
+  }
+  if (threadIdx.x == 0) {
+    double cr[15];
+    for (int r = 0; r < 15; r++) {
+      double s = C[r * 15] * rr[0];
+      for (int l = 1; l < 15; l++) s += C[r * 15 + l] * rr[l];
+      cr[r] = s;
+    }
+    double s = rr[0] * cr[0];
+    for (int r = 1; r < 15; r++) s += rr[r] * cr[r];
+    o[930] = s;
+  }
+}
+
+// IMU residuals only (give_evaluate(..., false)) at the trial state
+__device__ void imu_residual_lane(int k, const double* __restrict__ imurec, const double* __restrict__ bias,
+                                  const double* __restrict__ xt, double* __restrict__ res) {
+  const double* rec = &imurec[(size_t)k * kImuRec];
+  double rr[15];
+  imu_residual(rec, &bias[k * 12], &xt[(size_t)k * kX], &xt[(size_t)(k + 1) * kX], rr, nullptr);
+  double cr[15];
+  for (int r = 0; r < 15; r++) {
+    double s = rec[64 + r * 15] * rr[0];
+    for (int l = 1; l < 15; l++) s += rec[64 + r * 15 + l] * rr[l];
+    cr[r] = s;
+  }
+  double s = rr[0] * cr[0];
+  for (int r = 1; r < 15; r++) s += rr[r] * cr[r];
+  res[k] = s;
+}
+
 // acc_evaluate2 per (factor, frame) — factors.cpp:57-97. Outputs the
 // diagonal 6x6 block Hb (lower, 21), the gradient piece jjt (6) and the three
 // 6-vectors whose outer products make every off-diagonal block:
@@ -159,8 +276,15 @@ __global__ void __launch_bounds__(kHessThreads) k_ba_hess(int nf, int W, const i
                                                           const double* __restrict__ fac_eig,
                                                           const Clu* __restrict__ fac_pcr, const Clu* __restrict__ pcrs,
                                                           const int* __restrict__ mpring, const double* __restrict__ xs,
-                                                          double* __restrict__ part, const BaState* __restrict__ st) {
+                                                          double* __restrict__ part, const BaState* __restrict__ st,
+                                                          int nchunk, int nimu, const double* __restrict__ imurec,
+                                                          const double* __restrict__ bias, double* __restrict__ imuout) {
   if (st->done || !st->calc_hess) return;
+  if ((int)blockIdx.x >= nchunk) {  // IMU factors ride in the same launch (give_evaluate, jac_enable)
+    const int k = blockIdx.x - nchunk;
+    if (k < nimu) imu_factor_block(k, imurec, bias, xs, imuout);
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) double X[];
   __shared__ double S[kHessThreads];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -278,130 +402,6 @@ __global__ void __launch_bounds__(256) k_ba_hfinal(int nchunk, int nout, const d
   s += __shfl_down(s, 2, 8);
   s += __shfl_down(s, 1, 8);
   if (e < nout && sub == 0) out[e] = s;
-}
-
-// IMU record layout (doubles): R_delta 9, p_delta 3, v_delta 3, R_bg 9, p_bg 9,
-// p_ba 9, v_bg 9, v_ba 9, dtime 1 (=61), pad to 64, cov_inv 225.
-// bias state per factor: dbg 3, dba 3, dbg_buf 3, dba_buf 3.
-__device__ void imu_residual(const double* rec, const double* bias, const double* x1, const double* x2, double* rr,
-                             double* joc /*15x30 or null*/) {
-  const M3 Rd = ld_m3(rec), Rbg = ld_m3(rec + 15), pbg = ld_m3(rec + 24), pba = ld_m3(rec + 33),
-           vbg = ld_m3(rec + 42), vba = ld_m3(rec + 51);
-  const V3 pd = ld_v3(rec + 9), vd = ld_v3(rec + 12);
-  const double dtime = rec[60];
-  const V3 dbg = ld_v3(bias), dba = ld_v3(bias + 3);
-  const M3 R1 = ld_m3(x1), R2 = ld_m3(x2);
-  const V3 p1 = ld_v3(x1 + 9), p2 = ld_v3(x2 + 9), v1 = ld_v3(x1 + 12), v2 = ld_v3(x2 + 12);
-  const V3 bg1 = ld_v3(x1 + 15), bg2 = ld_v3(x2 + 15), ba1 = ld_v3(x1 + 18), ba2 = ld_v3(x2 + 18);
-  const V3 g1 = ld_v3(x1 + 21);
-  M3 Rc = mul(Rd, Exp(mul(Rbg, dbg)));
-  V3 tc = add(add(pd, mul(pbg, dbg)), mul(pba, dba));
-  V3 vc = add(add(vd, mul(vbg, dbg)), mul(vba, dba));
-  M3 res_r = mul(mul(tr(Rc), tr(R1)), R2);
-  V3 exp_v = mul(tr(R1), sub(sub(v2, v1), scl(g1, dtime)));
-  V3 res_v = sub(exp_v, vc);
-  V3 exp_t = mul(tr(R1), sub(sub(sub(p2, p1), scl(v1, dtime)), scl(g1, 0.5 * dtime * dtime)));
-  V3 res_t = sub(exp_t, tc);
-  V3 lr = Log(res_r);
-  for (int k = 0; k < 3; k++) {
-    rr[k] = lr[k];
-    rr[3 + k] = res_t[k];
-    rr[6 + k] = res_v[k];
-    rr[9 + k] = bg2[k] - bg1[k];
-    rr[12 + k] = ba2[k] - ba1[k];
-  }
-  if (!joc) return;
-  for (int k = 0; k < 450; k++) joc[k] = 0.0;
-  auto put = [&](int r0, int c0, const M3& m) {
-    for (int r = 0; r < 3; r++)
-      for (int c = 0; c < 3; c++) joc[(r0 + r) * 30 + c0 + c] = m(r, c);
-  };
-  const M3 JRi = jr_inv(res_r);
-  const M3 R1t = tr(R1);
-  put(0, 0, scl(mul(mul(JRi, tr(R2)), R1), -1.0));
-  put(0, 15, JRi);
-  put(0, 9, scl(mul(mul(mul(JRi, tr(res_r)), jr(mul(Rbg, dbg))), Rbg), -1.0));
-  put(3, 0, hat(exp_t));
-  put(3, 3, scl(R1t, -1.0));
-  put(3, 6, scl(R1t, -dtime));
-  put(3, 9, scl(pbg, -1.0));
-  put(3, 12, scl(pba, -1.0));
-  put(3, 18, R1t);
-  put(6, 0, hat(exp_v));
-  put(6, 6, scl(R1t, -1.0));
-  put(6, 9, scl(vbg, -1.0));
-  put(6, 12, scl(vba, -1.0));
-  put(6, 21, R1t);
-  put(9, 9, scl(M3::I(), -1.0));
-  put(12, 12, scl(M3::I(), -1.0));
-  put(9, 24, M3::I());
-  put(12, 27, M3::I());
-}
-
-// give_evaluate with jac_enable at the current state; out per factor: jtj 900, gg 30, res 1
-__global__ void __launch_bounds__(256) k_ba_imu(int nimu, const double* __restrict__ imurec,
-                                                const double* __restrict__ bias, const double* __restrict__ xs,
-                                                double* __restrict__ out, const BaState* __restrict__ st) {
-  if (st->done || !st->calc_hess) return;
-  const int k = blockIdx.x;
-  if (k >= nimu) return;
-  __shared__ double joc[450], rr[15], P[450], C[225];
-  const double* rec = &imurec[(size_t)k * kImuRec];
-  if (threadIdx.x == 0) imu_residual(rec, &bias[k * 12], &xs[(size_t)k * kX], &xs[(size_t)(k + 1) * kX], rr, joc);
-  for (int t = threadIdx.x; t < 225; t += blockDim.x) C[t] = rec[64 + t];
-  __syncthreads();
-  // P = joc^T C (30 x 15)
-  for (int t = threadIdx.x; t < 450; t += blockDim.x) {
-    int r = t / 15, l = t % 15;
-    double s = joc[0 * 30 + r] * C[0 * 15 + l];
-    for (int q = 1; q < 15; q++) s += joc[q * 30 + r] * C[q * 15 + l];
-    P[t] = s;
-  }
-  __syncthreads();
-  double* o = &out[(size_t)k * 931];
-  for (int t = threadIdx.x; t < 900; t += blockDim.x) {
-    int r = t / 30, c = t % 30;
-    double s = P[r * 15 + 0] * joc[0 * 30 + c];
-    for (int l = 1; l < 15; l++) s += P[r * 15 + l] * joc[l * 30 + c];
-    o[t] = s;
-  }
-  if (threadIdx.x < 30) {
-    int r = threadIdx.x;
-    double s = P[r * 15 + 0] * rr[0];
-    for (int l = 1; l < 15; l++) s += P[r * 15 + l] * rr[l];
-    o[900 + r] = s;
-  }
-  if (threadIdx.x == 0) {
-    double cr[15];
-    for (int r = 0; r < 15; r++) {
-      double s = C[r * 15] * rr[0];
-      for (int l = 1; l < 15; l++) s += C[r * 15 + l] * rr[l];
-      cr[r] = s;
-    }
-    double s = rr[0] * cr[0];
-    for (int r = 1; r < 15; r++) s += rr[r] * cr[r];
-    o[930] = s;
-  }
-}
-
-// IMU residuals only (give_evaluate(..., false)) at the trial state
-__global__ void __launch_bounds__(256) k_ba_imures(int nimu, const double* __restrict__ imurec, const double* __restrict__ bias,
-                            const double* __restrict__ xt, double* __restrict__ res, const BaState* __restrict__ st) {
-  if (st->done) return;
-  int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nimu) return;
-  const double* rec = &imurec[(size_t)k * kImuRec];
-  double rr[15];
-  imu_residual(rec, &bias[k * 12], &xt[(size_t)k * kX], &xt[(size_t)(k + 1) * kX], rr, nullptr);
-  double cr[15];
-  for (int r = 0; r < 15; r++) {
-    double s = rec[64 + r * 15] * rr[0];
-    for (int l = 1; l < 15; l++) s += rec[64 + r * 15 + l] * rr[l];
-    cr[r] = s;
-  }
-  double s = rr[0] * cr[0];
-  for (int r = 1; r < 15; r++) s += rr[r] * cr[r];
-  res[k] = s;
 }
 
 // packed lower storage of the n x n system (Hcalc)
@@ -780,8 +780,14 @@ __global__ void __launch_bounds__(256) k_ba_resid(int nf, int W, const int* __re
                                                   const Clu* __restrict__ pcr_fix, const Clu* __restrict__ pcrs,
                                                   const int* __restrict__ mpring, const double* __restrict__ xt,
                                                   double* __restrict__ fac_eig, Clu* __restrict__ fac_pcr,
-                                                  double* __restrict__ rpart, const BaState* __restrict__ st) {
+                                                  double* __restrict__ rpart, const BaState* __restrict__ st, int nrb,
+                                                  int nimu, const double* __restrict__ imurec,
+                                                  const double* __restrict__ bias, double* __restrict__ imures) {
   if (st->done) return;
+  if ((int)blockIdx.x >= nrb) {  // IMU residuals at the trial state in the same launch
+    if ((int)threadIdx.x < nimu) imu_residual_lane(threadIdx.x, imurec, bias, xt, imures);
+    return;
+  }
   double acc = 0.0;
   const int a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a < nf) {
@@ -1008,20 +1014,19 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double*
   // one LM iteration (optimizers.cpp:449-516); kernels early-exit on the
   // device-side flags once converged
   auto iteration = [&]() {
-    if (nf > 0) {
-      k_ba_hess<<<nchunk, kHessThreads, hess_lds, s>>>(nf, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
-                                                       ctx->map.pcrs, d.mpring, d.xs, d.part, d.st);
-      k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nchunk, nout, d.part, d.hl, d.st);
-    }
-    if (nimu > 0) k_ba_imu<<<nimu, 256, 0, s>>>(nimu, d.imurec, d.bias, d.xs, d.imuout, d.st);
+    if (nf > 0 || nimu > 0)
+      k_ba_hess<<<(nf > 0 ? nchunk : 0) + nimu, kHessThreads, hess_lds, s>>>(
+          nf, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr, ctx->map.pcrs, d.mpring, d.xs, d.part, d.st,
+          nf > 0 ? nchunk : 0, nimu, d.imurec, d.bias, d.imuout);
+    if (nf > 0) k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nchunk, nout, d.part, d.hl, d.st);
     k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
                                     d.dvec, d.jvec, d.ipg, d.st);
     k_ba_solve<<<1, 512, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
                                          d.st);
-    if (nf > 0)
-      k_ba_resid<<<nrb, 256, 0, s>>>(nf, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
-                                     ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st);
-    if (nimu > 0) k_ba_imures<<<1, 64, 0, s>>>(nimu, d.imurec, d.bias, d.xt, d.imures, d.st);
+    if (nf > 0 || nimu > 0)
+      k_ba_resid<<<(nf > 0 ? nrb : 0) + (nimu > 0 ? 1 : 0), 256, 0, s>>>(
+          nf, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt, ctx->ba.fac_eig, ctx->ba.fac_pcr,
+          d.rpart, d.st, nf > 0 ? nrb : 0, nimu, d.imurec, d.bias, d.imures);
     k_ba_control<<<1, 256, 0, s>>>(W, nimu, nf > 0 ? nrb : 0, ctx->cfg.imu_coef, d.hl, nl + L, d.imuout, d.imures,
                                    d.rpart, d.xs, d.xt, d.bias, d.st);
   };

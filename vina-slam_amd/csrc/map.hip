@@ -112,8 +112,10 @@ int map_reset(vg_ctx* ctx) {
 
 // Node records of freshly allocated nodes must be zero: the pool is zeroed
 // lazily per allocation range.
-__global__ void __launch_bounds__(256) k_zero_nodes(int first, const int* __restrict__ cnt_after, int W, PlaneRec* pl, Clu* pcr_add,
-                             Clu* pcr_fix, double* cov, double* eig, double* jour, Clu* pcrs) {
+__global__ void __launch_bounds__(256) k_zero_nodes(int first, const int* __restrict__ first_ptr,
+                                                   const int* __restrict__ cnt_after, int W, PlaneRec* pl, Clu* pcr_add,
+                                                   Clu* pcr_fix, double* cov, double* eig, double* jour, Clu* pcrs) {
+  if (first_ptr) first = *first_ptr;
   const int last = cnt_after[0];
   for (int id = first + blockIdx.x * blockDim.x + threadIdx.x; id < last; id += gridDim.x * blockDim.x) {
     PlaneRec& p = pl[id];
@@ -252,7 +254,7 @@ __global__ void __launch_bounds__(256) k_iekf(int n, const float* __restrict__ x
 // ordered two-level sum of the block partials: lane t sums rows t, t+256, ...
 // for all 34 values, then a fixed LDS tree (deterministic)
 __global__ void __launch_bounds__(256) k_iekf_final(int nb, const double* __restrict__ partials,
-                                                    double* __restrict__ out) {
+                                                    double* __restrict__ zc_out, int* __restrict__ zc_flag, int seq) {
   __shared__ double red[256][kIekfVals + 1];
   double acc[kIekfVals];
   for (int j = 0; j < kIekfVals; j++) acc[j] = 0.0;
@@ -265,7 +267,12 @@ __global__ void __launch_bounds__(256) k_iekf_final(int nb, const double* __rest
       for (int j = 0; j < kIekfVals; j++) red[threadIdx.x][j] += red[threadIdx.x + w][j];
     __syncthreads();
   }
-  if (threadIdx.x < kIekfVals) out[threadIdx.x] = red[0][threadIdx.x];
+  // publish to host-mapped memory with a sequence flag (the host spins on it:
+  // no copy, no event)
+  if (threadIdx.x < kIekfVals)
+    __hip_atomic_store(&zc_out[threadIdx.x], red[0][threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(zc_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 int iekf_reset_cache(vg_ctx* ctx, int n) {
@@ -278,16 +285,32 @@ int iekf_iter(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const f
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
   int nb = grid_for(n, 256, 512);
-  prof_begin(ctx, kProfIekfKernel);
+  const int seq = ++ctx->zc_seq;
+  const int ring = ctx->prof_on && ctx->iekf_ring_n < 8 ? ctx->iekf_ring_n++ : -1;
+  if (ring >= 0) (void)hipEventRecord(ctx->iekf_ev[ring][0], s);
   k_iekf<<<nb, 256, 0, s>>>(n, x, y, z, mp, pose, ctx->map, w.iekf_cache, w.partials);
-  prof_end(ctx, kProfIekfKernel);
-  k_iekf_final<<<1, 256, 0, s>>>(nb, w.partials, w.partials + (size_t)w.nparts * 38);
+  if (ring >= 0) (void)hipEventRecord(ctx->iekf_ev[ring][1], s);
+  k_iekf_final<<<1, 256, 0, s>>>(nb, w.partials, ctx->d_zc, reinterpret_cast<int*>(ctx->d_zc + 64), seq);
   VG_HIP(hipGetLastError());
-  VG_HIP(hipMemcpyAsync(ctx->h_pinned_d, w.partials + (size_t)w.nparts * 38, kIekfVals * sizeof(double),
-                        hipMemcpyDeviceToHost, s));
-  VG_HIP(stream_wait(ctx));
-  prof_collect(ctx);
-  for (int j = 0; j < kIekfVals; j++) out34[j] = ctx->h_pinned_d[j];
+  // spin on the sequence flag the last block publishes (host-mapped memory)
+  const int* flag = reinterpret_cast<const int*>(ctx->h_zc + 64);
+  for (long spin = 0; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; spin++) {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+    if ((spin & 4095) == 4095) {
+      const hipError_t e = hipStreamQuery(s);
+      if (e != hipSuccess && e != hipErrorNotReady) {
+        ctx->err = std::string("k_iekf: ") + hipGetErrorString(e);
+        return VG_E_HIP;
+      }
+      if (e == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+        ctx->err = "k_iekf finished without publishing its sums";
+        return VG_E_HIP;
+      }
+    }
+  }
+  for (int j = 0; j < kIekfVals; j++) out34[j] = ctx->h_zc[j];
   return VG_OK;
 }
 
@@ -299,6 +322,13 @@ __global__ void __launch_bounds__(256) k_ins_prep(int n, const float* __restrict
                            double* __restrict__ pw, uint32_t* __restrict__ hslot) {
   const M3 R = ld_m3(ps.R), rot_var = ld_m3(ps.rot_var), tsl_var = ld_m3(ps.tsl_var);
   const V3 p = ld_v3(ps.p);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // per-insert device counters (read by the later kernels)
+    m.counters[kCntNew] = m.counters[kCntNodes];  // first id of this scan's new roots
+    m.counters[kCntTouched] = 0;
+    m.counters[kCntCreate] = 0;
+    m.counters[kCntSeg] = 0;
+    m.counters[kCntMisc] = 0;  // insert abort flag (child-allocation overflow)
+  }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     V3 pnt;
     M3 var;
@@ -369,8 +399,9 @@ __global__ void __launch_bounds__(256) k_add_counter(int* counters, int idx, con
 
 // distinct roots touched by the scan (the thread_num quirk, voxel_map.cpp:94-97),
 // isexist on existing roots (voxel_map.cpp:70), surf_map_slide registration
-__global__ void __launch_bounds__(256) k_ins_touch(int n, const uint32_t* __restrict__ hslot, int epoch, int first_new, DevMap m,
+__global__ void __launch_bounds__(256) k_ins_touch(int n, const uint32_t* __restrict__ hslot, int epoch, DevMap m,
                            int* __restrict__ root_of) {
+  const int first_new = m.counters[kCntNew];
   for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
     const int i = base + threadIdx.x;
     int first = 0, add_slide = 0, root = -1;
@@ -396,8 +427,16 @@ __global__ void __launch_bounds__(256) k_ins_touch(int n, const uint32_t* __rest
 }
 
 // descend to a leaf; a missing child becomes a creation request (parent, octant)
-__global__ void __launch_bounds__(256) k_ins_descend(int n, const double* __restrict__ pw, DevMap m, int* __restrict__ leaf,
-                              int* __restrict__ reqlist) {
+// the later insert kernels do nothing when the scan touched fewer than
+// thread_num roots (voxel_map.cpp:96-97: no allocation at all) or when the
+// child allocation overflowed k_ins_alloc (the host replays them)
+__device__ __forceinline__ bool ins_skip(const DevMap& m, int thread_num) {
+  return m.counters[kCntTouched] < thread_num || m.counters[kCntMisc] != 0;
+}
+
+__global__ void __launch_bounds__(256) k_ins_descend(int n, int thread_num, const double* __restrict__ pw, DevMap m,
+                                                     int* __restrict__ leaf, int* __restrict__ reqlist) {
+  if (ins_skip(m, thread_num)) return;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int node = leaf[i];
     if (node < 0) continue;
@@ -437,7 +476,9 @@ __global__ void __launch_bounds__(256) k_child_count(int np, const int* __restri
 __global__ void __launch_bounds__(256) k_child_alloc(int np, const int* __restrict__ parents, const uint32_t* __restrict__ off, DevMap m,
                               int* __restrict__ next, int next_base);
 
-__global__ void __launch_bounds__(256) k_ins_resolve(int n, const double* __restrict__ pw, DevMap m, int* __restrict__ leaf) {
+__global__ void __launch_bounds__(256) k_ins_resolve(int n, int thread_num, const double* __restrict__ pw, DevMap m,
+                                                     int* __restrict__ leaf) {
+  if (ins_skip(m, thread_num)) return;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int node = leaf[i];
     if (node >= -1) continue;
@@ -447,7 +488,9 @@ __global__ void __launch_bounds__(256) k_ins_resolve(int n, const double* __rest
 }
 
 // sort key: (leaf << 27) | order
-__global__ void __launch_bounds__(256) k_ins_keys(int n, const int* __restrict__ leaf, uint64_t* __restrict__ keys) {
+__global__ void __launch_bounds__(256) k_ins_keys(int n, int thread_num, const DevMap m, const int* __restrict__ leaf,
+                                                  uint64_t* __restrict__ keys) {
+  if (ins_skip(m, thread_num)) return;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int l = leaf[i];
     keys[i] = l >= 0 ? (((uint64_t)l << 27) | (uint64_t)i) : ~0ull;
@@ -456,8 +499,10 @@ __global__ void __launch_bounds__(256) k_ins_keys(int n, const int* __restrict__
 
 // OctoTree::push (octree.cpp:151-177) for every point of a leaf segment, in order
 // segment heads of a sorted (leaf << 27 | order) key list -> compact list
-__global__ void __launch_bounds__(256) k_seg_heads(int n, const uint64_t* __restrict__ keys, int* __restrict__ heads,
+__global__ void __launch_bounds__(256) k_seg_heads(int n, int thread_num, const DevMap m,
+                                                   const uint64_t* __restrict__ keys, int* __restrict__ heads,
                                                    int* __restrict__ cnt) {
+  if (ins_skip(m, thread_num)) return;
   for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
     const int j = base + threadIdx.x;
     int head = 0;
@@ -477,8 +522,10 @@ constexpr int kPushWaves = 4;
 __global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __restrict__ heads,
                                                                  const int* __restrict__ nheads, int n,
                                                                  const uint64_t* __restrict__ keys, MP mp, int slot,
-                                                                 DevMap m, const double* __restrict__ pw) {
+                                                                 DevMap m, const double* __restrict__ pw,
+                                                                 int thread_num) {
   __shared__ double E[kPushWaves][64][kErec];
+  if (ins_skip(m, thread_num)) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int role = lane < 63 ? lane : -1;
   RoleIdx ri = role < 9 ? role_clu(role < 0 ? 0 : role, kEq) : role < 18 ? role_clu(role - 9, kEp) : role_cov(role - 18);
@@ -523,6 +570,137 @@ __global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __re
       m.hdr[leaf].isexist = 1;
     }
   }
+}
+
+// zero a freshly allocated node's records (the pool is zeroed lazily)
+__device__ __forceinline__ void zero_node(DevMap& m, int id) {
+  PlaneRec& p = m.pl[id];
+  for (int j = 0; j < 27; j++) (&p.center[0])[j] = 0.0;
+  p.radius = 0;
+  p.pad = 0;
+  clu_zero(m.pcr_add[id]);
+  clu_zero(m.pcr_fix[id]);
+  for (int j = 0; j < kCovN; j++) m.cov_add[(size_t)id * kCovN + j] = 0.0;
+  for (int j = 0; j < 12; j++) m.eig[(size_t)id * 12 + j] = 0.0;
+  m.jour[id] = 0.0;
+  for (int j = 0; j < m.W; j++) clu_zero(m.pcrs[(size_t)id * m.W + j]);
+}
+
+// children of parent p in octant order, ids id0, id0+1, ...; appended to next
+__device__ __forceinline__ void alloc_parent(DevMap& m, int p, int id0, int* next, int next_pos, bool zero) {
+  NodeHdr& ph = m.hdr[p];
+  int k = 0;
+  for (int o = 0; o < 8; o++) {
+    if (m.cfirst[(size_t)p * 8 + o] != -5) continue;
+    const int id = id0 + k;
+    k++;
+    m.cfirst[(size_t)p * 8 + o] = 0x7f7f7f7f;
+    if (id >= m.cap_nodes) {
+      atomicOr(&m.counters[kCntErr], 4);
+      continue;
+    }
+    int xyz[3] = {(o >> 2) & 1, (o >> 1) & 1, o & 1};
+    double c[3];
+    for (int j = 0; j < 3; j++) c[j] = ph.center[j] + (float)((2 * xyz[j] - 1) * ph.qlen);
+    init_node(m.hdr[id], c, ph.qlen / 2, ph.layer + 1, p);
+    if (zero) zero_node(m, id);
+    ph.child[o] = id;
+    if (next) next[next_pos + k - 1] = id;
+  }
+  m.nscr[(size_t)p * 4 + 1] = -1;
+}
+
+// exclusive prefix over one value per thread of a 1024-lane workgroup
+__device__ __forceinline__ int block_excl_scan(int v, int* s_wsum, int* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_wsum[wv] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); k++) {
+      int t = s_wsum[k];
+      s_wsum[k] = acc;
+      acc += t;
+    }
+    s_wsum[16] = acc;
+  }
+  __syncthreads();
+  const int r = s_wsum[wv] + x - v;
+  *total = s_wsum[16];
+  __syncthreads();
+  return r;
+}
+
+// ascending bitonic sort of n (power of two) keys in LDS by the whole workgroup
+template <typename T>
+__device__ void lds_bitonic(T* a, int n) {
+  for (int k = 2; k <= n; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int pj = i ^ j;
+        if (pj > i) {
+          const T x = a[i], y = a[pj];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            a[i] = y;
+            a[pj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+}
+
+// new roots: advance the node counter by the first-occurrence count
+__global__ void k_ins_roots(DevMap m, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ rank, int n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const int c = n > 0 ? (int)(rank[n - 1] + flag[n - 1]) : 0;
+    m.counters[kCntNodes] += c;
+    m.counters[kCntRoots] = c;
+  }
+}
+
+// children requested by k_ins_descend, in one workgroup: parents sorted
+// ascending (deterministic ids), per-parent octant order, ids base + prefix,
+// records zeroed. More than kInsAllocCap parents sets the abort flag and the
+// host replays the allocation on the host-sized path.
+constexpr int kInsAllocCap = 4096;
+__global__ void __launch_bounds__(1024) k_ins_alloc(int thread_num, DevMap m, const int* __restrict__ reqlist) {
+  __shared__ int sp[kInsAllocCap];
+  __shared__ int s_w[17];
+  if (m.counters[kCntTouched] < thread_num) return;
+  const int np = m.counters[kCntCreate];
+  if (np == 0) return;
+  if (np > kInsAllocCap) {
+    if (threadIdx.x == 0) m.counters[kCntMisc] = 1;
+    return;
+  }
+  int npad = 2;
+  while (npad < np) npad <<= 1;
+  for (int i = threadIdx.x; i < npad; i += blockDim.x) sp[i] = i < np ? reqlist[i] : 0x7fffffff;
+  __syncthreads();
+  lds_bitonic(sp, npad);
+  const int base = m.counters[kCntNodes];
+  int carry = 0;
+  for (int start = 0; start < np; start += blockDim.x) {
+    const int q = start + threadIdx.x;
+    const int p = q < np ? sp[q] : -1;
+    int cc = 0;
+    if (p >= 0)
+      for (int o = 0; o < 8; o++) cc += (m.cfirst[(size_t)p * 8 + o] == -5) ? 1 : 0;
+    int tot;
+    const int off = block_excl_scan(cc, s_w, &tot);
+    if (p >= 0) alloc_parent(m, p, base + carry + off, nullptr, 0, true);
+    carry += tot;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) m.counters[kCntNodes] = base + carry;
 }
 
 static int read_counters(vg_ctx* ctx) {
@@ -589,7 +767,7 @@ static int alloc_children(vg_ctx* ctx, int* plist, int np, int* next, int next_b
   VG_TRY(excl_scan(ctx, w.ac_cnt, w.ac_off, np));
   k_child_alloc<<<grid_for(np), kBlock, 0, s>>>(np, plist, w.ac_off, ctx->map, next, next_base);
   k_add_counter<<<1, 64, 0, s>>>(ctx->map.counters, kCntNodes, w.ac_cnt, w.ac_off, np);
-  k_zero_nodes<<<grid_for(1 << 16), kBlock, 0, s>>>(first, ctx->map.counters + kCntNodes, ctx->map.W, ctx->map.pl,
+  k_zero_nodes<<<grid_for(1 << 16), kBlock, 0, s>>>(first, nullptr, ctx->map.counters + kCntNodes, ctx->map.W, ctx->map.pl,
                                                   ctx->map.pcr_add, ctx->map.pcr_fix, ctx->map.cov_add, ctx->map.eig,
                                                   ctx->map.jour, ctx->map.pcrs);
   VG_HIP(hipGetLastError());
@@ -607,43 +785,51 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, const InsPose& pose, int n, 
   *roots_new = 0;
   *touched = 0;
   if (n <= 0) return VG_OK;
-  VG_TRY(read_counters(ctx));
-  const int first_new = ctx->h_pinned[kCntNodes];
-  int g = grid_for(n);
+  // every count stays on the device; one synchronisation at the end
+  const int g = grid_for(n);
+  const int key_bits = 27 + bits_for(m.cap_nodes);
+  const int gseg = (n + kPushWaves - 1) / kPushWaves < 2048 ? (n + kPushWaves - 1) / kPushWaves : 2048;
+  auto tail = [&]() -> int {  // leaves -> sorted (leaf, order) keys -> pushes
+    k_ins_resolve<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.leaf);
+    k_ins_keys<<<g, kBlock, 0, s>>>(n, thread_num, m, w.leaf, w.k0);
+    VG_TRY(sort_keys(ctx, w.k0, w.k1, n, key_bits));
+    k_seg_heads<<<g, kBlock, 0, s>>>(n, thread_num, m, w.k1, w.list1, m.counters + kCntSeg);
+    // ~one wave per leaf segment (the count stays on the device)
+    k_push_window<<<gseg, 64 * kPushWaves, 0, s>>>(w.list1, m.counters + kCntSeg, n, w.k1, mp, slot, m, w.pw,
+                                                  thread_num);
+    VG_HIP(hipGetLastError());
+    return VG_OK;
+  };
   k_ins_prep<<<g, kBlock, 0, s>>>(n, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, mp, pose, slot, m, w.pw, w.u0);
   k_ins_newflag<<<g, kBlock, 0, s>>>(n, w.u0, m.hval, m.hfirst, w.v0);
   VG_TRY(excl_scan(ctx, w.v0, w.v1, n));
   k_ins_newalloc<<<g, kBlock, 0, s>>>(n, w.u0, w.v0, w.v1, mp, m);
-  k_add_counter<<<1, 64, 0, s>>>(m.counters, kCntNodes, w.v0, w.v1, n);
-  k_zero_nodes<<<grid_for(1 << 16), kBlock, 0, s>>>(first_new, m.counters + kCntNodes, m.W, m.pl, m.pcr_add,
-                                                  m.pcr_fix, m.cov_add, m.eig, m.jour, m.pcrs);
-  VG_HIP(hipMemsetAsync(m.counters + kCntTouched, 0, sizeof(int), s));
-  k_ins_touch<<<g, kBlock, 0, s>>>(n, w.u0, epoch, first_new, m, w.leaf);
-  VG_HIP(hipGetLastError());
+  k_ins_roots<<<1, 64, 0, s>>>(m, w.v0, w.v1, n);
+  k_zero_nodes<<<grid_for(1 << 16), kBlock, 0, s>>>(0, m.counters + kCntNew, m.counters + kCntNodes, m.W, m.pl,
+                                                  m.pcr_add, m.pcr_fix, m.cov_add, m.eig, m.jour, m.pcrs);
+  k_ins_touch<<<g, kBlock, 0, s>>>(n, w.u0, epoch, m, w.leaf);
+  k_ins_descend<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.leaf, w.list2);
+  k_ins_alloc<<<1, 1024, 0, s>>>(thread_num, m, w.list2);
+  VG_TRY(tail());
   VG_TRY(read_counters(ctx));
-  *roots_new = ctx->h_pinned[kCntNodes] - first_new;
+  if (ctx->h_pinned[kCntMisc] && ctx->h_pinned[kCntTouched] >= thread_num) {
+    // more creation requests than k_ins_alloc holds: host-sized allocation,
+    // then the tail again
+    const int np = ctx->h_pinned[kCntCreate];
+    VG_HIP(hipMemsetAsync(m.counters + kCntMisc, 0, sizeof(int), s));
+    VG_HIP(hipMemsetAsync(m.counters + kCntSeg, 0, sizeof(int), s));
+    int created = 0;
+    VG_TRY(alloc_children(ctx, w.list2, np, nullptr, 0, false, &created));
+    VG_TRY(tail());
+    VG_TRY(read_counters(ctx));
+  }
+  *roots_new = ctx->h_pinned[kCntRoots];
   *touched = ctx->h_pinned[kCntTouched];
 #ifdef VG_PROBE
-  fprintf(stderr, "PROBE insert n=%d roots_new=%d touched=%d nodes=%d\n", n, *roots_new, *touched, ctx->h_pinned[kCntNodes]);
+  fprintf(stderr, "PROBE insert n=%d roots_new=%d touched=%d create=%d nodes=%d\n", n, *roots_new, *touched,
+          ctx->h_pinned[kCntCreate], ctx->h_pinned[kCntNodes]);
 #endif
-  if (*touched < thread_num) return VG_OK;  // voxel_map.cpp:96-97: no allocation at all
-  VG_HIP(hipMemsetAsync(m.counters + kCntCreate, 0, sizeof(int), s));
-  k_ins_descend<<<g, kBlock, 0, s>>>(n, w.pw, m, w.leaf, w.list2);
-  VG_TRY(read_counters(ctx));
-  int np = ctx->h_pinned[kCntCreate], created = 0;
-  if (np > 0) {
-    VG_TRY(alloc_children(ctx, w.list2, np, nullptr, 0, false, &created));
-    k_ins_resolve<<<g, kBlock, 0, s>>>(n, w.pw, m, w.leaf);
-  }
-  k_ins_keys<<<g, kBlock, 0, s>>>(n, w.leaf, w.k0);
-  VG_TRY(sort_keys(ctx, w.k0, w.k1, n, 27 + bits_for(ctx->h_pinned[kCntNodes])));
-  VG_HIP(hipMemsetAsync(m.counters + kCntSeg, 0, sizeof(int), s));
-  k_seg_heads<<<g, kBlock, 0, s>>>(n, w.k1, w.list1, m.counters + kCntSeg);
-  // ~one wave per leaf segment (the count stays on the device)
-  const int gseg = (n + kPushWaves - 1) / kPushWaves < 2048 ? (n + kPushWaves - 1) / kPushWaves : 2048;
-  k_push_window<<<gseg, 64 * kPushWaves, 0, s>>>(w.list1, m.counters + kCntSeg, n, w.k1, mp, slot, m, w.pw);
-  VG_HIP(hipGetLastError());
-  return read_counters(ctx);
+  return VG_OK;
 }
 
 // ------------------------------------------------------------------ recut (A5/A6)
@@ -759,44 +945,6 @@ __global__ void __launch_bounds__(256) k_rc_win(int L, int total, int cap_wp, co
   }
 }
 
-// zero a freshly allocated node's records (the pool is zeroed lazily)
-__device__ __forceinline__ void zero_node(DevMap& m, int id) {
-  PlaneRec& p = m.pl[id];
-  for (int j = 0; j < 27; j++) (&p.center[0])[j] = 0.0;
-  p.radius = 0;
-  p.pad = 0;
-  clu_zero(m.pcr_add[id]);
-  clu_zero(m.pcr_fix[id]);
-  for (int j = 0; j < kCovN; j++) m.cov_add[(size_t)id * kCovN + j] = 0.0;
-  for (int j = 0; j < 12; j++) m.eig[(size_t)id * 12 + j] = 0.0;
-  m.jour[id] = 0.0;
-  for (int j = 0; j < m.W; j++) clu_zero(m.pcrs[(size_t)id * m.W + j]);
-}
-
-// children of parent p in octant order, ids id0, id0+1, ...; appended to next
-__device__ __forceinline__ void alloc_parent(DevMap& m, int p, int id0, int* next, int next_pos, bool zero) {
-  NodeHdr& ph = m.hdr[p];
-  int k = 0;
-  for (int o = 0; o < 8; o++) {
-    if (m.cfirst[(size_t)p * 8 + o] != -5) continue;
-    const int id = id0 + k;
-    k++;
-    m.cfirst[(size_t)p * 8 + o] = 0x7f7f7f7f;
-    if (id >= m.cap_nodes) {
-      atomicOr(&m.counters[kCntErr], 4);
-      continue;
-    }
-    int xyz[3] = {(o >> 2) & 1, (o >> 1) & 1, o & 1};
-    double c[3];
-    for (int j = 0; j < 3; j++) c[j] = ph.center[j] + (float)((2 * xyz[j] - 1) * ph.qlen);
-    init_node(m.hdr[id], c, ph.qlen / 2, ph.layer + 1, p);
-    if (zero) zero_node(m, id);
-    ph.child[o] = id;
-    if (next) next[next_pos + k - 1] = id;
-  }
-  m.nscr[(size_t)p * 4 + 1] = -1;
-}
-
 __global__ void __launch_bounds__(256) k_child_alloc(int np, const int* __restrict__ parents, const uint32_t* __restrict__ off, DevMap m,
                               int* __restrict__ next, int next_base) {
   const int base = m.counters[kCntNodes];
@@ -885,53 +1033,6 @@ __device__ __forceinline__ void sub_finish(DevMap& m, int p) {
   h.fix_cap = 0;
   h.octo = 1;
   m.nscr[(size_t)p * 4 + 2] = -1;
-}
-
-// exclusive prefix over one value per thread of a 1024-lane workgroup
-__device__ __forceinline__ int block_excl_scan(int v, int* s_wsum, int* total) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    int y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
-  if (lane == 63) s_wsum[wv] = x;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int k = 0; k < (int)(blockDim.x >> 6); k++) {
-      int t = s_wsum[k];
-      s_wsum[k] = acc;
-      acc += t;
-    }
-    s_wsum[16] = acc;
-  }
-  __syncthreads();
-  const int r = s_wsum[wv] + x - v;
-  *total = s_wsum[16];
-  __syncthreads();
-  return r;
-}
-
-// ascending bitonic sort of n (power of two) keys in LDS by the whole workgroup
-template <typename T>
-__device__ void lds_bitonic(T* a, int n) {
-  for (int k = 2; k <= n; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int pj = i ^ j;
-        if (pj > i) {
-          const T x = a[i], y = a[pj];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) {
-            a[i] = y;
-            a[pj] = x;
-          }
-        }
-      }
-      __syncthreads();
-    }
 }
 
 __global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int ev_cap, MP mp, const WinD* __restrict__ win,

@@ -117,7 +117,7 @@ struct DevMap {
 };
 enum {
   kCntNodes = 0, kCntFix = 1, kCntSlide = 2, kCntNew = 3, kCntTouched = 4, kCntWork = 5, kCntNext = 6,
-  kCntSub = 7, kCntEvents = 8, kCntFactors = 9, kCntCreate = 10, kCntErr = 11, kCntLeaves = 12, kCntMisc = 13, kCntSeg = 14,
+  kCntSub = 7, kCntEvents = 8, kCntFactors = 9, kCntCreate = 10, kCntErr = 11, kCntLeaves = 12, kCntMisc = 13, kCntSeg = 14, kCntRoots = 15,
   kCntN = 16
 };
 
@@ -173,12 +173,18 @@ struct vg_ctx {
   vg::BaBufs ba;
   int* h_pinned = nullptr;  // small pinned host scratch for counters
   double* h_pinned_d = nullptr;
+  double* h_zc = nullptr;         // host-mapped zero-copy results (k_iekf): 64 doubles + flag
+  double* d_zc = nullptr;         // its device address
+  int zc_seq = 0;
+
   vg_stats stats;
   void* host = nullptr;     // host-side pipeline state (pipeline.cpp)
   // stage timing with HIP events on the context stream (vg_profile)
   bool prof_on = false;
   hipEvent_t prof_ev[8][2] = {};
   hipEvent_t sync_ev = nullptr;  // host-spin synchronisation (vg::stream_wait)
+  hipEvent_t iekf_ev[8][2] = {};  // k_iekf launches since the last full sync (vg_profile)
+  int iekf_ring_n = 0;
   int dbg_apply_cap = -1;        // test knob (vgx_debug): recut apply event capacity
   bool prof_pending[8] = {};
   double prof_ms[8] = {};
@@ -212,6 +218,14 @@ inline hipError_t stream_wait(vg_ctx* c) {
 }
 // call only after the stream has been synchronised past the recorded events
 inline void prof_collect(vg_ctx* c) {
+  for (int r = 0; r < c->iekf_ring_n; r++) {  // k_iekf launches (one event pair each)
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->iekf_ev[r][0], c->iekf_ev[r][1]) == hipSuccess) {
+      c->prof_ms[kProfIekfKernel] += ms;
+      c->prof_n[kProfIekfKernel] += 1;
+    }
+  }
+  c->iekf_ring_n = 0;
   for (int i = 0; i < kProfN; i++)
     if (c->prof_pending[i]) {
       float ms = 0;

@@ -84,10 +84,22 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
   }
   for (int i = 0; i < 8; i++)
     for (int j = 0; j < 2; j++)
+      if ((e = hipEventCreate(&ctx->iekf_ev[i][j])) != hipSuccess) {
+        ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
+        return fail(VG_E_HIP);
+      }
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 2; j++)
       if ((e = hipEventCreate(&ctx->prof_ev[i][j])) != hipSuccess) {
         ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
         return fail(VG_E_HIP);
       }
+  if ((e = hipHostMalloc((void**)&ctx->h_zc, 4096, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+      (e = hipHostGetDevicePointer((void**)&ctx->d_zc, ctx->h_zc, 0)) != hipSuccess) {
+    ctx->err = std::string("hipHostMalloc (mapped): ") + hipGetErrorString(e);
+    return fail(VG_E_HIP);
+  }
+  memset(ctx->h_zc, 0, 4096);
   if ((e = hipEventCreateWithFlags(&ctx->sync_ev, hipEventDisableTiming)) != hipSuccess) {
     ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
@@ -103,11 +115,15 @@ int vg_destroy(vg_ctx* ctx) {
   if (ctx->arena.base) (void)hipFree(ctx->arena.base);
   if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
   if (ctx->h_pinned_d) (void)hipHostFree(ctx->h_pinned_d);
+  if (ctx->h_zc) (void)hipHostFree(ctx->h_zc);
   if (ctx->host) host_free(ctx);
   for (int i = 0; i < 8; i++)
     for (int j = 0; j < 2; j++)
       if (ctx->prof_ev[i][j]) (void)hipEventDestroy(ctx->prof_ev[i][j]);
   if (ctx->sync_ev) (void)hipEventDestroy(ctx->sync_ev);
+  for (int i = 0; i < 8; i++)
+    for (int j = 0; j < 2; j++)
+      if (ctx->iekf_ev[i][j]) (void)hipEventDestroy(ctx->iekf_ev[i][j]);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return VG_OK;
