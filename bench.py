@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--cpu-scans", type=int, default=24, help="oracle sample: scans timed after its own warm-up")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seq", type=int, default=0)
+    ap.add_argument("--stage-scans", type=int, default=8, help="untimed profiled scans for the stage breakdown")
     return ap.parse_args()
 
 
@@ -63,12 +64,12 @@ def main():
                          ext_t=g["extrinsic_tran"])
     total = args.warmup + args.steps
     scans, imus = [], []
-    for k in range(total):
+    for k in range(total + args.stage_scans):
         xyz, inten, b, e = seq.scan(k)
         t = torch.from_numpy(np.ascontiguousarray(np.concatenate([xyz.T, inten[None]], 0))).to(dev)
         scans.append((t, xyz.shape[0], b, e))
         imus.append(seq.imu(k))
-    npts = int(np.mean([s[1] for s in scans]))
+    npts = int(np.mean([s[1] for s in scans[args.warmup:total]]))
     ctx = vgpu.Context(vgconfig.to_c(p), device=local, max_points=max(s[1] for s in scans) + 16)
     ctx.seed(seq.gt_state(0))
     torch.cuda.synchronize(dev)
@@ -94,11 +95,37 @@ def main():
     dt = time.perf_counter() - t0
     prof = ctx.profile_read()
     value, dt = aggregate(dt, args.steps, world, dev)
+    # per-stage breakdown: a separate, untimed profiled pass over further scans
+    # of the same sequence (stage events cost ~6 % of a step)
+    stage_ms = {}
+    extra = min(args.stage_scans, len(scans) - total)
+    if extra > 0:
+        ctx.profile(True, stages=True)
+        for k in range(total, total + extra):
+            run(k)
+        torch.cuda.synchronize(dev)
+        stage_ms = {k: round(v["ms"] / extra, 4) for k, v in ctx.profile_read().items()}
+        ctx.profile(False)
 
-    # roofline of the dominant kernel (IEKF point loop, k_iekf): algorithmic
-    # bytes per launch = 16 B per raw point (fp32 xyz + cached leaf id read)
-    # + 4 B per matched point (cached leaf write); plane/node records are
-    # cache-resident and not counted (lower bound)
+    # roofline of the dominant kernel by device time, k_ba_solve (the LM
+    # step's 15W x 15W LDL^T solve, one workgroup, fp64 MFMA trailing
+    # updates): algorithmic flops per launch = n^3/3 (LDL^T) + 2 n^2 (the two
+    # triangular solves), n = 15 * win_size; peak = MI355X fp64 matrix
+    # 78.6 TFLOP/s (AMD spec). Launch time: HIP events around each executed
+    # k_ba_solve on the context stream over the timed region.
+    W = p["LocalBA"]["win_size"]
+    n_sys = 15 * W
+    flops = n_sys ** 3 / 3.0 + 2.0 * n_sys ** 2
+    sol = prof["ba_solve"]
+    s_launch = sol["launches"]
+    s_avg = sol["ms"] * 1e-3 / max(s_launch, 1)
+    s_ach = flops / s_avg / 1e12 if s_avg > 0 else 0.0
+    roof = {"kernel": "k_ba_solve", "bound": "mfma", "achieved": round(s_ach, 5), "peak": 78.6, "unit": "TFLOP/s",
+            "frac": round(s_ach / 78.6, 7), "traffic": None, "avg_launch_us": round(s_avg * 1e6, 3),
+            "launches": s_launch, "flops_per_launch": int(flops), "stage_ms_per_scan": stage_ms}
+    # secondary: the IEKF point loop k_iekf (HBM-bound gather): 16 B per raw
+    # point (fp32 xyz + cached leaf id read) + 4 B per matched point (cached
+    # leaf write); plane/node records are cache-resident and not counted
     iek = prof["iekf"]
     n_launch = iek["launches"]
     pts = sum(s["n_raw"] * s["iekf_iters"] for s in stats)
@@ -106,9 +133,16 @@ def main():
     bytes_tot = 16.0 * pts + 4.0 * matched
     avg_s = iek["ms"] * 1e-3 / max(n_launch, 1)
     achieved = (bytes_tot / max(n_launch, 1)) / avg_s / 1e9 if avg_s > 0 else 0.0
-    roof = {"kernel": "k_iekf", "bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0, "unit": "GB/s",
-            "frac": round(achieved / 8000.0, 5), "traffic": None, "avg_launch_us": round(avg_s * 1e6, 3),
-            "launches": n_launch, "stage_ms_per_scan": {k: round(v["ms"] / args.steps, 4) for k, v in prof.items()}}
+    roof_iekf = {"kernel": "k_iekf", "bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0, "unit": "GB/s",
+                 "frac": round(achieved / 8000.0, 5), "traffic": None, "avg_launch_us": round(avg_s * 1e6, 3),
+                 "launches": n_launch}
+
+    pmc = pmc_traffic()
+    if "k_ba_solve" in pmc:
+        roof["traffic"] = pmc["k_ba_solve"]["traffic_bytes"]
+        roof["traffic_source"] = pmc["_file"]
+    if "k_iekf" in pmc:
+        roof_iekf["traffic"] = pmc["k_iekf"]["traffic_bytes"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -123,12 +157,25 @@ def main():
                        "points_per_scan": npts, "downsampled_per_scan": int(np.mean([s["n_ds"] for s in stats])),
                        "factors_per_scan": int(np.mean([s["n_factors"] for s in stats])),
                        "parallelism": "replica x%d" % world},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "roofline_k_iekf": roof_iekf, "cpu_baseline": cpu,
         }
         print(json.dumps(line))
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic():
+    """HBM bytes per launch from the newest committed PMC summary
+    (profiles/<round>/pmc_traffic.json, scripts/pmc_summary.py): rocprofv3
+    FETCH_SIZE (x2 on gfx950) + WRITE_SIZE, separate passes."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic.json")))
+    if not files:
+        return {}
+    d = json.load(open(files[-1]))["kernels"]
+    d["_file"] = os.path.relpath(files[-1], REPO)
+    return d
 
 
 def aggregate(dt, steps, world, dev):

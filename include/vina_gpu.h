@@ -143,8 +143,11 @@ int vg_trajectory(vg_ctx* ctx, double* out, int cap, int* n);
 
 /* Stage timing with HIP events on the context stream (device time). stage:
  * 0 downsample, 1 IEKF point-loop kernel (k_iekf), 2 map insert, 3 recut +
- * factor extraction, 4 BA, 5 margi, 6 whole IEKF. vg_profile resets the
- * accumulators; vg_profile_read returns total ms and the number of intervals. */
+ * factor extraction, 4 BA, 5 margi, 6 whole IEKF, 7 the LDL^T solve kernel
+ * (k_ba_solve). `on`: 0 off, 1 the k_iekf and k_ba_solve launches only
+ * (stages 1 and 7; cheap enough for a timed region), 3 every stage.
+ * vg_profile resets the accumulators; vg_profile_read returns total ms and the
+ * number of intervals. */
 int vg_profile(vg_ctx* ctx, int on);
 int vg_profile_read(vg_ctx* ctx, int stage, double* total_ms, int* count);
 

@@ -696,9 +696,10 @@ __global__ void __launch_bounds__(1024) k_ins_alloc(int thread_num, DevMap m, co
       for (int o = 0; o < 8; o++) cc += (m.cfirst[(size_t)p * 8 + o] == -5) ? 1 : 0;
     int tot;
     const int off = block_excl_scan(cc, s_w, &tot);
-    if (p >= 0) alloc_parent(m, p, base + carry + off, nullptr, 0, true);
+    if (p >= 0) alloc_parent(m, p, base + carry + off, nullptr, 0, false);
     carry += tot;
   }
+  for (int id = base + threadIdx.x; id < base + carry && id < m.cap_nodes; id += blockDim.x) zero_node(m, id);
   __syncthreads();
   if (threadIdx.x == 0) m.counters[kCntNodes] = base + carry;
 }
@@ -1101,7 +1102,8 @@ __global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int ev_cap, M
   const int base = m.counters[kCntNodes];
   const int nnext = rc[kRcLvl + L];
   __syncthreads();
-  if (p_t >= 0) alloc_parent(m, p_t, base + coff, next, nnext + coff, true);
+  if (p_t >= 0) alloc_parent(m, p_t, base + coff, next, nnext + coff, false);
+  for (int id = base + tid; id < base + ntot && id < m.cap_nodes; id += blockDim.x) zero_node(m, id);
   __syncthreads();
   if (tid == 0) {
     m.counters[kCntNodes] = base + ntot;

@@ -180,11 +180,13 @@ struct vg_ctx {
   vg_stats stats;
   void* host = nullptr;     // host-side pipeline state (pipeline.cpp)
   // stage timing with HIP events on the context stream (vg_profile)
-  bool prof_on = false;
+  bool prof_on = false;      // k_iekf launch events (vg_profile bit 0)
+  bool prof_stages = false;  // per-stage events (vg_profile bit 1)
   hipEvent_t prof_ev[8][2] = {};
   hipEvent_t sync_ev = nullptr;  // host-spin synchronisation (vg::stream_wait)
   hipEvent_t iekf_ev[8][2] = {};  // k_iekf launches since the last full sync (vg_profile)
   int iekf_ring_n = 0;
+  hipEvent_t solve_ev[10][2] = {};  // k_ba_solve launches of the current BA run (vg_profile)
   int dbg_apply_cap = -1;        // test knob (vgx_debug): recut apply event capacity
   bool prof_pending[8] = {};
   double prof_ms[8] = {};
@@ -193,12 +195,12 @@ struct vg_ctx {
 
 namespace vg {
 enum { kProfDownsample = 0, kProfIekfKernel = 1, kProfInsert = 2, kProfRecut = 3, kProfBA = 4, kProfMargi = 5,
-       kProfIekf = 6, kProfN = 7 };
+       kProfIekf = 6, kProfBaSolve = 7, kProfN = 8 };
 inline void prof_begin(vg_ctx* c, int id) {
-  if (c->prof_on) (void)hipEventRecord(c->prof_ev[id][0], c->stream);
+  if (c->prof_stages) (void)hipEventRecord(c->prof_ev[id][0], c->stream);
 }
 inline void prof_end(vg_ctx* c, int id) {
-  if (c->prof_on) {
+  if (c->prof_stages) {
     (void)hipEventRecord(c->prof_ev[id][1], c->stream);
     c->prof_pending[id] = true;
   }

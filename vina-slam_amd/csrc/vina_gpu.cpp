@@ -82,6 +82,12 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     ctx->err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
+  for (int i = 0; i < 10; i++)
+    for (int j = 0; j < 2; j++)
+      if ((e = hipEventCreate(&ctx->solve_ev[i][j])) != hipSuccess) {
+        ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
+        return fail(VG_E_HIP);
+      }
   for (int i = 0; i < 8; i++)
     for (int j = 0; j < 2; j++)
       if ((e = hipEventCreate(&ctx->iekf_ev[i][j])) != hipSuccess) {
@@ -124,6 +130,9 @@ int vg_destroy(vg_ctx* ctx) {
   for (int i = 0; i < 8; i++)
     for (int j = 0; j < 2; j++)
       if (ctx->iekf_ev[i][j]) (void)hipEventDestroy(ctx->iekf_ev[i][j]);
+  for (int i = 0; i < 10; i++)
+    for (int j = 0; j < 2; j++)
+      if (ctx->solve_ev[i][j]) (void)hipEventDestroy(ctx->solve_ev[i][j]);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return VG_OK;
@@ -339,7 +348,9 @@ int vg_win_count(vg_ctx* ctx, int* n) {
 
 int vg_profile(vg_ctx* ctx, int on) {
   if (!ctx) return VG_E_ARG;
-  ctx->prof_on = on != 0;
+  ctx->prof_on = (on & 1) != 0;
+  ctx->prof_stages = (on & 2) != 0;
+  ctx->iekf_ring_n = 0;
   for (int i = 0; i < 8; i++) {
     ctx->prof_ms[i] = 0;
     ctx->prof_n[i] = 0;

@@ -218,10 +218,11 @@ class Context:
     def win_count(self):
         return self._int_call(lib().vg_win_count, "vg_win_count")
 
-    PROFILE_STAGES = ["downsample", "iekf", "insert", "recut", "ba", "margi", "iekf_total"]
+    PROFILE_STAGES = ["downsample", "iekf", "insert", "recut", "ba", "margi", "iekf_total", "ba_solve"]
 
-    def profile(self, on=True):
-        self._chk(lib().vg_profile(self.h, 1 if on else 0), "vg_profile")
+    def profile(self, on=True, stages=False):
+        """on: k_iekf launch events; stages: per-stage events as well."""
+        self._chk(lib().vg_profile(self.h, (1 if on else 0) | (2 if stages else 0)), "vg_profile")
 
     def profile_read(self):
         out = {}
