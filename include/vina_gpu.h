@@ -101,8 +101,14 @@ int vg_step(vg_ctx* ctx, const float* xyz, const float* intensity, int n, double
 /* Same, with the scan already in HBM as SoA x/y/z/intensity device arrays. */
 int vg_step_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, const float* d_intensity, int n,
                 double pcl_beg_time, double pcl_end_time, const double* imu, int m);
+/* vg_step / vg_step_dev return once the scan is ENQUEUED: the device runs it
+ * asynchronously (the host waits only for device-side counts it needs, without
+ * draining the stream). Every query below completes the outstanding work first. */
 int vg_get_state(vg_ctx* ctx, double* state);
 int vg_get_stats(vg_ctx* ctx, vg_stats* out);
+/* Per-scan counters of every completed scan since vg_create / vg_reset, in
+ * order: copies min(n, cap) records, *n = total (out may be NULL to query). */
+int vg_stats_log(vg_ctx* ctx, vg_stats* out, int cap, int* n);
 /* Window states x_buf (win_count x 250 doubles); returns win_count via *n. */
 int vg_window_states(vg_ctx* ctx, double* out, int* n);
 

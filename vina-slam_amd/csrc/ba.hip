@@ -820,7 +820,8 @@ __global__ void __launch_bounds__(256) k_ba_resid(int nf, int W, const int* __re
 __global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, double imu_coef, const double* __restrict__ hl, int nl,
                              const double* __restrict__ imuout, const double* __restrict__ imures,
                              const double* __restrict__ rpart, double* __restrict__ xs,
-                             const double* __restrict__ xt, double* __restrict__ bias, BaState* __restrict__ st) {
+                             const double* __restrict__ xt, double* __restrict__ bias, BaState* __restrict__ st,
+                             Pub* __restrict__ pub, int seq) {
   __shared__ int accept;
   if (threadIdx.x == 0) {
     accept = -1;
@@ -867,6 +868,12 @@ __global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, do
       int k = t / 6, j = t % 6;
       bias[k * 12 + j] = bias[k * 12 + 6 + j];
     }
+  }
+  if (threadIdx.x == 0) {  // LM flags -> host (read without draining the stream)
+    __hip_atomic_store(&pub->ba_done, st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&pub->ba_iters, st->iters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __hip_atomic_store(&pub->seq_ba, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -965,13 +972,13 @@ static BaDev carve(vg_ctx* ctx) {
   p += n;
   d.dxi = p;
   p += n;
-  d.xs = p;
+  d.xs = ctx->st->xs;  // window states live in the device state (state.hip)
   p += kMaxW * kX;
   d.xt = p;
   p += kMaxW * kX;
   d.imurec = p;
   p += kMaxW * kImuRec;
-  d.bias = p;
+  d.bias = ctx->st->bias;
   p += kMaxW * 12;
   d.imuout = p;
   p += kMaxW * 931;
@@ -987,10 +994,12 @@ static BaDev carve(vg_ctx* ctx) {
   return d;
 }
 
-// Run damping_iter on the device. xs_io: W x 24 doubles (R,p,v,bg,ba,g), in/out.
-// imurec: (W-1) x kImuRec host records; bias_io: (W-1) x 12 (dbg, dba, bufs), in/out.
-int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double* imurec, double* bias_io,
-           int* iters) {
+const int* ba_iters_dev(vg_ctx* ctx) { return &carve(ctx).st->iters; }
+
+// Run damping_iter on the device state. imurec: (W-1) x kImuRec host records
+// (pinned staging, uploaded asynchronously). The window states and the IMU
+// bias records are read and written in DState.
+int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* iters) {
   const int W = ctx->cfg.win_size;
   if (15 * W > kMaxNB * kTile) {
     ctx->err = "win_size > 11 unsupported by the BA solve (LDS-resident 15W x 15W tile store)";
@@ -1000,10 +1009,13 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double*
   BaDev d = carve(ctx);
   const int nimu = W - 1;
   const int L = 6 * W, nl = L * (L + 1) / 2, nout = nl + L + 1;
-  VG_HIP(hipMemcpyAsync(d.xs, xs_io, (size_t)W * kX * sizeof(double), hipMemcpyHostToDevice, s));
-  VG_HIP(hipMemcpyAsync(d.imurec, imurec, (size_t)nimu * kImuRec * sizeof(double), hipMemcpyHostToDevice, s));
-  VG_HIP(hipMemcpyAsync(d.bias, bias_io, (size_t)nimu * 12 * sizeof(double), hipMemcpyHostToDevice, s));
-  VG_HIP(hipMemcpyAsync(d.mpring, mp_ring, W * sizeof(int), hipMemcpyHostToDevice, s));
+  // one H2D copy of the host-side inputs: IMU records, then the mp ring
+  double* stage = ctx->h_stage;
+  memcpy(stage, imurec, (size_t)nimu * kImuRec * sizeof(double));
+  memcpy(stage + (size_t)kMaxW * kImuRec, mp_ring, W * sizeof(int));
+  static_assert((size_t)kMaxW * kImuRec * sizeof(double) + 64 <= kStageBytes, "staging block too small");
+  VG_HIP(hipMemcpyAsync(d.imurec, stage, (size_t)nimu * kImuRec * sizeof(double), hipMemcpyHostToDevice, s));
+  VG_HIP(hipMemcpyAsync(d.mpring, stage + (size_t)kMaxW * kImuRec, W * sizeof(int), hipMemcpyHostToDevice, s));
   VG_HIP(hipMemsetAsync(d.hl, 0, nout * sizeof(double), s));
   k_ba_init<<<1, 1, 0, s>>>(d.st);
   const int nchunk = (nf + hess_chunk(W) - 1) / hess_chunk(W);
@@ -1011,10 +1023,11 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double*
   const size_t hess_lds = hess_lds_bytes(W);
   const size_t solve_lds = solve_lds_bytes(W);
   const int NBt = (15 * W + kTile - 1) / kTile, ntile = NBt * (NBt + 1) / 2;
+  const int seq0 = ctx->pub_seq + 1;
+  ctx->pub_seq += 10;
   // one LM iteration (optimizers.cpp:449-516); kernels early-exit on the
   // device-side flags once converged
-  int enq = 0;  // iterations enqueued so far (the lambda reads it)
-  auto iteration = [&]() {
+  auto iteration = [&](int k) {
     if (nf > 0 || nimu > 0)
       k_ba_hess<<<(nf > 0 ? nchunk : 0) + nimu, kHessThreads, hess_lds, s>>>(
           nf, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr, ctx->map.pcrs, d.mpring, d.xs, d.part, d.st,
@@ -1022,37 +1035,32 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double*
     if (nf > 0) k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nchunk, nout, d.part, d.hl, d.st);
     k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
                                     d.dvec, d.jvec, d.ipg, d.st);
-    if (ctx->prof_on && enq < 10) (void)hipEventRecord(ctx->solve_ev[enq][0], s);
+    if (ctx->prof_on) (void)hipEventRecord(ctx->solve_ev[k][0], s);
     k_ba_solve<<<1, 512, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
                                          d.st);
-    if (ctx->prof_on && enq < 10) (void)hipEventRecord(ctx->solve_ev[enq][1], s);
+    if (ctx->prof_on) (void)hipEventRecord(ctx->solve_ev[k][1], s);
     if (nf > 0 || nimu > 0)
       k_ba_resid<<<(nf > 0 ? nrb : 0) + (nimu > 0 ? 1 : 0), 256, 0, s>>>(
           nf, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt, ctx->ba.fac_eig, ctx->ba.fac_pcr,
           d.rpart, d.st, nf > 0 ? nrb : 0, nimu, d.imurec, d.bias, d.imures);
     k_ba_control<<<1, 256, 0, s>>>(W, nimu, nf > 0 ? nrb : 0, ctx->cfg.imu_coef, d.hl, nl + L, d.imuout, d.imures,
-                                   d.rpart, d.xs, d.xt, d.bias, d.st);
+                                   d.rpart, d.xs, d.xt, d.bias, d.st, ctx->d_pub, seq0 + k);
   };
-  // iterations are enqueued two at a time with a flag check in between: an
-  // early-exited iteration still costs ~7 launches, and the LM usually
-  // converges in 2-3 (optimizers.cpp:449, at most 10)
-  BaState* hflag = reinterpret_cast<BaState*>(ctx->h_pinned_d + 256);
-  while (enq < 10) {
-    for (int g = 0; g < 2 && enq < 10; g++, enq++) iteration();
-    if (enq >= 10) break;
-    VG_HIP(hipMemcpyAsync(hflag, d.st, sizeof(BaState), hipMemcpyDeviceToHost, s));
-    VG_HIP(stream_wait(ctx));
-    if (hflag->done) break;
+  // One iteration ahead: iteration k+1 is enqueued before the host waits for
+  // iteration k's flags, so the stream never drains; a converged LM leaves at
+  // most one early-exiting iteration behind (optimizers.cpp:449, at most 10).
+  iteration(0);
+  int done_iters = 0;
+  for (int k = 0; k < 10; k++) {
+    if (k + 1 < 10) iteration(k + 1);
+    VG_HIP(hipGetLastError());
+    VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ba, seq0 + k, "k_ba_control"));
+    done_iters = __atomic_load_n(&ctx->h_pub->ba_iters, __ATOMIC_ACQUIRE);
+    if (__atomic_load_n(&ctx->h_pub->ba_done, __ATOMIC_ACQUIRE)) break;
   }
-  VG_HIP(hipGetLastError());
-  BaState hs;
-  VG_HIP(hipMemcpyAsync(xs_io, d.xs, (size_t)W * kX * sizeof(double), hipMemcpyDeviceToHost, s));
-  VG_HIP(hipMemcpyAsync(bias_io, d.bias, (size_t)nimu * 12 * sizeof(double), hipMemcpyDeviceToHost, s));
-  VG_HIP(hipMemcpyAsync(&hs, d.st, sizeof(BaState), hipMemcpyDeviceToHost, s));
-  VG_HIP(stream_wait(ctx));
-  *iters = hs.iters;
+  *iters = done_iters;
   if (ctx->prof_on)  // k_ba_solve of the executed iterations only (the bench's roofline)
-    for (int it = 0; it < hs.iters && it < 10; it++) {
+    for (int it = 0; it < done_iters && it < 10; it++) {
       float ms = 0;
       if (hipEventElapsedTime(&ms, ctx->solve_ev[it][0], ctx->solve_ev[it][1]) == hipSuccess) {
         ctx->prof_ms[kProfBaSolve] += ms;

@@ -116,6 +116,31 @@ int ds_alloc(vg_ctx* ctx) {
   return VG_OK;
 }
 
+int ds_enqueue(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, int n, double voxel,
+               int pub_seq) {
+  DownsampleBufs& d = ctx->ds;
+  hipStream_t s = ctx->stream;
+  if (n > ctx->cap.max_points_per_scan) {
+    ctx->err = "scan larger than max_points_per_scan";
+    return VG_E_CAPACITY;
+  }
+  VG_HIP(hipMemsetAsync(d.flags, 0, 4 * sizeof(int), s));
+  if (n > 0) {
+    k_ds_keys<<<grid_for(n), kBlock, 0, s>>>(n, x, y, z, voxel, d.keys, d.idx, d.flags);
+    size_t tb = d.tmp_bytes;
+    VG_HIP(hipcub::DeviceRadixSort::SortPairs(d.tmp, tb, d.keys, d.keys_sorted, d.idx, d.idx_sorted, n, 0, 63, s));
+    k_ds_heads<<<grid_for(n), kBlock, 0, s>>>(n, d.keys_sorted, d.head);
+    tb = d.tmp_bytes;
+    VG_HIP(hipcub::DeviceScan::ExclusiveSum(d.tmp, tb, d.head, d.pos, n, s));
+    k_ds_segs<<<grid_for(n), kBlock, 0, s>>>(n, d.head, d.pos, d.seg, d.flags);
+    k_ds_mean<<<grid_for(n), kBlock, 0, s>>>(d.flags, d.seg, d.idx_sorted, x, y, z, in, d.ox, d.oy, d.oz, d.oi,
+                                             d.oc);
+  }
+  if (pub_seq > 0) VG_TRY(state_publish_ds(ctx, pub_seq));
+  VG_HIP(hipGetLastError());
+  return VG_OK;
+}
+
 int ds_run(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, int n, double voxel,
            int* n_out) {
   DownsampleBufs& d = ctx->ds;
@@ -124,21 +149,7 @@ int ds_run(vg_ctx* ctx, const float* x, const float* y, const float* z, const fl
     *n_out = 0;
     return VG_OK;
   }
-  if (n > ctx->cap.max_points_per_scan) {
-    ctx->err = "scan larger than max_points_per_scan";
-    return VG_E_CAPACITY;
-  }
-  VG_HIP(hipMemsetAsync(d.flags, 0, 4 * sizeof(int), s));
-  k_ds_keys<<<grid_for(n), kBlock, 0, s>>>(n, x, y, z, voxel, d.keys, d.idx, d.flags);
-  size_t tb = d.tmp_bytes;
-  VG_HIP(hipcub::DeviceRadixSort::SortPairs(d.tmp, tb, d.keys, d.keys_sorted, d.idx, d.idx_sorted, n, 0, 63, s));
-  k_ds_heads<<<grid_for(n), kBlock, 0, s>>>(n, d.keys_sorted, d.head);
-  tb = d.tmp_bytes;
-  VG_HIP(hipcub::DeviceScan::ExclusiveSum(d.tmp, tb, d.head, d.pos, n, s));
-  k_ds_segs<<<grid_for(n), kBlock, 0, s>>>(n, d.head, d.pos, d.seg, d.flags);
-  k_ds_mean<<<grid_for(n), kBlock, 0, s>>>(d.flags, d.seg, d.idx_sorted, x, y, z, in, d.ox, d.oy, d.oz, d.oi,
-                                           d.oc);
-  VG_HIP(hipGetLastError());
+  VG_TRY(ds_enqueue(ctx, x, y, z, in, n, voxel, 0));
   VG_HIP(hipMemcpyAsync(ctx->h_pinned, d.flags, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
   VG_HIP(stream_wait(ctx));
   if (ctx->h_pinned[0]) {

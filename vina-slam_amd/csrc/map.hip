@@ -183,13 +183,26 @@ __device__ __forceinline__ bool inside(const NodeHdr& h, const V3& w) {
 
 constexpr int kIekfVals = 34;
 
+// The pose (x_curr R, p and the rotation / translation covariance blocks) is
+// read from the device state the previous k_iekf_update wrote; the kernel is a
+// no-op once the IEKF has finished (st->done). Iteration 0 ignores the leaf
+// cache (no association yet, odometry.cpp:111-132).
 __global__ void __launch_bounds__(256) k_iekf(int n, const float* __restrict__ x, const float* __restrict__ y,
-                                              const float* __restrict__ z, MP mp, IekfPose ps, DevMap m,
-                                              int* __restrict__ cache, double* __restrict__ partials) {
+                                              const float* __restrict__ z, MP mp, const DState* __restrict__ st,
+                                              int it, DevMap m, int* __restrict__ cache,
+                                              double* __restrict__ partials) {
+  if (st->done) return;
   double acc[kIekfVals];
   for (int j = 0; j < kIekfVals; j++) acc[j] = 0.0;
-  const M3 R = ld_m3(ps.R), rot_var = ld_m3(ps.rot_var), tsl_var = ld_m3(ps.tsl_var);
-  const V3 p = ld_v3(ps.p);
+  const double* xc = st->xc;
+  M3 R, rot_var, tsl_var;
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) {
+      R(r, c) = xc[r * 3 + c];
+      rot_var(r, c) = xc[kXS + r * 15 + c];
+      tsl_var(r, c) = xc[kXS + (3 + r) * 15 + 3 + c];
+    }
+  const V3 p = ld_v3(xc + 9);
   const M3 Rt = tr(R);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     V3 pnt;
@@ -197,7 +210,7 @@ __global__ void __launch_bounds__(256) k_iekf(int n, const float* __restrict__ x
     var_init_pt(mp, x[i], y[i], z[i], pnt, var);
     M3 var_world = world_var(R, var, pnt, rot_var, tsl_var);
     V3 wld = rigid(R, pnt, p);
-    int leaf = cache[i];
+    int leaf = it > 0 ? cache[i] : -1;
     int flag = 0;
     double sigma = 0;
     if (leaf >= 0 && inside(m.hdr[leaf], wld)) {
@@ -213,6 +226,7 @@ __global__ void __launch_bounds__(256) k_iekf(int n, const float* __restrict__ x
         }
       }
     }
+    if (!flag && it == 0) cache[i] = -1;  // the reference's fresh per-scan association
     if (flag) {
       cache[i] = leaf;
       const PlaneRec& P = m.pl[leaf];
@@ -251,66 +265,15 @@ __global__ void __launch_bounds__(256) k_iekf(int n, const float* __restrict__ x
   }
 }
 
-// ordered two-level sum of the block partials: lane t sums rows t, t+256, ...
-// for all 34 values, then a fixed LDS tree (deterministic)
-__global__ void __launch_bounds__(256) k_iekf_final(int nb, const double* __restrict__ partials,
-                                                    double* __restrict__ zc_out, int* __restrict__ zc_flag, int seq) {
-  __shared__ double red[256][kIekfVals + 1];
-  double acc[kIekfVals];
-  for (int j = 0; j < kIekfVals; j++) acc[j] = 0.0;
-  for (int b = threadIdx.x; b < nb; b += 256)
-    for (int j = 0; j < kIekfVals; j++) acc[j] += partials[(size_t)b * kIekfVals + j];
-  for (int j = 0; j < kIekfVals; j++) red[threadIdx.x][j] = acc[j];
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (threadIdx.x < w)
-      for (int j = 0; j < kIekfVals; j++) red[threadIdx.x][j] += red[threadIdx.x + w][j];
-    __syncthreads();
-  }
-  // publish to host-mapped memory with a sequence flag (the host spins on it:
-  // no copy, no event)
-  if (threadIdx.x < kIekfVals)
-    __hip_atomic_store(&zc_out[threadIdx.x], red[0][threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(zc_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-int iekf_reset_cache(vg_ctx* ctx, int n) {
-  VG_HIP(hipMemsetAsync(ctx->wk.iekf_cache, 0xff, (size_t)n * sizeof(int), ctx->stream));
-  return VG_OK;
-}
-
-int iekf_iter(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n,
-              const IekfPose& pose, double* out34) {
+// one IEKF point loop (iteration `it`) -> block partials for k_iekf_update
+int iekf_point_loop(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
+                    int* nb_out) {
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
-  int nb = grid_for(n, 256, 512);
-  const int seq = ++ctx->zc_seq;
-  const int ring = ctx->prof_on && ctx->iekf_ring_n < 8 ? ctx->iekf_ring_n++ : -1;
-  if (ring >= 0) (void)hipEventRecord(ctx->iekf_ev[ring][0], s);
-  k_iekf<<<nb, 256, 0, s>>>(n, x, y, z, mp, pose, ctx->map, w.iekf_cache, w.partials);
-  if (ring >= 0) (void)hipEventRecord(ctx->iekf_ev[ring][1], s);
-  k_iekf_final<<<1, 256, 0, s>>>(nb, w.partials, ctx->d_zc, reinterpret_cast<int*>(ctx->d_zc + 64), seq);
+  const int nb = grid_for(n, 256, 512);
+  k_iekf<<<nb, 256, 0, s>>>(n, x, y, z, mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials);
   VG_HIP(hipGetLastError());
-  // spin on the sequence flag the last block publishes (host-mapped memory)
-  const int* flag = reinterpret_cast<const int*>(ctx->h_zc + 64);
-  for (long spin = 0; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; spin++) {
-#if defined(__x86_64__)
-    __builtin_ia32_pause();
-#endif
-    if ((spin & 4095) == 4095) {
-      const hipError_t e = hipStreamQuery(s);
-      if (e != hipSuccess && e != hipErrorNotReady) {
-        ctx->err = std::string("k_iekf: ") + hipGetErrorString(e);
-        return VG_E_HIP;
-      }
-      if (e == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
-        ctx->err = "k_iekf finished without publishing its sums";
-        return VG_E_HIP;
-      }
-    }
-  }
-  for (int j = 0; j < kIekfVals; j++) out34[j] = ctx->h_zc[j];
+  *nb_out = nb;
   return VG_OK;
 }
 
@@ -318,10 +281,18 @@ int iekf_iter(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const f
 // per downsampled point: var_init + pvec_update (world var), world point, root
 // key insert-or-find, first-occurrence marking of brand-new keys
 __global__ void __launch_bounds__(256) k_ins_prep(int n, const float* __restrict__ ox, const float* __restrict__ oy,
-                           const float* __restrict__ oz, MP mp, InsPose ps, int slot, DevMap m,
-                           double* __restrict__ pw, uint32_t* __restrict__ hslot) {
-  const M3 R = ld_m3(ps.R), rot_var = ld_m3(ps.rot_var), tsl_var = ld_m3(ps.tsl_var);
-  const V3 p = ld_v3(ps.p);
+                           const float* __restrict__ oz, MP mp, const DState* __restrict__ st, int slot,
+                           DevMap m, double* __restrict__ pw, uint32_t* __restrict__ hslot) {
+  // pose of x_buf[ord] = x_curr after the IEKF (device state)
+  const double* xc = st->xc;
+  M3 R, rot_var, tsl_var;
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++) {
+      R(r, c) = xc[r * 3 + c];
+      rot_var(r, c) = xc[kXS + r * 15 + c];
+      tsl_var(r, c) = xc[kXS + (3 + r) * 15 + 3 + c];
+    }
+  const V3 p = ld_v3(xc + 9);
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // per-insert device counters (read by the later kernels)
     m.counters[kCntNew] = m.counters[kCntNodes];  // first id of this scan's new roots
     m.counters[kCntTouched] = 0;
@@ -777,31 +748,36 @@ static int alloc_children(vg_ctx* ctx, int* plist, int np, int* next, int next_b
   return VG_OK;
 }
 
-// cut_voxel_multi (voxel_map.cpp:47-135) + pvec_update (point_utils.cpp:54-65)
-int map_insert(vg_ctx* ctx, const MP& mp, int slot, const InsPose& pose, int n, int epoch, int thread_num,
-               int* roots_new, int* touched) {
+// leaves -> sorted (leaf, order) keys -> pushes of one insert
+static int insert_tail(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
-  *roots_new = 0;
-  *touched = 0;
-  if (n <= 0) return VG_OK;
-  // every count stays on the device; one synchronisation at the end
   const int g = grid_for(n);
   const int key_bits = 27 + bits_for(m.cap_nodes);
   const int gseg = (n + kPushWaves - 1) / kPushWaves < 2048 ? (n + kPushWaves - 1) / kPushWaves : 2048;
-  auto tail = [&]() -> int {  // leaves -> sorted (leaf, order) keys -> pushes
-    k_ins_resolve<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.leaf);
-    k_ins_keys<<<g, kBlock, 0, s>>>(n, thread_num, m, w.leaf, w.k0);
-    VG_TRY(sort_keys(ctx, w.k0, w.k1, n, key_bits));
-    k_seg_heads<<<g, kBlock, 0, s>>>(n, thread_num, m, w.k1, w.list1, m.counters + kCntSeg);
-    // ~one wave per leaf segment (the count stays on the device)
-    k_push_window<<<gseg, 64 * kPushWaves, 0, s>>>(w.list1, m.counters + kCntSeg, n, w.k1, mp, slot, m, w.pw,
-                                                  thread_num);
-    VG_HIP(hipGetLastError());
-    return VG_OK;
-  };
-  k_ins_prep<<<g, kBlock, 0, s>>>(n, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, mp, pose, slot, m, w.pw, w.u0);
+  k_ins_resolve<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.leaf);
+  k_ins_keys<<<g, kBlock, 0, s>>>(n, thread_num, m, w.leaf, w.k0);
+  VG_TRY(sort_keys(ctx, w.k0, w.k1, n, key_bits));
+  k_seg_heads<<<g, kBlock, 0, s>>>(n, thread_num, m, w.k1, w.list1, m.counters + kCntSeg);
+  // ~one wave per leaf segment (the count stays on the device)
+  k_push_window<<<gseg, 64 * kPushWaves, 0, s>>>(w.list1, m.counters + kCntSeg, n, w.k1, mp, slot, m, w.pw,
+                                                thread_num);
+  VG_HIP(hipGetLastError());
+  return VG_OK;
+}
+
+// cut_voxel_multi (voxel_map.cpp:47-135) + pvec_update (point_utils.cpp:54-65).
+// Asynchronous: every count stays on the device. A child-allocation overflow
+// of k_ins_alloc sets kCntMisc; the insert tail and the recut kernels then skip
+// and map_recut reports it (kNeedInsertReplay) for map_insert_replay.
+int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num) {
+  DevMap& m = ctx->map;
+  Work& w = ctx->wk;
+  hipStream_t s = ctx->stream;
+  if (n <= 0) return VG_OK;
+  const int g = grid_for(n);
+  k_ins_prep<<<g, kBlock, 0, s>>>(n, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, mp, ctx->st, slot, m, w.pw, w.u0);
   k_ins_newflag<<<g, kBlock, 0, s>>>(n, w.u0, m.hval, m.hfirst, w.v0);
   VG_TRY(excl_scan(ctx, w.v0, w.v1, n));
   k_ins_newalloc<<<g, kBlock, 0, s>>>(n, w.u0, w.v0, w.v1, mp, m);
@@ -811,26 +787,20 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, const InsPose& pose, int n, 
   k_ins_touch<<<g, kBlock, 0, s>>>(n, w.u0, epoch, m, w.leaf);
   k_ins_descend<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.leaf, w.list2);
   k_ins_alloc<<<1, 1024, 0, s>>>(thread_num, m, w.list2);
-  VG_TRY(tail());
+  return insert_tail(ctx, mp, slot, n, thread_num);
+}
+
+// host-sized child allocation after a k_ins_alloc overflow, then the tail
+int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num) {
+  DevMap& m = ctx->map;
+  hipStream_t s = ctx->stream;
   VG_TRY(read_counters(ctx));
-  if (ctx->h_pinned[kCntMisc] && ctx->h_pinned[kCntTouched] >= thread_num) {
-    // more creation requests than k_ins_alloc holds: host-sized allocation,
-    // then the tail again
-    const int np = ctx->h_pinned[kCntCreate];
-    VG_HIP(hipMemsetAsync(m.counters + kCntMisc, 0, sizeof(int), s));
-    VG_HIP(hipMemsetAsync(m.counters + kCntSeg, 0, sizeof(int), s));
-    int created = 0;
-    VG_TRY(alloc_children(ctx, w.list2, np, nullptr, 0, false, &created));
-    VG_TRY(tail());
-    VG_TRY(read_counters(ctx));
-  }
-  *roots_new = ctx->h_pinned[kCntRoots];
-  *touched = ctx->h_pinned[kCntTouched];
-#ifdef VG_PROBE
-  fprintf(stderr, "PROBE insert n=%d roots_new=%d touched=%d create=%d nodes=%d\n", n, *roots_new, *touched,
-          ctx->h_pinned[kCntCreate], ctx->h_pinned[kCntNodes]);
-#endif
-  return VG_OK;
+  const int np = ctx->h_pinned[kCntCreate];
+  VG_HIP(hipMemsetAsync(m.counters + kCntMisc, 0, sizeof(int), s));
+  VG_HIP(hipMemsetAsync(m.counters + kCntSeg, 0, sizeof(int), s));
+  int created = 0;
+  VG_TRY(alloc_children(ctx, ctx->wk.list2, np, nullptr, 0, false, &created));
+  return insert_tail(ctx, mp, slot, n, thread_num);
 }
 
 // ------------------------------------------------------------------ recut (A5/A6)
@@ -1399,27 +1369,36 @@ static int recut_slow_apply(vg_ctx* ctx, int L, const MP& mp, WinD* dwin, int* n
   return read_counters(ctx);
 }
 
-// multi_recut (local_mapping.cpp:144-201) then tras_opt. Returns the factor count.
-int map_recut(vg_ctx* ctx, const MP& mp, const WinD& win, const int* nper, int thread_num, int* n_factors) {
+// recut start: zero the level counts and the factor count; an insert whose
+// child allocation overflowed (kCntMisc) blocks the whole recut (rc abort code
+// kInsAbort) until map_insert_replay has run
+constexpr int kInsAbort = 100;
+__global__ void k_recut_begin(DevMap m, int* __restrict__ rc, int thread_num) {
+  const int t = threadIdx.x;
+  for (int i = t; i < kRcN; i += blockDim.x) rc[i] = 0;
+  __syncthreads();
+  if (t == 0) {
+    m.counters[kCntFactors] = 0;
+    if (m.counters[kCntMisc] != 0 && m.counters[kCntTouched] >= thread_num) rc[kRcAbort] = kInsAbort;
+  }
+}
+
+// multi_recut (local_mapping.cpp:144-201) then tras_opt. Returns the factor
+// count, or kNeedInsertReplay when the preceding insert must be replayed first
+// (nothing of the recut ran).
+int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
   *n_factors = 0;
-  // upload the window (poses, ring) and per-ord point counts
+  // the window view (poses from the device state, ring, per-ord counts)
   WinD* dwin = (WinD*)ctx->ba.xs;
   int* dn = (int*)((char*)ctx->ba.xs + sizeof(WinD));
   int* dslot = dn + 32;
-  int hn[64];
-  for (int i = 0; i < 32; i++) {
-    hn[i] = i < win.win_count ? nper[i] : 0;
-    hn[32 + i] = win.mp[i];
-  }
-  VG_HIP(hipMemcpyAsync(dwin, &win, sizeof(WinD), hipMemcpyHostToDevice, s));
-  VG_HIP(hipMemcpyAsync(dn, hn, sizeof(hn), hipMemcpyHostToDevice, s));
+  VG_TRY(state_make_win(ctx, wa, dwin, dn, dslot));
   int total = 0;
-  for (int i = 0; i < win.win_count; i++) total += nper[i];
-  VG_HIP(hipMemsetAsync(w.rc, 0, kRcN * sizeof(int), s));
-  VG_HIP(hipMemsetAsync(m.counters + kCntFactors, 0, sizeof(int), s));
+  for (int i = 0; i < wa.win_count; i++) total += wa.nper[i];
+  k_recut_begin<<<1, 128, 0, s>>>(m, w.rc, thread_num);
   const int nlev = mp.max_layer + 1;  // children sit one layer down; leaves at max_layer do not subdivide
   auto list_of = [&](int L) { return (L % 2 == 1) ? w.list0 : w.list1; };  // worklist of level L >= 1
   const int gv = 256, gw = grid_for(total > 0 ? total : 1);
@@ -1439,6 +1418,7 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinD& win, const int* nper, int t
   VG_HIP(hipGetLastError());
   int* hrc = ctx->h_pinned + 128;
   VG_TRY(read_rc(ctx, hrc));
+  if (hrc[kRcAbort] == kInsAbort) return kNeedInsertReplay;
   if (hrc[kRcAbort]) {  // replay from the level that overflowed on the host-sized path
     const int L0 = hrc[kRcAbort] - 1;
 #ifdef VG_PROBE
@@ -1807,20 +1787,25 @@ __global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, doub
 // multi_margi (local_mapping.cpp:21-78): every count stays on the device;
 // the host enqueues max_layer+1 levels (no level can be deeper) and
 // synchronises once at the end for the error flags.
-int map_margi(vg_ctx* ctx, const MP& mp, const WinD& win, int n_oldest, int thread_num, double jour) {
+int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, double jour,
+              int pub_seq) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
   const int nlev = mp.max_layer + 1;
   WinD* dwin = (WinD*)ctx->ba.xs;
-  VG_HIP(hipMemcpyAsync(dwin, &win, sizeof(WinD), hipMemcpyHostToDevice, s));
+  int* dn = (int*)((char*)ctx->ba.xs + sizeof(WinD));
+  // x_curr.R/p <- x_buf.back() and the window view; then the state is final
+  // for this scan and is published before the margi kernels run
+  VG_TRY(state_make_win(ctx, wa, dwin, dn, dn + 32));
+  if (pub_seq > 0) VG_TRY(state_publish(ctx, wa.win_count, ba_iters_dev(ctx), pub_seq));
   VG_HIP(hipMemsetAsync(w.rc, 0, kRcN * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.counters + kCntLeaves, 0, sizeof(int), s));
   const int gl = 64;  // grid-stride over device-side counts
   k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour);
   for (int L = 0; L < nlev; L++) k_collect_level<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.list0, w.rc);
   // oldest slot segments by leaf (the slot's point count is known on the host)
-  const int s0 = win.mp[0];
+  const int s0 = wa.mp[0];
   if (n_oldest > 0) {
     k_margi_keys<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, s0, m, w.k0);
     VG_TRY(sort_keys(ctx, w.k0, w.k1, n_oldest, 64));
@@ -1835,7 +1820,7 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinD& win, int n_oldest, int thre
   for (int L = 0; L < nlev; L++) k_clear_mark<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc);
   k_slide_compact<<<1, 1024, 0, s>>>(thread_num, m);
   VG_HIP(hipGetLastError());
-  return read_counters(ctx);
+  return VG_OK;  // device error flags reach the host with the end-of-scan counters
 }
 
 }  // namespace vg

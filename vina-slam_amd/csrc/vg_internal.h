@@ -153,6 +153,45 @@ struct BaBufs {
   double* xs = nullptr;        // window poses (W x 12: R9 p3)
 };
 
+// ---- device-resident estimator state (state.hip) ----
+// The per-scan state lives in HBM for the whole scan: the IEKF update, the
+// window push, the BA and the slide all read and write it on the device, so
+// the host never waits for an intermediate result. The host mirror (pipeline.cpp)
+// is refreshed from the host-mapped publication block below.
+constexpr int kXS = 24;             // per-frame state: R 9, p 3, v 3, bg 3, ba 3, g 3
+constexpr int kXC = kXS + 225;      // x_curr: frame state + cov 15x15 (row-major)
+constexpr int kMaxWin = 32;
+struct DState {
+  double xc[256];                   // x_curr (IMUST, types.hpp:43-113)
+  double xp[256];                   // x_prop (odometry.cpp:67)
+  double cinv[232];                 // cov_inv = cov^-1 (odometry.cpp:82)
+  double G6[96];                    // G(:, 0:6) of the last IEKF iteration (odometry.cpp:198)
+  double nnt[8];                    // sum n n^T of the last iteration (odometry.cpp:145)
+  double traj[16];                  // R, p right after the IEKF (pub_localtraj, local_mapping.cpp:427)
+  double xs[kMaxWin * kXS];         // window states x_buf by ord (local_mapping.cpp:434)
+  double bias[kMaxWin * 12];        // IMU_PRE bias state per window factor: dbg, dba, dbg_buf, dba_buf
+  int it, rematch, done, iters, degenerate, matches[4], pad[7];
+};
+// Host-mapped publication block (written by the device with system-scope
+// stores, each part closed by a sequence flag the host spins on).
+struct Pub {
+  int seq_ds, n_ds, ds_err, pad0;          // downsample (after k_ds_*)
+  int seq_ba, ba_done, ba_iters, pad1;     // LM iteration flags (k_ba_control)
+  int seq1, iekf_iters, degenerate, matches[4], ba_iters1, pad2[4];  // P1: state after IEKF/BA
+  int seq2, pad3[3];
+  int counters[kCntN];                      // P2: map counters at the end of the scan
+  double xc[256];
+  double traj[16];
+  double xs[kMaxWin * kXS];
+};
+// window view for the map kernels, built on the device from DState::xs
+struct WinArg {
+  int mp[kMaxWin];      // mp[] ring (octree.cpp:75)
+  int nper[kMaxWin];    // window points per ord
+  int win_count;
+  int set_xc;           // x_curr.R/p <- x_buf.back() first (local_mapping.cpp:501-502)
+};
+
 }  // namespace vg
 
 struct vg_ctx {
@@ -171,11 +210,12 @@ struct vg_ctx {
   vg::DevMap map;
   vg::Work wk;
   vg::BaBufs ba;
+  vg::DState* st = nullptr;     // device-resident estimator state
+  vg::Pub* h_pub = nullptr;     // host-mapped publication block (host address)
+  vg::Pub* d_pub = nullptr;     // its device address
+  double* h_stage = nullptr;    // pinned staging for asynchronous H2D copies (kStageBytes)
+  int pub_seq = 0;
   int* h_pinned = nullptr;  // small pinned host scratch for counters
-  double* h_pinned_d = nullptr;
-  double* h_zc = nullptr;         // host-mapped zero-copy results (k_iekf): 64 doubles + flag
-  double* d_zc = nullptr;         // its device address
-  int zc_seq = 0;
 
   vg_stats stats;
   void* host = nullptr;     // host-side pipeline state (pipeline.cpp)
@@ -184,8 +224,8 @@ struct vg_ctx {
   bool prof_stages = false;  // per-stage events (vg_profile bit 1)
   hipEvent_t prof_ev[8][2] = {};
   hipEvent_t sync_ev = nullptr;  // host-spin synchronisation (vg::stream_wait)
-  hipEvent_t iekf_ev[8][2] = {};  // k_iekf launches since the last full sync (vg_profile)
-  int iekf_ring_n = 0;
+  hipEvent_t iekf_ev[16][2] = {};  // k_iekf launches of the last two scans (vg_profile), 8 per scan
+  int iekf_ring_n = 0, iekf_ring_base = 0;
   hipEvent_t solve_ev[10][2] = {};  // k_ba_solve launches of the current BA run (vg_profile)
   int dbg_apply_cap = -1;        // test knob (vgx_debug): recut apply event capacity
   bool prof_pending[8] = {};
@@ -194,6 +234,28 @@ struct vg_ctx {
 };
 
 namespace vg {
+constexpr size_t kStageBytes = 1 << 17;
+// Spin until a Pub sequence flag reaches seq (the device publishes with a
+// system-scope release); checks the stream for errors while spinning.
+inline int pub_wait(vg_ctx* c, const int* flag, int seq, const char* what) {
+  for (long spin = 0; __atomic_load_n(flag, __ATOMIC_ACQUIRE) < seq; spin++) {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+    if ((spin & 4095) == 4095) {
+      const hipError_t e = hipStreamQuery(c->stream);
+      if (e != hipSuccess && e != hipErrorNotReady) {
+        c->err = std::string(what) + ": " + hipGetErrorString(e);
+        return VG_E_HIP;
+      }
+      if (e == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) < seq) {
+        c->err = std::string(what) + ": stream drained without publishing";
+        return VG_E_HIP;
+      }
+    }
+  }
+  return VG_OK;
+}
 enum { kProfDownsample = 0, kProfIekfKernel = 1, kProfInsert = 2, kProfRecut = 3, kProfBA = 4, kProfMargi = 5,
        kProfIekf = 6, kProfBaSolve = 7, kProfN = 8 };
 inline void prof_begin(vg_ctx* c, int id) {
@@ -218,26 +280,6 @@ inline hipError_t stream_wait(vg_ctx* c) {
   }
   return e;
 }
-// call only after the stream has been synchronised past the recorded events
-inline void prof_collect(vg_ctx* c) {
-  for (int r = 0; r < c->iekf_ring_n; r++) {  // k_iekf launches (one event pair each)
-    float ms = 0;
-    if (hipEventElapsedTime(&ms, c->iekf_ev[r][0], c->iekf_ev[r][1]) == hipSuccess) {
-      c->prof_ms[kProfIekfKernel] += ms;
-      c->prof_n[kProfIekfKernel] += 1;
-    }
-  }
-  c->iekf_ring_n = 0;
-  for (int i = 0; i < kProfN; i++)
-    if (c->prof_pending[i]) {
-      float ms = 0;
-      if (hipEventElapsedTime(&ms, c->prof_ev[i][0], c->prof_ev[i][1]) == hipSuccess) {
-        c->prof_ms[i] += ms;
-        c->prof_n[i] += 1;
-      }
-      c->prof_pending[i] = false;
-    }
-}
 }  // namespace vg
 
 namespace vg {
@@ -260,14 +302,6 @@ struct WinD {           // window poses x_buf (by ord) and the ring mp[] (octree
   int pad;
 };
 
-struct IekfPose {
-  double R[9], p[3], rot_var[9], tsl_var[9];
-};
-
-struct InsPose {
-  double R[9], p[3], rot_var[9], tsl_var[9];
-};
-
 
 // downsample.hip
 int ds_alloc(vg_ctx* ctx);
@@ -276,33 +310,51 @@ int ds_alloc(vg_ctx* ctx);
 // (returns n_out).
 int ds_run(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, int n, double voxel,
            int* n_out);
+// Same, asynchronous: n_out and the range flag are published to Pub (seq_ds).
+int ds_enqueue(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, int n, double voxel,
+               int pub_seq);
 // map.hip
 int map_alloc(vg_ctx* ctx);
 int map_reset(vg_ctx* ctx);
-int iekf_reset_cache(vg_ctx* ctx, int n);
-int iekf_iter(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n,
-              const IekfPose& pose, double* out34);
-int map_insert(vg_ctx* ctx, const MP& mp, int slot, const InsPose& pose, int n, int epoch, int thread_num,
-               int* roots_new, int* touched);
-int map_recut(vg_ctx* ctx, const MP& mp, const WinD& win, const int* nper, int thread_num, int* n_factors);
-int map_margi(vg_ctx* ctx, const MP& mp, const WinD& win, int n_oldest, int thread_num, double jour);
+int iekf_point_loop(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
+                    int* nb_out);
+constexpr int kNeedInsertReplay = 1;  // map_recut: the insert overflowed k_ins_alloc, replay it first
+int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num);
+int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num);
+int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors);
+int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, double jour, int pub_seq);
+// state.hip
+int state_alloc(vg_ctx* ctx);
+int state_scan_begin(vg_ctx* ctx, const double* xc249);
+int state_iekf_update(vg_ctx* ctx, int nb, const double* partials, int it);
+int state_push(vg_ctx* ctx, int ord, int new_imu);
+int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot);
+int state_slide(vg_ctx* ctx, int win_count, int nimu);
+int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq);
+int state_publish_counters(vg_ctx* ctx, int seq);
+int state_publish_ds(vg_ctx* ctx, int seq);
 // ba.hip
 constexpr int kBaX = 24;        // per-frame state: R 9, p 3, v 3, bg 3, ba 3, g 3
 constexpr int kBaImuRec = 64 + 225;
 int ba_alloc(vg_ctx* ctx);
-int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, double* xs_io, const double* imurec, double* bias_io,
-           int* iters);
+// LM on the device state (window states and IMU bias records in DState);
+// imurec: (W-1) x kBaImuRec host records. Returns once the LM has converged on
+// the device (the flags are read without draining the stream).
+int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* iters);
+const int* ba_iters_dev(vg_ctx* ctx);
 // pipeline.cpp
 void host_init(vg_ctx* ctx);
 void host_free(vg_ctx* ctx);
 void host_reset(vg_ctx* ctx);
 void host_seed(vg_ctx* ctx, const double* s);
-void host_state(vg_ctx* ctx, double* s);
+int host_state(vg_ctx* ctx, double* s);
 int host_window(vg_ctx* ctx, double* out);
 int host_traj(vg_ctx* ctx, double* out, int cap);
 int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n, double beg,
               double end, const double* imu, int m);
 int host_win_count(vg_ctx* ctx);
+int host_sync(vg_ctx* ctx);
+int host_stats_log(vg_ctx* ctx, vg_stats* out, int cap);
 int stage_propagate(vg_ctx* ctx, const double* imu, int m, double end);
 int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n,
                      int* n_ds_out);

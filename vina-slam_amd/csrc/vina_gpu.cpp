@@ -56,7 +56,8 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     ctx->d_y = ctx->arena.take<float>(n);
     ctx->d_z = ctx->arena.take<float>(n);
     ctx->d_i = ctx->arena.take<float>(n);
-    int r = ds_alloc(ctx);
+    int r = state_alloc(ctx);
+    if (r == VG_OK) r = ds_alloc(ctx);
     if (r == VG_OK) r = map_alloc(ctx);
     if (r == VG_OK) r = ba_alloc(ctx);
     return r;
@@ -78,7 +79,7 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
   r = carve();
   if (r == VG_OK) r = map_reset(ctx);
   if (r != VG_OK) return fail(r);
-  if ((e = hipHostMalloc((void**)&ctx->h_pinned_d, 4096, hipHostMallocDefault)) != hipSuccess) {
+  if ((e = hipHostMalloc((void**)&ctx->h_stage, kStageBytes, hipHostMallocDefault)) != hipSuccess) {
     ctx->err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
@@ -88,7 +89,7 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
         ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
         return fail(VG_E_HIP);
       }
-  for (int i = 0; i < 8; i++)
+  for (int i = 0; i < 16; i++)
     for (int j = 0; j < 2; j++)
       if ((e = hipEventCreate(&ctx->iekf_ev[i][j])) != hipSuccess) {
         ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
@@ -100,12 +101,13 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
         ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
         return fail(VG_E_HIP);
       }
-  if ((e = hipHostMalloc((void**)&ctx->h_zc, 4096, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
-      (e = hipHostGetDevicePointer((void**)&ctx->d_zc, ctx->h_zc, 0)) != hipSuccess) {
+  if ((e = hipHostMalloc((void**)&ctx->h_pub, sizeof(Pub), hipHostMallocMapped | hipHostMallocCoherent)) !=
+          hipSuccess ||
+      (e = hipHostGetDevicePointer((void**)&ctx->d_pub, ctx->h_pub, 0)) != hipSuccess) {
     ctx->err = std::string("hipHostMalloc (mapped): ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
-  memset(ctx->h_zc, 0, 4096);
+  memset(ctx->h_pub, 0, sizeof(Pub));
   if ((e = hipEventCreateWithFlags(&ctx->sync_ev, hipEventDisableTiming)) != hipSuccess) {
     ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
@@ -120,14 +122,14 @@ int vg_destroy(vg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->arena.base) (void)hipFree(ctx->arena.base);
   if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
-  if (ctx->h_pinned_d) (void)hipHostFree(ctx->h_pinned_d);
-  if (ctx->h_zc) (void)hipHostFree(ctx->h_zc);
+  if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+  if (ctx->h_pub) (void)hipHostFree(ctx->h_pub);
   if (ctx->host) host_free(ctx);
   for (int i = 0; i < 8; i++)
     for (int j = 0; j < 2; j++)
       if (ctx->prof_ev[i][j]) (void)hipEventDestroy(ctx->prof_ev[i][j]);
   if (ctx->sync_ev) (void)hipEventDestroy(ctx->sync_ev);
-  for (int i = 0; i < 8; i++)
+  for (int i = 0; i < 16; i++)
     for (int j = 0; j < 2; j++)
       if (ctx->iekf_ev[i][j]) (void)hipEventDestroy(ctx->iekf_ev[i][j]);
   for (int i = 0; i < 10; i++)
@@ -144,6 +146,7 @@ void* vg_stream(vg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 int vg_reset(vg_ctx* ctx) {
   if (!ctx) return VG_E_ARG;
+  VG_HIP(hipStreamSynchronize(ctx->stream));
   VG_TRY(map_reset(ctx));
   host_reset(ctx);
   return VG_OK;
@@ -231,24 +234,34 @@ int vg_step_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_
 
 int vg_get_state(vg_ctx* ctx, double* state) {
   if (!ctx || !state) return VG_E_ARG;
-  host_state(ctx, state);
+  VG_TRY(host_state(ctx, state));
   return VG_OK;
 }
 
 int vg_get_stats(vg_ctx* ctx, vg_stats* out) {
   if (!ctx || !out) return VG_E_ARG;
+  VG_TRY(host_sync(ctx));
   *out = ctx->stats;
+  return VG_OK;
+}
+
+int vg_stats_log(vg_ctx* ctx, vg_stats* out, int cap, int* n) {
+  if (!ctx || !n || cap < 0) return VG_E_ARG;
+  VG_TRY(host_sync(ctx));
+  *n = host_stats_log(ctx, out, cap);
   return VG_OK;
 }
 
 int vg_window_states(vg_ctx* ctx, double* out, int* n) {
   if (!ctx || !n || !out) return VG_E_ARG;
+  VG_TRY(host_sync(ctx));
   *n = host_window(ctx, out);
   return VG_OK;
 }
 
 int vg_trajectory(vg_ctx* ctx, double* out, int cap, int* n) {
   if (!ctx || !n) return VG_E_ARG;
+  VG_TRY(host_sync(ctx));
   *n = host_traj(ctx, out, cap);
   return VG_OK;
 }

@@ -68,6 +68,7 @@ def lib():
         L.vg_step_dev.argtypes = [P, P, P, P, P, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
         L.vg_get_state.argtypes = [P, dp]
         L.vg_get_stats.argtypes = [P, ctypes.POINTER(Stats)]
+        L.vg_stats_log.argtypes = [P, ctypes.POINTER(Stats), ctypes.c_int, ip]
         L.vg_window_states.argtypes = [P, dp, ip]
         L.vg_trajectory.argtypes = [P, dp, ctypes.c_int, ip]
         L.vg_scan_load.argtypes = [P, fp, fp, ctypes.c_int]
@@ -161,6 +162,15 @@ class Context:
         s = Stats()
         self._chk(lib().vg_get_stats(self.h, ctypes.byref(s)), "vg_get_stats")
         return {k: (list(getattr(s, k)) if k == "iekf_matches" else getattr(s, k)) for k, _ in Stats._fields_}
+
+    def stats_log(self):
+        """Counters of every completed scan (drains the stream once)."""
+        n = ctypes.c_int(0)
+        self._chk(lib().vg_stats_log(self.h, None, 0, ctypes.byref(n)), "vg_stats_log")
+        arr = (Stats * max(n.value, 1))()
+        self._chk(lib().vg_stats_log(self.h, arr, n.value, ctypes.byref(n)), "vg_stats_log")
+        return [{k: (list(getattr(s, k)) if k == "iekf_matches" else getattr(s, k)) for k, _ in Stats._fields_}
+                for s in arr[: n.value]]
 
     def window_states(self):
         out = np.zeros((64, STATE_LEN))
