@@ -50,5 +50,31 @@ def main(nscan=40, lidar="64line"):
     ctx.close()
 
 
+
+
+def iekf(nscan=40, lidar="64line"):
+    """Phase clocks of the IEKF update run by the last k_iekf workgroup."""
+    p = vgconfig.load("mid360")
+    g = p["General"]
+    seq = synth.Sequence(lidar, 0, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
+    ctx = vgpu.Context(vgconfig.to_c(p), device=0)
+    ctx.seed(seq.gt_state(0))
+    L = vgpu.lib()
+    buf = (ctypes.c_ulonglong * 64)()
+    for k in range(nscan):
+        xyz, it, b, e = seq.scan(k)
+        ctx.step(xyz, it, b, e, seq.imu(k))
+        ctx.stats()
+        if k == 11:
+            L.vg_probe_read_map(buf, 64)
+    L.vg_probe_read_map(buf, 64)
+    n, nf = max(buf[61], 1), max(buf[60], 1)
+    print("iekf updates:", buf[61], "final:", buf[60])
+    for k, name in {24: "reduce partials", 25: "K6 (6x6 solve)", 26: "G6/vec/sol", 27: "plus/conv"}.items():
+        print("  %-16s %8.2f us/call" % (name, buf[k] * 0.01 / n))
+    for k, name in {28: "cov update", 29: "eig3/final"}.items():
+        print("  %-16s %8.2f us/final" % (name, buf[k] * 0.01 / nf))
+
+
 if __name__ == "__main__":
-    main()
+    iekf() if "iekf" in sys.argv else main()

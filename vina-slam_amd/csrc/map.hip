@@ -20,7 +20,7 @@
 // sums are deterministic and order-faithful.
 #include <hipcub/hipcub.hpp>
 #include <cstdio>
-#include "vg_dev.h"
+#include "vg_iekf.h"
 
 namespace vg {
 
@@ -181,14 +181,13 @@ __device__ __forceinline__ bool inside(const NodeHdr& h, const V3& w) {
           w[1] <= h.center[1] + hl && w[2] >= h.center[2] - hl && w[2] <= h.center[2] + hl);
 }
 
-constexpr int kIekfVals = 34;
 
 // The pose (x_curr R, p and the rotation / translation covariance blocks) is
 // read from the device state the previous k_iekf_update wrote; the kernel is a
 // no-op once the IEKF has finished (st->done). Iteration 0 ignores the leaf
 // cache (no association yet, odometry.cpp:111-132).
 __global__ void __launch_bounds__(256) k_iekf(int n, const float* __restrict__ x, const float* __restrict__ y,
-                                              const float* __restrict__ z, MP mp, const DState* __restrict__ st,
+                                              const float* __restrict__ z, MP mp, DState* __restrict__ st,
                                               int it, DevMap m, int* __restrict__ cache,
                                               double* __restrict__ partials) {
   if (st->done) return;
@@ -265,15 +264,30 @@ __global__ void __launch_bounds__(256) k_iekf(int n, const float* __restrict__ x
   }
 }
 
-// one IEKF point loop (iteration `it`) -> block partials for k_iekf_update
-int iekf_point_loop(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
-                    int* nb_out) {
+// The IEKF update of iteration `it` (vg_iekf.h) as its own one-workgroup
+// launch. (A last-workgroup-done ticket inside k_iekf would need an
+// agent-scope release per workgroup, which on the multi-XCD MI355X writes back
+// the XCD's L2 each time: measured ~20 us per iteration, far more than the
+// launch it saves.)
+__global__ void __launch_bounds__(256) k_iekf_update(int nb, const double* __restrict__ partials,
+                                                     DState* __restrict__ st, int it) {
+  __shared__ IekfLds L;
+  if (st->done) return;
+  iekf_update_block(nb, partials, st, it, L);
+}
+
+// one IEKF iteration: the point loop (block partials) and the update; the
+// optional event pair brackets k_iekf alone (vg_profile)
+int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
+                   hipEvent_t ev0, hipEvent_t ev1) {
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
   const int nb = grid_for(n, 256, 512);
+  if (ev0) (void)hipEventRecord(ev0, s);
   k_iekf<<<nb, 256, 0, s>>>(n, x, y, z, mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials);
+  if (ev1) (void)hipEventRecord(ev1, s);
+  k_iekf_update<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, it);
   VG_HIP(hipGetLastError());
-  *nb_out = nb;
   return VG_OK;
 }
 

@@ -218,6 +218,22 @@ static int map_error(vg_ctx* ctx, int e) {
   return (e & 1) ? VG_E_RANGE : VG_E_CAPACITY;
 }
 
+// LioStateEstimation's return value (odometry.cpp:244-254): lambda_min of
+// sum n n^T >= 14; bookkeeping only (degrade_cnt, local_mapping.cpp:413-423)
+static int degenerate_of(const double* nnt) {
+  M3 nn;
+  nn(0, 0) = nnt[0];
+  nn(0, 1) = nn(1, 0) = nnt[1];
+  nn(0, 2) = nn(2, 0) = nnt[2];
+  nn(1, 1) = nnt[3];
+  nn(1, 2) = nn(2, 1) = nnt[4];
+  nn(2, 2) = nnt[5];
+  V3 ev;
+  M3 U;
+  eig3(nn, ev, U);
+  return (ev[0] < 14) ? 1 : 0;
+}
+
 // P1 of the oldest pending scan: x_curr, post-IEKF pose, window states
 static int absorb_p1(vg_ctx* ctx, HostPipe* P, Pend& q) {
   if (q.seq1 == 0) return VG_OK;
@@ -247,7 +263,7 @@ static int absorb_p1(vg_ctx* ctx, HostPipe* P, Pend& q) {
   for (int i = 0; i < 12; i++) P->traj.push_back(pb.traj[i]);
   q.st.iekf_iters = pb.iekf_iters;
   for (int i = 0; i < 4; i++) q.st.iekf_matches[i] = pb.matches[i];
-  q.st.degenerate = pb.degenerate;
+  q.st.degenerate = degenerate_of(pb.nnt);
   q.st.ba_iters = pb.ba_iters1;
   if (q.jour_check) {  // local_mapping.cpp:525-533 with x_curr.p = x_buf.back().p after the BA
     double spat = norm3(sub(xc.p, P->last_pos));
@@ -399,11 +415,8 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   P->cur.ev_n = 0;
   for (int it = 0; it < num_max_iter; it++) {
     const int ring = ctx->prof_on ? ctx->iekf_ring_base + P->cur.ev_n++ : -1;
-    if (ring >= 0) (void)hipEventRecord(ctx->iekf_ev[ring][0], ctx->stream);
-    int nb = 0;
-    VG_TRY(iekf_point_loop(ctx, P->mpd, x, y, z, n, it, &nb));
-    if (ring >= 0) (void)hipEventRecord(ctx->iekf_ev[ring][1], ctx->stream);
-    VG_TRY(state_iekf_update(ctx, nb, ctx->wk.partials, it));
+    VG_TRY(iekf_iteration(ctx, P->mpd, x, y, z, n, it, ring >= 0 ? ctx->iekf_ev[ring][0] : nullptr,
+                          ring >= 0 ? ctx->iekf_ev[ring][1] : nullptr));
   }
   return VG_OK;
 }
@@ -538,9 +551,10 @@ int stage_iekf(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, i
   VG_TRY(lio_state_estimation(ctx, P, dx, dy, dz, n));
   prof_end(ctx, kProfIekf);
   if (degenerate_out) {  // stage API caller wants the flag now: read it from the device state
-    VG_HIP(hipMemcpyAsync(ctx->h_pinned, &ctx->st->degenerate, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    double* h = ctx->h_stage;
+    VG_HIP(hipMemcpyAsync(h, ctx->st->nnt, 6 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     VG_HIP(stream_wait(ctx));
-    *degenerate_out = ctx->h_pinned[0];
+    *degenerate_out = degenerate_of(h);
   }
   return VG_OK;
 }

@@ -1,0 +1,205 @@
+// vg_iekf.h — the IEKF update (odometry.cpp:192-254) as a workgroup-level
+// device routine, run by k_iekf_update after each k_iekf point loop (map.hip).
+//
+// The reference forms K_1 = (H_T_H + cov^-1)^-1 with two 15 x 15 inverses
+// (odometry.cpp:82, 194) but only ever uses its first six columns (K_1.block<15,6>,
+// 198-201). Since H_T_H is zero outside its 6 x 6 block, the push-through
+// (Woodbury) identity gives exactly those columns from one 6 x 6 system:
+//   K6 = K_1(:, 0:6) = cov(:, 0:6) (I + HTH cov(0:6, 0:6))^-1,
+// solved here by one wave (Gauss-Jordan with partial pivoting, one column of
+// [M^T | cov(:,0:6)^T] per lane, no barriers). Identical in exact arithmetic;
+// rounding differs from the 15 x 15 route at the 1e-13 relative level (the
+// parity tests bound the trajectory).
+#pragma once
+#include "vg_dev.h"
+
+namespace vg {
+
+constexpr int kIekfVals = 34;  // HTH upper 21, HTz 6, nnt upper 6, match count
+
+// LDS of iekf_update_block
+struct IekfLds {
+  double red[15][kIekfVals];
+  double o[kIekfVals], K6[15][6], G6[15][6], vec[15], sol[15], IG[15][15];
+  int fin;
+};
+
+// One IEKF update after iteration `it`'s point loop wrote nb block partials
+// (row-major nb x kIekfVals). Whole workgroup (>= 256 threads), uniform.
+// 64-bit broadcast of lane `ln` (a compile-time constant after unrolling)
+__device__ __forceinline__ double bcast_lane(double v, int ln) {
+  const long long b = __double_as_longlong(v);
+  const int lo32 = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), ln);
+  const int hi32 = __builtin_amdgcn_readlane((int)(b >> 32), ln);
+  return __longlong_as_double(((long long)hi32 << 32) | (unsigned int)lo32);
+}
+
+__device__ void iekf_update_block(int nb, const double* __restrict__ partials, DState* __restrict__ st, int it,
+                                  IekfLds& L) {
+  const int tid = threadIdx.x;
+  VG_PROBE_BEGIN();
+  {  // ordered sum: row group g = tid / 17 (rows g, g+15, ...), lane pair 2*(tid % 17); then groups in order
+    const int g = tid / 17, j2 = 2 * (tid % 17);
+    if (g < 15) {
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll 8
+      for (int b = g; b < nb; b += 15) {
+        const double2 v = *reinterpret_cast<const double2*>(&partials[(size_t)b * kIekfVals + j2]);
+        a0 += v.x;
+        a1 += v.y;
+      }
+      L.red[g][j2] = a0;
+      L.red[g][j2 + 1] = a1;
+    }
+    __syncthreads();
+    if (tid < kIekfVals) {
+      double s = L.red[0][tid];
+      for (int k = 1; k < 15; k++) s += L.red[k][tid];
+      L.o[tid] = s;
+    }
+    __syncthreads();
+  }
+  const double* o = L.o;
+  auto hth = [&](int i, int j) {
+    const int lo = i < j ? i : j, hi = i < j ? j : i;
+    return o[lo * 6 - lo * (lo - 1) / 2 + (hi - lo)];
+  };
+  if (tid == 0) {
+    st->iters = it + 1;
+    st->matches[it] = (int)o[33];
+    for (int k = 0; k < 6; k++) st->nnt[k] = o[27 + k];
+  }
+  VG_PROBE_MARK(24);
+  if (tid < 64) {  // K6 = cov(:, 0:6) M^-1, M = I + HTH cov66: solve M^T X = cov(:, 0:6)^T, K6 = X^T
+    const int lane = tid;
+    const double* cov = st->xc + kXS;
+    double col[6];
+    if (lane < 6) {  // column `lane` of M^T = row `lane` of M
+      for (int r = 0; r < 6; r++) {
+        double sm = hth(lane, 0) * cov[0 * 15 + r];
+        for (int l = 1; l < 6; l++) sm += hth(lane, l) * cov[l * 15 + r];
+        col[r] = ((lane == r) ? 1.0 : 0.0) + sm;
+      }
+    } else {
+      const int i = lane < 21 ? lane - 6 : 0;  // column i of cov(:, 0:6)^T = row i of cov, cols 0..5
+      for (int r = 0; r < 6; r++) col[r] = cov[i * 15 + r];
+    }
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+      double pc[6];
+#pragma unroll
+      for (int r = 0; r < 6; r++) pc[r] = bcast_lane(col[r], c);
+      int p = c;
+      double best = fabs(pc[c]);
+#pragma unroll
+      for (int r = c + 1; r < 6; r++)
+        if (fabs(pc[r]) > best) {
+          best = fabs(pc[r]);
+          p = r;
+        }
+      // swap rows c, p (pivot column and this lane's column)
+      double pv = pc[c], cv = col[c];
+#pragma unroll
+      for (int r = c + 1; r < 6; r++)
+        if (r == p) {
+          const double t = pc[r];
+          pc[r] = pv;
+          pv = t;
+          const double u = col[r];
+          col[r] = cv;
+          cv = u;
+        }
+      const double inv = 1.0 / pv;
+      cv *= inv;
+      col[c] = cv;
+#pragma unroll
+      for (int r = 0; r < 6; r++)
+        if (r != c && pc[r] != 0.0) col[r] -= pc[r] * cv;
+    }
+    if (lane >= 6 && lane < 21)
+      for (int r = 0; r < 6; r++) L.K6[lane - 6][r] = col[r];
+  }
+  __syncthreads();
+  VG_PROBE_MARK(25);
+  // G6 = K6 * HTH
+  if (tid < 90) {
+    const int r = tid / 6, c = tid % 6;
+    double s = L.K6[r][0] * hth(0, c);
+    for (int k = 1; k < 6; k++) s += L.K6[r][k] * hth(k, c);
+    L.G6[r][c] = s;
+    st->G6[r * 6 + c] = s;
+  }
+  if (tid == 128) {  // vec = x_prop ⊟ x_curr (IMUST::operator-, types.hpp:80-86)
+    const double* xp = st->xp;
+    const double* xc = st->xc;
+    const V3 rr = Log(mul(tr(ld_m3(xc)), ld_m3(xp)));
+    for (int k = 0; k < 3; k++) {
+      L.vec[k] = rr[k];
+      L.vec[3 + k] = xp[9 + k] - xc[9 + k];
+      L.vec[6 + k] = xp[12 + k] - xc[12 + k];
+      L.vec[9 + k] = xp[15 + k] - xc[15 + k];
+      L.vec[12 + k] = xp[18 + k] - xc[18 + k];
+    }
+  }
+  __syncthreads();
+  if (tid < 15) {  // sol = (K6 HTz + vec) - G6 v6
+    double s1 = L.K6[tid][0] * o[21];
+    for (int k = 1; k < 6; k++) s1 += L.K6[tid][k] * o[21 + k];
+    double s2 = L.G6[tid][0] * L.vec[0];
+    for (int k = 1; k < 6; k++) s2 += L.G6[tid][k] * L.vec[k];
+    L.sol[tid] = (s1 + L.vec[tid]) - s2;
+  }
+  __syncthreads();
+  VG_PROBE_MARK(26);
+  if (tid == 0) {  // x_curr ⊞= sol (types.hpp:67-78); convergence / rematch (odometry.cpp:205-227)
+    double* xc = st->xc;
+    const double* sol = L.sol;
+    const M3 Rn = mul(ld_m3(xc), Exp(v3(sol[0], sol[1], sol[2])));
+    for (int k = 0; k < 9; k++) xc[k] = Rn[k];
+    for (int k = 0; k < 3; k++) {
+      xc[9 + k] += sol[3 + k];
+      xc[12 + k] += sol[6 + k];
+      xc[15 + k] += sol[9 + k];
+      xc[18 + k] += sol[12 + k];
+    }
+    const double rot_add = norm3(v3(sol[0], sol[1], sol[2])), tra_add = norm3(v3(sol[3], sol[4], sol[5]));
+    const bool conv = (rot_add * 57.3 < 0.01) && (tra_add * 100 < 0.015);
+    int rm = st->rematch;
+    if (conv || ((rm == 0) && (it == 4 - 2))) rm++;
+    st->rematch = rm;
+    L.fin = (rm >= 2 || it == 4 - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  VG_PROBE_MARK(27);
+#ifdef VG_PROBE
+  if (tid == 0) atomicAdd(&g_probe[61], 1ull);
+#endif
+  if (!L.fin) return;
+  // cov = (I - G) cov (G zero outside columns 0..5)
+  for (int e = tid; e < 225; e += blockDim.x) {
+    const int r = e / 15, c = e % 15;
+    L.IG[r][c] = ((r == c) ? 1.0 : 0.0) - (c < 6 ? L.G6[r][c] : 0.0);
+  }
+  __syncthreads();
+  double cv = 0.0;
+  if (tid < 225) {
+    const int r = tid / 15, c = tid % 15;
+    const double* cov = st->xc + kXS;
+    double s = L.IG[r][0] * cov[c];
+    for (int k = 1; k < 15; k++) s += L.IG[r][k] * cov[k * 15 + c];
+    cv = s;
+  }
+  __syncthreads();
+  if (tid < 225) st->xc[kXS + tid] = cv;
+  VG_PROBE_MARK(28);
+  if (tid == 0) {  // the degeneracy test (odometry.cpp:244-254) runs on the host from nnt
+    for (int k = 0; k < 12; k++) st->traj[k] = st->xc[k];
+    st->done = 1;
+  }
+  VG_PROBE_MARK(29);
+#ifdef VG_PROBE
+  if (tid == 0) atomicAdd(&g_probe[60], 1ull);
+#endif
+}
+
+}  // namespace vg

@@ -164,13 +164,12 @@ constexpr int kMaxWin = 32;
 struct DState {
   double xc[256];                   // x_curr (IMUST, types.hpp:43-113)
   double xp[256];                   // x_prop (odometry.cpp:67)
-  double cinv[232];                 // cov_inv = cov^-1 (odometry.cpp:82)
   double G6[96];                    // G(:, 0:6) of the last IEKF iteration (odometry.cpp:198)
   double nnt[8];                    // sum n n^T of the last iteration (odometry.cpp:145)
   double traj[16];                  // R, p right after the IEKF (pub_localtraj, local_mapping.cpp:427)
   double xs[kMaxWin * kXS];         // window states x_buf by ord (local_mapping.cpp:434)
   double bias[kMaxWin * 12];        // IMU_PRE bias state per window factor: dbg, dba, dbg_buf, dba_buf
-  int it, rematch, done, iters, degenerate, matches[4], pad[7];
+  int it, rematch, done, iters, degenerate, matches[4], ticket, pad[6];
 };
 // Host-mapped publication block (written by the device with system-scope
 // stores, each part closed by a sequence flag the host spins on).
@@ -182,6 +181,7 @@ struct Pub {
   int counters[kCntN];                      // P2: map counters at the end of the scan
   double xc[256];
   double traj[16];
+  double nnt[8];
   double xs[kMaxWin * kXS];
 };
 // window view for the map kernels, built on the device from DState::xs
@@ -316,8 +316,8 @@ int ds_enqueue(vg_ctx* ctx, const float* x, const float* y, const float* z, cons
 // map.hip
 int map_alloc(vg_ctx* ctx);
 int map_reset(vg_ctx* ctx);
-int iekf_point_loop(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
-                    int* nb_out);
+int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
+                   hipEvent_t ev0, hipEvent_t ev1);
 constexpr int kNeedInsertReplay = 1;  // map_recut: the insert overflowed k_ins_alloc, replay it first
 int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num);
 int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num);
@@ -326,7 +326,6 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
 // state.hip
 int state_alloc(vg_ctx* ctx);
 int state_scan_begin(vg_ctx* ctx, const double* xc249);
-int state_iekf_update(vg_ctx* ctx, int nb, const double* partials, int it);
 int state_push(vg_ctx* ctx, int ord, int new_imu);
 int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot);
 int state_slide(vg_ctx* ctx, int win_count, int nimu);
