@@ -877,13 +877,22 @@ __global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, do
   }
 }
 
-__global__ void __launch_bounds__(256) k_ba_init(BaState* st) {
-  st->u = 0.01;
-  st->v = 2;
-  st->res1 = st->res2 = st->q1 = 0.0;
-  st->calc_hess = 1;
-  st->done = 0;
-  st->iters = 0;
+struct MpRing {
+  int mp[kMaxW];
+};
+// LM state (optimizers.cpp:436-441), the reduced-Hessian accumulator, the ring
+__global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict__ hl, int nout, MpRing ring,
+                                                 int* __restrict__ mpring, int W) {
+  for (int t = threadIdx.x; t < nout; t += blockDim.x) hl[t] = 0.0;
+  if ((int)threadIdx.x < W) mpring[threadIdx.x] = ring.mp[threadIdx.x];
+  if (threadIdx.x == 0) {
+    st->u = 0.01;
+    st->v = 2;
+    st->res1 = st->res2 = st->q1 = 0.0;
+    st->calc_hess = 1;
+    st->done = 0;
+    st->iters = 0;
+  }
 }
 
 struct BaDev {
@@ -1012,12 +1021,11 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* i
   // one H2D copy of the host-side inputs: IMU records, then the mp ring
   double* stage = ctx->h_stage;
   memcpy(stage, imurec, (size_t)nimu * kImuRec * sizeof(double));
-  memcpy(stage + (size_t)kMaxW * kImuRec, mp_ring, W * sizeof(int));
-  static_assert((size_t)kMaxW * kImuRec * sizeof(double) + 64 <= kStageBytes, "staging block too small");
+  static_assert((size_t)kMaxW * kImuRec * sizeof(double) <= kStageBytes, "staging block too small");
   VG_HIP(hipMemcpyAsync(d.imurec, stage, (size_t)nimu * kImuRec * sizeof(double), hipMemcpyHostToDevice, s));
-  VG_HIP(hipMemcpyAsync(d.mpring, stage + (size_t)kMaxW * kImuRec, W * sizeof(int), hipMemcpyHostToDevice, s));
-  VG_HIP(hipMemsetAsync(d.hl, 0, nout * sizeof(double), s));
-  k_ba_init<<<1, 1, 0, s>>>(d.st);
+  MpRing ring;
+  for (int i = 0; i < kMaxW; i++) ring.mp[i] = i < W ? mp_ring[i] : 0;
+  k_ba_init<<<1, 256, 0, s>>>(d.st, d.hl, nout, ring, d.mpring, W);
   const int nchunk = (nf + hess_chunk(W) - 1) / hess_chunk(W);
   const int nrb = (nf + 255) / 256;
   const size_t hess_lds = hess_lds_bytes(W);

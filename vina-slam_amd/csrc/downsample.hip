@@ -116,15 +116,14 @@ int ds_alloc(vg_ctx* ctx) {
   return VG_OK;
 }
 
-int ds_enqueue(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, int n, double voxel,
-               int pub_seq) {
+int ds_enqueue(vg_ctx* ctx, hipStream_t s, const float* x, const float* y, const float* z, const float* in, int n,
+               double voxel, int pub_seq) {
   DownsampleBufs& d = ctx->ds;
-  hipStream_t s = ctx->stream;
   if (n > ctx->cap.max_points_per_scan) {
     ctx->err = "scan larger than max_points_per_scan";
     return VG_E_CAPACITY;
   }
-  VG_HIP(hipMemsetAsync(d.flags, 0, 4 * sizeof(int), s));
+  // d.flags are zero here: zeroed at creation and by every k_publish_ds / ds_run
   if (n > 0) {
     k_ds_keys<<<grid_for(n), kBlock, 0, s>>>(n, x, y, z, voxel, d.keys, d.idx, d.flags);
     size_t tb = d.tmp_bytes;
@@ -136,7 +135,7 @@ int ds_enqueue(vg_ctx* ctx, const float* x, const float* y, const float* z, cons
     k_ds_mean<<<grid_for(n), kBlock, 0, s>>>(d.flags, d.seg, d.idx_sorted, x, y, z, in, d.ox, d.oy, d.oz, d.oi,
                                              d.oc);
   }
-  if (pub_seq > 0) VG_TRY(state_publish_ds(ctx, pub_seq));
+  if (pub_seq > 0) VG_TRY(state_publish_ds(ctx, s, pub_seq));
   VG_HIP(hipGetLastError());
   return VG_OK;
 }
@@ -149,8 +148,9 @@ int ds_run(vg_ctx* ctx, const float* x, const float* y, const float* z, const fl
     *n_out = 0;
     return VG_OK;
   }
-  VG_TRY(ds_enqueue(ctx, x, y, z, in, n, voxel, 0));
+  VG_TRY(ds_enqueue(ctx, s, x, y, z, in, n, voxel, 0));
   VG_HIP(hipMemcpyAsync(ctx->h_pinned, d.flags, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+  VG_HIP(hipMemsetAsync(d.flags, 0, 4 * sizeof(int), s));
   VG_HIP(stream_wait(ctx));
   if (ctx->h_pinned[0]) {
     ctx->err = "voxel key out of packed range (|key| >= 2^20)";

@@ -1704,35 +1704,36 @@ __global__ void __launch_bounds__(64 * kCopyWaves) k_margi_copy(const int* __res
   }
 }
 
-__global__ void __launch_bounds__(256) k_margi_segs_clear(int n, const uint64_t* __restrict__ keys, DevMap m) {
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-    uint64_t k = keys[j];
+// internal nodes bottom-up: isexist = OR(children) (octree.cpp:485-494); the
+// deepest level's launch also clears the oldest-slot segment records
+__device__ __forceinline__ void internal_exist(DevMap& m, int node) {
+  NodeHdr& h = m.hdr[node];
+  if (h.octo != 1) return;
+  int8_t e = 0;
+  for (int o = 0; o < 8; o++)
+    if (h.child[o] >= 0) e |= m.hdr[h.child[o]].isexist;
+  h.isexist = e ? 1 : 0;
+}
+__global__ void __launch_bounds__(256) k_margi_internal(int L, int thread_num, DevMap m, int* __restrict__ lists,
+                                                        const int* __restrict__ rc, int nseg,
+                                                        const uint64_t* __restrict__ segkeys) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nseg; j += gridDim.x * blockDim.x) {
+    const uint64_t k = segkeys[j];
     if (k == ~0ull) continue;
-    int l = (int)(k >> 27);
+    const int l = (int)(k >> 27);
     m.nscr[(size_t)l * 4 + 0] = -1;
     m.nscr[(size_t)l * 4 + 1] = -1;
   }
-}
-
-// internal nodes bottom-up: isexist = OR(children) (octree.cpp:485-494)
-__global__ void __launch_bounds__(256) k_margi_internal(int L, int thread_num, DevMap m, int* __restrict__ lists,
-                                                        const int* __restrict__ rc) {
   if (m.counters[kCntSlide] < thread_num) return;
   int* work;
   const int nw = margi_level(L, m, rc, lists, &work);
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) {
-    int node = work[q];
-    NodeHdr& h = m.hdr[node];
-    if (h.octo != 1) continue;
-    int8_t e = 0;
-    for (int o = 0; o < 8; o++)
-      if (h.child[o] >= 0) e |= m.hdr[h.child[o]].isexist;
-    h.isexist = e ? 1 : 0;
-  }
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) internal_exist(m, work[q]);
 }
 
 // erase dead roots from surf_map_slide (local_mapping.cpp:67-78) with
-// clear_slwd over their subtrees (octree.cpp:739-756)
+// clear_slwd over their subtrees (octree.cpp:739-756), top-down. Level 0 also
+// finishes the bottom-up isexist pass (its roots are level 0's own nodes);
+// level L also resets the dead marks of level L-2, which nobody reads any more.
 __global__ void __launch_bounds__(256) k_margi_erase_mark(int L, int thread_num, DevMap m, int* __restrict__ lists,
                                                           const int* __restrict__ rc) {
   if (m.counters[kCntSlide] < thread_num) return;
@@ -1743,6 +1744,7 @@ __global__ void __launch_bounds__(256) k_margi_erase_mark(int L, int thread_num,
     NodeHdr& h = m.hdr[node];
     int dead;
     if (L == 0) {
+      internal_exist(m, node);
       dead = h.isexist ? 0 : 1;
     } else {
       dead = m.nscr[(size_t)h.parent * 4 + 2] == 7 ? 1 : 0;
@@ -1754,45 +1756,76 @@ __global__ void __launch_bounds__(256) k_margi_erase_mark(int L, int thread_num,
       if (L == 0) m.in_slide[node] = 0;
     }
   }
+  if (L >= 2) {
+    const int nc = margi_level(L - 2, m, rc, lists, &work);
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nc; q += gridDim.x * blockDim.x)
+      m.nscr[(size_t)work[q] * 4 + 2] = -1;
+  }
 }
-__global__ void __launch_bounds__(256) k_clear_mark(int L, int thread_num, DevMap m, int* __restrict__ lists,
-                                                    const int* __restrict__ rc) {
+// reset the dead marks of levels L0 .. nlev-1
+__global__ void __launch_bounds__(256) k_clear_mark(int L0, int nlev, int thread_num, DevMap m,
+                                                    int* __restrict__ lists, const int* __restrict__ rc) {
   if (m.counters[kCntSlide] < thread_num) return;
-  int* work;
-  const int nw = margi_level(L, m, rc, lists, &work);
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x)
-    m.nscr[(size_t)work[q] * 4 + 2] = -1;
+  for (int L = L0 < 0 ? 0 : L0; L < nlev; L++) {
+    int* work;
+    const int nw = margi_level(L, m, rc, lists, &work);
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x)
+      m.nscr[(size_t)work[q] * 4 + 2] = -1;
+  }
 }
 // single block, order-preserving in-place compaction of the slide list (a
 // chunk is read completely before any of it is written; writes never pass
 // the read position)
-__global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m) {
+// then (the same workgroup) the x_buf / imu_pre_buf slide of the device state
+// (local_mapping.cpp:536-546) and the end-of-scan counter publication
+__global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m, DState* __restrict__ st, int wc,
+                                                        int nimu, Pub* __restrict__ pub, int seq2) {
   __shared__ int base;
   __shared__ int sc[1024];
   const int n = m.counters[kCntSlide];
-  if (n < thread_num) return;
-  if (threadIdx.x == 0) base = 0;
-  __syncthreads();
-  for (int start = 0; start < n; start += blockDim.x) {
-    const int q = start + threadIdx.x;
-    const int node = q < n ? m.slide[q] : -1;
-    const int keep = (node >= 0 && m.in_slide[node]) ? 1 : 0;
-    sc[threadIdx.x] = keep;
+  if (n >= thread_num) {
+    if (threadIdx.x == 0) base = 0;
     __syncthreads();
-    for (int off = 1; off < (int)blockDim.x; off <<= 1) {
-      int v = threadIdx.x >= (unsigned)off ? sc[threadIdx.x - off] : 0;
+    for (int start = 0; start < n; start += blockDim.x) {
+      const int q = start + threadIdx.x;
+      const int node = q < n ? m.slide[q] : -1;
+      const int keep = (node >= 0 && m.in_slide[node]) ? 1 : 0;
+      sc[threadIdx.x] = keep;
       __syncthreads();
-      sc[threadIdx.x] += v;
+      for (int off = 1; off < (int)blockDim.x; off <<= 1) {
+        int v = threadIdx.x >= (unsigned)off ? sc[threadIdx.x - off] : 0;
+        __syncthreads();
+        sc[threadIdx.x] += v;
+        __syncthreads();
+      }
+      if (keep) m.slide[base + sc[threadIdx.x] - 1] = node;
+      __syncthreads();
+      if (threadIdx.x == blockDim.x - 1) base += sc[threadIdx.x];
       __syncthreads();
     }
-    if (keep) m.slide[base + sc[threadIdx.x] - 1] = node;
-    __syncthreads();
-    if (threadIdx.x == blockDim.x - 1) base += sc[threadIdx.x];
-    __syncthreads();
+    if (threadIdx.x == 0) m.counters[kCntSlide] = base;
   }
-  if (threadIdx.x == 0) m.counters[kCntSlide] = base;
+  const int t = threadIdx.x;
+  const double v = (t < (wc - 1) * kXS) ? st->xs[kXS + t] : 0.0;
+  const double b = (t < (nimu - 1) * 12) ? st->bias[12 + t] : 0.0;
+  __syncthreads();
+  if (t < (wc - 1) * kXS) st->xs[t] = v;
+  if (t < (nimu - 1) * 12) st->bias[t] = b;
+  if (seq2 > 0) {
+    __syncthreads();
+    if (t < kCntN) __hip_atomic_store(&pub->counters[t], m.counters[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    if (t == 0) {
+      __threadfence_system();
+      __hip_atomic_store(&pub->seq2, seq2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
-__global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, double j) {
+__global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, double j, int* __restrict__ rc) {
+  if (blockIdx.x == 0) {  // margi level counts and the leaf count start at zero
+    for (int i = threadIdx.x; i < kRcN; i += blockDim.x) rc[i] = 0;
+    if (threadIdx.x == 0) m.counters[kCntLeaves] = 0;
+  }
   const int n = m.counters[kCntSlide];
   if (n < thread_num) return;
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) m.jour[m.slide[q]] = j;
@@ -1802,7 +1835,7 @@ __global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, doub
 // the host enqueues max_layer+1 levels (no level can be deeper) and
 // synchronises once at the end for the error flags.
 int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, double jour,
-              int pub_seq) {
+              int pub_seq, int pub_seq2) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
@@ -1813,10 +1846,8 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   // for this scan and is published before the margi kernels run
   VG_TRY(state_make_win(ctx, wa, dwin, dn, dn + 32));
   if (pub_seq > 0) VG_TRY(state_publish(ctx, wa.win_count, ba_iters_dev(ctx), pub_seq));
-  VG_HIP(hipMemsetAsync(w.rc, 0, kRcN * sizeof(int), s));
-  VG_HIP(hipMemsetAsync(m.counters + kCntLeaves, 0, sizeof(int), s));
   const int gl = 64;  // grid-stride over device-side counts
-  k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour);
+  k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour, w.rc);
   for (int L = 0; L < nlev; L++) k_collect_level<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.list0, w.rc);
   // oldest slot segments by leaf (the slot's point count is known on the host)
   const int s0 = wa.mp[0];
@@ -1828,11 +1859,18 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   k_margi_leaf<<<gl, kBlock, 0, s>>>(m.counters + kCntLeaves, w.list0, mp, dwin, m, ctx->ba.fac_eig, ctx->ba.fac_pcr,
                                      w.plan);
   k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, w.k1, dwin, m);
-  if (n_oldest > 0) k_margi_segs_clear<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, w.k1, m);
-  for (int L = nlev - 1; L >= 0; L--) k_margi_internal<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc);
+  for (int L = nlev - 1; L >= 1; L--)
+    k_margi_internal<<<L == nlev - 1 ? 128 : gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc,
+                                                                L == nlev - 1 ? n_oldest : 0, w.k1);
+  if (nlev == 1 && n_oldest > 0) k_margi_internal<<<128, kBlock, 0, s>>>(-1, 1 << 30, m, w.list1, w.rc, n_oldest, w.k1);
   for (int L = 0; L < nlev; L++) k_margi_erase_mark<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc);
-  for (int L = 0; L < nlev; L++) k_clear_mark<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc);
-  k_slide_compact<<<1, 1024, 0, s>>>(thread_num, m);
+  k_clear_mark<<<gl, kBlock, 0, s>>>(nlev - 2, nlev, thread_num, m, w.list1, w.rc);
+  // slide list compaction, the device-state slide, the counter publication
+  if (wa.win_count * kXS > 1024) {
+    ctx->err = "win_size too large for the state slide";
+    return VG_E_ARG;
+  }
+  k_slide_compact<<<1, 1024, 0, s>>>(thread_num, m, ctx->st, wa.win_count, mp.W - 1, ctx->d_pub, pub_seq2);
   VG_HIP(hipGetLastError());
   return VG_OK;  // device error flags reach the host with the end-of-scan counters
 }

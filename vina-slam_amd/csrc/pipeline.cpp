@@ -63,7 +63,7 @@ struct HImuPre {
   V3 p_delta = V3::Z(), v_delta = V3::Z(), bg, ba;
   double dtime = 0;
   M15 cov = M15::Z();
-  double bias[12] = {0};  // dbg, dba, dbg_buf, dba_buf
+  std::vector<double> rec;  // the BA's device record, fixed once integrated (record())
   HImuPre(const V3& bg1, const V3& ba1) : bg(bg1), ba(ba1) {}
   void add_imu(V3 gyr, V3 acc, double dt, const M6& nm, const M6& nw) {  // imu_preintegration.cpp:57-95
     dtime += dt;
@@ -501,10 +501,11 @@ static int resolve_ds(vg_ctx* ctx, HostPipe* P) {
   }
   int n_ds = ctx->h_pub->n_ds;
   if (n_ds < 2000) {
-    prof_begin(ctx, kProfDownsample);
+    prof_begin(ctx, kProfDownsample, ctx->stream_ds);
     P->ds_seq = ++ctx->pub_seq;
-    VG_TRY(ds_enqueue(ctx, P->sx, P->sy, P->sz, P->si, P->n_raw, c.down_size / 2, P->ds_seq));
-    prof_end(ctx, kProfDownsample);
+    VG_TRY(ds_enqueue(ctx, ctx->stream_ds, P->sx, P->sy, P->sz, P->si, P->n_raw, c.down_size / 2, P->ds_seq));
+    prof_end(ctx, kProfDownsample, ctx->stream_ds);
+    VG_HIP(hipEventRecord(ctx->ev_ds_done, ctx->stream_ds));
     VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ds, P->ds_seq, "downsample"));
     if (ctx->h_pub->ds_err) {
       ctx->err = "voxel key out of packed range (|key| >= 2^20)";
@@ -531,11 +532,14 @@ int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float*
   P->si = di;
   P->n_raw = n;
   P->cur.st.n_raw = n;
-  prof_begin(ctx, kProfDownsample);
+  // own stream: waits only until the previous insert has read the ds buffers
+  VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_ds_free, 0));
+  prof_begin(ctx, kProfDownsample, ctx->stream_ds);
   P->ds_seq = ++ctx->pub_seq;
   P->ds_n = -1;
-  VG_TRY(ds_enqueue(ctx, dx, dy, dz, di, n, c.down_size, P->ds_seq));
-  prof_end(ctx, kProfDownsample);
+  VG_TRY(ds_enqueue(ctx, ctx->stream_ds, dx, dy, dz, di, n, c.down_size, P->ds_seq));
+  prof_end(ctx, kProfDownsample, ctx->stream_ds);
+  VG_HIP(hipEventRecord(ctx->ev_ds_done, ctx->stream_ds));
   if (n_ds_out) {
     VG_TRY(resolve_ds(ctx, P));
     *n_ds_out = P->ds_n;
@@ -576,6 +580,8 @@ int stage_window_push(vg_ctx* ctx, const double* imu, int m) {
     const HX& xb = P->x_buf[P->win_count - 2];
     P->imu_pre.emplace_back(xb.bg, xb.ba);
     P->imu_pre.back().push_imu(to_imus(imu, m), P->noiseMeas, P->noiseWalk);
+    P->imu_pre.back().rec.resize(kBaImuRec);
+    P->imu_pre.back().record(P->imu_pre.back().rec.data());  // off the BA's critical path
     new_imu = P->win_count - 2;
   }
   return state_push(ctx, P->win_count - 1, new_imu);
@@ -599,9 +605,11 @@ int stage_insert(vg_ctx* ctx) {
   const int ord = P->win_count - 1;
   const int slot = P->mp[ord];
   P->epoch++;
+  VG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_ds_done, 0));
   prof_begin(ctx, kProfInsert);
   VG_TRY(map_insert(ctx, P->mpd, slot, P->ds_n, P->epoch, c.thread_num));
   prof_end(ctx, kProfInsert);
+  VG_HIP(hipEventRecord(ctx->ev_ds_free, ctx->stream));  // k_ins_prep has read the ds buffers
   P->wp_n[slot] = P->ds_n;
   P->ins_slot = slot;
   P->ins_n = P->ds_n;
@@ -639,7 +647,7 @@ int stage_ba(vg_ctx* ctx, int* iters_out) {
     return VG_E_STATE;
   }
   std::vector<double> rec((size_t)(W - 1) * kBaImuRec);
-  for (int j = 0; j < W - 1; j++) P->imu_pre[j].record(&rec[(size_t)j * kBaImuRec]);
+  for (int j = 0; j < W - 1; j++) memcpy(&rec[(size_t)j * kBaImuRec], P->imu_pre[j].rec.data(), kBaImuRec * 8);
   int iters = 0;
   prof_begin(ctx, kProfBA);
   VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), rec.data(), &iters));
@@ -661,12 +669,12 @@ int stage_margi_slide(vg_ctx* ctx) {
   }
   VG_TRY(need_open(ctx, P, "vg_multi_margi"));
   const WinArg wa = make_winarg(P, 1);
-  const int seq1 = ++ctx->pub_seq;
+  const int seq1 = ++ctx->pub_seq, seq2 = ++ctx->pub_seq;
   prof_begin(ctx, kProfMargi);
-  VG_TRY(map_margi(ctx, P->mpd, wa, P->wp_n[P->mp[0]], c.thread_num, P->jour, seq1));
+  VG_TRY(map_margi(ctx, P->mpd, wa, P->wp_n[P->mp[0]], c.thread_num, P->jour, seq1, seq2));
   prof_end(ctx, kProfMargi);
-  VG_TRY(state_slide(ctx, P->win_count, W - 1));
   P->cur.seq1 = seq1;
+  P->cur.seq2 = seq2;
   P->cur.shift = 1;
   P->published = true;
   const int mgsize = 1;
@@ -692,8 +700,10 @@ int stage_finish(vg_ctx* ctx) {
     P->cur.seq1 = ++ctx->pub_seq;
     VG_TRY(state_publish(ctx, P->win_count, nullptr, P->cur.seq1));
   }
-  P->cur.seq2 = ++ctx->pub_seq;
-  VG_TRY(state_publish_counters(ctx, P->cur.seq2));
+  if (P->cur.seq2 == 0) {
+    P->cur.seq2 = ++ctx->pub_seq;
+    VG_TRY(state_publish_counters(ctx, P->cur.seq2));
+  }
   P->pend.push_back(P->cur);
   P->in_scan = false;
   P->first = false;

@@ -142,10 +142,11 @@ __global__ void k_publish_counters(const int* __restrict__ counters, Pub* __rest
 }
 
 // downsample result (n_out, range error) -> host
-__global__ void k_publish_ds(const int* __restrict__ flags, Pub* __restrict__ pub, int seq) {
+__global__ void k_publish_ds(int* __restrict__ flags, Pub* __restrict__ pub, int seq) {
   if (threadIdx.x == 0) {
     pub_store(&pub->ds_err, flags[0]);
     pub_store(&pub->n_ds, flags[1]);
+    flags[0] = 0;  // ready for the next run
     pub_flag(&pub->seq_ds, seq);
   }
 }
@@ -203,8 +204,8 @@ int state_publish_counters(vg_ctx* ctx, int seq) {
   return VG_OK;
 }
 
-int state_publish_ds(vg_ctx* ctx, int seq) {
-  k_publish_ds<<<1, 64, 0, ctx->stream>>>(ctx->ds.flags, ctx->d_pub, seq);
+int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq) {
+  k_publish_ds<<<1, 64, 0, s>>>(ctx->ds.flags, ctx->d_pub, seq);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }

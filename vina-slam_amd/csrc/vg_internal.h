@@ -199,6 +199,10 @@ struct vg_ctx {
   vg_capacity cap;
   int device = 0;
   hipStream_t stream = nullptr;
+  // the downsample runs on its own stream: it reads only the raw scan, so it
+  // overlaps the previous scan's recut/BA/margi and this scan's IEKF
+  hipStream_t stream_ds = nullptr;
+  hipEvent_t ev_ds_done = nullptr, ev_ds_free = nullptr;
   std::string err;
   vg::Arena arena;
   // raw scan staging (SoA)
@@ -258,12 +262,12 @@ inline int pub_wait(vg_ctx* c, const int* flag, int seq, const char* what) {
 }
 enum { kProfDownsample = 0, kProfIekfKernel = 1, kProfInsert = 2, kProfRecut = 3, kProfBA = 4, kProfMargi = 5,
        kProfIekf = 6, kProfBaSolve = 7, kProfN = 8 };
-inline void prof_begin(vg_ctx* c, int id) {
-  if (c->prof_stages) (void)hipEventRecord(c->prof_ev[id][0], c->stream);
+inline void prof_begin(vg_ctx* c, int id, hipStream_t s = nullptr) {
+  if (c->prof_stages) (void)hipEventRecord(c->prof_ev[id][0], s ? s : c->stream);
 }
-inline void prof_end(vg_ctx* c, int id) {
+inline void prof_end(vg_ctx* c, int id, hipStream_t s = nullptr) {
   if (c->prof_stages) {
-    (void)hipEventRecord(c->prof_ev[id][1], c->stream);
+    (void)hipEventRecord(c->prof_ev[id][1], s ? s : c->stream);
     c->prof_pending[id] = true;
   }
 }
@@ -311,8 +315,8 @@ int ds_alloc(vg_ctx* ctx);
 int ds_run(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, int n, double voxel,
            int* n_out);
 // Same, asynchronous: n_out and the range flag are published to Pub (seq_ds).
-int ds_enqueue(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, int n, double voxel,
-               int pub_seq);
+int ds_enqueue(vg_ctx* ctx, hipStream_t s, const float* x, const float* y, const float* z, const float* in, int n,
+               double voxel, int pub_seq);
 // map.hip
 int map_alloc(vg_ctx* ctx);
 int map_reset(vg_ctx* ctx);
@@ -322,7 +326,10 @@ constexpr int kNeedInsertReplay = 1;  // map_recut: the insert overflowed k_ins_
 int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num);
 int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num);
 int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors);
-int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, double jour, int pub_seq);
+// multi_margi + the device-state slide; publishes the state (pub_seq, before
+// the margi kernels) and the end-of-scan counters (pub_seq2)
+int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, double jour, int pub_seq,
+              int pub_seq2);
 // state.hip
 int state_alloc(vg_ctx* ctx);
 int state_scan_begin(vg_ctx* ctx, const double* xc249);
@@ -331,7 +338,7 @@ int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* d
 int state_slide(vg_ctx* ctx, int win_count, int nimu);
 int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq);
 int state_publish_counters(vg_ctx* ctx, int seq);
-int state_publish_ds(vg_ctx* ctx, int seq);
+int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq);
 // ba.hip
 constexpr int kBaX = 24;        // per-frame state: R 9, p 3, v 3, bg 3, ba 3, g 3
 constexpr int kBaImuRec = 64 + 225;

@@ -41,6 +41,12 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     ctx->err = std::string("hipSetDevice: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
+  if ((e = hipStreamCreateWithFlags(&ctx->stream_ds, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_ds_done, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_ds_free, hipEventDisableTiming)) != hipSuccess) {
+    ctx->err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
+    return fail(VG_E_HIP);
+  }
   if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) {
     ctx->err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
@@ -136,6 +142,10 @@ int vg_destroy(vg_ctx* ctx) {
     for (int j = 0; j < 2; j++)
       if (ctx->solve_ev[i][j]) (void)hipEventDestroy(ctx->solve_ev[i][j]);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->stream_ds) (void)hipStreamSynchronize(ctx->stream_ds);
+  if (ctx->stream_ds) (void)hipStreamDestroy(ctx->stream_ds);
+  if (ctx->ev_ds_done) (void)hipEventDestroy(ctx->ev_ds_done);
+  if (ctx->ev_ds_free) (void)hipEventDestroy(ctx->ev_ds_free);
   delete ctx;
   return VG_OK;
 }
@@ -146,6 +156,7 @@ void* vg_stream(vg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 int vg_reset(vg_ctx* ctx) {
   if (!ctx) return VG_E_ARG;
+  VG_HIP(hipStreamSynchronize(ctx->stream_ds));
   VG_HIP(hipStreamSynchronize(ctx->stream));
   VG_TRY(map_reset(ctx));
   host_reset(ctx);
@@ -189,6 +200,7 @@ int vg_downsample(vg_ctx* ctx, const float* xyz, const float* intensity, int n, 
     return VG_OK;
   }
   if (n == 0) return VG_OK;
+  VG_HIP(hipStreamSynchronize(ctx->stream_ds));  // the pipeline's downsample shares the buffers
   VG_TRY(upload_aos(ctx, xyz, intensity, n));
   int m = 0;
   VG_TRY(ds_run(ctx, ctx->d_x, ctx->d_y, ctx->d_z, ctx->d_i, n, voxel_size, &m));
