@@ -121,6 +121,7 @@ def main():
     s_launch = sol["launches"]
     s_avg = sol["ms"] * 1e-3 / max(s_launch, 1)
     s_ach = flops / s_avg / 1e12 if s_avg > 0 else 0.0
+    host_ms = {k[5:]: round(v["ms"] / args.steps, 4) for k, v in prof.items() if k.startswith("host_")}
     roof = {"kernel": "k_ba_solve", "bound": "mfma", "achieved": round(s_ach, 5), "peak": 78.6, "unit": "TFLOP/s",
             "frac": round(s_ach / 78.6, 7), "traffic": None, "avg_launch_us": round(s_avg * 1e6, 3),
             "launches": s_launch, "flops_per_launch": int(flops), "stage_ms_per_scan": stage_ms}
@@ -158,7 +159,7 @@ def main():
                        "points_per_scan": npts, "downsampled_per_scan": int(np.mean([s["n_ds"] for s in stats])),
                        "factors_per_scan": int(np.mean([s["n_factors"] for s in stats])),
                        "parallelism": "replica x%d" % world},
-            "roofline": roof, "roofline_k_iekf": roof_iekf, "cpu_baseline": cpu,
+            "roofline": roof, "roofline_k_iekf": roof_iekf, "host_ms_per_scan": host_ms, "cpu_baseline": cpu,
         }
         print(json.dumps(line))
     ctx.close()

@@ -150,7 +150,8 @@ int vg_trajectory(vg_ctx* ctx, double* out, int cap, int* n);
 /* Stage timing with HIP events on the context stream (device time). stage:
  * 0 downsample, 1 IEKF point-loop kernel (k_iekf), 2 map insert, 3 recut +
  * factor extraction, 4 BA, 5 margi, 6 whole IEKF, 7 the LDL^T solve kernel
- * (k_ba_solve). `on`: 0 off, 1 the k_iekf and k_ba_solve launches only
+ * (k_ba_solve); 8..15 the HOST time of the stage calls (enqueue + waits):
+ * propagate, downsample, IEKF, window push, insert, recut, BA, margi. `on`: 0 off, 1 the k_iekf and k_ba_solve launches only
  * (stages 1 and 7; cheap enough for a timed region), 3 every stage.
  * vg_profile resets the accumulators; vg_profile_read returns total ms and the
  * number of intervals. */

@@ -548,7 +548,7 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
 // The backward solve runs blocked on wave 0. Rounding differs from Eigen's
 // sequential recurrences (tolerance-level; ties in |diag| may order
 // differently from its scan).
-__global__ void __launch_bounds__(512) k_ba_solve(int W, int nimu, const double* __restrict__ timg,
+__global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double* __restrict__ timg,
                                                   const double* __restrict__ bvec, const double* __restrict__ dvec,
                                                   const double* __restrict__ jvec, const int* __restrict__ ipg,
                                                   const double* __restrict__ xs, double* __restrict__ xt,
@@ -1044,7 +1044,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* i
     k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
                                     d.dvec, d.jvec, d.ipg, d.st);
     if (ctx->prof_on) (void)hipEventRecord(ctx->solve_ev[k][0], s);
-    k_ba_solve<<<1, 512, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
+    k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
                                          d.st);
     if (ctx->prof_on) (void)hipEventRecord(ctx->solve_ev[k][1], s);
     if (nf > 0 || nimu > 0)

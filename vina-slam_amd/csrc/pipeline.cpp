@@ -457,6 +457,7 @@ static int need_open(vg_ctx* ctx, HostPipe* P, const char* what) {
 // odom_ekf.process -> motion_blur state/covariance part (local_mapping.cpp:389);
 // opens the scan on the device (x_curr, x_prop, cov_inv)
 int stage_propagate(vg_ctx* ctx, const double* imu, int m, double end) {
+  HostTimer ht_(ctx, kHostPropagate);
   HostPipe* P = hp(ctx);
   if (P->in_scan) {
     ctx->err = "vg_propagate: previous scan not finished (vg_step_end)";
@@ -523,6 +524,7 @@ static int resolve_ds(vg_ctx* ctx, HostPipe* P) {
 // IEKF meanwhile
 int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n,
                      int* n_ds_out) {
+  HostTimer ht_(ctx, kHostDownsample);
   HostPipe* P = hp(ctx);
   VG_TRY(need_open(ctx, P, "vg_downsample_scan"));
   const vg_config& c = ctx->cfg;
@@ -549,6 +551,7 @@ int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float*
 
 // VNC_lio(no_ds_pptr) on the full cloud (local_mapping.cpp:408-430)
 int stage_iekf(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, int n, int* degenerate_out) {
+  HostTimer ht_(ctx, kHostIekf);
   HostPipe* P = hp(ctx);
   VG_TRY(need_open(ctx, P, "vg_lio_state_estimation"));
   prof_begin(ctx, kProfIekf);
@@ -565,6 +568,7 @@ int stage_iekf(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, i
 
 // x_buf / pvec_buf / imu_pre_buf push (local_mapping.cpp:434-441)
 int stage_window_push(vg_ctx* ctx, const double* imu, int m) {
+  HostTimer ht_(ctx, kHostPush);
   HostPipe* P = hp(ctx);
   VG_TRY(need_open(ctx, P, "vg_window_push"));
   if (P->win_count >= 32) {
@@ -589,6 +593,7 @@ int stage_window_push(vg_ctx* ctx, const double* imu, int m) {
 
 // pvec_update + cut_voxel_multi of the downsampled scan (local_mapping.cpp:425-448)
 int stage_insert(vg_ctx* ctx) {
+  HostTimer ht_(ctx, kHostInsert);
   HostPipe* P = hp(ctx);
   const vg_config& c = ctx->cfg;
   VG_TRY(need_open(ctx, P, "vg_cut_voxel_multi"));
@@ -618,6 +623,7 @@ int stage_insert(vg_ctx* ctx) {
 
 // multi_recut + tras_opt (local_mapping.cpp:451)
 int stage_recut(vg_ctx* ctx, int* nf_out) {
+  HostTimer ht_(ctx, kHostRecut);
   HostPipe* P = hp(ctx);
   const vg_config& c = ctx->cfg;
   VG_TRY(need_open(ctx, P, "vg_multi_recut"));
@@ -639,6 +645,7 @@ int stage_recut(vg_ctx* ctx, int* nf_out) {
 
 // LI_BA_Optimizer::damping_iter (local_mapping.cpp:492-497) on the device state
 int stage_ba(vg_ctx* ctx, int* iters_out) {
+  HostTimer ht_(ctx, kHostBA);
   HostPipe* P = hp(ctx);
   const int W = ctx->cfg.win_size;
   VG_TRY(need_open(ctx, P, "vg_damping_iter"));
@@ -660,6 +667,7 @@ int stage_ba(vg_ctx* ctx, int* iters_out) {
 // x_curr.R/p <- x_buf.back(), multi_margi, jour, mp[] rotation and buffer slide
 // (local_mapping.cpp:499-546)
 int stage_margi_slide(vg_ctx* ctx) {
+  HostTimer ht_(ctx, kHostMargi);
   HostPipe* P = hp(ctx);
   const vg_config& c = ctx->cfg;
   const int W = c.win_size;

@@ -5,6 +5,7 @@
 // arena) and the sliding-window state.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <chrono>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -232,9 +233,9 @@ struct vg_ctx {
   int iekf_ring_n = 0, iekf_ring_base = 0;
   hipEvent_t solve_ev[10][2] = {};  // k_ba_solve launches of the current BA run (vg_profile)
   int dbg_apply_cap = -1;        // test knob (vgx_debug): recut apply event capacity
-  bool prof_pending[8] = {};
-  double prof_ms[8] = {};
-  int prof_n[8] = {};
+  bool prof_pending[16] = {};
+  double prof_ms[16] = {};  // [0, 8): device time (events); [8, 16): host time of the stage calls
+  int prof_n[16] = {};
 };
 
 namespace vg {
@@ -261,7 +262,22 @@ inline int pub_wait(vg_ctx* c, const int* flag, int seq, const char* what) {
   return VG_OK;
 }
 enum { kProfDownsample = 0, kProfIekfKernel = 1, kProfInsert = 2, kProfRecut = 3, kProfBA = 4, kProfMargi = 5,
-       kProfIekf = 6, kProfBaSolve = 7, kProfN = 8 };
+       kProfIekf = 6, kProfBaSolve = 7, kProfN = 8,
+       // host (CPU) time spent in the stage calls: enqueue work plus any wait
+       kHostPropagate = 8, kHostDownsample = 9, kHostIekf = 10, kHostPush = 11, kHostInsert = 12, kHostRecut = 13,
+       kHostBA = 14, kHostMargi = 15, kProfAll = 16 };
+// host-time scope for a stage call (vg_profile bit 0)
+struct HostTimer {
+  vg_ctx* c;
+  int id;
+  std::chrono::steady_clock::time_point t0;
+  HostTimer(vg_ctx* ctx, int i) : c(ctx), id(i), t0(std::chrono::steady_clock::now()) {}
+  ~HostTimer() {
+    if (!c->prof_on) return;
+    c->prof_ms[id] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->prof_n[id] += 1;
+  }
+};
 inline void prof_begin(vg_ctx* c, int id, hipStream_t s = nullptr) {
   if (c->prof_stages) (void)hipEventRecord(c->prof_ev[id][0], s ? s : c->stream);
 }

@@ -376,7 +376,7 @@ int vg_profile(vg_ctx* ctx, int on) {
   ctx->prof_on = (on & 1) != 0;
   ctx->prof_stages = (on & 2) != 0;
   ctx->iekf_ring_n = 0;
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < vg::kProfAll; i++) {
     ctx->prof_ms[i] = 0;
     ctx->prof_n[i] = 0;
     ctx->prof_pending[i] = false;
@@ -385,7 +385,7 @@ int vg_profile(vg_ctx* ctx, int on) {
 }
 
 int vg_profile_read(vg_ctx* ctx, int stage, double* total_ms, int* count) {
-  if (!ctx || stage < 0 || stage >= vg::kProfN || !total_ms || !count) return VG_E_ARG;
+  if (!ctx || stage < 0 || stage >= vg::kProfAll || !total_ms || !count) return VG_E_ARG;
   *total_ms = ctx->prof_ms[stage];
   *count = ctx->prof_n[stage];
   return VG_OK;

@@ -228,7 +228,9 @@ class Context:
     def win_count(self):
         return self._int_call(lib().vg_win_count, "vg_win_count")
 
-    PROFILE_STAGES = ["downsample", "iekf", "insert", "recut", "ba", "margi", "iekf_total", "ba_solve"]
+    PROFILE_STAGES = ["downsample", "iekf", "insert", "recut", "ba", "margi", "iekf_total", "ba_solve",
+                      "host_propagate", "host_downsample", "host_iekf", "host_push", "host_insert", "host_recut",
+                      "host_ba", "host_margi"]
 
     def profile(self, on=True, stages=False):
         """on: k_iekf launch events; stages: per-stage events as well."""
