@@ -72,6 +72,7 @@ typedef struct vg_stats {
 } vg_stats;
 
 typedef struct vg_ctx vg_ctx;
+typedef int (*vg_host_allreduce_fn)(void* buf, int count, int dtype, void* user);
 
 /* Context lifecycle. Replaces the VINA_SLAM members surf_map, surf_map_slide,
  * sws, x_buf, pvec_buf, imu_pre_buf (node.hpp:34-70). device = HIP ordinal. */
@@ -146,6 +147,27 @@ int vg_win_count(vg_ctx* ctx, int* n);
  * local_mapping.cpp:427-430): n rows of 13 doubles [t, R row-major 9, p 3].
  * Copies min(n, cap) rows; *n = total rows. out may be NULL to query. */
 int vg_trajectory(vg_ctx* ctx, double* out, int cap, int* n);
+
+/* ---- Spatial-tile sharding (north_star: the voxel map shards by spatial tile
+ * across the GPUs of one node, with an all-reduce of the normal equations).
+ * One context per GPU runs the SAME sequence; each keeps only the root voxels
+ * of its tiles (16^3 root voxels, owner = hash(tile) mod world) and sums only
+ * its own points and factors. Per IEKF iteration the 34-value normal-equation
+ * block is all-reduced, per LM iteration the 6W x 6W LiDAR Hessian + gradient
+ * and the residual; three integer counts keep the reference's thread_num
+ * quirks global. State and IMU factors are replicated, so every rank computes
+ * the identical trajectory. Call once, before the first scan.
+ *   vg_shard_rccl: RCCL communicator inside the library, collectives ordered on
+ *                  the context stream (ncclAllReduce, no host synchronisation);
+ *                  id128 from vg_rccl_unique_id on rank 0, broadcast by the caller.
+ *   vg_shard_host: host callback fn(buf, count, dtype, user) summing `count`
+ *                  elements of host memory in place across ranks (dtype 0 =
+ *                  double, 1 = int32); the library stages through pinned memory
+ *                  and synchronises the stream around each call (tests, CPU-
+ *                  mediated transports). */
+int vg_rccl_unique_id(void* id128);
+int vg_shard_rccl(vg_ctx* ctx, int rank, int world, const void* id128);
+int vg_shard_host(vg_ctx* ctx, int rank, int world, vg_host_allreduce_fn fn, void* user);
 
 /* Stage timing with HIP events on the context stream (device time). stage:
  * 0 downsample, 1 IEKF point-loop kernel (k_iekf), 2 map insert, 3 recut +

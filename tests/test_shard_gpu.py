@@ -1,0 +1,93 @@
+"""Spatial-tile sharding of one sequence (include/vina_gpu.h vg_shard_*), two
+ranks on the one GPU of the test box with the host-callback transport over
+torch.distributed gloo (RCCL needs one GPU per rank; the bench's tile mode uses
+RCCL). Every rank must produce the unsharded trajectory (the state is
+replicated; only the fp summation order of the all-reduced sums differs), and
+the per-rank map counts must add up to the unsharded ones (each root voxel
+lives on exactly one rank)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import synth
+import vgconfig
+import vgpu
+
+pytestmark = pytest.mark.gpu
+CAP = dict(max_points=120_000, max_nodes=600_000, max_fix_points=2_000_000, hash_log2=20)
+NSCAN = 16
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(cfgname, rank, world, q, port):
+    import torch
+    import torch.distributed as dist
+    tag = rank if world > 1 else "single"
+    try:
+        p = vgconfig.load(cfgname)
+        g = p["General"]
+        seq = synth.Sequence("16line", 2, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
+        ctx = vgpu.Context(vgconfig.to_c(p), **CAP)
+        if world > 1:
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+
+            def allreduce(arr):
+                dist.all_reduce(torch.from_numpy(arr))
+
+            ctx.shard_host(rank, world, allreduce)
+        ctx.seed(seq.gt_state(0))
+        for k in range(NSCAN):
+            xyz, it, b, e = seq.scan(k)
+            ctx.step(xyz, it, b, e, seq.imu(k))
+        q.put((tag, ctx.trajectory(), ctx.stats_log()))
+        ctx.close()
+        if world > 1:
+            dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((tag, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("cfgname", ["mid360", "HILTI"])
+def test_two_shards_match_one(cfgname):
+    import torch.multiprocessing as mp
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _port()
+    procs = [ctxm.Process(target=_run, args=(cfgname, r, 2, q, port)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    _run(cfgname, 0, 1, q, port)  # the unsharded run, in this process
+    res = {}
+    for _ in range(3):
+        tag, tr, st = q.get(timeout=300)
+        assert not isinstance(tr, str), st
+        res[tag] = (tr, st)
+    for pr in procs:
+        pr.join(timeout=60)
+    (t1, s1), (ta, sa), (tb, sb) = res["single"], res[0], res[1]
+    assert len(s1) == len(sa) == len(sb) == NSCAN
+    for k, (a, b, c) in enumerate(zip(sa, sb, s1)):
+        print(k, "roots", a["roots_new"], b["roots_new"], c["roots_new"], "slide", a["n_slide"], b["n_slide"],
+              c["n_slide"], "factors", a["n_factors"], b["n_factors"], c["n_factors"])
+        assert a["roots_new"] + b["roots_new"] == c["roots_new"], k
+        assert a["n_slide"] + b["n_slide"] == c["n_slide"], k
+        assert a["n_factors"] + b["n_factors"] == c["n_factors"], k
+        assert a["iekf_iters"] == b["iekf_iters"] == c["iekf_iters"], k
+        assert a["ba_iters"] == b["ba_iters"] == c["ba_iters"], k
+        # the match count is part of the all-reduced normal equations: global on every rank
+        assert a["iekf_matches"] == b["iekf_matches"] == c["iekf_matches"], k
+    assert np.array_equal(ta, tb), "the ranks' trajectories must agree bit for bit"
+    err = synth.ate(t1, ta)
+    print("ATE sharded vs unsharded: %.3e m" % err)
+    assert err < 1e-4

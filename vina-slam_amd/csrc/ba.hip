@@ -816,6 +816,17 @@ __global__ void __launch_bounds__(256) k_ba_resid(int nf, int W, const int* __re
   if (threadIdx.x == 0) rpart[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
+// sharded mode: this shard's factor residual (ordered sum of the block partials)
+__global__ void k_ba_rsum(int nrb, const double* __restrict__ rpart, double* __restrict__ out,
+                          const BaState* __restrict__ st) {
+  if (threadIdx.x == 0) {
+    double r = 0.0;
+    if (!st->done)
+      for (int b = 0; b < nrb; b++) r += rpart[b];
+    out[0] = r;
+  }
+}
+
 // LM bookkeeping (optimizers.cpp:480-515)
 __global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, double imu_coef, const double* __restrict__ hl, int nl,
                              const double* __restrict__ imuout, const double* __restrict__ imures,
@@ -881,9 +892,12 @@ struct MpRing {
   int mp[kMaxW];
 };
 // LM state (optimizers.cpp:436-441), the reduced-Hessian accumulator, the ring
-__global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict__ hl, int nout, MpRing ring,
-                                                 int* __restrict__ mpring, int W) {
-  for (int t = threadIdx.x; t < nout; t += blockDim.x) hl[t] = 0.0;
+__global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict__ hl, double* __restrict__ hl_part,
+                                                 int nout, MpRing ring, int* __restrict__ mpring, int W) {
+  for (int t = threadIdx.x; t < nout; t += blockDim.x) {
+    hl[t] = 0.0;
+    hl_part[t] = 0.0;
+  }
   if ((int)threadIdx.x < W) mpring[threadIdx.x] = ring.mp[threadIdx.x];
   if (threadIdx.x == 0) {
     st->u = 0.01;
@@ -939,6 +953,7 @@ int ba_alloc(vg_ctx* ctx) {
   good &= (b.fac_pcr = ctx->arena.take<Clu>(b.cap_f)) != nullptr;
   good &= (b.hpart = ctx->arena.take<double>((size_t)(b.cap_f / hess_chunk(W) + 1) * nout)) != nullptr;
   good &= (b.hout = ctx->arena.take<double>(nout + 16)) != nullptr;
+  good &= (b.hout_part = ctx->arena.take<double>(nout + 16)) != nullptr;
   good &= (b.rpart = ctx->arena.take<double>(b.cap_f / 256 + 16)) != nullptr;
   good &= (b.xs = ctx->arena.take<double>(1024 + 2 * n * (n + 1) / 2 + 4 * n + kMaxNB * (kMaxNB + 1) / 2 * 256 + 4 * kMaxNB * kTile + 2 * kMaxW * kX + kMaxW * kImuRec +
                                           kMaxW * 12 + kMaxW * 931 + kMaxW + 64)) != nullptr;
@@ -1025,7 +1040,10 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* i
   VG_HIP(hipMemcpyAsync(d.imurec, stage, (size_t)nimu * kImuRec * sizeof(double), hipMemcpyHostToDevice, s));
   MpRing ring;
   for (int i = 0; i < kMaxW; i++) ring.mp[i] = i < W ? mp_ring[i] : 0;
-  k_ba_init<<<1, 256, 0, s>>>(d.st, d.hl, nout, ring, d.mpring, W);
+  const bool sharded = ctx->shard.world > 1;
+  double* hl_part = ctx->ba.hout_part;  // this shard's LiDAR Hessian (sharded mode)
+  double* rsum = ctx->shard.d_buf + 256;  // [0]: this shard's residual, [1]: all-reduced
+  k_ba_init<<<1, 256, 0, s>>>(d.st, d.hl, hl_part, nout, ring, d.mpring, W);
   const int nchunk = (nf + hess_chunk(W) - 1) / hess_chunk(W);
   const int nrb = (nf + 255) / 256;
   const size_t hess_lds = hess_lds_bytes(W);
@@ -1033,6 +1051,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* i
   const int NBt = (15 * W + kTile - 1) / kTile, ntile = NBt * (NBt + 1) / 2;
   const int seq0 = ctx->pub_seq + 1;
   ctx->pub_seq += 10;
+  int xerr = VG_OK;  // exchange errors (sharded mode)
   // one LM iteration (optimizers.cpp:449-516); kernels early-exit on the
   // device-side flags once converged
   auto iteration = [&](int k) {
@@ -1040,7 +1059,10 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* i
       k_ba_hess<<<(nf > 0 ? nchunk : 0) + nimu, kHessThreads, hess_lds, s>>>(
           nf, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr, ctx->map.pcrs, d.mpring, d.xs, d.part, d.st,
           nf > 0 ? nchunk : 0, nimu, d.imurec, d.bias, d.imuout);
-    if (nf > 0) k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nchunk, nout, d.part, d.hl, d.st);
+    if (nf > 0) k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nchunk, nout, d.part, sharded ? hl_part : d.hl, d.st);
+    // sharded: every shard's factors -> one LiDAR Hessian / gradient / residual
+    // (out of place: a rejected step re-reduces the unchanged partial)
+    if (sharded && xerr == VG_OK) xerr = shard_allreduce(ctx, hl_part, d.hl, nout, 0);
     k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
                                     d.dvec, d.jvec, d.ipg, d.st);
     if (ctx->prof_on) (void)hipEventRecord(ctx->solve_ev[k][0], s);
@@ -1051,8 +1073,13 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* i
       k_ba_resid<<<(nf > 0 ? nrb : 0) + (nimu > 0 ? 1 : 0), 256, 0, s>>>(
           nf, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt, ctx->ba.fac_eig, ctx->ba.fac_pcr,
           d.rpart, d.st, nf > 0 ? nrb : 0, nimu, d.imurec, d.bias, d.imures);
-    k_ba_control<<<1, 256, 0, s>>>(W, nimu, nf > 0 ? nrb : 0, ctx->cfg.imu_coef, d.hl, nl + L, d.imuout, d.imures,
-                                   d.rpart, d.xs, d.xt, d.bias, d.st, ctx->d_pub, seq0 + k);
+    if (sharded) {  // the residual over every shard's factors
+      k_ba_rsum<<<1, 64, 0, s>>>(nf > 0 ? nrb : 0, d.rpart, rsum, d.st);
+      if (xerr == VG_OK) xerr = shard_allreduce(ctx, rsum, rsum + 1, 1, 0);
+    }
+    k_ba_control<<<1, 256, 0, s>>>(W, nimu, sharded ? 1 : (nf > 0 ? nrb : 0), ctx->cfg.imu_coef, d.hl, nl + L,
+                                   d.imuout, d.imures, sharded ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st,
+                                   ctx->d_pub, seq0 + k);
   };
   // One iteration ahead: iteration k+1 is enqueued before the host waits for
   // iteration k's flags, so the stream never drains; a converged LM leaves at
@@ -1062,6 +1089,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* i
   for (int k = 0; k < 10; k++) {
     if (k + 1 < 10) iteration(k + 1);
     VG_HIP(hipGetLastError());
+    VG_TRY(xerr);
     VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ba, seq0 + k, "k_ba_control"));
     done_iters = __atomic_load_n(&ctx->h_pub->ba_iters, __ATOMIC_ACQUIRE);
     if (__atomic_load_n(&ctx->h_pub->ba_done, __ATOMIC_ACQUIRE)) break;

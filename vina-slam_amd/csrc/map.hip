@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(256) k_iekf(int n, const float* __restrict__ x
       flag = match_leaf(m.hdr[leaf], m.pl[leaf], wld, var_world, sigma);
     } else {
       uint64_t key;
-      if (pack_key(wld, mp.vs, key)) {
+      if (pack_key(wld, mp.vs, key) && owns(m, key)) {  // another shard's tile: not matched here
         int root = hash_find(m.hkey, m.hval, m.hash_mask, key);
         int lf = root >= 0 ? descend(m.hdr, root, wld) : -1;
         if (lf >= 0) {
@@ -275,6 +275,14 @@ __global__ void __launch_bounds__(256) k_iekf_update(int nb, const double* __res
   if (st->done) return;
   iekf_update_block(nb, partials, st, it, L);
 }
+// sharded mode: this shard's 34 sums (the update then runs on the all-reduced ones)
+__global__ void __launch_bounds__(256) k_iekf_reduce(int nb, const double* __restrict__ partials,
+                                                     const DState* __restrict__ st, double* __restrict__ out) {
+  __shared__ IekfLds L;
+  if (st->done) return;
+  iekf_reduce_block(nb, partials, L);
+  if (threadIdx.x < kIekfVals) out[threadIdx.x] = L.o[threadIdx.x];
+}
 
 // one IEKF iteration: the point loop (block partials) and the update; the
 // optional event pair brackets k_iekf alone (vg_profile)
@@ -286,7 +294,14 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
   if (ev0) (void)hipEventRecord(ev0, s);
   k_iekf<<<nb, 256, 0, s>>>(n, x, y, z, mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials);
   if (ev1) (void)hipEventRecord(ev1, s);
-  k_iekf_update<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, it);
+  if (ctx->shard.world > 1) {  // this shard's sums, all-reduced, then the (replicated) update
+    double* sums = ctx->shard.d_buf;
+    k_iekf_reduce<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, sums);
+    VG_TRY(shard_allreduce(ctx, sums, sums + 64, kIekfVals, 0));
+    k_iekf_update<<<1, 256, 0, s>>>(-1, sums + 64, ctx->st, it);
+  } else {
+    k_iekf_update<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, it);
+  }
   VG_HIP(hipGetLastError());
   return VG_OK;
 }
@@ -328,6 +343,10 @@ __global__ void __launch_bounds__(256) k_ins_prep(int n, const float* __restrict
     uint64_t key;
     if (!pack_key(w, mp.vs, key)) {
       atomicOr(&m.counters[kCntErr], 1);
+      hslot[i] = 0xffffffffu;
+      continue;
+    }
+    if (!owns(m, key)) {  // another shard's tile (sharded mode)
       hslot[i] = 0xffffffffu;
       continue;
     }
@@ -416,7 +435,11 @@ __global__ void __launch_bounds__(256) k_ins_touch(int n, const uint32_t* __rest
 // thread_num roots (voxel_map.cpp:96-97: no allocation at all) or when the
 // child allocation overflowed k_ins_alloc (the host replays them)
 __device__ __forceinline__ bool ins_skip(const DevMap& m, int thread_num) {
-  return m.counters[kCntTouched] < thread_num || m.counters[kCntMisc] != 0;
+  return g_touched(m) < thread_num || m.counters[kCntMisc] != 0;
+}
+
+__global__ void k_copy_int(const int* __restrict__ src, int* __restrict__ dst) {
+  if (threadIdx.x == 0) *dst = *src;
 }
 
 __global__ void __launch_bounds__(256) k_ins_descend(int n, int thread_num, const double* __restrict__ pw, DevMap m,
@@ -659,7 +682,7 @@ constexpr int kInsAllocCap = 4096;
 __global__ void __launch_bounds__(1024) k_ins_alloc(int thread_num, DevMap m, const int* __restrict__ reqlist) {
   __shared__ int sp[kInsAllocCap];
   __shared__ int s_w[17];
-  if (m.counters[kCntTouched] < thread_num) return;
+  if (g_touched(m) < thread_num) return;
   const int np = m.counters[kCntCreate];
   if (np == 0) return;
   if (np > kInsAllocCap) {
@@ -799,6 +822,10 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread
   k_zero_nodes<<<grid_for(1 << 16), kBlock, 0, s>>>(0, m.counters + kCntNew, m.counters + kCntNodes, m.W, m.pl,
                                                   m.pcr_add, m.pcr_fix, m.cov_add, m.eig, m.jour, m.pcrs);
   k_ins_touch<<<g, kBlock, 0, s>>>(n, w.u0, epoch, m, w.leaf);
+  if (m.shard_world > 1) {  // the thread_num quirk counts distinct roots over all shards
+    k_copy_int<<<1, 64, 0, s>>>(m.counters + kCntTouched, m.counters + kCntGTouched);
+    VG_TRY(shard_allreduce(ctx, m.counters + kCntGTouched, m.counters + kCntGTouched, 1, 1));
+  }
   k_ins_descend<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.leaf, w.list2);
   k_ins_alloc<<<1, 1024, 0, s>>>(thread_num, m, w.list2);
   return insert_tail(ctx, mp, slot, n, thread_num);
@@ -871,7 +898,7 @@ __global__ void __launch_bounds__(256) k_rc_visit(int L, int thread_num, const i
                                                   int* __restrict__ cand, int* __restrict__ rc) {
   if (rc[kRcAbort]) return;
   const int nw = (L == 0) ? m.counters[kCntSlide] : rc[kRcLvl + L - 1];
-  if (L == 0 && nw < thread_num) return;  // local_mapping.cpp:150-154
+  if (L == 0 && g_slide(m) < thread_num) return;  // local_mapping.cpp:150-154 (global count)
   const int* work = (L == 0) ? m.slide : work_in;
   for (int base = blockIdx.x * blockDim.x; base < nw; base += gridDim.x * blockDim.x) {
     const int q = base + threadIdx.x;
@@ -1393,14 +1420,15 @@ __global__ void k_recut_begin(DevMap m, int* __restrict__ rc, int thread_num) {
   __syncthreads();
   if (t == 0) {
     m.counters[kCntFactors] = 0;
-    if (m.counters[kCntMisc] != 0 && m.counters[kCntTouched] >= thread_num) rc[kRcAbort] = kInsAbort;
+    m.counters[kCntGSlide] = m.counters[kCntSlide];  // all-reduced next in sharded mode
+    if (m.counters[kCntMisc] != 0 && g_touched(m) >= thread_num) rc[kRcAbort] = kInsAbort;
   }
 }
 
 // multi_recut (local_mapping.cpp:144-201) then tras_opt. Returns the factor
 // count, or kNeedInsertReplay when the preceding insert must be replayed first
 // (nothing of the recut ran).
-int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors) {
+int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
@@ -1413,6 +1441,12 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* 
   int total = 0;
   for (int i = 0; i < wa.win_count; i++) total += wa.nper[i];
   k_recut_begin<<<1, 128, 0, s>>>(m, w.rc, thread_num);
+  if (m.shard_world > 1) {
+    if (!replay) {  // the global slide count (a replay re-uses it: the insert replay does not change it)
+      VG_TRY(shard_allreduce(ctx, m.counters + kCntGSlide, ctx->shard.d_buf + 512, 1, 1));
+    }
+    k_copy_int<<<1, 64, 0, s>>>((const int*)(ctx->shard.d_buf + 512), m.counters + kCntGSlide);
+  }
   const int nlev = mp.max_layer + 1;  // children sit one layer down; leaves at max_layer do not subdivide
   auto list_of = [&](int L) { return (L % 2 == 1) ? w.list0 : w.list1; };  // worklist of level L >= 1
   const int gv = 256, gw = grid_for(total > 0 ? total : 1);
@@ -1481,7 +1515,7 @@ __device__ __forceinline__ int margi_level(int L, const DevMap& m, const int* rc
 
 __global__ void __launch_bounds__(256) k_collect_level(int L, int thread_num, DevMap m, int* __restrict__ lists,
                                                        int* __restrict__ leaves, int* __restrict__ rc) {
-  if (m.counters[kCntSlide] < thread_num) return;
+  if (g_slide(m) < thread_num) return;
   int* work;
   const int nw = margi_level(L, m, rc, lists, &work);
   int* next;
@@ -1724,7 +1758,7 @@ __global__ void __launch_bounds__(256) k_margi_internal(int L, int thread_num, D
     m.nscr[(size_t)l * 4 + 0] = -1;
     m.nscr[(size_t)l * 4 + 1] = -1;
   }
-  if (m.counters[kCntSlide] < thread_num) return;
+  if (g_slide(m) < thread_num) return;
   int* work;
   const int nw = margi_level(L, m, rc, lists, &work);
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) internal_exist(m, work[q]);
@@ -1736,7 +1770,7 @@ __global__ void __launch_bounds__(256) k_margi_internal(int L, int thread_num, D
 // level L also resets the dead marks of level L-2, which nobody reads any more.
 __global__ void __launch_bounds__(256) k_margi_erase_mark(int L, int thread_num, DevMap m, int* __restrict__ lists,
                                                           const int* __restrict__ rc) {
-  if (m.counters[kCntSlide] < thread_num) return;
+  if (g_slide(m) < thread_num) return;
   int* work;
   const int nw = margi_level(L, m, rc, lists, &work);
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += gridDim.x * blockDim.x) {
@@ -1765,7 +1799,7 @@ __global__ void __launch_bounds__(256) k_margi_erase_mark(int L, int thread_num,
 // reset the dead marks of levels L0 .. nlev-1
 __global__ void __launch_bounds__(256) k_clear_mark(int L0, int nlev, int thread_num, DevMap m,
                                                     int* __restrict__ lists, const int* __restrict__ rc) {
-  if (m.counters[kCntSlide] < thread_num) return;
+  if (g_slide(m) < thread_num) return;
   for (int L = L0 < 0 ? 0 : L0; L < nlev; L++) {
     int* work;
     const int nw = margi_level(L, m, rc, lists, &work);
@@ -1783,7 +1817,7 @@ __global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m
   __shared__ int base;
   __shared__ int sc[1024];
   const int n = m.counters[kCntSlide];
-  if (n >= thread_num) {
+  if (g_slide(m) >= thread_num) {
     if (threadIdx.x == 0) base = 0;
     __syncthreads();
     for (int start = 0; start < n; start += blockDim.x) {
@@ -1827,7 +1861,7 @@ __global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, doub
     if (threadIdx.x == 0) m.counters[kCntLeaves] = 0;
   }
   const int n = m.counters[kCntSlide];
-  if (n < thread_num) return;
+  if (g_slide(m) < thread_num) return;
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) m.jour[m.slide[q]] = j;
 }
 

@@ -631,9 +631,9 @@ int stage_recut(vg_ctx* ctx, int* nf_out) {
   int nf = 0;
   prof_begin(ctx, kProfRecut);
   int r = map_recut(ctx, P->mpd, wa, c.thread_num, &nf);
-  if (r == kNeedInsertReplay) {
+  if (r == kNeedInsertReplay) {  // per shard; the replayed recut has no collective
     VG_TRY(map_insert_replay(ctx, P->mpd, P->ins_slot, P->ins_n, c.thread_num));
-    r = map_recut(ctx, P->mpd, wa, c.thread_num, &nf);
+    r = map_recut(ctx, P->mpd, wa, c.thread_num, &nf, true);
   }
   VG_TRY(r);
   prof_end(ctx, kProfRecut);

@@ -67,6 +67,28 @@ __device__ __forceinline__ int hash_insert(uint64_t* hkey, int mask, uint64_t ke
   return -1;
 }
 
+// owner rank of the 16^3-root-voxel tile holding a packed root key
+// (shard.cpp tile_owner_host is the same function)
+__host__ __device__ __forceinline__ int tile_owner(uint64_t key, int world) {
+  const uint64_t tx = (key >> 46) & 0x1ffff, ty = (key >> 25) & 0x1ffff, tz = (key >> 4) & 0x1ffff;
+  uint64_t h = (tx * 0x9E3779B97F4A7C15ull) ^ (ty * 0xC2B2AE3D27D4EB4Full) ^ (tz * 0x165667B19E3779F9ull);
+  h ^= h >> 31;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 29;
+  return (int)(h % (uint64_t)world);
+}
+__device__ __forceinline__ bool owns(const DevMap& m, uint64_t key) {
+  return m.shard_world <= 1 || tile_owner(key, m.shard_world) == m.shard_rank;
+}
+// the thread_num quirks (voxel_map.cpp:96-97, local_mapping.cpp:27, 93, 150)
+// compare GLOBAL counts: the all-reduced copies in sharded mode
+__device__ __forceinline__ int g_touched(const DevMap& m) {
+  return m.shard_world > 1 ? m.counters[kCntGTouched] : m.counters[kCntTouched];
+}
+__device__ __forceinline__ int g_slide(const DevMap& m) {
+  return m.shard_world > 1 ? m.counters[kCntGSlide] : m.counters[kCntSlide];
+}
+
 __device__ __forceinline__ int octant(const V3& p, const double* c) {
   return 4 * (p[0] > c[0] ? 1 : 0) + 2 * (p[1] > c[1] ? 1 : 0) + (p[2] > c[2] ? 1 : 0);
 }

@@ -25,7 +25,34 @@ struct IekfLds {
 };
 
 // One IEKF update after iteration `it`'s point loop wrote nb block partials
-// (row-major nb x kIekfVals). Whole workgroup (>= 256 threads), uniform.
+// (row-major nb x kIekfVals; nb < 0: `partials` is the final 34 sums). Whole
+// workgroup (>= 256 threads), uniform.
+// ordered sum of nb block partials (row-major nb x kIekfVals) into L.o: row
+// group g = tid / 17 (rows g, g+15, ...), lane pair 2*(tid % 17); then the 15
+// groups in order (deterministic)
+__device__ __forceinline__ void iekf_reduce_block(int nb, const double* __restrict__ partials, IekfLds& L) {
+  const int tid = threadIdx.x;
+  const int g = tid / 17, j2 = 2 * (tid % 17);
+  if (g < 15) {
+    double a0 = 0.0, a1 = 0.0;
+#pragma unroll 8
+    for (int b = g; b < nb; b += 15) {
+      const double2 v = *reinterpret_cast<const double2*>(&partials[(size_t)b * kIekfVals + j2]);
+      a0 += v.x;
+      a1 += v.y;
+    }
+    L.red[g][j2] = a0;
+    L.red[g][j2 + 1] = a1;
+  }
+  __syncthreads();
+  if (tid < kIekfVals) {
+    double s = L.red[0][tid];
+    for (int k = 1; k < 15; k++) s += L.red[k][tid];
+    L.o[tid] = s;
+  }
+  __syncthreads();
+}
+
 // 64-bit broadcast of lane `ln` (a compile-time constant after unrolling)
 __device__ __forceinline__ double bcast_lane(double v, int ln) {
   const long long b = __double_as_longlong(v);
@@ -38,25 +65,10 @@ __device__ void iekf_update_block(int nb, const double* __restrict__ partials, D
                                   IekfLds& L) {
   const int tid = threadIdx.x;
   VG_PROBE_BEGIN();
-  {  // ordered sum: row group g = tid / 17 (rows g, g+15, ...), lane pair 2*(tid % 17); then groups in order
-    const int g = tid / 17, j2 = 2 * (tid % 17);
-    if (g < 15) {
-      double a0 = 0.0, a1 = 0.0;
-#pragma unroll 8
-      for (int b = g; b < nb; b += 15) {
-        const double2 v = *reinterpret_cast<const double2*>(&partials[(size_t)b * kIekfVals + j2]);
-        a0 += v.x;
-        a1 += v.y;
-      }
-      L.red[g][j2] = a0;
-      L.red[g][j2 + 1] = a1;
-    }
-    __syncthreads();
-    if (tid < kIekfVals) {
-      double s = L.red[0][tid];
-      for (int k = 1; k < 15; k++) s += L.red[k][tid];
-      L.o[tid] = s;
-    }
+  if (nb >= 0) {
+    iekf_reduce_block(nb, partials, L);
+  } else {  // sharded mode: `partials` holds the all-reduced sums
+    if (tid < kIekfVals) L.o[tid] = partials[tid];
     __syncthreads();
   }
   const double* o = L.o;

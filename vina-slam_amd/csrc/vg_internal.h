@@ -94,6 +94,7 @@ constexpr int kCovN = 45;   // cov_add packed upper 9x9
 
 struct DevMap {
   int cap_nodes = 0, cap_fix = 0, hash_mask = 0, W = 0, cap_wp = 0;
+  int shard_rank = 0, shard_world = 1;  // spatial-tile sharding (shard.cpp)
   NodeHdr* hdr = nullptr;
   PlaneRec* pl = nullptr;
   Clu* pcr_add = nullptr;
@@ -119,7 +120,8 @@ struct DevMap {
 enum {
   kCntNodes = 0, kCntFix = 1, kCntSlide = 2, kCntNew = 3, kCntTouched = 4, kCntWork = 5, kCntNext = 6,
   kCntSub = 7, kCntEvents = 8, kCntFactors = 9, kCntCreate = 10, kCntErr = 11, kCntLeaves = 12, kCntMisc = 13, kCntSeg = 14, kCntRoots = 15,
-  kCntN = 16
+  kCntGTouched = 16, kCntGSlide = 17,  // all-reduced copies (sharded mode) for the thread_num quirks
+  kCntN = 18
 };
 
 // per-scan work buffers
@@ -150,6 +152,7 @@ struct BaBufs {
   Clu* fac_pcr = nullptr;      // trial merged cluster per factor
   double* hpart = nullptr;     // chunk partials
   double* hout = nullptr;      // reduced 60x60 upper + 60 + 1
+  double* hout_part = nullptr; // this shard's part of it (sharded mode)
   double* rpart = nullptr;
   double* xs = nullptr;        // window poses (W x 12: R9 p3)
 };
@@ -172,6 +175,21 @@ struct DState {
   double bias[kMaxWin * 12];        // IMU_PRE bias state per window factor: dbg, dba, dbg_buf, dba_buf
   int it, rematch, done, iters, degenerate, matches[4], ticket, pad[6];
 };
+// Spatial-tile sharding of one sequence over `world` contexts (one per GPU):
+// every context keeps the root voxels of the tiles it owns (tile_owner) and
+// sums only its own points / factors; the normal equations are all-reduced
+// (RCCL on the context stream, or a host callback for CPU-mediated tests).
+constexpr int kShardBuf = 4096;  // doubles of exchange scratch / staging
+struct Shard {
+  int rank = 0, world = 1;
+  int mode = 0;              // 0 none, 1 RCCL, 2 host callback
+  void* comm = nullptr;      // ncclComm_t
+  vg_host_allreduce_fn host_fn = nullptr;
+  void* user = nullptr;
+  double* h_buf = nullptr;   // pinned staging (host mode)
+  double* d_buf = nullptr;   // device scratch for the exchanged sums (4096 doubles)
+};
+
 // Host-mapped publication block (written by the device with system-scope
 // stores, each part closed by a sequence flag the host spins on).
 struct Pub {
@@ -216,6 +234,7 @@ struct vg_ctx {
   vg::Work wk;
   vg::BaBufs ba;
   vg::DState* st = nullptr;     // device-resident estimator state
+  vg::Shard shard;              // spatial-tile sharding across contexts (shard.cpp)
   vg::Pub* h_pub = nullptr;     // host-mapped publication block (host address)
   vg::Pub* d_pub = nullptr;     // its device address
   double* h_stage = nullptr;    // pinned staging for asynchronous H2D copies (kStageBytes)
@@ -341,7 +360,7 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
 constexpr int kNeedInsertReplay = 1;  // map_recut: the insert overflowed k_ins_alloc, replay it first
 int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num);
 int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num);
-int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors);
+int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay = false);
 // multi_margi + the device-state slide; publishes the state (pub_seq, before
 // the margi kernels) and the end-of-scan counters (pub_seq2)
 int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, double jour, int pub_seq,
@@ -375,6 +394,10 @@ int host_traj(vg_ctx* ctx, double* out, int cap);
 int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n, double beg,
               double end, const double* imu, int m);
 int host_win_count(vg_ctx* ctx);
+// shard.cpp
+int shard_alloc(vg_ctx* ctx);
+void shard_free(vg_ctx* ctx);
+int shard_allreduce(vg_ctx* ctx, const void* send, void* recv, int count, int dtype);
 int host_sync(vg_ctx* ctx);
 int host_stats_log(vg_ctx* ctx, vg_stats* out, int cap);
 int stage_propagate(vg_ctx* ctx, const double* imu, int m, double end);

@@ -63,6 +63,7 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     ctx->d_z = ctx->arena.take<float>(n);
     ctx->d_i = ctx->arena.take<float>(n);
     int r = state_alloc(ctx);
+    if (r == VG_OK) r = shard_alloc(ctx);
     if (r == VG_OK) r = ds_alloc(ctx);
     if (r == VG_OK) r = map_alloc(ctx);
     if (r == VG_OK) r = ba_alloc(ctx);
@@ -128,6 +129,7 @@ int vg_destroy(vg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->arena.base) (void)hipFree(ctx->arena.base);
   if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+  shard_free(ctx);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_pub) (void)hipHostFree(ctx->h_pub);
   if (ctx->host) host_free(ctx);

@@ -34,6 +34,18 @@ class Stats(ctypes.Structure):
                 ("pad1", ctypes.c_int)]
 
 
+# vg_host_allreduce_fn: int (*)(void* buf, int count, int dtype, void* user)
+HOST_ALLREDUCE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
+
+
+def rccl_unique_id():
+    buf = ctypes.create_string_buffer(128)
+    r = lib().vg_rccl_unique_id(buf)
+    if r != 0:
+        raise VgError("vg_rccl_unique_id failed (%d)" % r)
+    return buf.raw
+
+
 def build(jobs=8):
     subprocess.check_call(["make", "-s", "-j%d" % jobs, "-C", PKG])
 
@@ -85,6 +97,9 @@ def lib():
         L.vg_win_count.argtypes = [P, ip]
         L.vg_profile.argtypes = [P, ctypes.c_int]
         L.vg_profile_read.argtypes = [P, ctypes.c_int, dp, ip]
+        L.vg_rccl_unique_id.argtypes = [ctypes.c_char_p]
+        L.vg_shard_rccl.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]
+        L.vg_shard_host.argtypes = [P, ctypes.c_int, ctypes.c_int, HOST_ALLREDUCE, P]
         L.vg_stream.argtypes = [P]
         L.vg_stream.restype = P
         _lib = L
@@ -244,6 +259,26 @@ class Context:
             self._chk(lib().vg_profile_read(self.h, i, ctypes.byref(ms), ctypes.byref(n)), "vg_profile_read")
             out[name] = {"ms": ms.value, "launches": n.value}
         return out
+
+    def shard_rccl(self, rank, world, uid):
+        """Spatial-tile sharding over `world` contexts, RCCL inside the library."""
+        self._chk(lib().vg_shard_rccl(self.h, rank, world, uid), "vg_shard_rccl")
+
+    def shard_host(self, rank, world, allreduce):
+        """Spatial-tile sharding with a host all-reduce: allreduce(np.ndarray) sums
+        the array in place across ranks (e.g. torch.distributed gloo)."""
+        def cb(buf, count, dtype, user):
+            try:
+                ct = ctypes.c_double if dtype == 0 else ctypes.c_int32
+                arr = np.ctypeslib.as_array(ctypes.cast(buf, ctypes.POINTER(ct)), shape=(count,))
+                allreduce(arr)
+                return 0
+            except Exception:  # noqa: BLE001 - reported to the library as a failed exchange
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._cb = HOST_ALLREDUCE(cb)  # keep alive
+        self._chk(lib().vg_shard_host(self.h, rank, world, self._cb, None), "vg_shard_host")
 
     def stream(self):
         return lib().vg_stream(self.h)
