@@ -376,6 +376,7 @@ void cut_voxel_multi(MapParams* mpar, SurfMap& feat_map, PVec& pvec, int win_cou
   int plsize = (int)pvec.size();
   for (int i = 0; i < plsize; i++) {
     VOXEL_LOC position = voxel_key(pwld[i], mpar->voxel_size);
+    if (!shard_owns(mpar, position)) continue;  // another shard's tile (sharded mode)
     auto iter = feat_map.find(position);
     OctoTree* ot = nullptr;
     if (iter != feat_map.end()) {
@@ -402,7 +403,7 @@ void cut_voxel_multi(MapParams* mpar, SurfMap& feat_map, PVec& pvec, int win_cou
   }
   int thd_num = (int)sws.size();
   int g_size = (int)octs.size();
-  if (g_size < thd_num) return;
+  if (shard_count(mpar, g_size) < thd_num) return;  // voxel_map.cpp:96-97, over all shards
   double part = 1.0 * g_size / thd_num;
   int swsize = (int)sws[0].size() / thd_num;
   for (int i = 1; i < thd_num; i++) {
@@ -782,6 +783,20 @@ double LI_BA_Optimizer::divide_thread(std::vector<IMUST>& xs, LidarFactor& vox, 
   residual *= (mpar->imu_coef * 0.5);
   vox.acc_evaluate2(xs, 0, (int)part, hessians[0], jacobins[0], resis[0]);
   for (auto& t : th) t.join();
+  if (mpar->shard_world > 1) {  // this shard's LiDAR part, summed over the shards, then added
+    std::vector<double> l((size_t)jac_leng * jac_leng + jac_leng + 1, 0.0);
+    for (int i = 0; i < tthd_num; i++) {
+      for (size_t e = 0; e < (size_t)jac_leng * jac_leng; e++) l[e] += hessians[i].d[e];
+      for (int e = 0; e < jac_leng; e++) l[(size_t)jac_leng * jac_leng + e] += jacobins[i][e];
+      l.back() += resis[i];
+    }
+    shard_sum(mpar, l.data(), (int)l.size());
+    MatX hs(jac_leng, jac_leng);
+    for (size_t e = 0; e < (size_t)jac_leng * jac_leng; e++) hs.d[e] = l[e];
+    std::vector<double> js(l.begin() + (size_t)jac_leng * jac_leng, l.begin() + (size_t)jac_leng * jac_leng + jac_leng);
+    hess_plus(Hess, JacT, hs, js);
+    return residual + l.back();
+  }
   for (int i = 0; i < tthd_num; i++) {
     hess_plus(Hess, JacT, hessians[i], jacobins[i]);
     residual += resis[i];
@@ -812,6 +827,7 @@ double LI_BA_Optimizer::only_residual(std::vector<IMUST>& xs, LidarFactor& vox, 
   vox.evaluate_only_residual(xs, 0, (int)part, residuals[0]);
   for (auto& t : th) t.join();
   for (int i = 0; i < thd_num; i++) residual2 += residuals[i];
+  shard_sum(mpar, &residual2, 1);  // sharded mode: the factor residual over all shards
   return residual1 + residual2;
 }
 

@@ -25,7 +25,37 @@ struct MapParams {
   double imu_coef = 1e-4;                            // optimizers.cpp:8
   double imupre_scale_gravity = 1.0;                 // imu_preintegration.cpp:3
   M6 noiseMeas, noiseWalk;                           // imu_preintegration.cpp:4-5
+  // spatial-tile sharding; world 1 = the reference itself
+  int shard_rank = 0, shard_world = 1;
+  int (*allreduce)(double* buf, int n, void* user) = nullptr;  // in-place sum over ranks
+  void* ar_user = nullptr;
 };
+
+// owner rank of the 16^3-root-voxel tile of a root key (the product's
+// tile_owner, vina-slam_amd/csrc/vg_dev.h, on the same packed key)
+inline int tile_owner(const VOXEL_LOC& k, int world) {
+  const uint64_t off = 1ull << 20;
+  const uint64_t tx = (((uint64_t)(k.x + (int64_t)off)) >> 4) & 0x1ffff;
+  const uint64_t ty = (((uint64_t)(k.y + (int64_t)off)) >> 4) & 0x1ffff;
+  const uint64_t tz = (((uint64_t)(k.z + (int64_t)off)) >> 4) & 0x1ffff;
+  uint64_t h = (tx * 0x9E3779B97F4A7C15ull) ^ (ty * 0xC2B2AE3D27D4EB4Full) ^ (tz * 0x165667B19E3779F9ull);
+  h ^= h >> 31;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 29;
+  return (int)(h % (uint64_t)world);
+}
+inline bool shard_owns(const MapParams* m, const VOXEL_LOC& k) {
+  return m->shard_world <= 1 || tile_owner(k, m->shard_world) == m->shard_rank;
+}
+// sum over the ranks (no-op unsharded); counts travel as doubles (exact)
+inline void shard_sum(const MapParams* m, double* buf, int n) {
+  if (m->shard_world > 1 && m->allreduce) m->allreduce(buf, n, m->ar_user);
+}
+inline int shard_count(const MapParams* m, int local) {
+  double v = local;
+  shard_sum(m, &v, 1);
+  return (int)v;
+}
 
 // Plane — plane.hpp:5-24
 struct Plane {

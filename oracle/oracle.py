@@ -21,6 +21,10 @@ class Stats(ctypes.Structure):
                 ("n_factors", ctypes.c_int), ("ba_iters", ctypes.c_int), ("degenerate", ctypes.c_int)]
 
 
+# int (*)(double* buf, int n, void* user): in-place sum over the ranks
+ALLREDUCE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_void_p)
+
+
 def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
 
@@ -55,6 +59,7 @@ def lib():
         L.orc_get_state.argtypes = [P, dp]
         L.orc_step.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int, dp]
         L.orc_get_stats.argtypes = [P, ctypes.POINTER(Stats)]
+        L.orc_shard.argtypes = [P, ctypes.c_int, ctypes.c_int, ALLREDUCE, P]
         L.orc_traj_len.argtypes = [P]
         L.orc_get_traj.argtypes = [P, dp]
         L.orc_window_states.argtypes = [P, dp]
@@ -142,6 +147,17 @@ class Pipeline:
         s = np.zeros(STATE_LEN)
         lib().orc_get_state(self.h, _d(s))
         return s
+
+    def shard(self, rank, world, allreduce):
+        """Spatial-tile sharding: allreduce(np.ndarray) sums in place."""
+        def cb(buf, n, user):
+            try:
+                allreduce(np.ctypeslib.as_array(buf, shape=(n,)))
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+        self._cb = ALLREDUCE(cb)
+        lib().orc_shard(self.h, rank, world, self._cb, None)
 
     def stats(self):
         s = Stats()

@@ -222,6 +222,24 @@ struct Pipeline {
           // unreachable (finding 3): the VNC residual would be added here
         }
       }
+      if (mpar.shard_world > 1) {  // all-reduce the 34-value normal equations
+        double buf[34];
+        int k = 0;
+        for (int r = 0; r < 6; r++)
+          for (int c = r; c < 6; c++) buf[k++] = HTH(r, c);
+        for (int r = 0; r < 6; r++) buf[k++] = HTz[r];
+        for (int r = 0; r < 3; r++)
+          for (int c = r; c < 3; c++) buf[k++] = nnt(r, c);
+        buf[k++] = match_num;
+        shard_sum(&mpar, buf, 34);
+        k = 0;
+        for (int r = 0; r < 6; r++)
+          for (int c = r; c < 6; c++, k++) HTH(r, c) = HTH(c, r) = buf[k];
+        for (int r = 0; r < 6; r++) HTz[r] = buf[k++];
+        for (int r = 0; r < 3; r++)
+          for (int c = r; c < 3; c++, k++) nnt(r, c) = nnt(c, r) = buf[k];
+        match_num = (int)buf[k];
+      }
       st.iekf_matches[iterCount < 4 ? iterCount : 3] = match_num;
       H_T_H.setBlock(0, 0, HTH);
       M15 K_1 = inverse(H_T_H + cov_inv);
@@ -257,7 +275,7 @@ struct Pipeline {
     int thd_num = cfg.thread_num;
     std::vector<std::vector<OctoTree*>> octss(thd_num);
     int g_size = (int)surf_map_slide.size();
-    if (g_size < thd_num) return;
+    if (shard_count(&mpar, g_size) < thd_num) return;  // over all shards (sharded mode)
     double part = 1.0 * g_size / thd_num;
     int cnt = 0;
     for (auto& kv : surf_map_slide) {
@@ -288,7 +306,7 @@ struct Pipeline {
     int thd_num = cfg.thread_num;
     std::vector<std::vector<OctoTree*>> octs(thd_num);
     int g_size = (int)surf_map_slide.size();
-    if (g_size < thd_num) return;
+    if (shard_count(&mpar, g_size) < thd_num) return;  // over all shards (sharded mode)
     double part = 1.0 * g_size / thd_num;
     int cnt = 0;
     for (auto& kv : surf_map_slide) {
@@ -565,6 +583,13 @@ int orc_step(void* h, const float* xyz, const float* inten, int n, double beg, d
   return ((Pipeline*)h)->step(xyz, inten, n, beg, end, imus, timing);
 }
 void orc_get_stats(void* h, orc_stats* s) { *s = ((Pipeline*)h)->st; }
+void orc_shard(void* h, int rank, int world, int (*fn)(double*, int, void*), void* user) {
+  Pipeline* P = (Pipeline*)h;
+  P->mpar.shard_rank = rank;
+  P->mpar.shard_world = world;
+  P->mpar.allreduce = fn;
+  P->mpar.ar_user = user;
+}
 int orc_traj_len(void* h) { return (int)((Pipeline*)h)->traj.size() / 13; }
 void orc_get_traj(void* h, double* out) {
   Pipeline* p = (Pipeline*)h;

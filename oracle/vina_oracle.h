@@ -55,6 +55,10 @@ void orc_get_state(void* h, double* state);
 int orc_step(void* h, const float* xyz, const float* inten, int n, double beg, double end, const double* imu, int m,
              double* timing);
 void orc_get_stats(void* h, orc_stats* s);
+/* Spatial-tile sharding of the restatement: this pipeline keeps
+ * only the root voxels of tiles owned by `rank`; fn sums n doubles in place
+ * over the ranks at every exchange point. Call before the first step. */
+void orc_shard(void* h, int rank, int world, int (*fn)(double* buf, int n, void* user), void* user);
 int orc_traj_len(void* h);
 void orc_get_traj(void* h, double* out);
 int orc_window_states(void* h, double* out);
