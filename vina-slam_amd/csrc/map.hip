@@ -203,7 +203,13 @@ __global__ void __launch_bounds__(256) k_iekf(int n, const float* __restrict__ x
     }
   const V3 p = ld_v3(xc + 9);
   const M3 Rt = tr(R);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  // XCD-aware chunking (cdna_hip_programming.md T1): blocks are dealt
+  // round-robin over the 8 XCDs, so block b works on chunk (b % 8) * (nb / 8)
+  // + b / 8 — each XCD sweeps a contiguous run of the scan and the plane /
+  // node records of neighbouring points stay in its own L2 (nb % 8 == 0)
+  const int nb = gridDim.x;
+  const int vb = (nb % 8 == 0) ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
+  for (int i = vb * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     V3 pnt;
     M3 var;
     var_init_pt(mp, x[i], y[i], z[i], pnt, var);
@@ -290,7 +296,7 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
                    hipEvent_t ev0, hipEvent_t ev1) {
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
-  const int nb = grid_for(n, 256, 512);
+  const int nb = ((grid_for(n, 256, 512) + 7) / 8) * 8;  // a multiple of the 8 XCDs (k_iekf chunking)
   if (ev0) (void)hipEventRecord(ev0, s);
   k_iekf<<<nb, 256, 0, s>>>(n, x, y, z, mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials);
   if (ev1) (void)hipEventRecord(ev1, s);

@@ -495,7 +495,7 @@ int stage_propagate(vg_ctx* ctx, const double* imu, int m, double end) {
 static int resolve_ds(vg_ctx* ctx, HostPipe* P) {
   if (P->ds_n >= 0) return VG_OK;
   const vg_config& c = ctx->cfg;
-  VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ds, P->ds_seq, "downsample"));
+  VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ds, P->ds_seq, "downsample", ctx->stream_ds));
   if (ctx->h_pub->ds_err) {
     ctx->err = "voxel key out of packed range (|key| >= 2^20)";
     return VG_E_RANGE;
@@ -507,7 +507,7 @@ static int resolve_ds(vg_ctx* ctx, HostPipe* P) {
     VG_TRY(ds_enqueue(ctx, ctx->stream_ds, P->sx, P->sy, P->sz, P->si, P->n_raw, c.down_size / 2, P->ds_seq));
     prof_end(ctx, kProfDownsample, ctx->stream_ds);
     VG_HIP(hipEventRecord(ctx->ev_ds_done, ctx->stream_ds));
-    VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ds, P->ds_seq, "downsample"));
+    VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ds, P->ds_seq, "downsample", ctx->stream_ds));
     if (ctx->h_pub->ds_err) {
       ctx->err = "voxel key out of packed range (|key| >= 2^20)";
       return VG_E_RANGE;

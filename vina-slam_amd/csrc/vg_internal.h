@@ -261,13 +261,14 @@ namespace vg {
 constexpr size_t kStageBytes = 1 << 17;
 // Spin until a Pub sequence flag reaches seq (the device publishes with a
 // system-scope release); checks the stream for errors while spinning.
-inline int pub_wait(vg_ctx* c, const int* flag, int seq, const char* what) {
+inline int pub_wait(vg_ctx* c, const int* flag, int seq, const char* what, hipStream_t producer = nullptr) {
+  hipStream_t st = producer ? producer : c->stream;  // the stream the publishing kernel runs on
   for (long spin = 0; __atomic_load_n(flag, __ATOMIC_ACQUIRE) < seq; spin++) {
 #if defined(__x86_64__)
     __builtin_ia32_pause();
 #endif
     if ((spin & 4095) == 4095) {
-      const hipError_t e = hipStreamQuery(c->stream);
+      const hipError_t e = hipStreamQuery(st);
       if (e != hipSuccess && e != hipErrorNotReady) {
         c->err = std::string(what) + ": " + hipGetErrorString(e);
         return VG_E_HIP;

@@ -203,6 +203,11 @@ VG_HD M3 jr_inv(const M3& R) {
 
 // Symmetric 3x3 eigen-decomposition, cyclic Jacobi, ascending eigenvalues,
 // eigenvectors in columns (SelfAdjointEigenSolver<Matrix3d> semantics).
+// Stops once the off-diagonal mass is below 1e-18 of the diagonal's: the
+// eigenvalue error is then second order in it (far below one ulp) and the
+// eigenvector error ~1e-18 |A| / gap; 3-4 sweeps instead of the 5-6 an
+// exact-zero stop takes (a ~35 % shorter dependency chain on the GPU, where
+// one decomposition per thread is pure latency).
 VG_HD void eig3(const M3& Ain, V3& w, M3& V) {
   double a[3][3];
   for (int i = 0; i < 3; i++)
@@ -210,7 +215,7 @@ VG_HD void eig3(const M3& Ain, V3& w, M3& V) {
   double v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
   for (int sweep = 0; sweep < 60; sweep++) {
     double off = fabs(a[0][1]) + fabs(a[0][2]) + fabs(a[1][2]);
-    if (off == 0.0) break;
+    if (off == 0.0 || off <= 1e-18 * (fabs(a[0][0]) + fabs(a[1][1]) + fabs(a[2][2]))) break;
     for (int p = 0; p < 2; p++)
       for (int q = p + 1; q < 3; q++) {
         double apq = a[p][q];
