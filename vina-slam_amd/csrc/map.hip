@@ -88,7 +88,8 @@ int map_alloc(vg_ctx* ctx) {
   VG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, w.v0, w.v1, w.cap, ctx->stream));
   w.tmp_bytes = (b1 > b2 ? b1 : b2) + 256;
   w.tmp = ctx->arena.take<char>(w.tmp_bytes);
-  if (!w.tmp) {
+  w.tmp2 = ctx->arena.take<char>(w.tmp_bytes);  // the margi prefix sorts on the second stream
+  if (!w.tmp || !w.tmp2) {
     ctx->err = "arena exhausted (sort workspace)";
     return VG_E_CAPACITY;
   }
@@ -1874,8 +1875,33 @@ __global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, doub
 // multi_margi (local_mapping.cpp:21-78): every count stays on the device;
 // the host enqueues max_layer+1 levels (no level can be deeper) and
 // synchronises once at the end for the error flags.
-int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, double jour,
-              int pub_seq, int pub_seq2) {
+// The part of multi_margi that does not depend on the BA (jour stamps, the
+// slide-tree levels, the oldest slot's points grouped by leaf), enqueued right
+// after the recut on the second stream so it runs under the LM iterations.
+int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, double jour) {
+  DevMap& m = ctx->map;
+  Work& w = ctx->wk;
+  hipStream_t s = ctx->stream_ds;
+  const int nlev = mp.max_layer + 1;
+  VG_HIP(hipEventRecord(ctx->ev_recut_done, ctx->stream));
+  VG_HIP(hipStreamWaitEvent(s, ctx->ev_recut_done, 0));
+  const int gl = 64;  // grid-stride over device-side counts
+  k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour, w.rc);
+  for (int L = 0; L < nlev; L++) k_collect_level<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.list0, w.rc);
+  // oldest slot segments by leaf (the slot's point count is known on the host)
+  if (n_oldest > 0) {
+    k_margi_keys<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, slot0, m, w.k0);
+    size_t tb = w.tmp_bytes;
+    VG_HIP(hipcub::DeviceRadixSort::SortKeys(w.tmp2, tb, w.k0, w.k1, n_oldest, 0, 64, s));
+    k_margi_segs<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, w.k1, m);
+  }
+  VG_HIP(hipGetLastError());
+  VG_HIP(hipEventRecord(ctx->ev_prefix_done, s));
+  return VG_OK;
+}
+
+int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, int pub_seq,
+              int pub_seq2) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
@@ -1886,16 +1912,8 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   // for this scan and is published before the margi kernels run
   VG_TRY(state_make_win(ctx, wa, dwin, dn, dn + 32));
   if (pub_seq > 0) VG_TRY(state_publish(ctx, wa.win_count, ba_iters_dev(ctx), pub_seq));
-  const int gl = 64;  // grid-stride over device-side counts
-  k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour, w.rc);
-  for (int L = 0; L < nlev; L++) k_collect_level<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.list0, w.rc);
-  // oldest slot segments by leaf (the slot's point count is known on the host)
-  const int s0 = wa.mp[0];
-  if (n_oldest > 0) {
-    k_margi_keys<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, s0, m, w.k0);
-    VG_TRY(sort_keys(ctx, w.k0, w.k1, n_oldest, 64));
-    k_margi_segs<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, w.k1, m);
-  }
+  const int gl = 64;
+  VG_HIP(hipStreamWaitEvent(s, ctx->ev_prefix_done, 0));  // map_margi_prefix
   k_margi_leaf<<<gl, kBlock, 0, s>>>(m.counters + kCntLeaves, w.list0, mp, dwin, m, ctx->ba.fac_eig, ctx->ba.fac_pcr,
                                      w.plan);
   k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, w.k1, dwin, m);

@@ -166,6 +166,7 @@ struct HostPipe {
   const float *sx = nullptr, *sy = nullptr, *sz = nullptr, *si = nullptr;
   int ins_slot = -1, ins_n = 0;
   bool published = false;
+  bool prefix = false;     // map_margi_prefix enqueued for this scan
   std::deque<Pend> pend;   // enqueued scans awaiting absorption (oldest first)
   int sticky = VG_OK;      // deferred device error
 };
@@ -488,6 +489,7 @@ int stage_propagate(vg_ctx* ctx, const double* imu, int m, double end) {
   P->ds_seq = 0;
   P->ds_n = -1;
   P->ins_slot = -1;
+  P->prefix = false;
   return VG_OK;
 }
 
@@ -637,6 +639,10 @@ int stage_recut(vg_ctx* ctx, int* nf_out) {
   }
   VG_TRY(r);
   prof_end(ctx, kProfRecut);
+  if (P->win_count >= c.win_size) {  // margi's BA-independent part runs under the LM iterations
+    VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], c.thread_num, P->jour));
+    P->prefix = true;
+  }
   P->cur.st.n_factors = nf;
   P->n_factors = nf;
   if (nf_out) *nf_out = nf;
@@ -679,7 +685,9 @@ int stage_margi_slide(vg_ctx* ctx) {
   const WinArg wa = make_winarg(P, 1);
   const int seq1 = ++ctx->pub_seq, seq2 = ++ctx->pub_seq;
   prof_begin(ctx, kProfMargi);
-  VG_TRY(map_margi(ctx, P->mpd, wa, P->wp_n[P->mp[0]], c.thread_num, P->jour, seq1, seq2));
+  if (!P->prefix) VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], c.thread_num, P->jour));
+  P->prefix = false;
+  VG_TRY(map_margi(ctx, P->mpd, wa, P->wp_n[P->mp[0]], c.thread_num, seq1, seq2));
   prof_end(ctx, kProfMargi);
   P->cur.seq1 = seq1;
   P->cur.seq2 = seq2;

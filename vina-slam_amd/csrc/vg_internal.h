@@ -136,6 +136,7 @@ struct Work {
   int* leaf = nullptr;         // per ds point leaf / per event target
   double* pw = nullptr;        // per ds point world coords
   void* tmp = nullptr;
+  void* tmp2 = nullptr;        // sort workspace of the second stream
   size_t tmp_bytes = 0;
   double* partials = nullptr;  // reduction partials
   int* iekf_cache = nullptr;   // per raw point cached leaf
@@ -222,6 +223,7 @@ struct vg_ctx {
   // overlaps the previous scan's recut/BA/margi and this scan's IEKF
   hipStream_t stream_ds = nullptr;
   hipEvent_t ev_ds_done = nullptr, ev_ds_free = nullptr;
+  hipEvent_t ev_recut_done = nullptr, ev_prefix_done = nullptr;  // margi prefix on the second stream
   std::string err;
   vg::Arena arena;
   // raw scan staging (SoA)
@@ -364,8 +366,8 @@ int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num
 int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay = false);
 // multi_margi + the device-state slide; publishes the state (pub_seq, before
 // the margi kernels) and the end-of-scan counters (pub_seq2)
-int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, double jour, int pub_seq,
-              int pub_seq2);
+int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, double jour);
+int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, int pub_seq, int pub_seq2);
 // state.hip
 int state_alloc(vg_ctx* ctx);
 int state_scan_begin(vg_ctx* ctx, const double* xc249);

@@ -43,7 +43,9 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
   }
   if ((e = hipStreamCreateWithFlags(&ctx->stream_ds, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&ctx->ev_ds_done, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&ctx->ev_ds_free, hipEventDisableTiming)) != hipSuccess) {
+      (e = hipEventCreateWithFlags(&ctx->ev_ds_free, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_recut_done, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_prefix_done, hipEventDisableTiming)) != hipSuccess) {
     ctx->err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
@@ -148,6 +150,8 @@ int vg_destroy(vg_ctx* ctx) {
   if (ctx->stream_ds) (void)hipStreamDestroy(ctx->stream_ds);
   if (ctx->ev_ds_done) (void)hipEventDestroy(ctx->ev_ds_done);
   if (ctx->ev_ds_free) (void)hipEventDestroy(ctx->ev_ds_free);
+  if (ctx->ev_recut_done) (void)hipEventDestroy(ctx->ev_recut_done);
+  if (ctx->ev_prefix_done) (void)hipEventDestroy(ctx->ev_prefix_done);
   delete ctx;
   return VG_OK;
 }
