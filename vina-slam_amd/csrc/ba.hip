@@ -1023,7 +1023,8 @@ const int* ba_iters_dev(vg_ctx* ctx) { return &carve(ctx).st->iters; }
 // Run damping_iter on the device state. imurec: (W-1) x kImuRec host records
 // (pinned staging, uploaded asynchronously). The window states and the IMU
 // bias records are read and written in DState.
-int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* iters) {
+int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* iters,
+           const std::function<int()>& before_first_wait) {
   const int W = ctx->cfg.win_size;
   if (15 * W > kMaxNB * kTile) {
     ctx->err = "win_size > 11 unsupported by the BA solve (LDS-resident 15W x 15W tile store)";
@@ -1090,6 +1091,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* i
     if (k + 1 < 10) iteration(k + 1);
     VG_HIP(hipGetLastError());
     VG_TRY(xerr);
+    if (k == 0 && before_first_wait) VG_TRY(before_first_wait());
     VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ba, seq0 + k, "k_ba_control"));
     done_iters = __atomic_load_n(&ctx->h_pub->ba_iters, __ATOMIC_ACQUIRE);
     if (__atomic_load_n(&ctx->h_pub->ba_done, __ATOMIC_ACQUIRE)) break;

@@ -734,10 +734,14 @@ static int read_counters(vg_ctx* ctx) {
   return VG_OK;
 }
 
-static int sort_keys(vg_ctx* ctx, const uint64_t* in, uint64_t* out, int n, int end_bit) {
+// LSD radix sort of 64-bit keys over bits [begin_bit, end_bit). The sort is
+// stable, so keys (leaf << 27 | index) generated in index order need only
+// their leaf bits sorted (3 passes instead of 7) to come out ordered by
+// (leaf, index).
+static int sort_keys(vg_ctx* ctx, const uint64_t* in, uint64_t* out, int n, int end_bit, int begin_bit = 0) {
   size_t tb = ctx->wk.tmp_bytes;
   if (n <= 0) return VG_OK;
-  VG_HIP(hipcub::DeviceRadixSort::SortKeys(ctx->wk.tmp, tb, in, out, n, 0, end_bit, ctx->stream));
+  VG_HIP(hipcub::DeviceRadixSort::SortKeys(ctx->wk.tmp, tb, in, out, n, begin_bit, end_bit, ctx->stream));
   return VG_OK;
 }
 static int excl_scan(vg_ctx* ctx, const uint32_t* in, uint32_t* out, int n) {
@@ -752,21 +756,24 @@ static int bits_for(long v) {
   return b;
 }
 
-// sort an int list of n node ids in place (deterministic creation order);
-// scratch: the 32-bit buffers u0/u1 (k0/k1 may hold live events)
-__global__ void __launch_bounds__(256) k_i2u(int n, const int* __restrict__ a, uint32_t* __restrict__ k) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) k[i] = (uint32_t)a[i];
-}
-__global__ void __launch_bounds__(256) k_u2i(int n, const uint32_t* __restrict__ k, int* __restrict__ a) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) a[i] = (int)k[i];
-}
-static int sort_ids(vg_ctx* ctx, int* a, int n) {
+// sort a list of n (non-negative) node ids, ascending (deterministic creation
+// order), over the id bits only; returns the buffer holding the result (`a` or
+// the scratch w.u1 — k0/k1 may hold live events)
+static int sort_ids(vg_ctx* ctx, int* a, int n, int** result) {
+  *result = a;
   if (n <= 1) return VG_OK;
   Work& w = ctx->wk;
-  k_i2u<<<grid_for(n), kBlock, 0, ctx->stream>>>(n, a, w.u0);
+  hipcub::DoubleBuffer<uint32_t> db(reinterpret_cast<uint32_t*>(a), w.u1);
   size_t tb = w.tmp_bytes;
-  VG_HIP(hipcub::DeviceRadixSort::SortKeys(w.tmp, tb, w.u0, w.u1, n, 0, 32, ctx->stream));
-  k_u2i<<<grid_for(n), kBlock, 0, ctx->stream>>>(n, w.u1, a);
+  VG_HIP(hipcub::DeviceRadixSort::SortKeys(w.tmp, tb, db, n, 0, bits_for(ctx->map.cap_nodes), ctx->stream));
+  *result = reinterpret_cast<int*>(db.Current());
+  return VG_OK;
+}
+// in place
+static int sort_ids_inplace(vg_ctx* ctx, int* a, int n) {
+  int* r = a;
+  VG_TRY(sort_ids(ctx, a, n, &r));
+  if (r != a) VG_HIP(hipMemcpyAsync(a, r, (size_t)n * sizeof(int), hipMemcpyDeviceToDevice, ctx->stream));
   return VG_OK;
 }
 
@@ -776,7 +783,7 @@ static int alloc_children(vg_ctx* ctx, int* plist, int np, int* next, int next_b
   hipStream_t s = ctx->stream;
   *n_created = 0;
   if (np <= 0) return VG_OK;
-  if (!sorted) VG_TRY(sort_ids(ctx, plist, np));
+  if (!sorted) VG_TRY(sort_ids_inplace(ctx, plist, np));
   VG_TRY(read_counters(ctx));
   int first = ctx->h_pinned[kCntNodes];
   k_child_count<<<grid_for(np), kBlock, 0, s>>>(np, plist, ctx->map, w.ac_cnt);
@@ -802,7 +809,7 @@ static int insert_tail(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_nu
   const int gseg = (n + kPushWaves - 1) / kPushWaves < 2048 ? (n + kPushWaves - 1) / kPushWaves : 2048;
   k_ins_resolve<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.leaf);
   k_ins_keys<<<g, kBlock, 0, s>>>(n, thread_num, m, w.leaf, w.k0);
-  VG_TRY(sort_keys(ctx, w.k0, w.k1, n, key_bits));
+  VG_TRY(sort_keys(ctx, w.k0, w.k1, n, key_bits, 27));  // stable: leaf bits only
   k_seg_heads<<<g, kBlock, 0, s>>>(n, thread_num, m, w.k1, w.list1, m.counters + kCntSeg);
   // ~one wave per leaf segment (the count stays on the device)
   k_push_window<<<gseg, 64 * kPushWaves, 0, s>>>(w.list1, m.counters + kCntSeg, n, w.k1, mp, slot, m, w.pw,
@@ -1397,7 +1404,7 @@ static int recut_slow_apply(vg_ctx* ctx, int L, const MP& mp, WinD* dwin, int* n
     ctx->err = "subdivision event buffer overflow";
     return VG_E_CAPACITY;
   }
-  VG_TRY(sort_ids(ctx, w.list2, nsub));
+  VG_TRY(sort_ids_inplace(ctx, w.list2, nsub));
   VG_HIP(hipMemsetD32Async((hipDeviceptr_t)(m.counters + kCntEvents), nwin, 1, s));
   k_sub_fix_events<<<grid_for(nsub), kBlock, 0, s>>>(nsub, w.list2, m, w.k0, w.cap);
   VG_TRY(read_counters(ctx));
@@ -1495,8 +1502,9 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* 
     return VG_E_CAPACITY;
   }
   if (nf > 0) {
-    VG_TRY(sort_ids(ctx, w.cand, nf));
-    k_factor_finish<<<grid_for(nf), kBlock, 0, s>>>(nf, w.cand, m, ctx->ba.fac_node, ctx->ba.fac_eig,
+    int* sorted = w.cand;
+    VG_TRY(sort_ids(ctx, w.cand, nf, &sorted));
+    k_factor_finish<<<grid_for(nf), kBlock, 0, s>>>(nf, sorted, m, ctx->ba.fac_node, ctx->ba.fac_eig,
                                                     ctx->ba.fac_pcr);
     VG_HIP(hipGetLastError());
   }
@@ -1892,7 +1900,8 @@ int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thr
   if (n_oldest > 0) {
     k_margi_keys<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, slot0, m, w.k0);
     size_t tb = w.tmp_bytes;
-    VG_HIP(hipcub::DeviceRadixSort::SortKeys(w.tmp2, tb, w.k0, w.k1, n_oldest, 0, 64, s));
+    // stable LSD sort over the leaf bits only (keys generated in index order)
+    VG_HIP(hipcub::DeviceRadixSort::SortKeys(w.tmp2, tb, w.k0, w.k1, n_oldest, 27, 27 + bits_for(m.cap_nodes), s));
     k_margi_segs<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, w.k1, m);
   }
   VG_HIP(hipGetLastError());

@@ -639,10 +639,6 @@ int stage_recut(vg_ctx* ctx, int* nf_out) {
   }
   VG_TRY(r);
   prof_end(ctx, kProfRecut);
-  if (P->win_count >= c.win_size) {  // margi's BA-independent part runs under the LM iterations
-    VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], c.thread_num, P->jour));
-    P->prefix = true;
-  }
   P->cur.st.n_factors = nf;
   P->n_factors = nf;
   if (nf_out) *nf_out = nf;
@@ -663,7 +659,14 @@ int stage_ba(vg_ctx* ctx, int* iters_out) {
   for (int j = 0; j < W - 1; j++) memcpy(&rec[(size_t)j * kBaImuRec], P->imu_pre[j].rec.data(), kBaImuRec * 8);
   int iters = 0;
   prof_begin(ctx, kProfBA);
-  VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), rec.data(), &iters));
+  // margi's BA-independent part goes onto the second stream once the first LM
+  // iterations are enqueued, so it runs under them (map_margi_prefix)
+  auto prefix = [&]() -> int {
+    VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], ctx->cfg.thread_num, P->jour));
+    P->prefix = true;
+    return VG_OK;
+  };
+  VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), rec.data(), &iters, prefix));
   prof_end(ctx, kProfBA);
   P->cur.st.ba_iters = iters;
   if (iters_out) *iters_out = iters;
@@ -735,8 +738,11 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   (void)beg;
   const vg_config& c = ctx->cfg;
   VG_TRY(stage_propagate(ctx, imu, m, end));
-  VG_TRY(stage_downsample(ctx, dx, dy, dz, di, n, nullptr));
+  // the IEKF is enqueued before the downsample: both read only the raw scan
+  // (local_mapping.cpp:396-413), and the main stream should not idle while the
+  // host enqueues the downsample onto its own stream
   VG_TRY(stage_iekf(ctx, dx, dy, dz, n, nullptr));
+  VG_TRY(stage_downsample(ctx, dx, dy, dz, di, n, nullptr));
   VG_TRY(stage_window_push(ctx, imu, m));
   VG_TRY(stage_insert(ctx));
   VG_TRY(stage_recut(ctx, nullptr));

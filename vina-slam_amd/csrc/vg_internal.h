@@ -6,6 +6,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <chrono>
+#include <functional>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -384,7 +385,8 @@ int ba_alloc(vg_ctx* ctx);
 // LM on the device state (window states and IMU bias records in DState);
 // imurec: (W-1) x kBaImuRec host records. Returns once the LM has converged on
 // the device (the flags are read without draining the stream).
-int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* iters);
+int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* iters,
+           const std::function<int()>& before_first_wait = nullptr);
 const int* ba_iters_dev(vg_ctx* ctx);
 // pipeline.cpp
 void host_init(vg_ctx* ctx);
