@@ -105,6 +105,17 @@ int vg_step_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_
 /* vg_step / vg_step_dev return once the scan is ENQUEUED: the device runs it
  * asynchronously (the host waits only for device-side counts it needs, without
  * draining the stream). Every query below completes the outstanding work first. */
+/* SURVEY row f1 — the same scan step with IMUEKF::motion_blur's per-point
+ * deskew (imu_ekf.cpp:114-144) on the device first: `time` holds each point's
+ * offset from pcl_beg_time in seconds (the reference's `curvature` field),
+ * ascending (the reference's time-sorted cloud). The propagation records the
+ * IMU poses; one lane per point moves it into the LiDAR frame at
+ * pcl_end_time. Inputs as vg_step / vg_step_dev. */
+int vg_step_deskew(vg_ctx* ctx, const float* xyz, const float* intensity, const float* time, int n,
+                   double pcl_beg_time, double pcl_end_time, const double* imu, int m);
+int vg_step_deskew_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, const float* d_intensity,
+                       const float* d_time, int n, double pcl_beg_time, double pcl_end_time, const double* imu,
+                       int m);
 int vg_get_state(vg_ctx* ctx, double* state);
 int vg_get_stats(vg_ctx* ctx, vg_stats* out);
 /* Per-scan counters of every completed scan since vg_create / vg_reset, in

@@ -60,6 +60,9 @@ def lib():
         L.orc_step.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int, dp]
         L.orc_get_stats.argtypes = [P, ctypes.POINTER(Stats)]
         L.orc_shard.argtypes = [P, ctypes.c_int, ctypes.c_int, ALLREDUCE, P]
+        L.orc_step_deskew.argtypes = [P, fp, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int,
+                                      dp]
+        L.orc_deskew_only.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
         L.orc_traj_len.argtypes = [P]
         L.orc_get_traj.argtypes = [P, dp]
         L.orc_window_states.argtypes = [P, dp]
@@ -147,6 +150,24 @@ class Pipeline:
         s = np.zeros(STATE_LEN)
         lib().orc_get_state(self.h, _d(s))
         return s
+
+    def step_deskew(self, xyz, inten, times, beg, end, imu):
+        xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+        inten = np.ascontiguousarray(inten, dtype=np.float32)
+        times = np.ascontiguousarray(times, dtype=np.float32)
+        imu = np.ascontiguousarray(imu, dtype=np.float64)
+        tm = np.zeros(8)
+        lib().orc_step_deskew(self.h, _f(xyz), _f(inten), _f(times), xyz.shape[0], beg, end, _d(imu), imu.shape[0],
+                              _d(tm))
+        return tm
+
+    def deskew_only(self, xyz, times, beg, end, imu):
+        """Propagate with imu and deskew xyz (a copy is returned); the pipeline's state advances."""
+        out = np.ascontiguousarray(xyz, dtype=np.float32).copy()
+        times = np.ascontiguousarray(times, dtype=np.float32)
+        imu = np.ascontiguousarray(imu, dtype=np.float64)
+        npose = lib().orc_deskew_only(self.h, _f(out), _f(times), out.shape[0], beg, end, _d(imu), imu.shape[0])
+        return out, npose
 
     def shard(self, rank, world, allreduce):
         """Spatial-tile sharding: allreduce(np.ndarray) sums in place."""

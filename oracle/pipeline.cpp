@@ -80,8 +80,20 @@ struct Pipeline {
   // IMUEKF::motion_blur state/covariance part — imu_ekf.cpp:28-94. The deskew
   // (imu_ekf.cpp:114-144) is out of scope: callers hand in
   // motion-compensated scans.
+  // IMUEKF::imu_poses (ekf_imu.hpp): per processed IMU segment the offset of
+  // its start from pcl_beg_time, R, p, v, bias-corrected angular velocity and
+  // world acceleration (stored in the IMUST fields R, p, v, bg, ba as the
+  // reference does, imu_ekf.cpp:64)
+  struct ImuPose {
+    double t;
+    M3 R;
+    V3 p, v, w, a;
+  };
+  std::vector<ImuPose> imu_poses;
+
   void propagate(const std::vector<ImuSample>& imus, double pcl_beg, double pcl_end) {
     IMUST& xc = x_curr;
+    imu_poses.clear();
     V3 acc_imu, angvel_avr, acc_avr, vel_imu = xc.v, pos_imu = xc.p;
     M3 R_imu = xc.R;
     double dt = 0;
@@ -99,6 +111,7 @@ struct Pipeline {
       double cur_time = head.t;
       if (cur_time < last_pcl_end_time) cur_time = last_pcl_end_time;
       dt = tail.t - cur_time;
+      imu_poses.push_back({cur_time - pcl_beg, R_imu, pos_imu, vel_imu, angvel_avr, acc_imu});  // imu_ekf.cpp:64
       M3 acc_avr_skew = hat(acc_avr);
       M3 Exp_f = Exp(angvel_avr, dt);
       M15 F = M15::Identity(), cw;
@@ -130,7 +143,33 @@ struct Pipeline {
     }
     xc.t = pcl_end;
     last_pcl_end_time = pcl_end;
-    (void)pcl_beg;
+  }
+
+  // IMUEKF::motion_blur's per-point deskew (imu_ekf.cpp:114-144) on a cloud
+  // sorted by time (`curvature` = offset from pcl_beg_time, seconds): walking
+  // segments and points backwards, every point later than a segment's start
+  // is moved into the LiDAR frame at pcl_end_time. Faithful to the loop,
+  // including its tail: once the first point has been compensated the inner
+  // loop breaks, and each earlier segment whose start precedes that point's
+  // time compensates it again.
+  void deskew(float* xyz, const float* times, int n) {
+    if (n <= 0 || imu_poses.empty()) return;
+    const IMUST& xc = x_curr;
+    const M3& Lr = extrin.R;  // Lid_rot_to_IMU / Lid_offset_to_IMU
+    const V3& Lo = extrin.p;
+    int it = n - 1;
+    for (int i = (int)imu_poses.size() - 1; i >= 0; i--) {
+      const ImuPose& h = imu_poses[i];
+      for (; times[it] > h.t; it--) {
+        const double dt = times[it] - h.t;
+        const M3 R_i = h.R * Exp(h.w, dt);
+        const V3 T_ei = h.p + h.v * dt + h.a * 0.5 * dt * dt - xc.p;
+        const V3 P_i = v3((double)xyz[3 * it], (double)xyz[3 * it + 1], (double)xyz[3 * it + 2]);
+        const V3 Pc = Lr.T() * (xc.R.T() * (R_i * (Lr * P_i + Lo) + T_ei) - Lo);
+        for (int j = 0; j < 3; j++) xyz[3 * it + j] = (float)Pc[j];
+        if (it == 0) break;
+      }
+    }
   }
 
   // ---- VNC scan-plane prep + VNC residual loop: odometry.cpp:22-61, 84-96,
@@ -340,13 +379,21 @@ struct Pipeline {
   // One scan of thd_odometry_localmapping's steady-state branch,
   // local_mapping.cpp:389-547 (initialisation, SURVEY row f2, is replaced by a
   // seeded state and an empty map).
-  int step(const float* xyz, const float* inten, int n, double beg, double end, const std::vector<ImuSample>& imus,
-           double* timing) {
+  int step(const float* xyz_in, const float* inten, int n, double beg, double end, const std::vector<ImuSample>& imus,
+           double* timing, const float* times = nullptr) {
     using clk = std::chrono::steady_clock;
     auto t0 = clk::now();
     memset(&st, 0, sizeof(st));
+    imu_poses.clear();
     if (!first) propagate(imus, beg, end);
     else { x_curr.t = end; last_pcl_end_time = end; }
+    std::vector<float> xyz_d;
+    const float* xyz = xyz_in;
+    if (times) {  // odom_ekf.process -> motion_blur deskew (local_mapping.cpp:389, imu_ekf.cpp:114-144)
+      xyz_d.assign(xyz_in, xyz_in + 3 * (size_t)n);
+      deskew(xyz_d.data(), times, n);
+      xyz = xyz_d.data();
+    }
     std::vector<PointType> pcl(n);
     for (int i = 0; i < n; i++) {
       pcl[i].x = xyz[3 * i];
@@ -581,6 +628,28 @@ int orc_step(void* h, const float* xyz, const float* inten, int n, double beg, d
     imus[i].acc = v3(imu[7 * i + 4], imu[7 * i + 5], imu[7 * i + 6]);
   }
   return ((Pipeline*)h)->step(xyz, inten, n, beg, end, imus, timing);
+}
+int orc_step_deskew(void* h, const float* xyz, const float* inten, const float* times, int n, double beg, double end,
+                    const double* imu, int m, double* timing) {
+  std::vector<ImuSample> imus(m);
+  for (int i = 0; i < m; i++) {
+    imus[i].t = imu[7 * i];
+    imus[i].gyr = v3(imu[7 * i + 1], imu[7 * i + 2], imu[7 * i + 3]);
+    imus[i].acc = v3(imu[7 * i + 4], imu[7 * i + 5], imu[7 * i + 6]);
+  }
+  return ((Pipeline*)h)->step(xyz, inten, n, beg, end, imus, timing, times);
+}
+int orc_deskew_only(void* h, float* xyz, const float* times, int n, double beg, double end, const double* imu, int m) {
+  Pipeline* P = (Pipeline*)h;
+  std::vector<ImuSample> imus(m);
+  for (int i = 0; i < m; i++) {
+    imus[i].t = imu[7 * i];
+    imus[i].gyr = v3(imu[7 * i + 1], imu[7 * i + 2], imu[7 * i + 3]);
+    imus[i].acc = v3(imu[7 * i + 4], imu[7 * i + 5], imu[7 * i + 6]);
+  }
+  P->propagate(imus, beg, end);
+  P->deskew(xyz, times, n);
+  return (int)P->imu_poses.size();
 }
 void orc_get_stats(void* h, orc_stats* s) { *s = ((Pipeline*)h)->st; }
 void orc_shard(void* h, int rank, int world, int (*fn)(double*, int, void*), void* user) {

@@ -55,6 +55,12 @@ void orc_get_state(void* h, double* state);
 int orc_step(void* h, const float* xyz, const float* inten, int n, double beg, double end, const double* imu, int m,
              double* timing);
 void orc_get_stats(void* h, orc_stats* s);
+/* orc_step with IMUEKF::motion_blur's per-point deskew first (imu_ekf.cpp:114-144);
+ * times: per-point offset from beg in seconds (the reference's curvature), ascending. */
+int orc_step_deskew(void* h, const float* xyz, const float* inten, const float* times, int n, double beg, double end,
+                    const double* imu, int m, double* timing);
+/* propagation + deskew only, in place (returns the number of IMU poses) */
+int orc_deskew_only(void* h, float* xyz, const float* times, int n, double beg, double end, const double* imu, int m);
 /* Spatial-tile sharding of the restatement: this pipeline keeps
  * only the root voxels of tiles owned by `rank`; fn sums n doubles in place
  * over the ranks at every exchange point. Call before the first step. */

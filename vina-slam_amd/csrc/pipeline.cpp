@@ -158,6 +158,7 @@ struct HostPipe {
   M6 noiseMeas = M6::Z(), noiseWalk = M6::Z();
   std::vector<double> traj;
   std::vector<vg_stats> stats_log;
+  std::vector<double> poses;  // this scan's IMUEKF::imu_poses, 22 doubles each (deskew)
   int n_factors = 0;
   // current scan
   Pend cur;
@@ -345,7 +346,8 @@ int host_sync(vg_ctx* ctx) {
 
 // IMUEKF::motion_blur state/covariance propagation (imu_ekf.cpp:28-94); the
 // per-point deskew (114-144) is SURVEY row f1 (callers pass compensated scans).
-static void propagate(vg_ctx* ctx, HostPipe* P, const std::vector<Imu>& imus, double pcl_end) {
+static void propagate(vg_ctx* ctx, HostPipe* P, const std::vector<Imu>& imus, double pcl_beg, double pcl_end) {
+  P->poses.clear();
   const vg_config& c = ctx->cfg;
   HX& xc = P->x_curr;
   V3 acc_imu = V3::Z(), angvel = V3::Z(), acc_avr, vel = xc.v, pos = xc.p;
@@ -365,6 +367,16 @@ static void propagate(vg_ctx* ctx, HostPipe* P, const std::vector<Imu>& imus, do
     double cur = head.t;
     if (cur < P->last_pcl_end_time) cur = P->last_pcl_end_time;
     dt = tail.t - cur;
+    {  // imu_poses.emplace_back(offt, R_imu, pos_imu, vel_imu, angvel_avr, acc_imu) (imu_ekf.cpp:64)
+      double rec[22];
+      rec[0] = cur - pcl_beg;
+      memcpy(rec + 1, R_imu.a, 72);
+      memcpy(rec + 10, pos.a, 24);
+      memcpy(rec + 13, vel.a, 24);
+      memcpy(rec + 16, angvel.a, 24);
+      memcpy(rec + 19, acc_imu.a, 24);
+      P->poses.insert(P->poses.end(), rec, rec + 22);
+    }
     M3 ask = hat(acc_avr);
     M3 Exp_f = Exp(angvel, dt);
     M15 F = M15::I(), cw = M15::Z();
@@ -457,7 +469,7 @@ static int need_open(vg_ctx* ctx, HostPipe* P, const char* what) {
 
 // odom_ekf.process -> motion_blur state/covariance part (local_mapping.cpp:389);
 // opens the scan on the device (x_curr, x_prop, cov_inv)
-int stage_propagate(vg_ctx* ctx, const double* imu, int m, double end) {
+int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double end) {
   HostTimer ht_(ctx, kHostPropagate);
   HostPipe* P = hp(ctx);
   if (P->in_scan) {
@@ -465,8 +477,9 @@ int stage_propagate(vg_ctx* ctx, const double* imu, int m, double end) {
     return VG_E_STATE;
   }
   VG_TRY(absorb(ctx, P, false));  // x_curr / x_buf of the previous scan
+  P->poses.clear();
   if (!P->first) {
-    propagate(ctx, P, to_imus(imu, m), end);
+    propagate(ctx, P, to_imus(imu, m), beg, end);
   } else {
     P->x_curr.t = end;
     P->last_pcl_end_time = end;
@@ -538,6 +551,7 @@ int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float*
   P->cur.st.n_raw = n;
   // own stream: waits only until the previous insert has read the ds buffers
   VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_ds_free, 0));
+  VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_scan_ready, 0));  // a deskewed scan (no-op otherwise)
   prof_begin(ctx, kProfDownsample, ctx->stream_ds);
   P->ds_seq = ++ctx->pub_seq;
   P->ds_n = -1;
@@ -732,12 +746,51 @@ int stage_finish(vg_ctx* ctx) {
 
 int host_win_count(vg_ctx* ctx) { return hp(ctx)->win_count; }
 
+// IMUEKF::motion_blur's per-point deskew (imu_ekf.cpp:114-144), SURVEY row
+// f1: after the propagation (which recorded the IMU poses), the scan is moved
+// into the LiDAR frame at pcl_end_time by one lane per point, into the
+// context's staging buffers. Nothing to do on the first scan (no poses).
+int stage_deskew(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, const float* t,
+                 int n) {
+  HostPipe* P = hp(ctx);
+  VG_TRY(need_open(ctx, P, "vg_deskew"));
+  const int npose = (int)P->poses.size() / 22;
+  std::vector<double> par(24 + P->poses.size());
+  const HX& xc = P->x_curr;
+  memcpy(par.data(), xc.R.a, 72);
+  memcpy(par.data() + 9, xc.p.a, 24);
+  for (int i = 0; i < 9; i++) par[12 + i] = ctx->cfg.ext_R[i];
+  for (int i = 0; i < 3; i++) par[21 + i] = ctx->cfg.ext_t[i];
+  if (!P->poses.empty()) memcpy(par.data() + 24, P->poses.data(), P->poses.size() * sizeof(double));
+  VG_TRY(state_deskew(ctx, par.data(), npose, x, y, z, in, t, n));
+  VG_HIP(hipEventRecord(ctx->ev_scan_ready, ctx->stream));  // the downsample stream reads the result
+  return VG_OK;
+}
+
+// one scan with the deskew: the rest of the pipeline reads the staging buffers
+int host_step_deskew(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di,
+                     const float* dt, int n, double beg, double end, const double* imu, int m) {
+  const vg_config& c = ctx->cfg;
+  VG_TRY(stage_propagate(ctx, imu, m, beg, end));
+  VG_TRY(stage_deskew(ctx, dx, dy, dz, di, dt, n));
+  const float *x = ctx->d_x, *y = ctx->d_y, *z = ctx->d_z, *i = ctx->d_i;
+  VG_TRY(stage_iekf(ctx, x, y, z, n, nullptr));
+  VG_TRY(stage_downsample(ctx, x, y, z, i, n, nullptr));
+  VG_TRY(stage_window_push(ctx, imu, m));
+  VG_TRY(stage_insert(ctx));
+  VG_TRY(stage_recut(ctx, nullptr));
+  if (hp(ctx)->win_count >= c.win_size) {
+    if (c.if_BA == 1) VG_TRY(stage_ba(ctx, nullptr));
+    VG_TRY(stage_margi_slide(ctx));
+  }
+  return stage_finish(ctx);
+}
+
 // one scan of thd_odometry_localmapping's steady-state branch
 int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n, double beg,
               double end, const double* imu, int m) {
-  (void)beg;
   const vg_config& c = ctx->cfg;
-  VG_TRY(stage_propagate(ctx, imu, m, end));
+  VG_TRY(stage_propagate(ctx, imu, m, beg, end));
   // the IEKF is enqueued before the downsample: both read only the raw scan
   // (local_mapping.cpp:396-413), and the main stream should not idle while the
   // host enqueues the downsample onto its own stream

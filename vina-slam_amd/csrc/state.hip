@@ -151,10 +151,71 @@ __global__ void k_publish_ds(int* __restrict__ flags, Pub* __restrict__ pub, int
   }
 }
 
+// ---- IMUEKF::motion_blur's per-point deskew (imu_ekf.cpp:114-144)
+// par: [0..9) x_curr.R (after propagation), [9..12) x_curr.p, [12..21) the
+// LiDAR-to-IMU rotation, [21..24) offset, then npose records of 22 doubles
+// (t offset, R 9, p 3, v 3, w 3, a 3), ascending in t.
+constexpr int kDeskewHead = 24, kDeskewPose = 22;
+__device__ __forceinline__ V3 deskew_point(const double* par, const double* h, double t, V3 P) {
+  const double dt = t - h[0];
+  const M3 R_i = mul(ld_m3(h + 1), Exp(ld_v3(h + 16), dt));
+  const V3 hp = ld_v3(h + 10), hv = ld_v3(h + 13), ha = ld_v3(h + 19), xp = ld_v3(par + 9);
+  V3 T;
+  for (int j = 0; j < 3; j++) T[j] = ((hp[j] + hv[j] * dt) + ((ha[j] * 0.5) * dt) * dt) - xp[j];
+  const M3 Lr = ld_m3(par + 12);
+  const V3 Lo = ld_v3(par + 21);
+  const V3 a = add(mul(Lr, P), Lo);
+  const V3 b = add(mul(R_i, a), T);
+  const V3 c = sub(mul(tr(ld_m3(par)), b), Lo);
+  return mul(tr(Lr), c);
+}
+// One lane per point: the segment is the last IMU pose starting strictly
+// before the point (the reference's backward walk over a time-sorted cloud);
+// points at or before the first pose stay. Point 0 also gets the reference
+// loop's tail: after its own compensation every earlier pose that starts
+// before it compensates it again.
+__global__ void __launch_bounds__(256) k_deskew(int n, int npose, const double* __restrict__ par,
+                                                const float* __restrict__ x, const float* __restrict__ y,
+                                                const float* __restrict__ z, const float* __restrict__ in,
+                                                const float* __restrict__ t, float* __restrict__ ox,
+                                                float* __restrict__ oy, float* __restrict__ oz,
+                                                float* __restrict__ oi) {
+  const double* poses = par + kDeskewHead;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const double ti = (double)t[i];
+    V3 P = v3((double)x[i], (double)y[i], (double)z[i]);
+    int lo = -1, hi = npose - 1;  // last pose with start < ti
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (poses[(size_t)mid * kDeskewPose] < ti) lo = mid;
+      else hi = mid - 1;
+    }
+    float fx = x[i], fy = y[i], fz = z[i];
+    if (lo >= 0) {
+      P = deskew_point(par, poses + (size_t)lo * kDeskewPose, ti, P);
+      fx = (float)P[0];
+      fy = (float)P[1];
+      fz = (float)P[2];
+      if (i == 0)
+        for (int k = lo - 1; k >= 0 && ti > poses[(size_t)k * kDeskewPose]; k--) {
+          P = deskew_point(par, poses + (size_t)k * kDeskewPose, ti, v3((double)fx, (double)fy, (double)fz));
+          fx = (float)P[0];
+          fy = (float)P[1];
+          fz = (float)P[2];
+        }
+    }
+    ox[i] = fx;
+    oy[i] = fy;
+    oz[i] = fz;
+    if (oi != in) oi[i] = in ? in[i] : 0.0f;
+  }
+}
+
 // ---- host wrappers ----
 int state_alloc(vg_ctx* ctx) {
   ctx->st = ctx->arena.take<DState>(1);
-  if (!ctx->st) {
+  ctx->d_deskew = ctx->arena.take<double>(kDeskewBuf);
+  if (!ctx->st || !ctx->d_deskew) {
     ctx->err = "arena exhausted (state)";
     return VG_E_CAPACITY;
   }
@@ -200,6 +261,26 @@ int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq) 
 
 int state_publish_counters(vg_ctx* ctx, int seq) {
   k_publish_counters<<<1, 64, 0, ctx->stream>>>(ctx->map.counters, ctx->d_pub, seq);
+  VG_HIP(hipGetLastError());
+  return VG_OK;
+}
+
+// deskew the scan into the context's staging buffers (in place when the scan
+// already is there). par: the head and the poses (host), uploaded through the
+// pinned staging block.
+int state_deskew(vg_ctx* ctx, const double* par, int npose, const float* x, const float* y, const float* z,
+                 const float* in, const float* t, int n) {
+  const size_t nd = kDeskewHead + (size_t)npose * kDeskewPose;
+  if (nd > (size_t)kDeskewBuf) {
+    ctx->err = "deskew: too many IMU segments in one scan";
+    return VG_E_CAPACITY;
+  }
+  double* stage = ctx->h_stage + kStageDeskewOff;
+  memcpy(stage, par, nd * sizeof(double));
+  VG_HIP(hipMemcpyAsync(ctx->d_deskew, stage, nd * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  if (n > 0)
+    k_deskew<<<grid_for(n), 256, 0, ctx->stream>>>(n, npose, ctx->d_deskew, x, y, z, in, t, ctx->d_x, ctx->d_y,
+                                                    ctx->d_z, ctx->d_i);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }

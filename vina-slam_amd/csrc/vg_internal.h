@@ -225,10 +225,11 @@ struct vg_ctx {
   hipStream_t stream_ds = nullptr;
   hipEvent_t ev_ds_done = nullptr, ev_ds_free = nullptr;
   hipEvent_t ev_recut_done = nullptr, ev_prefix_done = nullptr;  // margi prefix on the second stream
+  hipEvent_t ev_scan_ready = nullptr;  // deskew done (row f1)  // margi prefix on the second stream
   std::string err;
   vg::Arena arena;
   // raw scan staging (SoA)
-  float *d_x = nullptr, *d_y = nullptr, *d_z = nullptr, *d_i = nullptr;
+  float *d_x = nullptr, *d_y = nullptr, *d_z = nullptr, *d_i = nullptr, *d_t = nullptr;
   // the scan the stage-level API works on (own staging or caller's HBM)
   const float *cur_x = nullptr, *cur_y = nullptr, *cur_z = nullptr, *cur_i = nullptr;
   int cur_n = -1;
@@ -241,6 +242,7 @@ struct vg_ctx {
   vg::Pub* h_pub = nullptr;     // host-mapped publication block (host address)
   vg::Pub* d_pub = nullptr;     // its device address
   double* h_stage = nullptr;    // pinned staging for asynchronous H2D copies (kStageBytes)
+  double* d_deskew = nullptr;   // deskew parameters (x_curr pose, extrinsic, IMU poses)
   int pub_seq = 0;
   int* h_pinned = nullptr;  // small pinned host scratch for counters
 
@@ -262,6 +264,8 @@ struct vg_ctx {
 
 namespace vg {
 constexpr size_t kStageBytes = 1 << 17;
+constexpr size_t kStageDeskewOff = 8192;  // doubles: the deskew block's part of the staging area
+constexpr int kDeskewBuf = 4096;          // doubles (up to 180 IMU segments per scan)
 // Spin until a Pub sequence flag reaches seq (the device publishes with a
 // system-scope release); checks the stream for errors while spinning.
 inline int pub_wait(vg_ctx* c, const int* flag, int seq, const char* what, hipStream_t producer = nullptr) {
@@ -378,6 +382,8 @@ int state_slide(vg_ctx* ctx, int win_count, int nimu);
 int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq);
 int state_publish_counters(vg_ctx* ctx, int seq);
 int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq);
+int state_deskew(vg_ctx* ctx, const double* par, int npose, const float* x, const float* y, const float* z,
+                 const float* in, const float* t, int n);
 // ba.hip
 constexpr int kBaX = 24;        // per-frame state: R 9, p 3, v 3, bg 3, ba 3, g 3
 constexpr int kBaImuRec = 64 + 225;
@@ -405,7 +411,11 @@ void shard_free(vg_ctx* ctx);
 int shard_allreduce(vg_ctx* ctx, const void* send, void* recv, int count, int dtype);
 int host_sync(vg_ctx* ctx);
 int host_stats_log(vg_ctx* ctx, vg_stats* out, int cap);
-int stage_propagate(vg_ctx* ctx, const double* imu, int m, double end);
+int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double end);
+int stage_deskew(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, const float* t,
+                 int n);
+int host_step_deskew(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di,
+                     const float* dt, int n, double beg, double end, const double* imu, int m);
 int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n,
                      int* n_ds_out);
 int stage_iekf(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, int n, int* degenerate_out);

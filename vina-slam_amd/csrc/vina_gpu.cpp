@@ -45,7 +45,8 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
       (e = hipEventCreateWithFlags(&ctx->ev_ds_done, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&ctx->ev_ds_free, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&ctx->ev_recut_done, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&ctx->ev_prefix_done, hipEventDisableTiming)) != hipSuccess) {
+      (e = hipEventCreateWithFlags(&ctx->ev_prefix_done, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_scan_ready, hipEventDisableTiming)) != hipSuccess) {
     ctx->err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
@@ -64,6 +65,7 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     ctx->d_y = ctx->arena.take<float>(n);
     ctx->d_z = ctx->arena.take<float>(n);
     ctx->d_i = ctx->arena.take<float>(n);
+    ctx->d_t = ctx->arena.take<float>(n);
     int r = state_alloc(ctx);
     if (r == VG_OK) r = shard_alloc(ctx);
     if (r == VG_OK) r = ds_alloc(ctx);
@@ -152,6 +154,7 @@ int vg_destroy(vg_ctx* ctx) {
   if (ctx->ev_ds_free) (void)hipEventDestroy(ctx->ev_ds_free);
   if (ctx->ev_recut_done) (void)hipEventDestroy(ctx->ev_recut_done);
   if (ctx->ev_prefix_done) (void)hipEventDestroy(ctx->ev_prefix_done);
+  if (ctx->ev_scan_ready) (void)hipEventDestroy(ctx->ev_scan_ready);
   delete ctx;
   return VG_OK;
 }
@@ -250,6 +253,32 @@ int vg_step_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_
   return host_step(ctx, d_x, d_y, d_z, d_intensity, n, pcl_beg_time, pcl_end_time, imu, m);
 }
 
+int vg_step_deskew_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, const float* d_intensity,
+                       const float* d_time, int n, double pcl_beg_time, double pcl_end_time, const double* imu,
+                       int m) {
+  if (!ctx || n < 0 || m < 0 || (m > 0 && !imu) || (n > 0 && (!d_x || !d_y || !d_z || !d_time))) return VG_E_ARG;
+  if (n > ctx->cap.max_points_per_scan) {
+    ctx->err = "scan larger than max_points_per_scan";
+    return VG_E_CAPACITY;
+  }
+  return host_step_deskew(ctx, d_x, d_y, d_z, d_intensity, d_time, n, pcl_beg_time, pcl_end_time, imu, m);
+}
+
+int vg_step_deskew(vg_ctx* ctx, const float* xyz, const float* intensity, const float* time, int n,
+                   double pcl_beg_time, double pcl_end_time, const double* imu, int m) {
+  if (!ctx || (n > 0 && (!xyz || !time)) || n < 0 || m < 0 || (m > 0 && !imu)) return VG_E_ARG;
+  if (n > ctx->cap.max_points_per_scan) {
+    ctx->err = "scan larger than max_points_per_scan";
+    return VG_E_CAPACITY;
+  }
+  if (n > 0) VG_TRY(upload_aos(ctx, xyz, intensity, n));
+  // times ride in the staging area's spare column block (after the 4 SoA planes)
+  float* d_t = ctx->d_t;
+  if (n > 0) VG_HIP(hipMemcpyAsync(d_t, time, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+  VG_HIP(hipStreamSynchronize(ctx->stream));
+  return host_step_deskew(ctx, ctx->d_x, ctx->d_y, ctx->d_z, ctx->d_i, d_t, n, pcl_beg_time, pcl_end_time, imu, m);
+}
+
 int vg_get_state(vg_ctx* ctx, double* state) {
   if (!ctx || !state) return VG_E_ARG;
   VG_TRY(host_state(ctx, state));
@@ -325,8 +354,7 @@ static int need_scan(vg_ctx* ctx) {
 
 int vg_propagate(vg_ctx* ctx, const double* imu, int m, double pcl_beg_time, double pcl_end_time) {
   if (!ctx || m < 0 || (m > 0 && !imu)) return VG_E_ARG;
-  (void)pcl_beg_time;
-  return stage_propagate(ctx, imu, m, pcl_end_time);
+  return stage_propagate(ctx, imu, m, pcl_beg_time, pcl_end_time);
 }
 
 int vg_downsample_scan(vg_ctx* ctx, int* n_ds) {

@@ -101,21 +101,23 @@ class Scene:
         self.panels = P
 
     def cast(self, o, d, max_range=80.0):
-        """Ray-cast from origin o (3,) along unit dirs d (n,3). Returns ranges (n,) and surface id."""
+        """Ray-cast from origin o ((3,) or per ray (n,3)) along unit dirs d (n,3). Returns ranges (n,) and
+        surface id."""
         n = d.shape[0]
+        o2 = np.broadcast_to(o, d.shape)
         best = np.full(n, np.inf)
         sid = np.full(n, -1, dtype=np.int32)
         with np.errstate(divide="ignore", invalid="ignore"):
             for ax in range(3):
                 for k, bound in enumerate((self.box_lo[ax], self.box_hi[ax])):
-                    t = (bound - o[ax]) / d[:, ax]
+                    t = (bound - o2[:, ax]) / d[:, ax]
                     ok = (t > 1e-6) & (t < best)
                     best = np.where(ok, t, best)
                     sid = np.where(ok, 2 * ax + k, sid)
             for j, (c, nrm, a, b, ha, hb) in enumerate(self.panels):
                 den = d @ nrm
-                t = ((c - o) @ nrm) / den
-                p = o[None, :] + t[:, None] * d
+                t = ((c[None, :] - o2) @ nrm) / den
+                p = o2 + t[:, None] * d
                 q = p - c[None, :]
                 ok = (t > 1e-6) & (t < best) & (np.abs(q @ a) <= ha) & (np.abs(q @ b) <= hb)
                 best = np.where(ok, t, best)
@@ -175,6 +177,38 @@ class Sequence:
         xyz = (dn * r[:, None]).astype(np.float32)
         inten = (sid[ok] % 97).astype(np.float32)
         return xyz, inten, te - 0.1, te
+
+    def scan_raw(self, k):
+        """The same sweep as it leaves the sensor: ray (a, ring) fires at
+        beg + 0.1 (a + 1) / A from the pose of that instant and is expressed in the
+        LiDAR frame of that instant (what IMUEKF::motion_blur deskews, SURVEY row
+        f1). Returns xyz float32 (n,3), intensity, per-point time offset from beg
+        (float32, ascending: azimuth-major firing order), beg, end."""
+        rng = np.random.default_rng((self.seed << 20) + k)
+        te = self.t_end(k)
+        beg = te - 0.1
+        na = self.A
+        tr = 0.1 * (np.arange(na) + 1) / na
+        Rs = np.stack([self.traj.rot(beg + t) for t in tr])                   # (A,3,3)
+        ps = np.stack([self.traj.pos(beg + t) for t in tr])
+        a_of = np.repeat(np.arange(na), self.L)                                 # ray -> azimuth index
+        Rl = Rs @ self.ext_R                                                    # (A,3,3)
+        o = (Rs @ self.ext_t) + ps                                              # (A,3)
+        dw = np.einsum("nij,nj->ni", Rl[a_of], self.dirs)
+        r, sid = self.scene.cast(o[a_of], dw)
+        ok = np.isfinite(r) & (r >= self.blind)
+        d = self.dirs[ok]
+        r = r[ok] + rng.normal(0, self.range_sigma, ok.sum())
+        t1 = np.cross(d, np.array([0.0, 0.0, 1.0]))
+        t1 /= np.maximum(np.linalg.norm(t1, axis=1, keepdims=True), 1e-9)
+        t2 = np.cross(d, t1)
+        e = rng.normal(0, self.bearing_sigma, (d.shape[0], 2))
+        dn = d + e[:, :1] * t1 + e[:, 1:] * t2
+        dn /= np.linalg.norm(dn, axis=1, keepdims=True)
+        xyz = (dn * r[:, None]).astype(np.float32)
+        inten = (sid[ok] % 97).astype(np.float32)
+        times = tr[a_of[ok]].astype(np.float32)
+        return xyz, inten, times, beg, te
 
     def imu(self, k):
         """IMU samples (m,7) [t, gx,gy,gz, ax,ay,az] covering [t_{k-1}, t_k] (empty for k=0)."""

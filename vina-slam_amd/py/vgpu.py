@@ -78,6 +78,9 @@ def lib():
         L.vg_seed.argtypes = [P, dp]
         L.vg_step.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
         L.vg_step_dev.argtypes = [P, P, P, P, P, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
+        L.vg_step_deskew.argtypes = [P, fp, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
+        L.vg_step_deskew_dev.argtypes = [P, P, P, P, P, P, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp,
+                                         ctypes.c_int]
         L.vg_get_state.argtypes = [P, dp]
         L.vg_get_stats.argtypes = [P, ctypes.POINTER(Stats)]
         L.vg_stats_log.argtypes = [P, ctypes.POINTER(Stats), ctypes.c_int, ip]
@@ -162,6 +165,21 @@ class Context:
         imu = np.ascontiguousarray(imu, dtype=np.float64).reshape(-1, 7)
         self._chk(lib().vg_step(self.h, _f(xyz), _f(inten), xyz.shape[0], beg, end, _d(imu), imu.shape[0]),
                   "vg_step")
+
+    def step_deskew(self, xyz, inten, times, beg, end, imu):
+        """One scan of raw (not motion-compensated) points with per-point times (row f1)."""
+        xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+        inten = np.ascontiguousarray(inten, dtype=np.float32)
+        times = np.ascontiguousarray(times, dtype=np.float32)
+        imu = np.ascontiguousarray(imu, dtype=np.float64)
+        self._chk(lib().vg_step_deskew(self.h, _f(xyz), _f(inten), _f(times), xyz.shape[0], beg, end, _d(imu),
+                                       imu.shape[0]), "vg_step_deskew")
+
+    def step_deskew_dev(self, dx, dy, dz, di, dt, n, beg, end, imu):
+        imu = np.ascontiguousarray(imu, dtype=np.float64)
+        self._chk(lib().vg_step_deskew_dev(self.h, ctypes.c_void_p(dx), ctypes.c_void_p(dy), ctypes.c_void_p(dz),
+                                           ctypes.c_void_p(di), ctypes.c_void_p(dt), n, beg, end, _d(imu),
+                                           imu.shape[0]), "vg_step_deskew_dev")
 
     def step_dev(self, dx, dy, dz, di, n, beg, end, imu):
         imu = np.ascontiguousarray(imu, dtype=np.float64).reshape(-1, 7)
