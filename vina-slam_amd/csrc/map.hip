@@ -187,11 +187,13 @@ __device__ __forceinline__ bool inside(const NodeHdr& h, const V3& w) {
 // read from the device state the previous k_iekf_update wrote; the kernel is a
 // no-op once the IEKF has finished (st->done). Iteration 0 ignores the leaf
 // cache (no association yet, odometry.cpp:111-132).
-__global__ void __launch_bounds__(256) k_iekf(int n, const float* __restrict__ x, const float* __restrict__ y,
-                                              const float* __restrict__ z, MP mp, DState* __restrict__ st,
-                                              int it, DevMap m, int* __restrict__ cache,
-                                              double* __restrict__ partials) {
+__global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, int it, DevMap m,
+                                              int* __restrict__ cache, double* __restrict__ partials) {
   if (st->done) return;
+  const int n = st->sn;
+  const float* __restrict__ x = st->sx;
+  const float* __restrict__ y = st->sy;
+  const float* __restrict__ z = st->sz;
   double acc[kIekfVals];
   for (int j = 0; j < kIekfVals; j++) acc[j] = 0.0;
   const double* xc = st->xc;
@@ -291,16 +293,26 @@ __global__ void __launch_bounds__(256) k_iekf_reduce(int nb, const double* __res
   if (threadIdx.x < kIekfVals) out[threadIdx.x] = L.o[threadIdx.x];
 }
 
+// grid of the IEKF point loop: sized by the context's capacity (the kernels
+// read the scan size from the device state), a multiple of the 8 XCDs
+static int iekf_blocks(vg_ctx* ctx) {
+  return ((grid_for(ctx->cap.max_points_per_scan, 256, 512) + 7) / 8) * 8;
+}
+
 // one IEKF iteration: the point loop (block partials) and the update; the
 // optional event pair brackets k_iekf alone (vg_profile)
 int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
                    hipEvent_t ev0, hipEvent_t ev1) {
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
-  const int nb = ((grid_for(n, 256, 512) + 7) / 8) * 8;  // a multiple of the 8 XCDs (k_iekf chunking)
-  if (ev0) (void)hipEventRecord(ev0, s);
-  k_iekf<<<nb, 256, 0, s>>>(n, x, y, z, mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials);
-  if (ev1) (void)hipEventRecord(ev1, s);
+  (void)x;
+  (void)y;
+  (void)z;
+  (void)n;  // the scan is read from the device state (state_set_scan)
+  const int nb = iekf_blocks(ctx);
+  if (ev0) VG_HIP(hipEventRecord(ev0, s));
+  k_iekf<<<nb, 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials);
+  if (ev1) VG_HIP(hipEventRecord(ev1, s));
   if (ctx->shard.world > 1) {  // this shard's sums, all-reduced, then the (replicated) update
     double* sums = ctx->shard.d_buf;
     k_iekf_reduce<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, sums);
@@ -310,6 +322,36 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
     k_iekf_update<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, it);
   }
   VG_HIP(hipGetLastError());
+  return VG_OK;
+}
+
+// the four IEKF iterations (odometry.cpp:68). The launches do not change from
+// scan to scan, so an unsharded context captures them once and replays the
+// graph: one host call instead of eight launches, and the device starts each
+// node without the per-launch dispatch gap. The per-stage profiling pass
+// (vg_profile bit 1) launches directly, with an event pair around each k_iekf.
+int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank) {
+  VG_TRY(state_set_scan(ctx, x, y, z, n));
+  const bool graph = ctx->use_graphs && ctx->shard.world <= 1 && !ctx->prof_stages;
+  const bool ev = ctx->prof_on && !graph;
+  auto enqueue = [&]() -> int {
+    for (int it = 0; it < 4; it++)
+      VG_TRY(iekf_iteration(ctx, mp, x, y, z, n, it, ev ? ctx->iekf_ev[bank + it][0] : nullptr,
+                            ev ? ctx->iekf_ev[bank + it][1] : nullptr));
+    return VG_OK;
+  };
+  if (!graph) return enqueue();
+  if (!ctx->g_iekf[0]) {
+    VG_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    const int r = enqueue();
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+    if (r != VG_OK) return r;
+    VG_HIP(e);
+    VG_HIP(hipGraphInstantiate(&ctx->g_iekf[0], g, nullptr, nullptr, 0));
+    VG_HIP(hipGraphDestroy(g));
+  }
+  VG_HIP(hipGraphLaunch(ctx->g_iekf[0], ctx->stream));
   return VG_OK;
 }
 

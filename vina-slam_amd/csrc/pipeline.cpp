@@ -420,18 +420,12 @@ static void propagate(vg_ctx* ctx, HostPipe* P, const std::vector<Imu>& imus, do
 // (SURVEY finding 3: matchVoxelMap always returns 0) and is skipped as
 // output-invariant.
 static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const float* y, const float* z, int n) {
-  const int num_max_iter = 4;
   // event pairs alternate between two banks: scan k's are collected while
   // scan k+1 is being enqueued
   ctx->iekf_ring_base = ctx->iekf_ring_base == 0 ? 8 : 0;
   P->cur.ev_base = ctx->iekf_ring_base;
-  P->cur.ev_n = 0;
-  for (int it = 0; it < num_max_iter; it++) {
-    const int ring = ctx->prof_on ? ctx->iekf_ring_base + P->cur.ev_n++ : -1;
-    VG_TRY(iekf_iteration(ctx, P->mpd, x, y, z, n, it, ring >= 0 ? ctx->iekf_ev[ring][0] : nullptr,
-                          ring >= 0 ? ctx->iekf_ev[ring][1] : nullptr));
-  }
-  return VG_OK;
+  P->cur.ev_n = (ctx->prof_on && (ctx->prof_stages || !ctx->use_graphs || ctx->shard.world > 1)) ? 4 : 0;
+  return iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base);
 }
 
 static WinArg make_winarg(const HostPipe* P, int set_xc) {

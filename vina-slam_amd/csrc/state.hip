@@ -59,6 +59,15 @@ __global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict
   }
 }
 
+__global__ void k_set_scan(DState* __restrict__ st, const float* x, const float* y, const float* z, int n) {
+  if (threadIdx.x == 0) {
+    st->sx = x;
+    st->sy = y;
+    st->sz = z;
+    st->sn = n;
+  }
+}
+
 // x_buf.push_back(x_curr) at ord; a new IMU_PRE (when win_count > 1) starts
 // with zero bias deltas (imu_preintegration.cpp:10-29)
 __global__ void k_push_state(DState* __restrict__ st, int ord, int new_imu) {
@@ -226,6 +235,12 @@ int state_scan_begin(vg_ctx* ctx, const double* xc249) {
   XcArg a;
   memcpy(a.x, xc249, sizeof(a.x));
   k_scan_begin<<<1, 256, 0, ctx->stream>>>(a, ctx->st);
+  VG_HIP(hipGetLastError());
+  return VG_OK;
+}
+
+int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n) {
+  k_set_scan<<<1, 64, 0, ctx->stream>>>(ctx->st, x, y, z, n);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }

@@ -176,6 +176,10 @@ struct DState {
   double xs[kMaxWin * kXS];         // window states x_buf by ord (local_mapping.cpp:434)
   double bias[kMaxWin * 12];        // IMU_PRE bias state per window factor: dbg, dba, dbg_buf, dba_buf
   int it, rematch, done, iters, degenerate, matches[4], ticket, pad[6];
+  // the scan this IEKF reads (set by k_scan_begin's caller, so the IEKF
+  // launches are the same every scan and replay as one hipGraph)
+  const float *sx, *sy, *sz;
+  int sn, pad2;
 };
 // Spatial-tile sharding of one sequence over `world` contexts (one per GPU):
 // every context keeps the root voxels of the tiles it owns (tile_owner) and
@@ -225,7 +229,10 @@ struct vg_ctx {
   hipStream_t stream_ds = nullptr;
   hipEvent_t ev_ds_done = nullptr, ev_ds_free = nullptr;
   hipEvent_t ev_recut_done = nullptr, ev_prefix_done = nullptr;  // margi prefix on the second stream
-  hipEvent_t ev_scan_ready = nullptr;  // deskew done (row f1)  // margi prefix on the second stream
+  hipEvent_t ev_scan_ready = nullptr;  // deskew done (row f1)
+  // the IEKF's 8 launches captured once and replayed (map.hip iekf_run)
+  hipGraphExec_t g_iekf[3] = {nullptr, nullptr, nullptr};
+  bool use_graphs = true;  // margi prefix on the second stream
   std::string err;
   vg::Arena arena;
   // raw scan staging (SoA)
@@ -365,6 +372,8 @@ int map_alloc(vg_ctx* ctx);
 int map_reset(vg_ctx* ctx);
 int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
                    hipEvent_t ev0, hipEvent_t ev1);
+// all four iterations; replays the captured graph when possible
+int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank);
 constexpr int kNeedInsertReplay = 1;  // map_recut: the insert overflowed k_ins_alloc, replay it first
 int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num);
 int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num);
@@ -376,6 +385,7 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
 // state.hip
 int state_alloc(vg_ctx* ctx);
 int state_scan_begin(vg_ctx* ctx, const double* xc249);
+int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n);
 int state_push(vg_ctx* ctx, int ord, int new_imu);
 int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot);
 int state_slide(vg_ctx* ctx, int win_count, int nimu);

@@ -147,6 +147,8 @@ int vg_destroy(vg_ctx* ctx) {
   for (int i = 0; i < 10; i++)
     for (int j = 0; j < 2; j++)
       if (ctx->solve_ev[i][j]) (void)hipEventDestroy(ctx->solve_ev[i][j]);
+  for (auto& g : ctx->g_iekf)
+    if (g) (void)hipGraphExecDestroy(g);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream_ds) (void)hipStreamSynchronize(ctx->stream_ds);
   if (ctx->stream_ds) (void)hipStreamDestroy(ctx->stream_ds);
@@ -431,6 +433,10 @@ int vg_profile_read(vg_ctx* ctx, int stage, double* total_ms, int* count) {
 // the single-workgroup recut apply (0 forces the host-sized replay path).
 extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
   if (!ctx) return VG_E_ARG;
+  if (key == 2) {  // 0: direct launches only (no hipGraph replay)
+    ctx->use_graphs = value != 0;
+    return VG_OK;
+  }
   if (key == 1) {
     ctx->dbg_apply_cap = value;
     return VG_OK;
