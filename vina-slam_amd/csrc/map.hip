@@ -910,7 +910,7 @@ int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num
 // k_rc_apply sets rc[kRcAbort]; the host then replays the rest of the recut
 // with the host-sized path (recut_slow_apply), which only happens while the
 // map is first built.
-enum { kRcLvl = 0, kRcSub = 16, kRcWin = 32, kRcAbort = 48, kRcCh = 64, kRcChBase = 80, kRcN = 128 };
+enum { kRcLvl = 0, kRcSub = 16, kRcWin = 32, kRcAbort = 48, kRcCh = 64, kRcChBase = 80, kRcNOld = 127, kRcN = 128 };
 constexpr int kApplyThreads = 1024;
 constexpr int kApplyEv = 4096;   // events sorted in LDS
 constexpr int kApplySub = kApplyThreads;  // subdividing leaves per level (one lane each)
@@ -1808,6 +1808,7 @@ __device__ __forceinline__ void internal_exist(DevMap& m, int node) {
 __global__ void __launch_bounds__(256) k_margi_internal(int L, int thread_num, DevMap m, int* __restrict__ lists,
                                                         const int* __restrict__ rc, int nseg,
                                                         const uint64_t* __restrict__ segkeys) {
+  if (nseg < 0) nseg = rc[kRcNOld];  // the oldest slot's point count (k_set_jour)
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nseg; j += gridDim.x * blockDim.x) {
     const uint64_t k = segkeys[j];
     if (k == ~0ull) continue;
@@ -1902,6 +1903,7 @@ __global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m
   __syncthreads();
   if (t < (wc - 1) * kXS) st->xs[t] = v;
   if (t < (nimu - 1) * 12) st->bias[t] = b;
+  if (seq2 < 0) seq2 = st->seq2;  // set by k_make_win (replayed graph)
   if (seq2 > 0) {
     __syncthreads();
     if (t < kCntN) __hip_atomic_store(&pub->counters[t], m.counters[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1912,9 +1914,10 @@ __global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m
     }
   }
 }
-__global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, double j, int* __restrict__ rc) {
+__global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, double j, int* __restrict__ rc,
+                                                  int n_oldest) {
   if (blockIdx.x == 0) {  // margi level counts and the leaf count start at zero
-    for (int i = threadIdx.x; i < kRcN; i += blockDim.x) rc[i] = 0;
+    for (int i = threadIdx.x; i < kRcN; i += blockDim.x) rc[i] = (i == kRcNOld) ? n_oldest : 0;
     if (threadIdx.x == 0) m.counters[kCntLeaves] = 0;
   }
   const int n = m.counters[kCntSlide];
@@ -1936,7 +1939,7 @@ int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thr
   VG_HIP(hipEventRecord(ctx->ev_recut_done, ctx->stream));
   VG_HIP(hipStreamWaitEvent(s, ctx->ev_recut_done, 0));
   const int gl = 64;  // grid-stride over device-side counts
-  k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour, w.rc);
+  k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour, w.rc, n_oldest);
   for (int L = 0; L < nlev; L++) k_collect_level<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.list0, w.rc);
   // oldest slot segments by leaf (the slot's point count is known on the host)
   if (n_oldest > 0) {
@@ -1959,28 +1962,49 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   const int nlev = mp.max_layer + 1;
   WinD* dwin = (WinD*)ctx->ba.xs;
   int* dn = (int*)((char*)ctx->ba.xs + sizeof(WinD));
-  // x_curr.R/p <- x_buf.back() and the window view; then the state is final
-  // for this scan and is published before the margi kernels run
-  VG_TRY(state_make_win(ctx, wa, dwin, dn, dn + 32));
-  if (pub_seq > 0) VG_TRY(state_publish(ctx, wa.win_count, ba_iters_dev(ctx), pub_seq));
-  const int gl = 64;
-  VG_HIP(hipStreamWaitEvent(s, ctx->ev_prefix_done, 0));  // map_margi_prefix
-  k_margi_leaf<<<gl, kBlock, 0, s>>>(m.counters + kCntLeaves, w.list0, mp, dwin, m, ctx->ba.fac_eig, ctx->ba.fac_pcr,
-                                     w.plan);
-  k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, w.k1, dwin, m);
-  for (int L = nlev - 1; L >= 1; L--)
-    k_margi_internal<<<L == nlev - 1 ? 128 : gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc,
-                                                                L == nlev - 1 ? n_oldest : 0, w.k1);
-  if (nlev == 1 && n_oldest > 0) k_margi_internal<<<128, kBlock, 0, s>>>(-1, 1 << 30, m, w.list1, w.rc, n_oldest, w.k1);
-  for (int L = 0; L < nlev; L++) k_margi_erase_mark<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc);
-  k_clear_mark<<<gl, kBlock, 0, s>>>(nlev - 2, nlev, thread_num, m, w.list1, w.rc);
-  // slide list compaction, the device-state slide, the counter publication
   if (wa.win_count * kXS > 1024) {
     ctx->err = "win_size too large for the state slide";
     return VG_E_ARG;
   }
-  k_slide_compact<<<1, 1024, 0, s>>>(thread_num, m, ctx->st, wa.win_count, mp.W - 1, ctx->d_pub, pub_seq2);
-  VG_HIP(hipGetLastError());
+  // x_curr.R/p <- x_buf.back() and the window view (k_make_win also stores
+  // the end-of-scan publication number); then the state is final for this
+  // scan and is published before the margi kernels run
+  WinArg wa2 = wa;
+  wa2.seq2 = pub_seq2;
+  VG_TRY(state_make_win(ctx, wa2, dwin, dn, dn + 32));
+  if (pub_seq > 0) VG_TRY(state_publish(ctx, wa.win_count, ba_iters_dev(ctx), pub_seq));
+  VG_HIP(hipStreamWaitEvent(s, ctx->ev_prefix_done, 0));  // map_margi_prefix
+  // the rest reads every per-scan value from the device (n_oldest: rc, the
+  // publication number: the state), so it is captured once and replayed
+  const int gl = 64;
+  auto body = [&]() -> int {
+    k_margi_leaf<<<gl, kBlock, 0, s>>>(m.counters + kCntLeaves, w.list0, mp, dwin, m, ctx->ba.fac_eig,
+                                       ctx->ba.fac_pcr, w.plan);
+    k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, w.k1, dwin, m);
+    for (int L = nlev - 1; L >= 1; L--)
+      k_margi_internal<<<L == nlev - 1 ? 128 : gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc,
+                                                                  L == nlev - 1 ? -1 : 0, w.k1);
+    if (nlev == 1) k_margi_internal<<<128, kBlock, 0, s>>>(-1, 1 << 30, m, w.list1, w.rc, -1, w.k1);
+    for (int L = 0; L < nlev; L++) k_margi_erase_mark<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc);
+    k_clear_mark<<<gl, kBlock, 0, s>>>(nlev - 2, nlev, thread_num, m, w.list1, w.rc);
+    // slide list compaction, the device-state slide, the counter publication
+    k_slide_compact<<<1, 1024, 0, s>>>(thread_num, m, ctx->st, wa.win_count, mp.W - 1, ctx->d_pub, -1);
+    VG_HIP(hipGetLastError());
+    return VG_OK;
+  };
+  (void)n_oldest;
+  if (!ctx->use_graphs || ctx->prof_stages) return body();
+  if (!ctx->g_margi) {
+    VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    const int r = body();
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(s, &g);
+    if (r != VG_OK) return r;
+    VG_HIP(e);
+    VG_HIP(hipGraphInstantiate(&ctx->g_margi, g, nullptr, nullptr, 0));
+    VG_HIP(hipGraphDestroy(g));
+  }
+  VG_HIP(hipGraphLaunch(ctx->g_margi, s));
   return VG_OK;  // device error flags reach the host with the end-of-scan counters
 }
 

@@ -99,6 +99,7 @@ __global__ void k_make_win(DState* __restrict__ st, WinArg wa, WinD* __restrict_
   if (t == 0) {
     win->win_count = wc;
     win->pad = 0;
+    st->seq2 = wa.seq2;
   }
 }
 

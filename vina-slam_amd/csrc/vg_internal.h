@@ -179,7 +179,7 @@ struct DState {
   // the scan this IEKF reads (set by k_scan_begin's caller, so the IEKF
   // launches are the same every scan and replay as one hipGraph)
   const float *sx, *sy, *sz;
-  int sn, pad2;
+  int sn, seq2;
 };
 // Spatial-tile sharding of one sequence over `world` contexts (one per GPU):
 // every context keeps the root voxels of the tiles it owns (tile_owner) and
@@ -215,6 +215,8 @@ struct WinArg {
   int nper[kMaxWin];    // window points per ord
   int win_count;
   int set_xc;           // x_curr.R/p <- x_buf.back() first (local_mapping.cpp:501-502)
+  int seq2;             // end-of-scan publication number (stored in DState::seq2)
+  int pad;
 };
 
 }  // namespace vg
@@ -232,6 +234,7 @@ struct vg_ctx {
   hipEvent_t ev_scan_ready = nullptr;  // deskew done (row f1)
   // the IEKF's 8 launches captured once and replayed (map.hip iekf_run)
   hipGraphExec_t g_iekf[3] = {nullptr, nullptr, nullptr};
+  hipGraphExec_t g_margi = nullptr;  // margi after the window view (map.hip map_margi)
   bool use_graphs = true;  // margi prefix on the second stream
   std::string err;
   vg::Arena arena;

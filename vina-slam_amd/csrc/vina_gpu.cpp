@@ -149,6 +149,7 @@ int vg_destroy(vg_ctx* ctx) {
       if (ctx->solve_ev[i][j]) (void)hipEventDestroy(ctx->solve_ev[i][j]);
   for (auto& g : ctx->g_iekf)
     if (g) (void)hipGraphExecDestroy(g);
+  if (ctx->g_margi) (void)hipGraphExecDestroy(ctx->g_margi);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream_ds) (void)hipStreamSynchronize(ctx->stream_ds);
   if (ctx->stream_ds) (void)hipStreamDestroy(ctx->stream_ds);
