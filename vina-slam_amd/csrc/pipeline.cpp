@@ -191,6 +191,10 @@ void host_init(vg_ctx* ctx) {
   for (int i = 0; i < 3; i++) m.extt[i] = c.ext_t[i];
   m.dept = (float)c.dept_err;
   m.beam = (float)c.beam_err;
+  {
+    const double sb = sin(m.beam * M_PI / 180.0);  // calcBodyVar's (float degree_inc) * M_PI / 180.0
+    m.beam_dv = sb * sb;
+  }
   m.max_layer = c.max_layer;
   m.max_points = c.max_points;
   m.W = c.win_size;

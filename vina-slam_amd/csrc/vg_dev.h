@@ -94,12 +94,12 @@ __device__ __forceinline__ int octant(const V3& p, const double* c) {
 }
 
 // calcBodyVar — point_utils.cpp:3-34 (modifies pb[2] when 0, like the reference)
-__device__ __forceinline__ M3 calc_body_var(V3& pb, float range_inc, float degree_inc) {
+// dv = sin^2(degree_inc * pi / 180) is a per-configuration constant, computed
+// once on the host (MP::beam_dv) instead of one fp64 sin per point
+__device__ __forceinline__ M3 calc_body_var(V3& pb, float range_inc, double dv) {
   if (pb[2] == 0) pb[2] = 0.0001;
   float range = sqrt(pb[0] * pb[0] + pb[1] * pb[1] + pb[2] * pb[2]);
   float range_var = range_inc * range_inc;
-  double s = sin(degree_inc * M_PI / 180.0);
-  double dv = s * s;
   double nb = norm3(pb);
   V3 d = v3(pb[0] / nb, pb[1] / nb, pb[2] / nb);
   M3 dhat = hat(d);
@@ -126,7 +126,7 @@ __device__ __forceinline__ M3 calc_body_var(V3& pb, float range_inc, float degre
 // extrinsic) and its covariance.
 __device__ __forceinline__ void var_init_pt(const MP& mp, float x, float y, float z, V3& pnt, M3& var) {
   V3 pb = v3(x, y, z);
-  M3 vb = calc_body_var(pb, mp.dept, mp.beam);
+  M3 vb = calc_body_var(pb, mp.dept, mp.beam_dv);
   M3 eR = ld_m3(mp.extR);
   pnt = rigid(eR, pb, ld_v3(mp.extt));
   var = mul(mul(eR, vb), tr(eR));

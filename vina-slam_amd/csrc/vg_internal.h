@@ -349,6 +349,7 @@ struct MP {
   double extR[9], extt[3];
   float dept, beam;   // dept_err / beam_err as the float params of calcBodyVar
   int max_layer, max_points, W, pad;
+  double beam_dv;     // sin^2(beam * pi / 180) of calcBodyVar (point_utils.cpp:13-14), with beam in float
 };
 
 struct WinD {           // window poses x_buf (by ord) and the ring mp[] (octree.cpp:75)
