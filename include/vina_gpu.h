@@ -185,7 +185,8 @@ int vg_shard_host(vg_ctx* ctx, int rank, int world, vg_host_allreduce_fn fn, voi
  * factor extraction, 4 BA, 5 margi, 6 whole IEKF, 7 the LDL^T solve kernel
  * (k_ba_solve); 8..15 the HOST time of the stage calls (enqueue + waits):
  * propagate, downsample, IEKF, window push, insert, recut, BA, margi. `on`: 0 off, 1 the k_iekf and k_ba_solve launches only
- * (stages 1 and 7; cheap enough for a timed region), 3 every stage.
+ * (stages 1 and 7; cheap enough for a timed region), 3 every stage; bits 8-15
+ * (n > 1) time k_ba_solve on every n-th BA run only.
  * vg_profile resets the accumulators; vg_profile_read returns total ms and the
  * number of intervals. */
 int vg_profile(vg_ctx* ctx, int on);

@@ -83,15 +83,19 @@ def test_cpp_replay_driver_matches(oracle_lib):
     assert np.abs(tum[:, 1:4] - to[:, 10:13]).max() < 1e-6
 
 
-def test_recut_replay_path_equals_fast_path():
-    """The host-sized recut replay (taken when a level's subdivision exceeds the
-    single-workgroup apply's LDS capacity) gives bit-identical results."""
-    import ctypes
+@pytest.mark.parametrize("knob", [1, 3, 4], ids=["recut-level-replay", "insert-replay", "host-factor-sort"])
+def test_recut_replay_path_equals_fast_path(knob):
+    """The host-sized fallbacks give bit-identical results: the recut replay
+    (a level's subdivision exceeds the single-workgroup apply's LDS capacity,
+    knob 1), the insert replay (k_ins_alloc's capacity, knob 3) and the host
+    factor sort (more factors than the device sort holds, knob 4). In the
+    window-full scans the recut runs asynchronously, so these exercise the
+    LM-skip / host-completion path of stage_ba as well."""
     p = vgconfig.load("mid360")
     seq = _seq(p, seq_id=6)
     a = vgpu.Context(vgconfig.to_c(p), **CAP)
     b = vgpu.Context(vgconfig.to_c(p), **CAP)
-    assert vgpu.lib().vgx_debug(b.h, 1, 0) == 0  # every level replays
+    assert vgpu.lib().vgx_debug(b.h, knob, 0) == 0  # capacity 0: every occurrence takes the fallback
     a.seed(seq.gt_state(0))
     b.seed(seq.gt_state(0))
     for k in range(14):

@@ -34,7 +34,7 @@ namespace vg {
 
 constexpr int kMaxW = 16;
 constexpr int kCompF = 24;    // per factor: umumT 9, ukukT 9, uk 3, NN, coe, lmbd0
-constexpr int kImuRec = 64 + 225;  // preintegration record + cov_inv
+constexpr int kImuRec = kBaImuRec;  // preintegration record + cov_inv
 
 struct BaState {             // device-resident LM state
   double u, v, res1, res2, q1;
@@ -126,11 +126,15 @@ __device__ void imu_residual(const double* rec, const double* bias, const double
   put(12, 27, M3::I());
 }
 
+// IMU record k of DState's ring (pushed by k_push_state, slid by moving the head)
+__device__ __forceinline__ const double* imu_rec(const double* imurec, int head, int k) {
+  return &imurec[(size_t)((head + k) % kMaxWin) * kImuRec];
+}
 // give_evaluate with jac_enable at the current state; out per factor: jtj 900, gg 30, res 1
-__device__ void imu_factor_block(int k, const double* __restrict__ imurec, const double* __restrict__ bias,
+__device__ void imu_factor_block(int k, const double* __restrict__ imurec, int head, const double* __restrict__ bias,
                                  const double* __restrict__ xs, double* __restrict__ out) {
   __shared__ double joc[450], rr[15], P[450], C[225];
-  const double* rec = &imurec[(size_t)k * kImuRec];
+  const double* rec = imu_rec(imurec, head, k);
   if (threadIdx.x == 0) imu_residual(rec, &bias[k * 12], &xs[(size_t)k * kX], &xs[(size_t)(k + 1) * kX], rr, joc);
   for (int t = threadIdx.x; t < 225; t += blockDim.x) C[t] = rec[64 + t];
   __syncthreads();
@@ -169,9 +173,9 @@ __device__ void imu_factor_block(int k, const double* __restrict__ imurec, const
 }
 
 // IMU residuals only (give_evaluate(..., false)) at the trial state
-__device__ void imu_residual_lane(int k, const double* __restrict__ imurec, const double* __restrict__ bias,
+__device__ void imu_residual_lane(int k, const double* __restrict__ imurec, int head, const double* __restrict__ bias,
                                   const double* __restrict__ xt, double* __restrict__ res) {
-  const double* rec = &imurec[(size_t)k * kImuRec];
+  const double* rec = imu_rec(imurec, head, k);
   double rr[15];
   imu_residual(rec, &bias[k * 12], &xt[(size_t)k * kX], &xt[(size_t)(k + 1) * kX], rr, nullptr);
   double cr[15];
@@ -260,6 +264,8 @@ __device__ __forceinline__ void factor_frame(const double* e, const Clu& pa, con
 __device__ __forceinline__ int lower_idx(int r, int c) { return r * (r + 1) / 2 + c; }
 
 constexpr int kHessThreads = 256;
+constexpr int kHessGridMax = 256;  // k_ba_hess chunk workgroups (more chunks loop)
+constexpr int kResidBlocks = 64;   // k_ba_resid workgroups (more factors loop)
 __host__ __device__ constexpr int hess_fs(int W) { return kHessThreads / W < 64 ? kHessThreads / W : 64; }  // factors per sub-chunk
 __host__ __device__ constexpr int hess_ks(int W) { return (3 * hess_fs(W) + 3) / 4 * 4; }  // GEMM K per sub-chunk
 __host__ __device__ constexpr int hess_nt(int W) { return (6 * W + 15) / 16; }           // 16-wide output tiles
@@ -272,19 +278,11 @@ __host__ __device__ constexpr int hess_chunk(int W) { return 2 * hess_fs(W); }  
 // X (LDS); the off-diagonal blocks are then X^T S X on v_mfma_f64_16x16x4
 // (one wave per lower 16x16 output tile, accumulators live across
 // sub-chunks). Chunk partials go to `part` (summed by k_ba_hfinal).
-__global__ void __launch_bounds__(kHessThreads) k_ba_hess(int nf, int W, const int* __restrict__ fac_node,
-                                                          const double* __restrict__ fac_eig,
-                                                          const Clu* __restrict__ fac_pcr, const Clu* __restrict__ pcrs,
-                                                          const int* __restrict__ mpring, const double* __restrict__ xs,
-                                                          double* __restrict__ part, const BaState* __restrict__ st,
-                                                          int nchunk, int nimu, const double* __restrict__ imurec,
-                                                          const double* __restrict__ bias, double* __restrict__ imuout) {
-  if (st->done || !st->calc_hess) return;
-  if ((int)blockIdx.x >= nchunk) {  // IMU factors ride in the same launch (give_evaluate, jac_enable)
-    const int k = blockIdx.x - nchunk;
-    if (k < nimu) imu_factor_block(k, imurec, bias, xs, imuout);
-    return;
-  }
+__device__ __forceinline__ void hess_chunk_eval(int ch, int nf, int W, const int* __restrict__ fac_node,
+                                                const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
+                                                const Clu* __restrict__ pcrs, const int* __restrict__ mpring,
+                                                const double* __restrict__ xs, double* __restrict__ part) {
+  __syncthreads();  // the previous chunk's reduction has read the LDS
   extern __shared__ __attribute__((aligned(16))) double X[];
   __shared__ double S[kHessThreads];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -292,7 +290,7 @@ __global__ void __launch_bounds__(kHessThreads) k_ba_hess(int nf, int W, const i
   const int L = 6 * W, nl = L * (L + 1) / 2, nout = nl + L + 1;
   const int f = tid / W, i = tid % W;
   const bool active = f < FS;
-  const int a_begin = blockIdx.x * hess_chunk(W);
+  const int a_begin = ch * hess_chunk(W);
   const int a_end = min(nf, a_begin + hess_chunk(W));
   double hb[21], jj[6], res = 0.0;
   for (int k = 0; k < 21; k++) hb[k] = 0.0;
@@ -347,7 +345,7 @@ __global__ void __launch_bounds__(kHessThreads) k_ba_hess(int nf, int W, const i
     }
     __syncthreads();
   }
-  double* out = &part[(size_t)blockIdx.x * nout];
+  double* out = &part[(size_t)ch * nout];
   // off-diagonal blocks from the MFMA tiles (diagonal 6x6 blocks come from Hb)
   for (int q = wave, slot = 0; q < ntl; q += kHessThreads / 64, slot++) {
     int TI = 0;
@@ -388,11 +386,35 @@ __global__ void __launch_bounds__(kHessThreads) k_ba_hess(int nf, int W, const i
   }
 }
 
+// The factor count is read on the device (*nfp): workgroups [0, G) loop over
+// the chunks (chunk c -> partial c, whatever G), G + k evaluates IMU factor k.
+__global__ void __launch_bounds__(kHessThreads) k_ba_hess(const int* __restrict__ nfp, int W,
+                                                          const int* __restrict__ fac_node,
+                                                          const double* __restrict__ fac_eig,
+                                                          const Clu* __restrict__ fac_pcr, const Clu* __restrict__ pcrs,
+                                                          const int* __restrict__ mpring, const double* __restrict__ xs,
+                                                          double* __restrict__ part, const BaState* __restrict__ st,
+                                                          int G, int nimu, const double* __restrict__ imurec,
+                                                          const int* __restrict__ imu_head,
+                                                          const double* __restrict__ bias, double* __restrict__ imuout) {
+  if (st->done || !st->calc_hess) return;
+  if ((int)blockIdx.x >= G) {  // IMU factors ride in the same launch (give_evaluate, jac_enable)
+    const int k = blockIdx.x - G;
+    if (k < nimu) imu_factor_block(k, imurec, *imu_head, bias, xs, imuout);
+    return;
+  }
+  const int nf = *nfp;
+  const int nchunk = (nf + hess_chunk(W) - 1) / hess_chunk(W);
+  for (int ch = blockIdx.x; ch < nchunk; ch += G) hess_chunk_eval(ch, nf, W, fac_node, fac_eig, fac_pcr, pcrs, mpring, xs, part);
+}
+
 // ordered sum of the chunk partials: 8 lanes per output split the chunks
 // (stride 8), then a fixed 3-step shuffle tree (deterministic)
-__global__ void __launch_bounds__(256) k_ba_hfinal(int nchunk, int nout, const double* __restrict__ part,
-                                                   double* __restrict__ out, const BaState* __restrict__ st) {
+__global__ void __launch_bounds__(256) k_ba_hfinal(const int* __restrict__ nfp, int chunk, int nout,
+                                                   const double* __restrict__ part, double* __restrict__ out,
+                                                   const BaState* __restrict__ st) {
   if (st->done || !st->calc_hess) return;
+  const int nchunk = (*nfp + chunk - 1) / chunk;
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = gt >> 3, sub = gt & 7;
   double s = 0.0;
@@ -775,22 +797,24 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
 #endif
 }
 
-// evaluate_only_residual (factors.cpp:128-158) at the trial poses
-__global__ void __launch_bounds__(256) k_ba_resid(int nf, int W, const int* __restrict__ fac_node,
+// evaluate_only_residual (factors.cpp:128-158) at the trial poses; workgroup
+// b < nrb sums factors b*256 + t + k*nrb*256 (the device factor count *nfp)
+__global__ void __launch_bounds__(256) k_ba_resid(const int* __restrict__ nfp, int W, const int* __restrict__ fac_node,
                                                   const Clu* __restrict__ pcr_fix, const Clu* __restrict__ pcrs,
                                                   const int* __restrict__ mpring, const double* __restrict__ xt,
                                                   double* __restrict__ fac_eig, Clu* __restrict__ fac_pcr,
                                                   double* __restrict__ rpart, const BaState* __restrict__ st, int nrb,
                                                   int nimu, const double* __restrict__ imurec,
+                                                  const int* __restrict__ imu_head,
                                                   const double* __restrict__ bias, double* __restrict__ imures) {
   if (st->done) return;
   if ((int)blockIdx.x >= nrb) {  // IMU residuals at the trial state in the same launch
-    if ((int)threadIdx.x < nimu) imu_residual_lane(threadIdx.x, imurec, bias, xt, imures);
+    if ((int)threadIdx.x < nimu) imu_residual_lane(threadIdx.x, imurec, *imu_head, bias, xt, imures);
     return;
   }
   double acc = 0.0;
-  const int a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a < nf) {
+  const int nf = *nfp;
+  for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < nf; a += nrb * blockDim.x) {
     const int node = fac_node[a];
     Clu sig = pcr_fix[node];
     for (int i = 0; i < W; i++) {
@@ -807,7 +831,7 @@ __global__ void __launch_bounds__(256) k_ba_resid(int nf, int W, const int* __re
     for (int j = 0; j < 3; j++) e[j] = ev[j];
     for (int j = 0; j < 9; j++) e[3 + j] = U[j];
     fac_pcr[a] = sig;
-    acc = 1.0 * ev[0];
+    acc += 1.0 * ev[0];
   }
   __shared__ double red[4];
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
@@ -893,7 +917,8 @@ struct MpRing {
 };
 // LM state (optimizers.cpp:436-441), the reduced-Hessian accumulator, the ring
 __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict__ hl, double* __restrict__ hl_part,
-                                                 int nout, MpRing ring, int* __restrict__ mpring, int W) {
+                                                 int nout, MpRing ring, int* __restrict__ mpring, int W,
+                                                 const int* __restrict__ rc_status) {
   for (int t = threadIdx.x; t < nout; t += blockDim.x) {
     hl[t] = 0.0;
     hl_part[t] = 0.0;
@@ -904,7 +929,7 @@ __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict
     st->v = 2;
     st->res1 = st->res2 = st->q1 = 0.0;
     st->calc_hess = 1;
-    st->done = 0;
+    st->done = (rc_status && *rc_status) ? 1 : 0;  // an asynchronous recut that needs the host: skip
     st->iters = 0;
   }
 }
@@ -954,7 +979,7 @@ int ba_alloc(vg_ctx* ctx) {
   good &= (b.hpart = ctx->arena.take<double>((size_t)(b.cap_f / hess_chunk(W) + 1) * nout)) != nullptr;
   good &= (b.hout = ctx->arena.take<double>(nout + 16)) != nullptr;
   good &= (b.hout_part = ctx->arena.take<double>(nout + 16)) != nullptr;
-  good &= (b.rpart = ctx->arena.take<double>(b.cap_f / 256 + 16)) != nullptr;
+  good &= (b.rpart = ctx->arena.take<double>(kResidBlocks + 16)) != nullptr;
   good &= (b.xs = ctx->arena.take<double>(1024 + 2 * n * (n + 1) / 2 + 4 * n + kMaxNB * (kMaxNB + 1) / 2 * 256 + 4 * kMaxNB * kTile + 2 * kMaxW * kX + kMaxW * kImuRec +
                                           kMaxW * 12 + kMaxW * 931 + kMaxW + 64)) != nullptr;
   if (!good) {
@@ -1000,7 +1025,7 @@ static BaDev carve(vg_ctx* ctx) {
   p += kMaxW * kX;
   d.xt = p;
   p += kMaxW * kX;
-  d.imurec = p;
+  d.imurec = ctx->st->imurec;
   p += kMaxW * kImuRec;
   d.bias = ctx->st->bias;
   p += kMaxW * 12;
@@ -1023,7 +1048,7 @@ const int* ba_iters_dev(vg_ctx* ctx) { return &carve(ctx).st->iters; }
 // Run damping_iter on the device state. imurec: (W-1) x kImuRec host records
 // (pinned staging, uploaded asynchronously). The window states and the IMU
 // bias records are read and written in DState.
-int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* iters,
+int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
            const std::function<int()>& before_first_wait) {
   const int W = ctx->cfg.win_size;
   if (15 * W > kMaxNB * kTile) {
@@ -1034,51 +1059,53 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* i
   BaDev d = carve(ctx);
   const int nimu = W - 1;
   const int L = 6 * W, nl = L * (L + 1) / 2, nout = nl + L + 1;
-  // one H2D copy of the host-side inputs: IMU records, then the mp ring
-  double* stage = ctx->h_stage;
-  memcpy(stage, imurec, (size_t)nimu * kImuRec * sizeof(double));
-  static_assert((size_t)kMaxW * kImuRec * sizeof(double) <= kStageBytes, "staging block too small");
-  VG_HIP(hipMemcpyAsync(d.imurec, stage, (size_t)nimu * kImuRec * sizeof(double), hipMemcpyHostToDevice, s));
+  // the IMU records are in DState's ring (k_push_state), the mp ring rides in k_ba_init's arguments
   MpRing ring;
   for (int i = 0; i < kMaxW; i++) ring.mp[i] = i < W ? mp_ring[i] : 0;
   const bool sharded = ctx->shard.world > 1;
   double* hl_part = ctx->ba.hout_part;  // this shard's LiDAR Hessian (sharded mode)
   double* rsum = ctx->shard.d_buf + 256;  // [0]: this shard's residual, [1]: all-reduced
-  k_ba_init<<<1, 256, 0, s>>>(d.st, d.hl, hl_part, nout, ring, d.mpring, W);
-  const int nchunk = (nf + hess_chunk(W) - 1) / hess_chunk(W);
-  const int nrb = (nf + 255) / 256;
+  k_ba_init<<<1, 256, 0, s>>>(d.st, d.hl, hl_part, nout, ring, d.mpring, W, map_rc_status(ctx));
+  // factor count on the device (the recut's kCntFactors): fixed grids, so an
+  // asynchronous recut needs no host round trip before the LM
+  (void)nf;
+  const int* nfp = ctx->map.counters + kCntFactors;
+  const int G = std::min(kHessGridMax, ctx->ba.cap_f / hess_chunk(W) + 1);
+  const int nrb = kResidBlocks;
   const size_t hess_lds = hess_lds_bytes(W);
   const size_t solve_lds = solve_lds_bytes(W);
   const int NBt = (15 * W + kTile - 1) / kTile, ntile = NBt * (NBt + 1) / 2;
   const int seq0 = ctx->pub_seq + 1;
   ctx->pub_seq += 10;
   int xerr = VG_OK;  // exchange errors (sharded mode)
+  // k_ba_solve launch events (vg_profile): on every prof_every-th run only, so
+  // that timing a long run costs the stream little (each record is a gap)
+  const bool solve_ev = ctx->prof_on && (ctx->prof_every <= 1 || ctx->prof_runs++ % ctx->prof_every == 0);
   // one LM iteration (optimizers.cpp:449-516); kernels early-exit on the
   // device-side flags once converged
   auto iteration = [&](int k) {
-    if (nf > 0 || nimu > 0)
-      k_ba_hess<<<(nf > 0 ? nchunk : 0) + nimu, kHessThreads, hess_lds, s>>>(
-          nf, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr, ctx->map.pcrs, d.mpring, d.xs, d.part, d.st,
-          nf > 0 ? nchunk : 0, nimu, d.imurec, d.bias, d.imuout);
-    if (nf > 0) k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nchunk, nout, d.part, sharded ? hl_part : d.hl, d.st);
+    k_ba_hess<<<G + nimu, kHessThreads, hess_lds, s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
+                                                      ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, nimu, d.imurec, &ctx->st->imu_head,
+                                                      d.bias, d.imuout);
+    k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, sharded ? hl_part : d.hl,
+                                                       d.st);
     // sharded: every shard's factors -> one LiDAR Hessian / gradient / residual
     // (out of place: a rejected step re-reduces the unchanged partial)
     if (sharded && xerr == VG_OK) xerr = shard_allreduce(ctx, hl_part, d.hl, nout, 0);
     k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
                                     d.dvec, d.jvec, d.ipg, d.st);
-    if (ctx->prof_on) (void)hipEventRecord(ctx->solve_ev[k][0], s);
+    if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][0], s);
     k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
                                          d.st);
-    if (ctx->prof_on) (void)hipEventRecord(ctx->solve_ev[k][1], s);
-    if (nf > 0 || nimu > 0)
-      k_ba_resid<<<(nf > 0 ? nrb : 0) + (nimu > 0 ? 1 : 0), 256, 0, s>>>(
-          nf, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt, ctx->ba.fac_eig, ctx->ba.fac_pcr,
-          d.rpart, d.st, nf > 0 ? nrb : 0, nimu, d.imurec, d.bias, d.imures);
+    if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][1], s);
+    k_ba_resid<<<nrb + 1, 256, 0, s>>>(nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
+                                       ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, nimu, d.imurec, &ctx->st->imu_head, d.bias,
+                                       d.imures);
     if (sharded) {  // the residual over every shard's factors
-      k_ba_rsum<<<1, 64, 0, s>>>(nf > 0 ? nrb : 0, d.rpart, rsum, d.st);
+      k_ba_rsum<<<1, 64, 0, s>>>(nrb, d.rpart, rsum, d.st);
       if (xerr == VG_OK) xerr = shard_allreduce(ctx, rsum, rsum + 1, 1, 0);
     }
-    k_ba_control<<<1, 256, 0, s>>>(W, nimu, sharded ? 1 : (nf > 0 ? nrb : 0), ctx->cfg.imu_coef, d.hl, nl + L,
+    k_ba_control<<<1, 256, 0, s>>>(W, nimu, sharded ? 1 : nrb, ctx->cfg.imu_coef, d.hl, nl + L,
                                    d.imuout, d.imures, sharded ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st,
                                    ctx->d_pub, seq0 + k);
   };
@@ -1097,7 +1124,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* i
     if (__atomic_load_n(&ctx->h_pub->ba_done, __ATOMIC_ACQUIRE)) break;
   }
   *iters = done_iters;
-  if (ctx->prof_on)  // k_ba_solve of the executed iterations only (the bench's roofline)
+  if (solve_ev)  // k_ba_solve of the executed iterations only (the bench's roofline)
     for (int it = 0; it < done_iters && it < 10; it++) {
       float ms = 0;
       if (hipEventElapsedTime(&ms, ctx->solve_ev[it][0], ctx->solve_ev[it][1]) == hipSuccess) {

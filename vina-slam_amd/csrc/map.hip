@@ -76,6 +76,7 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(w.pw = ctx->arena.take<double>(cw * 3));
   good &= ok(w.iekf_cache = ctx->arena.take<int>(cw));
   good &= ok(w.rc = ctx->arena.take<int>(128));
+  good &= ok(w.cand_bits = ctx->arena.take<uint32_t>(ctx->cap.max_nodes / 32 + 1));
   good &= ok(w.plan = ctx->arena.take<int>(cn * 8));
   w.nparts = 1024;
   good &= ok(w.partials = ctx->arena.take<double>((size_t)w.nparts * 40));
@@ -93,7 +94,7 @@ int map_alloc(vg_ctx* ctx) {
     ctx->err = "arena exhausted (sort workspace)";
     return VG_E_CAPACITY;
   }
-  return VG_OK;
+  return map_set_attrs(ctx);
 }
 
 int map_reset(vg_ctx* ctx) {
@@ -104,6 +105,7 @@ int map_reset(vg_ctx* ctx) {
   VG_HIP(hipMemsetAsync(m.hval, 0xff, hs * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.hfirst, 0x7f, hs * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.counters, 0, kCntN * sizeof(int), s));
+  VG_HIP(hipMemsetAsync(ctx->wk.cand_bits, 0, (ctx->cap.max_nodes / 32 + 1) * sizeof(uint32_t), s));
   VG_HIP(hipMemsetAsync(m.in_slide, 0, m.cap_nodes, s));
   VG_HIP(hipMemsetAsync(m.cfirst, 0x7f, (size_t)m.cap_nodes * 8 * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.nscr, 0xff, (size_t)m.cap_nodes * 4 * sizeof(int), s));
@@ -728,13 +730,14 @@ __global__ void k_ins_roots(DevMap m, const uint32_t* __restrict__ flag, const u
 // records zeroed. More than kInsAllocCap parents sets the abort flag and the
 // host replays the allocation on the host-sized path.
 constexpr int kInsAllocCap = 4096;
-__global__ void __launch_bounds__(1024) k_ins_alloc(int thread_num, DevMap m, const int* __restrict__ reqlist) {
+__global__ void __launch_bounds__(1024) k_ins_alloc(int thread_num, DevMap m, const int* __restrict__ reqlist,
+                                                    int cap) {
   __shared__ int sp[kInsAllocCap];
   __shared__ int s_w[17];
   if (g_touched(m) < thread_num) return;
   const int np = m.counters[kCntCreate];
   if (np == 0) return;
-  if (np > kInsAllocCap) {
+  if (np > cap) {
     if (threadIdx.x == 0) m.counters[kCntMisc] = 1;
     return;
   }
@@ -883,7 +886,8 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread
     VG_TRY(shard_allreduce(ctx, m.counters + kCntGTouched, m.counters + kCntGTouched, 1, 1));
   }
   k_ins_descend<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.leaf, w.list2);
-  k_ins_alloc<<<1, 1024, 0, s>>>(thread_num, m, w.list2);
+  const int ins_cap = (ctx->dbg_ins_cap >= 0 && ctx->dbg_ins_cap < kInsAllocCap) ? ctx->dbg_ins_cap : kInsAllocCap;
+  k_ins_alloc<<<1, 1024, 0, s>>>(thread_num, m, w.list2, ins_cap);
   return insert_tail(ctx, mp, slot, n, thread_num);
 }
 
@@ -910,7 +914,8 @@ int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num
 // k_rc_apply sets rc[kRcAbort]; the host then replays the rest of the recut
 // with the host-sized path (recut_slow_apply), which only happens while the
 // map is first built.
-enum { kRcLvl = 0, kRcSub = 16, kRcWin = 32, kRcAbort = 48, kRcCh = 64, kRcChBase = 80, kRcNOld = 127, kRcN = 128 };
+enum { kRcLvl = 0, kRcSub = 16, kRcWin = 32, kRcAbort = 48, kRcCh = 64, kRcChBase = 80, kRcStatus = 126, kRcNOld = 127,
+       kRcN = 128 };
 constexpr int kApplyThreads = 1024;
 constexpr int kApplyEv = 4096;   // events sorted in LDS
 constexpr int kApplySub = kApplyThreads;  // subdividing leaves per level (one lane each)
@@ -951,7 +956,8 @@ __device__ __forceinline__ void recut_visit_node(int node, const MP& mp, DevMap&
 
 __global__ void __launch_bounds__(256) k_rc_visit(int L, int thread_num, const int* __restrict__ work_in, MP mp,
                                                   DevMap m, int* __restrict__ next, int* __restrict__ sub,
-                                                  int* __restrict__ cand, int* __restrict__ rc) {
+                                                  int* __restrict__ cand, int* __restrict__ rc,
+                                                  uint32_t* __restrict__ cand_bits) {
   if (rc[kRcAbort]) return;
   const int nw = (L == 0) ? m.counters[kCntSlide] : rc[kRcLvl + L - 1];
   if (L == 0 && g_slide(m) < thread_num) return;  // local_mapping.cpp:150-154 (global count)
@@ -965,7 +971,10 @@ __global__ void __launch_bounds__(256) k_rc_visit(int L, int thread_num, const i
     int o2 = wave_append(&m.counters[kCntFactors], is_cand);
     int o3 = wave_append(&rc[kRcSub + L], is_sub);
     for (int j = 0; j < nchild; j++) next[o1 + j] = kids[j];
-    if (is_cand) cand[o2] = node;
+    if (is_cand) {
+      cand[o2] = node;
+      if (cand_bits) atomicOr(&cand_bits[node >> 5], 1u << (node & 31));  // k_fac_sort's id order
+    }
     if (is_sub) sub[o3] = node;
   }
 }
@@ -1481,47 +1490,77 @@ __global__ void k_recut_begin(DevMap m, int* __restrict__ rc, int thread_num) {
   }
 }
 
-// multi_recut (local_mapping.cpp:144-201) then tras_opt. Returns the factor
-// count, or kNeedInsertReplay when the preceding insert must be replayed first
-// (nothing of the recut ran).
-int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay) {
-  DevMap& m = ctx->map;
+// Asynchronous factor extraction (tras_opt, octree.cpp:491-516) sized on the
+// device. k_rc_visit marks every candidate in a bitmap over node ids; one
+// workgroup turns the bitmap into the id-ascending factor list (the host
+// path's sort order) with one prefix sum over the allocated id range, clearing
+// it as it reads, then k_factor_finish_dev fills the factor arrays. k_fac_sort
+// also publishes the recut status and the factor count (Pub::seq_rc) and
+// leaves the status in rc[kRcStatus], where k_ba_init reads it: a recut that
+// needs the host-sized path (insert replay, level overflow, more factors than
+// max_fac) makes the LM skip, and the host completes the recut and reruns it.
+constexpr int kFacMax = 1 << 20;
+constexpr int kRcBig = 200;
+__global__ void __launch_bounds__(1024) k_fac_sort(DevMap m, int* __restrict__ rc, uint32_t* __restrict__ bits,
+                                                   int* __restrict__ fac_node, int cap_f, Pub* __restrict__ pub,
+                                                   int seq, int max_fac) {
+  __shared__ int s_w[17];
+  const int nf = m.counters[kCntFactors];
+  int status = rc[kRcAbort];
+  if (status == 0 && (nf > cap_f || nf > max_fac)) status = kRcBig;
+  const int words = (m.counters[kCntNodes] + 31) >> 5;
+  const int per = (words + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int w0 = threadIdx.x * per, w1 = min(words, w0 + per);
+  int cnt = 0;
+  for (int w = w0; w < w1; w++) cnt += __popc(bits[w]);
+  int total;
+  int pos = block_excl_scan(cnt, s_w, &total);
+  if (status == 0 && total != nf) status = kRcBig;  // the two counts disagree: let the host path decide
+  for (int w = w0; w < w1; w++) {
+    uint32_t b = bits[w];
+    if (b == 0) continue;
+    bits[w] = 0;
+    if (status == 0)
+      while (b) {
+        const int k = __ffs(b) - 1;
+        b &= b - 1;
+        fac_node[pos++] = (w << 5) + k;
+      }
+  }
+  if (threadIdx.x == 0) {
+    rc[kRcStatus] = status;
+    __hip_atomic_store(&pub->rc_status, status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&pub->rc_nf, nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __hip_atomic_store(&pub->seq_rc, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+__global__ void __launch_bounds__(256) k_factor_finish_dev(const int* __restrict__ rc, DevMap m,
+                                                           const int* __restrict__ fac_node,
+                                                           double* __restrict__ fac_eig, Clu* __restrict__ fac_pcr) {
+  if (rc[kRcStatus]) return;
+  const int nf = m.counters[kCntFactors];
+  for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < nf; a += gridDim.x * blockDim.x) {
+    const int node = fac_node[a];
+    m.hdr[node].opt_state = a;
+    for (int j = 0; j < 12; j++) fac_eig[(size_t)a * 12 + j] = m.eig[(size_t)node * 12 + j];
+    fac_pcr[a] = m.pcr_add[node];
+  }
+}
+const int* map_rc_status(vg_ctx* ctx) { return ctx->wk.rc + kRcStatus; }
+int map_set_attrs(vg_ctx* ctx) {
+  (void)ctx;
+  return VG_OK;
+}
+
+// the host-sized rest of a recut whose device status (hrc) is in: insert
+// replay request, level-overflow replay, factor sort and extraction
+static int recut_complete(vg_ctx* ctx, const MP& mp, int nlev, int* hrc, int* n_factors) {
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
-  *n_factors = 0;
-  // the window view (poses from the device state, ring, per-ord counts)
+  DevMap& m = ctx->map;
   WinD* dwin = (WinD*)ctx->ba.xs;
-  int* dn = (int*)((char*)ctx->ba.xs + sizeof(WinD));
-  int* dslot = dn + 32;
-  VG_TRY(state_make_win(ctx, wa, dwin, dn, dslot));
-  int total = 0;
-  for (int i = 0; i < wa.win_count; i++) total += wa.nper[i];
-  k_recut_begin<<<1, 128, 0, s>>>(m, w.rc, thread_num);
-  if (m.shard_world > 1) {
-    if (!replay) {  // the global slide count (a replay re-uses it: the insert replay does not change it)
-      VG_TRY(shard_allreduce(ctx, m.counters + kCntGSlide, ctx->shard.d_buf + 512, 1, 1));
-    }
-    k_copy_int<<<1, 64, 0, s>>>((const int*)(ctx->shard.d_buf + 512), m.counters + kCntGSlide);
-  }
-  const int nlev = mp.max_layer + 1;  // children sit one layer down; leaves at max_layer do not subdivide
-  auto list_of = [&](int L) { return (L % 2 == 1) ? w.list0 : w.list1; };  // worklist of level L >= 1
-  const int gv = 256, gw = grid_for(total > 0 ? total : 1);
-  const int ev_cap = (ctx->dbg_apply_cap >= 0 && ctx->dbg_apply_cap < kApplyEv) ? ctx->dbg_apply_cap : kApplyEv;
-  auto enqueue_level = [&](int L) {
-    k_rc_visit<<<gv, kBlock, 0, s>>>(L, thread_num, L > 0 ? list_of(L) : nullptr, mp, m, list_of(L + 1), w.list2,
-                                     w.cand, w.rc);
-    if (total > 0)
-      k_rc_win<<<gw, kBlock, 0, s>>>(L, total, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc, w.cap, w.rc);
-  };
-  for (int L = 0; L < nlev; L++) {
-    enqueue_level(L);
-    k_rc_apply<<<1, kApplyThreads, 0, s>>>(L, ev_cap, mp, dwin, m, list_of(L + 1), w.list2, w.k0, w.evsrc, w.k1,
-                                           (int*)w.ac_off, w.rc);
-    k_rc_push<<<64, 64 * kRcPushWaves, 0, s>>>(L, w.k1, (const int*)w.ac_off, mp, dwin, m, w.rc);
-  }
-  VG_HIP(hipGetLastError());
-  int* hrc = ctx->h_pinned + 128;
-  VG_TRY(read_rc(ctx, hrc));
+  auto list_of = [&](int L) { return (L % 2 == 1) ? w.list0 : w.list1; };
   if (hrc[kRcAbort] == kInsAbort) return kNeedInsertReplay;
   if (hrc[kRcAbort]) {  // replay from the level that overflowed on the host-sized path
     const int L0 = hrc[kRcAbort] - 1;
@@ -1531,13 +1570,21 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* 
 #endif
     VG_HIP(hipMemsetAsync(w.rc + kRcAbort, 0, sizeof(int), s));
     VG_TRY(recut_slow_apply(ctx, L0, mp, dwin, list_of(L0 + 1), hrc));
+    int* dn = (int*)((char*)ctx->ba.xs + sizeof(WinD));
+    int* dslot = dn + 32;
+    const int total = ctx->rc_total;
     for (int L = L0 + 1; L < nlev; L++) {
-      enqueue_level(L);
+      k_rc_visit<<<256, kBlock, 0, s>>>(L, ctx->rc_thread_num, list_of(L), mp, m, list_of(L + 1), w.list2, w.cand,
+                                        w.rc, nullptr);
+      if (total > 0)
+        k_rc_win<<<grid_for(total), kBlock, 0, s>>>(L, total, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc, w.cap,
+                                                     w.rc);
       VG_TRY(read_rc(ctx, hrc));
       VG_TRY(recut_slow_apply(ctx, L, mp, dwin, list_of(L + 1), hrc));
     }
-    VG_TRY(read_counters(ctx));
   }
+  VG_HIP(hipMemsetAsync(w.rc + kRcStatus, 0, sizeof(int), s));  // the LM rerun reads it
+  VG_TRY(read_counters(ctx));
   const int nf = ctx->h_pinned[kCntFactors];
   if (nf > ctx->ba.cap_f) {
     ctx->err = "factor capacity exceeded";
@@ -1552,6 +1599,70 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* 
   }
   *n_factors = nf;
   return VG_OK;
+}
+
+// multi_recut (local_mapping.cpp:144-201) then tras_opt. Synchronous
+// (pub_seq == 0): returns the factor count, or kNeedInsertReplay when the
+// preceding insert must be replayed first (nothing of the recut ran).
+// Asynchronous (pub_seq > 0): the factor extraction is sized on the device and
+// nothing waits; *n_factors = -1 and the status arrives with Pub::seq_rc ==
+// pub_seq (map_recut_resume completes a recut that needs the host).
+int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay,
+              int pub_seq) {
+  DevMap& m = ctx->map;
+  Work& w = ctx->wk;
+  hipStream_t s = ctx->stream;
+  *n_factors = 0;
+  // the window view (poses from the device state, ring, per-ord counts)
+  WinD* dwin = (WinD*)ctx->ba.xs;
+  int* dn = (int*)((char*)ctx->ba.xs + sizeof(WinD));
+  int* dslot = dn + 32;
+  VG_TRY(state_make_win(ctx, wa, dwin, dn, dslot));
+  int total = 0;
+  for (int i = 0; i < wa.win_count; i++) total += wa.nper[i];
+  ctx->rc_total = total;
+  ctx->rc_thread_num = thread_num;
+  k_recut_begin<<<1, 128, 0, s>>>(m, w.rc, thread_num);
+  if (m.shard_world > 1) {
+    if (!replay) {  // the global slide count (a replay re-uses it: the insert replay does not change it)
+      VG_TRY(shard_allreduce(ctx, m.counters + kCntGSlide, ctx->shard.d_buf + 512, 1, 1));
+    }
+    k_copy_int<<<1, 64, 0, s>>>((const int*)(ctx->shard.d_buf + 512), m.counters + kCntGSlide);
+  }
+  const int nlev = mp.max_layer + 1;  // children sit one layer down; leaves at max_layer do not subdivide
+  auto list_of = [&](int L) { return (L % 2 == 1) ? w.list0 : w.list1; };  // worklist of level L >= 1
+  const int gv = 256, gw = grid_for(total > 0 ? total : 1);
+  const int ev_cap = (ctx->dbg_apply_cap >= 0 && ctx->dbg_apply_cap < kApplyEv) ? ctx->dbg_apply_cap : kApplyEv;
+  for (int L = 0; L < nlev; L++) {
+    k_rc_visit<<<gv, kBlock, 0, s>>>(L, thread_num, L > 0 ? list_of(L) : nullptr, mp, m, list_of(L + 1), w.list2,
+                                     w.cand, w.rc, pub_seq > 0 ? w.cand_bits : nullptr);
+    if (total > 0)
+      k_rc_win<<<gw, kBlock, 0, s>>>(L, total, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc, w.cap, w.rc);
+    k_rc_apply<<<1, kApplyThreads, 0, s>>>(L, ev_cap, mp, dwin, m, list_of(L + 1), w.list2, w.k0, w.evsrc, w.k1,
+                                           (int*)w.ac_off, w.rc);
+    k_rc_push<<<64, 64 * kRcPushWaves, 0, s>>>(L, w.k1, (const int*)w.ac_off, mp, dwin, m, w.rc);
+  }
+  VG_HIP(hipGetLastError());
+  if (pub_seq > 0) {
+    const int max_fac = (ctx->dbg_fac_max >= 0 && ctx->dbg_fac_max < kFacMax) ? ctx->dbg_fac_max : kFacMax;
+    k_fac_sort<<<1, 1024, 0, s>>>(m, w.rc, w.cand_bits, ctx->ba.fac_node, ctx->ba.cap_f, ctx->d_pub, pub_seq,
+                                  max_fac);
+    k_factor_finish_dev<<<64, 256, 0, s>>>(w.rc, m, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr);
+    VG_HIP(hipGetLastError());
+    *n_factors = -1;
+    return VG_OK;
+  }
+  int* hrc = ctx->h_pinned + 128;
+  VG_TRY(read_rc(ctx, hrc));
+  return recut_complete(ctx, mp, nlev, hrc, n_factors);
+}
+
+// complete an asynchronous recut whose published status was nonzero (the LM
+// skipped): same outcomes as the synchronous call
+int map_recut_resume(vg_ctx* ctx, const MP& mp, int* n_factors) {
+  int* hrc = ctx->h_pinned + 128;
+  VG_TRY(read_rc(ctx, hrc));
+  return recut_complete(ctx, mp, mp.max_layer + 1, hrc, n_factors);
 }
 
 // ------------------------------------------------------------------ margi (A10)
@@ -1903,6 +2014,7 @@ __global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m
   __syncthreads();
   if (t < (wc - 1) * kXS) st->xs[t] = v;
   if (t < (nimu - 1) * 12) st->bias[t] = b;
+  if (t == 0) st->imu_head = (st->imu_head + 1) % kMaxWin;  // imu_pre_buf.pop_front (the record ring)
   if (seq2 < 0) seq2 = st->seq2;  // set by k_make_win (replayed graph)
   if (seq2 > 0) {
     __syncthreads();

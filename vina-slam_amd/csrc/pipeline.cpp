@@ -168,6 +168,7 @@ struct HostPipe {
   int ins_slot = -1, ins_n = 0;
   bool published = false;
   bool prefix = false;     // map_margi_prefix enqueued for this scan
+  int rc_seq = 0;          // > 0: this scan's recut ran asynchronously (status with Pub::seq_rc == rc_seq)
   std::deque<Pend> pend;   // enqueued scans awaiting absorption (oldest first)
   int sticky = VG_OK;      // deferred device error
 };
@@ -602,7 +603,7 @@ int stage_window_push(vg_ctx* ctx, const double* imu, int m) {
     P->imu_pre.back().record(P->imu_pre.back().rec.data());  // off the BA's critical path
     new_imu = P->win_count - 2;
   }
-  return state_push(ctx, P->win_count - 1, new_imu);
+  return state_push(ctx, P->win_count - 1, new_imu, new_imu >= 0 ? P->imu_pre.back().rec.data() : nullptr);
 }
 
 // pvec_update + cut_voxel_multi of the downsampled scan (local_mapping.cpp:425-448)
@@ -644,6 +645,15 @@ int stage_recut(vg_ctx* ctx, int* nf_out) {
   const WinArg wa = make_winarg(P, 0);
   int nf = 0;
   prof_begin(ctx, kProfRecut);
+  P->rc_seq = 0;
+  if (!nf_out && P->win_count >= c.win_size && c.if_BA == 1 && ctx->shard.world == 1) {
+    // the LM follows: its kernels read the factor count on the device, and the
+    // host learns the recut's outcome only once the LM is enqueued (stage_ba)
+    P->rc_seq = ++ctx->pub_seq;
+    VG_TRY(map_recut(ctx, P->mpd, wa, c.thread_num, &nf, false, P->rc_seq));
+    prof_end(ctx, kProfRecut);
+    return VG_OK;
+  }
   int r = map_recut(ctx, P->mpd, wa, c.thread_num, &nf);
   if (r == kNeedInsertReplay) {  // per shard; the replayed recut has no collective
     VG_TRY(map_insert_replay(ctx, P->mpd, P->ins_slot, P->ins_n, c.thread_num));
@@ -667,18 +677,42 @@ int stage_ba(vg_ctx* ctx, int* iters_out) {
     ctx->err = "vg_ba: window not full";
     return VG_E_STATE;
   }
-  std::vector<double> rec((size_t)(W - 1) * kBaImuRec);
-  for (int j = 0; j < W - 1; j++) memcpy(&rec[(size_t)j * kBaImuRec], P->imu_pre[j].rec.data(), kBaImuRec * 8);
   int iters = 0;
   prof_begin(ctx, kProfBA);
   // margi's BA-independent part goes onto the second stream once the first LM
-  // iterations are enqueued, so it runs under them (map_margi_prefix)
+  // iterations are enqueued, so it runs under them (map_margi_prefix). After
+  // an asynchronous recut, the host first reads its published outcome: a
+  // status other than 0 means the recut needs the host-sized path, and the LM
+  // kernels skip (k_ba_init read the same status).
+  int rc_status = 0;
   auto prefix = [&]() -> int {
+    if (P->rc_seq > 0) {
+      VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_rc, P->rc_seq, "k_fac_sort"));
+      rc_status = __atomic_load_n(&ctx->h_pub->rc_status, __ATOMIC_ACQUIRE);
+      if (rc_status) return VG_OK;
+      P->n_factors = __atomic_load_n(&ctx->h_pub->rc_nf, __ATOMIC_ACQUIRE);
+      P->cur.st.n_factors = P->n_factors;
+    }
     VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], ctx->cfg.thread_num, P->jour));
     P->prefix = true;
     return VG_OK;
   };
-  VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), rec.data(), &iters, prefix));
+  VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), &iters, prefix));
+  if (rc_status) {  // complete the recut on the host (stream order), then the LM again
+    P->rc_seq = 0;
+    int nf = 0;
+    int r = map_recut_resume(ctx, P->mpd, &nf);
+    if (r == kNeedInsertReplay) {
+      VG_TRY(map_insert_replay(ctx, P->mpd, P->ins_slot, P->ins_n, ctx->cfg.thread_num));
+      const WinArg wa = make_winarg(P, 0);
+      r = map_recut(ctx, P->mpd, wa, ctx->cfg.thread_num, &nf, true);
+    }
+    VG_TRY(r);
+    P->n_factors = nf;
+    P->cur.st.n_factors = nf;
+    VG_TRY(ba_run(ctx, nf, P->mp.data(), &iters, prefix));
+  }
+  P->rc_seq = 0;
   prof_end(ctx, kProfBA);
   P->cur.st.ba_iters = iters;
   if (iters_out) *iters_out = iters;

@@ -70,10 +70,19 @@ __global__ void k_set_scan(DState* __restrict__ st, const float* x, const float*
 
 // x_buf.push_back(x_curr) at ord; a new IMU_PRE (when win_count > 1) starts
 // with zero bias deltas (imu_preintegration.cpp:10-29)
-__global__ void k_push_state(DState* __restrict__ st, int ord, int new_imu) {
+// the IMU_PRE record rides in the kernel arguments (2.3 KB): no copy-engine
+// transfer on the stream
+struct ImuRecArg {
+  double r[kBaImuRec];
+};
+__global__ void k_push_state(DState* __restrict__ st, int ord, int new_imu, ImuRecArg rec) {
   const int t = threadIdx.x;
   if (t < kXS) st->xs[ord * kXS + t] = st->xc[t];
-  if (new_imu >= 0 && t < 12) st->bias[new_imu * 12 + t] = 0.0;
+  if (new_imu >= 0) {
+    if (t < 12) st->bias[new_imu * 12 + t] = 0.0;
+    double* d = &st->imurec[(size_t)((st->imu_head + new_imu) % kMaxWin) * kBaImuRec];
+    for (int e = t; e < kBaImuRec; e += blockDim.x) d[e] = rec.r[e];
+  }
 }
 
 // window view for the map kernels: poses by ord, ring, per-ord counts / slots
@@ -124,6 +133,7 @@ __global__ void k_slide_state(DState* __restrict__ st, int win_count, int nimu) 
     const int e = t + k * blockDim.x;
     if (e < (nimu - 1) * 12) st->bias[e] = b[k];
   }
+  if (t == 0) st->imu_head = (st->imu_head + 1) % kMaxWin;
 }
 
 // P1: x_curr, the post-IEKF pose, window states, IEKF / BA summary
@@ -246,8 +256,11 @@ int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, 
   return VG_OK;
 }
 
-int state_push(vg_ctx* ctx, int ord, int new_imu) {
-  k_push_state<<<1, 64, 0, ctx->stream>>>(ctx->st, ord, new_imu);
+int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec) {
+  ImuRecArg rec;
+  if (new_imu >= 0) memcpy(rec.r, imurec, sizeof(rec.r));
+  else memset(rec.r, 0, sizeof(rec.r));
+  k_push_state<<<1, 64, 0, ctx->stream>>>(ctx->st, ord, new_imu, rec);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }

@@ -142,6 +142,7 @@ struct Work {
   double* partials = nullptr;  // reduction partials
   int* iekf_cache = nullptr;   // per raw point cached leaf
   int* rc = nullptr;           // device-side level counts (recut / margi, map.hip kRc*)
+  uint32_t* cand_bits = nullptr;  // factor candidates of an asynchronous recut, one bit per node id
   int* plan = nullptr;         // per-leaf point_fix copy plan (margi)
   int nparts = 0;
 };
@@ -167,6 +168,7 @@ struct BaBufs {
 constexpr int kXS = 24;             // per-frame state: R 9, p 3, v 3, bg 3, ba 3, g 3
 constexpr int kXC = kXS + 225;      // x_curr: frame state + cov 15x15 (row-major)
 constexpr int kMaxWin = 32;
+constexpr int kBaImuRec = 64 + 225;  // IMU_PRE record (doubles): deltas, bias Jacobians, dtime, cov_inv
 struct DState {
   double xc[256];                   // x_curr (IMUST, types.hpp:43-113)
   double xp[256];                   // x_prop (odometry.cpp:67)
@@ -180,6 +182,11 @@ struct DState {
   // launches are the same every scan and replay as one hipGraph)
   const float *sx, *sy, *sz;
   int sn, seq2;
+  // IMU_PRE records of the window factors (preintegrated deltas, bias
+  // Jacobians, cov_inv; constant once pushed): a ring, factor k at slot
+  // (imu_head + k) % kMaxWin, so the slide is one index step
+  int imu_head, pad_h[3];
+  double imurec[kMaxWin * kBaImuRec];
 };
 // Spatial-tile sharding of one sequence over `world` contexts (one per GPU):
 // every context keeps the root voxels of the tiles it owns (tile_owner) and
@@ -201,6 +208,7 @@ struct Shard {
 struct Pub {
   int seq_ds, n_ds, ds_err, pad0;          // downsample (after k_ds_*)
   int seq_ba, ba_done, ba_iters, pad1;     // LM iteration flags (k_ba_control)
+  int seq_rc, rc_status, rc_nf, pad5;      // asynchronous recut status (k_fac_sort)
   int seq1, iekf_iters, degenerate, matches[4], ba_iters1, pad2[4];  // P1: state after IEKF/BA
   int seq2, pad3[3];
   int counters[kCntN];                      // P2: map counters at the end of the scan
@@ -260,6 +268,9 @@ struct vg_ctx {
   void* host = nullptr;     // host-side pipeline state (pipeline.cpp)
   // stage timing with HIP events on the context stream (vg_profile)
   bool prof_on = false;      // k_iekf launch events (vg_profile bit 0)
+  int prof_every = 0;        // sample k_ba_solve events on every n-th BA run (vg_profile bits 8-15)
+  long prof_runs = 0;
+  int rc_total = 0, rc_thread_num = 0;  // the last recut's window point total / thread_num (its resume)
   bool prof_stages = false;  // per-stage events (vg_profile bit 1)
   hipEvent_t prof_ev[8][2] = {};
   hipEvent_t sync_ev = nullptr;  // host-spin synchronisation (vg::stream_wait)
@@ -267,6 +278,8 @@ struct vg_ctx {
   int iekf_ring_n = 0, iekf_ring_base = 0;
   hipEvent_t solve_ev[10][2] = {};  // k_ba_solve launches of the current BA run (vg_profile)
   int dbg_apply_cap = -1;        // test knob (vgx_debug): recut apply event capacity
+  int dbg_ins_cap = -1;   // vgx_debug 3: k_ins_alloc capacity override (forces the insert replay)
+  int dbg_fac_max = -1;   // vgx_debug 4: device factor-sort limit override (forces the host factor path)
   bool prof_pending[16] = {};
   double prof_ms[16] = {};  // [0, 8): device time (events); [8, 16): host time of the stage calls
   int prof_n[16] = {};
@@ -381,7 +394,11 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
 constexpr int kNeedInsertReplay = 1;  // map_recut: the insert overflowed k_ins_alloc, replay it first
 int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num);
 int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num);
-int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay = false);
+int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay = false,
+              int pub_seq = 0);
+int map_recut_resume(vg_ctx* ctx, const MP& mp, int* n_factors);
+int map_set_attrs(vg_ctx* ctx);
+const int* map_rc_status(vg_ctx* ctx);  // the asynchronous recut's status word (k_fac_sort)
 // multi_margi + the device-state slide; publishes the state (pub_seq, before
 // the margi kernels) and the end-of-scan counters (pub_seq2)
 int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, double jour);
@@ -390,7 +407,7 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
 int state_alloc(vg_ctx* ctx);
 int state_scan_begin(vg_ctx* ctx, const double* xc249);
 int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n);
-int state_push(vg_ctx* ctx, int ord, int new_imu);
+int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec);  // imurec: kBaImuRec doubles (new_imu >= 0)
 int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot);
 int state_slide(vg_ctx* ctx, int win_count, int nimu);
 int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq);
@@ -400,12 +417,11 @@ int state_deskew(vg_ctx* ctx, const double* par, int npose, const float* x, cons
                  const float* in, const float* t, int n);
 // ba.hip
 constexpr int kBaX = 24;        // per-frame state: R 9, p 3, v 3, bg 3, ba 3, g 3
-constexpr int kBaImuRec = 64 + 225;
 int ba_alloc(vg_ctx* ctx);
-// LM on the device state (window states and IMU bias records in DState);
-// imurec: (W-1) x kBaImuRec host records. Returns once the LM has converged on
-// the device (the flags are read without draining the stream).
-int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, const double* imurec, int* iters,
+// LM on the device state (window states, IMU_PRE records and bias records in
+// DState; the factor count in the map counters). Returns once the LM has
+// converged on the device (the flags are read without draining the stream).
+int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
            const std::function<int()>& before_first_wait = nullptr);
 const int* ba_iters_dev(vg_ctx* ctx);
 // pipeline.cpp

@@ -412,6 +412,8 @@ int vg_profile(vg_ctx* ctx, int on) {
   if (!ctx) return VG_E_ARG;
   ctx->prof_on = (on & 1) != 0;
   ctx->prof_stages = (on & 2) != 0;
+  ctx->prof_every = (on >> 8) & 0xff;  // k_ba_solve events on every prof_every-th BA run (0/1: every run)
+  ctx->prof_runs = 0;
   ctx->iekf_ring_n = 0;
   for (int i = 0; i < vg::kProfAll; i++) {
     ctx->prof_ms[i] = 0;
@@ -440,6 +442,14 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
   }
   if (key == 1) {
     ctx->dbg_apply_cap = value;
+    return VG_OK;
+  }
+  if (key == 3) {
+    ctx->dbg_ins_cap = value;
+    return VG_OK;
+  }
+  if (key == 4) {
+    ctx->dbg_fac_max = value;
     return VG_OK;
   }
   return VG_E_ARG;

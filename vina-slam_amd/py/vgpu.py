@@ -265,9 +265,11 @@ class Context:
                       "host_propagate", "host_downsample", "host_iekf", "host_push", "host_insert", "host_recut",
                       "host_ba", "host_margi"]
 
-    def profile(self, on=True, stages=False):
-        """on: k_iekf launch events; stages: per-stage events as well."""
-        self._chk(lib().vg_profile(self.h, (1 if on else 0) | (2 if stages else 0)), "vg_profile")
+    def profile(self, on=True, stages=False, every=1):
+        """on: k_iekf / k_ba_solve launch events (the solve's on every `every`-th
+        BA run); stages: per-stage events as well."""
+        flags = (1 if on else 0) | (2 if stages else 0) | ((max(1, min(255, every)) & 0xff) << 8)
+        self._chk(lib().vg_profile(self.h, flags), "vg_profile")
 
     def profile_read(self):
         out = {}
