@@ -38,7 +38,7 @@ constexpr int kImuRec = kBaImuRec;  // preintegration record + cov_inv
 
 struct BaState {             // device-resident LM state
   double u, v, res1, res2, q1;
-  int calc_hess, done, iters, pad;
+  int calc_hess, done, iters, seq;  // seq: the next LM publication number (k_ba_control)
 };
 
 typedef double v4d __attribute__((ext_vector_type(4)));
@@ -856,7 +856,7 @@ __global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, do
                              const double* __restrict__ imuout, const double* __restrict__ imures,
                              const double* __restrict__ rpart, double* __restrict__ xs,
                              const double* __restrict__ xt, double* __restrict__ bias, BaState* __restrict__ st,
-                             Pub* __restrict__ pub, int seq) {
+                             Pub* __restrict__ pub) {
   __shared__ int accept;
   if (threadIdx.x == 0) {
     accept = -1;
@@ -905,6 +905,8 @@ __global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, do
     }
   }
   if (threadIdx.x == 0) {  // LM flags -> host (read without draining the stream)
+    const int seq = st->seq;  // one publication per launch, numbered on the device (graph replays)
+    st->seq = seq + 1;
     __hip_atomic_store(&pub->ba_done, st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&pub->ba_iters, st->iters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __threadfence_system();
@@ -918,7 +920,7 @@ struct MpRing {
 // LM state (optimizers.cpp:436-441), the reduced-Hessian accumulator, the ring
 __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict__ hl, double* __restrict__ hl_part,
                                                  int nout, MpRing ring, int* __restrict__ mpring, int W,
-                                                 const int* __restrict__ rc_status) {
+                                                 const int* __restrict__ rc_status, int seq0) {
   for (int t = threadIdx.x; t < nout; t += blockDim.x) {
     hl[t] = 0.0;
     hl_part[t] = 0.0;
@@ -931,6 +933,7 @@ __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict
     st->calc_hess = 1;
     st->done = (rc_status && *rc_status) ? 1 : 0;  // an asynchronous recut that needs the host: skip
     st->iters = 0;
+    st->seq = seq0;
   }
 }
 
@@ -1065,7 +1068,9 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
   const bool sharded = ctx->shard.world > 1;
   double* hl_part = ctx->ba.hout_part;  // this shard's LiDAR Hessian (sharded mode)
   double* rsum = ctx->shard.d_buf + 256;  // [0]: this shard's residual, [1]: all-reduced
-  k_ba_init<<<1, 256, 0, s>>>(d.st, d.hl, hl_part, nout, ring, d.mpring, W, map_rc_status(ctx));
+  const int seq0 = ctx->pub_seq + 1;
+  ctx->pub_seq += 10;
+  k_ba_init<<<1, 256, 0, s>>>(d.st, d.hl, hl_part, nout, ring, d.mpring, W, map_rc_status(ctx), seq0);
   // factor count on the device (the recut's kCntFactors): fixed grids, so an
   // asynchronous recut needs no host round trip before the LM
   (void)nf;
@@ -1075,15 +1080,16 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
   const size_t hess_lds = hess_lds_bytes(W);
   const size_t solve_lds = solve_lds_bytes(W);
   const int NBt = (15 * W + kTile - 1) / kTile, ntile = NBt * (NBt + 1) / 2;
-  const int seq0 = ctx->pub_seq + 1;
-  ctx->pub_seq += 10;
   int xerr = VG_OK;  // exchange errors (sharded mode)
   // k_ba_solve launch events (vg_profile): on every prof_every-th run only, so
   // that timing a long run costs the stream little (each record is a gap)
   const bool solve_ev = ctx->prof_on && (ctx->prof_every <= 1 || ctx->prof_runs++ % ctx->prof_every == 0);
   // one LM iteration (optimizers.cpp:449-516); kernels early-exit on the
-  // device-side flags once converged
-  auto iteration = [&](int k) {
+  // device-side flags once converged. Every argument is fixed per context (the
+  // factor count, the flags and the publication number live on the device),
+  // so an unsharded run replays one captured graph per iteration; the sampled
+  // solve-timing runs launch directly (events around k_ba_solve).
+  auto enqueue = [&](int k) {
     k_ba_hess<<<G + nimu, kHessThreads, hess_lds, s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
                                                       ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, nimu, d.imurec, &ctx->st->imu_head,
                                                       d.bias, d.imuout);
@@ -1107,7 +1113,25 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
     }
     k_ba_control<<<1, 256, 0, s>>>(W, nimu, sharded ? 1 : nrb, ctx->cfg.imu_coef, d.hl, nl + L,
                                    d.imuout, d.imures, sharded ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st,
-                                   ctx->d_pub, seq0 + k);
+                                   ctx->d_pub);
+  };
+  const bool graph = ctx->use_graphs && !sharded && !solve_ev;
+  if (graph && !ctx->g_ba) {
+    VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    enqueue(0);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(s, &g);
+    VG_HIP(e);
+    VG_HIP(hipGraphInstantiate(&ctx->g_ba, g, nullptr, nullptr, 0));
+    VG_HIP(hipGraphDestroy(g));
+  }
+  auto iteration = [&](int k) {
+    if (!graph) return enqueue(k);
+    const hipError_t e = hipGraphLaunch(ctx->g_ba, s);
+    if (e != hipSuccess && xerr == VG_OK) {
+      ctx->err = std::string("hipGraphLaunch (LM iteration): ") + hipGetErrorString(e);
+      xerr = VG_E_HIP;
+    }
   };
   // One iteration ahead: iteration k+1 is enqueued before the host waits for
   // iteration k's flags, so the stream never drains; a converged LM leaves at

@@ -243,6 +243,7 @@ struct vg_ctx {
   // the IEKF's 8 launches captured once and replayed (map.hip iekf_run)
   hipGraphExec_t g_iekf[3] = {nullptr, nullptr, nullptr};
   hipGraphExec_t g_margi = nullptr;  // margi after the window view (map.hip map_margi)
+  hipGraphExec_t g_ba = nullptr;     // one LM iteration (ba.hip ba_run)
   bool use_graphs = true;  // margi prefix on the second stream
   std::string err;
   vg::Arena arena;

@@ -150,6 +150,7 @@ int vg_destroy(vg_ctx* ctx) {
   for (auto& g : ctx->g_iekf)
     if (g) (void)hipGraphExecDestroy(g);
   if (ctx->g_margi) (void)hipGraphExecDestroy(ctx->g_margi);
+  if (ctx->g_ba) (void)hipGraphExecDestroy(ctx->g_ba);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream_ds) (void)hipStreamSynchronize(ctx->stream_ds);
   if (ctx->stream_ds) (void)hipStreamDestroy(ctx->stream_ds);
