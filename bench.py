@@ -129,11 +129,12 @@ def main():
     # roofline of the dominant kernel by device time, k_ba_solve (the LM
     # step's 15W x 15W LDL^T solve, one workgroup, fp64 MFMA trailing
     # updates): algorithmic flops per launch = n^3/3 (LDL^T) + 2 n^2 (the two
-    # triangular solves), n = 15 * win_size; peak = MI355X fp64 matrix
+    # triangular solves), n = 15 * win_size - 15 (the gauge frame's 15
+    # unknowns are decoupled and not factored); peak = MI355X fp64 matrix
     # 78.6 TFLOP/s (AMD spec). Launch time: HIP events around each executed
     # k_ba_solve on the context stream over the timed region.
     W = p["LocalBA"]["win_size"]
-    n_sys = 15 * W
+    n_sys = 15 * W - 15
     flops = n_sys ** 3 / 3.0 + 2.0 * n_sys ** 2
     sol = prof["ba_solve"]
     s_launch = sol["launches"]

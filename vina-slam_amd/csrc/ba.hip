@@ -497,6 +497,10 @@ __device__ __forceinline__ double asm_grad(int t, int nimu, double imu_coef, con
 // tile of P A P^T to the tile image; on Hessian iterations it also stores
 // the assembled entries it visits (each lower entry exactly once) for the
 // damping-only retries. Block 0 writes the permuted right-hand side.
+// The gauge frame's 15 variables (optimizers.cpp:460-463: unit rows and
+// columns, zero gradient) are decoupled from the rest, so wherever Eigen's
+// pivot order puts them their elimination changes nothing and their solution
+// is 0: they are left out of the factored system (n - 15 unknowns).
 __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coef, const double* __restrict__ hl,
                                                  const double* __restrict__ imuout, double* __restrict__ Hcalc,
                                                  double* __restrict__ Jcalc, double* __restrict__ timg,
@@ -507,17 +511,17 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
   constexpr int kN = kMaxNB * kTile;
   __shared__ double Dv[kN], Jg[kN];
   __shared__ int ip[kN];
-  const int n = 15 * W, L = 6 * W, NB = (n + kTile - 1) / kTile, N = NB * kTile;
+  const int n = 15 * W, L = 6 * W, m = n - 15, NB = (m + kTile - 1) / kTile, N = NB * kTile;
   const int tid = threadIdx.x, q = blockIdx.x;
   const bool calc = st->calc_hess != 0;
   const double u = st->u;
   for (int t = tid; t < n; t += blockDim.x)
     Dv[t] = t < 15 ? 1.0 : (calc ? asm_entry(t, t, nimu, imu_coef, hl, imuout, L) : Hcalc[lo(t, t)]);
   __syncthreads();
-  for (int i = tid; i < n; i += blockDim.x) {  // rank of |D + u D| descending, index ascending on ties
+  for (int i = 15 + tid; i < n; i += blockDim.x) {  // rank of |D + u D| descending, index ascending on ties
     const unsigned long long ki = (unsigned long long)__double_as_longlong(fabs(Dv[i] + u * Dv[i]));
     int c = 0;
-    for (int j = 0; j < n; j++) {
+    for (int j = 15; j < n; j++) {
       const unsigned long long kj = (unsigned long long)__double_as_longlong(fabs(Dv[j] + u * Dv[j]));
       c += (kj > ki) || (kj == ki && j < i);
     }
@@ -530,15 +534,13 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
   for (int e = tid; e < 256; e += blockDim.x) {
     const int r = e >> 4, c = e & 15, R = TI * 16 + r, C = TJ * 16 + c;
     double v;
-    if (R >= n || C >= n) {
+    if (R >= m || C >= m) {
       v = (R == C) ? 1.0 : 0.0;
     } else {
       const int pr = ip[R], pc = ip[C], a = pr > pc ? pr : pc, bb = pr > pc ? pc : pr;
       const double raw = calc ? asm_entry(a, bb, nimu, imu_coef, hl, imuout, L) : Hcalc[lo(a, bb)];
       if (calc && R >= C) Hcalc[lo(a, bb)] = raw;
-      if (pr == pc) v = Dv[pr] + u * Dv[pr];
-      else if (pr < 15 || pc < 15) v = 0.0;  // gauge frame 0 (optimizers.cpp:460-463)
-      else v = raw;
+      v = (pr == pc) ? Dv[pr] + u * Dv[pr] : raw;
     }
     timg[(size_t)q * 256 + tel(r, c)] = v;
   }
@@ -548,13 +550,11 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
       if (calc) Jcalc[t] = raw;
       Jg[t] = t < 15 ? 0.0 : raw;
       dvec[t] = Dv[t];
-      ipg[t] = ip[t];
+      if (t < m) ipg[t] = ip[t];
     }
     __syncthreads();
-    for (int t = tid; t < N; t += blockDim.x) {
-      bvec[t] = t < n ? -Jg[ip[t]] : 0.0;
-      if (t < n) jvec[t] = Jg[t];
-    }
+    for (int t = tid; t < N; t += blockDim.x) bvec[t] = t < m ? -Jg[ip[t]] : 0.0;
+    for (int t = tid; t < n; t += blockDim.x) jvec[t] = Jg[t];
   }
 }
 
@@ -582,8 +582,8 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
   __shared__ double Jv[kN], Dv[kN], xv[kN], col[kN], sM[256], dK[16], rdK[16], tb[16];
   __shared__ int ip[kN];
   __shared__ unsigned char tI[kMaxNB * (kMaxNB + 1) / 2], tJ[kMaxNB * (kMaxNB + 1) / 2];
-  const int n = 15 * W;
-  const int NB = (n + kTile - 1) / kTile, N = NB * kTile;
+  const int n = 15 * W, m = n - 15;  // the gauge frame's unknowns are not factored (k_ba_prep)
+  const int NB = (m + kTile - 1) / kTile, N = NB * kTile;
   const int ntile = NB * (NB + 1) / 2;
   const int tid = threadIdx.x, nt = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nwave = nt >> 6;
@@ -598,7 +598,7 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
   for (int t = tid; t < n; t += nt) {
     Dv[t] = dvec[t];
     Jv[t] = jvec[t];
-    ip[t] = ipg[t];
+    if (t < m) ip[t] = ipg[t];
   }
   if (tid < ntile) {
     int I = 0;
@@ -759,7 +759,10 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
   }
   __syncthreads();
   VG_PROBE_MARK(7);
-  for (int t = tid; t < n; t += nt) col[ip[t]] = xv[t];
+  for (int t = tid; t < n; t += nt) {
+    if (t < m) col[ip[t]] = xv[t];
+    else col[t - m] = 0.0;  // the gauge frame (t - m < 15)
+  }
   __syncthreads();
   // trial states (optimizers.cpp:468-475) and IMU bias trial (477-478)
   if (tid < W) {
@@ -966,7 +969,7 @@ static size_t hess_lds_bytes(int W) {
 }
 
 static size_t solve_lds_bytes(int W) {
-  const int NB = (15 * W + kTile - 1) / kTile;
+  const int NB = (15 * W - 15 + kTile - 1) / kTile;  // the gauge frame is not factored
   return (size_t)NB * (NB + 1) / 2 * 256 * sizeof(double);
 }
 
@@ -1079,7 +1082,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
   const int nrb = kResidBlocks;
   const size_t hess_lds = hess_lds_bytes(W);
   const size_t solve_lds = solve_lds_bytes(W);
-  const int NBt = (15 * W + kTile - 1) / kTile, ntile = NBt * (NBt + 1) / 2;
+  const int NBt = (15 * W - 15 + kTile - 1) / kTile, ntile = NBt * (NBt + 1) / 2;
   int xerr = VG_OK;  // exchange errors (sharded mode)
   // k_ba_solve launch events (vg_profile): on every prof_every-th run only, so
   // that timing a long run costs the stream little (each record is a gap)
