@@ -15,7 +15,7 @@ import synth  # noqa: E402
 import vgconfig  # noqa: E402
 import vgpu  # noqa: E402
 
-PHASES = {3: "load tiles", 4: "diag+Linv+z", 5: "panel mfma", 6: "b-upd+trailing", 7: "backward solve",
+PHASES = {3: "load tiles", 9: "diag(0)", 5: "panel mfma", 6: "trailing || diag(K+1)", 7: "backward solve",
           8: "trial/q1"}
 
 

@@ -579,7 +579,7 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
   if (st->done) return;
   extern __shared__ __attribute__((aligned(16))) double T[];
   constexpr int kN = kMaxNB * kTile;
-  __shared__ double Jv[kN], Dv[kN], xv[kN], col[kN], sM[256], dK[16], rdK[16], tb[16];
+  __shared__ double Jv[kN], Dv[kN], xv[kN], col[kN], sMb[2][256], dKb[2][16], tb[16];
   __shared__ int ip[kN];
   __shared__ unsigned char tI[kMaxNB * (kMaxNB + 1) / 2], tJ[kMaxNB * (kMaxNB + 1) / 2];
   const int n = 15 * W, m = n - 15;  // the gauge frame's unknowns are not factored (k_ba_prep)
@@ -609,72 +609,117 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
   __syncthreads();
   VG_PROBE_MARK(3);
 
-  for (int K = 0; K < NB; K++) {
+  // (1) diagonal tile K on wave 0 (see below); M and d go to parity buffer pb
+  auto diag = [&](int K, int pb) __attribute__((always_inline)) {
     double* Tkk = &T[tix(K, K) * 256];
-    if (wave == 0) {
-      // (1) diagonal tile, lane (r = lane/4, q = lane%4) holds a(r, q + 4s)
-      //     and X(r, q + 4s) (X -> L^-1 by the same row operations):
-      //     column j: L(r,j) = a(r,j)/d_j; a(r,m) -= L(r,j) (d_j L(m,j));
-      //     X(r,:) -= L(r,j) X(j,:). Exchanges by DPP / ds_bpermute only.
-      const int r = lane >> 2, q = lane & 3;
-      double a[4], X[4];
+    // (1) diagonal tile, lane (r = lane/4, q = lane%4) holds a(r, q + 4s)
+    //     and X(r, q + 4s) (X -> L^-1 by the same row operations):
+    //     column j: L(r,j) = a(r,j)/d_j; a(r,m) -= L(r,j) a(m,j);
+    //     X(r,:) -= L(r,j) X(j,:). The column's undivided values a(m,j)
+    //     (= d_j L(m,j)) and row X(j,:) do not wait for the reciprocal, so
+    //     their exchanges (DPP / ds_bpermute) overlap it; the reciprocal is
+    //     v_rcp_f64 plus one Newton step.
+    const int r = lane >> 2, q = lane & 3;
+    double a[4], X[4];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; s4++) {
-        a[s4] = Tkk[tel(r, q + 4 * s4)];
-        X[s4] = (q + 4 * s4 == r) ? 1.0 : 0.0;
-      }
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const int qj = j & 3, sj = j >> 2;
-        const double dj = bcast(a[sj], 4 * j + qj);
-        const double rdj = (dj != 0.0) ? 1.0 / dj : 1.0;  // Eigen leaves a zero pivot's column undivided
-        const double l = quad_bcast(a[sj] * rdj, qj);
-        if (r > j && q == qj) a[sj] = l;
-        const double t = dj * l;
-        double tv[4], xj[4];
-#pragma unroll
-        for (int s4 = 0; s4 < 4; s4++) {
-          tv[s4] = __shfl(t, 4 * (q + 4 * s4), 64);
-          xj[s4] = __shfl(X[s4], 4 * j + q, 64);
-        }
-#pragma unroll
-        for (int s4 = 0; s4 < 4; s4++) {
-          const int m = q + 4 * s4;
-          if (m > j && m <= r) a[s4] -= l * tv[s4];
-          if (r > j) X[s4] -= l * xj[s4];
-        }
-      }
-      double myd = 0.0;
-#pragma unroll
-      for (int s4 = 0; s4 < 4; s4++)
-        if (q + 4 * s4 == r) myd = a[s4];
-      myd = __shfl(myd, 4 * r + (r & 3), 64);
-      const double rd = (myd != 0.0) ? 1.0 / myd : 1.0;
-      // z_r = D^+ (X b_K)_r (Eigen: |d| > DBL_MIN divides, else 0)
-      double zp = 0.0;
-#pragma unroll
-      for (int s4 = 0; s4 < 4; s4++) zp += X[s4] * xv[16 * K + q + 4 * s4];
-      zp += __shfl_xor(zp, 1, 64);
-      zp += __shfl_xor(zp, 2, 64);
-      const double zr = (fabs(myd) > 2.2250738585072014e-308) ? zp / myd : 0.0;
-#pragma unroll
-      for (int s4 = 0; s4 < 4; s4++) {
-        const int c = q + 4 * s4;
-        if (c <= r) Tkk[tel(r, c)] = a[s4];
-        if (c < r) Tkk[tel(c, r)] = X[s4];  // Linv(r, c) in the unused upper half
-        sM[c * 16 + r] = X[s4] * rd;       // M = L^-T D^-1
-      }
-      if (q == 0) {
-        dK[r] = myd;
-        rdK[r] = rd;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (q == 0) xv[16 * K + r] = zr;
+    for (int s4 = 0; s4 < 4; s4++) {
+      a[s4] = Tkk[tel(r, q + 4 * s4)];
+      X[s4] = (q + 4 * s4 == r) ? 1.0 : 0.0;
     }
-    __syncthreads();
-    VG_PROBE_MARK(4);
+    // Only blocks s4 >= j/4 of a change (entries right of column j; rows
+    // r <= j there are strictly upper and never read) and only blocks
+    // s4 <= j/4 of X (X(j,:) is zero right of j), so each column needs no
+    // per-element predicates and 5 block updates instead of 8.
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const int qj = j & 3, sj = j >> 2;
+      const double dj = bcast(a[sj], 4 * j + qj);
+      const double acol = quad_bcast(a[sj], qj);  // a(r, j) in every lane of row r
+      double tv[4], xj[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; s4++) {
+        if (s4 >= sj) tv[s4] = __shfl(acol, 4 * (q + 4 * s4), 64);  // a(m, j), m = q + 4 s4
+        if (s4 <= sj) xj[s4] = __shfl(X[s4], 4 * j + q, 64);        // X(j, m)
+      }
+      double rdj = 1.0;  // Eigen leaves a zero pivot's column undivided
+      if (dj != 0.0) {
+        rdj = __builtin_amdgcn_rcp(dj);
+        rdj = fma(rdj, fma(-dj, rdj, 1.0), rdj);
+      }
+      const double l = acol * rdj;
+      const double lu = (dj != 0.0) ? l : 0.0;  // a zero pivot updates nothing (d_j L(m,j) = 0)
+      const double lx = (r > j) ? l : 0.0;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; s4++) {
+        if (s4 > sj) a[s4] -= lu * tv[s4];
+        if (s4 <= sj) X[s4] -= lx * xj[s4];
+      }
+      if (q > qj) a[sj] -= lu * tv[sj];
+      else if (q == qj && r > j) a[sj] = l;
+    }
+    double myd = 0.0;
+#pragma unroll
+    for (int s4 = 0; s4 < 4; s4++)
+      if (q + 4 * s4 == r) myd = a[s4];
+    myd = __shfl(myd, 4 * r + (r & 3), 64);
+    const double rd = (myd != 0.0) ? 1.0 / myd : 1.0;
+    // z_r = D^+ (X b_K)_r (Eigen: |d| > DBL_MIN divides, else 0)
+    double zp = 0.0;
+#pragma unroll
+    for (int s4 = 0; s4 < 4; s4++) zp += X[s4] * xv[16 * K + q + 4 * s4];
+    zp += __shfl_xor(zp, 1, 64);
+    zp += __shfl_xor(zp, 2, 64);
+    const double zr = (fabs(myd) > 2.2250738585072014e-308) ? zp / myd : 0.0;
+#pragma unroll
+    for (int s4 = 0; s4 < 4; s4++) {
+      const int c = q + 4 * s4;
+      if (c <= r) Tkk[tel(r, c)] = a[s4];
+      if (c < r) Tkk[tel(c, r)] = X[s4];  // Linv(r, c) in the unused upper half
+      sMb[pb][c * 16 + r] = X[s4] * rd;  // M = L^-T D^-1
+    }
+    if (q == 0) dKb[pb][r] = myd;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (q == 0) xv[16 * K + r] = zr;
+  };
+  // (3) one trailing job of panel K on one wave: tile A_IJ -= L_IK diag(d)
+  //     L_JK^T, or (brow) the bordered right-hand side b_I -= L_IK diag(d) z_K
+  //     (column 0 of an MFMA tile)
+  auto tjob = [&](int K, int I, int J, bool brow, const double* dk) __attribute__((always_inline)) {
+    const double* Aik = &T[tix(I, K) * 256];
+    const double* Ajk = &T[tix(J, K) * 256];
+    double* Tij = &T[tix(I, J) * 256];
+    const int cc = lane & 15, rq = lane >> 4;
+    v4d acc;
+#pragma unroll
+    for (int g = 0; g < 4; g++) acc[g] = brow ? (cc == 0 ? xv[16 * I + rq + 4 * g] : 0.0) : Tij[tel(rq + 4 * g, cc)];
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++) {
+      const int kk = 4 * ks + rq;
+      const double av = -(Aik[tel(cc, kk)] * dk[kk]);
+      const double bv = brow ? (cc == 0 ? xv[16 * K + kk] : 0.0) : Ajk[tel(cc, kk)];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+    if (brow) {
+      if (cc == 0)
+#pragma unroll
+        for (int g = 0; g < 4; g++) xv[16 * I + rq + 4 * g] = acc[g];
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; g++) Tij[tel(rq + 4 * g, cc)] = acc[g];
+    }
+  };
+  // Right-looking with one panel of lookahead: after panel K, wave 0 brings
+  // tile (K+1, K+1) and b_{K+1} up to date and factors tile K+1 while the
+  // other waves run the rest of panel K's trailing update, so the trailing
+  // work leaves the critical path (two barriers per panel). M and d are
+  // double-buffered by panel parity.
+  if (wave == 0) diag(0, 0);
+  __syncthreads();
+  VG_PROBE_MARK(9);
+  for (int K = 0; K < NB; K++) {
+    const int pb = K & 1;
     // (2) panel: L_IK = A_IK M (in place, one wave per tile)
     for (int I = K + 1 + wave; I < NB; I += nwave) {
       double* Tik = &T[tix(I, K) * 256];
@@ -683,7 +728,7 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
 #pragma unroll
       for (int ks = 0; ks < 4; ks++) {
         const int kk = 4 * ks + rq;
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Tik[tel(cc, kk)], sM[kk * 16 + cc], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Tik[tel(cc, kk)], sMb[pb][kk * 16 + cc], acc, 0, 0, 0);
       }
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -691,35 +736,25 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
     }
     __syncthreads();
     VG_PROBE_MARK(5);
-    // (3) trailing tiles A_IJ -= L_IK diag(d) L_JK^T and the bordered
-    //     right-hand side b_I -= L_IK diag(d) z_K (column 0 of an MFMA tile),
-    //     one wave per job
+    if (K + 1 == NB) break;
     const int Rm = NB - K - 1;
     const int ntr = Rm * (Rm + 1) / 2;
-    for (int q = wave; q < ntr + Rm; q += nwave) {
-      const bool brow = q >= ntr;
-      const int I = brow ? K + 1 + (q - ntr) : K + 1 + tI[q], J = brow ? 0 : K + 1 + tJ[q];
-      const double* Aik = &T[tix(I, K) * 256];
-      const double* Ajk = &T[tix(J, K) * 256];
-      double* Tij = &T[tix(I, J) * 256];
-      const int cc = lane & 15, rq = lane >> 4;
-      v4d acc;
-#pragma unroll
-      for (int g = 0; g < 4; g++) acc[g] = brow ? (cc == 0 ? xv[16 * I + rq + 4 * g] : 0.0) : Tij[tel(rq + 4 * g, cc)];
-#pragma unroll
-      for (int ks = 0; ks < 4; ks++) {
-        const int kk = 4 * ks + rq;
-        const double av = -(Aik[tel(cc, kk)] * dK[kk]);
-        const double bv = brow ? (cc == 0 ? xv[16 * K + kk] : 0.0) : Ajk[tel(cc, kk)];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-      }
-      if (brow) {
-        if (cc == 0)
-#pragma unroll
-          for (int g = 0; g < 4; g++) xv[16 * I + rq + 4 * g] = acc[g];
-      } else {
-#pragma unroll
-        for (int g = 0; g < 4; g++) Tij[tel(rq + 4 * g, cc)] = acc[g];
+    if (wave == 0) {
+      tjob(K, K + 1, K + 1, false, dKb[pb]);
+      tjob(K, K + 1, 0, true, dKb[pb]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      diag(K + 1, pb ^ 1);
+    } else if (wave & 3) {
+      // jobs 0 (tile (K+1, K+1)) and ntr (b_{K+1}) belong to wave 0; the
+      // waves sharing its SIMD (wave % 4 == 0) stay idle so that its
+      // latency-bound column chain has the SIMD to itself
+      const int wk = wave - (wave >> 2) - 1, nwk = nwave - (nwave >> 2);
+      for (int q = 1 + wk; q < ntr + Rm; q += nwk) {
+        if (q == ntr) continue;
+        const bool brow = q > ntr;
+        tjob(K, brow ? K + 1 + (q - ntr) : K + 1 + tI[q], brow ? 0 : K + 1 + tJ[q], brow, dKb[pb]);
       }
     }
     __syncthreads();
@@ -727,16 +762,18 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
   }
 
   // backward solve on wave 0, lane (r = lane & 15, qd = lane >> 4):
-  // x_I = Linv_II^T (z_I - sum_{J>I} L_JI^T x_J)
+  // x_I = Linv_II^T (z_I - sum_{J>I} L_JI^T x_J), right-looking: once x_I is
+  // known its contributions to every earlier tile go into per-tile register
+  // accumulators (independent chains), so a step waits on 4 products only.
   if (wave == 0) {
     const int r = lane & 15, qd = lane >> 4;
-    for (int I = NB - 1; I >= 0; I--) {
-      double sacc = 0.0;
-      for (int J = I + 1; J < NB; J++) {
-        const double* Tt = &T[tix(J, I) * 256];
+    double acc[kMaxNB];
 #pragma unroll
-        for (int c = qd; c < 16; c += 4) sacc += Tt[tel(c, r)] * xv[16 * J + c];
-      }
+    for (int J = 0; J < kMaxNB; J++) acc[J] = 0.0;
+#pragma unroll
+    for (int I = kMaxNB - 1; I >= 0; I--) {
+      if (I >= NB) continue;
+      double sacc = acc[I];
       sacc += __shfl_xor(sacc, 16, 64);
       sacc += __shfl_xor(sacc, 32, 64);
       const double z = xv[16 * I + r] - sacc;
@@ -755,6 +792,12 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int J = 0; J < I; J++) {
+        const double* Tt = &T[tix(I, J) * 256];
+#pragma unroll
+        for (int c = qd; c < 16; c += 4) acc[J] += Tt[tel(c, r)] * xv[16 * I + c];
+      }
     }
   }
   __syncthreads();
@@ -789,10 +832,12 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
     }
   }
   for (int t = tid; t < n; t += nt) dxi_out[t] = col[t];
-  if (tid == 0) {
+  if (wave == 1) {  // q1 on its own wave (the trial states run on wave 0): lane-strided sums, fixed xor tree
     double q1 = 0.0;
-    for (int r = 0; r < n; r++) q1 += col[r] * (u * Dv[r] * col[r] - Jv[r]);
-    st->q1 = 0.5 * q1;
+    for (int r = lane; r < n; r += 64) q1 += col[r] * (u * Dv[r] * col[r] - Jv[r]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) q1 += __shfl_xor(q1, off, 64);
+    if (lane == 0) st->q1 = 0.5 * q1;
   }
   VG_PROBE_MARK(8);
 #ifdef VG_PROBE
