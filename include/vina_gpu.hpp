@@ -38,6 +38,15 @@ class LioCore {
                   imu7.data(), (int)(imu7.size() / 7)),
           "vg_step");
   }
+  // one raw sweep: IMUEKF::motion_blur's deskew (imu_ekf.cpp:114-144, row f1)
+  // on the device, then the steady-state branch; time[i] = the point's offset
+  // from beg in seconds (the reference's `curvature` field), ascending
+  void process_raw(const std::vector<float>& xyz, const std::vector<float>& intensity, const std::vector<float>& time,
+                   double beg, double end, const std::vector<double>& imu7) {
+    check(vg_step_deskew(ctx_, xyz.data(), intensity.empty() ? nullptr : intensity.data(), time.data(),
+                         (int)(xyz.size() / 3), beg, end, imu7.data(), (int)(imu7.size() / 7)),
+          "vg_step_deskew");
+  }
 
   // ---- the same, call by call (reference names) ----
   void load_scan(const float* xyz, const float* intensity, int n) { check(vg_scan_load(ctx_, xyz, intensity, n), "vg_scan_load"); }
