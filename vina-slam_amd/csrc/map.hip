@@ -1985,8 +1985,32 @@ __global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m
                                                         int nimu, Pub* __restrict__ pub, int seq2) {
   __shared__ int base;
   __shared__ int sc[1024];
+  __shared__ int s_w[17];
   const int n = m.counters[kCntSlide];
-  if (g_slide(m) >= thread_num) {
+  constexpr int kPer = 16;
+  if (g_slide(m) >= thread_num && n <= kPer * (int)blockDim.x) {
+    // one pass: every lane reads a contiguous run into registers, one block
+    // scan orders the survivors (all reads precede the scan's barriers, so the
+    // in-place writes cannot overtake them)
+    const int per = (n + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int q0 = threadIdx.x * per;
+    int nodes[kPer];
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const int q = q0 + k;
+      int node = (k < per && q < n) ? m.slide[q] : -1;
+      if (node >= 0 && !m.in_slide[node]) node = -1;
+      nodes[k] = node;
+      cnt += node >= 0 ? 1 : 0;
+    }
+    int total;
+    int pos = block_excl_scan(cnt, s_w, &total);
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+      if (nodes[k] >= 0) m.slide[pos++] = nodes[k];
+    if (threadIdx.x == 0) m.counters[kCntSlide] = total;
+  } else if (g_slide(m) >= thread_num) {
     if (threadIdx.x == 0) base = 0;
     __syncthreads();
     for (int start = 0; start < n; start += blockDim.x) {
