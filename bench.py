@@ -160,6 +160,24 @@ def main():
                  "frac": round(achieved / 8000.0, 5), "traffic": None, "avg_launch_us": round(avg_s * 1e6, 3),
                  "launches": n_launch}
 
+    # whole-scan algorithmic bytes over the timed scans, a LOWER
+    # bound: the per-scan counters do not give the distinct plane records
+    # read per IEKF iteration (P_k) or the leaves an insert touches (V_ins),
+    # so those terms are left out, and the Hessian passes count once per LM run
+    W = p["LocalBA"]["win_size"]
+    b_scan = 0.0
+    for st in stats:
+        b_scan += 16.0 * st["n_raw"] + 16.0 * st["n_ds"]  # read xyz+t, write centroid+count
+        b_scan += st["iekf_iters"] * 16.0 * st["n_raw"]  # body xyz + cached leaf per IEKF iteration
+        b_scan += 12.0 * st["n_ds"]  # insert
+        b_scan += st["n_slide"] * (W * 80.0 + 80.0)  # recut
+        b_scan += (1 + st["ba_iters"]) * st["n_factors"] * (W * 80.0 + 176.0)  # BA Hessian + residual passes
+    b_scan /= max(len(stats), 1)
+    scan_gbps = b_scan / (dt / args.steps) / 1e9 if dt > 0 else 0.0
+    roof_scan = {"bound": "hbm", "achieved": round(scan_gbps, 2), "peak": 8000.0, "unit": "GB/s",
+                 "frac": round(scan_gbps / 8000.0, 6), "bytes_per_scan": int(b_scan),
+                 "note": "SURVEY 8(d) algorithmic bytes per scan / ms_per_step; lower bound (P_k, V_ins omitted)"}
+
     pmc = pmc_traffic()
     if "k_ba_solve" in pmc:
         roof["traffic"] = pmc["k_ba_solve"]["traffic_bytes"]
@@ -180,7 +198,8 @@ def main():
                        "points_per_scan": npts, "downsampled_per_scan": int(np.mean([s["n_ds"] for s in stats])),
                        "factors_per_scan": int(np.mean([s["n_factors"] for s in stats])),
                        "parallelism": ("tile-sharded x%d" if tile else "replica x%d") % world},
-            "roofline": roof, "roofline_k_iekf": roof_iekf, "host_ms_per_scan": host_ms, "cpu_baseline": cpu,
+            "roofline": roof, "roofline_k_iekf": roof_iekf, "roofline_scan": roof_scan, "host_ms_per_scan": host_ms,
+            "cpu_baseline": cpu,
         }
         print(json.dumps(line))
     ctx.close()

@@ -265,7 +265,7 @@ __device__ __forceinline__ int lower_idx(int r, int c) { return r * (r + 1) / 2 
 
 constexpr int kHessThreads = 256;
 constexpr int kHessGridMax = 256;  // k_ba_hess chunk workgroups (more chunks loop)
-constexpr int kResidBlocks = 64;   // k_ba_resid workgroups (more factors loop)
+constexpr int kResidBlocks = 512;  // k_ba_resid workgroups (more chunks loop)
 __host__ __device__ constexpr int hess_fs(int W) { return kHessThreads / W < 64 ? kHessThreads / W : 64; }  // factors per sub-chunk
 __host__ __device__ constexpr int hess_ks(int W) { return (3 * hess_fs(W) + 3) / 4 * 4; }  // GEMM K per sub-chunk
 __host__ __device__ constexpr int hess_nt(int W) { return (6 * W + 15) / 16; }           // 16-wide output tiles
@@ -845,8 +845,12 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
 #endif
 }
 
-// evaluate_only_residual (factors.cpp:128-158) at the trial poses; workgroup
-// b < nrb sums factors b*256 + t + k*nrb*256 (the device factor count *nfp)
+// evaluate_only_residual (factors.cpp:128-158) at the trial poses. A chunk of
+// 256/W factors per workgroup step: lane (f, i) moves factor f's frame-i
+// cluster to the trial pose (independent work, in parallel), then lane f merges
+// them onto pcr_fix in frame order (the reference's order) and takes the 3x3
+// eigen-decomposition. Workgroup b < nrb takes chunks b, b + nrb, ... of the
+// device factor count *nfp; its residual partial goes to rpart[b].
 __global__ void __launch_bounds__(256) k_ba_resid(const int* __restrict__ nfp, int W, const int* __restrict__ fac_node,
                                                   const Clu* __restrict__ pcr_fix, const Clu* __restrict__ pcrs,
                                                   const int* __restrict__ mpring, const double* __restrict__ xt,
@@ -860,28 +864,45 @@ __global__ void __launch_bounds__(256) k_ba_resid(const int* __restrict__ nfp, i
     if ((int)threadIdx.x < nimu) imu_residual_lane(threadIdx.x, imurec, *imu_head, bias, xt, imures);
     return;
   }
-  double acc = 0.0;
-  const int nf = *nfp;
-  for (int a = blockIdx.x * blockDim.x + threadIdx.x; a < nf; a += nrb * blockDim.x) {
-    const int node = fac_node[a];
-    Clu sig = pcr_fix[node];
-    for (int i = 0; i < W; i++) {
-      const Clu s = pcrs[(size_t)node * W + mpring[i]];
-      if (s.N != 0) {
-        Clu t = clu_transform(s, ld_m3(&xt[(size_t)i * kX]), ld_v3(&xt[(size_t)i * kX + 9]));
-        clu_add(sig, t);
-      }
-    }
-    V3 ev;
-    M3 U;
-    eig3(clu_cov(sig), ev, U);
-    double* e = &fac_eig[(size_t)a * 12];
-    for (int j = 0; j < 3; j++) e[j] = ev[j];
-    for (int j = 0; j < 9; j++) e[3 + j] = U[j];
-    fac_pcr[a] = sig;
-    acc += 1.0 * ev[0];
-  }
+  __shared__ Clu s_t[256];
   __shared__ double red[4];
+  const int FS = 256 / W;
+  const int f = threadIdx.x / W, i = threadIdx.x % W;
+  const int nf = *nfp;
+  const int nchunk = (nf + FS - 1) / FS;
+  double acc = 0.0;
+  for (int ch = blockIdx.x; ch < nchunk; ch += nrb) {
+    const int a = ch * FS + f;
+    if (f < FS && a < nf) {
+      const Clu src = pcrs[(size_t)fac_node[a] * W + mpring[i]];
+      Clu t;
+      if (src.N != 0) {
+        t = clu_transform(src, ld_m3(&xt[(size_t)i * kX]), ld_v3(&xt[(size_t)i * kX + 9]));
+      } else {
+        clu_zero(t);
+        t.N = 0;
+      }
+      s_t[threadIdx.x] = t;
+    }
+    __syncthreads();
+    const int a2 = ch * FS + (int)threadIdx.x;
+    if ((int)threadIdx.x < FS && a2 < nf) {
+      Clu sig = pcr_fix[fac_node[a2]];
+      for (int k = 0; k < W; k++) {
+        const Clu& t = s_t[threadIdx.x * W + k];
+        if (t.N != 0) clu_add(sig, t);
+      }
+      V3 ev;
+      M3 U;
+      eig3(clu_cov(sig), ev, U);
+      double* e = &fac_eig[(size_t)a2 * 12];
+      for (int j = 0; j < 3; j++) e[j] = ev[j];
+      for (int j = 0; j < 9; j++) e[3 + j] = U[j];
+      fac_pcr[a2] = sig;
+      acc += 1.0 * ev[0];
+    }
+    __syncthreads();
+  }
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
@@ -906,6 +927,18 @@ __global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, do
                              const double* __restrict__ xt, double* __restrict__ bias, BaState* __restrict__ st,
                              Pub* __restrict__ pub) {
   __shared__ int accept;
+  __shared__ double s_r[256];
+  {  // residual partials: lane-strided sums, then a fixed tree (deterministic)
+    double part = 0.0;
+    if (!st->done)
+      for (int b = threadIdx.x; b < nrb; b += blockDim.x) part += rpart[b];
+    s_r[threadIdx.x] = part;
+    __syncthreads();
+    for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) s_r[threadIdx.x] += s_r[threadIdx.x + w];
+      __syncthreads();
+    }
+  }
   if (threadIdx.x == 0) {
     accept = -1;
     if (!st->done) {
@@ -919,8 +952,7 @@ __global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, do
       double r1 = 0.0;
       for (int k = 0; k < nimu; k++) r1 += imures[k];
       r1 *= imu_coef * 0.5;
-      double r2 = 0.0;
-      for (int b = 0; b < nrb; b++) r2 += rpart[b];
+      const double r2 = s_r[0];
       const double residual2 = r1 + r2;
       st->res2 = residual2;
       const double residual1 = st->res1;
