@@ -116,6 +116,21 @@ int vg_step_deskew(vg_ctx* ctx, const float* xyz, const float* intensity, const 
 int vg_step_deskew_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, const float* d_intensity,
                        const float* d_time, int n, double pcl_beg_time, double pcl_end_time, const double* imu,
                        int m);
+/* SURVEY row A14 — VINA_SLAM::lio_state_estimation_kdtree (odometry.cpp:267-439),
+ * the initialisation-phase LIO (node.cpp:317). xyz: the scan downsampled at
+ * max(down_size, 0.5), raw LiDAR frame, n x 3 floats (var_init applies the
+ * extrinsic). state: 250 doubles (vg_get_state layout), updated in place.
+ * While the context's init map holds fewer than 100 points the scan only seeds
+ * it (*valid = -1, *iters = 0); otherwise up to 4 IEKF iterations against the
+ * exact 5 nearest map points (device hashed grid in place of the kd-tree,
+ * plane fit by column-pivoting Householder QR as colPivHouseholderQr), then the
+ * registered scan is appended and the map re-downsampled at 0.5 m.
+ * *valid: correspondences of the last iteration. vg_reset clears the map.
+ * Synchronous; completes outstanding work first. */
+int vg_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* valid, int* iters);
+/* the init map (float xyz, n x 3, key order of its last downsample): *n = its
+ * size; up to cap points copied when xyz != NULL */
+int vg_kdmap_get(vg_ctx* ctx, float* xyz, int cap, int* n);
 int vg_get_state(vg_ctx* ctx, double* state);
 int vg_get_stats(vg_ctx* ctx, vg_stats* out);
 /* Per-scan counters of every completed scan since vg_create / vg_reset, in

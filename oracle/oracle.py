@@ -66,6 +66,11 @@ def lib():
         L.orc_traj_len.argtypes = [P]
         L.orc_get_traj.argtypes = [P, dp]
         L.orc_window_states.argtypes = [P, dp]
+        L.orc_lio_kdtree.argtypes = [P, fp, ctypes.c_int, ip, ip]
+        L.orc_kdmap_size.argtypes = [P]
+        L.orc_kdmap_get.argtypes = [P, fp]
+        L.orc_qr_solve.argtypes = [dp, ctypes.c_int, dp, dp]
+        L.orc_knn.argtypes = [fp, ctypes.c_int, fp, ctypes.c_int, ip, fp]
         _lib = L
     return _lib
 
@@ -108,6 +113,25 @@ def inverse15(A):
     o = np.zeros((15, 15))
     lib().orc_inverse15(_d(A), _d(o))
     return o
+
+
+def qr_solve(A, b):
+    """Eigen ColPivHouseholderQR(A).solve(b) restated (m x 3, m <= 8)."""
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(3)
+    lib().orc_qr_solve(_d(A), A.shape[0], _d(b), _d(x))
+    return x
+
+
+def knn(pts, q, k):
+    """Exact k nearest (float squared distances, ties by index): indices, distances."""
+    pts = np.ascontiguousarray(pts, dtype=np.float32)
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    idx = np.zeros(k, dtype=np.int32)
+    sq = np.zeros(k, dtype=np.float32)
+    n = lib().orc_knn(_f(pts), pts.shape[0], _f(q), k, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _f(sq))
+    return idx[:n], sq[:n]
 
 
 def ldlt_solve(A, b):
@@ -195,3 +219,20 @@ class Pipeline:
         out = np.zeros((64, STATE_LEN))
         n = lib().orc_window_states(self.h, _d(out))
         return out[:n]
+
+    def lio_kdtree(self, xyz):
+        """lio_state_estimation_kdtree on a scan downsampled at
+        max(down_size, 0.5); returns (valid correspondences or -1 when the scan
+        only seeded the map, IEKF iterations)."""
+        xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+        v = ctypes.c_int(0)
+        it = ctypes.c_int(0)
+        lib().orc_lio_kdtree(self.h, _f(xyz), xyz.shape[0], ctypes.byref(v), ctypes.byref(it))
+        return v.value, it.value
+
+    def kdmap(self):
+        n = lib().orc_kdmap_size(self.h)
+        out = np.zeros((n, 3), dtype=np.float32)
+        if n:
+            lib().orc_kdmap_get(self.h, _f(out))
+        return out

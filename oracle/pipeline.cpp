@@ -14,6 +14,8 @@
 #include "map.hpp"
 #include "vina_oracle.h"
 
+#include "kdlio.hpp"
+
 namespace orc {
 
 struct Pipeline {
@@ -34,6 +36,118 @@ struct Pipeline {
   // counters of the last step
   orc_stats st;
   std::vector<V3> pwld;
+  std::vector<PointType> pl_tree;  // the initialisation map (odometry.cpp:269 pl_tree)
+
+  // lio_state_estimation_kdtree — odometry.cpp:267-439. Returns
+  // the valid correspondence count of the last iteration, or -1 when the map
+  // held fewer than 100 points and the scan only seeded it (275-310).
+  int lio_kdtree(PVec& pptr, int* iters_out) {
+    *iters_out = 0;
+    if (pptr.empty()) return -1;
+    if (pl_tree.size() < 100) {
+      for (pointVar pv : pptr) {
+        pv.pnt = x_curr.R * pv.pnt + x_curr.p;
+        PointType pp;
+        pp.x = (float)pv.pnt[0];
+        pp.y = (float)pv.pnt[1];
+        pp.z = (float)pv.pnt[2];
+        pl_tree.push_back(pp);
+      }
+      return -1;
+    }
+    const int num_max_iter = 4;
+    IMUST x_prop = x_curr;
+    const int psize = (int)pptr.size();
+    bool EKF_stop_flg = false, flg_EKF_converged = false;
+    M15 G, H_T_H;
+    const M15 I_STATE = M15::Identity();
+    int rematch_num = 0;
+    M15 cov_inv = inverse(x_curr.cov);
+    std::vector<double> ds(psize, -1);
+    std::vector<V3> directs(psize);
+    bool refind = true;
+    int valid = 0;
+    for (int iterCount = 0; iterCount < num_max_iter; iterCount++) {
+      (*iters_out)++;
+      M6 HTH;
+      V6 HTz;
+      valid = 0;
+      for (int i = 0; i < psize; i++) {
+        pointVar& pv = pptr[i];
+        M3 phat = hat(pv.pnt);
+        V3 wld = x_curr.R * pv.pnt + x_curr.p;
+        if (refind) {
+          int nearInd[kNMatch];
+          float sqdis[kNMatch];
+          knn_brute(pl_tree, (float)wld[0], (float)wld[1], (float)wld[2], kNMatch, nearInd, sqdis);
+          double A[kNMatch * 3], b[kNMatch];
+          for (int r = 0; r < kNMatch; r++) {
+            const PointType& pp = pl_tree[nearInd[r]];
+            A[r * 3 + 0] = pp.x;
+            A[r * 3 + 1] = pp.y;
+            A[r * 3 + 2] = pp.z;
+            b[r] = -1.0;
+          }
+          double dir[3];
+          colpiv_qr_solve(A, kNMatch, b, dir);
+          bool check_flag = false;
+          for (int r = 0; r < kNMatch; r++)
+            if (std::fabs(((dir[0] * A[r * 3] + dir[1] * A[r * 3 + 1]) + dir[2] * A[r * 3 + 2]) + 1.0) > 0.1)
+              check_flag = true;
+          if (check_flag) {
+            ds[i] = -1;
+            continue;
+          }
+          const V3 direct = v3(dir[0], dir[1], dir[2]);
+          const double d = 1.0 / norm(direct);
+          ds[i] = d;
+          directs[i] = direct * d;
+        }
+        if (ds[i] >= 0) {
+          const double pd2 = dot(directs[i], wld) + ds[i];
+          V6 jac_s;
+          jac_s.setBlock(0, 0, (phat * x_curr.R.T()) * directs[i]);
+          jac_s.setBlock(3, 0, directs[i]);
+          HTH += jac_s * jac_s.T();
+          HTz += jac_s * (-pd2);
+          valid++;
+        }
+      }
+      H_T_H.setBlock(0, 0, HTH);
+      M15 kin = H_T_H;
+      for (int r = 0; r < 15; r++)
+        for (int c = 0; c < 15; c++) kin(r, c) = H_T_H(r, c) + cov_inv(r, c) / 1000;  // odometry.cpp:393
+      M15 K_1 = inverse(kin);
+      Mat<15, 6> K6 = K_1.block<15, 6>(0, 0);
+      G.setBlock(0, 0, K6 * HTH);
+      V15 vec = x_prop.minus(x_curr);
+      V15 solution = K6 * HTz + vec - G.block<15, 6>(0, 0) * vec.block<6, 1>(0, 0);
+      x_curr += solution;
+      const V3 rot_add = solution.block<3, 1>(0, 0), tra_add = solution.block<3, 1>(3, 0);
+      refind = false;
+      if ((norm(rot_add) * 57.3 < 0.01) && (norm(tra_add) * 100 < 0.015)) {
+        refind = true;
+        flg_EKF_converged = true;
+        rematch_num++;
+      }
+      if (iterCount == num_max_iter - 2 && !flg_EKF_converged) refind = true;
+      if (rematch_num >= 2 || (iterCount == num_max_iter - 1)) {
+        x_curr.cov = (I_STATE - G) * x_curr.cov;
+        EKF_stop_flg = true;
+      }
+      if (EKF_stop_flg) break;
+    }
+    for (pointVar pv : pptr) {
+      pv.pnt = x_curr.R * pv.pnt + x_curr.p;
+      PointType ap;
+      ap.x = (float)pv.pnt[0];
+      ap.y = (float)pv.pnt[1];
+      ap.z = (float)pv.pnt[2];
+      pl_tree.push_back(ap);
+    }
+    down_sampling_voxel(pl_tree, 0.5);
+    return valid;
+  }
 
   explicit Pipeline(const orc_config& c) : voxhess(c.win_size) {
     cfg = c;
@@ -652,6 +766,41 @@ int orc_deskew_only(void* h, float* xyz, const float* times, int n, double beg, 
   return (int)P->imu_poses.size();
 }
 void orc_get_stats(void* h, orc_stats* s) { *s = ((Pipeline*)h)->st; }
+// one lio_state_estimation_kdtree call on the scan downsampled at
+// max(down_size, 0.5) (raw LiDAR frame; var_init applies the extrinsic),
+// with the context's x_curr (orc_seed / orc_get_state) as the state
+int orc_lio_kdtree(void* h, const float* xyz, int n, int* valid, int* iters) {
+  Pipeline* P = (Pipeline*)h;
+  std::vector<PointType> pl(n);
+  for (int i = 0; i < n; i++) {
+    pl[i].x = xyz[3 * i];
+    pl[i].y = xyz[3 * i + 1];
+    pl[i].z = xyz[3 * i + 2];
+  }
+  PVec pv;
+  var_init(P->extrin, pl, pv, P->cfg.dept_err, P->cfg.beam_err);
+  *valid = P->lio_kdtree(pv, iters);
+  return 0;
+}
+int orc_kdmap_size(void* h) { return (int)((Pipeline*)h)->pl_tree.size(); }
+void orc_kdmap_get(void* h, float* xyz) {
+  const std::vector<PointType>& t = ((Pipeline*)h)->pl_tree;
+  for (size_t i = 0; i < t.size(); i++) {
+    xyz[3 * i] = t[i].x;
+    xyz[3 * i + 1] = t[i].y;
+    xyz[3 * i + 2] = t[i].z;
+  }
+}
+void orc_qr_solve(const double* A, int m, const double* b, double* x) { colpiv_qr_solve(A, m, b, x); }
+int orc_knn(const float* pts, int np, const float* q, int k, int* idx, float* sq) {
+  std::vector<PointType> v(np);
+  for (int i = 0; i < np; i++) {
+    v[i].x = pts[3 * i];
+    v[i].y = pts[3 * i + 1];
+    v[i].z = pts[3 * i + 2];
+  }
+  return knn_brute(v, q[0], q[1], q[2], k, idx, sq);
+}
 void orc_shard(void* h, int rank, int world, int (*fn)(double*, int, void*), void* user) {
   Pipeline* P = (Pipeline*)h;
   P->mpar.shard_rank = rank;

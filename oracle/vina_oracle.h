@@ -69,6 +69,16 @@ int orc_traj_len(void* h);
 void orc_get_traj(void* h, double* out);
 int orc_window_states(void* h, double* out);
 
+/* VINA_SLAM::lio_state_estimation_kdtree (odometry.cpp:267-439) on
+ * the context's x_curr and its initialisation map; valid = -1 when the scan
+ * only seeded the map (< 100 points). Helpers: the ColPivHouseholderQR solve
+ * and the exact kNN it restates. */
+int orc_lio_kdtree(void* h, const float* xyz, int n, int* valid, int* iters);
+int orc_kdmap_size(void* h);
+void orc_kdmap_get(void* h, float* xyz);
+void orc_qr_solve(const double* A, int m, const double* b, double* x);
+int orc_knn(const float* pts, int np, const float* q, int k, int* idx, float* sq);
+
 #ifdef __cplusplus
 }
 #endif

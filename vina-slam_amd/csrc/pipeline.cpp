@@ -859,6 +859,107 @@ static void state_out(const HX& x, double* s) {
   memcpy(s + 22, x.g.a, 24);
   memcpy(s + 25, x.cov.a, 225 * sizeof(double));
 }
+// lio_state_estimation_kdtree (odometry.cpp:267-439) on an
+// explicit state (250 doubles in/out): the per-point kNN, plane fit and
+// normal-equation sums on the device (kdlio.hip), the 15x15 update here. The
+// scan is the init-phase cloud downsampled at max(down_size, 0.5), raw LiDAR
+// frame (xyz AoS). *valid = -1 when the map held < 100 points and the scan
+// only seeded it.
+int host_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* valid, int* iters) {
+  VG_TRY(host_sync(ctx));  // the scan staging and downsample buffers are shared with the pipeline
+  if (n > ctx->cap.max_points_per_scan) {
+    ctx->err = "vg_lio_kdtree: scan larger than max_points_per_scan";
+    return VG_E_CAPACITY;
+  }
+  *valid = -1;
+  *iters = 0;
+  HX x_curr;
+  x_curr.t = state[0];
+  memcpy(x_curr.R.a, state + 1, 72);
+  memcpy(x_curr.p.a, state + 10, 24);
+  memcpy(x_curr.v.a, state + 13, 24);
+  memcpy(x_curr.bg.a, state + 16, 24);
+  memcpy(x_curr.ba.a, state + 19, 24);
+  memcpy(x_curr.g.a, state + 22, 24);
+  memcpy(x_curr.cov.a, state + 25, 225 * sizeof(double));
+  {
+    std::vector<float> soa((size_t)3 * n);
+    for (int i = 0; i < n; i++) {
+      soa[i] = xyz[3 * i];
+      soa[(size_t)n + i] = xyz[3 * i + 1];
+      soa[(size_t)2 * n + i] = xyz[3 * i + 2];
+    }
+    VG_HIP(hipMemcpy(ctx->d_x, soa.data(), (size_t)n * sizeof(float), hipMemcpyHostToDevice));
+    VG_HIP(hipMemcpy(ctx->d_y, soa.data() + n, (size_t)n * sizeof(float), hipMemcpyHostToDevice));
+    VG_HIP(hipMemcpy(ctx->d_z, soa.data() + 2 * (size_t)n, (size_t)n * sizeof(float), hipMemcpyHostToDevice));
+  }
+  if (n == 0) return VG_OK;
+  if (ctx->kd.n < 100) {  // 275-310: seed the map with the scan at the current pose
+    VG_TRY(kd_update(ctx, n, x_curr.R.a, x_curr.p.a, false));
+    return VG_OK;
+  }
+  const int num_max_iter = 4;
+  const HX x_prop = x_curr;
+  bool flg_conv = false;
+  int rematch_num = 0;
+  M15 G = M15::Z(), cov_inv = inverse(x_curr.cov);
+  bool refind = true;
+  for (int it = 0; it < num_max_iter; it++) {
+    (*iters)++;
+    double sums[28];
+    VG_TRY(kd_pass(ctx, n, x_curr.R.a, x_curr.p.a, refind ? 1 : 0, sums));
+    M15 HTH15 = M15::Z();
+    double HTz[6];
+    int k = 0;
+    for (int r = 0; r < 6; r++)
+      for (int c = r; c < 6; c++, k++) HTH15(r, c) = HTH15(c, r) = sums[k];
+    for (int r = 0; r < 6; r++) HTz[r] = sums[21 + r];
+    *valid = (int)sums[27];
+    M15 Kin;  // H_T_H + cov_inv / 1000 (odometry.cpp:393)
+    for (int r = 0; r < 15; r++)
+      for (int c = 0; c < 15; c++) Kin(r, c) = HTH15(r, c) + cov_inv(r, c) / 1000;
+    const M15 K_1 = inverse(Kin);
+    for (int r = 0; r < 15; r++)  // G(:, 0:6) = K_1(:, 0:6) HTH
+      for (int c = 0; c < 6; c++) {
+        double g = 0.0;
+        for (int q = 0; q < 6; q++) g += K_1(r, q) * HTH15(q, c);
+        G(r, c) = g;
+      }
+    const V15 vec = x_prop.minus(x_curr);
+    V15 sol;
+    for (int r = 0; r < 15; r++) {  // K_1(:,0:6) HTz + vec - G(:,0:6) vec(0:6)
+      double a = 0.0, b = 0.0;
+      for (int q = 0; q < 6; q++) a += K_1(r, q) * HTz[q];
+      for (int q = 0; q < 6; q++) b += G(r, q) * vec[q];
+      sol[r] = (a + vec[r]) - b;
+    }
+    x_curr.plus(sol);
+    const double rn = sqrt((sol[0] * sol[0] + sol[1] * sol[1]) + sol[2] * sol[2]);
+    const double tn = sqrt((sol[3] * sol[3] + sol[4] * sol[4]) + sol[5] * sol[5]);
+    refind = false;
+    if ((rn * 57.3 < 0.01) && (tn * 100 < 0.015)) {
+      refind = true;
+      flg_conv = true;
+      rematch_num++;
+    }
+    if (it == num_max_iter - 2 && !flg_conv) refind = true;
+    if (rematch_num >= 2 || it == num_max_iter - 1) {  // cov = (I - G) cov
+      M15 nc;
+      for (int r = 0; r < 15; r++)
+        for (int c = 0; c < 15; c++) {
+          double a = 0.0;
+          for (int q = 0; q < 15; q++) a += ((r == q ? 1.0 : 0.0) - G(r, q)) * x_curr.cov(q, c);
+          nc(r, c) = a;
+        }
+      x_curr.cov = nc;
+      break;
+    }
+  }
+  VG_TRY(kd_update(ctx, n, x_curr.R.a, x_curr.p.a, true));  // 427-437
+  state_out(x_curr, state);
+  return VG_OK;
+}
+
 // x_curr now: between scans the absorbed host mirror; inside a scan (e.g.
 // save_pose_tum right after VNC_lio, local_mapping.cpp:429) the device state
 int host_state(vg_ctx* ctx, double* s) {

@@ -63,6 +63,24 @@ struct Arena {
   }
 };
 
+// Initialisation map of lio_state_estimation_kdtree (odometry.cpp:267-439,
+// SURVEY A14): float points (0.5 m downsampled), bucketed by 1 m cells for an
+// exact k = 5 nearest-neighbour search (kdlio.hip)
+struct KdMap {
+  float *x = nullptr, *y = nullptr, *z = nullptr;     // map points (key order of the last downsample)
+  float *sx = nullptr, *sy = nullptr, *sz = nullptr;  // the same, grouped by cell
+  int* sidx = nullptr;                                // map index of each grouped point
+  uint64_t *keys = nullptr, *keys_s = nullptr;
+  uint32_t *idx = nullptr, *idx_s = nullptr;
+  uint64_t* hkey = nullptr;                           // cell hash: key -> [start, end) in s*
+  int *hstart = nullptr, *hend = nullptr;
+  int hmask = 0, cap = 0, n = 0;
+  double *ds = nullptr, *dir = nullptr, *part = nullptr;  // per scan point: plane offset, normal; block partials
+  double* h_part = nullptr;                           // pinned copy of the partials
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+};
+
 struct DownsampleBufs {
   uint64_t *keys = nullptr, *keys_sorted = nullptr;
   uint32_t *idx = nullptr, *idx_sorted = nullptr;
@@ -253,6 +271,7 @@ struct vg_ctx {
   const float *cur_x = nullptr, *cur_y = nullptr, *cur_z = nullptr, *cur_i = nullptr;
   int cur_n = -1;
   vg::DownsampleBufs ds;
+  vg::KdMap kd;
   vg::DevMap map;
   vg::Work wk;
   vg::BaBufs ba;
@@ -377,6 +396,16 @@ struct WinD {           // window poses x_buf (by ord) and the ring mp[] (octree
 
 // downsample.hip
 int ds_alloc(vg_ctx* ctx);
+// kdlio.hip
+int kd_alloc(vg_ctx* ctx);
+int kd_reset(vg_ctx* ctx);
+// one pass of the kd-tree IEKF over the scan in ctx->d_x/y/z (n points, raw
+// LiDAR frame) at pose (R row-major 9, p 3): refind -> kNN + plane fits, then
+// the 28 sums (HTH upper 21, HTz 6, valid count) -> out28 (synchronous)
+int kd_pass(vg_ctx* ctx, int n, const double* R, const double* p, int refind, double* out28);
+// append the scan at pose (R, p) to the map, re-downsample at 0.5 m, rebuild
+// the cell index (synchronous); or only append + index when the map is seeding
+int kd_update(vg_ctx* ctx, int n, const double* R, const double* p, bool downsample);
 // Voxel-grid downsample of a device-resident SoA cloud; results land in
 // ctx->ds.o* (n_out voxels, ascending packed-key order). Host-synchronous
 // (returns n_out).
@@ -441,6 +470,7 @@ int shard_alloc(vg_ctx* ctx);
 void shard_free(vg_ctx* ctx);
 int shard_allreduce(vg_ctx* ctx, const void* send, void* recv, int count, int dtype);
 int host_sync(vg_ctx* ctx);
+int host_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* valid, int* iters);
 int host_stats_log(vg_ctx* ctx, vg_stats* out, int cap);
 int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double end);
 int stage_deskew(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, const float* t,

@@ -383,3 +383,120 @@ VG_HD M<N, N> inverse(const M<N, N>& Ain) {
   return o;
 }
 }  // namespace vg
+
+namespace vg {
+// Eigen ColPivHouseholderQR(A).solve(b) for A m x 3 (m <= 8, row-major),
+// restated from Eigen's algorithm (odometry.cpp:362): Householder
+// QR with column pivoting on the largest remaining column norm (first on ties),
+// the sqrt(eps) norm-downdate recompute rule, the rank cut of its
+// nonzero-pivot count, Q^T b, back substitution, inverse column permutation.
+// Reductions are sequential (Eigen vectorises them: rounding-level).
+VG_HD void colpiv_qr_solve(const double* Ain, int m, const double* b, double* x) {
+  const int n = 3, size = m < n ? m : n;
+  double A[8 * 3];
+  for (int i = 0; i < m * n; i++) A[i] = Ain[i];
+  double tau[3], normU[3], normD[3];
+  int trans[3];
+  double maxnorm = 0.0;
+  for (int j = 0; j < n; j++) {
+    double s = 0.0;
+    for (int r = 0; r < m; r++) s += A[r * 3 + j] * A[r * 3 + j];
+    normD[j] = normU[j] = sqrt(s);
+    if (normU[j] > maxnorm) maxnorm = normU[j];
+  }
+  const double eps = 2.220446049250313e-16;
+  const double thr_helper = (maxnorm * eps) * (maxnorm * eps) / m;
+  const double downdate_thr = sqrt(eps);
+  int nonzero = size;
+  for (int k = 0; k < size; k++) {
+    int big = k;
+    for (int j = k + 1; j < n; j++)
+      if (normU[j] > normU[big]) big = j;
+    const double big_sq = normU[big] * normU[big];
+    if (nonzero == size && big_sq < thr_helper * (m - k)) nonzero = k;
+    trans[k] = big;
+    if (k != big) {
+      for (int r = 0; r < m; r++) {
+        const double t = A[r * 3 + k];
+        A[r * 3 + k] = A[r * 3 + big];
+        A[r * 3 + big] = t;
+      }
+      double t = normU[k];
+      normU[k] = normU[big];
+      normU[big] = t;
+      t = normD[k];
+      normD[k] = normD[big];
+      normD[big] = t;
+    }
+    double tail = 0.0;
+    for (int r = k + 1; r < m; r++) tail += A[r * 3 + k] * A[r * 3 + k];
+    const double c0 = A[k * 3 + k];
+    double beta;
+    if (tail <= 2.2250738585072014e-308) {
+      tau[k] = 0.0;
+      beta = c0;
+      for (int r = k + 1; r < m; r++) A[r * 3 + k] = 0.0;
+    } else {
+      beta = sqrt(c0 * c0 + tail);
+      if (c0 >= 0.0) beta = -beta;
+      for (int r = k + 1; r < m; r++) A[r * 3 + k] = A[r * 3 + k] / (c0 - beta);
+      tau[k] = (beta - c0) / beta;
+    }
+    A[k * 3 + k] = beta;
+    for (int j = k + 1; j < n; j++) {
+      if (m - k == 1) {
+        A[k * 3 + j] *= (1.0 - tau[k]);
+      } else if (tau[k] != 0.0) {
+        double t = 0.0;
+        for (int r = k + 1; r < m; r++) t += A[r * 3 + k] * A[r * 3 + j];
+        t += A[k * 3 + j];
+        A[k * 3 + j] -= tau[k] * t;
+        for (int r = k + 1; r < m; r++) A[r * 3 + j] -= tau[k] * A[r * 3 + k] * t;
+      }
+    }
+    for (int j = k + 1; j < n; j++) {
+      if (normU[j] != 0.0) {
+        double t = fabs(A[k * 3 + j]) / normU[j];
+        t = (1.0 + t) * (1.0 - t);
+        if (t < 0.0) t = 0.0;
+        const double q = normU[j] / normD[j];
+        const double t2 = t * q * q;
+        if (t2 <= downdate_thr) {
+          double s = 0.0;
+          for (int r = k + 1; r < m; r++) s += A[r * 3 + j] * A[r * 3 + j];
+          normD[j] = sqrt(s);
+          normU[j] = normD[j];
+        } else {
+          normU[j] *= sqrt(t);
+        }
+      }
+    }
+  }
+  double c[8];
+  for (int r = 0; r < m; r++) c[r] = b[r];
+  for (int k = 0; k < nonzero; k++) {
+    if (m - k == 1) {
+      c[k] *= (1.0 - tau[k]);
+    } else if (tau[k] != 0.0) {
+      double t = 0.0;
+      for (int r = k + 1; r < m; r++) t += A[r * 3 + k] * c[r];
+      t += c[k];
+      c[k] -= tau[k] * t;
+      for (int r = k + 1; r < m; r++) c[r] -= tau[k] * A[r * 3 + k] * t;
+    }
+  }
+  double y[3] = {0.0, 0.0, 0.0};
+  for (int i = nonzero - 1; i >= 0; i--) {
+    double s = c[i];
+    for (int j = i + 1; j < nonzero; j++) s -= A[i * 3 + j] * y[j];
+    y[i] = s / A[i * 3 + i];
+  }
+  int perm[3] = {0, 1, 2};
+  for (int k = 0; k < size; k++) {
+    const int t = perm[k];
+    perm[k] = perm[trans[k]];
+    perm[trans[k]] = t;
+  }
+  for (int i = 0; i < n; i++) x[perm[i]] = y[i];
+}
+}  // namespace vg

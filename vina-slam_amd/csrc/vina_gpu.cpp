@@ -71,6 +71,7 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     if (r == VG_OK) r = ds_alloc(ctx);
     if (r == VG_OK) r = map_alloc(ctx);
     if (r == VG_OK) r = ba_alloc(ctx);
+    if (r == VG_OK) r = kd_alloc(ctx);
     return r;
   };
   ctx->arena.measure = true;
@@ -172,6 +173,7 @@ int vg_reset(vg_ctx* ctx) {
   VG_HIP(hipStreamSynchronize(ctx->stream_ds));
   VG_HIP(hipStreamSynchronize(ctx->stream));
   VG_TRY(map_reset(ctx));
+  VG_TRY(kd_reset(ctx));
   host_reset(ctx);
   return VG_OK;
 }
@@ -455,3 +457,28 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
   }
   return VG_E_ARG;
 }
+
+int vg_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* valid, int* iters) {
+  if (!ctx || (!xyz && n > 0) || n < 0 || !state || !valid || !iters) return VG_E_ARG;
+  return host_lio_kdtree(ctx, xyz, n, state, valid, iters);
+}
+
+int vg_kdmap_get(vg_ctx* ctx, float* xyz, int cap, int* n) {
+  if (!ctx || !n) return VG_E_ARG;
+  *n = ctx->kd.n;
+  if (!xyz || cap <= 0) return VG_OK;
+  const int m = ctx->kd.n < cap ? ctx->kd.n : cap;
+  std::vector<float> t((size_t)3 * m);
+  if (m > 0) {
+    VG_HIP(hipMemcpy(t.data(), ctx->kd.x, (size_t)m * sizeof(float), hipMemcpyDeviceToHost));
+    VG_HIP(hipMemcpy(t.data() + m, ctx->kd.y, (size_t)m * sizeof(float), hipMemcpyDeviceToHost));
+    VG_HIP(hipMemcpy(t.data() + 2 * (size_t)m, ctx->kd.z, (size_t)m * sizeof(float), hipMemcpyDeviceToHost));
+  }
+  for (int i = 0; i < m; i++) {
+    xyz[3 * i] = t[i];
+    xyz[3 * i + 1] = t[(size_t)m + i];
+    xyz[3 * i + 2] = t[2 * (size_t)m + i];
+  }
+  return VG_OK;
+}
+

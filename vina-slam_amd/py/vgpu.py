@@ -76,6 +76,8 @@ def lib():
         L.vg_reset.argtypes = [P]
         L.vg_downsample.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, fp, ip]
         L.vg_seed.argtypes = [P, dp]
+        L.vg_lio_kdtree.argtypes = [P, fp, ctypes.c_int, dp, ip, ip]
+        L.vg_kdmap_get.argtypes = [P, fp, ctypes.c_int, ip]
         L.vg_step.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
         L.vg_step_dev.argtypes = [P, P, P, P, P, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
         L.vg_step_deskew.argtypes = [P, fp, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
@@ -190,6 +192,25 @@ class Context:
         s = np.zeros(STATE_LEN)
         self._chk(lib().vg_get_state(self.h, _d(s)), "vg_get_state")
         return s
+
+    def lio_kdtree(self, xyz, state):
+        """SURVEY A14 (init-phase LIO against the kNN map): returns (state,
+        valid correspondences or -1 when the scan only seeded the map, IEKF
+        iterations). xyz: the scan downsampled at max(down_size, 0.5)."""
+        xyz = np.ascontiguousarray(xyz, dtype=np.float32).reshape(-1, 3)
+        st = np.array(state, dtype=np.float64, copy=True)
+        v = ctypes.c_int(0)
+        it = ctypes.c_int(0)
+        self._chk(lib().vg_lio_kdtree(self.h, _f(xyz), xyz.shape[0], _d(st), ctypes.byref(v), ctypes.byref(it)),
+                  "vg_lio_kdtree")
+        return st, v.value, it.value
+
+    def kdmap(self):
+        n = ctypes.c_int(0)
+        self._chk(lib().vg_kdmap_get(self.h, None, 0, ctypes.byref(n)), "vg_kdmap_get")
+        out = np.zeros((max(n.value, 1), 3), dtype=np.float32)
+        self._chk(lib().vg_kdmap_get(self.h, _f(out), n.value, ctypes.byref(n)), "vg_kdmap_get")
+        return out[: n.value]
 
     def stats(self):
         s = Stats()
