@@ -51,6 +51,8 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(m.hfirst = ctx->arena.take<int>(hs));
   good &= ok(m.slide = ctx->arena.take<int>(cn));
   good &= ok(m.in_slide = ctx->arena.take<uint8_t>(cn));
+  good &= ok(m.leaf_cnt = ctx->arena.take<int>(cn));
+  good &= ok(m.leaf_seg = ctx->arena.take<int>(cn));
   good &= ok(m.fix_pnt = ctx->arena.take<double>((size_t)m.cap_fix * 3));
   good &= ok(m.fix_var = ctx->arena.take<double>((size_t)m.cap_fix * 9));
   good &= ok(m.wp_pnt = ctx->arena.take<double>(cw * W * 3));
@@ -107,6 +109,7 @@ int map_reset(vg_ctx* ctx) {
   VG_HIP(hipMemsetAsync(m.counters, 0, kCntN * sizeof(int), s));
   VG_HIP(hipMemsetAsync(ctx->wk.cand_bits, 0, (ctx->cap.max_nodes / 32 + 1) * sizeof(uint32_t), s));
   VG_HIP(hipMemsetAsync(m.in_slide, 0, m.cap_nodes, s));
+  VG_HIP(hipMemsetAsync(m.leaf_cnt, 0, (size_t)m.cap_nodes * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.cfirst, 0x7f, (size_t)m.cap_nodes * 8 * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.nscr, 0xff, (size_t)m.cap_nodes * 4 * sizeof(int), s));
   VG_HIP(hipStreamSynchronize(s));
@@ -535,63 +538,108 @@ __global__ void __launch_bounds__(256) k_child_count(int np, const int* __restri
 __global__ void __launch_bounds__(256) k_child_alloc(int np, const int* __restrict__ parents, const uint32_t* __restrict__ off, DevMap m,
                               int* __restrict__ next, int next_base);
 
+// the final leaf of every point, and its bucket: a point count per leaf
+// (m.leaf_cnt, zero between inserts) and, for the leaf's first point, a
+// segment (seg_leaf[s] = leaf, m.leaf_seg[leaf] = s). Segment order is free:
+// k_push_window treats every leaf on its own; only the order of a leaf's
+// points matters, and k_push_window restores it.
 __global__ void __launch_bounds__(256) k_ins_resolve(int n, int thread_num, const double* __restrict__ pw, DevMap m,
-                                                     int* __restrict__ leaf) {
-  if (ins_skip(m, thread_num)) return;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    int node = leaf[i];
-    if (node >= -1) continue;
-    int code = -2 - node;
-    leaf[i] = m.hdr[code >> 3].child[code & 7];
-  }
-}
-
-// sort key: (leaf << 27) | order
-__global__ void __launch_bounds__(256) k_ins_keys(int n, int thread_num, const DevMap m, const int* __restrict__ leaf,
-                                                  uint64_t* __restrict__ keys) {
-  if (ins_skip(m, thread_num)) return;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    int l = leaf[i];
-    keys[i] = l >= 0 ? (((uint64_t)l << 27) | (uint64_t)i) : ~0ull;
-  }
-}
-
-// OctoTree::push (octree.cpp:151-177) for every point of a leaf segment, in order
-// segment heads of a sorted (leaf << 27 | order) key list -> compact list
-__global__ void __launch_bounds__(256) k_seg_heads(int n, int thread_num, const DevMap m,
-                                                   const uint64_t* __restrict__ keys, int* __restrict__ heads,
-                                                   int* __restrict__ cnt) {
+                                                     int* __restrict__ leaf, int* __restrict__ seg_leaf) {
   if (ins_skip(m, thread_num)) return;
   for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-    const int j = base + threadIdx.x;
-    int head = 0;
-    if (j < n) {
-      const uint64_t k = keys[j];
-      head = k != ~0ull && (j == 0 || (keys[j - 1] >> 27) != (k >> 27)) ? 1 : 0;
+    const int i = base + threadIdx.x;
+    int node = i < n ? leaf[i] : -1;
+    if (node < -1) {
+      const int code = -2 - node;
+      node = m.hdr[code >> 3].child[code & 7];
+      leaf[i] = node;
     }
-    const int pos = wave_append(cnt, head);
-    if (head) heads[pos] = j;
+    const bool first = node >= 0 && atomicAdd(&m.leaf_cnt[node], 1) == 0;
+    const int s = wave_append(&m.counters[kCntSeg], first ? 1 : 0);
+    if (first) {
+      seg_leaf[s] = node;
+      m.leaf_seg[node] = s;
+    }
+  }
+}
+
+__device__ __forceinline__ int block_excl_scan(int v, int* s_wsum, int* total);
+// one workgroup: segment offsets = prefix over the segments' point counts;
+// the counts return to zero (k_ins_scatter counts the fill again)
+__global__ void __launch_bounds__(1024) k_seg_offsets(int thread_num, DevMap m, const int* __restrict__ seg_leaf,
+                                                      int* __restrict__ seg_off) {
+  __shared__ int s_w[17];
+  if (ins_skip(m, thread_num)) return;
+  const int ns = m.counters[kCntSeg];
+  const int per = (ns + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int s0 = threadIdx.x * per, s1 = min(ns, s0 + per);
+  int cnt = 0;
+  for (int q = s0; q < s1; q++) cnt += m.leaf_cnt[seg_leaf[q]];
+  int total;
+  int pos = block_excl_scan(cnt, s_w, &total);
+  for (int q = s0; q < s1; q++) {
+    const int l = seg_leaf[q];
+    seg_off[q] = pos;
+    pos += m.leaf_cnt[l];
+    m.leaf_cnt[l] = 0;
+  }
+  if (threadIdx.x == 0) seg_off[ns] = total;
+}
+
+// every point into its segment (arbitrary order inside it)
+__global__ void __launch_bounds__(256) k_ins_scatter(int n, int thread_num, DevMap m, const int* __restrict__ leaf,
+                                                     const int* __restrict__ seg_off, int* __restrict__ order) {
+  if (ins_skip(m, thread_num)) return;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int l = leaf[i];
+    if (l < 0) continue;
+    order[seg_off[m.leaf_seg[l]] + atomicAdd(&m.leaf_cnt[l], 1)] = i;
   }
 }
 
 // pvec_update into the leaves (voxel_map.cpp:104-131 / octree.cpp:151-177):
-// one wave per leaf segment of the sorted keys; lanes 0-8 own the frame
-// cluster, 9-17 the accumulated cluster, 18-62 cov_add (see role_inc)
+// one wave per leaf segment (k_ins_resolve / k_seg_offsets / k_ins_scatter);
+// lanes 0-8 own the frame cluster, 9-17 the accumulated cluster, 18-62
+// cov_add (see role_inc)
 constexpr int kPushWaves = 4;
-__global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __restrict__ heads,
-                                                                 const int* __restrict__ nheads, int n,
-                                                                 const uint64_t* __restrict__ keys, MP mp, int slot,
-                                                                 DevMap m, const double* __restrict__ pw,
-                                                                 int thread_num) {
+__global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __restrict__ seg_leaf,
+                                                                 const int* __restrict__ seg_off,
+                                                                 const int* __restrict__ order,
+                                                                 int* __restrict__ order2, MP mp, int slot, DevMap m,
+                                                                 const double* __restrict__ pw, int thread_num) {
   __shared__ double E[kPushWaves][64][kErec];
   if (ins_skip(m, thread_num)) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int role = lane < 63 ? lane : -1;
   RoleIdx ri = role < 9 ? role_clu(role < 0 ? 0 : role, kEq) : role < 18 ? role_clu(role - 9, kEp) : role_cov(role - 18);
-  const int nseg = *nheads;
+  const int nseg = m.counters[kCntSeg];
   for (int sg = blockIdx.x * kPushWaves + wv; sg < nseg; sg += gridDim.x * kPushWaves) {
-    const int j0 = heads[sg];
-    const int leaf = (int)(keys[j0] >> 27);
+    const int j0 = seg_off[sg], L = seg_off[sg + 1] - j0;
+    const int leaf = seg_leaf[sg];
+    // the leaf's points in index order (the reference's push order): up to 64
+    // sorted across the lanes (bitonic by xor shuffles), longer segments ranked
+    // into order2
+    int mine = lane < L ? order[j0 + lane] : 0x7fffffff;
+    if (L <= 64) {
+#pragma unroll
+      for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          const int other = __shfl_xor(mine, j, 64);
+          const bool up = (lane & k) == 0, low = (lane & j) == 0;
+          mine = (low == up) ? min(mine, other) : max(mine, other);
+        }
+    } else {
+      for (int e = lane; e < L; e += 64) {
+        const int x = order[j0 + e];
+        int r = 0;
+        for (int t = 0; t < L; t++) r += order[j0 + t] < x ? 1 : 0;
+        order2[j0 + r] = x;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
     const bool listed = m.hdr[leaf].layer < mp.max_layer;
     Clu* loc = &m.pcrs[(size_t)leaf * mp.W + slot];
     Clu* add = &m.pcr_add[leaf];
@@ -600,33 +648,30 @@ __global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __re
                     : role < 18 ? (role < 15 ? &add->P[role - 9] : &add->v[role - 15])
                                 : &m.cov_add[(size_t)leaf * kCovN + role - 18];
     double acc = acc_p ? *acc_p : 0.0;
-    int cnt = 0;
-    for (int base = j0;; base += 64) {
+    for (int base = 0; base < L; base += 64) {
       const int e = base + lane;
-      const uint64_t kk = e < n ? keys[e] : ~0ull;
-      const bool valid = kk != ~0ull && (int)(kk >> 27) == leaf;
+      const bool valid = e < L;
       if (valid) {
-        const int i = (int)(kk & ((1u << 27) - 1));
+        const int i = L <= 64 ? mine : order2[j0 + e];
         const size_t b = (size_t)slot * m.cap_wp + i;
         fill_record(E[wv][lane], ld_v3(&m.wp_pnt[b * 3]), v3(pw[3 * i], pw[3 * i + 1], pw[3 * i + 2]),
                     ld_m3(&m.wp_var[b * 9]));
         if (listed) m.wp_leaf[b] = leaf;
       }
-      const int nb = __popcll(__ballot(valid));
+      const int nb = min(64, L - base);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       for (int k = 0; k < nb; k++) acc += role_inc(E[wv][k], ri);
-      cnt += nb;
       __builtin_amdgcn_wave_barrier();
-      if (nb < 64) break;
     }
     if (acc_p) *acc_p = acc;
     if (lane == 0) {
-      loc->N += cnt;
-      add->N += cnt;
+      loc->N += L;
+      add->N += L;
       m.hdr[leaf].has_sw = 1;
       m.hdr[leaf].isexist = 1;
+      m.leaf_cnt[leaf] = 0;  // bucketing invariant: zero between inserts
     }
   }
 }
@@ -850,15 +895,17 @@ static int insert_tail(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_nu
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
   const int g = grid_for(n);
-  const int key_bits = 27 + bits_for(m.cap_nodes);
   const int gseg = (n + kPushWaves - 1) / kPushWaves < 2048 ? (n + kPushWaves - 1) / kPushWaves : 2048;
-  k_ins_resolve<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.leaf);
-  k_ins_keys<<<g, kBlock, 0, s>>>(n, thread_num, m, w.leaf, w.k0);
-  VG_TRY(sort_keys(ctx, w.k0, w.k1, n, key_bits, 27));  // stable: leaf bits only
-  k_seg_heads<<<g, kBlock, 0, s>>>(n, thread_num, m, w.k1, w.list1, m.counters + kCntSeg);
+  int* seg_leaf = w.list1;
+  int* seg_off = reinterpret_cast<int*>(w.v0);
+  int* order = reinterpret_cast<int*>(w.k0);
+  int* order2 = reinterpret_cast<int*>(w.k1);
+  // leaves -> per-leaf buckets (no sort: the order between leaves is free)
+  k_ins_resolve<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.leaf, seg_leaf);
+  k_seg_offsets<<<1, 1024, 0, s>>>(thread_num, m, seg_leaf, seg_off);
+  k_ins_scatter<<<g, kBlock, 0, s>>>(n, thread_num, m, w.leaf, seg_off, order);
   // ~one wave per leaf segment (the count stays on the device)
-  k_push_window<<<gseg, 64 * kPushWaves, 0, s>>>(w.list1, m.counters + kCntSeg, n, w.k1, mp, slot, m, w.pw,
-                                                thread_num);
+  k_push_window<<<gseg, 64 * kPushWaves, 0, s>>>(seg_leaf, seg_off, order, order2, mp, slot, m, w.pw, thread_num);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }

@@ -129,6 +129,8 @@ struct DevMap {
   int* hfirst = nullptr;
   int* slide = nullptr;        // surf_map_slide (root ids)
   uint8_t* in_slide = nullptr;
+  int* leaf_cnt = nullptr;     // insert bucketing: points of this scan per leaf (0 between inserts)
+  int* leaf_seg = nullptr;     // insert bucketing: the leaf's segment
   double* fix_pnt = nullptr;   // point_fix arena: pnt (world) 3, var 6
   double* fix_var = nullptr;
   double* wp_pnt = nullptr;    // window points per physical slot: body pnt
