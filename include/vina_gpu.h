@@ -131,6 +131,34 @@ int vg_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* vali
 /* the init map (float xyz, n x 3, key order of its last downsample): *n = its
  * size; up to cap points copied when xyz != NULL */
 int vg_kdmap_get(vg_ctx* ctx, float* xyz, int cap, int* n);
+/* SURVEY row f3 — sensor decode (LidarPointCloudDecoder, lidar_pointcloud_decoder.cpp:21-240)
+ * and pcl_handler's scan preparation (lidar_decoder.cpp:7-43): per record the
+ * xyz / intensity / per-point time of the sensor format, the point_filter_num
+ * stride and blind test, then ascending time order and the tail beyond 0.11 s
+ * dropped (an empty result becomes the reference's two dummy points).
+ * records: n little-endian records of `stride` bytes; offsets are byte offsets
+ * of the fields, -1 when absent. Field types per kind (the reference's point
+ * structs): LIVOX x,y,z f32, reflectivity u8, offset_time u32 ns; VELODYNE
+ * x,y,z,time f32 (a sweep without usable times takes the yaw-derived time,
+ * omega_l deg/s, sequentially on the host as the reference does); OUSTER
+ * x,y,z,intensity f32, t u32 ns; HESAI x,y,z,intensity f32, timestamp f64
+ * (minus the first record's); ROBOSENSE x,y,z,intensity f32, timestamp f64
+ * (minus time_base, the header stamp; blind on x,y only); TARTANAIR x,y,z f32
+ * (no filter, time 0). blind in metres (squared as node.cpp:210 does).
+ * Outputs (host, capacity n + 2): xyz n_out x 3, intensity, time (s). The
+ * time sort is stable (std::sort's order among equal times is unspecified). */
+enum { VG_LIVOX = 0, VG_VELODYNE = 1, VG_OUSTER = 2, VG_HESAI = 3, VG_ROBOSENSE = 4, VG_TARTANAIR = 5 };
+typedef struct vg_lidar_format {
+  int kind;
+  int stride;
+  int off_x, off_y, off_z, off_intensity, off_time;
+  int point_filter_num;
+  double blind;
+  double omega_l;
+  double time_base;
+} vg_lidar_format;
+int vg_decode_scan(vg_ctx* ctx, const void* records, int n, const vg_lidar_format* fmt, float* xyz, float* intensity,
+                   float* time, int* n_out);
 int vg_get_state(vg_ctx* ctx, double* state);
 int vg_get_stats(vg_ctx* ctx, vg_stats* out);
 /* Per-scan counters of every completed scan since vg_create / vg_reset, in

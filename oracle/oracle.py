@@ -71,6 +71,8 @@ def lib():
         L.orc_kdmap_get.argtypes = [P, fp]
         L.orc_qr_solve.argtypes = [dp, ctypes.c_int, dp, dp]
         L.orc_knn.argtypes = [fp, ctypes.c_int, fp, ctypes.c_int, ip, fp]
+        L.orc_decode_scan.argtypes = [P, ctypes.c_int] + [ctypes.c_int] * 8 + [ctypes.c_double] * 3 + [fp,
+                                                                                                 ctypes.c_int]
         _lib = L
     return _lib
 
@@ -132,6 +134,20 @@ def knn(pts, q, k):
     sq = np.zeros(k, dtype=np.float32)
     n = lib().orc_knn(_f(pts), pts.shape[0], _f(q), k, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _f(sq))
     return idx[:n], sq[:n]
+
+
+def decode_scan(records, fmt):
+    """Sensor decoders + pcl_handler. records: bytes-like of n
+    little-endian records; fmt: dict of vg_lidar_format fields. Returns an
+    (m, 5) float32 array x, y, z, intensity, time."""
+    buf = np.frombuffer(bytes(records), dtype=np.uint8)
+    n = buf.size // fmt["stride"] if fmt["stride"] else 0
+    out = np.zeros((n + 2, 5), dtype=np.float32)
+    m = lib().orc_decode_scan(buf.ctypes.data_as(ctypes.c_void_p), n, fmt["kind"], fmt["stride"], fmt["off_x"],
+                              fmt["off_y"], fmt["off_z"], fmt["off_intensity"], fmt["off_time"],
+                              fmt["point_filter_num"], fmt["blind"], fmt.get("omega_l", 3610.0),
+                              fmt.get("time_base", 0.0), _f(out), n + 2)
+    return out[:m]
 
 
 def ldlt_solve(A, b):

@@ -14,6 +14,7 @@
 #include "map.hpp"
 #include "vina_oracle.h"
 
+#include "decode.hpp"
 #include "kdlio.hpp"
 
 namespace orc {
@@ -817,6 +818,23 @@ int orc_window_states(void* h, double* out) {
   Pipeline* p = (Pipeline*)h;
   for (size_t i = 0; i < p->x_buf.size(); i++) state_to(p->x_buf[i], out + 250 * i);
   return (int)p->x_buf.size();
+}
+
+// decoders + pcl_handler over little-endian records
+int orc_decode_scan(const void* rec, int n, int kind, int stride, int off_x, int off_y, int off_z, int off_i,
+                    int off_t, int filter_num, double blind, double omega_l, double time_base, float* out5,
+                    int cap) {
+  DecFormat f{kind, stride, off_x, off_y, off_z, off_i, off_t, filter_num, blind, omega_l, time_base};
+  std::vector<DecPoint> v = decode_records((const unsigned char*)rec, n, f);
+  const int m = (int)v.size() < cap ? (int)v.size() : cap;
+  for (int j = 0; j < m; j++) {
+    out5[5 * j] = v[j].x;
+    out5[5 * j + 1] = v[j].y;
+    out5[5 * j + 2] = v[j].z;
+    out5[5 * j + 3] = v[j].intensity;
+    out5[5 * j + 4] = v[j].curvature;
+  }
+  return (int)v.size();
 }
 
 }  // extern "C"

@@ -79,6 +79,11 @@ void orc_kdmap_get(void* h, float* xyz);
 void orc_qr_solve(const double* A, int m, const double* b, double* x);
 int orc_knn(const float* pts, int np, const float* q, int k, int* idx, float* sq);
 
+/* sensor decoders + pcl_handler (kind = LID_TYPE order); out5 =
+ * x, y, z, intensity, time per point (capacity cap); returns the count */
+int orc_decode_scan(const void* rec, int n, int kind, int stride, int off_x, int off_y, int off_z, int off_i,
+                    int off_t, int filter_num, double blind, double omega_l, double time_base, float* out5, int cap);
+
 #ifdef __cplusplus
 }
 #endif

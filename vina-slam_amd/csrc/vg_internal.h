@@ -473,6 +473,8 @@ void shard_free(vg_ctx* ctx);
 int shard_allreduce(vg_ctx* ctx, const void* send, void* recv, int count, int dtype);
 int host_sync(vg_ctx* ctx);
 int host_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* valid, int* iters);
+int decode_scan(vg_ctx* ctx, const void* records, int n, const vg_lidar_format* fmt, float* xyz, float* inten,
+                float* time, int* n_out);  // decode.hip
 int host_stats_log(vg_ctx* ctx, vg_stats* out, int cap);
 int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double end);
 int stage_deskew(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, const float* t,

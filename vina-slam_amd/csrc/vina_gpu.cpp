@@ -482,3 +482,9 @@ int vg_kdmap_get(vg_ctx* ctx, float* xyz, int cap, int* n) {
   return VG_OK;
 }
 
+int vg_decode_scan(vg_ctx* ctx, const void* records, int n, const vg_lidar_format* fmt, float* xyz, float* intensity,
+                   float* time, int* n_out) {
+  if (!ctx || !fmt || (!records && n > 0) || n < 0 || !xyz || !time || !n_out) return VG_E_ARG;
+  return decode_scan(ctx, records, n, fmt, xyz, intensity, time, n_out);
+}
+

@@ -26,6 +26,14 @@ class Capacity(ctypes.Structure):
                 ("max_fix_points", ctypes.c_int), ("hash_log2", ctypes.c_int)]
 
 
+class LidarFormat(ctypes.Structure):
+    """vg_lidar_format."""
+    _fields_ = [("kind", ctypes.c_int), ("stride", ctypes.c_int), ("off_x", ctypes.c_int), ("off_y", ctypes.c_int),
+                ("off_z", ctypes.c_int), ("off_intensity", ctypes.c_int), ("off_time", ctypes.c_int),
+                ("point_filter_num", ctypes.c_int), ("blind", ctypes.c_double), ("omega_l", ctypes.c_double),
+                ("time_base", ctypes.c_double)]
+
+
 class Stats(ctypes.Structure):
     _fields_ = [("n_raw", ctypes.c_int), ("n_ds", ctypes.c_int), ("iekf_iters", ctypes.c_int),
                 ("iekf_matches", ctypes.c_int * 4), ("roots_new", ctypes.c_int), ("n_slide", ctypes.c_int),
@@ -78,6 +86,7 @@ def lib():
         L.vg_seed.argtypes = [P, dp]
         L.vg_lio_kdtree.argtypes = [P, fp, ctypes.c_int, dp, ip, ip]
         L.vg_kdmap_get.argtypes = [P, fp, ctypes.c_int, ip]
+        L.vg_decode_scan.argtypes = [P, P, ctypes.c_int, ctypes.POINTER(LidarFormat), fp, fp, fp, ip]
         L.vg_step.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
         L.vg_step_dev.argtypes = [P, P, P, P, P, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
         L.vg_step_deskew.argtypes = [P, fp, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
@@ -204,6 +213,19 @@ class Context:
         self._chk(lib().vg_lio_kdtree(self.h, _f(xyz), xyz.shape[0], _d(st), ctypes.byref(v), ctypes.byref(it)),
                   "vg_lio_kdtree")
         return st, v.value, it.value
+
+    def decode_scan(self, records, fmt):
+        """Sensor records -> time-ordered scan: (xyz (m, 3), intensity, time)."""
+        buf = np.frombuffer(bytes(records), dtype=np.uint8)
+        f = LidarFormat(**{k: fmt.get(k, 3610.0 if k == "omega_l" else 0.0) for k, _ in LidarFormat._fields_})
+        n = buf.size // f.stride
+        xyz = np.zeros((n + 2, 3), dtype=np.float32)
+        it = np.zeros(n + 2, dtype=np.float32)
+        tm = np.zeros(n + 2, dtype=np.float32)
+        m = ctypes.c_int(0)
+        self._chk(lib().vg_decode_scan(self.h, buf.ctypes.data_as(ctypes.c_void_p), n, ctypes.byref(f), _f(xyz),
+                                       _f(it), _f(tm), ctypes.byref(m)), "vg_decode_scan")
+        return xyz[: m.value], it[: m.value], tm[: m.value]
 
     def kdmap(self):
         n = ctypes.c_int(0)
