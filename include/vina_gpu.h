@@ -159,6 +159,22 @@ typedef struct vg_lidar_format {
 } vg_lidar_format;
 int vg_decode_scan(vg_ctx* ctx, const void* records, int n, const vg_lidar_format* fmt, float* xyz, float* intensity,
                    float* time, int* n_out);
+/* SURVEY row f3 (replay side) — sync_packages (src/sensor/sync.cpp:18-96) as a
+ * host packager, no context: push scans (header time, the last point's time
+ * offset after vg_decode_scan, an id) and IMU samples (t, gyr 3, acc 3) in
+ * arrival order; vg_sync_pop sets *ready = 1 with one scan's window [beg, end]
+ * and its IMU samples (stamped <= end; up to cap copied, *m = count) once an
+ * IMU sample newer than end has arrived; *ready = 0: wait for more data;
+ * *ready = -1: a scan was consumed and dropped (<= 4 samples, as the
+ * reference), pop again. point_notime (Odometry.point_notime) windows scans by
+ * consecutive header times. VG_E_STATE: the IMU queue ran dry (the reference
+ * exits). */
+typedef struct vg_sync vg_sync;
+vg_sync* vg_sync_create(int point_notime);
+void vg_sync_destroy(vg_sync* s);
+int vg_sync_push_scan(vg_sync* s, double header_time, double last_point_time, int scan_id);
+int vg_sync_push_imu(vg_sync* s, const double* imu7);
+int vg_sync_pop(vg_sync* s, int* scan_id, double* beg, double* end, double* imu7, int cap, int* m, int* ready);
 int vg_get_state(vg_ctx* ctx, double* state);
 int vg_get_stats(vg_ctx* ctx, vg_stats* out);
 /* Per-scan counters of every completed scan since vg_create / vg_reset, in

@@ -142,3 +142,82 @@ def test_gpu_decode_matches_oracle(oracle_lib, name):
     assert np.array_equal(got[:, 4], ref[:, 4])
     assert np.array_equal(_rows(got), _rows(ref))
     ctx.close()
+
+
+def _ref_sync(events, point_notime):
+    """sync_packages (src/sensor/sync.cpp:18-96) restated in Python over an event
+    stream; returns the packages in order and whether the IMU stream ran dry."""
+    scans, imu, out = [], [], []
+    st = dict(ready=False, last_pcl=-1.0, imu_last=-1.0, cur=None, beg=0.0, end=0.0)
+
+    def step():
+        if not st["ready"]:
+            if not scans:
+                return False
+            sid, hb, last = scans.pop(0)
+            st["cur"], st["beg"], st["end"] = sid, hb, hb + last
+            if point_notime:
+                if st["last_pcl"] < 0:
+                    st["last_pcl"] = st["beg"]
+                    return False
+                st["end"] = st["beg"]
+                st["beg"] = st["last_pcl"]
+                st["last_pcl"] = st["end"]
+            st["ready"] = True
+        if st["imu_last"] <= st["end"]:
+            return False
+        taken = []
+        t = imu[0][0]
+        while imu and t < st["end"]:
+            t = imu[0][0]
+            if t > st["end"]:
+                break
+            taken.append(imu.pop(0))
+        st["ready"] = False
+        if not imu:
+            raise RuntimeError("dry")
+        if len(taken) > 4:
+            out.append((st["cur"], st["beg"], st["end"], np.array(taken)))
+        return True
+
+    for ev in events:
+        if ev[0] == "scan":
+            scans.append(ev[1:])
+        else:
+            imu.append(ev[1])
+            st["imu_last"] = ev[1][0]
+        while step():
+            pass
+    return out
+
+
+@pytest.mark.parametrize("point_notime", [0, 1])
+def test_sync_packages_match_reference_rules(point_notime):
+    import vgpu
+    rng = np.random.default_rng(point_notime + 4)
+    events, t_imu = [], 0.0
+    for k in range(30):
+        hb = 0.1 * k + rng.uniform(0, 0.002)
+        last = 0.0995 if k % 7 else 0.02  # a short scan gets too few IMU samples
+        while t_imu < hb + 0.12:
+            t_imu += 0.005 + rng.uniform(-1e-4, 1e-4)
+            events.append(("imu", np.array([t_imu, *rng.normal(size=6)])))
+        events.insert(len(events) - rng.integers(0, 10), ("scan", k, hb, last))
+    ref = _ref_sync(events, point_notime)
+    s = vgpu.Sync(point_notime)
+    got = []
+    for ev in events:
+        if ev[0] == "scan":
+            s.push_scan(ev[2], ev[3], ev[1])
+        else:
+            s.push_imu(ev[1])
+        while True:
+            p = s.pop()
+            if p is None:
+                break
+            if p != "dropped":
+                got.append(p)
+    s.close()
+    assert len(got) == len(ref) and len(ref) > 10
+    for (a, b, c, d), (e, f, g, h) in zip(got, ref):
+        assert a == e and b == f and c == g and np.array_equal(d, h)

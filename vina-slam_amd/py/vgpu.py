@@ -87,6 +87,12 @@ def lib():
         L.vg_lio_kdtree.argtypes = [P, fp, ctypes.c_int, dp, ip, ip]
         L.vg_kdmap_get.argtypes = [P, fp, ctypes.c_int, ip]
         L.vg_decode_scan.argtypes = [P, P, ctypes.c_int, ctypes.POINTER(LidarFormat), fp, fp, fp, ip]
+        L.vg_sync_create.argtypes = [ctypes.c_int]
+        L.vg_sync_create.restype = P
+        L.vg_sync_destroy.argtypes = [P]
+        L.vg_sync_push_scan.argtypes = [P, ctypes.c_double, ctypes.c_double, ctypes.c_int]
+        L.vg_sync_push_imu.argtypes = [P, dp]
+        L.vg_sync_pop.argtypes = [P, ip, dp, dp, dp, ctypes.c_int, ip, ip]
         L.vg_step.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
         L.vg_step_dev.argtypes = [P, P, P, P, P, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
         L.vg_step_deskew.argtypes = [P, fp, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
@@ -345,3 +351,37 @@ class Context:
 
     def stream(self):
         return lib().vg_stream(self.h)
+
+
+class Sync:
+    """sync_packages (replay side): host packager of scans and IMU samples."""
+
+    def __init__(self, point_notime=0):
+        self.h = lib().vg_sync_create(point_notime)
+
+    def close(self):
+        if self.h:
+            lib().vg_sync_destroy(self.h)
+            self.h = None
+
+    def push_scan(self, header_time, last_point_time, scan_id):
+        lib().vg_sync_push_scan(self.h, header_time, last_point_time, scan_id)
+
+    def push_imu(self, imu7):
+        a = np.ascontiguousarray(imu7, dtype=np.float64)
+        lib().vg_sync_push_imu(self.h, _d(a))
+
+    def pop(self, cap=4096):
+        """(scan_id, beg, end, imu (m, 7)), "dropped" (a scan with <= 4 IMU samples was
+        consumed), or None (wait for data); VgError when the IMU stream ran dry."""
+        sid, m, rd = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+        b, e = ctypes.c_double(0), ctypes.c_double(0)
+        out = np.zeros((cap, 7))
+        r = lib().vg_sync_pop(self.h, ctypes.byref(sid), ctypes.byref(b), ctypes.byref(e), _d(out), cap,
+                              ctypes.byref(m), ctypes.byref(rd))
+        if r != 0:
+            raise VgError("vg_sync_pop: IMU stream ran dry (%d)" % r)
+        if rd.value < 0:
+            return "dropped"
+        return (sid.value, b.value, e.value, out[: m.value].copy()) if rd.value else None
+
