@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seq", type=int, default=0)
     ap.add_argument("--stage-scans", type=int, default=8, help="untimed profiled scans for the stage breakdown")
+    ap.add_argument("--target-steps", type=int, default=20,
+                    help="N=1 only: scans timed on the north star's target workload (synthetic 128-line "
+                         "/ 200 k rays), reported beside the metric; 0 skips it")
     ap.add_argument("--mode", choices=["replica", "tile"], default="replica",
                     help="replica: an independent sequence per GPU (weak scaling); tile: ONE sequence with its "
                          "voxel map sharded by spatial tile over the GPUs, RCCL all-reduce of the normal "
@@ -188,6 +191,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args, p, seq)
+    target = None
+    if world == 1 and args.target_steps > 0 and args.lidar != "128line":
+        target = target_workload(args, p, dev)
 
     if rank == 0:
         line = {
@@ -199,12 +205,54 @@ def main():
                        "factors_per_scan": int(np.mean([s["n_factors"] for s in stats])),
                        "parallelism": ("tile-sharded x%d" if tile else "replica x%d") % world},
             "roofline": roof, "roofline_k_iekf": roof_iekf, "roofline_scan": roof_scan, "host_ms_per_scan": host_ms,
-            "cpu_baseline": cpu,
+            "cpu_baseline": cpu, "target_128line": target,
         }
         print(json.dumps(line))
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def target_workload(args, p, dev):
+    """The north star's target workload (synthetic 128-line clouds, 200,064
+    rays) on one GPU, same pipeline and protocol as the metric, fewer scans:
+    reported beside the metric, never as `value`."""
+    import torch
+
+    import synth
+    import vgconfig
+    import vgpu
+    g = p["General"]
+    seq = synth.Sequence("128line", args.seq, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
+    warm, steps = args.warmup, args.target_steps
+    scans, imus = [], []
+    for k in range(warm + steps):
+        xyz, inten, b, e = seq.scan(k)
+        t = torch.from_numpy(np.ascontiguousarray(np.concatenate([xyz.T, inten[None]], 0))).to(dev)
+        scans.append((t, xyz.shape[0], b, e))
+        imus.append(seq.imu(k))
+    ctx = vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=max(s[1] for s in scans) + 16)
+    ctx.seed(seq.gt_state(0))
+
+    def run(k):
+        t, n, b, e = scans[k]
+        ctx.step_dev(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), n, b, e, imus[k])
+
+    for k in range(warm):
+        run(k)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(warm, warm + steps):
+        run(k)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    st = ctx.stats_log()[warm:]
+    ctx.close()
+    return {"workload": "synthetic-128line@%s.yaml" % args.config, "value": round(steps / dt, 3), "unit": "scans/s",
+            "ms_per_step": round(dt * 1e3 / steps, 4), "steps": steps, "warmup": warm,
+            "points_per_scan": int(np.mean([s[1] for s in scans[warm:]])),
+            "downsampled_per_scan": int(np.mean([x["n_ds"] for x in st])) if st else None,
+            "factors_per_scan": int(np.mean([x["n_factors"] for x in st])) if st else None}
 
 
 def pmc_traffic():
