@@ -573,15 +573,36 @@ __global__ void __launch_bounds__(1024) k_seg_offsets(int thread_num, DevMap m, 
   const int ns = m.counters[kCntSeg];
   const int per = (ns + (int)blockDim.x - 1) / (int)blockDim.x;
   const int s0 = threadIdx.x * per, s1 = min(ns, s0 + per);
-  int cnt = 0;
-  for (int q = s0; q < s1; q++) cnt += m.leaf_cnt[seg_leaf[q]];
+  constexpr int kPer = 32;
   int total;
-  int pos = block_excl_scan(cnt, s_w, &total);
-  for (int q = s0; q < s1; q++) {
-    const int l = seg_leaf[q];
-    seg_off[q] = pos;
-    pos += m.leaf_cnt[l];
-    m.leaf_cnt[l] = 0;
+  if (per <= kPer) {  // all loads of a lane issued before any is used (two round trips, not 2 per segment)
+    int lf[kPer], c[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) lf[k] = s0 + k < s1 ? seg_leaf[s0 + k] : -1;
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      c[k] = lf[k] >= 0 ? m.leaf_cnt[lf[k]] : 0;
+      cnt += c[k];
+    }
+    int pos = block_excl_scan(cnt, s_w, &total);
+#pragma unroll
+    for (int k = 0; k < kPer; k++)
+      if (lf[k] >= 0) {
+        seg_off[s0 + k] = pos;
+        pos += c[k];
+        m.leaf_cnt[lf[k]] = 0;
+      }
+  } else {
+    int cnt = 0;
+    for (int q = s0; q < s1; q++) cnt += m.leaf_cnt[seg_leaf[q]];
+    int pos = block_excl_scan(cnt, s_w, &total);
+    for (int q = s0; q < s1; q++) {
+      const int l = seg_leaf[q];
+      seg_off[q] = pos;
+      pos += m.leaf_cnt[l];
+      m.leaf_cnt[l] = 0;
+    }
   }
   if (threadIdx.x == 0) seg_off[ns] = total;
 }
