@@ -263,14 +263,14 @@ __device__ __forceinline__ void factor_frame(const double* e, const Clu& pa, con
 // (row-major lower), then 6W gradient, then the residual
 __device__ __forceinline__ int lower_idx(int r, int c) { return r * (r + 1) / 2 + c; }
 
-constexpr int kHessThreads = 256;
+constexpr int kHessThreads = 512;  // 8 waves: a chunk's (factor, frame) lanes in one pass
 constexpr int kHessGridMax = 256;  // k_ba_hess chunk workgroups (more chunks loop)
 constexpr int kResidBlocks = 512;  // k_ba_resid workgroups (more chunks loop)
 __host__ __device__ constexpr int hess_fs(int W) { return kHessThreads / W < 64 ? kHessThreads / W : 64; }  // factors per sub-chunk
 __host__ __device__ constexpr int hess_ks(int W) { return (3 * hess_fs(W) + 3) / 4 * 4; }  // GEMM K per sub-chunk
 __host__ __device__ constexpr int hess_nt(int W) { return (6 * W + 15) / 16; }           // 16-wide output tiles
 __host__ __device__ constexpr int hess_xs(int W) { return hess_nt(W) * 16 + 16; }        // X row stride (+16: rows k, k+1 in opposite LDS halves)
-__host__ __device__ constexpr int hess_chunk(int W) { return 2 * hess_fs(W); }      // factors per workgroup
+__host__ __device__ constexpr int hess_chunk(int W) { return hess_fs(W); }      // factors per workgroup (one sub-chunk)
 
 // One workgroup per chunk of factors, no HBM intermediates: lane (f, i)
 // evaluates factor f of the sub-chunk at frame i, keeps the coe-weighted
