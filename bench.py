@@ -6,15 +6,20 @@ sequences, MI355X.
 
 N > 1 is launched by torch.distributed.run: one process per GPU, each running an
 independent sequence (replica mode, "scaling": "weak" — the path has no
-cross-sequence exchange). Timed region: K scans after W warm-up scans (the
-window must fill before BA/margi run), bracketed by barrier + synchronize;
-max over ranks. Inputs are resident in HBM before timing starts.
+cross-sequence exchange). Timed region: K scans after W warm-up scans, bracketed
+by barrier + synchronize; max over ranks. The warm-up is raised to at least
+win_size + 2 whatever the command line says: the LM and margi run only once the
+window is full, so every timed scan is a steady-state scan. Inputs are resident
+in HBM before timing starts (vg_step_dev); the host-input rate (vg_step, H2D
+copy inside) is reported beside it.
 
 Rank 0 at N = 1 also times the CPU restatement (oracle, test infrastructure) on
-a bounded sample of the same sequence: the cpu_baseline object.
+a bounded sample of the same sequence (5 worker threads as the reference, and
+1 thread): the cpu_baseline object, and the GPU trajectory's ATE against it.
 """
 import argparse
 import json
+import multiprocessing as mproc
 import os
 import sys
 import time
@@ -25,6 +30,8 @@ sys.path.insert(0, os.path.join(REPO, "vina-slam_amd", "py"))
 import numpy as np  # noqa: E402
 
 METRIC = "scans/sec (downsample+kNN+LM solve), 64-line LiDAR, 1/2/4/8 MI355X; ATE vs CPU"
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
+FP64_MFMA_TFLOPS = 78.6  # MI355X dense fp64 matrix peak
 
 
 def parse():
@@ -34,7 +41,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=12)
     ap.add_argument("--lidar", default="64line")
     ap.add_argument("--config", default="mid360")
-    ap.add_argument("--cpu-scans", type=int, default=24, help="oracle sample: scans timed after its own warm-up")
+    ap.add_argument("--cpu-warmup", type=int, default=20, help="oracle warm-up scans (BASELINE.md: 20)")
+    ap.add_argument("--cpu-scans", type=int, default=40, help="oracle sample: timed scans after its warm-up")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seq", type=int, default=0)
     ap.add_argument("--stage-scans", type=int, default=8, help="untimed profiled scans for the stage breakdown")
@@ -45,39 +53,72 @@ def parse():
                     help="replica: an independent sequence per GPU (weak scaling); tile: ONE sequence with its "
                          "voxel map sharded by spatial tile over the GPUs, RCCL all-reduce of the normal "
                          "equations (strong scaling)")
+    ap.add_argument("--workers", type=int, default=0, help="scan-generation processes (0: min(16, cpus))")
     return ap.parse_args()
+
+
+# ---- synthetic scans, generated before the GPU is touched (a process pool;
+# the ray caster is numpy and ~0.4 s per 64-line scan)
+def _gen(job):
+    import synth
+    lidar, seq_id, blind, ext_R, ext_t, k = job
+    seq = synth.Sequence(lidar, seq_id, blind=blind, ext_R=ext_R, ext_t=ext_t)
+    xyz, inten, b, e = seq.scan(k)
+    return xyz, inten, b, e, seq.imu(k)
+
+
+def gen_scans(lidar, seq_id, general, n, workers):
+    jobs = [(lidar, seq_id, general["blind"], general["extrinsic_rota"], general["extrinsic_tran"], k)
+            for k in range(n)]
+    if workers <= 1 or n <= 2:
+        return [_gen(j) for j in jobs]
+    with mproc.get_context("fork").Pool(min(workers, n)) as pool:
+        return pool.map(_gen, jobs, chunksize=1)
 
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
     import synth
     import vgconfig
-    import vgpu
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    tile = args.mode == "tile" and world > 1
+    p = vgconfig.load(args.config)
+    g = p["General"]
+    W = p["LocalBA"]["win_size"]
+    warmup = max(args.warmup, W + 2)
+    total = warmup + args.steps
+    cpu_on = rank == 0 and world == 1 and not args.no_cpu
+    n_need = max(total + args.stage_scans, args.cpu_warmup + args.cpu_scans if cpu_on else 0)
+    workers = args.workers or min(16, os.cpu_count() or 8)
+    if world > 1:
+        workers = max(1, workers // world)
+    seq_id = args.seq + (0 if tile else rank)
+    host_scans = gen_scans(args.lidar, seq_id, g, n_need, workers)
+    tgt_scans = {}
+    if world == 1 and args.target_steps > 0 and args.lidar != "128line":
+        for cfg in ("mid360", "robosense"):
+            gg = vgconfig.load(cfg)["General"]
+            tgt_scans[cfg] = gen_scans("128line", args.seq, gg, warmup + args.target_steps, workers)
+
+    import torch
+    import torch.distributed as dist
+
+    import vgpu
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    seq = synth.Sequence(args.lidar, seq_id, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
 
-    p = vgconfig.load(args.config)
-    g = p["General"]
-    tile = args.mode == "tile" and world > 1
-    seq = synth.Sequence(args.lidar, args.seq + (0 if tile else rank), blind=g["blind"], ext_R=g["extrinsic_rota"],
-                         ext_t=g["extrinsic_tran"])
-    total = args.warmup + args.steps
-    scans, imus = [], []
-    for k in range(total + args.stage_scans):
-        xyz, inten, b, e = seq.scan(k)
+    scans = []
+    for xyz, inten, b, e, _ in host_scans[: total + args.stage_scans]:
         t = torch.from_numpy(np.ascontiguousarray(np.concatenate([xyz.T, inten[None]], 0))).to(dev)
         scans.append((t, xyz.shape[0], b, e))
-        imus.append(seq.imu(k))
-    npts = int(np.mean([s[1] for s in scans[args.warmup:total]]))
+    imus = [h[4] for h in host_scans]
+    npts = int(np.mean([s[1] for s in scans[warmup:total]]))
     ctx = vgpu.Context(vgconfig.to_c(p), device=local, max_points=max(s[1] for s in scans) + 16)
     if tile:  # one RCCL communicator inside the library, id from rank 0
         obj = [vgpu.rccl_unique_id() if rank == 0 else None]
@@ -90,18 +131,17 @@ def main():
         t, n, b, e = scans[k]
         ctx.step_dev(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), n, b, e, imus[k])
 
-    for k in range(args.warmup):
+    for k in range(warmup):
         run(k)
     # k_ba_solve launch events on every 4th scan's LM run: each event record
     # leaves a few-us gap in the stream
     ctx.profile(True, every=4)
-    stats = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     nlog0 = len(ctx.stats_log())
     t0 = time.perf_counter()
-    for k in range(args.warmup, total):
+    for k in range(warmup, total):
         run(k)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -113,10 +153,9 @@ def main():
     if tile:  # every rank worked on the same scans
         value /= world
     # per-stage breakdown: a separate, untimed profiled pass over further scans
-    # of the same sequence (stage events cost ~6 % of a step)
-    stage_ms = {}
-    stage_prof = {}
-    stage_stats = []
+    # of the same sequence (stage events cost ~6 % of a step); it also counts
+    # the distinct plane records each IEKF iteration reads (P_k)
+    stage_ms, stage_prof, stage_stats = {}, {}, []
     extra = min(args.stage_scans, len(scans) - total)
     if extra > 0:
         ctx.profile(True, stages=True)
@@ -128,92 +167,138 @@ def main():
         stage_stats = ctx.stats_log()[nlog1:]
         stage_ms = {k: round(v["ms"] / extra, 4) for k, v in stage_prof.items() if not k.startswith("host_")}
         ctx.profile(False)
+    traj_gpu = ctx.trajectory()
+    ctx.close()
+    host_ms = {k[5:]: round(v["ms"] / args.steps, 4) for k, v in prof.items() if k.startswith("host_")}
 
-    # roofline of the dominant kernel by device time, k_ba_solve (the LM
-    # step's 15W x 15W LDL^T solve, one workgroup, fp64 MFMA trailing
-    # updates): algorithmic flops per launch = n^3/3 (LDL^T) + 2 n^2 (the two
-    # triangular solves), n = 15 * win_size - 15 (the gauge frame's 15
-    # unknowns are decoupled and not factored); peak = MI355X fp64 matrix
-    # 78.6 TFLOP/s (AMD spec). Launch time: HIP events around each executed
-    # k_ba_solve on the context stream over the timed region.
-    W = p["LocalBA"]["win_size"]
+    # ---- headline roofline: the whole scan against HBM -------
+    roof = scan_roofline(stats, stage_stats, W, dt / args.steps)
+    # ---- per-kernel rooflines ----------------------------------------------
+    # k_ba_solve (the LM step's 15W x 15W LDL^T, one workgroup, fp64 MFMA
+    # trailing updates): algorithmic flops per launch = n^3/3 + 2 n^2 with
+    # n = 15 W - 15 (the gauge frame is not factored) over its HIP-event launch
+    # time on the context stream in the timed region
     n_sys = 15 * W - 15
     flops = n_sys ** 3 / 3.0 + 2.0 * n_sys ** 2
     sol = prof["ba_solve"]
-    s_launch = sol["launches"]
-    s_avg = sol["ms"] * 1e-3 / max(s_launch, 1)
+    s_avg = sol["ms"] * 1e-3 / max(sol["launches"], 1)
     s_ach = flops / s_avg / 1e12 if s_avg > 0 else 0.0
-    host_ms = {k[5:]: round(v["ms"] / args.steps, 4) for k, v in prof.items() if k.startswith("host_")}
-    roof = {"kernel": "k_ba_solve", "bound": "mfma", "achieved": round(s_ach, 5), "peak": 78.6, "unit": "TFLOP/s",
-            "frac": round(s_ach / 78.6, 7), "traffic": None, "avg_launch_us": round(s_avg * 1e6, 3),
-            "launches": s_launch, "flops_per_launch": int(flops), "stage_ms_per_scan": stage_ms}
-    # secondary: the IEKF point loop k_iekf (HBM-bound gather): 16 B per raw
-    # point (fp32 xyz + cached leaf id read) + 4 B per matched point (cached
-    # leaf write); plane/node records are cache-resident and not counted. In
-    # the timed region the IEKF replays as one hipGraph, so its per-launch
-    # events come from the per-stage pass (direct launches, same scans' kind)
+    roof_solve = {"kernel": "k_ba_solve", "bound": "mfma", "achieved": round(s_ach, 5), "peak": FP64_MFMA_TFLOPS,
+                  "unit": "TFLOP/s", "frac": round(s_ach / FP64_MFMA_TFLOPS, 7), "traffic": None,
+                  "avg_launch_us": round(s_avg * 1e6, 3), "launches": sol["launches"], "flops_per_launch": int(flops)}
+    # k_iekf (hot loop #1, HBM-bound gather): 16 B per raw point (fp32 xyz +
+    # cached leaf) + 112 B per distinct plane record (P_k) per launch; in the
+    # timed region the IEKF replays as one hipGraph, so its per-launch events
+    # come from the per-stage pass (direct launches, same sequence)
     iek = stage_prof.get("iekf", {"ms": 0.0, "launches": 0})
     n_launch = iek["launches"]
-    pts = sum(s["n_raw"] * s["iekf_iters"] for s in stage_stats)
-    matched = sum(sum(s["iekf_matches"][: s["iekf_iters"]]) for s in stage_stats)
-    bytes_tot = 16.0 * pts + 4.0 * matched
+    bytes_tot = sum(s["iekf_iters"] * 16.0 * s["n_raw"] + 112.0 * sum(s["iekf_planes"][: s["iekf_iters"]])
+                    for s in stage_stats)
     avg_s = iek["ms"] * 1e-3 / max(n_launch, 1)
     achieved = (bytes_tot / max(n_launch, 1)) / avg_s / 1e9 if avg_s > 0 else 0.0
-    roof_iekf = {"kernel": "k_iekf", "bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0, "unit": "GB/s",
-                 "frac": round(achieved / 8000.0, 5), "traffic": None, "avg_launch_us": round(avg_s * 1e6, 3),
-                 "launches": n_launch}
-
-    # whole-scan algorithmic bytes over the timed scans, a LOWER
-    # bound: the per-scan counters do not give the distinct plane records
-    # read per IEKF iteration (P_k) or the leaves an insert touches (V_ins),
-    # so those terms are left out, and the Hessian passes count once per LM run
-    W = p["LocalBA"]["win_size"]
-    b_scan = 0.0
-    for st in stats:
-        b_scan += 16.0 * st["n_raw"] + 16.0 * st["n_ds"]  # read xyz+t, write centroid+count
-        b_scan += st["iekf_iters"] * 16.0 * st["n_raw"]  # body xyz + cached leaf per IEKF iteration
-        b_scan += 12.0 * st["n_ds"]  # insert
-        b_scan += st["n_slide"] * (W * 80.0 + 80.0)  # recut
-        b_scan += (1 + st["ba_iters"]) * st["n_factors"] * (W * 80.0 + 176.0)  # BA Hessian + residual passes
-    b_scan /= max(len(stats), 1)
-    scan_gbps = b_scan / (dt / args.steps) / 1e9 if dt > 0 else 0.0
-    roof_scan = {"bound": "hbm", "achieved": round(scan_gbps, 2), "peak": 8000.0, "unit": "GB/s",
-                 "frac": round(scan_gbps / 8000.0, 6), "bytes_per_scan": int(b_scan),
-                 "note": "SURVEY 8(d) algorithmic bytes per scan / ms_per_step; lower bound (P_k, V_ins omitted)"}
-
+    roof_iekf = {"kernel": "k_iekf", "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
+                 "avg_launch_us": round(avg_s * 1e6, 3), "launches": n_launch,
+                 "bytes_per_launch": int(bytes_tot / max(n_launch, 1))}
     pmc = pmc_traffic()
-    if "k_ba_solve" in pmc:
-        roof["traffic"] = pmc["k_ba_solve"]["traffic_bytes"]
-        roof["traffic_source"] = pmc["_file"]
-    if "k_iekf" in pmc:
-        roof_iekf["traffic"] = pmc["k_iekf"]["traffic_bytes"]
+    for r in (roof_solve, roof_iekf):
+        if r["kernel"] in pmc:
+            r["traffic"] = pmc[r["kernel"]]["traffic_bytes"]
+            r["traffic_source"] = pmc["_file"]
+    roof["stage_ms_per_scan"] = stage_ms
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(args, p, seq)
-    target = None
-    if world == 1 and args.target_steps > 0 and args.lidar != "128line":
-        target = target_workload(args, p, dev)
+    h2d = None
+    if world == 1:
+        h2d = host_input_rate(p, seq, host_scans, imus, warmup, args.steps, dev)
+    cpu, ate_cpu = None, None
+    if cpu_on:
+        cpu, traj_cpu = cpu_baseline(args, p, seq, host_scans)
+        lo, hi = warmup, min(total, traj_cpu.shape[0], traj_gpu.shape[0])
+        if hi > lo:
+            d = np.linalg.norm(traj_cpu[lo:hi, 10:13] - traj_gpu[lo:hi, 10:13], axis=1)
+            ate_cpu = {"ate_m": float("%.3e" % np.sqrt(np.mean(d ** 2))), "max_m": float("%.3e" % d.max()),
+                       "scans": hi - lo, "reference": "CPU restatement, 5 threads, same scans",
+                       "tolerance_m": 0.01}
+    targets = {cfg: target_workload(args, cfg, sc, warmup, dev) for cfg, sc in tgt_scans.items()}
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "scans/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 4), "higher_is_better": True,
-            "scaling": "strong" if tile else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "warmup": warmup, "warmup_requested": args.warmup, "ms_per_step": round(dt * 1e3 / args.steps, 4),
+            "higher_is_better": True, "scaling": "strong" if tile else "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
             "config": {"workload": "synthetic-%s@%s.yaml" % (args.lidar, args.config), "lidar": args.lidar,
+                       "rays_per_scan": int(synth.LIDARS[args.lidar][0] * synth.LIDARS[args.lidar][1]),
                        "points_per_scan": npts, "downsampled_per_scan": int(np.mean([s["n_ds"] for s in stats])),
                        "factors_per_scan": int(np.mean([s["n_factors"] for s in stats])),
+                       "lm_iters_per_scan": round(float(np.mean([s["ba_iters"] for s in stats])), 2),
                        "parallelism": ("tile-sharded x%d" if tile else "replica x%d") % world},
-            "roofline": roof, "roofline_k_iekf": roof_iekf, "roofline_scan": roof_scan, "host_ms_per_scan": host_ms,
-            "cpu_baseline": cpu, "target_128line": target,
+            "roofline": roof, "roofline_k_ba_solve": roof_solve, "roofline_k_iekf": roof_iekf,
+            "host_ms_per_scan": host_ms, "host_input": h2d, "cpu_baseline": cpu, "ate_vs_cpu": ate_cpu,
+            "target_128line": targets or None,
         }
         print(json.dumps(line))
-    ctx.close()
     if world > 1:
         dist.destroy_process_group()
 
 
-def target_workload(args, p, dev):
+def scan_roofline(stats, stage_stats, W, t_scan):
+    """Whole-scan algorithmic bytes per timed scan / its wall time:
+    B = 16 N_raw + 16 N_ds + sum_k (12 N_raw + 4 N_raw + 112 P_k) + 12 N_ds
+        + 2 V_ins 440 + V_slide (80 W + 80) + (I_H + I_R) F (80 W + 176).
+    Every counter is the timed scan's own (I_H = Hessian passes, I_R = LM
+    iterations), except P_k, which is counted only in the per-stage pass
+    (distinct plane records per IEKF iteration) and enters as that pass's mean
+    per executed iteration."""
+    it_n = sum(s["iekf_iters"] for s in stage_stats)
+    p_mean = sum(sum(s["iekf_planes"][: s["iekf_iters"]]) for s in stage_stats) / it_n if it_n else 0.0
+    b = 0.0
+    for s in stats:
+        b += 16.0 * s["n_raw"] + 16.0 * s["n_ds"]
+        b += s["iekf_iters"] * (16.0 * s["n_raw"] + 112.0 * p_mean)
+        b += 12.0 * s["n_ds"] + 2.0 * s["v_ins"] * 440.0
+        b += s["n_slide"] * (W * 80.0 + 80.0)
+        b += (s["ba_hess"] + s["ba_iters"]) * s["n_factors"] * (W * 80.0 + 176.0)
+    b /= max(len(stats), 1)
+    gbps = b / t_scan / 1e9 if t_scan > 0 else 0.0
+    mean = lambda k: round(float(np.mean([s[k] for s in stats])), 1)  # noqa: E731
+    return {"kernel": "whole scan (every kernel of the per-scan path)", "bound": "hbm", "achieved": round(gbps, 2),
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 6), "traffic": None,
+            "bytes_per_scan": int(b), "scan_us": round(t_scan * 1e6, 2),
+            "counters_mean": {"N_raw": mean("n_raw"), "N_ds": mean("n_ds"), "K": mean("iekf_iters"),
+                              "P_k": round(p_mean, 1), "V_ins": mean("v_ins"), "V_slide": mean("n_slide"),
+                              "F": mean("n_factors"), "I_H": mean("ba_hess"), "I_R": mean("ba_iters")},
+            "note": "SURVEY 8(d) algorithmic bytes per scan / ms_per_step; P_k from the per-stage pass"}
+
+
+def host_input_rate(p, seq, host_scans, imus, warmup, steps, dev):
+    """The same protocol through vg_step with host buffers (the scan's H2D copy
+    inside the timed region, as a src/pipeline caller would pay it)."""
+    import torch
+
+    import vgconfig
+    import vgpu
+    n = min(warmup + steps, len(host_scans))
+    ctx = vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=max(h[0].shape[0] for h in host_scans) + 16)
+    ctx.seed(seq.gt_state(0))
+    xs = [np.ascontiguousarray(h[0]) for h in host_scans[:n]]
+    its = [np.ascontiguousarray(h[1]) for h in host_scans[:n]]
+    for k in range(warmup):
+        ctx.step(xs[k], its[k], host_scans[k][2], host_scans[k][3], imus[k])
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(warmup, n):
+        ctx.step(xs[k], its[k], host_scans[k][2], host_scans[k][3], imus[k])
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    ctx.stats_log()
+    ctx.close()
+    k = n - warmup
+    return {"value": round(k / dt, 3), "unit": "scans/s", "ms_per_step": round(dt * 1e3 / k, 4), "steps": k,
+            "note": "vg_step: host xyz (AoS) + intensity, SoA conversion and H2D copy inside the timed region"}
+
+
+def target_workload(args, cfg, host, warm, dev):
     """The north star's target workload (synthetic 128-line clouds, 200,064
     rays) on one GPU, same pipeline and protocol as the metric, fewer scans:
     reported beside the metric, never as `value`."""
@@ -222,21 +307,20 @@ def target_workload(args, p, dev):
     import synth
     import vgconfig
     import vgpu
+    p = vgconfig.load(cfg)
     g = p["General"]
     seq = synth.Sequence("128line", args.seq, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
-    warm, steps = args.warmup, args.target_steps
-    scans, imus = [], []
-    for k in range(warm + steps):
-        xyz, inten, b, e = seq.scan(k)
+    steps = len(host) - warm
+    scans = []
+    for xyz, inten, b, e, _ in host:
         t = torch.from_numpy(np.ascontiguousarray(np.concatenate([xyz.T, inten[None]], 0))).to(dev)
         scans.append((t, xyz.shape[0], b, e))
-        imus.append(seq.imu(k))
     ctx = vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=max(s[1] for s in scans) + 16)
     ctx.seed(seq.gt_state(0))
 
     def run(k):
         t, n, b, e = scans[k]
-        ctx.step_dev(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), n, b, e, imus[k])
+        ctx.step_dev(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), n, b, e, host[k][4])
 
     for k in range(warm):
         run(k)
@@ -248,11 +332,12 @@ def target_workload(args, p, dev):
     dt = time.perf_counter() - t0
     st = ctx.stats_log()[warm:]
     ctx.close()
-    return {"workload": "synthetic-128line@%s.yaml" % args.config, "value": round(steps / dt, 3), "unit": "scans/s",
-            "ms_per_step": round(dt * 1e3 / steps, 4), "steps": steps, "warmup": warm,
+    return {"workload": "synthetic-128line@%s.yaml" % cfg, "value": round(steps / dt, 3), "unit": "scans/s",
+            "ms_per_step": round(dt * 1e3 / steps, 4), "steps": steps, "warmup": warm, "rays_per_scan": 200064,
             "points_per_scan": int(np.mean([s[1] for s in scans[warm:]])),
             "downsampled_per_scan": int(np.mean([x["n_ds"] for x in st])) if st else None,
-            "factors_per_scan": int(np.mean([x["n_factors"] for x in st])) if st else None}
+            "factors_per_scan": int(np.mean([x["n_factors"] for x in st])) if st else None,
+            "lm": bool(p["General"]["if_BA"])}
 
 
 def pmc_traffic():
@@ -280,27 +365,60 @@ def aggregate(dt, steps, world, dev):
     return world * steps / dt, dt
 
 
-def cpu_baseline(args, p, seq):
-    """Time the CPU restatement (oracle) on a bounded sample of the same sequence."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(args, p, seq, host_scans):
+    """Time the CPU restatement (oracle) on a bounded sample of the same
+    sequence: 5 std::threads for the map/BA fan-outs as the reference
+    (thread_num, optimizers.cpp:184), IEKF single-threaded, the dead VNC prep
+    included (the reference pays it); and the same with one thread. Per scan
+    steady_clock; median and p90 over the scans after the warm-up."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # test infrastructure: the baseline leg only
     import vgconfig
 
     oracle.build()
-    pl = oracle.Pipeline(vgconfig.to_c(p, use_threads=1, vnc_prep=1))
-    pl.seed(seq.gt_state(0))
-    warm = min(args.warmup, 12)
-    times = []
-    for k in range(warm + args.cpu_scans):
-        xyz, it, b, e = seq.scan(k)
-        tm = pl.step(xyz, it, b, e, seq.imu(k))
-        if k >= warm:
-            times.append(tm[6])
-    tot = float(np.sum(times))
-    return {"value": round(len(times) / tot, 3), "unit": "scans/s", "cores": 5, "kind": "port",
-            "sample": "%d scans after %d warm-up scans of the same synthetic %s sequence, %s.yaml; "
-                      "IEKF single-threaded, map/BA 5 std::threads as the reference; median %.1f ms/scan"
-                      % (len(times), warm, args.lidar, args.config, 1e3 * float(np.median(times)))}
+    warm, n = args.cpu_warmup, args.cpu_warmup + args.cpu_scans
+    out, traj5 = {}, None
+    for threads in (5, 1):
+        pl = oracle.Pipeline(vgconfig.to_c(p, use_threads=1 if threads > 1 else 0, vnc_prep=1))
+        pl.seed(seq.gt_state(0))
+        tms, stages = [], []
+        for k in range(n):
+            xyz, it, b, e, imu = host_scans[k]
+            tm = pl.step(xyz, it, b, e, imu)
+            if k >= warm:
+                tms.append(tm[6])
+                stages.append(tm[:6])
+        if threads == 5:
+            traj5 = pl.trajectory()
+        pl.close()
+        tms = np.array(tms)
+        st = np.median(np.array(stages), axis=0) * 1e3
+        out[threads] = {"value": round(len(tms) / float(np.sum(tms)), 3), "median_ms": round(1e3 * np.median(tms), 2),
+                        "p90_ms": round(1e3 * np.percentile(tms, 90), 2),
+                        "stage_median_ms": {k: round(float(v), 2) for k, v in zip(
+                            ("prep_downsample", "iekf", "insert", "recut", "ba", "margi"), st)}}
+    r = out[5]
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return ({"value": r["value"], "unit": "scans/s", "cores": 5, "kind": "port",
+             "sample": "%d scans after %d warm-up scans of the same synthetic %s sequence, %s.yaml; IEKF "
+                       "single-threaded, map/BA fan-outs on 5 std::threads as the reference, VNC prep included"
+                       % (n - warm, warm, args.lidar, args.config),
+             "median_ms": r["median_ms"], "p90_ms": r["p90_ms"], "stage_median_ms": r["stage_median_ms"],
+             "one_thread": dict(out[1], cores=1), "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+             "cpus_available": avail}, traj5)
 
 
 if __name__ == "__main__":

@@ -54,6 +54,14 @@ typedef struct vg_config {
   int thread_num;                   /* LocalBA.thread_num: only its semantic quirks (voxel_map.cpp:96-97, local_mapping.cpp:27,93) */
   int if_BA;                        /* General.if_BA (default 0, node.cpp:96) */
   int reserved0, reserved1, reserved2;
+  /* IMUEKF::scale_gravity / imupre_scale_gravity (ekf_imu.hpp:27,
+   * imu_preintegration.cpp:3): every accelerometer sample is multiplied by it
+   * in the propagation (imu_ekf.cpp:51) and the preintegration
+   * (imu_preintegration.cpp:51). 1 for IMUs reporting m/s^2; the reference
+   * sets G_m_s2 = 9.8 when the static mean |acc| < 2 (IMU in g, e.g. Livox
+   * Mid-360; imu_ekf.cpp:182-185, node.cpp:309). vg_imu_init derives it the
+   * same way. 0 is read as 1. */
+  double scale_gravity;
 } vg_config;
 
 /* Capacities of the device-resident map (HBM). Zero fields take defaults. */
@@ -68,7 +76,15 @@ typedef struct vg_capacity {
 typedef struct vg_stats {
   int n_raw, n_ds, iekf_iters, iekf_matches[4];
   int roots_new, n_slide, n_factors, ba_iters, degenerate;
-  int nodes_used, fix_used, pad0, pad1;
+  int nodes_used, fix_used;
+  int plane_updates; /* margi: OctoTree::plane_update calls this scan (octree.cpp:441-446) */
+  int fix_full;      /* margi: leaves past max_points, pcr_fix.N >= max_points (octree.cpp:461-469) */
+  /* SURVEY 8(d) byte-model inputs: distinct plane records read per IEKF
+   * iteration (P_k; counted in vg_profile's per-stage pass only, else 0),
+   * leaves the insert touched (V_ins), LM Hessian passes (I_H) */
+  int iekf_planes[4];
+  int v_ins;
+  int ba_hess;
 } vg_stats;
 
 typedef struct vg_ctx vg_ctx;

@@ -209,7 +209,9 @@ void OctoTree::margi(int win_count, int mgsize, const std::vector<IMUST>& x_buf,
       if (pcr_add.N - last_num >= 5 || last_num <= 10) {
         plane_update();
         last_num = pcr_add.N;
+        mpar->cnt_plane_update++;
       }
+    if (pcr_fix.N >= mpar->max_points) mpar->cnt_fix_full++;
     if (pcr_fix.N < mpar->max_points) {
       for (int i = 0; i < mgsize; i++)
         if (pcrs_world[i].N != 0) {

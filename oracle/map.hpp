@@ -8,6 +8,7 @@
 // The reference's process-wide globals (octree.cpp:67-75, optimizers.cpp:8,
 // imu_preintegration.cpp:3-5) live in one MapParams object per pipeline.
 #pragma once
+#include <atomic>
 #include <mutex>
 #include <vector>
 #include "core.hpp"
@@ -29,6 +30,10 @@ struct MapParams {
   int shard_rank = 0, shard_world = 1;
   int (*allreduce)(double* buf, int n, void* user) = nullptr;  // in-place sum over ranks
   void* ar_user = nullptr;
+  // per-scan branch counters of OctoTree::margi (observability for the parity
+  // tests; the reference keeps none): plane_update calls (octree.cpp:441-446)
+  // and leaves past max_points (octree.cpp:461-469)
+  std::atomic<int> cnt_plane_update{0}, cnt_fix_full{0};
 };
 
 // owner rank of the 16^3-root-voxel tile of a root key (the product's

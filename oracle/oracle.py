@@ -18,7 +18,8 @@ STATE_LEN = 250
 class Stats(ctypes.Structure):
     _fields_ = [("n_raw", ctypes.c_int), ("n_ds", ctypes.c_int), ("iekf_iters", ctypes.c_int),
                 ("iekf_matches", ctypes.c_int * 4), ("roots_new", ctypes.c_int), ("n_slide", ctypes.c_int),
-                ("n_factors", ctypes.c_int), ("ba_iters", ctypes.c_int), ("degenerate", ctypes.c_int)]
+                ("n_factors", ctypes.c_int), ("ba_iters", ctypes.c_int), ("degenerate", ctypes.c_int),
+                ("plane_updates", ctypes.c_int), ("fix_full", ctypes.c_int)]
 
 
 # int (*)(double* buf, int n, void* user): in-place sum over the ranks

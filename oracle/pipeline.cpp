@@ -163,7 +163,7 @@ struct Pipeline {
     mpar.mp.resize(c.win_size);
     for (int i = 0; i < c.win_size; i++) mpar.mp[i] = i;
     mpar.imu_coef = c.imu_coef;
-    mpar.imupre_scale_gravity = 1.0;
+    mpar.imupre_scale_gravity = c.scale_gravity > 0 ? c.scale_gravity : 1.0;  // node.cpp:309
     mpar.noiseMeas.setZero();
     mpar.noiseWalk.setZero();
     for (int i = 0; i < 3; i++) {  // node.cpp:262-265
@@ -221,7 +221,7 @@ struct Pipeline {
         acc_avr[j] = 0.5 * (head.acc[j] + tail.acc[j]);
       }
       angvel_avr -= xc.bg;
-      acc_avr = acc_avr * 1.0 - xc.ba;  // scale_gravity = 1 (m/s^2 input)
+      acc_avr = acc_avr * mpar.imupre_scale_gravity - xc.ba;  // imu_ekf.cpp:51 (scale_gravity)
       acc_imu = R_imu * acc_avr + xc.g;
       double cur_time = head.t;
       if (cur_time < last_pcl_end_time) cur_time = last_pcl_end_time;
@@ -564,7 +564,11 @@ struct Pipeline {
       x_curr.R = x_buf[win_count - 1].R;
       x_curr.p = x_buf[win_count - 1].p;
       t5 = clk::now();
+      mpar.cnt_plane_update = 0;
+      mpar.cnt_fix_full = 0;
       multi_margi();
+      st.plane_updates = mpar.cnt_plane_update;
+      st.fix_full = mpar.cnt_fix_full;
       t6 = clk::now();
       const int mgsize = 1;
       if ((win_base + win_count) % 10 == 0) {

@@ -32,11 +32,14 @@ typedef struct orc_config {
   int use_threads;                /* oracle only: spawn real std::threads */
   int vnc_prep;                   /* oracle only: run the dead VNC prep (cost fidelity) */
   int pad;
+  double scale_gravity;           /* IMUEKF::scale_gravity = imupre_scale_gravity (imu_ekf.cpp:51,
+                                     imu_preintegration.cpp:51); 0 is read as 1 */
 } orc_config;
 
 typedef struct orc_stats {
   int n_raw, n_ds, iekf_iters, iekf_matches[4];
   int roots_new, n_slide, n_factors, ba_iters, degenerate;
+  int plane_updates, fix_full; /* margi branch counters (octree.cpp:441-446, 461-469) */
 } orc_stats;
 
 void orc_voxel_key_d(const double* xyz, int n, double size, int64_t* out);

@@ -14,7 +14,35 @@ def test_header_symbols_exported():
     assert not missing, missing
 
 
-def test_config_struct_layout_matches_header():
+def _c_layout(tmp_path, struct, fields):
+    """sizeof / offsetof of a header struct, from a C compiler (gcc)."""
+    import os
+    import subprocess
+    inc = os.path.join(os.path.dirname(vgpu.HEADER))
+    body = "".join('printf("%%zu\\n", offsetof(%s, %s));' % (struct, f) for f in fields)
+    src = tmp_path / "lay.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "vina_gpu.h"\n'
+                   'int main(void){printf("%%zu\\n", sizeof(%s));%s return 0;}\n' % (struct, body))
+    exe = tmp_path / "lay"
+    subprocess.check_call(["gcc", "-I", inc, "-o", str(exe), str(src)])
+    out = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    return out[0], out[1:]
+
+
+def test_config_struct_layout_matches_header(tmp_path):
+    """vgconfig.CConfig (the Python binding, also the oracle's orc_config) is
+    field-for-field vg_config: same size and offsets (the oracle-only ints sit
+    in vg_config's reserved slots)."""
     from vgconfig import CConfig
-    # 9 doubles + 4 + 4 + 8 scalars + 4 + 4 ... computed from the header field list
-    assert ctypes.sizeof(CConfig) == 8 * (3 + 4 + 4 + 2 + 1 + 4 + 4 + 9 + 3) + 4 * 8
+    names = [f for f, _ in CConfig._fields_]
+    hdr = {"use_threads": "reserved0", "vnc_prep": "reserved1", "pad": "reserved2"}
+    size, offs = _c_layout(tmp_path, "vg_config", [hdr.get(f, f).split("[")[0] for f in names])
+    assert ctypes.sizeof(CConfig) == size
+    assert [getattr(CConfig, f).offset for f in names] == offs
+
+
+def test_stats_struct_layout_matches_header(tmp_path):
+    names = [f for f, _ in vgpu.Stats._fields_]
+    size, offs = _c_layout(tmp_path, "vg_stats", names)
+    assert ctypes.sizeof(vgpu.Stats) == size
+    assert [getattr(vgpu.Stats, f).offset for f in names] == offs

@@ -39,7 +39,9 @@ constexpr int kImuRec = kBaImuRec;  // preintegration record + cov_inv
 struct BaState {             // device-resident LM state
   double u, v, res1, res2, q1;
   int calc_hess, done, iters, seq;  // seq: the next LM publication number (k_ba_control)
+  int nhess;                        // Hessian passes executed (I_H, SURVEY 8(d) byte model)
 };
+static_assert(sizeof(BaState) <= 8 * sizeof(double), "BaState is carved as 8 doubles");
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
@@ -942,6 +944,7 @@ __global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, do
   if (threadIdx.x == 0) {
     accept = -1;
     if (!st->done) {
+      if (st->calc_hess) st->nhess += 1;
       if (st->calc_hess) {  // residual1 of divide_thread at the current state
         double r = 0.0;
         for (int k = 0; k < nimu; k++) r += imuout[(size_t)k * 931 + 930];
@@ -1013,6 +1016,7 @@ __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict
     st->calc_hess = 1;
     st->done = (rc_status && *rc_status) ? 1 : 0;  // an asynchronous recut that needs the host: skip
     st->iters = 0;
+    st->nhess = 0;
     st->seq = seq0;
   }
 }
@@ -1127,6 +1131,7 @@ static BaDev carve(vg_ctx* ctx) {
 }
 
 const int* ba_iters_dev(vg_ctx* ctx) { return &carve(ctx).st->iters; }
+const int* ba_hess_dev(vg_ctx* ctx) { return &carve(ctx).st->nhess; }
 
 // Run damping_iter on the device state. imurec: (W-1) x kImuRec host records
 // (pinned staging, uploaded asynchronously). The window states and the IMU

@@ -59,6 +59,7 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(m.wp_var = ctx->arena.take<double>(cw * W * 9));
   good &= ok(m.wp_leaf = ctx->arena.take<int>(cw * W));
   good &= ok(m.counters = ctx->arena.take<int>(kCntN));
+  good &= ok(m.stamp = ctx->arena.take<int>(cn));
   Work& w = ctx->wk;
   w.cap = (int)(cw * (W + 1));
   good &= ok(w.k0 = ctx->arena.take<uint64_t>(w.cap));
@@ -107,6 +108,7 @@ int map_reset(vg_ctx* ctx) {
   VG_HIP(hipMemsetAsync(m.hval, 0xff, hs * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.hfirst, 0x7f, hs * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.counters, 0, kCntN * sizeof(int), s));
+  VG_HIP(hipMemsetAsync(m.stamp, 0, (size_t)m.cap_nodes * sizeof(int), s));
   VG_HIP(hipMemsetAsync(ctx->wk.cand_bits, 0, (ctx->cap.max_nodes / 32 + 1) * sizeof(uint32_t), s));
   VG_HIP(hipMemsetAsync(m.in_slide, 0, m.cap_nodes, s));
   VG_HIP(hipMemsetAsync(m.leaf_cnt, 0, (size_t)m.cap_nodes * sizeof(int), s));
@@ -193,8 +195,9 @@ __device__ __forceinline__ bool inside(const NodeHdr& h, const V3& w) {
 // no-op once the IEKF has finished (st->done). Iteration 0 ignores the leaf
 // cache (no association yet, odometry.cpp:111-132).
 __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, int it, DevMap m,
-                                              int* __restrict__ cache, double* __restrict__ partials) {
+                                              int* __restrict__ cache, double* __restrict__ partials, int tag) {
   if (st->done) return;
+  int nplanes = 0;  // distinct plane records read by this iteration (tag != 0: the profiling pass only)
   const int n = st->sn;
   const float* __restrict__ x = st->sx;
   const float* __restrict__ y = st->sy;
@@ -242,6 +245,7 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
     if (!flag && it == 0) cache[i] = -1;  // the reference's fresh per-scan association
     if (flag) {
       cache[i] = leaf;
+      if (tag && m.stamp[leaf] != tag && atomicExch(&m.stamp[leaf], tag) != tag) nplanes++;
       const PlaneRec& P = m.pl[leaf];
       V3 nn = ld_v3(P.normal), c = ld_v3(P.center);
       double R_inv = 1.0 / (0.0005 + sigma);
@@ -263,6 +267,7 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
       acc[33] += 1.0;
     }
   }
+  if (tag) wave_append(&st->planes[it], nplanes);
   // block reduction: wave shuffles then LDS across the 4 waves (fixed tree)
   __shared__ double red[4][kIekfVals];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -307,7 +312,7 @@ static int iekf_blocks(vg_ctx* ctx) {
 // one IEKF iteration: the point loop (block partials) and the update; the
 // optional event pair brackets k_iekf alone (vg_profile)
 int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
-                   hipEvent_t ev0, hipEvent_t ev1) {
+                   hipEvent_t ev0, hipEvent_t ev1, int tag) {
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
   (void)x;
@@ -316,7 +321,7 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
   (void)n;  // the scan is read from the device state (state_set_scan)
   const int nb = iekf_blocks(ctx);
   if (ev0) VG_HIP(hipEventRecord(ev0, s));
-  k_iekf<<<nb, 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials);
+  k_iekf<<<nb, 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials, tag);
   if (ev1) VG_HIP(hipEventRecord(ev1, s));
   if (ctx->shard.world > 1) {  // this shard's sums, all-reduced, then the (replicated) update
     double* sums = ctx->shard.d_buf;
@@ -342,7 +347,8 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
   auto enqueue = [&]() -> int {
     for (int it = 0; it < 4; it++)
       VG_TRY(iekf_iteration(ctx, mp, x, y, z, n, it, ev ? ctx->iekf_ev[bank + it][0] : nullptr,
-                            ev ? ctx->iekf_ev[bank + it][1] : nullptr));
+                            ev ? ctx->iekf_ev[bank + it][1] : nullptr,
+                            graph || !ctx->prof_stages ? 0 : ++ctx->plane_tag));
     return VG_OK;
   };
   if (!graph) return enqueue();
@@ -382,6 +388,8 @@ __global__ void __launch_bounds__(256) k_ins_prep(int n, const float* __restrict
     m.counters[kCntCreate] = 0;
     m.counters[kCntSeg] = 0;
     m.counters[kCntMisc] = 0;  // insert abort flag (child-allocation overflow)
+    m.counters[kCntPlaneUpd] = 0;  // margi's per-scan branch counters (vg_stats)
+    m.counters[kCntFixFull] = 0;
   }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     V3 pnt;
@@ -1854,6 +1862,7 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
                                                     const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
                                                     int* __restrict__ plan) {
   const int nl = *nleaves;
+  int n_pu = 0, n_full = 0;  // plane_update calls / leaves past max_points (per-scan counters)
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nl; q += gridDim.x * blockDim.x) {
     int node = leaves[q];
     NodeHdr& h = m.hdr[node];
@@ -1900,7 +1909,9 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
       if (add_.N - h.last_num >= 5 || h.last_num <= 10) {
         plane_update_dev(m, node, add_, e);
         h.last_num = add_.N;
+        n_pu++;
       }
+    if (fix_.N >= mp.max_points) n_full++;
     if (fix_.N < mp.max_points) {
       if (w0.N != 0) {
         clu_add(fix_, w0);
@@ -1934,6 +1945,8 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
     m.pcr_add[node] = add_;
     h.isexist = (fix_.N >= add_.N) ? 0 : 1;
   }
+  wave_append(&m.counters[kCntPlaneUpd], n_pu);
+  wave_append(&m.counters[kCntFixFull], n_full);
 }
 
 // the point_fix copies planned by k_margi_leaf, one wave per leaf: the live

@@ -57,6 +57,9 @@ struct Imu {
   double gyr[3], acc[3];
 };
 
+// IMUEKF::scale_gravity = imupre_scale_gravity (vg_config; 0 reads as 1)
+static inline double gravity_scale(const vg_config& c) { return c.scale_gravity > 0 ? c.scale_gravity : 1.0; }
+
 // IMU_PRE host part (preintegration.hpp:12-51)
 struct HImuPre {
   M3 R_delta = M3::I(), R_bg = M3::Z(), p_bg = M3::Z(), p_ba = M3::Z(), v_bg = M3::Z(), v_ba = M3::Z();
@@ -105,7 +108,8 @@ struct HImuPre {
     }
     R_delta = mul(R_delta, rinc);
   }
-  void push_imu(const std::vector<Imu>& buf, const M6& nm, const M6& nw) {  // imu_preintegration.cpp:31-55
+  // imu_preintegration.cpp:31-55; sg = imupre_scale_gravity (line 51)
+  void push_imu(const std::vector<Imu>& buf, const M6& nm, const M6& nw, double sg) {
     for (size_t k = 1; k < buf.size(); k++) {
       const Imu& a = buf[k - 1];
       const Imu& b = buf[k];
@@ -113,7 +117,7 @@ struct HImuPre {
       V3 gyr, acc;
       for (int j = 0; j < 3; j++) {
         gyr[j] = 0.5 * (a.gyr[j] + b.gyr[j]) - bg[j];
-        acc[j] = 0.5 * (a.acc[j] + b.acc[j]) * 1.0 - ba[j];
+        acc[j] = 0.5 * (a.acc[j] + b.acc[j]) * sg - ba[j];
       }
       add_imu(gyr, acc, dt, nm, nw);
     }
@@ -272,6 +276,8 @@ static int absorb_p1(vg_ctx* ctx, HostPipe* P, Pend& q) {
   for (int i = 0; i < 4; i++) q.st.iekf_matches[i] = pb.matches[i];
   q.st.degenerate = degenerate_of(pb.nnt);
   q.st.ba_iters = pb.ba_iters1;
+  q.st.ba_hess = pb.ba_hess1;
+  for (int i = 0; i < 4; i++) q.st.iekf_planes[i] = pb.planes[i];
   if (q.jour_check) {  // local_mapping.cpp:525-533 with x_curr.p = x_buf.back().p after the BA
     double spat = norm3(sub(xc.p, P->last_pos));
     if (spat > 0.5) {
@@ -303,6 +309,9 @@ static int absorb_p2(vg_ctx* ctx, HostPipe* P, Pend& q) {
   q.st.nodes_used = c[kCntNodes];
   q.st.fix_used = c[kCntFix];
   q.st.roots_new = c[kCntRoots];
+  q.st.plane_updates = c[kCntPlaneUpd];
+  q.st.fix_full = c[kCntFixFull];
+  q.st.v_ins = c[kCntSeg];
   // events recorded while this scan was enqueued are complete now
   collect_iekf_events(ctx, q);
   for (int i = 0; i < kProfN; i++)
@@ -367,7 +376,7 @@ static void propagate(vg_ctx* ctx, HostPipe* P, const std::vector<Imu>& imus, do
       acc_avr[j] = 0.5 * (head.acc[j] + tail.acc[j]);
     }
     angvel = sub(angvel, xc.bg);
-    acc_avr = sub(scl(acc_avr, 1.0), xc.ba);
+    acc_avr = sub(scl(acc_avr, gravity_scale(c)), xc.ba);  // imu_ekf.cpp:51
     acc_imu = add(mul(R_imu, acc_avr), xc.g);
     double cur = head.t;
     if (cur < P->last_pcl_end_time) cur = P->last_pcl_end_time;
@@ -598,7 +607,7 @@ int stage_window_push(vg_ctx* ctx, const double* imu, int m) {
   if (P->win_count > 1) {
     const HX& xb = P->x_buf[P->win_count - 2];
     P->imu_pre.emplace_back(xb.bg, xb.ba);
-    P->imu_pre.back().push_imu(to_imus(imu, m), P->noiseMeas, P->noiseWalk);
+    P->imu_pre.back().push_imu(to_imus(imu, m), P->noiseMeas, P->noiseWalk, gravity_scale(ctx->cfg));
     P->imu_pre.back().rec.resize(kBaImuRec);
     P->imu_pre.back().record(P->imu_pre.back().rec.data());  // off the BA's critical path
     new_imu = P->win_count - 2;

@@ -56,6 +56,7 @@ __global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict
     st->degenerate = 0;
     st->ticket = 0;
     for (int k = 0; k < 4; k++) st->matches[k] = 0;
+    for (int k = 0; k < 4; k++) st->planes[k] = 0;
   }
 }
 
@@ -138,7 +139,8 @@ __global__ void k_slide_state(DState* __restrict__ st, int win_count, int nimu) 
 
 // P1: x_curr, the post-IEKF pose, window states, IEKF / BA summary
 __global__ void k_publish_state(const DState* __restrict__ st, int win_count, int ba_iters_valid,
-                                const int* __restrict__ ba_iters, Pub* __restrict__ pub, int seq) {
+                                const int* __restrict__ ba_iters, const int* __restrict__ ba_hess,
+                                Pub* __restrict__ pub, int seq) {
   const int t = threadIdx.x;
   for (int e = t; e < kXC; e += blockDim.x) pub_store(&pub->xc[e], st->xc[e]);
   for (int e = t; e < 12; e += blockDim.x) pub_store(&pub->traj[e], st->traj[e]);
@@ -148,6 +150,8 @@ __global__ void k_publish_state(const DState* __restrict__ st, int win_count, in
     pub_store(&pub->iekf_iters, st->iters);
     for (int k = 0; k < 4; k++) pub_store(&pub->matches[k], st->matches[k]);
     pub_store(&pub->ba_iters1, ba_iters_valid ? *ba_iters : 0);
+    pub_store(&pub->ba_hess1, ba_iters_valid ? *ba_hess : 0);
+    for (int k = 0; k < 4; k++) pub_store(&pub->planes[k], st->planes[k]);
   }
   __syncthreads();
   if (t == 0) pub_flag(&pub->seq1, seq);
@@ -282,8 +286,8 @@ int state_slide(vg_ctx* ctx, int win_count, int nimu) {
 }
 
 int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq) {
-  k_publish_state<<<1, 256, 0, ctx->stream>>>(ctx->st, win_count, ba_iters_dev != nullptr, ba_iters_dev, ctx->d_pub,
-                                              seq);
+  k_publish_state<<<1, 256, 0, ctx->stream>>>(ctx->st, win_count, ba_iters_dev != nullptr, ba_iters_dev,
+                                              ba_iters_dev ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, seq);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }

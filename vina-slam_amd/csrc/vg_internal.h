@@ -137,12 +137,14 @@ struct DevMap {
   double* wp_var = nullptr;    // world var (after pvec_update), packed 6
   int* wp_leaf = nullptr;      // leaf holding the point in its list, -1 = not listed
   int* counters = nullptr;     // device counters (see kCnt*)
+  int* stamp = nullptr;        // per-node tag of the last IEKF iteration that read its plane (P_k, profiling pass)
 };
 enum {
   kCntNodes = 0, kCntFix = 1, kCntSlide = 2, kCntNew = 3, kCntTouched = 4, kCntWork = 5, kCntNext = 6,
   kCntSub = 7, kCntEvents = 8, kCntFactors = 9, kCntCreate = 10, kCntErr = 11, kCntLeaves = 12, kCntMisc = 13, kCntSeg = 14, kCntRoots = 15,
   kCntGTouched = 16, kCntGSlide = 17,  // all-reduced copies (sharded mode) for the thread_num quirks
-  kCntN = 18
+  kCntPlaneUpd = 18, kCntFixFull = 19,  // margi: plane_update calls, leaves with pcr_fix.N >= max_points
+  kCntN = 20
 };
 
 // per-scan work buffers
@@ -197,7 +199,7 @@ struct DState {
   double traj[16];                  // R, p right after the IEKF (pub_localtraj, local_mapping.cpp:427)
   double xs[kMaxWin * kXS];         // window states x_buf by ord (local_mapping.cpp:434)
   double bias[kMaxWin * 12];        // IMU_PRE bias state per window factor: dbg, dba, dbg_buf, dba_buf
-  int it, rematch, done, iters, degenerate, matches[4], ticket, pad[6];
+  int it, rematch, done, iters, degenerate, matches[4], ticket, planes[4], pad[2];  // planes: P_k (profiling pass)
   // the scan this IEKF reads (set by k_scan_begin's caller, so the IEKF
   // launches are the same every scan and replay as one hipGraph)
   const float *sx, *sy, *sz;
@@ -229,7 +231,7 @@ struct Pub {
   int seq_ds, n_ds, ds_err, pad0;          // downsample (after k_ds_*)
   int seq_ba, ba_done, ba_iters, pad1;     // LM iteration flags (k_ba_control)
   int seq_rc, rc_status, rc_nf, pad5;      // asynchronous recut status (k_fac_sort)
-  int seq1, iekf_iters, degenerate, matches[4], ba_iters1, pad2[4];  // P1: state after IEKF/BA
+  int seq1, iekf_iters, degenerate, matches[4], ba_iters1, ba_hess1, planes[4], pad2[3];  // P1: state after IEKF/BA
   int seq2, pad3[3];
   int counters[kCntN];                      // P2: map counters at the end of the scan
   double xc[256];
@@ -284,6 +286,7 @@ struct vg_ctx {
   double* h_stage = nullptr;    // pinned staging for asynchronous H2D copies (kStageBytes)
   double* d_deskew = nullptr;   // deskew parameters (x_curr pose, extrinsic, IMU poses)
   int pub_seq = 0;
+  int plane_tag = 0;        // IEKF iteration tag of the P_k count (vg_profile stages)
   int* h_pinned = nullptr;  // small pinned host scratch for counters
 
   vg_stats stats;
@@ -420,7 +423,7 @@ int ds_enqueue(vg_ctx* ctx, hipStream_t s, const float* x, const float* y, const
 int map_alloc(vg_ctx* ctx);
 int map_reset(vg_ctx* ctx);
 int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
-                   hipEvent_t ev0, hipEvent_t ev1);
+                   hipEvent_t ev0, hipEvent_t ev1, int tag = 0);
 // all four iterations; replays the captured graph when possible
 int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank);
 constexpr int kNeedInsertReplay = 1;  // map_recut: the insert overflowed k_ins_alloc, replay it first
@@ -456,6 +459,7 @@ int ba_alloc(vg_ctx* ctx);
 int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
            const std::function<int()>& before_first_wait = nullptr);
 const int* ba_iters_dev(vg_ctx* ctx);
+const int* ba_hess_dev(vg_ctx* ctx);  // Hessian passes of the last LM run (I_H of SURVEY 8(d))
 // pipeline.cpp
 void host_init(vg_ctx* ctx);
 void host_free(vg_ctx* ctx);

@@ -130,7 +130,7 @@ class Sequence:
     """A synthetic LiDAR-inertial sequence. scan(k) covers (t_k - 0.1, t_k]."""
 
     def __init__(self, lidar="64line", seq_id=0, blind=3.0, ext_R=None, ext_t=None, range_sigma=0.02,
-                 bearing_sigma_deg=0.05, gyr_sigma=0.002, acc_sigma=0.02):
+                 bearing_sigma_deg=0.05, gyr_sigma=0.002, acc_sigma=0.02, imu_in_g=False):
         self.L, self.A = LIDARS[lidar]
         self.seed = 0x5EED0000 + seq_id
         rng = np.random.default_rng(self.seed)
@@ -142,6 +142,9 @@ class Sequence:
         self.range_sigma = range_sigma
         self.bearing_sigma = np.deg2rad(bearing_sigma_deg)
         self.gyr_sigma, self.acc_sigma = gyr_sigma, acc_sigma
+        # accelerometer unit: m/s^2, or g (Livox Mid-360's IMU; the reference
+        # then multiplies every sample by scale_gravity = 9.8, imu_ekf.cpp:182-185)
+        self.acc_unit = 9.8 if imu_in_g else 1.0
         self.bg = rng.normal(0, 0.002, 3)
         self.ba = rng.normal(0, 0.02, 3)
         el = np.deg2rad(np.linspace(-25.0, 15.0, self.L))
@@ -227,7 +230,7 @@ class Sequence:
             nr = np.random.default_rng((self.seed << 22) + j)
             out[i, 0] = t
             out[i, 1:4] = w + self.bg + nr.normal(0, self.gyr_sigma, 3)
-            out[i, 4:7] = f + self.ba + nr.normal(0, self.acc_sigma, 3)
+            out[i, 4:7] = (f + self.ba + nr.normal(0, self.acc_sigma, 3)) / self.acc_unit
         return out
 
     def gt_state(self, k):

@@ -38,8 +38,14 @@ class Stats(ctypes.Structure):
     _fields_ = [("n_raw", ctypes.c_int), ("n_ds", ctypes.c_int), ("iekf_iters", ctypes.c_int),
                 ("iekf_matches", ctypes.c_int * 4), ("roots_new", ctypes.c_int), ("n_slide", ctypes.c_int),
                 ("n_factors", ctypes.c_int), ("ba_iters", ctypes.c_int), ("degenerate", ctypes.c_int),
-                ("nodes_used", ctypes.c_int), ("fix_used", ctypes.c_int), ("pad0", ctypes.c_int),
-                ("pad1", ctypes.c_int)]
+                ("nodes_used", ctypes.c_int), ("fix_used", ctypes.c_int), ("plane_updates", ctypes.c_int),
+                ("fix_full", ctypes.c_int), ("iekf_planes", ctypes.c_int * 4), ("v_ins", ctypes.c_int),
+                ("ba_hess", ctypes.c_int)]
+
+
+def _stats_dict(s):
+    return {k: (list(getattr(s, k)) if k in ("iekf_matches", "iekf_planes") else getattr(s, k))
+            for k, _ in Stats._fields_}
 
 
 # vg_host_allreduce_fn: int (*)(void* buf, int count, int dtype, void* user)
@@ -243,7 +249,7 @@ class Context:
     def stats(self):
         s = Stats()
         self._chk(lib().vg_get_stats(self.h, ctypes.byref(s)), "vg_get_stats")
-        return {k: (list(getattr(s, k)) if k == "iekf_matches" else getattr(s, k)) for k, _ in Stats._fields_}
+        return _stats_dict(s)
 
     def stats_log(self):
         """Counters of every completed scan (drains the stream once)."""
@@ -251,8 +257,7 @@ class Context:
         self._chk(lib().vg_stats_log(self.h, None, 0, ctypes.byref(n)), "vg_stats_log")
         arr = (Stats * max(n.value, 1))()
         self._chk(lib().vg_stats_log(self.h, arr, n.value, ctypes.byref(n)), "vg_stats_log")
-        return [{k: (list(getattr(s, k)) if k == "iekf_matches" else getattr(s, k)) for k, _ in Stats._fields_}
-                for s in arr[: n.value]]
+        return [_stats_dict(s) for s in arr[: n.value]]
 
     def window_states(self):
         out = np.zeros((64, STATE_LEN))
