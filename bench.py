@@ -53,7 +53,9 @@ def parse():
                     help="replica: an independent sequence per GPU (weak scaling); tile: ONE sequence with its "
                          "voxel map sharded by spatial tile over the GPUs, RCCL all-reduce of the normal "
                          "equations (strong scaling)")
-    ap.add_argument("--workers", type=int, default=0, help="scan-generation processes (0: min(16, cpus))")
+    ap.add_argument("--workers", type=int, default=0,
+                    help="scan-generation processes (0: min(16, cpus); 1 under a profiler)")
+    ap.add_argument("--no-h2d", action="store_true", help="skip the host-input (vg_step) rate")
     return ap.parse_args()
 
 
@@ -208,7 +210,7 @@ def main():
     roof["stage_ms_per_scan"] = stage_ms
 
     h2d = None
-    if world == 1:
+    if world == 1 and not args.no_h2d:
         h2d = host_input_rate(p, seq, host_scans, imus, warmup, args.steps, dev)
     cpu, ate_cpu = None, None
     if cpu_on:

@@ -676,7 +676,7 @@ void IMU_PRE::add_imu(V3 cur_gyr, V3 cur_acc, double dt) {
 
 // give_evaluate — imu_preintegration.cpp:97-163
 double IMU_PRE::give_evaluate(const IMUST& st1, const IMUST& st2, Mat<30, 30>& jtj, Mat<30, 1>& gg,
-                              bool jac) const {
+                              bool jac, V15* rr_out, Mat<15, 30>* joc_out) const {
   M15 joca, jocb;
   V15 rr;
   M3 R_correct = R_delta * Exp(R_bg * dbg);
@@ -723,7 +723,9 @@ double IMU_PRE::give_evaluate(const IMUST& st1, const IMUST& st2, Mat<30, 30>& j
     Mat<30, 15> jT = joc.T();
     jtj = (jT * cov_inv) * joc;
     gg = (jT * cov_inv) * rr;
+    if (joc_out) *joc_out = joc;
   }
+  if (rr_out) *rr_out = rr;
   return dot(rr, cov_inv * rr);
 }
 
@@ -771,10 +773,17 @@ double LI_BA_Optimizer::divide_thread(std::vector<IMUST>& xs, LidarFactor& vox, 
   }
   Mat<30, 30> jtj;
   Mat<30, 1> gg;
+  std::vector<double> cap_imu;
   for (int i = 0; i < win_size - 1; i++) {
     jtj.setZero();
     gg.setZero();
-    residual += imus[i]->give_evaluate(xs[i], xs[i + 1], jtj, gg, true);
+    const double ri = imus[i]->give_evaluate(xs[i], xs[i + 1], jtj, gg, true);
+    residual += ri;
+    if (mpar->capture == 1) {  // test hook: this IMU factor's blocks
+      cap_imu.insert(cap_imu.end(), jtj.d, jtj.d + 900);
+      cap_imu.insert(cap_imu.end(), gg.d, gg.d + 30);
+      cap_imu.push_back(ri);
+    }
     for (int r = 0; r < 2 * DIM; r++) {
       JacT[i * DIM + r] += gg[r];
       for (int c = 0; c < 2 * DIM; c++) Hess(i * DIM + r, i * DIM + c) += jtj(r, c);
@@ -785,6 +794,17 @@ double LI_BA_Optimizer::divide_thread(std::vector<IMUST>& xs, LidarFactor& vox, 
   residual *= (mpar->imu_coef * 0.5);
   vox.acc_evaluate2(xs, 0, (int)part, hessians[0], jacobins[0], resis[0]);
   for (auto& t : th) t.join();
+  if (mpar->capture == 1) {  // test hook: the LiDAR part summed over the thread partitions, then the IMU blocks
+    std::vector<double>& c = mpar->captured;
+    c.assign((size_t)jac_leng * jac_leng + jac_leng + 1, 0.0);
+    for (int i = 0; i < tthd_num; i++) {
+      for (size_t e = 0; e < (size_t)jac_leng * jac_leng; e++) c[e] += hessians[i].d[e];
+      for (int e = 0; e < jac_leng; e++) c[(size_t)jac_leng * jac_leng + e] += jacobins[i][e];
+      c.back() += resis[i];
+    }
+    c.insert(c.end(), cap_imu.begin(), cap_imu.end());
+    mpar->capture = 2;
+  }
   if (mpar->shard_world > 1) {  // this shard's LiDAR part, summed over the shards, then added
     std::vector<double> l((size_t)jac_leng * jac_leng + jac_leng + 1, 0.0);
     for (int i = 0; i < tthd_num; i++) {

@@ -34,6 +34,9 @@ struct MapParams {
   // tests; the reference keeps none): plane_update calls (octree.cpp:441-446)
   // and leaves past max_points (octree.cpp:461-469)
   std::atomic<int> cnt_plane_update{0}, cnt_fix_full{0};
+  // test hook (orc_capture_*): the next LM run's first divide_thread pass
+  int capture = 0;  // 1 armed, 2 captured
+  std::vector<double> captured;
 };
 
 // owner rank of the 16^3-root-voxel tile of a root key (the product's
@@ -69,6 +72,16 @@ struct Plane {
   float radius = 0;
   bool is_plane = false;
 };
+
+// Point-to-plane residual and Jacobian of LioStateEstimation's point loop
+// (odometry.cpp:136-142): r = n.(w - c), j = [hat(pnt) R^T n ; n] for the
+// right-perturbed pose (R Exp(dtheta), p + dp)
+inline void p2p_residual_jacobian(const M3& R, const V3& pnt, const V3& wld, const V3& normal, const V3& center,
+                                  double& resi, V6& jac) {
+  resi = dot(normal, wld - center);
+  jac.setBlock(0, 0, (hat(pnt) * R.T()) * normal);
+  jac.setBlock(3, 0, normal);
+}
 
 // Bf_var — octree.cpp:83-92
 inline void Bf_var(const pointVar& pv, M9& bcov, const V3& vec) {
@@ -189,7 +202,8 @@ struct IMU_PRE {
   IMU_PRE(const MapParams* m, const V3& bg1, const V3& ba1);
   void push_imu(const std::vector<ImuSample>& buf);
   void add_imu(V3 gyr, V3 acc, double dt);
-  double give_evaluate(const IMUST& st1, const IMUST& st2, Mat<30, 30>& jtj, Mat<30, 1>& gg, bool jac) const;
+  double give_evaluate(const IMUST& st1, const IMUST& st2, Mat<30, 30>& jtj, Mat<30, 1>& gg, bool jac,
+                       V15* rr_out = nullptr, Mat<15, 30>* joc_out = nullptr) const;
   void update_state(const V15& dxi);
 };
 

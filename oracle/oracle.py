@@ -67,6 +67,12 @@ def lib():
         L.orc_traj_len.argtypes = [P]
         L.orc_get_traj.argtypes = [P, dp]
         L.orc_window_states.argtypes = [P, dp]
+        L.orc_capture_arm.argtypes = [P]
+        L.orc_kat_p2p.argtypes = [dp] * 7
+        L.orc_kat_lidar_factor.argtypes = [ctypes.c_int, dp, dp, dp, dp, dp, dp]
+        L.orc_kat_imu.argtypes = [dp, ctypes.c_int, dp, dp, dp, dp, dp, ctypes.c_double, dp, dp]
+        L.orc_kat_imu.restype = ctypes.c_double
+        L.orc_capture_get.argtypes = [P, dp, ctypes.c_int]
         L.orc_lio_kdtree.argtypes = [P, fp, ctypes.c_int, ip, ip]
         L.orc_kdmap_size.argtypes = [P]
         L.orc_kdmap_get.argtypes = [P, fp]
@@ -149,6 +155,40 @@ def decode_scan(records, fmt):
                               fmt["point_filter_num"], fmt["blind"], fmt.get("omega_l", 3610.0),
                               fmt.get("time_base", 0.0), _f(out), n + 2)
     return out[:m]
+
+
+def _a(x):
+    return np.ascontiguousarray(x, dtype=np.float64)
+
+
+def kat_p2p(R, p, pnt, n, c):
+    """LioStateEstimation's point-to-plane residual and Jacobian (odometry.cpp:136-142)."""
+    r = np.zeros(1)
+    j = np.zeros(6)
+    lib().orc_kat_p2p(_d(_a(R)), _d(_a(p)), _d(_a(pnt)), _d(_a(n)), _d(_a(c)), _d(r), _d(j))
+    return r[0], j
+
+
+def kat_lidar_factor(clusters, fix, poses, hess=True):
+    """One LidarFactor voxel (factors.cpp:11-126): clusters (W, 13) [P9 v3 N],
+    fix (13,), poses (W, 12) [R9 p3] -> (lambda_min, JacT (6W,), Hess (6W, 6W))."""
+    clusters, fix, poses = _a(clusters), _a(fix), _a(poses)
+    W = clusters.shape[0]
+    r = np.zeros(1)
+    j = np.zeros(6 * W)
+    h = np.zeros((6 * W, 6 * W))
+    lib().orc_kat_lidar_factor(W, _d(clusters), _d(fix), _d(poses), _d(r), _d(j), _d(h) if hess else None)
+    return r[0], j, h
+
+
+def kat_imu(imu, bias0, dbias, x1, x2, noise, sg=1.0):
+    """One IMU_PRE factor (imu_preintegration.cpp:31-163): (r^T C r, rr (15,), joc (15, 30))."""
+    imu = _a(imu)
+    rr = np.zeros(15)
+    joc = np.zeros((15, 30))
+    cost = lib().orc_kat_imu(_d(imu), imu.shape[0], _d(_a(bias0)), _d(_a(dbias)), _d(_a(x1)), _d(_a(x2)),
+                             _d(_a(noise)), sg, _d(rr), _d(joc))
+    return cost, rr, joc
 
 
 def ldlt_solve(A, b):
@@ -236,6 +276,17 @@ class Pipeline:
         out = np.zeros((64, STATE_LEN))
         n = lib().orc_window_states(self.h, _d(out))
         return out[:n]
+
+    def capture_arm(self):
+        """Capture the next LM run's first Hessian pass (capture_get)."""
+        lib().orc_capture_arm(self.h)
+
+    def capture_get(self):
+        n = lib().orc_capture_get(self.h, None, 0)
+        out = np.zeros(n)
+        if n:
+            lib().orc_capture_get(self.h, _d(out), n)
+        return out
 
     def lio_kdtree(self, xyz):
         """lio_state_estimation_kdtree on a scan downsampled at

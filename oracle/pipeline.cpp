@@ -354,10 +354,9 @@ struct Pipeline {
         if (flag) {
           Plane& pp = *pla;
           double R_inv = 1.0 / (0.0005 + sigma_d);
-          double resi = dot(pp.normal, wld - pp.center);
+          double resi;
           V6 jac;
-          jac.setBlock(0, 0, (phat * x_curr.R.T()) * pp.normal);
-          jac.setBlock(3, 0, pp.normal);
+          p2p_residual_jacobian(x_curr.R, p.pnt, wld, pp.normal, pp.center, resi, jac);
           HTH += (jac * R_inv) * jac.T();
           HTz -= jac * (R_inv * resi);
           nnt += outer(pp.normal, pp.normal);
@@ -822,6 +821,16 @@ int orc_window_states(void* h, double* out) {
   Pipeline* p = (Pipeline*)h;
   for (size_t i = 0; i < p->x_buf.size(); i++) state_to(p->x_buf[i], out + 250 * i);
   return (int)p->x_buf.size();
+}
+void orc_capture_arm(void* h) {
+  Pipeline* p = (Pipeline*)h;
+  p->mpar.capture = 1;
+  p->mpar.captured.clear();
+}
+int orc_capture_get(void* h, double* out, int cap) {
+  const std::vector<double>& c = ((Pipeline*)h)->mpar.captured;
+  if (out) memcpy(out, c.data(), (c.size() < (size_t)cap ? c.size() : (size_t)cap) * sizeof(double));
+  return (int)c.size();
 }
 
 // decoders + pcl_handler over little-endian records

@@ -71,6 +71,19 @@ void orc_shard(void* h, int rank, int world, int (*fn)(double* buf, int n, void*
 int orc_traj_len(void* h);
 void orc_get_traj(void* h, double* out);
 int orc_window_states(void* h, double* out);
+/* test hook: the next LM run's first divide_thread pass (optimizers.cpp:181-245)
+ * as [6W x 6W LiDAR Hessian summed over the factors (row-major), 6W gradient,
+ * residual, then per IMU factor: J^T C J 30x30, J^T C r 30, r^T C r] */
+void orc_capture_arm(void* h);
+/* known-answer hooks (oracle/kat.cpp): the restatement's p2p Jacobian, one
+ * LidarFactor voxel and one IMU_PRE factor on caller-given inputs */
+void orc_kat_p2p(const double* R9, const double* p3, const double* pnt3, const double* n3, const double* c3,
+                 double* r, double* j6);
+void orc_kat_lidar_factor(int W, const double* clu, const double* fix, const double* poses, double* res,
+                          double* jac, double* hess);
+double orc_kat_imu(const double* imu, int m, const double* bias0, const double* dbias, const double* x1,
+                   const double* x2, const double* noise, double sg, double* rr, double* joc);
+int orc_capture_get(void* h, double* out, int cap);
 
 /* VINA_SLAM::lio_state_estimation_kdtree (odometry.cpp:267-439) on
  * the context's x_curr and its initialisation map; valid = -1 when the scan

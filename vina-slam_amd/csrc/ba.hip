@@ -7,18 +7,17 @@
 // (imu_preintegration.cpp:97-163, 239-246).
 //
 // Per LM iteration, all device-resident, no host round trip:
-//   k_ba_hess    one workgroup per chunk of 2 x (256/W) factors: one lane per
-//                (factor, frame) evaluates Auk, the diagonal 6x6 block and the
-//                gradient piece (fp64 VALU); the off-diagonal blocks, sums of
-//                rank-1 terms, are reduced as X^T S X on fp64 MFMA from LDS
-//                -> per-chunk partials (deterministic)
+//   k_ba_hess    one 512-lane workgroup per chunk of min(512/W, 64) factors:
+//                one lane per (factor, frame) evaluates Auk, the diagonal 6x6
+//                block and the gradient piece (fp64 VALU); the off-diagonal
+//                blocks, sums of rank-1 terms, are reduced as X^T S X on fp64
+//                MFMA from LDS -> per-chunk partials (deterministic). The IMU
+//                factors ride in the same launch (one workgroup each)
 //   k_ba_hfinal  ordered sum of the chunk partials
-//   k_ba_imu     one workgroup per IMU factor: residual, 15x30 Jacobian,
-//                J^T C J (30x30) and J^T C r
-//   k_ba_solve   one 256-lane workgroup: assemble the 15W x 15W system
-//                (IMU blocks x imu_coef + LiDAR 6x6 blocks), gauge frame 0,
-//                Marquardt damping, blocked LDL^T of the pivoted system in
-//                LDS (16x16 tiles, MFMA f64 trailing updates), the trial
+//   k_ba_prep    assemble the 15W x 15W system (IMU blocks x imu_coef + LiDAR
+//                6x6 blocks), gauge, Marquardt damping, pivoted tile image
+//   k_ba_solve   one 1024-lane workgroup: blocked LDL^T of the pivoted
+//                system in LDS (16x16 tiles, MFMA f64 trailing updates), the trial
 //                state and q1
 //   k_ba_resid   one lane per factor: merge clusters at the trial poses, 3x3
 //                eigen, write the trial eig/cluster (the side effect margi
@@ -298,7 +297,7 @@ __device__ __forceinline__ void hess_chunk_eval(int ch, int nf, int W, const int
   for (int k = 0; k < 21; k++) hb[k] = 0.0;
   for (int k = 0; k < 6; k++) jj[k] = 0.0;
   const int ntl = NT * (NT + 1) / 2;
-  v4d acc[4];  // <= 15 lower tiles (W <= 11) over 4 waves
+  v4d acc[4];  // <= 15 lower tiles (W <= 11) over the 8 waves (<= 2 per wave; 4 slots)
   for (int s = 0; s < 4; s++) acc[s] = v4d{0.0, 0.0, 0.0, 0.0};
   for (int sub = a_begin; sub < a_end; sub += FS) {
     for (int t = tid; t < KS * XS; t += kHessThreads) X[t] = 0.0;
@@ -1044,10 +1043,16 @@ struct BaDev {
 };
 static BaDev g_dummy;
 
+// dynamic LDS of k_ba_hess: the X operand of a sub-chunk, reused as the
+// per-lane (hb, jj, res) rows of the final reduction (512 x 28 doubles =
+// 112 KB); with the static S[512] (4 KB) it must fit gfx950's 160 KB LDS,
+// checked at context creation (ba_alloc) against the device limit
 static size_t hess_lds_bytes(int W) {
   const size_t gemm = (size_t)hess_ks(W) * hess_xs(W), red = (size_t)kHessThreads * 28;
   return (gemm > red ? gemm : red) * sizeof(double);
 }
+static_assert((size_t)kHessThreads * 28 * sizeof(double) + kHessThreads * sizeof(double) <= 160 * 1024,
+              "k_ba_hess reduction rows exceed gfx950 LDS");
 
 static size_t solve_lds_bytes(int W) {
   const int NB = (15 * W - 15 + kTile - 1) / kTile;  // the gauge frame is not factored
@@ -1076,6 +1081,16 @@ int ba_alloc(vg_ctx* ctx) {
   if (W > kMaxW || 15 * W > kMaxNB * kTile) {
     ctx->err = "win_size > 11 unsupported by the BA solve (LDS-resident 15W x 15W tile store)";
     return VG_E_ARG;
+  }
+  {  // both LM kernels keep their working set in LDS: check the device limit up front
+    int lds_max = 0;
+    VG_HIP(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, ctx->device));
+    const size_t hess_total = hess_lds_bytes(W) + kHessThreads * sizeof(double);
+    if (lds_max > 0 && (hess_total > (size_t)lds_max || solve_lds_bytes(W) > (size_t)lds_max)) {
+      ctx->err = "LM kernels need " + std::to_string(hess_total) + " / " + std::to_string(solve_lds_bytes(W)) +
+                 " B of LDS per workgroup; the device allows " + std::to_string(lds_max);
+      return VG_E_ARG;
+    }
   }
   VG_HIP(hipFuncSetAttribute((const void*)k_ba_solve, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)solve_lds_bytes(W)));
@@ -1183,6 +1198,13 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
     // sharded: every shard's factors -> one LiDAR Hessian / gradient / residual
     // (out of place: a rejected step re-reduces the unchanged partial)
     if (sharded && xerr == VG_OK) xerr = shard_allreduce(ctx, hl_part, d.hl, nout, 0);
+    if (k == 0 && ctx->dbg_capture == 1 && ctx->dbg_cap_buf) {  // test knob (vgx_debug 5): the first pass
+      (void)hipMemcpyAsync(ctx->dbg_cap_buf, d.hl, nout * sizeof(double), hipMemcpyDeviceToDevice, s);
+      (void)hipMemcpyAsync(ctx->dbg_cap_buf + nout, d.imuout, (size_t)nimu * 931 * sizeof(double),
+                           hipMemcpyDeviceToDevice, s);
+      ctx->dbg_cap_n = nout + nimu * 931;
+      ctx->dbg_capture = 2;
+    }
     k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
                                     d.dvec, d.jvec, d.ipg, d.st);
     if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][0], s);
@@ -1200,7 +1222,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
                                    d.imuout, d.imures, sharded ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st,
                                    ctx->d_pub);
   };
-  const bool graph = ctx->use_graphs && !sharded && !solve_ev;
+  const bool graph = ctx->use_graphs && !sharded && !solve_ev && ctx->dbg_capture != 1;
   if (graph && !ctx->g_ba) {
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     enqueue(0);

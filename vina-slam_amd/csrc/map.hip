@@ -78,6 +78,7 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(w.leaf = ctx->arena.take<int>(cw));
   good &= ok(w.pw = ctx->arena.take<double>(cw * 3));
   good &= ok(w.iekf_cache = ctx->arena.take<int>(cw));
+  good &= ok(w.pk_leaf = ctx->arena.take<int>(cw));
   good &= ok(w.rc = ctx->arena.take<int>(128));
   good &= ok(w.cand_bits = ctx->arena.take<uint32_t>(ctx->cap.max_nodes / 32 + 1));
   good &= ok(w.plan = ctx->arena.take<int>(cn * 8));
@@ -195,9 +196,9 @@ __device__ __forceinline__ bool inside(const NodeHdr& h, const V3& w) {
 // no-op once the IEKF has finished (st->done). Iteration 0 ignores the leaf
 // cache (no association yet, odometry.cpp:111-132).
 __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, int it, DevMap m,
-                                              int* __restrict__ cache, double* __restrict__ partials, int tag) {
+                                              int* __restrict__ cache, double* __restrict__ partials,
+                                              int* __restrict__ pk) {
   if (st->done) return;
-  int nplanes = 0;  // distinct plane records read by this iteration (tag != 0: the profiling pass only)
   const int n = st->sn;
   const float* __restrict__ x = st->sx;
   const float* __restrict__ y = st->sy;
@@ -243,9 +244,9 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
       }
     }
     if (!flag && it == 0) cache[i] = -1;  // the reference's fresh per-scan association
+    if (pk) pk[i] = flag ? leaf : -1;     // the leaf whose plane this iteration read (profiling pass)
     if (flag) {
       cache[i] = leaf;
-      if (tag && m.stamp[leaf] != tag && atomicExch(&m.stamp[leaf], tag) != tag) nplanes++;
       const PlaneRec& P = m.pl[leaf];
       V3 nn = ld_v3(P.normal), c = ld_v3(P.center);
       double R_inv = 1.0 / (0.0005 + sigma);
@@ -267,7 +268,6 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
       acc[33] += 1.0;
     }
   }
-  if (tag) wave_append(&st->planes[it], nplanes);
   // block reduction: wave shuffles then LDS across the 4 waves (fixed tree)
   __shared__ double red[4][kIekfVals];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -281,6 +281,20 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
     int j = threadIdx.x;
     partials[(size_t)blockIdx.x * kIekfVals + j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
   }
+}
+
+// P_k of SURVEY 8(d), the profiling pass only: distinct plane records the
+// iteration read, deduplicated with a per-node tag (outside k_iekf's timing)
+__global__ void __launch_bounds__(256) k_iekf_planes(const DState* __restrict__ st, DevMap m,
+                                                     const int* __restrict__ pk, int tag, int* __restrict__ out) {
+  if (st->done) return;
+  const int n = st->sn;
+  int cnt = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int leaf = pk[i];
+    if (leaf >= 0 && m.stamp[leaf] != tag && atomicExch(&m.stamp[leaf], tag) != tag) cnt++;
+  }
+  wave_append(out, cnt);
 }
 
 // The IEKF update of iteration `it` (vg_iekf.h) as its own one-workgroup
@@ -321,8 +335,9 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
   (void)n;  // the scan is read from the device state (state_set_scan)
   const int nb = iekf_blocks(ctx);
   if (ev0) VG_HIP(hipEventRecord(ev0, s));
-  k_iekf<<<nb, 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials, tag);
+  k_iekf<<<nb, 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials, tag ? w.pk_leaf : nullptr);
   if (ev1) VG_HIP(hipEventRecord(ev1, s));
+  if (tag) k_iekf_planes<<<nb, 256, 0, s>>>(ctx->st, ctx->map, w.pk_leaf, tag, &ctx->st->planes[it]);
   if (ctx->shard.world > 1) {  // this shard's sums, all-reduced, then the (replicated) update
     double* sums = ctx->shard.d_buf;
     k_iekf_reduce<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, sums);

@@ -163,6 +163,7 @@ struct Work {
   size_t tmp_bytes = 0;
   double* partials = nullptr;  // reduction partials
   int* iekf_cache = nullptr;   // per raw point cached leaf
+  int* pk_leaf = nullptr;      // per raw point leaf read by the profiled IEKF iteration (P_k count)
   int* rc = nullptr;           // device-side level counts (recut / margi, map.hip kRc*)
   uint32_t* cand_bits = nullptr;  // factor candidates of an asynchronous recut, one bit per node id
   int* plan = nullptr;         // per-leaf point_fix copy plan (margi)
@@ -305,6 +306,9 @@ struct vg_ctx {
   int dbg_apply_cap = -1;        // test knob (vgx_debug): recut apply event capacity
   int dbg_ins_cap = -1;   // vgx_debug 3: k_ins_alloc capacity override (forces the insert replay)
   int dbg_fac_max = -1;   // vgx_debug 4: device factor-sort limit override (forces the host factor path)
+  int dbg_capture = 0;    // vgx_debug 5: capture the next LM run's first Hessian pass (vgx_ba_capture)
+  double* dbg_cap_buf = nullptr;  // device copy: LiDAR hl (lower) + IMU factor blocks
+  int dbg_cap_n = 0;
   bool prof_pending[16] = {};
   double prof_ms[16] = {};  // [0, 8): device time (events); [8, 16): host time of the stage calls
   int prof_n[16] = {};

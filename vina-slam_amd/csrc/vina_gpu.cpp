@@ -134,6 +134,7 @@ int vg_destroy(vg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->arena.base) (void)hipFree(ctx->arena.base);
   if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+  if (ctx->dbg_cap_buf) (void)hipFree(ctx->dbg_cap_buf);
   shard_free(ctx);
   if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
   if (ctx->h_pub) (void)hipHostFree(ctx->h_pub);
@@ -455,7 +456,39 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     ctx->dbg_fac_max = value;
     return VG_OK;
   }
+  if (key == 5) {  // arm: the next LM run copies its first Hessian pass (LiDAR hl + IMU blocks)
+    if (!ctx->dbg_cap_buf)
+      VG_HIP(hipMalloc((void**)&ctx->dbg_cap_buf, (size_t)(4096 + 32 * 931) * sizeof(double)));
+    ctx->dbg_capture = value ? 1 : 0;
+    ctx->dbg_cap_n = 0;
+    return VG_OK;
+  }
   return VG_E_ARG;
+}
+
+// Test-only: the captured first Hessian pass of an LM run (vgx_debug 5), as
+// [6W x 6W LiDAR Hessian (full, row-major), 6W gradient, residual, then per
+// IMU factor k: J^T C J 30 x 30, J^T C r 30, r^T C r] — the oracle's
+// orc_capture_get layout (acc_evaluate2 summed over factors, factors.cpp:22-126;
+// give_evaluate, imu_preintegration.cpp:97-163). *n = doubles written.
+extern "C" int vgx_ba_capture(vg_ctx* ctx, double* out, int cap, int* n) {
+  if (!ctx || !n) return VG_E_ARG;
+  VG_TRY(vg::host_sync(ctx));
+  *n = 0;
+  if (ctx->dbg_capture != 2 || ctx->dbg_cap_n <= 0) return VG_OK;
+  const int W = ctx->cfg.win_size, L = 6 * W, nl = L * (L + 1) / 2, nout = nl + L + 1;
+  std::vector<double> raw(ctx->dbg_cap_n);
+  VG_HIP(hipMemcpy(raw.data(), ctx->dbg_cap_buf, raw.size() * sizeof(double), hipMemcpyDeviceToHost));
+  std::vector<double> o;
+  o.resize((size_t)L * L);
+  for (int r = 0; r < L; r++)
+    for (int c = 0; c <= r; c++) o[(size_t)r * L + c] = o[(size_t)c * L + r] = raw[(size_t)r * (r + 1) / 2 + c];
+  o.insert(o.end(), raw.begin() + nl, raw.begin() + nout);
+  o.insert(o.end(), raw.begin() + nout, raw.end());
+  const int m = (int)o.size() < cap ? (int)o.size() : cap;
+  if (out) memcpy(out, o.data(), (size_t)m * sizeof(double));
+  *n = (int)o.size();
+  return VG_OK;
 }
 
 int vg_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* valid, int* iters) {

@@ -128,6 +128,8 @@ def lib():
         L.vg_shard_host.argtypes = [P, ctypes.c_int, ctypes.c_int, HOST_ALLREDUCE, P]
         L.vg_stream.argtypes = [P]
         L.vg_stream.restype = P
+        L.vgx_debug.argtypes = [P, ctypes.c_int, ctypes.c_int]
+        L.vgx_ba_capture.argtypes = [P, dp, ctypes.c_int, ip]
         _lib = L
     return _lib
 
@@ -356,6 +358,21 @@ class Context:
 
     def stream(self):
         return lib().vg_stream(self.h)
+
+    # ---- test-only knobs (vgx_*, not part of include/vina_gpu.h)
+    def debug(self, key, value):
+        self._chk(lib().vgx_debug(self.h, key, value), "vgx_debug")
+
+    def capture_arm(self):
+        """Capture the next LM run's first Hessian pass (vgx_debug 5)."""
+        self.debug(5, 1)
+
+    def capture_get(self):
+        n = ctypes.c_int(0)
+        self._chk(lib().vgx_ba_capture(self.h, None, 0, ctypes.byref(n)), "vgx_ba_capture")
+        out = np.zeros(max(n.value, 1))
+        self._chk(lib().vgx_ba_capture(self.h, _d(out), n.value, ctypes.byref(n)), "vgx_ba_capture")
+        return out[: n.value]
 
 
 class Sync:
