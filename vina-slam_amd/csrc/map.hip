@@ -355,8 +355,10 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
 // graph: one host call instead of eight launches, and the device starts each
 // node without the per-launch dispatch gap. The per-stage profiling pass
 // (vg_profile bit 1) launches directly, with an event pair around each k_iekf.
-int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank) {
-  VG_TRY(state_set_scan(ctx, x, y, z, n));
+int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank,
+             const double* begin_xc) {
+  if (begin_xc) VG_TRY(state_scan_begin(ctx, begin_xc, x, y, z, n));  // the scan opens here (pipeline.cpp)
+  else VG_TRY(state_set_scan(ctx, x, y, z, n));
   const bool graph = ctx->use_graphs && ctx->shard.world <= 1 && !ctx->prof_stages;
   const bool ev = ctx->prof_on && !graph;
   auto enqueue = [&]() -> int {
@@ -385,8 +387,12 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
 // per downsampled point: var_init + pvec_update (world var), world point, root
 // key insert-or-find, first-occurrence marking of brand-new keys
 __global__ void __launch_bounds__(256) k_ins_prep(int n, const float* __restrict__ ox, const float* __restrict__ oy,
-                           const float* __restrict__ oz, MP mp, const DState* __restrict__ st, int slot,
-                           DevMap m, double* __restrict__ pw, uint32_t* __restrict__ hslot) {
+                           const float* __restrict__ oz, MP mp, DState* __restrict__ st, int slot,
+                           DevMap m, double* __restrict__ pw, uint32_t* __restrict__ hslot, int do_push,
+                           PushArg pa) {
+  // the window push (local_mapping.cpp:434-441) rides in block 0: it copies
+  // x_curr into x_buf[ord], which this kernel only reads
+  if (do_push && blockIdx.x == 0) push_state_block(st, pa);
   // pose of x_buf[ord] = x_curr after the IEKF (device state)
   const double* xc = st->xc;
   M3 R, rot_var, tsl_var;
@@ -399,6 +405,7 @@ __global__ void __launch_bounds__(256) k_ins_prep(int n, const float* __restrict
   const V3 p = ld_v3(xc + 9);
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // per-insert device counters (read by the later kernels)
     m.counters[kCntNew] = m.counters[kCntNodes];  // first id of this scan's new roots
+    m.counters[kCntSlideBase] = m.counters[kCntSlide];  // surf_map_slide size before this scan's roots
     m.counters[kCntTouched] = 0;
     m.counters[kCntCreate] = 0;
     m.counters[kCntSeg] = 0;
@@ -435,7 +442,7 @@ __global__ void __launch_bounds__(256) k_ins_prep(int n, const float* __restrict
       continue;
     }
     hslot[i] = (uint32_t)s;
-    if (m.hval[s] < 0) atomicMin(&m.hfirst[s], i);
+    atomicMin(&m.hfirst[s], i);  // the root's first point this scan (k_ins_flags)
   }
 }
 
@@ -444,6 +451,146 @@ __global__ void __launch_bounds__(256) k_ins_newflag(int n, const uint32_t* __re
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     uint32_t s = hslot[i];
     flag[i] = (s != 0xffffffffu && hval[s] < 0 && hfirst[s] == i) ? 1u : 0u;
+  }
+}
+
+// Root registration of cut_voxel_multi (voxel_map.cpp:57-90) in two launches
+// (flags + per-tile ranks, then allocation), replacing a flag / scan /
+// allocate / count / zero / touch chain. Points are taken in index tiles of
+// kRootTile; a point is its root's first point this scan iff hfirst[slot] == i
+// (k_ins_prep). Per tile: how many first points, new roots, and roots joining
+// surf_map_slide (new ones, and existing ones not yet in it), with each
+// point's rank inside its tile. Ids and slide positions then follow point
+// index order: deterministic.
+constexpr int kRootTile = 1024;  // points per workgroup (256 threads x 4)
+__device__ __forceinline__ void zero_node(DevMap& m, int id);
+__device__ __forceinline__ int ins_root_code(const DevMap& m, const uint32_t* __restrict__ hslot, int i, int n) {
+  // bit 0: first point of its root, bit 1: new root, bit 2: joins the slide map
+  if (i >= n) return 0;
+  const uint32_t s = hslot[i];
+  if (s == 0xffffffffu || m.hfirst[s] != i) return 0;
+  const int r = m.hval[s];
+  if (r < 0) return 7;
+  return m.in_slide[r] ? 1 : 5;
+}
+// exclusive block scan of three counts packed 3 x 21 bits
+typedef unsigned long long u64;
+__device__ __forceinline__ u64 pack3(int code) {
+  return (u64)(code & 1) | ((u64)((code >> 1) & 1) << 21) | ((u64)((code >> 2) & 1) << 42);
+}
+__device__ __forceinline__ u64 block_excl_scan3(u64 v, u64* s_w, u64* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  u64 x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const u64 y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  u64 base = 0, tot = 0;
+  for (int k = 0; k < nw; k++) {
+    if (k < wv) base += s_w[k];
+    tot += s_w[k];
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+__global__ void __launch_bounds__(256) k_ins_flags(int n, const uint32_t* __restrict__ hslot, DevMap m,
+                                                   uint32_t* __restrict__ rank, int* __restrict__ tile_cnt) {
+  __shared__ u64 s_w[4];
+  const int i0 = blockIdx.x * kRootTile + threadIdx.x * 4;
+  int code[4];
+  u64 v = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    code[k] = ins_root_code(m, hslot, i0 + k, n);
+    v += pack3(code[k]);
+  }
+  u64 tot;
+  u64 r = block_excl_scan3(v, s_w, &tot);
+  constexpr u64 kF = (1ull << 21) - 1;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {  // rank: new-root rank | slide rank << 16 (< 1024 each), code in the top bits
+    if (i0 + k < n)
+      rank[i0 + k] = (unsigned)((r >> 21) & kF) | ((unsigned)((r >> 42) & kF) << 16) | ((unsigned)code[k] << 29);
+    r += pack3(code[k]);
+  }
+  if (threadIdx.x == 0) {
+    tile_cnt[blockIdx.x * 3 + 0] = (int)(tot & kF);
+    tile_cnt[blockIdx.x * 3 + 1] = (int)((tot >> 21) & kF);
+    tile_cnt[blockIdx.x * 3 + 2] = (int)((tot >> 42) & kF);
+  }
+}
+// new roots at kCntNew + (new roots of earlier tiles) + rank, centre
+// (0.5 + k) voxel_size, records zeroed; existing first-touched roots isexist
+// (voxel_map.cpp:70); slide appends in point order; the root counters. The
+// point -> root lookup itself is left to k_ins_descend (after this launch).
+__global__ void __launch_bounds__(256) k_ins_roots_alloc(int n, int ntile, const uint32_t* __restrict__ hslot,
+                                                         const uint32_t* __restrict__ rank,
+                                                         const int* __restrict__ tile_cnt, MP mp, DevMap m) {
+  __shared__ int s_red[3][4];
+  int a[3] = {0, 0, 0}, t[3] = {0, 0, 0};
+  for (int b = threadIdx.x; b < ntile; b += blockDim.x)
+    for (int j = 0; j < 3; j++) {
+      const int c = tile_cnt[b * 3 + j];
+      t[j] += c;
+      if (b < (int)blockIdx.x) a[j] += c;
+    }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int off[3], tot[3];
+  for (int j = 0; j < 3; j++) {  // (a: this tile's offset, t: the totals) over the block
+    int x = a[j], y = t[j];
+    for (int o = 32; o > 0; o >>= 1) {
+      x += __shfl_down(x, o, 64);
+      y += __shfl_down(y, o, 64);
+    }
+    if (lane == 0) s_red[j][wv] = x;
+    __syncthreads();
+    off[j] = s_red[j][0] + s_red[j][1] + s_red[j][2] + s_red[j][3];
+    __syncthreads();
+    if (lane == 0) s_red[j][wv] = y;
+    __syncthreads();
+    tot[j] = s_red[j][0] + s_red[j][1] + s_red[j][2] + s_red[j][3];
+    __syncthreads();
+  }
+  const int base = m.counters[kCntNew], sbase = m.counters[kCntSlideBase];
+  const int i0 = blockIdx.x * kRootTile;
+  for (int i = i0 + threadIdx.x; i < min(n, i0 + kRootTile); i += blockDim.x) {
+    const uint32_t rk = rank[i];
+    const int code = (int)(rk >> 29);
+    if (!(code & 1)) continue;
+    const uint32_t s = hslot[i];
+    int r;
+    if (code & 2) {  // a new root (voxel_map.cpp:77-83): centre, quater_length, empty records
+      r = base + off[1] + (int)(rk & 0xffffu);
+      if (r >= m.cap_nodes) {
+        atomicOr(&m.counters[kCntErr], 4);
+        continue;
+      }
+      const uint64_t key = m.hkey[s];
+      double c[3];
+      const int64_t k[3] = {unpack_axis(key, 42), unpack_axis(key, 21), unpack_axis(key, 0)};
+      for (int j = 0; j < 3; j++) c[j] = (0.5 + k[j]) * mp.vs;
+      init_node(m.hdr[r], c, (float)(mp.vs / 4.0), 0, -1);
+      zero_node(m, r);
+      m.hval[s] = r;
+    } else {
+      r = m.hval[s];
+      m.hdr[r].isexist = 1;
+    }
+    if (code & 4) {
+      m.in_slide[r] = 1;
+      m.slide[sbase + off[2] + (int)((rk >> 16) & 0x1fffu)] = r;
+    }
+    m.hfirst[s] = 0x7f7f7f7f;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    m.counters[kCntNodes] = min(base + tot[1], m.cap_nodes);
+    m.counters[kCntRoots] = tot[1];
+    m.counters[kCntTouched] = tot[0];
+    m.counters[kCntSlide] = sbase + tot[2];
   }
 }
 
@@ -520,10 +667,13 @@ __global__ void k_copy_int(const int* __restrict__ src, int* __restrict__ dst) {
 }
 
 __global__ void __launch_bounds__(256) k_ins_descend(int n, int thread_num, const double* __restrict__ pw, DevMap m,
-                                                     int* __restrict__ leaf, int* __restrict__ reqlist) {
+                                                     const uint32_t* __restrict__ hslot, int* __restrict__ leaf,
+                                                     int* __restrict__ reqlist) {
   if (ins_skip(m, thread_num)) return;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    int node = leaf[i];
+    const uint32_t hs = hslot[i];
+    int node = hs != 0xffffffffu ? m.hval[hs] : -1;  // the point's root (registered by k_ins_roots_alloc)
+    leaf[i] = node;
     if (node < 0) continue;
     V3 w = v3(pw[3 * i], pw[3 * i + 1], pw[3 * i + 2]);
     for (int d = 0; d < 8; d++) {
@@ -958,25 +1108,26 @@ static int insert_tail(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_nu
 // Asynchronous: every count stays on the device. A child-allocation overflow
 // of k_ins_alloc sets kCntMisc; the insert tail and the recut kernels then skip
 // and map_recut reports it (kNeedInsertReplay) for map_insert_replay.
-int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num) {
+int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num, const PushArg* push) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
-  if (n <= 0) return VG_OK;
+  if (n <= 0) {
+    if (push) VG_TRY(state_push(ctx, push->ord, push->new_imu, push->rec));
+    return VG_OK;
+  }
   const int g = grid_for(n);
-  k_ins_prep<<<g, kBlock, 0, s>>>(n, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, mp, ctx->st, slot, m, w.pw, w.u0);
-  k_ins_newflag<<<g, kBlock, 0, s>>>(n, w.u0, m.hval, m.hfirst, w.v0);
-  VG_TRY(excl_scan(ctx, w.v0, w.v1, n));
-  k_ins_newalloc<<<g, kBlock, 0, s>>>(n, w.u0, w.v0, w.v1, mp, m);
-  k_ins_roots<<<1, 64, 0, s>>>(m, w.v0, w.v1, n);
-  k_zero_nodes<<<grid_for(1 << 16), kBlock, 0, s>>>(0, m.counters + kCntNew, m.counters + kCntNodes, m.W, m.pl,
-                                                  m.pcr_add, m.pcr_fix, m.cov_add, m.eig, m.jour, m.pcrs);
-  k_ins_touch<<<g, kBlock, 0, s>>>(n, w.u0, epoch, m, w.leaf);
+  k_ins_prep<<<g, kBlock, 0, s>>>(n, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, mp, ctx->st, slot, m, w.pw, w.u0,
+                                  push ? 1 : 0, push ? *push : PushArg());
+  const int ntile = (n + kRootTile - 1) / kRootTile;
+  (void)epoch;
+  k_ins_flags<<<ntile, kBlock, 0, s>>>(n, w.u0, m, w.v1, (int*)w.ac_cnt);
+  k_ins_roots_alloc<<<ntile, kBlock, 0, s>>>(n, ntile, w.u0, w.v1, (const int*)w.ac_cnt, mp, m);
   if (m.shard_world > 1) {  // the thread_num quirk counts distinct roots over all shards
     k_copy_int<<<1, 64, 0, s>>>(m.counters + kCntTouched, m.counters + kCntGTouched);
     VG_TRY(shard_allreduce(ctx, m.counters + kCntGTouched, m.counters + kCntGTouched, 1, 1));
   }
-  k_ins_descend<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.leaf, w.list2);
+  k_ins_descend<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.u0, w.leaf, w.list2);
   const int ins_cap = (ctx->dbg_ins_cap >= 0 && ctx->dbg_ins_cap < kInsAllocCap) ? ctx->dbg_ins_cap : kInsAllocCap;
   k_ins_alloc<<<1, 1024, 0, s>>>(thread_num, m, w.list2, ins_cap);
   return insert_tail(ctx, mp, slot, n, thread_num);
@@ -1727,6 +1878,9 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* 
   for (int L = 0; L < nlev; L++) {
     k_rc_visit<<<gv, kBlock, 0, s>>>(L, thread_num, L > 0 ? list_of(L) : nullptr, mp, m, list_of(L + 1), w.list2,
                                      w.cand, w.rc, pub_seq > 0 ? w.cand_bits : nullptr);
+    // nodes at layer max_layer never subdivide (recut_visit_node, octree.cpp:371-372):
+    // the deepest level has no window events, no apply and no pushes
+    if (L == mp.max_layer) break;
     if (total > 0)
       k_rc_win<<<gw, kBlock, 0, s>>>(L, total, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc, w.cap, w.rc);
     k_rc_apply<<<1, kApplyThreads, 0, s>>>(L, ev_cap, mp, dwin, m, list_of(L + 1), w.list2, w.k0, w.evsrc, w.k1,

@@ -175,7 +175,27 @@ struct HostPipe {
   int rc_seq = 0;          // > 0: this scan's recut ran asynchronously (status with Pub::seq_rc == rc_seq)
   std::deque<Pend> pend;   // enqueued scans awaiting absorption (oldest first)
   int sticky = VG_OK;      // deferred device error
+  // device work deferred to the next launch that can carry it (one launch
+  // fewer each): the scan opening rides with the IEKF's scan binding, the
+  // window push with the insert's first kernel
+  bool begin_pending = false;
+  double begin_xc[kXC];
+  bool push_pending = false;
+  PushArg push;
 };
+
+// enqueue deferred device work on its own when the next stage cannot carry it
+static int flush_begin(vg_ctx* ctx, HostPipe* P) {
+  if (!P->begin_pending) return VG_OK;
+  P->begin_pending = false;
+  return state_scan_begin(ctx, P->begin_xc);
+}
+static int flush_deferred(vg_ctx* ctx, HostPipe* P) {
+  VG_TRY(flush_begin(ctx, P));
+  if (!P->push_pending) return VG_OK;
+  P->push_pending = false;
+  return state_push(ctx, P->push.ord, P->push.new_imu, P->push.rec);
+}
 
 static HostPipe* hp(vg_ctx* ctx) { return (HostPipe*)ctx->host; }
 
@@ -433,13 +453,22 @@ static void propagate(vg_ctx* ctx, HostPipe* P, const std::vector<Imu>& imus, do
 // device. The VNC scan-plane prep (84-96, 150-190) contributes nothing
 // (SURVEY finding 3: matchVoxelMap always returns 0) and is skipped as
 // output-invariant.
+static int flush_deferred_push(vg_ctx* ctx, HostPipe* P) {
+  if (!P->push_pending) return VG_OK;
+  VG_TRY(flush_begin(ctx, P));
+  P->push_pending = false;
+  return state_push(ctx, P->push.ord, P->push.new_imu, P->push.rec);
+}
 static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const float* y, const float* z, int n) {
   // event pairs alternate between two banks: scan k's are collected while
   // scan k+1 is being enqueued
   ctx->iekf_ring_base = ctx->iekf_ring_base == 0 ? 8 : 0;
   P->cur.ev_base = ctx->iekf_ring_base;
   P->cur.ev_n = (ctx->prof_on && (ctx->prof_stages || !ctx->use_graphs || ctx->shard.world > 1)) ? 4 : 0;
-  return iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base);
+  VG_TRY(flush_deferred_push(ctx, P));
+  const bool begin = P->begin_pending;
+  P->begin_pending = false;
+  return iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, begin ? P->begin_xc : nullptr);
 }
 
 static WinArg make_winarg(const HostPipe* P, int set_xc) {
@@ -492,7 +521,7 @@ int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double en
     P->x_curr.t = end;
     P->last_pcl_end_time = end;
   }
-  double xc[kXC];
+  double* xc = P->begin_xc;  // opened on the device with the IEKF's first launch (flush_begin otherwise)
   const HX& h = P->x_curr;
   memcpy(xc, h.R.a, 72);
   memcpy(xc + 9, h.p.a, 24);
@@ -501,7 +530,8 @@ int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double en
   memcpy(xc + 18, h.ba.a, 24);
   memcpy(xc + 21, h.g.a, 24);
   memcpy(xc + kXS, h.cov.a, 225 * sizeof(double));
-  VG_TRY(state_scan_begin(ctx, xc));
+  P->begin_pending = true;
+  P->push_pending = false;
   P->cur = Pend();
   memset(&P->cur.st, 0, sizeof(P->cur.st));
   P->cur.t = end;
@@ -612,7 +642,13 @@ int stage_window_push(vg_ctx* ctx, const double* imu, int m) {
     P->imu_pre.back().record(P->imu_pre.back().rec.data());  // off the BA's critical path
     new_imu = P->win_count - 2;
   }
-  return state_push(ctx, P->win_count - 1, new_imu, new_imu >= 0 ? P->imu_pre.back().rec.data() : nullptr);
+  // deferred: the insert's first launch carries it (map_insert), else flush_deferred
+  P->push.ord = P->win_count - 1;
+  P->push.new_imu = new_imu;
+  if (new_imu >= 0) memcpy(P->push.rec, P->imu_pre.back().rec.data(), sizeof(P->push.rec));
+  else memset(P->push.rec, 0, sizeof(P->push.rec));
+  P->push_pending = true;
+  return VG_OK;
 }
 
 // pvec_update + cut_voxel_multi of the downsampled scan (local_mapping.cpp:425-448)
@@ -635,8 +671,11 @@ int stage_insert(vg_ctx* ctx) {
   const int slot = P->mp[ord];
   P->epoch++;
   VG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_ds_done, 0));
+  VG_TRY(flush_begin(ctx, P));
   prof_begin(ctx, kProfInsert);
-  VG_TRY(map_insert(ctx, P->mpd, slot, P->ds_n, P->epoch, c.thread_num));
+  const bool push = P->push_pending;
+  P->push_pending = false;
+  VG_TRY(map_insert(ctx, P->mpd, slot, P->ds_n, P->epoch, c.thread_num, push ? &P->push : nullptr));
   prof_end(ctx, kProfInsert);
   VG_HIP(hipEventRecord(ctx->ev_ds_free, ctx->stream));  // k_ins_prep has read the ds buffers
   P->wp_n[slot] = P->ds_n;
@@ -651,6 +690,7 @@ int stage_recut(vg_ctx* ctx, int* nf_out) {
   HostPipe* P = hp(ctx);
   const vg_config& c = ctx->cfg;
   VG_TRY(need_open(ctx, P, "vg_multi_recut"));
+  VG_TRY(flush_deferred(ctx, P));
   const WinArg wa = make_winarg(P, 0);
   int nf = 0;
   prof_begin(ctx, kProfRecut);
@@ -682,6 +722,7 @@ int stage_ba(vg_ctx* ctx, int* iters_out) {
   HostPipe* P = hp(ctx);
   const int W = ctx->cfg.win_size;
   VG_TRY(need_open(ctx, P, "vg_damping_iter"));
+  VG_TRY(flush_deferred(ctx, P));
   if (P->win_count < W) {
     ctx->err = "vg_ba: window not full";
     return VG_E_STATE;
@@ -740,6 +781,7 @@ int stage_margi_slide(vg_ctx* ctx) {
     return VG_E_STATE;
   }
   VG_TRY(need_open(ctx, P, "vg_multi_margi"));
+  VG_TRY(flush_deferred(ctx, P));
   const WinArg wa = make_winarg(P, 1);
   const int seq1 = ++ctx->pub_seq, seq2 = ++ctx->pub_seq;
   prof_begin(ctx, kProfMargi);
@@ -770,6 +812,7 @@ int stage_margi_slide(vg_ctx* ctx) {
 int stage_finish(vg_ctx* ctx) {
   HostPipe* P = hp(ctx);
   VG_TRY(need_open(ctx, P, "vg_step_end"));
+  VG_TRY(flush_deferred(ctx, P));
   if (!P->published) {
     P->cur.seq1 = ++ctx->pub_seq;
     VG_TRY(state_publish(ctx, P->win_count, nullptr, P->cur.seq1));
@@ -978,6 +1021,7 @@ int host_state(vg_ctx* ctx, double* s) {
     state_out(P->x_curr, s);
     return VG_OK;
   }
+  VG_TRY(flush_deferred(ctx, P));
   double* h = ctx->h_stage;
   VG_HIP(hipMemcpyAsync(h, ctx->st->xc, kXC * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   VG_HIP(stream_wait(ctx));

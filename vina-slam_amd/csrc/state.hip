@@ -41,9 +41,17 @@ __device__ __forceinline__ void pub_flag(int* dst, int v) {
   __hip_atomic_store(dst, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// x_curr after propagation; x_prop; cov_inv; IEKF flags
-__global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict__ st) {
+// x_curr after propagation; x_prop; cov_inv; IEKF flags; the scan the IEKF
+// reads (set_scan: one launch for both)
+__global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict__ st, const float* x, const float* y,
+                                                    const float* z, int n, int set_scan) {
   const int tid = threadIdx.x;
+  if (set_scan && tid == 64) {
+    st->sx = x;
+    st->sy = y;
+    st->sz = z;
+    st->sn = n;
+  }
   for (int t = tid; t < kXC; t += blockDim.x) {
     st->xc[t] = xa.x[t];
     st->xp[t] = xa.x[t];
@@ -73,18 +81,7 @@ __global__ void k_set_scan(DState* __restrict__ st, const float* x, const float*
 // with zero bias deltas (imu_preintegration.cpp:10-29)
 // the IMU_PRE record rides in the kernel arguments (2.3 KB): no copy-engine
 // transfer on the stream
-struct ImuRecArg {
-  double r[kBaImuRec];
-};
-__global__ void k_push_state(DState* __restrict__ st, int ord, int new_imu, ImuRecArg rec) {
-  const int t = threadIdx.x;
-  if (t < kXS) st->xs[ord * kXS + t] = st->xc[t];
-  if (new_imu >= 0) {
-    if (t < 12) st->bias[new_imu * 12 + t] = 0.0;
-    double* d = &st->imurec[(size_t)((st->imu_head + new_imu) % kMaxWin) * kBaImuRec];
-    for (int e = t; e < kBaImuRec; e += blockDim.x) d[e] = rec.r[e];
-  }
-}
+__global__ void k_push_state(DState* __restrict__ st, PushArg pa) { push_state_block(st, pa); }
 
 // window view for the map kernels: poses by ord, ring, per-ord counts / slots
 __global__ void k_make_win(DState* __restrict__ st, WinArg wa, WinD* __restrict__ win, int* __restrict__ nper,
@@ -246,10 +243,10 @@ int state_alloc(vg_ctx* ctx) {
   return VG_OK;
 }
 
-int state_scan_begin(vg_ctx* ctx, const double* xc249) {
+int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x, const float* y, const float* z, int n) {
   XcArg a;
   memcpy(a.x, xc249, sizeof(a.x));
-  k_scan_begin<<<1, 256, 0, ctx->stream>>>(a, ctx->st);
+  k_scan_begin<<<1, 256, 0, ctx->stream>>>(a, ctx->st, x, y, z, n, x != nullptr ? 1 : 0);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }
@@ -261,10 +258,12 @@ int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, 
 }
 
 int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec) {
-  ImuRecArg rec;
-  if (new_imu >= 0) memcpy(rec.r, imurec, sizeof(rec.r));
-  else memset(rec.r, 0, sizeof(rec.r));
-  k_push_state<<<1, 64, 0, ctx->stream>>>(ctx->st, ord, new_imu, rec);
+  PushArg pa;
+  pa.ord = ord;
+  pa.new_imu = new_imu;
+  if (new_imu >= 0) memcpy(pa.rec, imurec, sizeof(pa.rec));
+  else memset(pa.rec, 0, sizeof(pa.rec));
+  k_push_state<<<1, 64, 0, ctx->stream>>>(ctx->st, pa);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }

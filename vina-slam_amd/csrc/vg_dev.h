@@ -314,4 +314,17 @@ __device__ __forceinline__ void init_node(NodeHdr& h, const double c[3], float q
   h.parent = parent;
 }
 
+// x_buf.push_back(x_curr) at ord and a fresh IMU_PRE record with zero bias
+// deltas (local_mapping.cpp:434-441, imu_preintegration.cpp:10-29); one
+// workgroup (k_push_state, or block 0 of k_ins_prep)
+__device__ __forceinline__ void push_state_block(DState* __restrict__ st, const PushArg& pa) {
+  const int t = threadIdx.x;
+  if (t < kXS) st->xs[pa.ord * kXS + t] = st->xc[t];
+  if (pa.new_imu >= 0) {
+    if (t < 12) st->bias[pa.new_imu * 12 + t] = 0.0;
+    double* d = &st->imurec[(size_t)((st->imu_head + pa.new_imu) % kMaxWin) * kBaImuRec];
+    for (int e = t; e < kBaImuRec; e += blockDim.x) d[e] = pa.rec[e];
+  }
+}
+
 }  // namespace vg

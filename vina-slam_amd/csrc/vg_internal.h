@@ -144,7 +144,8 @@ enum {
   kCntSub = 7, kCntEvents = 8, kCntFactors = 9, kCntCreate = 10, kCntErr = 11, kCntLeaves = 12, kCntMisc = 13, kCntSeg = 14, kCntRoots = 15,
   kCntGTouched = 16, kCntGSlide = 17,  // all-reduced copies (sharded mode) for the thread_num quirks
   kCntPlaneUpd = 18, kCntFixFull = 19,  // margi: plane_update calls, leaves with pcr_fix.N >= max_points
-  kCntN = 20
+  kCntSlideBase = 20,                   // insert: surf_map_slide size before the scan's roots
+  kCntN = 21
 };
 
 // per-scan work buffers
@@ -210,6 +211,12 @@ struct DState {
   // (imu_head + k) % kMaxWin, so the slide is one index step
   int imu_head, pad_h[3];
   double imurec[kMaxWin * kBaImuRec];
+};
+// x_buf.push_back(x_curr) + a new IMU_PRE record, as kernel arguments (k_push_state,
+// or folded into the insert's first launch, map_insert)
+struct PushArg {
+  int ord, new_imu;
+  double rec[kBaImuRec];
 };
 // Spatial-tile sharding of one sequence over `world` contexts (one per GPU):
 // every context keeps the root voxels of the tiles it owns (tile_owner) and
@@ -429,9 +436,13 @@ int map_reset(vg_ctx* ctx);
 int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
                    hipEvent_t ev0, hipEvent_t ev1, int tag = 0);
 // all four iterations; replays the captured graph when possible
-int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank);
+// begin_xc != nullptr: open the scan on the device first (x_curr after
+// propagation, one launch with the scan binding)
+int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank,
+             const double* begin_xc = nullptr);
 constexpr int kNeedInsertReplay = 1;  // map_recut: the insert overflowed k_ins_alloc, replay it first
-int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num);
+// push: the window push to fold into the insert's first launch (or nullptr)
+int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num, const PushArg* push = nullptr);
 int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num);
 int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay = false,
               int pub_seq = 0);
@@ -444,7 +455,9 @@ int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thr
 int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, int pub_seq, int pub_seq2);
 // state.hip
 int state_alloc(vg_ctx* ctx);
-int state_scan_begin(vg_ctx* ctx, const double* xc249);
+// x_curr / x_prop / IEKF flags; with x != nullptr also the scan the IEKF reads
+int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x = nullptr, const float* y = nullptr,
+                     const float* z = nullptr, int n = 0);
 int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n);
 int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec);  // imurec: kBaImuRec doubles (new_imu >= 0)
 int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot);
