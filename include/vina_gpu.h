@@ -53,7 +53,17 @@ typedef struct vg_config {
   int win_size;                     /* LocalBA.win_size */
   int thread_num;                   /* LocalBA.thread_num: only its semantic quirks (voxel_map.cpp:96-97, local_mapping.cpp:27,93) */
   int if_BA;                        /* General.if_BA (default 0, node.cpp:96) */
-  int reserved0, reserved1, reserved2;
+  int reserved0, reserved1;
+  /* 1: cold start — the reference's initialisation (node.cpp:293-366, SURVEY
+   * row f2) runs on the first scans: IMU_init (+ gravity scale), then per scan
+   * the kd-tree LIO (A14) until the window is full, then motion_init (map
+   * rounds with the gravity-optimising BA, align_gravity, gravity-norm and
+   * degeneracy checks; failure -> system_reset); the steady state follows.
+   * Scans given with per-point times (vg_step_deskew*) are deskewed as the
+   * reference's; without, every point is at pcl_end_time. Only the whole-scan
+   * entry points (vg_step*) may be used until vg_stats::init_phase reports 3.
+   * 0: start from vg_seed's state on an empty map. */
+  int cold_start;
   /* IMUEKF::scale_gravity / imupre_scale_gravity (ekf_imu.hpp:27,
    * imu_preintegration.cpp:3): every accelerometer sample is multiplied by it
    * in the propagation (imu_ekf.cpp:51) and the preintegration
@@ -85,6 +95,12 @@ typedef struct vg_stats {
   int iekf_planes[4];
   int v_ins;
   int ba_hess;
+  /* cold start (vg_config::cold_start): 0 steady state, 1 IMU_init consumed
+   * the scan, 2 initialisation-window scan (kd-tree LIO), 3 motion_init
+   * succeeded on this scan (which then ran the window tail too), 4 motion_init
+   * failed (system_reset); motion_init rounds run on this scan; the kd-tree
+   * LIO's valid correspondences (-1: the scan seeded the map) */
+  int init_phase, init_rounds, init_valid;
 } vg_stats;
 
 typedef struct vg_ctx vg_ctx;
@@ -105,6 +121,15 @@ int vg_reset(vg_ctx* ctx);
  * is identical, bit-for-bit). Returns the voxel count in *n_out. */
 int vg_downsample(vg_ctx* ctx, const float* xyz, const float* intensity, int n, double voxel_size,
                   float* out_xyzic, int* n_out);
+/* f2 — down_sampling_close (include/vina_slam/core/point_utils.hpp:46-113) +
+ * the time sort of VINA_SLAM::initialization (node.cpp:337-345): per voxel the
+ * input point nearest the float mean of the voxel's points. time: n floats
+ * (may be NULL: every point at time 0). out_xyzt: n x 4 floats [x, y, z, time]
+ * sorted by time; equal times in ascending voxel-key order (the reference
+ * std::sorts its unordered_map order, leaving their order unspecified).
+ * Synchronous; drains the pipeline first (diagnostic / test entry point). */
+int vg_downsample_close(vg_ctx* ctx, const float* xyz, const float* time, int n, double voxel_size, float* out_xyzt,
+                        int* n_out);
 
 /* Per-scan pipeline — the steady-state branch of
  * VINA_SLAM::thd_odometry_localmapping (local_mapping.cpp:389-547):

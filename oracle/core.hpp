@@ -210,8 +210,13 @@ struct PointType {
 };
 
 // down_sampling_voxel — point_utils.hpp:7-44. Output order = unordered_map
-// iteration order (libstdc++, same hash), exactly as the reference.
-inline void down_sampling_voxel(std::vector<PointType>& pl, double voxel_size) {
+// iteration order (libstdc++, same hash), exactly as the reference; or, with
+// key_order, ascending (x, y, z) voxel key (the device's order). The
+// initialisation path uses key order: its kd map is re-downsampled after every
+// scan, so the order of the points inside a voxel — which the reference leaves
+// to the standard library's hash-table layout — sets the float means bit for
+// bit, and only a fixed order makes the cold start reproducible.
+inline void down_sampling_voxel(std::vector<PointType>& pl, double voxel_size, bool key_order = false) {
   if (voxel_size < 0.001) return;
   VoxMap<PointType> feat_map;
   float loc[3];
@@ -235,7 +240,17 @@ inline void down_sampling_voxel(std::vector<PointType>& pl, double voxel_size) {
     }
   }
   pl.clear();
-  for (auto& kv : feat_map) pl.push_back(kv.second);
+  if (!key_order) {
+    for (auto& kv : feat_map) pl.push_back(kv.second);
+    return;
+  }
+  std::vector<std::pair<VOXEL_LOC, PointType>> v(feat_map.begin(), feat_map.end());
+  std::sort(v.begin(), v.end(), [](const std::pair<VOXEL_LOC, PointType>& a, const std::pair<VOXEL_LOC, PointType>& b) {
+    if (a.first.x != b.first.x) return a.first.x < b.first.x;
+    if (a.first.y != b.first.y) return a.first.y < b.first.y;
+    return a.first.z < b.first.z;
+  });
+  for (auto& kv : v) pl.push_back(kv.second);
 }
 
 // calcBodyVar — point_utils.cpp:3-34

@@ -729,6 +729,30 @@ double IMU_PRE::give_evaluate(const IMUST& st1, const IMUST& st2, Mat<30, 30>& j
   return dot(rr, cov_inv * rr);
 }
 
+// give_evaluate_g — imu_preintegration.cpp:165-237: give_evaluate's residual
+// plus the gravity Jacobian jocg (rows 3-8) of the shared gravity unknowns
+double IMU_PRE::give_evaluate_g(const IMUST& st1, const IMUST& st2, Mat<33, 33>& jtj, Mat<33, 1>& gg,
+                                bool jac) const {
+  Mat<30, 30> j30;
+  Mat<30, 1> g30;
+  V15 rr;
+  Mat<15, 30> joc;
+  const double cost = give_evaluate(st1, st2, j30, g30, jac, &rr, &joc);
+  if (jac) {
+    Mat<15, 33> J;
+    for (int r = 0; r < 15; r++)
+      for (int c = 0; c < 30; c++) J(r, c) = joc(r, c);
+    const double dt = dtime;
+    J.setBlock(3, 30, st1.R.T() * (-0.5 * dt * dt));
+    J.setBlock(6, 30, st1.R.T() * (-dt));
+    const M15 cov_inv = inverse(cov);
+    const Mat<33, 15> jT = J.T();
+    jtj = (jT * cov_inv) * J;
+    gg = (jT * cov_inv) * rr;
+  }
+  return cost;
+}
+
 // update_state — imu_preintegration.cpp:239-246
 void IMU_PRE::update_state(const V15& dxi) {
   dbg_buf = dbg;
@@ -932,6 +956,178 @@ int LI_BA_Optimizer::damping_iter(std::vector<IMUST>& xs, LidarFactor& vox, std:
     if (std::fabs((residual1 - residual2) / residual1) < 1e-6) break;
   }
   return it;
+}
+
+// ---------------------------------------------------------------- LI_BA_OptimizerGravity
+// hess_plus — optimizers.cpp:629-638
+void LI_BA_OptimizerGravity::hess_plus(MatX& Hess, std::vector<double>& JacT, const MatX& hs,
+                                       const std::vector<double>& js) {
+  for (int i = 0; i < win_size; i++) {
+    for (int r = 0; r < 6; r++) JacT[i * DIM + r] += js[i * 6 + r];
+    for (int j = 0; j < win_size; j++)
+      for (int r = 0; r < 6; r++)
+        for (int c = 0; c < 6; c++) Hess(i * DIM + r, j * DIM + c) += hs(i * 6 + r, j * 6 + c);
+  }
+}
+
+// divide_thread — optimizers.cpp:640-707
+double LI_BA_OptimizerGravity::divide_thread(std::vector<IMUST>& xs, LidarFactor& vox, std::vector<IMU_PRE*>& imus,
+                                             MatX& Hess, std::vector<double>& JacT) {
+  const int thd_num = 5;
+  double residual = 0;
+  Hess.setZero();
+  std::fill(JacT.begin(), JacT.end(), 0.0);
+  std::vector<MatX> hessians(thd_num, MatX(jac_leng, jac_leng));
+  std::vector<std::vector<double>> jacobins(thd_num, std::vector<double>(jac_leng, 0.0));
+  std::vector<double> resis(thd_num, 0);
+  int tthd_num = thd_num;
+  const int g_size = (int)vox.plvec_voxels.size();
+  if (g_size < tthd_num) tthd_num = 1;
+  const double part = 1.0 * g_size / tthd_num;
+  std::vector<std::thread> th;
+  for (int i = 1; i < tthd_num; i++) {
+    const int head = (int)(part * i), tail = (int)(part * (i + 1));
+    if (use_threads)
+      th.emplace_back([&, i, head, tail]() { vox.acc_evaluate2(xs, head, tail, hessians[i], jacobins[i], resis[i]); });
+    else
+      vox.acc_evaluate2(xs, head, tail, hessians[i], jacobins[i], resis[i]);
+  }
+  const int g0 = imu_leng - 3;
+  Mat<33, 33> jtj;
+  Mat<33, 1> gg;
+  for (int i = 0; i < win_size - 1; i++) {
+    jtj.setZero();
+    gg.setZero();
+    residual += imus[i]->give_evaluate_g(xs[i], xs[i + 1], jtj, gg, true);
+    for (int r = 0; r < 2 * DIM; r++) {
+      for (int c = 0; c < 2 * DIM; c++) Hess(i * DIM + r, i * DIM + c) += jtj(r, c);
+      for (int c = 0; c < 3; c++) Hess(i * DIM + r, g0 + c) += jtj(r, 2 * DIM + c);
+    }
+    for (int r = 0; r < 3; r++) {
+      for (int c = 0; c < 2 * DIM; c++) Hess(g0 + r, i * DIM + c) += jtj(2 * DIM + r, c);
+      for (int c = 0; c < 3; c++) Hess(g0 + r, g0 + c) += jtj(2 * DIM + r, 2 * DIM + c);
+    }
+    for (int r = 0; r < 2 * DIM; r++) JacT[i * DIM + r] += gg[r];
+    for (int r = 0; r < 3; r++) JacT[g0 + r] += gg[2 * DIM + r];
+  }
+  for (double& h : Hess.d) h *= mpar->imu_coef;
+  for (double& j : JacT) j *= mpar->imu_coef;
+  residual *= (mpar->imu_coef * 0.5);
+  vox.acc_evaluate2(xs, 0, (int)part, hessians[0], jacobins[0], resis[0]);
+  for (auto& t : th) t.join();
+  for (int i = 0; i < tthd_num; i++) {
+    hess_plus(Hess, JacT, hessians[i], jacobins[i]);
+    residual += resis[i];
+  }
+  return residual;
+}
+
+// only_residual — optimizers.cpp:709-743
+double LI_BA_OptimizerGravity::only_residual(std::vector<IMUST>& xs, LidarFactor& vox, std::vector<IMU_PRE*>& imus) {
+  double residual1 = 0, residual2 = 0;
+  Mat<33, 33> jtj;
+  Mat<33, 1> gg;
+  int thd_num = 5;
+  std::vector<double> residuals(thd_num, 0);
+  const int g_size = (int)vox.plvec_voxels.size();
+  if (g_size < thd_num) thd_num = 1;
+  const double part = 1.0 * g_size / thd_num;
+  std::vector<std::thread> th;
+  for (int i = 1; i < thd_num; i++) {
+    const int head = (int)(part * i), tail = (int)(part * (i + 1));
+    if (use_threads)
+      th.emplace_back([&, i, head, tail]() { vox.evaluate_only_residual(xs, head, tail, residuals[i]); });
+    else
+      vox.evaluate_only_residual(xs, head, tail, residuals[i]);
+  }
+  for (int i = 0; i < win_size - 1; i++) residual1 += imus[i]->give_evaluate_g(xs[i], xs[i + 1], jtj, gg, false);
+  residual1 *= (mpar->imu_coef * 0.5);
+  vox.evaluate_only_residual(xs, 0, (int)part, residuals[0]);
+  for (auto& t : th) t.join();
+  for (int i = 0; i < thd_num; i++) residual2 += residuals[i];
+  return residual1 + residual2;
+}
+
+// damping_iter — optimizers.cpp:745-826. Faithful to its state handling:
+// x_stats_temp is initialised once, so a rejected step's gravity increment
+// stays in x_stats_temp[0].g for the next trial (line 775)
+void LI_BA_OptimizerGravity::damping_iter(std::vector<IMUST>& xs, LidarFactor& vox, std::vector<IMU_PRE*>& imus,
+                                          std::vector<double>& resis, int max_iter) {
+  win_size = vox.win_size;
+  jac_leng = win_size * 6;
+  imu_leng = win_size * DIM + 3;
+  double u = 0.01, v = 2;
+  MatX Hess(imu_leng, imu_leng);
+  std::vector<double> JacT(imu_leng, 0.0), D(imu_leng, 0.0);
+  double residual1 = 0, residual2 = 0, q;
+  bool is_calc_hess = true;
+  std::vector<IMUST> xs_temp = xs;
+  MatX Hcalc;
+  std::vector<double> Jcalc;
+  for (int i = 0; i < max_iter; i++) {
+    if (is_calc_hess) {
+      residual1 = divide_thread(xs, vox, imus, Hess, JacT);
+      Hcalc = Hess;
+      Jcalc = JacT;
+    } else {
+      Hess = Hcalc;  // the gauged rows below are rewritten identically
+      JacT = Jcalc;
+    }
+    if (i == 0) resis.push_back(residual1);
+    for (int r = 0; r < 6; r++)
+      for (int c = 0; c < imu_leng; c++) {
+        Hess(r, c) = 0;
+        Hess(c, r) = 0;
+      }
+    for (int r = 0; r < 6; r++) Hess(r, r) = 1;
+    for (int r = 0; r < 6; r++) JacT[r] = 0;
+    for (int r = 0; r < imu_leng; r++) D[r] = Hess(r, r);
+    MatX A = Hess;
+    for (int r = 0; r < imu_leng; r++) A(r, r) += u * D[r];
+    std::vector<double> mJ(imu_leng);
+    for (int r = 0; r < imu_leng; r++) mJ[r] = -JacT[r];
+    const std::vector<double> dxi = ldlt_solve(A, mJ);
+    for (int k = 0; k < 3; k++) xs_temp[0].g[k] += dxi[imu_leng - 3 + k];
+    for (int j = 0; j < win_size; j++) {
+      xs_temp[j].R = xs[j].R * Exp(v3(dxi[DIM * j], dxi[DIM * j + 1], dxi[DIM * j + 2]));
+      for (int k = 0; k < 3; k++) {
+        xs_temp[j].p[k] = xs[j].p[k] + dxi[DIM * j + 3 + k];
+        xs_temp[j].v[k] = xs[j].v[k] + dxi[DIM * j + 6 + k];
+        xs_temp[j].bg[k] = xs[j].bg[k] + dxi[DIM * j + 9 + k];
+        xs_temp[j].ba[k] = xs[j].ba[k] + dxi[DIM * j + 12 + k];
+      }
+      xs_temp[j].g = xs_temp[0].g;
+    }
+    for (int j = 0; j < win_size - 1; j++) {
+      V15 d;
+      for (int k = 0; k < DIM; k++) d[k] = dxi[DIM * j + k];
+      imus[j]->update_state(d);
+    }
+    double q1 = 0;  // 0.5 * dxi.dot(u * D * dxi - JacT)
+    for (int r = 0; r < imu_leng; r++) q1 += dxi[r] * (u * D[r] * dxi[r] - JacT[r]);
+    q1 *= 0.5;
+    residual2 = only_residual(xs_temp, vox, imus);
+    q = residual1 - residual2;
+    if (q > 0) {
+      xs = xs_temp;
+      const double one_three = 1.0 / 3;
+      q = q / q1;
+      v = 2;
+      q = 1 - std::pow(2 * q - 1, 3);
+      u *= (q < one_three ? one_three : q);
+      is_calc_hess = true;
+    } else {
+      u = u * v;
+      v = 2 * v;
+      is_calc_hess = false;
+      for (int j = 0; j < win_size - 1; j++) {
+        imus[j]->dbg = imus[j]->dbg_buf;
+        imus[j]->dba = imus[j]->dba_buf;
+      }
+    }
+    if (std::fabs((residual1 - residual2) / residual1) < 1e-6) break;
+  }
+  resis.push_back(residual2);
 }
 
 }  // namespace orc

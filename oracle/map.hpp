@@ -204,6 +204,8 @@ struct IMU_PRE {
   void add_imu(V3 gyr, V3 acc, double dt);
   double give_evaluate(const IMUST& st1, const IMUST& st2, Mat<30, 30>& jtj, Mat<30, 1>& gg, bool jac,
                        V15* rr_out = nullptr, Mat<15, 30>* joc_out = nullptr) const;
+  // with the 3 gravity columns (imu_preintegration.cpp:165-237): jtj 33 x 33, gg 33
+  double give_evaluate_g(const IMUST& st1, const IMUST& st2, Mat<33, 33>& jtj, Mat<33, 1>& gg, bool jac) const;
   void update_state(const V15& dxi);
 };
 
@@ -217,6 +219,21 @@ struct LI_BA_Optimizer {
                        std::vector<double>& JacT);
   double only_residual(std::vector<IMUST>& xs, LidarFactor& vox, std::vector<IMU_PRE*>& imus);
   int damping_iter(std::vector<IMUST>& xs, LidarFactor& vox, std::vector<IMU_PRE*>& imus);
+};
+
+// LI_BA_OptimizerGravity — optimizers.cpp:629-826 (initialisation only): the
+// same LM with a shared gravity vector as 3 extra unknowns and only frame 0's
+// rotation / position gauged
+struct LI_BA_OptimizerGravity {
+  MapParams* mpar;
+  int win_size = 0, jac_leng = 0, imu_leng = 0;
+  bool use_threads = true;
+  void hess_plus(MatX& Hess, std::vector<double>& JacT, const MatX& hs, const std::vector<double>& js);
+  double divide_thread(std::vector<IMUST>& xs, LidarFactor& vox, std::vector<IMU_PRE*>& imus, MatX& Hess,
+                       std::vector<double>& JacT);
+  double only_residual(std::vector<IMUST>& xs, LidarFactor& vox, std::vector<IMU_PRE*>& imus);
+  void damping_iter(std::vector<IMUST>& xs, LidarFactor& vox, std::vector<IMU_PRE*>& imus,
+                    std::vector<double>& resis, int max_iter);
 };
 
 }  // namespace orc

@@ -19,7 +19,8 @@ class Stats(ctypes.Structure):
     _fields_ = [("n_raw", ctypes.c_int), ("n_ds", ctypes.c_int), ("iekf_iters", ctypes.c_int),
                 ("iekf_matches", ctypes.c_int * 4), ("roots_new", ctypes.c_int), ("n_slide", ctypes.c_int),
                 ("n_factors", ctypes.c_int), ("ba_iters", ctypes.c_int), ("degenerate", ctypes.c_int),
-                ("plane_updates", ctypes.c_int), ("fix_full", ctypes.c_int)]
+                ("plane_updates", ctypes.c_int), ("fix_full", ctypes.c_int), ("init_phase", ctypes.c_int),
+                ("init_rounds", ctypes.c_int), ("init_valid", ctypes.c_int)]
 
 
 # int (*)(double* buf, int n, void* user): in-place sum over the ranks
@@ -48,6 +49,7 @@ def lib():
         L.orc_voxel_hash.argtypes = [ctypes.c_int64] * 3
         L.orc_voxel_hash.restype = ctypes.c_size_t
         L.orc_downsample.argtypes = [fp, fp, ctypes.c_int, ctypes.c_double, fp, ip]
+        L.orc_down_sampling_close.argtypes = [fp, fp, ctypes.c_int, ctypes.c_double, fp]
         L.orc_calc_body_var.argtypes = [dp, ctypes.c_double, ctypes.c_double, dp, dp]
         L.orc_eig3.argtypes = [dp, dp, dp]
         L.orc_inverse15.argtypes = [dp, dp]
@@ -107,6 +109,15 @@ def downsample(xyz, inten, size):
     n = ctypes.c_int(0)
     lib().orc_downsample(_f(xyz), _f(inten), xyz.shape[0], size, _f(out), ctypes.byref(n))
     return out[: n.value]
+
+
+def down_sampling_close(xyz, times, size):
+    """down_sampling_close + the init's time sort; (m,4) [x,y,z,t], equal times in voxel-key order."""
+    xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+    t = None if times is None else np.ascontiguousarray(times, dtype=np.float32)
+    out = np.zeros((xyz.shape[0], 4), dtype=np.float32)
+    m = lib().orc_down_sampling_close(_f(xyz), None if t is None else _f(t), xyz.shape[0], size, _f(out))
+    return out[:m]
 
 
 def eig3(A):

@@ -146,12 +146,13 @@ struct Pipeline {
       ap.z = (float)pv.pnt[2];
       pl_tree.push_back(ap);
     }
-    down_sampling_voxel(pl_tree, 0.5);
+    down_sampling_voxel(pl_tree, 0.5, true);
     return valid;
   }
 
   explicit Pipeline(const orc_config& c) : voxhess(c.win_size) {
     cfg = c;
+    motion_init_flag = c.cold_start != 0;
     mpar.voxel_size = c.voxel_size;
     mpar.max_layer = c.max_layer;
     mpar.max_points = c.max_points;
@@ -490,6 +491,54 @@ struct Pipeline {
     }
   }
 
+  // local_mapping.cpp:489-546: with a full window, LI_BA damping_iter, x_curr.R/p
+  // from the window's last frame, multi_margi, jour, the mp ring and the slide
+  template <class TP>
+  void window_tail(TP* t5, TP* t6) {
+    using clk = std::chrono::steady_clock;
+    if (cfg.if_BA == 1) {
+      LI_BA_Optimizer opt;
+      opt.mpar = &mpar;
+      opt.use_threads = cfg.use_threads != 0;
+      st.ba_iters = opt.damping_iter(x_buf, voxhess, imu_pre_buf);
+    }
+    x_curr.R = x_buf[win_count - 1].R;
+    x_curr.p = x_buf[win_count - 1].p;
+    *t5 = clk::now();
+    mpar.cnt_plane_update = 0;
+    mpar.cnt_fix_full = 0;
+    multi_margi();
+    st.plane_updates = mpar.cnt_plane_update;
+    st.fix_full = mpar.cnt_fix_full;
+    *t6 = clk::now();
+    const int mgsize = 1;
+    if ((win_base + win_count) % 10 == 0) {
+      double spat = norm(x_curr.p - last_pos);
+      if (spat > 0.5) {
+        jour += spat;
+        last_pos = x_curr.p;
+      }
+    }
+    for (int i = 0; i < cfg.win_size; i++) {
+      mpar.mp[i] += mgsize;
+      if (mpar.mp[i] >= cfg.win_size) mpar.mp[i] -= cfg.win_size;
+    }
+    for (int i = mgsize; i < win_count; i++) {
+      x_buf[i - mgsize] = x_buf[i];
+      std::swap(pvec_buf[i - mgsize], pvec_buf[i]);
+    }
+    for (int i = win_count - mgsize; i < win_count; i++) {
+      x_buf.pop_back();
+      pvec_buf.pop_back();
+      delete imu_pre_buf.front();
+      imu_pre_buf.erase(imu_pre_buf.begin());
+    }
+    win_base += mgsize;
+    win_count -= mgsize;
+  }
+
+#include "init.inc"
+
   // One scan of thd_odometry_localmapping's steady-state branch,
   // local_mapping.cpp:389-547 (initialisation, SURVEY row f2, is replaced by a
   // seeded state and an empty map).
@@ -499,6 +548,23 @@ struct Pipeline {
     auto t0 = clk::now();
     memset(&st, 0, sizeof(st));
     imu_poses.clear();
+    if (motion_init_flag) {  // local_mapping.cpp:362-386: the initialisation branch
+      const int r = initialization(imus, xyz_in, inten, times, n, beg, end);
+      st.init_phase = init_phase;
+      if (r != 1) {
+        if (r == -1) system_reset(imus);
+        if (timing) timing[6] = std::chrono::duration<double>(clk::now() - t0).count();
+        return 0;
+      }
+      motion_init_flag = false;  // init success: the same scan continues into the window tail
+      st.n_factors = (int)voxhess.plvec_voxels.size();
+      st.roots_new = (int)surf_map.size();
+      auto t5 = clk::now(), t6 = t5;
+      if (win_count >= cfg.win_size) window_tail(&t5, &t6);
+      st.n_slide = (int)surf_map_slide.size();
+      if (timing) timing[6] = std::chrono::duration<double>(clk::now() - t0).count();
+      return 0;
+    }
     if (!first) propagate(imus, beg, end);
     else { x_curr.t = end; last_pcl_end_time = end; }
     std::vector<float> xyz_d;
@@ -553,47 +619,7 @@ struct Pipeline {
     st.n_factors = (int)voxhess.plvec_voxels.size();
     auto t4 = clk::now();
     auto t5 = t4, t6 = t4;
-    if (win_count >= cfg.win_size) {
-      if (cfg.if_BA == 1) {
-        LI_BA_Optimizer opt;
-        opt.mpar = &mpar;
-        opt.use_threads = cfg.use_threads != 0;
-        st.ba_iters = opt.damping_iter(x_buf, voxhess, imu_pre_buf);
-      }
-      x_curr.R = x_buf[win_count - 1].R;
-      x_curr.p = x_buf[win_count - 1].p;
-      t5 = clk::now();
-      mpar.cnt_plane_update = 0;
-      mpar.cnt_fix_full = 0;
-      multi_margi();
-      st.plane_updates = mpar.cnt_plane_update;
-      st.fix_full = mpar.cnt_fix_full;
-      t6 = clk::now();
-      const int mgsize = 1;
-      if ((win_base + win_count) % 10 == 0) {
-        double spat = norm(x_curr.p - last_pos);
-        if (spat > 0.5) {
-          jour += spat;
-          last_pos = x_curr.p;
-        }
-      }
-      for (int i = 0; i < cfg.win_size; i++) {
-        mpar.mp[i] += mgsize;
-        if (mpar.mp[i] >= cfg.win_size) mpar.mp[i] -= cfg.win_size;
-      }
-      for (int i = mgsize; i < win_count; i++) {
-        x_buf[i - mgsize] = x_buf[i];
-        std::swap(pvec_buf[i - mgsize], pvec_buf[i]);
-      }
-      for (int i = win_count - mgsize; i < win_count; i++) {
-        x_buf.pop_back();
-        pvec_buf.pop_back();
-        delete imu_pre_buf.front();
-        imu_pre_buf.erase(imu_pre_buf.begin());
-      }
-      win_base += mgsize;
-      win_count -= mgsize;
-    }
+    if (win_count >= cfg.win_size) window_tail(&t5, &t6);
     first = false;
     st.n_slide = (int)surf_map_slide.size();
     auto t7 = clk::now();
@@ -661,6 +687,26 @@ void orc_voxel_key_d(const double* xyz, int n, double size, int64_t* out) {
 }
 
 size_t orc_voxel_hash(int64_t x, int64_t y, int64_t z) { return VoxHash()(VOXEL_LOC(x, y, z)); }
+
+// down_sampling_close + the stable time sort of initialization (node.cpp:337-345)
+int orc_down_sampling_close(const float* xyz, const float* times, int n, double size, float* out_xyzt) {
+  std::vector<PointType> pl(n);
+  for (int i = 0; i < n; i++) {
+    pl[i].x = xyz[3 * i];
+    pl[i].y = xyz[3 * i + 1];
+    pl[i].z = xyz[3 * i + 2];
+    pl[i].curvature = times ? times[i] : 0.f;
+  }
+  Pipeline::down_sampling_close(pl, size);
+  std::stable_sort(pl.begin(), pl.end(), [](const PointType& a, const PointType& b) { return a.curvature < b.curvature; });
+  for (size_t i = 0; i < pl.size(); i++) {
+    out_xyzt[4 * i] = pl[i].x;
+    out_xyzt[4 * i + 1] = pl[i].y;
+    out_xyzt[4 * i + 2] = pl[i].z;
+    out_xyzt[4 * i + 3] = pl[i].curvature;
+  }
+  return (int)pl.size();
+}
 
 int orc_downsample(const float* xyz, const float* inten, int n, double size, float* out_xyzic, int* n_out) {
   std::vector<PointType> pl(n);

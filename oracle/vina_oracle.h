@@ -31,7 +31,8 @@ typedef struct orc_config {
   int if_BA;                      /* General.if_BA (default 0) */
   int use_threads;                /* oracle only: spawn real std::threads */
   int vnc_prep;                   /* oracle only: run the dead VNC prep (cost fidelity) */
-  int pad;
+  int cold_start;                 /* 1: the reference's initialisation (IMU_init, kd-tree LIO, motion_init;
+                                     SURVEY row f2) instead of a seeded state */
   double scale_gravity;           /* IMUEKF::scale_gravity = imupre_scale_gravity (imu_ekf.cpp:51,
                                      imu_preintegration.cpp:51); 0 is read as 1 */
 } orc_config;
@@ -40,11 +41,17 @@ typedef struct orc_stats {
   int n_raw, n_ds, iekf_iters, iekf_matches[4];
   int roots_new, n_slide, n_factors, ba_iters, degenerate;
   int plane_updates, fix_full; /* margi branch counters (octree.cpp:441-446, 461-469) */
+  int init_phase;   /* cold start: 0 steady state, 1 IMU_init consumed the scan, 2 init-window scan
+                       (kd-tree LIO), 3 motion_init succeeded (the scan ran the window tail too),
+                       4 motion_init failed (system_reset) */
+  int init_rounds;  /* motion_init rounds run on this scan */
+  int init_valid;   /* init-window scan: kd-tree LIO correspondences (-1 = map seeded) */
 } orc_stats;
 
 void orc_voxel_key_d(const double* xyz, int n, double size, int64_t* out);
 size_t orc_voxel_hash(int64_t x, int64_t y, int64_t z);
 int orc_downsample(const float* xyz, const float* inten, int n, double size, float* out_xyzic, int* n_out);
+int orc_down_sampling_close(const float* xyz, const float* times, int n, double size, float* out_xyzt);
 void orc_calc_body_var(const double* p, double range_inc, double degree_inc, double* pnt_out, double* var_out);
 void orc_eig3(const double* A, double* w, double* V);
 void orc_inverse15(const double* A, double* out);

@@ -35,7 +35,7 @@ def test_config_struct_layout_matches_header(tmp_path):
     in vg_config's reserved slots)."""
     from vgconfig import CConfig
     names = [f for f, _ in CConfig._fields_]
-    hdr = {"use_threads": "reserved0", "vnc_prep": "reserved1", "pad": "reserved2"}
+    hdr = {"use_threads": "reserved0", "vnc_prep": "reserved1"}
     size, offs = _c_layout(tmp_path, "vg_config", [hdr.get(f, f).split("[")[0] for f in names])
     assert ctypes.sizeof(CConfig) == size
     assert [getattr(CConfig, f).offset for f in names] == offs

@@ -29,6 +29,8 @@
 // enqueues two iterations at a time and reads `done` in between.
 #include "vg_dev.h"
 
+#include "vg_imu.h"  // imu_residual (host and device)
+
 namespace vg {
 
 constexpr int kMaxW = 16;
@@ -67,64 +69,6 @@ __device__ __forceinline__ void factor_basics(const double* e, const Clu& pcr, d
   f[21] = (double)pcr.N;
   f[22] = 1.0;  // coe (octree.cpp:507)
   f[23] = e[0];
-}
-
-// IMU record layout (doubles): R_delta 9, p_delta 3, v_delta 3, R_bg 9, p_bg 9,
-// p_ba 9, v_bg 9, v_ba 9, dtime 1 (=61), pad to 64, cov_inv 225.
-// bias state per factor: dbg 3, dba 3, dbg_buf 3, dba_buf 3.
-__device__ void imu_residual(const double* rec, const double* bias, const double* x1, const double* x2, double* rr,
-                             double* joc /*15x30 or null*/) {
-  const M3 Rd = ld_m3(rec), Rbg = ld_m3(rec + 15), pbg = ld_m3(rec + 24), pba = ld_m3(rec + 33),
-           vbg = ld_m3(rec + 42), vba = ld_m3(rec + 51);
-  const V3 pd = ld_v3(rec + 9), vd = ld_v3(rec + 12);
-  const double dtime = rec[60];
-  const V3 dbg = ld_v3(bias), dba = ld_v3(bias + 3);
-  const M3 R1 = ld_m3(x1), R2 = ld_m3(x2);
-  const V3 p1 = ld_v3(x1 + 9), p2 = ld_v3(x2 + 9), v1 = ld_v3(x1 + 12), v2 = ld_v3(x2 + 12);
-  const V3 bg1 = ld_v3(x1 + 15), bg2 = ld_v3(x2 + 15), ba1 = ld_v3(x1 + 18), ba2 = ld_v3(x2 + 18);
-  const V3 g1 = ld_v3(x1 + 21);
-  M3 Rc = mul(Rd, Exp(mul(Rbg, dbg)));
-  V3 tc = add(add(pd, mul(pbg, dbg)), mul(pba, dba));
-  V3 vc = add(add(vd, mul(vbg, dbg)), mul(vba, dba));
-  M3 res_r = mul(mul(tr(Rc), tr(R1)), R2);
-  V3 exp_v = mul(tr(R1), sub(sub(v2, v1), scl(g1, dtime)));
-  V3 res_v = sub(exp_v, vc);
-  V3 exp_t = mul(tr(R1), sub(sub(sub(p2, p1), scl(v1, dtime)), scl(g1, 0.5 * dtime * dtime)));
-  V3 res_t = sub(exp_t, tc);
-  V3 lr = Log(res_r);
-  for (int k = 0; k < 3; k++) {
-    rr[k] = lr[k];
-    rr[3 + k] = res_t[k];
-    rr[6 + k] = res_v[k];
-    rr[9 + k] = bg2[k] - bg1[k];
-    rr[12 + k] = ba2[k] - ba1[k];
-  }
-  if (!joc) return;
-  for (int k = 0; k < 450; k++) joc[k] = 0.0;
-  auto put = [&](int r0, int c0, const M3& m) {
-    for (int r = 0; r < 3; r++)
-      for (int c = 0; c < 3; c++) joc[(r0 + r) * 30 + c0 + c] = m(r, c);
-  };
-  const M3 JRi = jr_inv(res_r);
-  const M3 R1t = tr(R1);
-  put(0, 0, scl(mul(mul(JRi, tr(R2)), R1), -1.0));
-  put(0, 15, JRi);
-  put(0, 9, scl(mul(mul(mul(JRi, tr(res_r)), jr(mul(Rbg, dbg))), Rbg), -1.0));
-  put(3, 0, hat(exp_t));
-  put(3, 3, scl(R1t, -1.0));
-  put(3, 6, scl(R1t, -dtime));
-  put(3, 9, scl(pbg, -1.0));
-  put(3, 12, scl(pba, -1.0));
-  put(3, 18, R1t);
-  put(6, 0, hat(exp_v));
-  put(6, 6, scl(R1t, -1.0));
-  put(6, 9, scl(vbg, -1.0));
-  put(6, 12, scl(vba, -1.0));
-  put(6, 21, R1t);
-  put(9, 9, scl(M3::I(), -1.0));
-  put(12, 12, scl(M3::I(), -1.0));
-  put(9, 24, M3::I());
-  put(12, 27, M3::I());
 }
 
 // IMU record k of DState's ring (pushed by k_push_state, slid by moving the head)
@@ -1264,6 +1208,74 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
       }
     }
   (void)g_dummy;
+  return VG_OK;
+}
+
+// ---- LiDAR factor passes for a host-driven LM (the initialisation's
+// LI_BA_OptimizerGravity, optimizers.cpp:640-743): the same kernels, no IMU
+// factors (the host evaluates those), synchronous.
+// poses: W x kX frame states (R 9, p 3, v 3, bg 3, ba 3, g 3) by ord.
+// out (Hessian pass): the 6W x 6W LiDAR Hessian as packed lower rows, then the
+// 6W gradient, then the residual (acc_evaluate2 summed over the factors);
+// out (residual pass): the residual (evaluate_only_residual, which also stores
+// each factor's eigen system and merged cluster at these poses, as the
+// reference's does).
+int ba_lidar_pass(vg_ctx* ctx, bool hessian, const double* poses, const int* mp_ring, double* out) {
+  const int W = ctx->cfg.win_size;
+  hipStream_t s = ctx->stream;
+  BaDev d = carve(ctx);
+  const int L = 6 * W, nout = L * (L + 1) / 2 + L + 1;
+  BaState bs;
+  memset(&bs, 0, sizeof(bs));
+  bs.calc_hess = 1;
+  int ring[kMaxW];
+  for (int i = 0; i < kMaxW; i++) ring[i] = i < W ? mp_ring[i] : 0;
+  double* h = ctx->h_stage;  // pinned staging
+  memcpy(h, poses, (size_t)W * kX * sizeof(double));
+  memcpy(h + W * kX, &bs, sizeof(bs));
+  memcpy(h + W * kX + 8, ring, sizeof(ring));
+  double* target = hessian ? d.xs : d.xt;
+  VG_HIP(hipMemcpyAsync(target, h, (size_t)W * kX * sizeof(double), hipMemcpyHostToDevice, s));
+  VG_HIP(hipMemcpyAsync(d.st, h + W * kX, sizeof(bs), hipMemcpyHostToDevice, s));
+  VG_HIP(hipMemcpyAsync(d.mpring, h + W * kX + 8, sizeof(ring), hipMemcpyHostToDevice, s));
+  const int* nfp = ctx->map.counters + kCntFactors;
+  if (hessian) {
+    const int G = std::min(kHessGridMax, ctx->ba.cap_f / hess_chunk(W) + 1);
+    k_ba_hess<<<G, kHessThreads, hess_lds_bytes(W), s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
+                                                        ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, 0, d.imurec,
+                                                        &ctx->st->imu_head, d.bias, d.imuout);
+    k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, d.hl, d.st);
+    VG_HIP(hipGetLastError());
+    VG_HIP(hipMemcpyAsync(h, d.hl, nout * sizeof(double), hipMemcpyDeviceToHost, s));
+    VG_HIP(hipStreamSynchronize(s));
+    memcpy(out, h, nout * sizeof(double));
+    return VG_OK;
+  }
+  const int nrb = kResidBlocks;
+  k_ba_resid<<<nrb, 256, 0, s>>>(nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
+                                 ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, 0, d.imurec, &ctx->st->imu_head,
+                                 d.bias, d.imures);
+  VG_HIP(hipGetLastError());
+  VG_HIP(hipMemcpyAsync(h, d.rpart, nrb * sizeof(double), hipMemcpyDeviceToHost, s));
+  VG_HIP(hipStreamSynchronize(s));
+  double r = 0.0;
+  for (int b = 0; b < nrb; b++) r += h[b];
+  *out = r;
+  return VG_OK;
+}
+
+// the factors' eigenvectors (column 0 = the plane normal) and count, host copy
+int ba_factor_normals(vg_ctx* ctx, std::vector<double>& normals) {
+  hipStream_t s = ctx->stream;  // stream-ordered: the context stream is non-blocking
+  VG_HIP(hipMemcpyAsync(ctx->h_pinned, ctx->map.counters + kCntFactors, sizeof(int), hipMemcpyDeviceToHost, s));
+  VG_HIP(hipStreamSynchronize(s));
+  const int nf = ctx->h_pinned[0];
+  std::vector<double> e((size_t)nf * 12);
+  if (nf > 0) VG_HIP(hipMemcpyAsync(e.data(), ctx->ba.fac_eig, e.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  VG_HIP(hipStreamSynchronize(s));
+  normals.resize((size_t)nf * 3);
+  for (int a = 0; a < nf; a++)
+    for (int k = 0; k < 3; k++) normals[(size_t)a * 3 + k] = e[(size_t)a * 12 + 3 + k * 3];  // U(k, 0), row-major
   return VG_OK;
 }
 

@@ -385,16 +385,23 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
 
 // ------------------------------------------------------------------ insert (A3/A4)
 // per downsampled point: var_init + pvec_update (world var), world point, root
-// key insert-or-find, first-occurrence marking of brand-new keys
+// key insert-or-find, first-occurrence marking of brand-new keys.
+// kPre (the initialisation's cut_voxel, initialization.cpp:229-246): body
+// points already motion-compensated (pin, fp64), the pose and covariance of
+// x_buf[i] in xsrc (kXC layout), and either the identity body covariance
+// without pvec_update (var_identity, rounds before convergence) or calcBodyVar
+// on the body point + pvec_update.
+template <bool kPre>
 __global__ void __launch_bounds__(256) k_ins_prep(int n, const float* __restrict__ ox, const float* __restrict__ oy,
                            const float* __restrict__ oz, MP mp, DState* __restrict__ st, int slot,
                            DevMap m, double* __restrict__ pw, uint32_t* __restrict__ hslot, int do_push,
-                           PushArg pa) {
+                           PushArg pa, const double* __restrict__ pin, const double* __restrict__ xsrc,
+                           int var_identity) {
   // the window push (local_mapping.cpp:434-441) rides in block 0: it copies
   // x_curr into x_buf[ord], which this kernel only reads
-  if (do_push && blockIdx.x == 0) push_state_block(st, pa);
+  if (!kPre && do_push && blockIdx.x == 0) push_state_block(st, pa);
   // pose of x_buf[ord] = x_curr after the IEKF (device state)
-  const double* xc = st->xc;
+  const double* xc = kPre ? xsrc : st->xc;
   M3 R, rot_var, tsl_var;
   for (int r = 0; r < 3; r++)
     for (int c = 0; c < 3; c++) {
@@ -415,9 +422,20 @@ __global__ void __launch_bounds__(256) k_ins_prep(int n, const float* __restrict
   }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     V3 pnt;
-    M3 var;
-    var_init_pt(mp, ox[i], oy[i], oz[i], pnt, var);
-    M3 vw = world_var(R, var, pnt, rot_var, tsl_var);
+    M3 vw;
+    if (kPre) {
+      pnt = v3(pin[(size_t)i * 3], pin[(size_t)i * 3 + 1], pin[(size_t)i * 3 + 2]);
+      if (var_identity) {
+        vw = M3::I();
+      } else {
+        const M3 var = calc_body_var(pnt, mp.dept, mp.beam_dv);
+        vw = world_var(R, var, pnt, rot_var, tsl_var);
+      }
+    } else {
+      M3 var;
+      var_init_pt(mp, ox[i], oy[i], oz[i], pnt, var);
+      vw = world_var(R, var, pnt, rot_var, tsl_var);
+    }
     V3 w = rigid(R, pnt, p);
     size_t base = (size_t)slot * m.cap_wp + i;
     for (int j = 0; j < 3; j++) m.wp_pnt[base * 3 + j] = pnt[j];
@@ -1108,7 +1126,8 @@ static int insert_tail(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_nu
 // Asynchronous: every count stays on the device. A child-allocation overflow
 // of k_ins_alloc sets kCntMisc; the insert tail and the recut kernels then skip
 // and map_recut reports it (kNeedInsertReplay) for map_insert_replay.
-int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num, const PushArg* push) {
+int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num, const PushArg* push,
+               const InsPre* pre) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
@@ -1117,8 +1136,12 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread
     return VG_OK;
   }
   const int g = grid_for(n);
-  k_ins_prep<<<g, kBlock, 0, s>>>(n, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, mp, ctx->st, slot, m, w.pw, w.u0,
-                                  push ? 1 : 0, push ? *push : PushArg());
+  if (pre)
+    k_ins_prep<true><<<g, kBlock, 0, s>>>(n, nullptr, nullptr, nullptr, mp, ctx->st, slot, m, w.pw, w.u0, 0,
+                                          PushArg(), pre->pnt, pre->pose, pre->var_identity);
+  else
+    k_ins_prep<false><<<g, kBlock, 0, s>>>(n, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, mp, ctx->st, slot, m, w.pw, w.u0,
+                                           push ? 1 : 0, push ? *push : PushArg(), nullptr, nullptr, 0);
   const int ntile = (n + kRootTile - 1) / kRootTile;
   (void)epoch;
   k_ins_flags<<<ntile, kBlock, 0, s>>>(n, w.u0, m, w.v1, (int*)w.ac_cnt);

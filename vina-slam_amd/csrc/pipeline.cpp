@@ -16,173 +16,9 @@
 #include <cstring>
 #include <deque>
 #include <vector>
-#include "vg_internal.h"
+#include "vg_host.h"
 
 namespace vg {
-
-struct HX {  // IMUST (types.hpp:43-113)
-  double t = 0;
-  M3 R = M3::I();
-  V3 p = V3::Z(), v = V3::Z(), bg = V3::Z(), ba = V3::Z(), g = v3(0, 0, -9.8);
-  M15 cov;
-  HX() {
-    cov = M15::Z();
-    for (int i = 0; i < 15; i++) cov(i, i) = (i < 9) ? 0.0001 : 0.00001;
-  }
-  void plus(const V15& d) {
-    R = mul(R, Exp(v3(d[0], d[1], d[2])));
-    for (int k = 0; k < 3; k++) {
-      p[k] += d[3 + k];
-      v[k] += d[6 + k];
-      bg[k] += d[9 + k];
-      ba[k] += d[12 + k];
-    }
-  }
-  V15 minus(const HX& b) const {  // *this - b
-    V15 a;
-    V3 r = Log(mul(tr(b.R), R));
-    for (int k = 0; k < 3; k++) {
-      a[k] = r[k];
-      a[3 + k] = p[k] - b.p[k];
-      a[6 + k] = v[k] - b.v[k];
-      a[9 + k] = bg[k] - b.bg[k];
-      a[12 + k] = ba[k] - b.ba[k];
-    }
-    return a;
-  }
-};
-
-struct Imu {
-  double t;
-  double gyr[3], acc[3];
-};
-
-// IMUEKF::scale_gravity = imupre_scale_gravity (vg_config; 0 reads as 1)
-static inline double gravity_scale(const vg_config& c) { return c.scale_gravity > 0 ? c.scale_gravity : 1.0; }
-
-// IMU_PRE host part (preintegration.hpp:12-51)
-struct HImuPre {
-  M3 R_delta = M3::I(), R_bg = M3::Z(), p_bg = M3::Z(), p_ba = M3::Z(), v_bg = M3::Z(), v_ba = M3::Z();
-  V3 p_delta = V3::Z(), v_delta = V3::Z(), bg, ba;
-  double dtime = 0;
-  M15 cov = M15::Z();
-  std::vector<double> rec;  // the BA's device record, fixed once integrated (record())
-  HImuPre(const V3& bg1, const V3& ba1) : bg(bg1), ba(ba1) {}
-  void add_imu(V3 gyr, V3 acc, double dt, const M6& nm, const M6& nw) {  // imu_preintegration.cpp:57-95
-    dtime += dt;
-    M3 rinc = Exp(gyr, dt);
-    M3 rj = jr(scl(gyr, dt));
-    M3 rdt = scl(R_delta, dt);
-    M3 rdt2 = scl(R_delta, 0.5 * dt * dt);
-    M3 ask = hat(acc);
-    p_ba = sub(add(p_ba, scl(v_ba, dt)), rdt2);
-    p_bg = sub(add(p_bg, scl(v_bg, dt)), mul(mul(rdt2, ask), R_bg));
-    v_ba = sub(v_ba, rdt);
-    v_bg = sub(v_bg, mul(mul(rdt, ask), R_bg));
-    R_bg = sub(mul(tr(rinc), R_bg), scl(rj, dt));
-    M<9, 9> A = M<9, 9>::I();
-    M<9, 6> B = M<9, 6>::Z();
-    for (int r = 0; r < 3; r++)
-      for (int c = 0; c < 3; c++) {
-        A(r, c) = rinc(c, r);
-        A(3 + r, c) = -mul(rdt2, ask)(r, c);
-        A(3 + r, 6 + c) = (r == c) ? dt : 0.0;
-        A(6 + r, c) = -mul(rdt, ask)(r, c);
-        B(r, c) = rj(r, c) * dt;
-        B(3 + r, 3 + c) = rdt2(r, c);
-        B(6 + r, 3 + c) = rdt(r, c);
-      }
-    M<9, 9> c9;
-    for (int r = 0; r < 9; r++)
-      for (int c = 0; c < 9; c++) c9(r, c) = cov(r, c);
-    M<9, 9> nc = add(mul(mul(A, c9), tr(A)), mul(mul(B, nm), tr(B)));
-    for (int r = 0; r < 9; r++)
-      for (int c = 0; c < 9; c++) cov(r, c) = nc(r, c);
-    for (int r = 0; r < 6; r++)
-      for (int c = 0; c < 6; c++) cov(9 + r, 9 + c) += nw(r, c) * dt;
-    V3 dp = add(scl(v_delta, dt), mul(rdt2, acc));
-    V3 dv = mul(rdt, acc);
-    for (int k = 0; k < 3; k++) {
-      p_delta[k] += dp[k];
-      v_delta[k] += dv[k];
-    }
-    R_delta = mul(R_delta, rinc);
-  }
-  // imu_preintegration.cpp:31-55; sg = imupre_scale_gravity (line 51)
-  void push_imu(const std::vector<Imu>& buf, const M6& nm, const M6& nw, double sg) {
-    for (size_t k = 1; k < buf.size(); k++) {
-      const Imu& a = buf[k - 1];
-      const Imu& b = buf[k];
-      double dt = b.t - a.t;
-      V3 gyr, acc;
-      for (int j = 0; j < 3; j++) {
-        gyr[j] = 0.5 * (a.gyr[j] + b.gyr[j]) - bg[j];
-        acc[j] = 0.5 * (a.acc[j] + b.acc[j]) * sg - ba[j];
-      }
-      add_imu(gyr, acc, dt, nm, nw);
-    }
-  }
-  void record(double* rec) const {
-    memset(rec, 0, kBaImuRec * sizeof(double));
-    memcpy(rec, R_delta.a, 72);
-    memcpy(rec + 9, p_delta.a, 24);
-    memcpy(rec + 12, v_delta.a, 24);
-    memcpy(rec + 15, R_bg.a, 72);
-    memcpy(rec + 24, p_bg.a, 72);
-    memcpy(rec + 33, p_ba.a, 72);
-    memcpy(rec + 42, v_bg.a, 72);
-    memcpy(rec + 51, v_ba.a, 72);
-    rec[60] = dtime;
-    M15 ci = inverse(cov);
-    memcpy(rec + 64, ci.a, 225 * sizeof(double));
-  }
-};
-
-struct Pend {          // a scan whose device results the host has not absorbed yet
-  int seq1 = 0, seq2 = 0;  // P1 (state) and P2 (counters) sequence numbers
-  int shift = 0;           // x_buf slid on the host after P1 was published
-  int jour_check = 0;      // local_mapping.cpp:525-533 pending on the BA result
-  int pushed = -1;         // x_buf index pushed by this scan (cov from x_curr)
-  int ev_base = 0, ev_n = 0;  // this scan's k_iekf event pairs (vg_profile)
-  double t = 0;            // scan end time (trajectory row)
-  vg_stats st;
-};
-
-struct HostPipe {
-  HX x_curr;
-  std::vector<HX> x_buf;
-  std::deque<HImuPre> imu_pre;
-  std::vector<int> mp;
-  int win_count = 0, win_base = 0, epoch = 0;
-  double jour = 0, last_pcl_end_time = 0;
-  V3 last_pos = V3::Z();
-  bool first = true;
-  int wp_n[32] = {0};
-  MP mpd;
-  M6 noiseMeas = M6::Z(), noiseWalk = M6::Z();
-  std::vector<double> traj;
-  std::vector<vg_stats> stats_log;
-  std::vector<double> poses;  // this scan's IMUEKF::imu_poses, 22 doubles each (deskew)
-  int n_factors = 0;
-  // current scan
-  Pend cur;
-  bool in_scan = false;
-  int ds_seq = 0, ds_n = -1, n_raw = 0;
-  const float *sx = nullptr, *sy = nullptr, *sz = nullptr, *si = nullptr;
-  int ins_slot = -1, ins_n = 0;
-  bool published = false;
-  bool prefix = false;     // map_margi_prefix enqueued for this scan
-  int rc_seq = 0;          // > 0: this scan's recut ran asynchronously (status with Pub::seq_rc == rc_seq)
-  std::deque<Pend> pend;   // enqueued scans awaiting absorption (oldest first)
-  int sticky = VG_OK;      // deferred device error
-  // device work deferred to the next launch that can carry it (one launch
-  // fewer each): the scan opening rides with the IEKF's scan binding, the
-  // window push with the insert's first kernel
-  bool begin_pending = false;
-  double begin_xc[kXC];
-  bool push_pending = false;
-  PushArg push;
-};
 
 // enqueue deferred device work on its own when the next stage cannot carry it
 static int flush_begin(vg_ctx* ctx, HostPipe* P) {
@@ -197,7 +33,6 @@ static int flush_deferred(vg_ctx* ctx, HostPipe* P) {
   return state_push(ctx, P->push.ord, P->push.new_imu, P->push.rec);
 }
 
-static HostPipe* hp(vg_ctx* ctx) { return (HostPipe*)ctx->host; }
 
 void host_init(vg_ctx* ctx) {
   HostPipe* P = new HostPipe();
@@ -229,9 +64,12 @@ void host_init(vg_ctx* ctx) {
     P->noiseWalk(i, i) = c.ba_rdw_gyr;
     P->noiseWalk(3 + i, 3 + i) = c.ba_rdw_acc;
   }
+  P->sg = gravity_scale(c);
+  if (c.cold_start) P->init = init_create(ctx);
   ctx->host = P;
 }
 void host_free(vg_ctx* ctx) {
+  if (hp(ctx) && hp(ctx)->init) init_destroy(hp(ctx)->init);
   delete hp(ctx);
   ctx->host = nullptr;
 }
@@ -289,12 +127,13 @@ static int absorb_p1(vg_ctx* ctx, HostPipe* P, Pend& q) {
     memcpy(h.g.a, o + 21, 24);
   }
   if (q.pushed >= 0 && q.pushed < (int)P->x_buf.size()) P->x_buf[q.pushed].cov = xc.cov;
-  // trajectory row (pub_localtraj / save_pose_tum, local_mapping.cpp:427-430)
-  P->traj.push_back(q.t);
-  for (int i = 0; i < 12; i++) P->traj.push_back(pb.traj[i]);
-  q.st.iekf_iters = pb.iekf_iters;
-  for (int i = 0; i < 4; i++) q.st.iekf_matches[i] = pb.matches[i];
-  q.st.degenerate = degenerate_of(pb.nnt);
+  if (!q.init_tail) {  // trajectory row (pub_localtraj / save_pose_tum, local_mapping.cpp:427-430)
+    P->traj.push_back(q.t);
+    for (int i = 0; i < 12; i++) P->traj.push_back(pb.traj[i]);
+    q.st.iekf_iters = pb.iekf_iters;
+    for (int i = 0; i < 4; i++) q.st.iekf_matches[i] = pb.matches[i];
+    q.st.degenerate = degenerate_of(pb.nnt);
+  }
   q.st.ba_iters = pb.ba_iters1;
   q.st.ba_hess = pb.ba_hess1;
   for (int i = 0; i < 4; i++) q.st.iekf_planes[i] = pb.planes[i];
@@ -328,7 +167,7 @@ static int absorb_p2(vg_ctx* ctx, HostPipe* P, Pend& q) {
   q.st.n_slide = c[kCntSlide];
   q.st.nodes_used = c[kCntNodes];
   q.st.fix_used = c[kCntFix];
-  q.st.roots_new = c[kCntRoots];
+  if (!q.init_tail) q.st.roots_new = c[kCntRoots];  // init: the rebuilt map's roots (init.cpp)
   q.st.plane_updates = c[kCntPlaneUpd];
   q.st.fix_full = c[kCntFixFull];
   q.st.v_ins = c[kCntSeg];
@@ -351,7 +190,7 @@ static int absorb_p2(vg_ctx* ctx, HostPipe* P, Pend& q) {
 
 // absorb every pending scan whose results are needed (all of P1, and P2 when
 // `full`); blocking
-static int absorb(vg_ctx* ctx, HostPipe* P, bool full) {
+int absorb(vg_ctx* ctx, HostPipe* P, bool full) {
   if (P->sticky != VG_OK) return P->sticky;
   int r = VG_OK;
   while (!P->pend.empty()) {
@@ -380,7 +219,7 @@ int host_sync(vg_ctx* ctx) {
 
 // IMUEKF::motion_blur state/covariance propagation (imu_ekf.cpp:28-94); the
 // per-point deskew (114-144) is SURVEY row f1 (callers pass compensated scans).
-static void propagate(vg_ctx* ctx, HostPipe* P, const std::vector<Imu>& imus, double pcl_beg, double pcl_end) {
+void propagate(vg_ctx* ctx, HostPipe* P, const std::vector<Imu>& imus, double pcl_beg, double pcl_end) {
   P->poses.clear();
   const vg_config& c = ctx->cfg;
   HX& xc = P->x_curr;
@@ -396,7 +235,7 @@ static void propagate(vg_ctx* ctx, HostPipe* P, const std::vector<Imu>& imus, do
       acc_avr[j] = 0.5 * (head.acc[j] + tail.acc[j]);
     }
     angvel = sub(angvel, xc.bg);
-    acc_avr = sub(scl(acc_avr, gravity_scale(c)), xc.ba);  // imu_ekf.cpp:51
+    acc_avr = sub(scl(acc_avr, P->sg), xc.ba);  // imu_ekf.cpp:51
     acc_imu = add(mul(R_imu, acc_avr), xc.g);
     double cur = head.t;
     if (cur < P->last_pcl_end_time) cur = P->last_pcl_end_time;
@@ -483,18 +322,6 @@ static WinArg make_winarg(const HostPipe* P, int set_xc) {
 
 // ---- stage entry points (one per reference call in local_mapping.cpp:389-547)
 
-static std::vector<Imu> to_imus(const double* imu, int m) {
-  std::vector<Imu> imus(m > 0 ? m : 0);
-  for (int i = 0; i < m; i++) {
-    imus[i].t = imu[7 * i];
-    for (int j = 0; j < 3; j++) {
-      imus[i].gyr[j] = imu[7 * i + 1 + j];
-      imus[i].acc[j] = imu[7 * i + 4 + j];
-    }
-  }
-  return imus;
-}
-
 static int need_open(vg_ctx* ctx, HostPipe* P, const char* what) {
   if (P->sticky != VG_OK) return P->sticky;
   if (!P->in_scan) {
@@ -511,6 +338,10 @@ int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double en
   HostPipe* P = hp(ctx);
   if (P->in_scan) {
     ctx->err = "vg_propagate: previous scan not finished (vg_step_end)";
+    return VG_E_STATE;
+  }
+  if (init_active(P)) {
+    ctx->err = "vg_propagate: cold-start initialisation in progress (use vg_step* until init_phase 3)";
     return VG_E_STATE;
   }
   VG_TRY(absorb(ctx, P, false));  // x_curr / x_buf of the previous scan
@@ -637,7 +468,7 @@ int stage_window_push(vg_ctx* ctx, const double* imu, int m) {
   if (P->win_count > 1) {
     const HX& xb = P->x_buf[P->win_count - 2];
     P->imu_pre.emplace_back(xb.bg, xb.ba);
-    P->imu_pre.back().push_imu(to_imus(imu, m), P->noiseMeas, P->noiseWalk, gravity_scale(ctx->cfg));
+    P->imu_pre.back().push_imu(to_imus(imu, m), P->noiseMeas, P->noiseWalk, P->sg);
     P->imu_pre.back().rec.resize(kBaImuRec);
     P->imu_pre.back().record(P->imu_pre.back().rec.data());  // off the BA's critical path
     new_imu = P->win_count - 2;
@@ -855,6 +686,7 @@ int stage_deskew(vg_ctx* ctx, const float* x, const float* y, const float* z, co
 int host_step_deskew(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di,
                      const float* dt, int n, double beg, double end, const double* imu, int m) {
   const vg_config& c = ctx->cfg;
+  if (init_active(hp(ctx))) return init_step(ctx, dx, dy, dz, di, dt, n, beg, end, imu, m);
   VG_TRY(stage_propagate(ctx, imu, m, beg, end));
   VG_TRY(stage_deskew(ctx, dx, dy, dz, di, dt, n));
   const float *x = ctx->d_x, *y = ctx->d_y, *z = ctx->d_z, *i = ctx->d_i;
@@ -874,6 +706,7 @@ int host_step_deskew(vg_ctx* ctx, const float* dx, const float* dy, const float*
 int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n, double beg,
               double end, const double* imu, int m) {
   const vg_config& c = ctx->cfg;
+  if (init_active(hp(ctx))) return init_step(ctx, dx, dy, dz, di, nullptr, n, beg, end, imu, m);
   VG_TRY(stage_propagate(ctx, imu, m, beg, end));
   // the IEKF is enqueued before the downsample: both read only the raw scan
   // (local_mapping.cpp:396-413), and the main stream should not idle while the
@@ -946,6 +779,16 @@ int host_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* va
     VG_HIP(hipMemcpy(ctx->d_z, soa.data() + 2 * (size_t)n, (size_t)n * sizeof(float), hipMemcpyHostToDevice));
   }
   if (n == 0) return VG_OK;
+  VG_TRY(kd_lio(ctx, n, x_curr, valid, iters));
+  state_out(x_curr, state);
+  return VG_OK;
+}
+
+// the kd-tree IEKF on the scan in ctx->d_x/y/z (n points, raw LiDAR frame);
+// x_curr in/out; the map is extended with the scan at the result
+int kd_lio(vg_ctx* ctx, int n, HX& x_curr, int* valid, int* iters) {
+  *valid = -1;
+  *iters = 0;
   if (ctx->kd.n < 100) {  // 275-310: seed the map with the scan at the current pose
     VG_TRY(kd_update(ctx, n, x_curr.R.a, x_curr.p.a, false));
     return VG_OK;
@@ -1008,7 +851,6 @@ int host_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* va
     }
   }
   VG_TRY(kd_update(ctx, n, x_curr.R.a, x_curr.p.a, true));  // 427-437
-  state_out(x_curr, state);
   return VG_OK;
 }
 

@@ -232,7 +232,89 @@ __global__ void __launch_bounds__(256) k_deskew(int n, int npose, const double* 
   }
 }
 
+// ---- Initialization::motion_blur (initialization.cpp:64-156),
+// the per-point part. The host integrates the IMU poses backwards from the
+// scan-end state (one record per IMU segment, descending start time, the
+// deskew's 22-double layout) and plans the output: the reference walks the
+// time-sorted cloud backwards, giving each point the first pose (in list
+// order) that starts strictly before it, and, once point 0 is reached, pushes
+// point 0 again with every later pose. Output o < n - j0 is point n-1-o; the
+// rest are point 0 with poses q0+1, q0+2, ... One lane per output point:
+//   pnt = R_c^T (R_i (R_L P + t_L) + T_ei)   (IMU frame at the scan end, fp64)
+// par: [0..9) x_buf[i].R, [9..12) x_buf[i].p, [12..21) R_L, [21..24) t_L,
+// then the pose records.
+__global__ void __launch_bounds__(256) k_blur_init(int nout, int n, int j0, int npose, int q0,
+                                                   const float4* __restrict__ pts, const double* __restrict__ par,
+                                                   double* __restrict__ pnt) {
+  const double* poses = par + kDeskewHead;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < nout; o += gridDim.x * blockDim.x) {
+    int j, q;
+    if (o < n - j0) {
+      j = n - 1 - o;
+      const double tj = (double)pts[j].w;
+      int lo = 0, hi = npose - 1;  // first pose (descending starts) with start < tj; exists for j >= j0
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (poses[(size_t)mid * kDeskewPose] < tj) hi = mid;
+        else lo = mid + 1;
+      }
+      q = lo;
+    } else {
+      j = 0;
+      q = q0 + 1 + (o - (n - j0));
+    }
+    const float4 pt = pts[j];
+    const double* h = poses + (size_t)q * kDeskewPose;
+    const double dt = (double)pt.w - h[0];
+    const M3 R_i = mul(ld_m3(h + 1), Exp(ld_v3(h + 16), dt));
+    const V3 hp = ld_v3(h + 10), hv = ld_v3(h + 13), ha = ld_v3(h + 19), xp = ld_v3(par + 9);
+    V3 T;
+    for (int k = 0; k < 3; k++) T[k] = ((hp[k] + hv[k] * dt) + ((ha[k] * 0.5) * dt) * dt) - xp[k];
+    const V3 a = add(mul(ld_m3(par + 12), v3((double)pt.x, (double)pt.y, (double)pt.z)), ld_v3(par + 21));
+    const V3 r = mul(tr(ld_m3(par)), add(mul(R_i, a), T));
+    for (int k = 0; k < 3; k++) pnt[(size_t)o * 3 + k] = r[k];
+  }
+}
+
 // ---- host wrappers ----
+int state_blur_init(vg_ctx* ctx, const double* par, int npose, const float4* pts, int n, int j0, int q0, int nout,
+                    double* d_par, double* pnt) {
+  const size_t nd = kDeskewHead + (size_t)npose * kDeskewPose;
+  if (nd > (size_t)kDeskewBuf) {
+    ctx->err = "motion_blur (init): too many IMU segments in one scan";
+    return VG_E_CAPACITY;
+  }
+  double* stage = ctx->h_stage + kStageDeskewOff;
+  memcpy(stage, par, nd * sizeof(double));
+  VG_HIP(hipMemcpyAsync(d_par, stage, nd * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  if (nout > 0) k_blur_init<<<grid_for(nout), 256, 0, ctx->stream>>>(nout, n, j0, npose, q0, pts, d_par, pnt);
+  VG_HIP(hipGetLastError());
+  VG_HIP(stream_wait(ctx));  // the staging block is reused by the next call
+  return VG_OK;
+}
+
+// the window states x_buf (kXS each, by ord), x_curr (kXC), the IMU_PRE records
+// of the window factors (ring from slot 0) with zero bias deltas: the
+// initialisation's hand-over to the steady state (and the recut's poses)
+int state_load(vg_ctx* ctx, const double* xs, int nw, const double* xc, const double* recs, int nrec) {
+  hipStream_t s = ctx->stream;
+  DState* st = ctx->st;
+  if (nw > kMaxWin || nrec > kMaxWin) {
+    ctx->err = "state_load: window too large";
+    return VG_E_ARG;
+  }
+  if (nw > 0) VG_HIP(hipMemcpyAsync(st->xs, xs, (size_t)nw * kXS * sizeof(double), hipMemcpyHostToDevice, s));
+  if (xc) VG_HIP(hipMemcpyAsync(st->xc, xc, kXC * sizeof(double), hipMemcpyHostToDevice, s));
+  if (recs) {
+    if (nrec > 0)
+      VG_HIP(hipMemcpyAsync(st->imurec, recs, (size_t)nrec * kBaImuRec * sizeof(double), hipMemcpyHostToDevice, s));
+    VG_HIP(hipMemsetAsync(st->bias, 0, sizeof(st->bias), s));
+    VG_HIP(hipMemsetAsync(&st->imu_head, 0, sizeof(int), s));
+  }
+  VG_HIP(hipStreamSynchronize(s));
+  return VG_OK;
+}
+
 int state_alloc(vg_ctx* ctx) {
   ctx->st = ctx->arena.take<DState>(1);
   ctx->d_deskew = ctx->arena.take<double>(kDeskewBuf);

@@ -427,6 +427,12 @@ int kd_update(vg_ctx* ctx, int n, const double* R, const double* p, bool downsam
 // (returns n_out).
 int ds_run(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, int n, double voxel,
            int* n_out);
+// down_sampling_close of a device cloud (the initialisation's raw-cloud
+// reduction): out = the chosen points (x, y, z, t) sorted by time, stable over
+// ascending voxel keys; t == nullptr gives every point the time tconst.
+// Host-synchronous.
+int ds_close(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* t, float tconst, int n,
+             double voxel, float4* out, int* n_out);
 // Same, asynchronous: n_out and the range flag are published to Pub (seq_ds).
 int ds_enqueue(vg_ctx* ctx, hipStream_t s, const float* x, const float* y, const float* z, const float* in, int n,
                double voxel, int pub_seq);
@@ -441,8 +447,17 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
 int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank,
              const double* begin_xc = nullptr);
 constexpr int kNeedInsertReplay = 1;  // map_recut: the insert overflowed k_ins_alloc, replay it first
-// push: the window push to fold into the insert's first launch (or nullptr)
-int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num, const PushArg* push = nullptr);
+// the initialisation's insert source (cut_voxel, initialization.cpp:229-246):
+// n fp64 body points, the kXC pose/covariance block of x_buf[i], both device
+struct InsPre {
+  const double* pnt;
+  const double* pose;
+  int var_identity;  // 1: identity body covariance, no pvec_update (before convergence)
+};
+// push: the window push to fold into the insert's first launch (or nullptr);
+// pre: insert precomputed body points instead of the downsampled scan
+int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num, const PushArg* push = nullptr,
+               const InsPre* pre = nullptr);
 int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num);
 int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay = false,
               int pub_seq = 0);
@@ -467,6 +482,13 @@ int state_publish_counters(vg_ctx* ctx, int seq);
 int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq);
 int state_deskew(vg_ctx* ctx, const double* par, int npose, const float* x, const float* y, const float* z,
                  const float* in, const float* t, int n);
+// initialisation: motion_blur's per-point part on a close-downsampled
+// cloud (pts, ascending time) -> nout fp64 body points; par (host): frame pose,
+// extrinsic, npose IMU pose records (descending start); synchronous
+int state_blur_init(vg_ctx* ctx, const double* par, int npose, const float4* pts, int n, int j0, int q0, int nout,
+                    double* d_par, double* pnt);
+// window states / x_curr / IMU records (+ zero bias, ring head 0) -> DState; synchronous
+int state_load(vg_ctx* ctx, const double* xs, int nw, const double* xc, const double* recs, int nrec);
 // ba.hip
 constexpr int kBaX = 24;        // per-frame state: R 9, p 3, v 3, bg 3, ba 3, g 3
 int ba_alloc(vg_ctx* ctx);
@@ -477,6 +499,11 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
            const std::function<int()>& before_first_wait = nullptr);
 const int* ba_iters_dev(vg_ctx* ctx);
 const int* ba_hess_dev(vg_ctx* ctx);  // Hessian passes of the last LM run (I_H of SURVEY 8(d))
+// LiDAR factor passes for a host-driven LM (initialisation): Hessian pass at
+// `poses` (lower 6W x 6W, gradient, residual into out) or residual pass at
+// `poses` (*out); synchronous
+int ba_lidar_pass(vg_ctx* ctx, bool hessian, const double* poses, const int* mp_ring, double* out);
+int ba_factor_normals(vg_ctx* ctx, std::vector<double>& normals);  // column 0 of each factor's eigenvectors
 // pipeline.cpp
 void host_init(vg_ctx* ctx);
 void host_free(vg_ctx* ctx);

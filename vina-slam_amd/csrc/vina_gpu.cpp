@@ -233,6 +233,41 @@ int vg_downsample(vg_ctx* ctx, const float* xyz, const float* intensity, int n, 
   return VG_OK;
 }
 
+int vg_downsample_close(vg_ctx* ctx, const float* xyz, const float* time, int n, double voxel_size, float* out_xyzt,
+                        int* n_out) {
+  if (!ctx || (!xyz && n > 0) || !out_xyzt || !n_out || n < 0) return VG_E_ARG;
+  if (n > ctx->cap.max_points_per_scan) {
+    ctx->err = "scan larger than max_points_per_scan";
+    return VG_E_CAPACITY;
+  }
+  *n_out = 0;
+  if (n == 0) return VG_OK;
+  if (voxel_size < 0.001) {  // point_utils.hpp:48: no-op (the time sort still applies in the caller's use)
+    ctx->err = "vg_downsample_close: voxel_size < 0.001 is a no-op in the reference";
+    return VG_E_ARG;
+  }
+  VG_TRY(host_sync(ctx));
+  VG_HIP(hipStreamSynchronize(ctx->stream_ds));
+  VG_TRY(upload_aos(ctx, xyz, nullptr, n));
+  if (time) VG_HIP(hipMemcpy(ctx->d_t, time, (size_t)n * sizeof(float), hipMemcpyHostToDevice));
+  float4* out = nullptr;
+  VG_HIP(hipMalloc((void**)&out, (size_t)n * sizeof(float4)));
+  int m = 0;
+  const int r = ds_close(ctx, ctx->d_x, ctx->d_y, ctx->d_z, time ? ctx->d_t : nullptr, 0.0f, n, voxel_size, out, &m);
+  if (r == VG_OK && m > 0) {
+    const hipError_t e = hipMemcpy(out_xyzt, out, (size_t)m * sizeof(float4), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      (void)hipFree(out);
+      ctx->err = std::string("vg_downsample_close: ") + hipGetErrorString(e);
+      return VG_E_HIP;
+    }
+  }
+  (void)hipFree(out);
+  VG_TRY(r);
+  *n_out = m;
+  return VG_OK;
+}
+
 int vg_seed(vg_ctx* ctx, const double* state) {
   if (!ctx || !state) return VG_E_ARG;
   host_seed(ctx, state);

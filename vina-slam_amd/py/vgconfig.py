@@ -36,7 +36,7 @@ class CConfig(ctypes.Structure):
         ("ext_R", ctypes.c_double * 9), ("ext_t", ctypes.c_double * 3),
         ("max_layer", ctypes.c_int), ("max_points", ctypes.c_int), ("win_size", ctypes.c_int),
         ("thread_num", ctypes.c_int), ("if_BA", ctypes.c_int), ("use_threads", ctypes.c_int),
-        ("vnc_prep", ctypes.c_int), ("pad", ctypes.c_int), ("scale_gravity", ctypes.c_double),
+        ("vnc_prep", ctypes.c_int), ("cold_start", ctypes.c_int), ("scale_gravity", ctypes.c_double),
     ]
 
 
@@ -53,7 +53,7 @@ def load(name_or_path):
     return out
 
 
-def to_c(p, use_threads=1, vnc_prep=1, scale_gravity=1.0):
+def to_c(p, use_threads=1, vnc_prep=1, scale_gravity=1.0, cold_start=0):
     g, o, b = p["General"], p["Odometry"], p["LocalBA"]
     c = CConfig()
     c.voxel_size = o["voxel_size"]
@@ -78,4 +78,5 @@ def to_c(p, use_threads=1, vnc_prep=1, scale_gravity=1.0):
     c.use_threads = use_threads
     c.vnc_prep = vnc_prep
     c.scale_gravity = scale_gravity
+    c.cold_start = cold_start
     return c

@@ -40,7 +40,8 @@ class Stats(ctypes.Structure):
                 ("n_factors", ctypes.c_int), ("ba_iters", ctypes.c_int), ("degenerate", ctypes.c_int),
                 ("nodes_used", ctypes.c_int), ("fix_used", ctypes.c_int), ("plane_updates", ctypes.c_int),
                 ("fix_full", ctypes.c_int), ("iekf_planes", ctypes.c_int * 4), ("v_ins", ctypes.c_int),
-                ("ba_hess", ctypes.c_int)]
+                ("ba_hess", ctypes.c_int), ("init_phase", ctypes.c_int), ("init_rounds", ctypes.c_int),
+                ("init_valid", ctypes.c_int)]
 
 
 def _stats_dict(s):
@@ -89,6 +90,7 @@ def lib():
         L.vg_last_error.restype = ctypes.c_char_p
         L.vg_reset.argtypes = [P]
         L.vg_downsample.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, fp, ip]
+        L.vg_downsample_close.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, fp, ip]
         L.vg_seed.argtypes = [P, dp]
         L.vg_lio_kdtree.argtypes = [P, fp, ctypes.c_int, dp, ip, ip]
         L.vg_kdmap_get.argtypes = [P, fp, ctypes.c_int, ip]
@@ -178,6 +180,16 @@ class Context:
         n = ctypes.c_int(0)
         self._chk(lib().vg_downsample(self.h, _f(xyz), _f(inten), xyz.shape[0], size, _f(out), ctypes.byref(n)),
                   "vg_downsample")
+        return out[: n.value]
+
+    def downsample_close(self, xyz, times, size):
+        """down_sampling_close + the init's time sort: (m,4) [x,y,z,t]."""
+        xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+        t = None if times is None else np.ascontiguousarray(times, dtype=np.float32)
+        out = np.zeros((max(xyz.shape[0], 1), 4), dtype=np.float32)
+        n = ctypes.c_int(0)
+        self._chk(lib().vg_downsample_close(self.h, _f(xyz), None if t is None else _f(t), xyz.shape[0], size,
+                                            _f(out), ctypes.byref(n)), "vg_downsample_close")
         return out[: n.value]
 
     def seed(self, state):
