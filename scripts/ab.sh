@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 for i in 1 2 3; do
   for v in A B; do
     if [ $v = B ]; then export VINA_GPU_LIB=$PWD/vina-slam_amd/lib_alt/libvina_gpu.so; else unset VINA_GPU_LIB; fi
-    timeout -k 10 200 python bench.py --no-cpu --stage-scans 0 > gpurun_out/ab_$v$i.json 2>/dev/null || { echo "bench $v failed"; exit 1; }
+    timeout -k 10 200 python bench.py --no-cpu --stage-scans 0 --target-steps 0 --no-h2d ${AB_ARGS} > gpurun_out/ab_$v$i.json 2>/dev/null || { echo "bench $v failed"; exit 1; }
     python -c "import json; d=json.load(open('gpurun_out/ab_$v$i.json')); print('$v', d['value'], d['ms_per_step'])"
   done
 done

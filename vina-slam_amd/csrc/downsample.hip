@@ -203,6 +203,245 @@ int ds_close(vg_ctx* ctx, const float* x, const float* y, const float* z, const 
   return VG_OK;
 }
 
+// ---- the per-scan pipeline's downsample (down_sampling_voxel + the /2
+// fallback, local_mapping.cpp:396-403) without a sort and without the host:
+//  1. k_hds_insert  one lane per point: the key, insert-or-find in an open
+//                   addressing table, atomicMin of the voxel's first point
+//                   index, atomicAdd of its point count;
+//  2. k_hds_tiles   per 1024-point tile: first points and their voxels' points;
+//  3. k_hds_rank    per tile: prefix over the earlier tiles + block scan ->
+//                   each voxel's output rank (= order of first occurrence, so
+//                   deterministic) and the offset of its point segment; the
+//                   voxel count; the fallback flag (fewer than 2000 voxels);
+//  4. k_hds_scatter point indices into their voxel's segment (atomic slots);
+//  5. k_hds_mean    one lane per voxel: insertion-sorts its segment back to
+//                   input order, runs the reference's float recurrence
+//                   (bit-identical to k_ds_mean), writes the voxel at its rank
+//                   and clears its table slot for the next scan.
+// The fallback pass at half the voxel size is enqueued behind it on the same
+// stream and early-exits on the device flag, so no count ever travels to the
+// host. Output order = first-occurrence order (the sorted path's is key order;
+// the reference's is unordered_map order: the set is the same).
+__device__ __forceinline__ uint32_t hds_hash(uint64_t k, int mask) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return (uint32_t)k & (uint32_t)mask;
+}
+constexpr int kHdsTile = 1024;  // points per tile (256 lanes x 4)
+constexpr int kHdsEmptyFirst = 0x7f7f7f7f;  // above every point index (ds_reset's memset byte)
+
+__global__ void __launch_bounds__(256) k_hds_insert(int n, const float* __restrict__ x, const float* __restrict__ y,
+                                                    const float* __restrict__ z, double size, DownsampleBufs d,
+                                                    const int* __restrict__ need) {
+  if (need && !*need) return;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int64_t kx = key_axis_f(x[i], size) + kKeyOff;
+    int64_t ky = key_axis_f(y[i], size) + kKeyOff;
+    int64_t kz = key_axis_f(z[i], size) + kKeyOff;
+    const bool bad = (kx < 0) | (ky < 0) | (kz < 0) | (kx >= 2 * kKeyOff) | (ky >= 2 * kKeyOff) | (kz >= 2 * kKeyOff);
+    if (bad) {
+      atomicOr(&d.hflags[0], 1);
+      kx = ky = kz = 0;
+    }
+    const uint64_t key = ((uint64_t)kx << 42) | ((uint64_t)ky << 21) | (uint64_t)kz;
+    uint32_t s = hds_hash(key, d.hmask);
+    while (true) {
+      const unsigned long long prev =
+          atomicCAS((unsigned long long*)&d.hkey[s], (unsigned long long)kKeyEmpty, (unsigned long long)key);
+      if (prev == kKeyEmpty || prev == key) break;
+      s = (s + 1) & (uint32_t)d.hmask;
+    }
+    atomicMin(&d.hfirst[s], i);
+    atomicAdd(&d.hcnt[s], 1);
+    d.pslot[i] = s;
+  }
+}
+
+// (first point?, its voxel's point count) of point i
+__device__ __forceinline__ void hds_code(const DownsampleBufs& d, int i, int n, int& f, int& c) {
+  f = 0;
+  c = 0;
+  if (i >= n) return;
+  const uint32_t s = d.pslot[i];
+  if (d.hfirst[s] == i) {
+    f = 1;
+    c = d.hcnt[s];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_hds_tiles(int n, DownsampleBufs d, const int* __restrict__ need) {
+  if (need && !*need) return;
+  __shared__ int s_f[4], s_c[4];
+  const int i0 = blockIdx.x * kHdsTile + threadIdx.x * 4;
+  int F = 0, C = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    int f, c;
+    hds_code(d, i0 + k, n, f, c);
+    F += f;
+    C += c;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    F += __shfl_down(F, o, 64);
+    C += __shfl_down(C, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_f[threadIdx.x >> 6] = F;
+    s_c[threadIdx.x >> 6] = C;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    d.tsum[2 * blockIdx.x] = s_f[0] + s_f[1] + s_f[2] + s_f[3];
+    d.tsum[2 * blockIdx.x + 1] = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+  }
+}
+
+// need_in: this pass's predicate (nullptr: always); need_out: the fallback flag
+// this pass decides (nullptr: none)
+__global__ void __launch_bounds__(256) k_hds_rank(int n, int ntile, DownsampleBufs d, const int* __restrict__ need_in,
+                                                  int* __restrict__ need_out, int min_out) {
+  if (need_in && !*need_in) return;
+  __shared__ unsigned long long s_w[4];
+  __shared__ int s_b[2][4];
+  // prefix of the earlier tiles (first points, points)
+  int bf = 0, bc = 0;
+  for (int t = threadIdx.x; t < (int)blockIdx.x; t += blockDim.x) {
+    bf += d.tsum[2 * t];
+    bc += d.tsum[2 * t + 1];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    bf += __shfl_down(bf, o, 64);
+    bc += __shfl_down(bc, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) {
+    s_b[0][wv] = bf;
+    s_b[1][wv] = bc;
+  }
+  __syncthreads();
+  bf = s_b[0][0] + s_b[0][1] + s_b[0][2] + s_b[0][3];
+  bc = s_b[1][0] + s_b[1][1] + s_b[1][2] + s_b[1][3];
+  // exclusive scan of (f, c) packed in 64 bits (c < 2^32: points per scan)
+  const int i0 = blockIdx.x * kHdsTile + threadIdx.x * 4;
+  int f[4], c[4];
+  unsigned long long v = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    hds_code(d, i0 + k, n, f[k], c[k]);
+    v += ((unsigned long long)f[k] << 32) | (unsigned long long)c[k];
+  }
+  unsigned long long x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long yv = __shfl_up(x, o, 64);
+    if (lane >= o) x += yv;
+  }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  unsigned long long base = 0, tot = 0;
+  for (int k = 0; k < 4; k++) {
+    if (k < wv) base += s_w[k];
+    tot += s_w[k];
+  }
+  unsigned long long r = base + x - v;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (f[k]) {
+      const uint32_t s = d.pslot[i0 + k];
+      d.hrank[s] = bf + (int)(r >> 32);
+      d.hoff[s] = bc + (int)(r & 0xffffffffull);
+    }
+    r += ((unsigned long long)f[k] << 32) | (unsigned long long)c[k];
+  }
+  if (blockIdx.x == ntile - 1 && threadIdx.x == 0) {
+    const int nv = bf + (int)(tot >> 32);
+    d.hflags[1] = nv;
+    if (need_out) *need_out = nv < min_out ? 1 : 0;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_hds_scatter(int n, DownsampleBufs d, const int* __restrict__ need) {
+  if (need && !*need) return;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t s = d.pslot[i];
+    const int pos = atomicAdd(&d.hfill[s], 1);
+    d.pseg[d.hoff[s] + pos] = (uint32_t)i;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_hds_mean(int n, DownsampleBufs d, const float* __restrict__ x,
+                                                  const float* __restrict__ y, const float* __restrict__ z,
+                                                  const float* __restrict__ in, const int* __restrict__ need) {
+  if (need && !*need) return;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t s = d.pslot[i];
+    if (d.hfirst[s] != i) continue;
+    const int b = d.hoff[s], cnt = d.hcnt[s], v = d.hrank[s];
+    uint32_t* sg = d.pseg + b;
+    for (int a = 1; a < cnt; a++) {  // back to input order (segments are short)
+      const uint32_t key = sg[a];
+      int q = a - 1;
+      while (q >= 0 && sg[q] > key) {
+        sg[q + 1] = sg[q];
+        q--;
+      }
+      sg[q + 1] = key;
+    }
+    float px = x[i], py = y[i], pz = z[i], c = 1.0f;
+    for (int a = 1; a < cnt; a++) {
+      const uint32_t j = sg[a];
+      // point_utils.hpp:34-37, evaluated exactly as written (no contraction)
+      px = (px * c + x[j]) / (c + 1);
+      py = (py * c + y[j]) / (c + 1);
+      pz = (pz * c + z[j]) / (c + 1);
+      c += 1;
+    }
+    d.ox[v] = px;
+    d.oy[v] = py;
+    d.oz[v] = pz;
+    d.oi[v] = in ? in[i] : 0.0f;
+    d.oc[v] = c;
+    d.hkey[s] = kKeyEmpty;  // the slot is this lane's alone: clear it for the next run
+    d.hfirst[s] = kHdsEmptyFirst;
+    d.hcnt[s] = 0;
+    d.hfill[s] = 0;
+  }
+}
+
+// the pipeline's downsample, asynchronous on stream s; with `fallback`, the
+// /2 pass of local_mapping.cpp:399-403 runs on the device when fewer than
+// 2000 voxels came out. hflags[1] = the voxel count (device), published to
+// Pub (seq_ds) when pub_seq > 0.
+int ds_enqueue_hashed(vg_ctx* ctx, hipStream_t s, const float* x, const float* y, const float* z, const float* in,
+                      int n, double voxel, bool fallback, int pub_seq) {
+  DownsampleBufs& d = ctx->ds;
+  if (n > ctx->cap.max_points_per_scan) {
+    ctx->err = "scan larger than max_points_per_scan";
+    return VG_E_CAPACITY;
+  }
+  const int g = grid_for(n), ntile = (n + kHdsTile - 1) / kHdsTile;
+  int* need = d.hflags + 2;
+  if (n == 0) {
+    VG_HIP(hipMemsetAsync(d.hflags + 1, 0, 2 * sizeof(int), s));
+  } else {
+    for (int pass = 0; pass < (fallback ? 2 : 1); pass++) {
+      const int* pin = pass ? need : nullptr;
+      const double vs = pass ? voxel / 2 : voxel;
+      k_hds_insert<<<g, kBlock, 0, s>>>(n, x, y, z, vs, d, pin);
+      k_hds_tiles<<<ntile, kBlock, 0, s>>>(n, d, pin);
+      k_hds_rank<<<ntile, kBlock, 0, s>>>(n, ntile, d, pin, pass == 0 && fallback ? need : nullptr, 2000);
+      k_hds_scatter<<<g, kBlock, 0, s>>>(n, d, pin);
+      k_hds_mean<<<g, kBlock, 0, s>>>(n, d, x, y, z, in, pin);
+    }
+  }
+  if (pub_seq > 0) VG_TRY(state_publish_ds(ctx, s, pub_seq, d.hflags, false));
+  VG_HIP(hipGetLastError());
+  return VG_OK;
+}
+
 int ds_alloc(vg_ctx* ctx) {
   const int n = ctx->cap.max_points_per_scan;
   DownsampleBufs& d = ctx->ds;
@@ -227,7 +466,20 @@ int ds_alloc(vg_ctx* ctx) {
                                             d.idx_sorted, n, 0, 32, ctx->stream));  // ds_close's time sort
   d.tmp_bytes = std::max(b1, std::max(b2, b3));
   d.tmp = ctx->arena.take<char>(d.tmp_bytes);
-  if (!d.keys || !d.seg || !d.oc || !d.tmp) {
+  int hs = 1024;
+  while (hs < 2 * n) hs <<= 1;
+  d.hmask = hs - 1;
+  d.hkey = ctx->arena.take<uint64_t>(hs);
+  d.hfirst = ctx->arena.take<int>(hs);
+  d.hcnt = ctx->arena.take<int>(hs);
+  d.hfill = ctx->arena.take<int>(hs);
+  d.hrank = ctx->arena.take<int>(hs);
+  d.hoff = ctx->arena.take<int>(hs);
+  d.pslot = ctx->arena.take<uint32_t>(n);
+  d.pseg = ctx->arena.take<uint32_t>(n);
+  d.tsum = ctx->arena.take<int>(2 * ((size_t)n / kHdsTile + 2));
+  d.hflags = ctx->arena.take<int>(4);
+  if (!d.keys || !d.seg || !d.oc || !d.tmp || !d.hkey || !d.hoff || !d.pseg || !d.tsum || !d.hflags) {
     ctx->err = "arena exhausted (downsample)";
     return VG_E_CAPACITY;
   }
@@ -247,8 +499,23 @@ int ds_enqueue(vg_ctx* ctx, hipStream_t s, const float* x, const float* y, const
     k_ds_mean<<<grid_for(n), kBlock, 0, s>>>(d.flags, d.seg, d.idx_sorted, x, y, z, in, d.ox, d.oy, d.oz, d.oi,
                                              d.oc);
   }
-  if (pub_seq > 0) VG_TRY(state_publish_ds(ctx, s, pub_seq));
+  if (pub_seq > 0) VG_TRY(state_publish_ds(ctx, s, pub_seq, d.flags, true));
   VG_HIP(hipGetLastError());
+  return VG_OK;
+}
+
+// the hashed downsample's tables at rest: empty keys, no first points, zero
+// counts (vg_create, vg_reset; k_hds_mean restores this after every run)
+int ds_reset(vg_ctx* ctx) {
+  DownsampleBufs& d = ctx->ds;
+  hipStream_t s = ctx->stream;
+  const size_t hs = (size_t)d.hmask + 1;
+  VG_HIP(hipMemsetAsync(d.hkey, 0xff, hs * sizeof(uint64_t), s));
+  VG_HIP(hipMemsetAsync(d.hfirst, 0x7f, hs * sizeof(int), s));  // 0x7f7f7f7f: above every point index
+  VG_HIP(hipMemsetAsync(d.hcnt, 0, hs * sizeof(int), s));
+  VG_HIP(hipMemsetAsync(d.hfill, 0, hs * sizeof(int), s));
+  VG_HIP(hipMemsetAsync(d.hflags, 0, 4 * sizeof(int), s));
+  VG_HIP(hipStreamSynchronize(s));
   return VG_OK;
 }
 

@@ -60,6 +60,7 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(m.wp_leaf = ctx->arena.take<int>(cw * W));
   good &= ok(m.counters = ctx->arena.take<int>(kCntN));
   good &= ok(m.stamp = ctx->arena.take<int>(cn));
+  good &= ok(m.wpn = ctx->arena.take<int>(kMaxWin));
   Work& w = ctx->wk;
   w.cap = (int)(cw * (W + 1));
   good &= ok(w.k0 = ctx->arena.take<uint64_t>(w.cap));
@@ -110,13 +111,14 @@ int map_reset(vg_ctx* ctx) {
   VG_HIP(hipMemsetAsync(m.hfirst, 0x7f, hs * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.counters, 0, kCntN * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.stamp, 0, (size_t)m.cap_nodes * sizeof(int), s));
+  VG_HIP(hipMemsetAsync(m.wpn, 0, kMaxWin * sizeof(int), s));
   VG_HIP(hipMemsetAsync(ctx->wk.cand_bits, 0, (ctx->cap.max_nodes / 32 + 1) * sizeof(uint32_t), s));
   VG_HIP(hipMemsetAsync(m.in_slide, 0, m.cap_nodes, s));
   VG_HIP(hipMemsetAsync(m.leaf_cnt, 0, (size_t)m.cap_nodes * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.cfirst, 0x7f, (size_t)m.cap_nodes * 8 * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.nscr, 0xff, (size_t)m.cap_nodes * 4 * sizeof(int), s));
   VG_HIP(hipStreamSynchronize(s));
-  return VG_OK;
+  return ds_reset(ctx);  // the pipeline downsample's voxel table
 }
 
 // Node records of freshly allocated nodes must be zero: the pool is zeroed
@@ -392,14 +394,15 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
 // without pvec_update (var_identity, rounds before convergence) or calcBodyVar
 // on the body point + pvec_update.
 template <bool kPre>
-__global__ void __launch_bounds__(256) k_ins_prep(int n, const float* __restrict__ ox, const float* __restrict__ oy,
+__global__ void __launch_bounds__(256) k_ins_prep(int n_arg, const int* __restrict__ nd, const float* __restrict__ ox, const float* __restrict__ oy,
                            const float* __restrict__ oz, MP mp, DState* __restrict__ st, int slot,
-                           DevMap m, double* __restrict__ pw, uint32_t* __restrict__ hslot, int do_push,
-                           PushArg pa, const double* __restrict__ pin, const double* __restrict__ xsrc,
-                           int var_identity) {
+                           DevMap m, double* __restrict__ pw, uint32_t* __restrict__ hslot,
+                           const PushArg* __restrict__ pa, const double* __restrict__ pin, const double* __restrict__ xsrc,
+                           int var_identity, int* __restrict__ dsf) {
+  const int n = nd ? *nd : n_arg;  // the downsampled count on the device (ds_enqueue_hashed)
   // the window push (local_mapping.cpp:434-441) rides in block 0: it copies
   // x_curr into x_buf[ord], which this kernel only reads
-  if (!kPre && do_push && blockIdx.x == 0) push_state_block(st, pa);
+  if (!kPre && pa && blockIdx.x == 0) push_state_block(st, *pa);  // pa: host-mapped (vg_ctx::d_in)
   // pose of x_buf[ord] = x_curr after the IEKF (device state)
   const double* xc = kPre ? xsrc : st->xc;
   M3 R, rot_var, tsl_var;
@@ -419,6 +422,12 @@ __global__ void __launch_bounds__(256) k_ins_prep(int n, const float* __restrict
     m.counters[kCntMisc] = 0;  // insert abort flag (child-allocation overflow)
     m.counters[kCntPlaneUpd] = 0;  // margi's per-scan branch counters (vg_stats)
     m.counters[kCntFixFull] = 0;
+    m.counters[kCntNds] = n;
+    m.wpn[slot] = n;  // window points of this physical slot (k_make_win)
+    if (dsf && dsf[0]) {  // the downsample's key-range error (no host wait in between)
+      atomicOr(&m.counters[kCntErr], 1);
+      dsf[0] = 0;
+    }
   }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     V3 pnt;
@@ -515,8 +524,9 @@ __device__ __forceinline__ u64 block_excl_scan3(u64 v, u64* s_w, u64* total) {
   *total = tot;
   return base + x - v;
 }
-__global__ void __launch_bounds__(256) k_ins_flags(int n, const uint32_t* __restrict__ hslot, DevMap m,
+__global__ void __launch_bounds__(256) k_ins_flags(int n_arg, const int* __restrict__ nd, const uint32_t* __restrict__ hslot, DevMap m,
                                                    uint32_t* __restrict__ rank, int* __restrict__ tile_cnt) {
+  const int n = nd ? *nd : n_arg;  // the downsampled count on the device (ds_enqueue_hashed)
   __shared__ u64 s_w[4];
   const int i0 = blockIdx.x * kRootTile + threadIdx.x * 4;
   int code[4];
@@ -545,9 +555,10 @@ __global__ void __launch_bounds__(256) k_ins_flags(int n, const uint32_t* __rest
 // (0.5 + k) voxel_size, records zeroed; existing first-touched roots isexist
 // (voxel_map.cpp:70); slide appends in point order; the root counters. The
 // point -> root lookup itself is left to k_ins_descend (after this launch).
-__global__ void __launch_bounds__(256) k_ins_roots_alloc(int n, int ntile, const uint32_t* __restrict__ hslot,
+__global__ void __launch_bounds__(256) k_ins_roots_alloc(int n_arg, const int* __restrict__ nd, int ntile, const uint32_t* __restrict__ hslot,
                                                          const uint32_t* __restrict__ rank,
                                                          const int* __restrict__ tile_cnt, MP mp, DevMap m) {
+  const int n = nd ? *nd : n_arg;  // the downsampled count on the device (ds_enqueue_hashed)
   __shared__ int s_red[3][4];
   int a[3] = {0, 0, 0}, t[3] = {0, 0, 0};
   for (int b = threadIdx.x; b < ntile; b += blockDim.x)
@@ -684,9 +695,10 @@ __global__ void k_copy_int(const int* __restrict__ src, int* __restrict__ dst) {
   if (threadIdx.x == 0) *dst = *src;
 }
 
-__global__ void __launch_bounds__(256) k_ins_descend(int n, int thread_num, const double* __restrict__ pw, DevMap m,
+__global__ void __launch_bounds__(256) k_ins_descend(int n_arg, const int* __restrict__ nd, int thread_num, const double* __restrict__ pw, DevMap m,
                                                      const uint32_t* __restrict__ hslot, int* __restrict__ leaf,
                                                      int* __restrict__ reqlist) {
+  const int n = nd ? *nd : n_arg;  // the downsampled count on the device (ds_enqueue_hashed)
   if (ins_skip(m, thread_num)) return;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t hs = hslot[i];
@@ -734,8 +746,9 @@ __global__ void __launch_bounds__(256) k_child_alloc(int np, const int* __restri
 // segment (seg_leaf[s] = leaf, m.leaf_seg[leaf] = s). Segment order is free:
 // k_push_window treats every leaf on its own; only the order of a leaf's
 // points matters, and k_push_window restores it.
-__global__ void __launch_bounds__(256) k_ins_resolve(int n, int thread_num, const double* __restrict__ pw, DevMap m,
+__global__ void __launch_bounds__(256) k_ins_resolve(int n_arg, const int* __restrict__ nd, int thread_num, const double* __restrict__ pw, DevMap m,
                                                      int* __restrict__ leaf, int* __restrict__ seg_leaf) {
+  const int n = nd ? *nd : n_arg;  // the downsampled count on the device (ds_enqueue_hashed)
   if (ins_skip(m, thread_num)) return;
   for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
     const int i = base + threadIdx.x;
@@ -799,8 +812,9 @@ __global__ void __launch_bounds__(1024) k_seg_offsets(int thread_num, DevMap m, 
 }
 
 // every point into its segment (arbitrary order inside it)
-__global__ void __launch_bounds__(256) k_ins_scatter(int n, int thread_num, DevMap m, const int* __restrict__ leaf,
+__global__ void __launch_bounds__(256) k_ins_scatter(int n_arg, const int* __restrict__ nd, int thread_num, DevMap m, const int* __restrict__ leaf,
                                                      const int* __restrict__ seg_off, int* __restrict__ order) {
+  const int n = nd ? *nd : n_arg;  // the downsampled count on the device (ds_enqueue_hashed)
   if (ins_skip(m, thread_num)) return;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int l = leaf[i];
@@ -1102,7 +1116,7 @@ static int alloc_children(vg_ctx* ctx, int* plist, int np, int* next, int next_b
 }
 
 // leaves -> sorted (leaf, order) keys -> pushes of one insert
-static int insert_tail(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num) {
+static int insert_tail(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num, const int* nd = nullptr) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
@@ -1113,9 +1127,9 @@ static int insert_tail(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_nu
   int* order = reinterpret_cast<int*>(w.k0);
   int* order2 = reinterpret_cast<int*>(w.k1);
   // leaves -> per-leaf buckets (no sort: the order between leaves is free)
-  k_ins_resolve<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.leaf, seg_leaf);
+  k_ins_resolve<<<g, kBlock, 0, s>>>(n, nd, thread_num, w.pw, m, w.leaf, seg_leaf);
   k_seg_offsets<<<1, 1024, 0, s>>>(thread_num, m, seg_leaf, seg_off);
-  k_ins_scatter<<<g, kBlock, 0, s>>>(n, thread_num, m, w.leaf, seg_off, order);
+  k_ins_scatter<<<g, kBlock, 0, s>>>(n, nd, thread_num, m, w.leaf, seg_off, order);
   // ~one wave per leaf segment (the count stays on the device)
   k_push_window<<<gseg, 64 * kPushWaves, 0, s>>>(seg_leaf, seg_off, order, order2, mp, slot, m, w.pw, thread_num);
   VG_HIP(hipGetLastError());
@@ -1127,7 +1141,7 @@ static int insert_tail(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_nu
 // of k_ins_alloc sets kCntMisc; the insert tail and the recut kernels then skip
 // and map_recut reports it (kNeedInsertReplay) for map_insert_replay.
 int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num, const PushArg* push,
-               const InsPre* pre) {
+               const InsPre* pre, const int* nd) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
@@ -1135,25 +1149,31 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread
     if (push) VG_TRY(state_push(ctx, push->ord, push->new_imu, push->rec));
     return VG_OK;
   }
-  const int g = grid_for(n);
+  // device count: n is an upper bound, the kernels stride over the real one
+  const int g = nd ? grid_for(n, kBlock, 2048) : grid_for(n);
   if (pre)
-    k_ins_prep<true><<<g, kBlock, 0, s>>>(n, nullptr, nullptr, nullptr, mp, ctx->st, slot, m, w.pw, w.u0, 0,
-                                          PushArg(), pre->pnt, pre->pose, pre->var_identity);
-  else
-    k_ins_prep<false><<<g, kBlock, 0, s>>>(n, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, mp, ctx->st, slot, m, w.pw, w.u0,
-                                           push ? 1 : 0, push ? *push : PushArg(), nullptr, nullptr, 0);
+    k_ins_prep<true><<<g, kBlock, 0, s>>>(n, nullptr, nullptr, nullptr, nullptr, mp, ctx->st, slot, m, w.pw, w.u0,
+                                          nullptr, pre->pnt, pre->pose, pre->var_identity, nullptr);
+  else {
+    // the push record goes through host-mapped memory, so a replayed graph
+    // picks up each scan's record (the host writes it before the launch)
+    if (push) ctx->h_in->push = *push;
+    k_ins_prep<false><<<g, kBlock, 0, s>>>(n, nd, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, mp, ctx->st, slot, m, w.pw,
+                                           w.u0, push ? &ctx->d_in->push : nullptr, nullptr, nullptr, 0,
+                                           nd ? ctx->ds.hflags : nullptr);
+  }
   const int ntile = (n + kRootTile - 1) / kRootTile;
   (void)epoch;
-  k_ins_flags<<<ntile, kBlock, 0, s>>>(n, w.u0, m, w.v1, (int*)w.ac_cnt);
-  k_ins_roots_alloc<<<ntile, kBlock, 0, s>>>(n, ntile, w.u0, w.v1, (const int*)w.ac_cnt, mp, m);
+  k_ins_flags<<<ntile, kBlock, 0, s>>>(n, nd, w.u0, m, w.v1, (int*)w.ac_cnt);
+  k_ins_roots_alloc<<<ntile, kBlock, 0, s>>>(n, nd, ntile, w.u0, w.v1, (const int*)w.ac_cnt, mp, m);
   if (m.shard_world > 1) {  // the thread_num quirk counts distinct roots over all shards
     k_copy_int<<<1, 64, 0, s>>>(m.counters + kCntTouched, m.counters + kCntGTouched);
     VG_TRY(shard_allreduce(ctx, m.counters + kCntGTouched, m.counters + kCntGTouched, 1, 1));
   }
-  k_ins_descend<<<g, kBlock, 0, s>>>(n, thread_num, w.pw, m, w.u0, w.leaf, w.list2);
+  k_ins_descend<<<g, kBlock, 0, s>>>(n, nd, thread_num, w.pw, m, w.u0, w.leaf, w.list2);
   const int ins_cap = (ctx->dbg_ins_cap >= 0 && ctx->dbg_ins_cap < kInsAllocCap) ? ctx->dbg_ins_cap : kInsAllocCap;
   k_ins_alloc<<<1, 1024, 0, s>>>(thread_num, m, w.list2, ins_cap);
-  return insert_tail(ctx, mp, slot, n, thread_num);
+  return insert_tail(ctx, mp, slot, n, thread_num, nd);
 }
 
 // host-sized child allocation after a k_ins_alloc overflow, then the tail
@@ -1266,11 +1286,13 @@ __device__ __forceinline__ bool win_event(int g, int cap_wp, const int* nper, co
   return true;
 }
 
-__global__ void __launch_bounds__(256) k_rc_win(int L, int total, int cap_wp, const int* __restrict__ nper,
+__global__ void __launch_bounds__(256) k_rc_win(int L, const int* __restrict__ total_p, int cap_wp,
+                                                const int* __restrict__ nper,
                                                 const int* __restrict__ slot_of, const WinD* __restrict__ win,
                                                 DevMap m, uint64_t* __restrict__ ev, uint32_t* __restrict__ evsrc,
                                                 int cap, int* __restrict__ rc) {
   if (rc[kRcAbort] || rc[kRcSub + L] == 0) return;
+  const int total = *total_p;  // k_make_win
   for (int base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
     const int g = base + threadIdx.x;
     int leaf = -1, o = 0, ord = 0, i = 0;
@@ -1768,7 +1790,7 @@ constexpr int kFacMax = 1 << 20;
 constexpr int kRcBig = 200;
 __global__ void __launch_bounds__(1024) k_fac_sort(DevMap m, int* __restrict__ rc, uint32_t* __restrict__ bits,
                                                    int* __restrict__ fac_node, int cap_f, Pub* __restrict__ pub,
-                                                   int seq, int max_fac) {
+                                                   int* __restrict__ seq_ctr, int max_fac) {
   __shared__ int s_w[17];
   const int nf = m.counters[kCntFactors];
   int status = rc[kRcAbort];
@@ -1793,6 +1815,8 @@ __global__ void __launch_bounds__(1024) k_fac_sort(DevMap m, int* __restrict__ r
       }
   }
   if (threadIdx.x == 0) {
+    const int seq = *seq_ctr + 1;  // the device's count of asynchronous recuts (the host mirrors it)
+    *seq_ctr = seq;
     rc[kRcStatus] = status;
     __hip_atomic_store(&pub->rc_status, status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&pub->rc_nf, nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1842,8 +1866,8 @@ static int recut_complete(vg_ctx* ctx, const MP& mp, int nlev, int* hrc, int* n_
       k_rc_visit<<<256, kBlock, 0, s>>>(L, ctx->rc_thread_num, list_of(L), mp, m, list_of(L + 1), w.list2, w.cand,
                                         w.rc, nullptr);
       if (total > 0)
-        k_rc_win<<<grid_for(total), kBlock, 0, s>>>(L, total, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc, w.cap,
-                                                     w.rc);
+        k_rc_win<<<grid_for(total), kBlock, 0, s>>>(L, dn + 64, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc,
+                                                     w.cap, w.rc);
       VG_TRY(read_rc(ctx, hrc));
       VG_TRY(recut_slow_apply(ctx, L, mp, dwin, list_of(L + 1), hrc));
     }
@@ -1872,8 +1896,8 @@ static int recut_complete(vg_ctx* ctx, const MP& mp, int nlev, int* hrc, int* n_
 // Asynchronous (pub_seq > 0): the factor extraction is sized on the device and
 // nothing waits; *n_factors = -1 and the status arrives with Pub::seq_rc ==
 // pub_seq (map_recut_resume completes a recut that needs the host).
-int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay,
-              int pub_seq) {
+static int map_recut_impl(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay,
+                          int pub_seq) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
@@ -1896,7 +1920,7 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* 
   }
   const int nlev = mp.max_layer + 1;  // children sit one layer down; leaves at max_layer do not subdivide
   auto list_of = [&](int L) { return (L % 2 == 1) ? w.list0 : w.list1; };  // worklist of level L >= 1
-  const int gv = 256, gw = grid_for(total > 0 ? total : 1);
+  const int gv = 256, gw = grid_for(total > 0 ? total : 1, kBlock, 2048);  // grid-stride over the device total
   const int ev_cap = (ctx->dbg_apply_cap >= 0 && ctx->dbg_apply_cap < kApplyEv) ? ctx->dbg_apply_cap : kApplyEv;
   for (int L = 0; L < nlev; L++) {
     k_rc_visit<<<gv, kBlock, 0, s>>>(L, thread_num, L > 0 ? list_of(L) : nullptr, mp, m, list_of(L + 1), w.list2,
@@ -1905,7 +1929,7 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* 
     // the deepest level has no window events, no apply and no pushes
     if (L == mp.max_layer) break;
     if (total > 0)
-      k_rc_win<<<gw, kBlock, 0, s>>>(L, total, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc, w.cap, w.rc);
+      k_rc_win<<<gw, kBlock, 0, s>>>(L, dn + 64, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc, w.cap, w.rc);
     k_rc_apply<<<1, kApplyThreads, 0, s>>>(L, ev_cap, mp, dwin, m, list_of(L + 1), w.list2, w.k0, w.evsrc, w.k1,
                                            (int*)w.ac_off, w.rc);
     k_rc_push<<<64, 64 * kRcPushWaves, 0, s>>>(L, w.k1, (const int*)w.ac_off, mp, dwin, m, w.rc);
@@ -1913,8 +1937,8 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* 
   VG_HIP(hipGetLastError());
   if (pub_seq > 0) {
     const int max_fac = (ctx->dbg_fac_max >= 0 && ctx->dbg_fac_max < kFacMax) ? ctx->dbg_fac_max : kFacMax;
-    k_fac_sort<<<1, 1024, 0, s>>>(m, w.rc, w.cand_bits, ctx->ba.fac_node, ctx->ba.cap_f, ctx->d_pub, pub_seq,
-                                  max_fac);
+    k_fac_sort<<<1, 1024, 0, s>>>(m, w.rc, w.cand_bits, ctx->ba.fac_node, ctx->ba.cap_f, ctx->d_pub,
+                                  &ctx->st->rc_ctr, max_fac);
     k_factor_finish_dev<<<64, 256, 0, s>>>(w.rc, m, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr);
     VG_HIP(hipGetLastError());
     *n_factors = -1;
@@ -1927,10 +1951,24 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* 
 
 // complete an asynchronous recut whose published status was nonzero (the LM
 // skipped): same outcomes as the synchronous call
-int map_recut_resume(vg_ctx* ctx, const MP& mp, int* n_factors) {
+static int map_recut_resume_impl(vg_ctx* ctx, const MP& mp, int* n_factors) {
   int* hrc = ctx->h_pinned + 128;
   VG_TRY(read_rc(ctx, hrc));
   return recut_complete(ctx, mp, mp.max_layer + 1, hrc, n_factors);
+}
+
+// the recut's end on the main stream: the margi prefix (second stream) starts
+// from it, under the LM iterations enqueued behind it
+int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay,
+              int pub_seq) {
+  const int r = map_recut_impl(ctx, mp, wa, thread_num, n_factors, replay, pub_seq);
+  if (!ctx->capturing) VG_HIP(hipEventRecord(ctx->ev_recut_done, ctx->stream));  // else after the graph launch
+  return r;
+}
+int map_recut_resume(vg_ctx* ctx, const MP& mp, int* n_factors) {
+  const int r = map_recut_resume_impl(ctx, mp, n_factors);
+  VG_HIP(hipEventRecord(ctx->ev_recut_done, ctx->stream));
+  return r;
 }
 
 // ------------------------------------------------------------------ margi (A10)
@@ -2326,7 +2364,9 @@ __global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m
 __global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, double j, int* __restrict__ rc,
                                                   int n_oldest) {
   if (blockIdx.x == 0) {  // margi level counts and the leaf count start at zero
-    for (int i = threadIdx.x; i < kRcN; i += blockDim.x) rc[i] = (i == kRcNOld) ? n_oldest : 0;
+    // kRcStatus is the recut's (k_ba_init may read it concurrently on the main stream)
+    for (int i = threadIdx.x; i < kRcN; i += blockDim.x)
+      if (i != kRcStatus) rc[i] = (i == kRcNOld) ? n_oldest : 0;
     if (threadIdx.x == 0) m.counters[kCntLeaves] = 0;
   }
   const int n = m.counters[kCntSlide];
@@ -2345,8 +2385,7 @@ int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thr
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream_ds;
   const int nlev = mp.max_layer + 1;
-  VG_HIP(hipEventRecord(ctx->ev_recut_done, ctx->stream));
-  VG_HIP(hipStreamWaitEvent(s, ctx->ev_recut_done, 0));
+  VG_HIP(hipStreamWaitEvent(s, ctx->ev_recut_done, 0));  // recorded at the recut's end (map_recut)
   const int gl = 64;  // grid-stride over device-side counts
   k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour, w.rc, n_oldest);
   for (int L = 0; L < nlev; L++) k_collect_level<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.list0, w.rc);

@@ -169,6 +169,10 @@ static int absorb_p2(vg_ctx* ctx, HostPipe* P, Pend& q) {
   q.st.fix_used = c[kCntFix];
   if (!q.init_tail) q.st.roots_new = c[kCntRoots];  // init: the rebuilt map's roots (init.cpp)
   q.st.plane_updates = c[kCntPlaneUpd];
+  if (!q.init_tail) {  // the insert's downsampled count (the insert read it on the device)
+    q.st.n_ds = c[kCntNds];
+    if (q.ins_slot >= 0) P->wp_n[q.ins_slot] = c[kCntNds];
+  }
   q.st.fix_full = c[kCntFixFull];
   q.st.v_ins = c[kCntSeg];
   // events recorded while this scan was enqueued are complete now
@@ -375,37 +379,24 @@ int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double en
   return VG_OK;
 }
 
-// the downsampled point count (and the /2 fallback, local_mapping.cpp:399-403)
+// the downsampled point count for a caller of the stage-level API (the
+// pipeline itself never waits for it: the insert reads it on the device)
 static int resolve_ds(vg_ctx* ctx, HostPipe* P) {
   if (P->ds_n >= 0) return VG_OK;
-  const vg_config& c = ctx->cfg;
   VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ds, P->ds_seq, "downsample", ctx->stream_ds));
   if (ctx->h_pub->ds_err) {
     ctx->err = "voxel key out of packed range (|key| >= 2^20)";
     return VG_E_RANGE;
   }
-  int n_ds = ctx->h_pub->n_ds;
-  if (n_ds < 2000) {
-    prof_begin(ctx, kProfDownsample, ctx->stream_ds);
-    P->ds_seq = ++ctx->pub_seq;
-    VG_TRY(ds_enqueue(ctx, ctx->stream_ds, P->sx, P->sy, P->sz, P->si, P->n_raw, c.down_size / 2, P->ds_seq));
-    prof_end(ctx, kProfDownsample, ctx->stream_ds);
-    VG_HIP(hipEventRecord(ctx->ev_ds_done, ctx->stream_ds));
-    VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ds, P->ds_seq, "downsample", ctx->stream_ds));
-    if (ctx->h_pub->ds_err) {
-      ctx->err = "voxel key out of packed range (|key| >= 2^20)";
-      return VG_E_RANGE;
-    }
-    n_ds = ctx->h_pub->n_ds;
-  }
-  P->ds_n = n_ds;
-  P->cur.st.n_ds = n_ds;
+  P->ds_n = ctx->h_pub->n_ds;
+  P->cur.st.n_ds = P->ds_n;
   return VG_OK;
 }
 
-// down_sampling_voxel(pl_down, down_size) (local_mapping.cpp:396-403); the
-// count is resolved when it is first needed (the insert), so the GPU runs the
-// IEKF meanwhile
+// down_sampling_voxel(pl_down, down_size) and its /2 fallback below 2000
+// voxels (local_mapping.cpp:396-403), both decided on the device
+// (ds_enqueue_hashed): the host never waits for the count, the GPU runs the
+// IEKF meanwhile and the insert reads the count where it lands
 int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n,
                      int* n_ds_out) {
   HostTimer ht_(ctx, kHostDownsample);
@@ -422,9 +413,9 @@ int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float*
   VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_ds_free, 0));
   VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_scan_ready, 0));  // a deskewed scan (no-op otherwise)
   prof_begin(ctx, kProfDownsample, ctx->stream_ds);
-  P->ds_seq = ++ctx->pub_seq;
+  P->ds_seq = n_ds_out ? ++ctx->pub_seq : -1;  // published only for a stage-level caller
   P->ds_n = -1;
-  VG_TRY(ds_enqueue(ctx, ctx->stream_ds, dx, dy, dz, di, n, c.down_size, P->ds_seq));
+  VG_TRY(ds_enqueue_hashed(ctx, ctx->stream_ds, dx, dy, dz, di, n, c.down_size, true, n_ds_out ? P->ds_seq : 0));
   prof_end(ctx, kProfDownsample, ctx->stream_ds);
   VG_HIP(hipEventRecord(ctx->ev_ds_done, ctx->stream_ds));
   if (n_ds_out) {
@@ -496,7 +487,6 @@ int stage_insert(vg_ctx* ctx) {
     ctx->err = "vg_cut_voxel_multi: no downsampled scan";
     return VG_E_STATE;
   }
-  VG_TRY(resolve_ds(ctx, P));
   VG_TRY(absorb(ctx, P, true));  // earlier scans are complete by now (stream order)
   const int ord = P->win_count - 1;
   const int slot = P->mp[ord];
@@ -506,12 +496,82 @@ int stage_insert(vg_ctx* ctx) {
   prof_begin(ctx, kProfInsert);
   const bool push = P->push_pending;
   P->push_pending = false;
-  VG_TRY(map_insert(ctx, P->mpd, slot, P->ds_n, P->epoch, c.thread_num, push ? &P->push : nullptr));
+  // the downsampled count stays on the device (n_raw bounds the grids)
+  VG_TRY(map_insert(ctx, P->mpd, slot, P->n_raw, P->epoch, c.thread_num, push ? &P->push : nullptr, nullptr,
+                    ctx->ds.hflags + 1));
   prof_end(ctx, kProfInsert);
-  VG_HIP(hipEventRecord(ctx->ev_ds_free, ctx->stream));  // k_ins_prep has read the ds buffers
-  P->wp_n[slot] = P->ds_n;
+  VG_HIP(hipEventRecord(ctx->ev_ds_free, ctx->stream));  // the insert has read the ds buffers
+  P->wp_n[slot] = P->n_raw;  // an upper bound until the scan's counters are absorbed (absorb_p2)
   P->ins_slot = slot;
-  P->ins_n = P->ds_n;
+  P->cur.ins_slot = slot;
+  P->ins_n = -1;
+  return VG_OK;
+}
+
+// the insert's downsampled count, read back (the rare insert-replay path only)
+static int insert_replay(vg_ctx* ctx, HostPipe* P) {
+  if (P->ins_n < 0) {
+    VG_HIP(hipMemcpyAsync(ctx->h_pinned, ctx->ds.hflags + 1, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    VG_HIP(hipStreamSynchronize(ctx->stream));
+    P->ins_n = ctx->h_pinned[0];
+  }
+  return map_insert_replay(ctx, P->mpd, P->ins_slot, P->ins_n, ctx->cfg.thread_num);
+}
+
+// The steady state's insert + recut (local_mapping.cpp:425-451) as one
+// replayed graph per ring position mp[0]: every argument is fixed for a full
+// window (slot = mp[W-1], the window view, grids sized by the capacity), every
+// count lives on the device, and the scan's push record is read from
+// host-mapped memory. One launch instead of ~26, each kernel ~2-3 us cheaper
+// to dispatch. Conditions: graphs on, unsharded, the LM follows (the recut's
+// factor extraction is the asynchronous one), no debug capacity overrides.
+static bool mid_graph_ok(vg_ctx* ctx, const HostPipe* P) {
+  const vg_config& c = ctx->cfg;
+  return ctx->use_graphs && !ctx->prof_stages && ctx->shard.world == 1 && c.if_BA == 1 &&
+         P->win_count == c.win_size && P->push_pending && P->push.ord == c.win_size - 1 && !P->begin_pending &&
+         ctx->dbg_apply_cap < 0 && ctx->dbg_ins_cap < 0 && ctx->dbg_fac_max < 0 && P->ds_seq != 0;
+}
+static int stage_insert_recut(vg_ctx* ctx) {
+  HostTimer ht_(ctx, kHostInsert);
+  HostPipe* P = hp(ctx);
+  const vg_config& c = ctx->cfg;
+  VG_TRY(need_open(ctx, P, "vg_cut_voxel_multi"));
+  VG_TRY(absorb(ctx, P, true));  // earlier scans are complete by now (stream order)
+  const int W = c.win_size;
+  const int slot = P->mp[W - 1], ring0 = P->mp[0];
+  P->epoch++;
+  VG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_ds_done, 0));
+  P->push_pending = false;
+  ctx->h_in->push = P->push;  // this scan's record, read by the replay
+  hipGraphExec_t& ge = ctx->g_mid[ring0];
+  if (!ge) {
+    const int cap = ctx->cap.max_points_per_scan;
+    WinArg wa = make_winarg(P, 0);
+    for (int i = 0; i < W; i++) wa.nper[i] = cap;  // grid bounds only: the kernels read the device counts
+    hipStream_t s = ctx->stream;
+    VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    ctx->capturing = true;
+    int nf = 0;
+    int r = map_insert(ctx, P->mpd, slot, cap, P->epoch, c.thread_num, &P->push, nullptr, ctx->ds.hflags + 1);
+    if (r == VG_OK) r = map_recut(ctx, P->mpd, wa, c.thread_num, &nf, false, 1);
+    ctx->capturing = false;
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(s, &g);
+    VG_TRY(r);
+    VG_HIP(e);
+    VG_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    VG_HIP(hipGraphDestroy(g));
+  }
+  prof_begin(ctx, kProfInsert);
+  VG_HIP(hipGraphLaunch(ge, ctx->stream));
+  prof_end(ctx, kProfInsert);
+  VG_HIP(hipEventRecord(ctx->ev_ds_free, ctx->stream));     // the insert has read the ds buffers
+  VG_HIP(hipEventRecord(ctx->ev_recut_done, ctx->stream));  // the margi prefix starts from here
+  P->wp_n[slot] = P->n_raw;  // an upper bound until the scan's counters are absorbed (absorb_p2)
+  P->ins_slot = slot;
+  P->cur.ins_slot = slot;
+  P->ins_n = -1;
+  P->rc_seq = ++ctx->rc_pub;  // k_fac_sort in the graph publishes the same number
   return VG_OK;
 }
 
@@ -529,14 +589,14 @@ int stage_recut(vg_ctx* ctx, int* nf_out) {
   if (!nf_out && P->win_count >= c.win_size && c.if_BA == 1 && ctx->shard.world == 1) {
     // the LM follows: its kernels read the factor count on the device, and the
     // host learns the recut's outcome only once the LM is enqueued (stage_ba)
-    P->rc_seq = ++ctx->pub_seq;
-    VG_TRY(map_recut(ctx, P->mpd, wa, c.thread_num, &nf, false, P->rc_seq));
+    P->rc_seq = ++ctx->rc_pub;  // the device counts its asynchronous recuts the same way (k_fac_sort)
+    VG_TRY(map_recut(ctx, P->mpd, wa, c.thread_num, &nf, false, 1));
     prof_end(ctx, kProfRecut);
     return VG_OK;
   }
   int r = map_recut(ctx, P->mpd, wa, c.thread_num, &nf);
   if (r == kNeedInsertReplay) {  // per shard; the replayed recut has no collective
-    VG_TRY(map_insert_replay(ctx, P->mpd, P->ins_slot, P->ins_n, c.thread_num));
+    VG_TRY(insert_replay(ctx, P));
     r = map_recut(ctx, P->mpd, wa, c.thread_num, &nf, true);
   }
   VG_TRY(r);
@@ -584,7 +644,7 @@ int stage_ba(vg_ctx* ctx, int* iters_out) {
     int nf = 0;
     int r = map_recut_resume(ctx, P->mpd, &nf);
     if (r == kNeedInsertReplay) {
-      VG_TRY(map_insert_replay(ctx, P->mpd, P->ins_slot, P->ins_n, ctx->cfg.thread_num));
+      VG_TRY(insert_replay(ctx, P));
       const WinArg wa = make_winarg(P, 0);
       r = map_recut(ctx, P->mpd, wa, ctx->cfg.thread_num, &nf, true);
     }
@@ -693,8 +753,12 @@ int host_step_deskew(vg_ctx* ctx, const float* dx, const float* dy, const float*
   VG_TRY(stage_iekf(ctx, x, y, z, n, nullptr));
   VG_TRY(stage_downsample(ctx, x, y, z, i, n, nullptr));
   VG_TRY(stage_window_push(ctx, imu, m));
-  VG_TRY(stage_insert(ctx));
-  VG_TRY(stage_recut(ctx, nullptr));
+  if (mid_graph_ok(ctx, hp(ctx))) {
+    VG_TRY(stage_insert_recut(ctx));
+  } else {
+    VG_TRY(stage_insert(ctx));
+    VG_TRY(stage_recut(ctx, nullptr));
+  }
   if (hp(ctx)->win_count >= c.win_size) {
     if (c.if_BA == 1) VG_TRY(stage_ba(ctx, nullptr));
     VG_TRY(stage_margi_slide(ctx));
@@ -714,8 +778,12 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   VG_TRY(stage_iekf(ctx, dx, dy, dz, n, nullptr));
   VG_TRY(stage_downsample(ctx, dx, dy, dz, di, n, nullptr));
   VG_TRY(stage_window_push(ctx, imu, m));
-  VG_TRY(stage_insert(ctx));
-  VG_TRY(stage_recut(ctx, nullptr));
+  if (mid_graph_ok(ctx, hp(ctx))) {
+    VG_TRY(stage_insert_recut(ctx));
+  } else {
+    VG_TRY(stage_insert(ctx));
+    VG_TRY(stage_recut(ctx, nullptr));
+  }
   if (hp(ctx)->win_count >= c.win_size) {
     if (c.if_BA == 1) VG_TRY(stage_ba(ctx, nullptr));
     VG_TRY(stage_margi_slide(ctx));

@@ -84,8 +84,8 @@ __global__ void k_set_scan(DState* __restrict__ st, const float* x, const float*
 __global__ void k_push_state(DState* __restrict__ st, PushArg pa) { push_state_block(st, pa); }
 
 // window view for the map kernels: poses by ord, ring, per-ord counts / slots
-__global__ void k_make_win(DState* __restrict__ st, WinArg wa, WinD* __restrict__ win, int* __restrict__ nper,
-                           int* __restrict__ slot_of) {
+__global__ void k_make_win(DState* __restrict__ st, WinArg wa, const int* __restrict__ wpn, WinD* __restrict__ win,
+                           int* __restrict__ nper, int* __restrict__ slot_of) {
   const int t = threadIdx.x;
   const int wc = wa.win_count;
   if (wa.set_xc && wc > 0) {
@@ -100,8 +100,13 @@ __global__ void k_make_win(DState* __restrict__ st, WinArg wa, WinD* __restrict_
   }
   if (t < kMaxWin) {
     win->mp[t] = wa.mp[t];
-    nper[t] = t < wc ? wa.nper[t] : 0;
+    nper[t] = t < wc ? wpn[wa.mp[t]] : 0;  // the inserts' counts (device: no host round trip)
     slot_of[t] = wa.mp[t];
+  }
+  if (t == 0) {  // the window's point total (the recut's window-event grid reads it)
+    int tot = 0;
+    for (int k = 0; k < wc && k < kMaxWin; k++) tot += wpn[wa.mp[k]];
+    nper[64] = tot;
   }
   if (t == 0) {
     win->win_count = wc;
@@ -163,11 +168,11 @@ __global__ void k_publish_counters(const int* __restrict__ counters, Pub* __rest
 }
 
 // downsample result (n_out, range error) -> host
-__global__ void k_publish_ds(int* __restrict__ flags, Pub* __restrict__ pub, int seq) {
+__global__ void k_publish_ds(int* __restrict__ flags, Pub* __restrict__ pub, int seq, int reset) {
   if (threadIdx.x == 0) {
     pub_store(&pub->ds_err, flags[0]);
     pub_store(&pub->n_ds, flags[1]);
-    flags[0] = 0;  // ready for the next run
+    if (reset) flags[0] = 0;  // ready for the next run (the hashed path's insert takes it instead)
     pub_flag(&pub->seq_ds, seq);
   }
 }
@@ -351,7 +356,7 @@ int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec) {
 }
 
 int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot) {
-  k_make_win<<<1, 256, 0, ctx->stream>>>(ctx->st, wa, dwin, dnper, dslot);
+  k_make_win<<<1, 256, 0, ctx->stream>>>(ctx->st, wa, ctx->map.wpn, dwin, dnper, dslot);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }
@@ -399,8 +404,8 @@ int state_deskew(vg_ctx* ctx, const double* par, int npose, const float* x, cons
   return VG_OK;
 }
 
-int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq) {
-  k_publish_ds<<<1, 64, 0, s>>>(ctx->ds.flags, ctx->d_pub, seq);
+int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq, int* flags, bool reset) {
+  k_publish_ds<<<1, 64, 0, s>>>(flags, ctx->d_pub, seq, reset ? 1 : 0);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }

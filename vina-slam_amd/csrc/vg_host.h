@@ -132,6 +132,7 @@ struct Pend {          // a scan whose device results the host has not absorbed 
   int shift = 0;           // x_buf slid on the host after P1 was published
   int jour_check = 0;      // local_mapping.cpp:525-533 pending on the BA result
   int pushed = -1;         // x_buf index pushed by this scan (cov from x_curr)
+  int ins_slot = -1;       // physical window slot its insert filled (wp_n once absorbed)
   int ev_base = 0, ev_n = 0;  // this scan's k_iekf event pairs (vg_profile)
   double t = 0;            // scan end time (trajectory row)
   bool init_tail = false;  // the scan motion_init succeeded on: its trajectory row and

@@ -89,6 +89,15 @@ struct DownsampleBufs {
   int* flags = nullptr;  // [0] range error, [1] n_out
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
+  // the per-scan pipeline's downsample (ds_enqueue): hashed grouping, every
+  // count on the device. Voxel table (open addressing, cleared by its users):
+  uint64_t* hkey = nullptr;
+  int *hfirst = nullptr, *hcnt = nullptr, *hfill = nullptr, *hrank = nullptr, *hoff = nullptr;
+  int hmask = 0;
+  uint32_t* pslot = nullptr;  // per point: its voxel's table slot
+  uint32_t* pseg = nullptr;   // point indices grouped by voxel
+  int* tsum = nullptr;        // per 1024-point tile: first points, their points
+  int* hflags = nullptr;      // [0] range error (until the insert takes it), [1] n_out, [2] fallback needed
 };
 
 // ---- device-resident voxel map (replaces unordered_map<VOXEL_LOC, OctoTree*>
@@ -138,6 +147,7 @@ struct DevMap {
   int* wp_leaf = nullptr;      // leaf holding the point in its list, -1 = not listed
   int* counters = nullptr;     // device counters (see kCnt*)
   int* stamp = nullptr;        // per-node tag of the last IEKF iteration that read its plane (P_k, profiling pass)
+  int* wpn = nullptr;          // window points per physical slot (written by the insert, read by k_make_win)
 };
 enum {
   kCntNodes = 0, kCntFix = 1, kCntSlide = 2, kCntNew = 3, kCntTouched = 4, kCntWork = 5, kCntNext = 6,
@@ -145,7 +155,8 @@ enum {
   kCntGTouched = 16, kCntGSlide = 17,  // all-reduced copies (sharded mode) for the thread_num quirks
   kCntPlaneUpd = 18, kCntFixFull = 19,  // margi: plane_update calls, leaves with pcr_fix.N >= max_points
   kCntSlideBase = 20,                   // insert: surf_map_slide size before the scan's roots
-  kCntN = 21
+  kCntNds = 21,                         // insert: the downsampled points it took (N_ds of the scan)
+  kCntN = 22
 };
 
 // per-scan work buffers
@@ -201,7 +212,8 @@ struct DState {
   double traj[16];                  // R, p right after the IEKF (pub_localtraj, local_mapping.cpp:427)
   double xs[kMaxWin * kXS];         // window states x_buf by ord (local_mapping.cpp:434)
   double bias[kMaxWin * 12];        // IMU_PRE bias state per window factor: dbg, dba, dbg_buf, dba_buf
-  int it, rematch, done, iters, degenerate, matches[4], ticket, planes[4], pad[2];  // planes: P_k (profiling pass)
+  int it, rematch, done, iters, degenerate, matches[4], ticket, planes[4], rc_ctr, pad1;  // planes: P_k (profiling pass)
+  // rc_ctr: asynchronous recuts so far (k_fac_sort publishes it; vg_ctx::rc_pub mirrors it)
   // the scan this IEKF reads (set by k_scan_begin's caller, so the IEKF
   // launches are the same every scan and replay as one hipGraph)
   const float *sx, *sy, *sz;
@@ -217,6 +229,11 @@ struct DState {
 struct PushArg {
   int ord, new_imu;
   double rec[kBaImuRec];
+};
+// per-scan inputs of the replayed graphs, in host-mapped memory: the host
+// writes them before the launch, the kernels read them in place
+struct HostIn {
+  PushArg push;
 };
 // Spatial-tile sharding of one sequence over `world` contexts (one per GPU):
 // every context keeps the root voxels of the tiles it owns (tile_owner) and
@@ -274,6 +291,12 @@ struct vg_ctx {
   hipGraphExec_t g_iekf[3] = {nullptr, nullptr, nullptr};
   hipGraphExec_t g_margi = nullptr;  // margi after the window view (map.hip map_margi)
   hipGraphExec_t g_ba = nullptr;     // one LM iteration (ba.hip ba_run)
+  // steady state: the insert + recut of one scan, per ring position mp[0] (pipeline.cpp stage_insert_recut)
+  hipGraphExec_t g_mid[vg::kMaxWin] = {};
+  bool capturing = false;  // a stream capture is open (host-side steps that cannot be captured are deferred)
+  int rc_pub = 0;          // asynchronous recuts enqueued (mirrors DState::rc_ctr, k_fac_sort)
+  vg::HostIn* h_in = nullptr;  // host-mapped per-scan inputs of replayed graphs (host address)
+  vg::HostIn* d_in = nullptr;  // its device address
   bool use_graphs = true;  // margi prefix on the second stream
   std::string err;
   vg::Arena arena;
@@ -433,6 +456,12 @@ int ds_run(vg_ctx* ctx, const float* x, const float* y, const float* z, const fl
 // Host-synchronous.
 int ds_close(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* t, float tconst, int n,
              double voxel, float4* out, int* n_out);
+// The per-scan pipeline's downsample (hashed, no sort, no host count; output
+// in first-occurrence order), asynchronous on s, with the /2 fallback on the
+// device when `fallback`; the voxel count stays in ds.hflags[1].
+int ds_enqueue_hashed(vg_ctx* ctx, hipStream_t s, const float* x, const float* y, const float* z, const float* in,
+                      int n, double voxel, bool fallback, int pub_seq);
+int ds_reset(vg_ctx* ctx);
 // Same, asynchronous: n_out and the range flag are published to Pub (seq_ds).
 int ds_enqueue(vg_ctx* ctx, hipStream_t s, const float* x, const float* y, const float* z, const float* in, int n,
                double voxel, int pub_seq);
@@ -456,8 +485,9 @@ struct InsPre {
 };
 // push: the window push to fold into the insert's first launch (or nullptr);
 // pre: insert precomputed body points instead of the downsampled scan
+// nd: the point count on the device (n is then an upper bound, for grid sizes)
 int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread_num, const PushArg* push = nullptr,
-               const InsPre* pre = nullptr);
+               const InsPre* pre = nullptr, const int* nd = nullptr);
 int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num);
 int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* n_factors, bool replay = false,
               int pub_seq = 0);
@@ -479,7 +509,7 @@ int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* d
 int state_slide(vg_ctx* ctx, int win_count, int nimu);
 int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq);
 int state_publish_counters(vg_ctx* ctx, int seq);
-int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq);
+int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq, int* flags, bool reset);
 int state_deskew(vg_ctx* ctx, const double* par, int npose, const float* x, const float* y, const float* z,
                  const float* in, const float* t, int n);
 // initialisation: motion_blur's per-point part on a close-downsampled

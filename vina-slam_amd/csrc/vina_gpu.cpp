@@ -120,6 +120,13 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     return fail(VG_E_HIP);
   }
   memset(ctx->h_pub, 0, sizeof(Pub));
+  if ((e = hipHostMalloc((void**)&ctx->h_in, sizeof(HostIn), hipHostMallocMapped | hipHostMallocCoherent)) !=
+          hipSuccess ||
+      (e = hipHostGetDevicePointer((void**)&ctx->d_in, ctx->h_in, 0)) != hipSuccess) {
+    ctx->err = std::string("hipHostMalloc (mapped inputs): ") + hipGetErrorString(e);
+    return fail(VG_E_HIP);
+  }
+  memset(ctx->h_in, 0, sizeof(HostIn));
   if ((e = hipEventCreateWithFlags(&ctx->sync_ev, hipEventDisableTiming)) != hipSuccess) {
     ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
@@ -153,6 +160,9 @@ int vg_destroy(vg_ctx* ctx) {
     if (g) (void)hipGraphExecDestroy(g);
   if (ctx->g_margi) (void)hipGraphExecDestroy(ctx->g_margi);
   if (ctx->g_ba) (void)hipGraphExecDestroy(ctx->g_ba);
+  for (auto& g : ctx->g_mid)
+    if (g) (void)hipGraphExecDestroy(g);
+  if (ctx->h_in) (void)hipHostFree(ctx->h_in);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream_ds) (void)hipStreamSynchronize(ctx->stream_ds);
   if (ctx->stream_ds) (void)hipStreamDestroy(ctx->stream_ds);
