@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--workers", type=int, default=0,
                     help="scan-generation processes (0: min(16, cpus); 1 under a profiler)")
     ap.add_argument("--no-h2d", action="store_true", help="skip the host-input (vg_step) rate")
+    ap.add_argument("--multi", default="2,4,8",
+                    help="multi-sequence mode (vg_multi_*): B values to time at N=1 (empty: skip)")
     return ap.parse_args()
 
 
@@ -222,6 +224,9 @@ def main():
                        "scans": hi - lo, "reference": "CPU restatement, 5 threads, same scans",
                        "tolerance_m": 0.01}
     targets = {cfg: target_workload(args, cfg, sc, warmup, dev) for cfg, sc in tgt_scans.items()}
+    multi = None
+    if world == 1 and args.multi:
+        multi = multi_sequence(p, seq, scans, imus, warmup, total, dev, [int(b) for b in args.multi.split(",")])
 
     if rank == 0:
         line = {
@@ -237,7 +242,7 @@ def main():
                        "parallelism": ("tile-sharded x%d" if tile else "replica x%d") % world},
             "roofline": roof, "roofline_k_ba_solve": roof_solve, "roofline_k_iekf": roof_iekf,
             "host_ms_per_scan": host_ms, "host_input": h2d, "cpu_baseline": cpu, "ate_vs_cpu": ate_cpu,
-            "target_128line": targets or None,
+            "target_128line": targets or None, "multi_sequence": multi,
         }
         print(json.dumps(line))
     if world > 1:
@@ -271,6 +276,47 @@ def scan_roofline(stats, stage_stats, W, t_scan):
                               "P_k": round(p_mean, 1), "V_ins": mean("v_ins"), "V_slide": mean("n_slide"),
                               "F": mean("n_factors"), "I_H": mean("ba_hess"), "I_R": mean("ba_iters")},
             "note": "SURVEY 8(d) algorithmic bytes per scan / ms_per_step; P_k from the per-stage pass"}
+
+
+def multi_sequence(p, seq, scans, imus, warmup, total, dev, Bs):
+    """Multi-sequence mode (BASELINE config 5, vg_multi_*): B contexts on one
+    GPU, one native worker thread each, every context fed the same resident
+    scans (the throughput does not depend on the seed; tests/test_multi_gpu.py
+    checks distinct sequences bit for bit against lone runs). Whole-job
+    scans/s over the timed scans after the warm-up."""
+    import torch
+
+    import vgconfig
+    import vgpu
+    out = {"unit": "scans/s", "steps": total - warmup, "workers": "one native thread + two streams per sequence",
+           "wait_policy": "spin", "by_B": {}}
+    npmax = max(s[1] for s in scans) + 16
+    for B in Bs:
+        ctxs = [vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=npmax) for _ in range(B)]
+        for c in ctxs:
+            c.seed(seq.gt_state(0))
+        mv = vgpu.Multi(ctxs, 0, 0)
+
+        def step(k):
+            t, n, b, e = scans[k]
+            mv.step_dev([(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), 0, n, b, e,
+                          imus[k])] * B)
+
+        for k in range(warmup):
+            step(k)
+        mv.sync()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(warmup, total):
+            step(k)
+        mv.sync()
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        out["by_B"][str(B)] = round(B * (total - warmup) / dt, 1)
+        mv.close()
+        for c in ctxs:
+            c.close()
+    return out
 
 
 def host_input_rate(p, seq, host_scans, imus, warmup, steps, dev):

@@ -295,6 +295,33 @@ int vg_profile_read(vg_ctx* ctx, int stage, double* total_ms, int* count);
 /* HIP stream the context enqueues on (hipStream_t as void*). */
 void* vg_stream(vg_ctx* ctx);
 
+/* How the host waits for device results: spin for spin_us, then poll every
+ * sleep_us (sleep_us 0: spin only, the default and the lowest latency). Use
+ * sleeping polls when several contexts run from their own threads. */
+int vg_set_wait_policy(vg_ctx* ctx, int spin_us, int sleep_us);
+
+/* Multi-sequence mode (BASELINE config 5): B independent sequences on one
+ * GPU, each in its own context. vg_multi_create starts one native worker
+ * thread per context (and sets their wait policy); vg_multi_step_dev queues
+ * one scan per sequence (device-resident SoA, as vg_step_dev, or
+ * vg_step_deskew_dev when d_time != NULL; the point buffers must stay valid
+ * until vg_multi_sync, the IMU samples are copied) and returns — it blocks
+ * only when a sequence has 4 scans queued; the workers run free, in order per
+ * sequence. vg_multi_sync completes every queued scan. Each sequence's
+ * results are exactly those of a lone context. */
+typedef struct vg_scan_dev {
+  const float *d_x, *d_y, *d_z, *d_intensity, *d_time;
+  int n;
+  double pcl_beg_time, pcl_end_time;
+  const double* imu; /* host, m x 7 */
+  int m;
+} vg_scan_dev;
+typedef struct vg_multi vg_multi;
+vg_multi* vg_multi_create(vg_ctx** ctxs, int B, int spin_us, int sleep_us);
+int vg_multi_step_dev(vg_multi* mv, const vg_scan_dev* scans);
+int vg_multi_sync(vg_multi* mv);
+void vg_multi_destroy(vg_multi* mv);
+
 #ifdef __cplusplus
 }
 #endif

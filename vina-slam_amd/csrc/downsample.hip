@@ -351,8 +351,10 @@ __global__ void __launch_bounds__(256) k_hds_rank(int n, int ntile, DownsampleBu
   for (int k = 0; k < 4; k++) {
     if (f[k]) {
       const uint32_t s = d.pslot[i0 + k];
-      d.hrank[s] = bf + (int)(r >> 32);
+      const int v = bf + (int)(r >> 32);
+      d.hrank[s] = v;
       d.hoff[s] = bc + (int)(r & 0xffffffffull);
+      d.vfirst[v] = i0 + k;  // k_hds_mean walks the voxels, not the points
     }
     r += ((unsigned long long)f[k] << 32) | (unsigned long long)c[k];
   }
@@ -372,14 +374,15 @@ __global__ void __launch_bounds__(256) k_hds_scatter(int n, DownsampleBufs d, co
   }
 }
 
-__global__ void __launch_bounds__(256) k_hds_mean(int n, DownsampleBufs d, const float* __restrict__ x,
+__global__ void __launch_bounds__(256) k_hds_mean(DownsampleBufs d, const float* __restrict__ x,
                                                   const float* __restrict__ y, const float* __restrict__ z,
                                                   const float* __restrict__ in, const int* __restrict__ need) {
   if (need && !*need) return;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  const int nv = d.hflags[1];
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += gridDim.x * blockDim.x) {
+    const int i = d.vfirst[v];
     const uint32_t s = d.pslot[i];
-    if (d.hfirst[s] != i) continue;
-    const int b = d.hoff[s], cnt = d.hcnt[s], v = d.hrank[s];
+    const int b = d.hoff[s], cnt = d.hcnt[s];
     uint32_t* sg = d.pseg + b;
     for (int a = 1; a < cnt; a++) {  // back to input order (segments are short)
       const uint32_t key = sg[a];
@@ -434,7 +437,7 @@ int ds_enqueue_hashed(vg_ctx* ctx, hipStream_t s, const float* x, const float* y
       k_hds_tiles<<<ntile, kBlock, 0, s>>>(n, d, pin);
       k_hds_rank<<<ntile, kBlock, 0, s>>>(n, ntile, d, pin, pass == 0 && fallback ? need : nullptr, 2000);
       k_hds_scatter<<<g, kBlock, 0, s>>>(n, d, pin);
-      k_hds_mean<<<g, kBlock, 0, s>>>(n, d, x, y, z, in, pin);
+      k_hds_mean<<<g, kBlock, 0, s>>>(d, x, y, z, in, pin);
     }
   }
   if (pub_seq > 0) VG_TRY(state_publish_ds(ctx, s, pub_seq, d.hflags, false));
@@ -477,6 +480,7 @@ int ds_alloc(vg_ctx* ctx) {
   d.hoff = ctx->arena.take<int>(hs);
   d.pslot = ctx->arena.take<uint32_t>(n);
   d.pseg = ctx->arena.take<uint32_t>(n);
+  d.vfirst = ctx->arena.take<int>(n);
   d.tsum = ctx->arena.take<int>(2 * ((size_t)n / kHdsTile + 2));
   d.hflags = ctx->arena.take<int>(4);
   if (!d.keys || !d.seg || !d.oc || !d.tmp || !d.hkey || !d.hoff || !d.pseg || !d.tsum || !d.hflags) {

@@ -1,0 +1,137 @@
+// multi.cpp — multi-sequence mode: B independent sequences on one GPU, each
+// context driven by its own native worker thread (BASELINE config 5, SURVEY §7
+// "Hard parts"). vg_multi_step_dev queues one scan per sequence and returns;
+// every worker runs its context's scans in order, free-running (no lock-step
+// between sequences), so the contexts' own streams (two each) overlap on the
+// device. Each worker runs exactly the single-sequence path (host_step), so
+// every sequence's results are those of a lone context, bit for bit.
+//
+// Why threads and not one launch for B sequences: the per-scan path is ~90
+// small dependent kernels whose cost is dispatch + cross-XCD memory latency,
+// not arithmetic; on MI355X independent per-stream launches overlap
+// (scripts/micro/concurrency.hip: 1.6M kernels/s over 16 streams vs 0.3M for
+// one graph holding the same parallel chains), so per-sequence streams are the
+// shape that fills the chip. The workers sleep-poll their waits
+// (vg_set_wait_policy) because the box's CPU quota is shared by all of them.
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+#include "vg_host.h"
+
+namespace {
+struct Job {
+  vg_scan_dev sc;
+  std::vector<double> imu;  // the scan's IMU samples (the caller's buffer may be reused)
+};
+struct Worker {
+  std::deque<Job> q;
+  int rc = VG_OK;
+};
+}  // namespace
+
+struct vg_multi {
+  std::vector<vg_ctx*> ctx;
+  std::vector<Worker> wk;
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv_job, cv_room;
+  bool quit = false;
+  int depth = 4;  // scans queued per sequence before vg_multi_step_dev blocks
+  int busy = 0;   // workers inside a step
+};
+
+static void worker(vg_multi* M, int b) {
+  for (;;) {
+    Job j;
+    {
+      std::unique_lock<std::mutex> lk(M->mu);
+      M->cv_job.wait(lk, [&] { return M->quit || !M->wk[b].q.empty(); });
+      if (M->wk[b].q.empty()) return;  // quit with nothing left
+      j = std::move(M->wk[b].q.front());
+      M->wk[b].q.pop_front();
+      M->busy++;
+    }
+    M->cv_room.notify_all();
+    vg_ctx* c = M->ctx[b];
+    const vg_scan_dev& sc = j.sc;
+    const double* imu = j.imu.empty() ? nullptr : j.imu.data();
+    int r;
+    if (sc.d_time)
+      r = vg_step_deskew_dev(c, sc.d_x, sc.d_y, sc.d_z, sc.d_intensity, sc.d_time, sc.n, sc.pcl_beg_time,
+                             sc.pcl_end_time, imu, sc.m);
+    else
+      r = vg_step_dev(c, sc.d_x, sc.d_y, sc.d_z, sc.d_intensity, sc.n, sc.pcl_beg_time, sc.pcl_end_time, imu, sc.m);
+    {
+      std::lock_guard<std::mutex> lk(M->mu);
+      if (r != VG_OK && M->wk[b].rc == VG_OK) M->wk[b].rc = r;
+      M->busy--;
+    }
+    M->cv_room.notify_all();
+  }
+}
+
+extern "C" {
+
+vg_multi* vg_multi_create(vg_ctx** ctxs, int B, int spin_us, int sleep_us) {
+  if (!ctxs || B <= 0) return nullptr;
+  vg_multi* M = new vg_multi();
+  M->ctx.assign(ctxs, ctxs + B);
+  M->wk.resize(B);
+  for (int b = 0; b < B; b++) vg_set_wait_policy(ctxs[b], spin_us, sleep_us);
+  for (int b = 0; b < B; b++) M->th.emplace_back(worker, M, b);
+  return M;
+}
+
+int vg_multi_step_dev(vg_multi* M, const vg_scan_dev* scans) {
+  if (!M || !scans) return VG_E_ARG;
+  std::unique_lock<std::mutex> lk(M->mu);
+  for (size_t b = 0; b < M->ctx.size(); b++) {
+    M->cv_room.wait(lk, [&] { return (int)M->wk[b].q.size() < M->depth; });
+    if (M->wk[b].rc != VG_OK) return M->wk[b].rc;
+    Job j;
+    j.sc = scans[b];
+    if (scans[b].imu && scans[b].m > 0) j.imu.assign(scans[b].imu, scans[b].imu + 7 * (size_t)scans[b].m);
+    j.sc.imu = nullptr;
+    M->wk[b].q.push_back(std::move(j));
+  }
+  lk.unlock();
+  M->cv_job.notify_all();
+  return VG_OK;
+}
+
+int vg_multi_sync(vg_multi* M) {
+  if (!M) return VG_E_ARG;
+  {
+    std::unique_lock<std::mutex> lk(M->mu);
+    M->cv_room.wait(lk, [&] {
+      if (M->busy) return false;
+      for (const Worker& w : M->wk)
+        if (!w.q.empty()) return false;
+      return true;
+    });
+    for (const Worker& w : M->wk)
+      if (w.rc != VG_OK) return w.rc;
+  }
+  int rc = VG_OK;
+  for (vg_ctx* c : M->ctx) {
+    vg_stats st;
+    const int r = vg_get_stats(c, &st);  // completes every enqueued scan of the context
+    if (r != VG_OK && rc == VG_OK) rc = r;
+  }
+  return rc;
+}
+
+void vg_multi_destroy(vg_multi* M) {
+  if (!M) return;
+  {
+    std::lock_guard<std::mutex> lk(M->mu);
+    M->quit = true;
+  }
+  M->cv_job.notify_all();
+  for (auto& t : M->th) t.join();
+  delete M;
+}
+
+}  // extern "C"

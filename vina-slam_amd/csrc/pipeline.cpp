@@ -772,11 +772,12 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   const vg_config& c = ctx->cfg;
   if (init_active(hp(ctx))) return init_step(ctx, dx, dy, dz, di, nullptr, n, beg, end, imu, m);
   VG_TRY(stage_propagate(ctx, imu, m, beg, end));
-  // the IEKF is enqueued before the downsample: both read only the raw scan
-  // (local_mapping.cpp:396-413), and the main stream should not idle while the
-  // host enqueues the downsample onto its own stream
-  VG_TRY(stage_iekf(ctx, dx, dy, dz, n, nullptr));
+  // both read only the raw scan (local_mapping.cpp:396-413). The downsample is
+  // enqueued first: its stream waits only for the previous insert, so it runs
+  // under the previous scan's margi, and the IEKF (queued behind that margi on
+  // the main stream) loses nothing
   VG_TRY(stage_downsample(ctx, dx, dy, dz, di, n, nullptr));
+  VG_TRY(stage_iekf(ctx, dx, dy, dz, n, nullptr));
   VG_TRY(stage_window_push(ctx, imu, m));
   if (mid_graph_ok(ctx, hp(ctx))) {
     VG_TRY(stage_insert_recut(ctx));

@@ -9,6 +9,7 @@
 #include <functional>
 #include <cstdint>
 #include <string>
+#include <thread>
 #include <vector>
 #include "../../include/vina_gpu.h"
 #include "vg_la.h"
@@ -96,6 +97,7 @@ struct DownsampleBufs {
   int hmask = 0;
   uint32_t* pslot = nullptr;  // per point: its voxel's table slot
   uint32_t* pseg = nullptr;   // point indices grouped by voxel
+  int* vfirst = nullptr;      // per voxel (output rank): its first point
   int* tsum = nullptr;        // per 1024-point tile: first points, their points
   int* hflags = nullptr;      // [0] range error (until the insert takes it), [1] n_out, [2] fallback needed
 };
@@ -317,6 +319,7 @@ struct vg_ctx {
   double* h_stage = nullptr;    // pinned staging for asynchronous H2D copies (kStageBytes)
   double* d_deskew = nullptr;   // deskew parameters (x_curr pose, extrinsic, IMU poses)
   int pub_seq = 0;
+  int wait_spin_us = 0, wait_sleep_us = 0;  // vg_set_wait_policy (0 sleep: spin)
   int plane_tag = 0;        // IEKF iteration tag of the P_k count (vg_profile stages)
   int* h_pinned = nullptr;  // small pinned host scratch for counters
 
@@ -350,12 +353,16 @@ constexpr size_t kStageDeskewOff = 8192;  // doubles: the deskew block's part of
 constexpr int kDeskewBuf = 4096;          // doubles (up to 180 IMU segments per scan)
 // Spin until a Pub sequence flag reaches seq (the device publishes with a
 // system-scope release); checks the stream for errors while spinning.
+// Wait policy (vg_set_wait_policy): spin for spin_us, then sleep sleep_us per
+// poll. Pure spinning (the default) has the lowest latency for one context;
+// several contexts driven from their own threads under a CPU quota need the
+// sleeping polls, or the spinning threads starve each other's launches.
+inline void wait_pause(const vg_ctx* c, long spin, std::chrono::steady_clock::time_point t0);
 inline int pub_wait(vg_ctx* c, const int* flag, int seq, const char* what, hipStream_t producer = nullptr) {
   hipStream_t st = producer ? producer : c->stream;  // the stream the publishing kernel runs on
+  const auto t0 = std::chrono::steady_clock::now();
   for (long spin = 0; __atomic_load_n(flag, __ATOMIC_ACQUIRE) < seq; spin++) {
-#if defined(__x86_64__)
-    __builtin_ia32_pause();
-#endif
+    wait_pause(c, spin, t0);
     if ((spin & 4095) == 4095) {
       const hipError_t e = hipStreamQuery(st);
       if (e != hipSuccess && e != hipErrorNotReady) {
@@ -402,12 +409,17 @@ inline void prof_end(vg_ctx* c, int id, hipStream_t s = nullptr) {
 inline hipError_t stream_wait(vg_ctx* c) {
   hipError_t e = hipEventRecord(c->sync_ev, c->stream);
   if (e != hipSuccess) return e;
-  while ((e = hipEventQuery(c->sync_ev)) == hipErrorNotReady) {
-#if defined(__x86_64__)
-    __builtin_ia32_pause();
-#endif
-  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (long spin = 0; (e = hipEventQuery(c->sync_ev)) == hipErrorNotReady; spin++) wait_pause(c, spin, t0);
   return e;
+}
+inline void wait_pause(const vg_ctx* c, long spin, std::chrono::steady_clock::time_point t0) {
+#if defined(__x86_64__)
+  __builtin_ia32_pause();
+#endif
+  if (c->wait_sleep_us <= 0 || (spin & 63) != 63) return;
+  const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  if (us >= c->wait_spin_us) std::this_thread::sleep_for(std::chrono::microseconds(c->wait_sleep_us));
 }
 }  // namespace vg
 

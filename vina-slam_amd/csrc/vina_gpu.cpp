@@ -457,6 +457,13 @@ int vg_win_count(vg_ctx* ctx, int* n) {
   return VG_OK;
 }
 
+int vg_set_wait_policy(vg_ctx* ctx, int spin_us, int sleep_us) {
+  if (!ctx || spin_us < 0 || sleep_us < 0) return VG_E_ARG;
+  ctx->wait_spin_us = spin_us;
+  ctx->wait_sleep_us = sleep_us;
+  return VG_OK;
+}
+
 int vg_profile(vg_ctx* ctx, int on) {
   if (!ctx) return VG_E_ARG;
   ctx->prof_on = (on & 1) != 0;

@@ -34,6 +34,13 @@ class LidarFormat(ctypes.Structure):
                 ("time_base", ctypes.c_double)]
 
 
+class ScanDev(ctypes.Structure):
+    _fields_ = [("d_x", ctypes.c_void_p), ("d_y", ctypes.c_void_p), ("d_z", ctypes.c_void_p),
+                ("d_intensity", ctypes.c_void_p), ("d_time", ctypes.c_void_p), ("n", ctypes.c_int),
+                ("pcl_beg_time", ctypes.c_double), ("pcl_end_time", ctypes.c_double),
+                ("imu", ctypes.POINTER(ctypes.c_double)), ("m", ctypes.c_int)]
+
+
 class Stats(ctypes.Structure):
     _fields_ = [("n_raw", ctypes.c_int), ("n_ds", ctypes.c_int), ("iekf_iters", ctypes.c_int),
                 ("iekf_matches", ctypes.c_int * 4), ("roots_new", ctypes.c_int), ("n_slide", ctypes.c_int),
@@ -68,7 +75,7 @@ def build(jobs=8):
 def header_symbols():
     """Every function the C-ABI header declares."""
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void\*|const char\*)\s+(vg_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void\*?|const char\*|vg_\w+\*)\s+(vg_\w+)\s*\(", txt, re.M)))
 
 
 _lib = None
@@ -130,6 +137,12 @@ def lib():
         L.vg_shard_host.argtypes = [P, ctypes.c_int, ctypes.c_int, HOST_ALLREDUCE, P]
         L.vg_stream.argtypes = [P]
         L.vg_stream.restype = P
+        L.vg_set_wait_policy.argtypes = [P, ctypes.c_int, ctypes.c_int]
+        L.vg_multi_create.argtypes = [ctypes.POINTER(P), ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.vg_multi_create.restype = P
+        L.vg_multi_step_dev.argtypes = [P, ctypes.POINTER(ScanDev)]
+        L.vg_multi_sync.argtypes = [P]
+        L.vg_multi_destroy.argtypes = [P]
         L.vgx_debug.argtypes = [P, ctypes.c_int, ctypes.c_int]
         L.vgx_ba_capture.argtypes = [P, dp, ctypes.c_int, ip]
         _lib = L
@@ -418,4 +431,41 @@ class Sync:
         if rd.value < 0:
             return "dropped"
         return (sid.value, b.value, e.value, out[: m.value].copy()) if rd.value else None
+
+
+class Multi:
+    """Multi-sequence mode (vg_multi_*): B contexts stepped together, one
+    native worker thread each."""
+
+    def __init__(self, contexts, spin_us=20, sleep_us=20):
+        self.contexts = list(contexts)
+        arr = (ctypes.c_void_p * len(self.contexts))(*[c.h.value for c in self.contexts])
+        self.h = lib().vg_multi_create(arr, len(self.contexts), spin_us, sleep_us)
+        if not self.h:
+            raise VgError("vg_multi_create failed")
+        self._keep = []
+
+    def step_dev(self, scans):
+        """scans: per context (d_x, d_y, d_z, d_intensity, d_time or 0, n, beg, end, imu (m,7) float64)."""
+        B = len(self.contexts)
+        arr = (ScanDev * B)()
+        keep = []
+        for b, (x, y, z, i, t, n, beg, end, imu) in enumerate(scans):
+            imu = np.ascontiguousarray(imu, dtype=np.float64).reshape(-1, 7)
+            keep.append(imu)
+            arr[b] = ScanDev(x, y, z, i, t or None, n, beg, end, _d(imu), imu.shape[0])
+        r = lib().vg_multi_step_dev(self.h, arr)
+        if r != 0:
+            raise VgError("vg_multi_step_dev failed (%d): %s" % (
+                r, "; ".join(lib().vg_last_error(c.h).decode() for c in self.contexts)))
+
+    def sync(self):
+        r = lib().vg_multi_sync(self.h)
+        if r != 0:
+            raise VgError("vg_multi_sync failed (%d)" % r)
+
+    def close(self):
+        if self.h:
+            lib().vg_multi_destroy(self.h)
+            self.h = None
 
