@@ -82,6 +82,10 @@ def gen_scans(lidar, seq_id, general, n, workers):
 
 def main():
     args = parse()
+    if args.multi and "GPU_MAX_HW_QUEUES" not in os.environ:
+        # the multi-sequence leg runs two streams per sequence: let HIP map them
+        # to separate hardware queues (HIP's default is 4; read at HIP start-up)
+        os.environ["GPU_MAX_HW_QUEUES"] = "16"
     import synth
     import vgconfig
 

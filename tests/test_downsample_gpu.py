@@ -71,3 +71,52 @@ def test_downsample_golden(ctx):
     d = np.load(os.path.join(os.path.dirname(__file__), "golden", "downsample_tiny.npz"))
     g = ctx.downsample(d["xyz"], d["inten"], float(d["size"]))
     assert np.array_equal(_canon(g).view(np.uint32), _canon(d["out"]).view(np.uint32))
+
+
+def _first_occurrence_order(xyz, size):
+    """The hashed path's documented output order: voxels by their first point index."""
+    loc = (np.asarray(xyz, np.float32).astype(np.float64) / size).astype(np.float32)
+    loc = np.where(loc < 0, (loc.astype(np.float64) - 1.0).astype(np.float32), loc)
+    keys = [tuple(k) for k in loc.astype(np.int64)]
+    seen, order = set(), []
+    for k in keys:
+        if k not in seen:
+            seen.add(k)
+            order.append(k)
+    return order
+
+
+@pytest.mark.parametrize("case", ["scan", "dense", "giant", "ring_wrap"])
+def test_hashed_downsample_bit_exact(ctx, oracle_lib, case):
+    """The per-scan pipeline's hashed downsample (ds_enqueue_hashed: no sort,
+    the voxel count on the device) = the oracle's down_sampling_voxel bit for
+    bit as a set, emitted in first-occurrence order — including dense voxels
+    (> 32 points: the workgroup bitmap path) with index ranges wider than one
+    bitmap window."""
+    rng = np.random.default_rng(7)
+    size = 0.1
+    if case == "scan":
+        seq = synth.Sequence("64line", seq_id=3, blind=1.0)
+        xyz, inten, _, _ = seq.scan(5)
+    elif case == "dense":  # many voxels of 40-400 points
+        c = rng.uniform(-5, 5, (300, 3))
+        xyz = (c[rng.integers(0, 300, 60_000)] + rng.normal(0, 0.01, (60_000, 3))).astype(np.float32)
+        inten = rng.uniform(0, 100, 60_000).astype(np.float32)
+    elif case == "giant":  # one voxel holding 50 k points
+        xyz = (rng.normal(0, 0.005, (50_000, 3)) + 3.05).astype(np.float32)
+        inten = np.arange(50_000, dtype=np.float32)
+    else:  # one voxel's points at both ends of a 300 k-point sweep (index range > one bitmap window)
+        bg = rng.uniform(-50, 50, (300_000, 3)).astype(np.float32)
+        bg[:100] = (rng.normal(0, 0.005, (100, 3)) + 7.05).astype(np.float32)
+        bg[-100:] = (rng.normal(0, 0.005, (100, 3)) + 7.05).astype(np.float32)
+        xyz, inten = bg, rng.uniform(0, 1, 300_000).astype(np.float32)
+    g = ctx.downsample_hashed(xyz, inten, size)
+    o = oracle.downsample(xyz, inten, size)
+    assert g.shape == o.shape
+    assert np.array_equal(_canon(g).view(np.uint32), _canon(o).view(np.uint32))
+    if case != "scan":
+        order = _first_occurrence_order(xyz, size)
+        loc = (g[:, :3].astype(np.float64) / size).astype(np.float32)
+        got = [tuple(k) for k in np.where(loc < 0, (loc.astype(np.float64) - 1.0).astype(np.float32),
+                                          loc).astype(np.int64)]
+        assert got == order

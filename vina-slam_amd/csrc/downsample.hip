@@ -231,6 +231,7 @@ __device__ __forceinline__ uint32_t hds_hash(uint64_t k, int mask) {
   return (uint32_t)k & (uint32_t)mask;
 }
 constexpr int kHdsTile = 1024;  // points per tile (256 lanes x 4)
+constexpr int kHdsSmall = 32;   // a lane sorts a voxel's segment itself up to this many points
 constexpr int kHdsEmptyFirst = 0x7f7f7f7f;  // above every point index (ds_reset's memset byte)
 
 __global__ void __launch_bounds__(256) k_hds_insert(int n, const float* __restrict__ x, const float* __restrict__ y,
@@ -361,6 +362,7 @@ __global__ void __launch_bounds__(256) k_hds_rank(int n, int ntile, DownsampleBu
   if (blockIdx.x == ntile - 1 && threadIdx.x == 0) {
     const int nv = bf + (int)(tot >> 32);
     d.hflags[1] = nv;
+    d.hflags[3] = 0;  // dense voxels deferred by k_hds_mean
     if (need_out) *need_out = nv < min_out ? 1 : 0;
   }
 }
@@ -383,8 +385,12 @@ __global__ void __launch_bounds__(256) k_hds_mean(DownsampleBufs d, const float*
     const int i = d.vfirst[v];
     const uint32_t s = d.pslot[i];
     const int b = d.hoff[s], cnt = d.hcnt[s];
+    if (cnt > kHdsSmall) {  // a dense voxel: a workgroup puts it back in order (k_hds_big)
+      d.bigv[atomicAdd(&d.hflags[3], 1)] = v;
+      continue;
+    }
     uint32_t* sg = d.pseg + b;
-    for (int a = 1; a < cnt; a++) {  // back to input order (segments are short)
+    for (int a = 1; a < cnt; a++) {  // back to input order (short segments)
       const uint32_t key = sg[a];
       int q = a - 1;
       while (q >= 0 && sg[q] > key) {
@@ -414,6 +420,93 @@ __global__ void __launch_bounds__(256) k_hds_mean(DownsampleBufs d, const float*
   }
 }
 
+// Dense voxels (more than kHdsSmall points): one workgroup each restores the
+// input order of the voxel's segment with an LDS bitmap over its index range
+// (windows of kHdsBits indices; set bits compacted by a block scan — O(points +
+// range/32), exact for any size), then three lanes run the x, y and z
+// recurrences (the same arithmetic as k_hds_mean, bit for bit).
+constexpr int kHdsBits = 1 << 18;          // indices per bitmap window (32 KB of LDS)
+constexpr int kHdsWords = kHdsBits / 32;
+__global__ void __launch_bounds__(256) k_hds_big(DownsampleBufs d, const float* __restrict__ x,
+                                                 const float* __restrict__ y, const float* __restrict__ z,
+                                                 const float* __restrict__ in, const int* __restrict__ need) {
+  if (need && !*need) return;
+  __shared__ uint32_t bm[kHdsWords];
+  __shared__ int s_w[4], s_base;
+  const int nbig = d.hflags[3];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int q = blockIdx.x; q < nbig; q += gridDim.x) {
+    const int v = d.bigv[q];
+    const int i0 = d.vfirst[v];  // the voxel's smallest index
+    const uint32_t s = d.pslot[i0];
+    const int b = d.hoff[s], cnt = d.hcnt[s];
+    const uint32_t* sg = d.pseg + b;
+    uint32_t* out = d.pseg2 + b;
+    int hi = i0;
+    for (int e = tid; e < cnt; e += blockDim.x) hi = max(hi, (int)sg[e]);
+    for (int o = 32; o > 0; o >>= 1) hi = max(hi, __shfl_down(hi, o, 64));
+    if (lane == 0) s_w[wv] = hi;
+    __syncthreads();
+    hi = max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3]));
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+    for (int w0 = i0; w0 <= hi; w0 += kHdsBits) {
+      for (int k = tid; k < kHdsWords; k += blockDim.x) bm[k] = 0u;
+      __syncthreads();
+      for (int e = tid; e < cnt; e += blockDim.x) {
+        const int off = (int)sg[e] - w0;
+        if (off >= 0 && off < kHdsBits) atomicOr(&bm[off >> 5], 1u << (off & 31));
+      }
+      __syncthreads();
+      constexpr int per = kHdsWords / 256;  // words per thread, contiguous
+      int mine = 0;
+      for (int k = 0; k < per; k++) mine += __popc(bm[tid * per + k]);
+      int xs = mine;  // block exclusive scan
+      for (int o = 1; o < 64; o <<= 1) {
+        const int yv = __shfl_up(xs, o, 64);
+        if (lane >= o) xs += yv;
+      }
+      __syncthreads();
+      if (lane == 63) s_w[wv] = xs;
+      __syncthreads();
+      int base = s_base;
+      for (int k = 0; k < wv; k++) base += s_w[k];
+      base += xs - mine;
+      for (int k = 0; k < per; k++) {
+        uint32_t m = bm[tid * per + k];
+        while (m) {
+          const int bit = __ffs(m) - 1;
+          m &= m - 1;
+          out[base++] = (uint32_t)(w0 + (tid * per + k) * 32 + bit);
+        }
+      }
+      __syncthreads();
+      if (tid == 0) s_base += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+      __syncthreads();
+    }
+    if (tid < 3) {  // point_utils.hpp:34-37 per coordinate, as written
+      const float* a = tid == 0 ? x : (tid == 1 ? y : z);
+      float p = a[i0], c = 1.0f;
+      for (int e = 1; e < cnt; e++) {
+        p = (p * c + a[out[e]]) / (c + 1);
+        c += 1;
+      }
+      (tid == 0 ? d.ox : (tid == 1 ? d.oy : d.oz))[v] = p;
+      if (tid == 0) {
+        d.oi[v] = in ? in[i0] : 0.0f;
+        d.oc[v] = c;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      d.hkey[s] = kKeyEmpty;
+      d.hfirst[s] = kHdsEmptyFirst;
+      d.hcnt[s] = 0;
+      d.hfill[s] = 0;
+    }
+  }
+}
+
 // the pipeline's downsample, asynchronous on stream s; with `fallback`, the
 // /2 pass of local_mapping.cpp:399-403 runs on the device when fewer than
 // 2000 voxels came out. hflags[1] = the voxel count (device), published to
@@ -438,6 +531,7 @@ int ds_enqueue_hashed(vg_ctx* ctx, hipStream_t s, const float* x, const float* y
       k_hds_rank<<<ntile, kBlock, 0, s>>>(n, ntile, d, pin, pass == 0 && fallback ? need : nullptr, 2000);
       k_hds_scatter<<<g, kBlock, 0, s>>>(n, d, pin);
       k_hds_mean<<<g, kBlock, 0, s>>>(d, x, y, z, in, pin);
+      k_hds_big<<<64, kBlock, 0, s>>>(d, x, y, z, in, pin);
     }
   }
   if (pub_seq > 0) VG_TRY(state_publish_ds(ctx, s, pub_seq, d.hflags, false));
@@ -481,6 +575,8 @@ int ds_alloc(vg_ctx* ctx) {
   d.pslot = ctx->arena.take<uint32_t>(n);
   d.pseg = ctx->arena.take<uint32_t>(n);
   d.vfirst = ctx->arena.take<int>(n);
+  d.bigv = ctx->arena.take<int>(n);
+  d.pseg2 = ctx->arena.take<uint32_t>(n);
   d.tsum = ctx->arena.take<int>(2 * ((size_t)n / kHdsTile + 2));
   d.hflags = ctx->arena.take<int>(4);
   if (!d.keys || !d.seg || !d.oc || !d.tmp || !d.hkey || !d.hoff || !d.pseg || !d.tsum || !d.hflags) {

@@ -518,6 +518,33 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
   return VG_E_ARG;
 }
 
+// Test-only: the per-scan pipeline's hashed downsample (ds_enqueue_hashed,
+// fallback off) of a host cloud: [x, y, z, intensity, count] per voxel in its
+// first-occurrence order.
+extern "C" int vgx_downsample_hashed(vg_ctx* ctx, const float* xyz, const float* intensity, int n, double voxel,
+                                     float* out_xyzic, int* n_out) {
+  if (!ctx || !xyz || !out_xyzic || !n_out || n <= 0) return VG_E_ARG;
+  VG_TRY(host_sync(ctx));
+  VG_HIP(hipStreamSynchronize(ctx->stream_ds));
+  VG_TRY(upload_aos(ctx, xyz, intensity, n));
+  VG_TRY(ds_enqueue_hashed(ctx, ctx->stream, ctx->d_x, ctx->d_y, ctx->d_z, ctx->d_i, n, voxel, false, 0));
+  hipStream_t s = ctx->stream;
+  VG_HIP(hipMemcpyAsync(ctx->h_pinned, ctx->ds.hflags, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+  VG_HIP(hipStreamSynchronize(s));
+  const int m = ctx->h_pinned[1];
+  const DownsampleBufs& d = ctx->ds;
+  std::vector<float> buf((size_t)m * 5);
+  const float* cols[5] = {d.ox, d.oy, d.oz, d.oi, d.oc};
+  for (int c = 0; c < 5; c++)
+    VG_HIP(hipMemcpyAsync(buf.data() + (size_t)c * m, cols[c], m * sizeof(float), hipMemcpyDeviceToHost, s));
+  VG_HIP(hipMemsetAsync(ctx->ds.hflags, 0, sizeof(int), s));  // the range flag (no insert consumes it here)
+  VG_HIP(hipStreamSynchronize(s));
+  for (int v = 0; v < m; v++)
+    for (int c = 0; c < 5; c++) out_xyzic[5 * v + c] = buf[(size_t)c * m + v];
+  *n_out = m;
+  return ctx->h_pinned[0] ? VG_E_RANGE : VG_OK;
+}
+
 // Test-only: the captured first Hessian pass of an LM run (vgx_debug 5), as
 // [6W x 6W LiDAR Hessian (full, row-major), 6W gradient, residual, then per
 // IMU factor k: J^T C J 30 x 30, J^T C r 30, r^T C r] — the oracle's

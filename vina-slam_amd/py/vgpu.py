@@ -144,6 +144,7 @@ def lib():
         L.vg_multi_sync.argtypes = [P]
         L.vg_multi_destroy.argtypes = [P]
         L.vgx_debug.argtypes = [P, ctypes.c_int, ctypes.c_int]
+        L.vgx_downsample_hashed.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, fp, ip]
         L.vgx_ba_capture.argtypes = [P, dp, ctypes.c_int, ip]
         _lib = L
     return _lib
@@ -193,6 +194,16 @@ class Context:
         n = ctypes.c_int(0)
         self._chk(lib().vg_downsample(self.h, _f(xyz), _f(inten), xyz.shape[0], size, _f(out), ctypes.byref(n)),
                   "vg_downsample")
+        return out[: n.value]
+
+    def downsample_hashed(self, xyz, inten, size):
+        """The per-scan pipeline's downsample (test hook): (m,5) in first-occurrence order."""
+        xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+        inten = np.ascontiguousarray(inten, dtype=np.float32)
+        out = np.zeros((max(xyz.shape[0], 1), 5), dtype=np.float32)
+        n = ctypes.c_int(0)
+        self._chk(lib().vgx_downsample_hashed(self.h, _f(xyz), _f(inten), xyz.shape[0], size, _f(out),
+                                              ctypes.byref(n)), "vgx_downsample_hashed")
         return out[: n.value]
 
     def downsample_close(self, xyz, times, size):
