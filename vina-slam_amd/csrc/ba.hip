@@ -1187,18 +1187,24 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
   // One iteration ahead: iteration k+1 is enqueued before the host waits for
   // iteration k's flags, so the stream never drains; a converged LM leaves at
   // most one early-exiting iteration behind (optimizers.cpp:449, at most 10).
+  // Except at the iteration count the previous LM run converged at: there the
+  // host waits first (a round trip, ~15 us) rather than queue an iteration
+  // that most likely early-exits (~35 us of dispatches). Results do not depend
+  // on it: the device-side flags decide.
   iteration(0);
-  int done_iters = 0;
+  int enq = 1, done_iters = 0;  // iterations enqueued so far
   for (int k = 0; k < 10; k++) {
-    if (k + 1 < 10) iteration(k + 1);
+    if (enq == k + 1 && enq < 10 && enq < ctx->ba_last_iters) iteration(enq++);  // one ahead
     VG_HIP(hipGetLastError());
     VG_TRY(xerr);
     if (k == 0 && before_first_wait) VG_TRY(before_first_wait());
     VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ba, seq0 + k, "k_ba_control"));
     done_iters = __atomic_load_n(&ctx->h_pub->ba_iters, __ATOMIC_ACQUIRE);
     if (__atomic_load_n(&ctx->h_pub->ba_done, __ATOMIC_ACQUIRE)) break;
+    if (enq == k + 1 && enq < 10) iteration(enq++);  // not queued ahead: now
   }
   *iters = done_iters;
+  ctx->ba_last_iters = done_iters > 0 ? done_iters : 2;
   if (solve_ev)  // k_ba_solve of the executed iterations only (the bench's roofline)
     for (int it = 0; it < done_iters && it < 10; it++) {
       float ms = 0;

@@ -299,6 +299,7 @@ struct vg_ctx {
   hipGraphExec_t g_mid[vg::kMaxWin] = {};
   bool capturing = false;  // a stream capture is open (host-side steps that cannot be captured are deferred)
   int rc_pub = 0;          // asynchronous recuts enqueued (mirrors DState::rc_ctr, k_fac_sort)
+  int ba_last_iters = 2;   // LM iterations of the previous run (ba_run's enqueue-ahead policy)
   vg::HostIn* h_in = nullptr;  // host-mapped per-scan inputs of replayed graphs (host address)
   vg::HostIn* d_in = nullptr;  // its device address
   bool use_graphs = true;  // margi prefix on the second stream
