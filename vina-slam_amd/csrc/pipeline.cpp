@@ -223,6 +223,31 @@ int host_sync(vg_ctx* ctx) {
 
 // IMUEKF::motion_blur state/covariance propagation (imu_ekf.cpp:28-94); the
 // per-point deskew (114-144) is SURVEY row f1 (callers pass compensated scans).
+// one row of a sparse 15x15 matrix: its non-zero columns, ascending
+struct SpRow {
+  int n;
+  int k[7];
+  double v[7];
+};
+// F C F^T + Q with F given by its rows; every sum in ascending column order
+// (the dense product's order, zero terms dropped)
+static M15 sandwich(const SpRow* F, const M15& C, const M15& Q) {
+  M15 A, out;
+  for (int i = 0; i < 15; i++)
+    for (int j = 0; j < 15; j++) {
+      double s = F[i].v[0] * C(F[i].k[0], j);
+      for (int t = 1; t < F[i].n; t++) s += F[i].v[t] * C(F[i].k[t], j);
+      A(i, j) = s;
+    }
+  for (int i = 0; i < 15; i++)
+    for (int j = 0; j < 15; j++) {
+      double s = A(i, F[j].k[0]) * F[j].v[0];
+      for (int t = 1; t < F[j].n; t++) s += A(i, F[j].k[t]) * F[j].v[t];
+      out(i, j) = s + Q(i, j);
+    }
+  return out;
+}
+
 void propagate(vg_ctx* ctx, HostPipe* P, const std::vector<Imu>& imus, double pcl_beg, double pcl_end) {
   P->poses.clear();
   const vg_config& c = ctx->cfg;
@@ -256,25 +281,31 @@ void propagate(vg_ctx* ctx, HostPipe* P, const std::vector<Imu>& imus, double pc
     }
     M3 ask = hat(acc_avr);
     M3 Exp_f = Exp(angvel, dt);
-    M15 F = M15::I(), cw = M15::Z();
+    M15 cw = M15::Z();
     M3 F00 = Exp(angvel, -dt), F60 = scl(mul(R_imu, ask), -dt), F612 = scl(R_imu, -dt);
     M3 ca = M3::Z();
     for (int j = 0; j < 3; j++) ca(j, j) = c.odo_cov_acc;
     M3 cw66 = scl(mul(mul(R_imu, ca), tr(R_imu)), dt * dt);
     for (int r = 0; r < 3; r++) {
-      for (int q = 0; q < 3; q++) {
-        F(r, q) = F00(r, q);
-        F(6 + r, q) = F60(r, q);
-        F(6 + r, 12 + q) = F612(r, q);
-        cw(6 + r, 6 + q) = cw66(r, q);
-      }
-      F(r, 9 + r) = -dt;
-      F(3 + r, 6 + r) = dt;
+      for (int q = 0; q < 3; q++) cw(6 + r, 6 + q) = cw66(r, q);
       cw(r, r) = c.odo_cov_gyr * dt * dt;
       cw(9 + r, 9 + r) = c.odo_rdw_gyr * dt * dt;
       cw(12 + r, 12 + r) = c.odo_rdw_acc * dt * dt;
     }
-    xc.cov = add(mul(mul(F, xc.cov), tr(F)), cw);
+    // cov = F cov F^T + cw (imu_ekf.cpp:79) with F's non-zeros only: F is the
+    // identity but for rows 0-2 (F00, -dt I), 3-5 (I, dt I) and 6-8 (F60, I,
+    // F612). Terms are summed in ascending column order, as the dense product
+    // does, and the zero terms it adds are exact no-ops: same bits, 5x fewer
+    // flops on the host's per-scan critical path.
+    SpRow Fr[15];
+    for (int r = 0; r < 3; r++) {
+      Fr[r] = SpRow{4, {0, 1, 2, 9 + r}, {F00(r, 0), F00(r, 1), F00(r, 2), -dt}};
+      Fr[3 + r] = SpRow{2, {3 + r, 6 + r}, {1.0, dt}};
+      Fr[6 + r] = SpRow{7, {0, 1, 2, 6 + r, 12, 13, 14}, {F60(r, 0), F60(r, 1), F60(r, 2), 1.0, F612(r, 0),
+                                                           F612(r, 1), F612(r, 2)}};
+    }
+    for (int r = 9; r < 15; r++) Fr[r] = SpRow{1, {r}, {1.0}};
+    xc.cov = sandwich(Fr, xc.cov, cw);
     pos = add(add(pos, scl(vel, dt)), scl(acc_imu, 0.5 * dt * dt));
     vel = add(vel, scl(acc_imu, dt));
     R_imu = mul(R_imu, Exp_f);
@@ -772,12 +803,11 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   const vg_config& c = ctx->cfg;
   if (init_active(hp(ctx))) return init_step(ctx, dx, dy, dz, di, nullptr, n, beg, end, imu, m);
   VG_TRY(stage_propagate(ctx, imu, m, beg, end));
-  // both read only the raw scan (local_mapping.cpp:396-413). The downsample is
-  // enqueued first: its stream waits only for the previous insert, so it runs
-  // under the previous scan's margi, and the IEKF (queued behind that margi on
-  // the main stream) loses nothing
-  VG_TRY(stage_downsample(ctx, dx, dy, dz, di, n, nullptr));
+  // both read only the raw scan (local_mapping.cpp:396-413); the IEKF opens
+  // the main stream's critical path, the downsample (its count stays on the
+  // device) runs beside it on its own stream
   VG_TRY(stage_iekf(ctx, dx, dy, dz, n, nullptr));
+  VG_TRY(stage_downsample(ctx, dx, dy, dz, di, n, nullptr));
   VG_TRY(stage_window_push(ctx, imu, m));
   if (mid_graph_ok(ctx, hp(ctx))) {
     VG_TRY(stage_insert_recut(ctx));

@@ -81,11 +81,26 @@ def header_symbols():
 _lib = None
 
 
+def _torch_first():
+    """PyTorch-ROCm carries its own HIP runtime beside /opt/rocm's (which the
+    library links). Both share the process's device address space, but the
+    one that opens the GPU second must not be torch's: its init then reports
+    "No HIP GPUs are available". Callers hand torch device buffers to the
+    library, so open torch's runtime first whenever torch is installed."""
+    try:
+        import torch
+    except ImportError:
+        return
+    if torch.cuda.is_available():
+        torch.cuda.init()
+
+
 def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB):
             raise RuntimeError("libvina_gpu.so not built: run `make -C vina-slam_amd` (no CPU fallback exists)")
+        _torch_first()
         L = ctypes.CDLL(LIB)
         P = ctypes.c_void_p
         dp = ctypes.POINTER(ctypes.c_double)
