@@ -41,6 +41,7 @@ struct BaState {             // device-resident LM state
   double u, v, res1, res2, q1;
   int calc_hess, done, iters, seq;  // seq: the next LM publication number (k_ba_control)
   int nhess;                        // Hessian passes executed (I_H, SURVEY 8(d) byte model)
+  int fin;                          // the run has finished (converged or 10 iterations): the margi tail's gate
 };
 static_assert(sizeof(BaState) <= 8 * sizeof(double), "BaState is carved as 8 doubles");
 
@@ -931,6 +932,7 @@ __global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, do
     }
   }
   if (threadIdx.x == 0) {  // LM flags -> host (read without draining the stream)
+    st->fin = (st->done || st->iters >= 10) ? 1 : 0;
     const int seq = st->seq;  // one publication per launch, numbered on the device (graph replays)
     st->seq = seq + 1;
     __hip_atomic_store(&pub->ba_done, st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -961,6 +963,7 @@ __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict
     st->iters = 0;
     st->nhess = 0;
     st->seq = seq0;
+    st->fin = 0;
   }
 }
 
@@ -1091,12 +1094,13 @@ static BaDev carve(vg_ctx* ctx) {
 
 const int* ba_iters_dev(vg_ctx* ctx) { return &carve(ctx).st->iters; }
 const int* ba_hess_dev(vg_ctx* ctx) { return &carve(ctx).st->nhess; }
+const int* ba_gate_dev(vg_ctx* ctx) { return &carve(ctx).st->fin; }
 
 // Run damping_iter on the device state. imurec: (W-1) x kImuRec host records
 // (pinned staging, uploaded asynchronously). The window states and the IMU
 // bias records are read and written in DState.
-int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
-           const std::function<int()>& before_first_wait) {
+int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::function<int()>& before_first_wait,
+           const std::function<int(bool*)>& spec_tail, bool* tail_ok) {
   const int W = ctx->cfg.win_size;
   if (15 * W > kMaxNB * kTile) {
     ctx->err = "win_size > 11 unsupported by the BA solve (LDS-resident 15W x 15W tile store)";
@@ -1191,18 +1195,29 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
   // host waits first (a round trip, ~15 us) rather than queue an iteration
   // that most likely early-exits (~35 us of dispatches). Results do not depend
   // on it: the device-side flags decide.
+  // The margi tail goes in right behind the iteration count the previous run
+  // converged at (steady state: 2 of 2), gated on the device: if the LM needs
+  // more, that copy runs as no-ops and the caller enqueues it again after the
+  // last iteration. So the tail starts as soon as the LM ends instead of one
+  // host round trip later.
   iteration(0);
-  int enq = 1, done_iters = 0;  // iterations enqueued so far
+  int enq = 1, done_iters = 0, tail_at = 0;  // iterations enqueued so far / ahead of the speculative tail
   for (int k = 0; k < 10; k++) {
     if (enq == k + 1 && enq < 10 && enq < ctx->ba_last_iters) iteration(enq++);  // one ahead
     VG_HIP(hipGetLastError());
     VG_TRY(xerr);
     if (k == 0 && before_first_wait) VG_TRY(before_first_wait());
+    if (spec_tail && !tail_at && enq >= ctx->ba_last_iters) {
+      bool queued = false;
+      VG_TRY(spec_tail(&queued));
+      if (queued) tail_at = enq;
+    }
     VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ba, seq0 + k, "k_ba_control"));
     done_iters = __atomic_load_n(&ctx->h_pub->ba_iters, __ATOMIC_ACQUIRE);
     if (__atomic_load_n(&ctx->h_pub->ba_done, __ATOMIC_ACQUIRE)) break;
     if (enq == k + 1 && enq < 10) iteration(enq++);  // not queued ahead: now
   }
+  if (tail_ok) *tail_ok = tail_at > 0 && done_iters <= tail_at;  // the gate opened for that copy
   *iters = done_iters;
   ctx->ba_last_iters = done_iters > 0 ? done_iters : 2;
   if (solve_ev)  // k_ba_solve of the executed iterations only (the bench's roofline)

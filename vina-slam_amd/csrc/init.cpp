@@ -759,7 +759,7 @@ int init_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   P->ins_slot = -1;
   P->prefix = false;
   P->rc_seq = 0;
-  if (c.if_BA == 1) VG_TRY(stage_ba(ctx, nullptr));
+  if (c.if_BA == 1) VG_TRY(stage_ba(ctx, nullptr, true));
   VG_TRY(stage_margi_slide(ctx));
   return stage_finish(ctx);
 }

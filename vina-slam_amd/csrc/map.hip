@@ -1906,7 +1906,7 @@ static int map_recut_impl(vg_ctx* ctx, const MP& mp, const WinArg& wa, int threa
   WinD* dwin = (WinD*)ctx->ba.xs;
   int* dn = (int*)((char*)ctx->ba.xs + sizeof(WinD));
   int* dslot = dn + 32;
-  VG_TRY(state_make_win(ctx, wa, dwin, dn, dslot));
+  VG_TRY(state_make_win(ctx, wa, dwin, dn, dslot, nullptr));
   int total = 0;
   for (int i = 0; i < wa.win_count; i++) total += wa.nper[i];
   ctx->rc_total = total;
@@ -2090,7 +2090,8 @@ __device__ void plane_update_dev(DevMap& m, int node, const Clu& pcr_add, const 
 __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nleaves, const int* __restrict__ leaves,
                                                     MP mp, WinD* __restrict__ win, DevMap m,
                                                     const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
-                                                    int* __restrict__ plan) {
+                                                    int* __restrict__ plan, const int* __restrict__ gate) {
+  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   const int nl = *nleaves;
   int n_pu = 0, n_full = 0;  // plane_update calls / leaves past max_points (per-scan counters)
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nl; q += gridDim.x * blockDim.x) {
@@ -2186,7 +2187,8 @@ constexpr int kCopyWaves = 4;
 __global__ void __launch_bounds__(64 * kCopyWaves) k_margi_copy(const int* __restrict__ nleaves,
                                                                 const int* __restrict__ plan,
                                                                 const uint64_t* __restrict__ keys,
-                                                                const WinD* __restrict__ win, DevMap m) {
+                                                                const WinD* __restrict__ win, DevMap m, const int* __restrict__ gate) {
+  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   const int lane = threadIdx.x & 63;
   const int nl = *nleaves;
   const int s0 = win->mp[0];
@@ -2229,7 +2231,8 @@ __device__ __forceinline__ void internal_exist(DevMap& m, int node) {
 }
 __global__ void __launch_bounds__(256) k_margi_internal(int L, int thread_num, DevMap m, int* __restrict__ lists,
                                                         const int* __restrict__ rc, int nseg,
-                                                        const uint64_t* __restrict__ segkeys) {
+                                                        const uint64_t* __restrict__ segkeys, const int* __restrict__ gate) {
+  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   if (nseg < 0) nseg = rc[kRcNOld];  // the oldest slot's point count (k_set_jour)
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nseg; j += gridDim.x * blockDim.x) {
     const uint64_t k = segkeys[j];
@@ -2249,7 +2252,8 @@ __global__ void __launch_bounds__(256) k_margi_internal(int L, int thread_num, D
 // finishes the bottom-up isexist pass (its roots are level 0's own nodes);
 // level L also resets the dead marks of level L-2, which nobody reads any more.
 __global__ void __launch_bounds__(256) k_margi_erase_mark(int L, int thread_num, DevMap m, int* __restrict__ lists,
-                                                          const int* __restrict__ rc) {
+                                                          const int* __restrict__ rc, const int* __restrict__ gate) {
+  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   if (g_slide(m) < thread_num) return;
   int* work;
   const int nw = margi_level(L, m, rc, lists, &work);
@@ -2278,7 +2282,8 @@ __global__ void __launch_bounds__(256) k_margi_erase_mark(int L, int thread_num,
 }
 // reset the dead marks of levels L0 .. nlev-1
 __global__ void __launch_bounds__(256) k_clear_mark(int L0, int nlev, int thread_num, DevMap m,
-                                                    int* __restrict__ lists, const int* __restrict__ rc) {
+                                                    int* __restrict__ lists, const int* __restrict__ rc, const int* __restrict__ gate) {
+  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   if (g_slide(m) < thread_num) return;
   for (int L = L0 < 0 ? 0 : L0; L < nlev; L++) {
     int* work;
@@ -2293,7 +2298,8 @@ __global__ void __launch_bounds__(256) k_clear_mark(int L0, int nlev, int thread
 // then (the same workgroup) the x_buf / imu_pre_buf slide of the device state
 // (local_mapping.cpp:536-546) and the end-of-scan counter publication
 __global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m, DState* __restrict__ st, int wc,
-                                                        int nimu, Pub* __restrict__ pub, int seq2) {
+                                                        int nimu, Pub* __restrict__ pub, int seq2, const int* __restrict__ gate) {
+  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   __shared__ int base;
   __shared__ int sc[1024];
   __shared__ int s_w[17];
@@ -2403,7 +2409,7 @@ int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thr
 }
 
 int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, int pub_seq,
-              int pub_seq2) {
+              int pub_seq2, const int* gate) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
@@ -2419,40 +2425,42 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   // scan and is published before the margi kernels run
   WinArg wa2 = wa;
   wa2.seq2 = pub_seq2;
-  VG_TRY(state_make_win(ctx, wa2, dwin, dn, dn + 32));
-  if (pub_seq > 0) VG_TRY(state_publish(ctx, wa.win_count, ba_iters_dev(ctx), pub_seq));
+  VG_TRY(state_make_win(ctx, wa2, dwin, dn, dn + 32, gate));
+  if (pub_seq > 0) VG_TRY(state_publish(ctx, wa.win_count, ba_iters_dev(ctx), pub_seq, gate));
   VG_HIP(hipStreamWaitEvent(s, ctx->ev_prefix_done, 0));  // map_margi_prefix
   // the rest reads every per-scan value from the device (n_oldest: rc, the
   // publication number: the state), so it is captured once and replayed
   const int gl = 64;
   auto body = [&]() -> int {
     k_margi_leaf<<<gl, kBlock, 0, s>>>(m.counters + kCntLeaves, w.list0, mp, dwin, m, ctx->ba.fac_eig,
-                                       ctx->ba.fac_pcr, w.plan);
-    k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, w.k1, dwin, m);
+                                       ctx->ba.fac_pcr, w.plan, gate);
+    k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, w.k1, dwin, m, gate);
     for (int L = nlev - 1; L >= 1; L--)
       k_margi_internal<<<L == nlev - 1 ? 128 : gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc,
-                                                                  L == nlev - 1 ? -1 : 0, w.k1);
-    if (nlev == 1) k_margi_internal<<<128, kBlock, 0, s>>>(-1, 1 << 30, m, w.list1, w.rc, -1, w.k1);
-    for (int L = 0; L < nlev; L++) k_margi_erase_mark<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc);
-    k_clear_mark<<<gl, kBlock, 0, s>>>(nlev - 2, nlev, thread_num, m, w.list1, w.rc);
+                                                                  L == nlev - 1 ? -1 : 0, w.k1, gate);
+    if (nlev == 1) k_margi_internal<<<128, kBlock, 0, s>>>(-1, 1 << 30, m, w.list1, w.rc, -1, w.k1, gate);
+    for (int L = 0; L < nlev; L++)
+      k_margi_erase_mark<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc, gate);
+    k_clear_mark<<<gl, kBlock, 0, s>>>(nlev - 2, nlev, thread_num, m, w.list1, w.rc, gate);
     // slide list compaction, the device-state slide, the counter publication
-    k_slide_compact<<<1, 1024, 0, s>>>(thread_num, m, ctx->st, wa.win_count, mp.W - 1, ctx->d_pub, -1);
+    k_slide_compact<<<1, 1024, 0, s>>>(thread_num, m, ctx->st, wa.win_count, mp.W - 1, ctx->d_pub, -1, gate);
     VG_HIP(hipGetLastError());
     return VG_OK;
   };
   (void)n_oldest;
   if (!ctx->use_graphs || ctx->prof_stages) return body();
-  if (!ctx->g_margi) {
+  hipGraphExec_t& ge = ctx->g_margi[gate ? 1 : 0];
+  if (!ge) {
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     const int r = body();
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(s, &g);
     if (r != VG_OK) return r;
     VG_HIP(e);
-    VG_HIP(hipGraphInstantiate(&ctx->g_margi, g, nullptr, nullptr, 0));
+    VG_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     VG_HIP(hipGraphDestroy(g));
   }
-  VG_HIP(hipGraphLaunch(ctx->g_margi, s));
+  VG_HIP(hipGraphLaunch(ge, s));
   return VG_OK;  // device error flags reach the host with the end-of-scan counters
 }
 

@@ -407,6 +407,7 @@ int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double en
   P->ds_n = -1;
   P->ins_slot = -1;
   P->prefix = false;
+  P->tail_queued = false;
   return VG_OK;
 }
 
@@ -638,8 +639,10 @@ int stage_recut(vg_ctx* ctx, int* nf_out) {
   return VG_OK;
 }
 
+static int margi_enqueue(vg_ctx* ctx, HostPipe* P, const int* gate, int* seq1, int* seq2);
+
 // LI_BA_Optimizer::damping_iter (local_mapping.cpp:492-497) on the device state
-int stage_ba(vg_ctx* ctx, int* iters_out) {
+int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows) {
   HostTimer ht_(ctx, kHostBA);
   HostPipe* P = hp(ctx);
   const int W = ctx->cfg.win_size;
@@ -669,7 +672,17 @@ int stage_ba(vg_ctx* ctx, int* iters_out) {
     P->prefix = true;
     return VG_OK;
   };
-  VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), &iters, prefix));
+  // the margi tail behind the LM (see ba_run): fused step, plain graph path
+  const bool spec_ok = margi_follows && ctx->use_graphs && !ctx->prof_stages && ctx->shard.world == 1;
+  std::function<int(bool*)> spec = [&](bool* queued) -> int {
+    if (rc_status || !P->prefix) return VG_OK;
+    VG_TRY(margi_enqueue(ctx, P, ba_gate_dev(ctx), &P->tail_seq1, &P->tail_seq2));
+    *queued = true;
+    return VG_OK;
+  };
+  bool tail_ok = false;
+  VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), &iters, prefix, spec_ok ? spec : std::function<int(bool*)>(), &tail_ok));
+  P->tail_queued = tail_ok;
   if (rc_status) {  // complete the recut on the host (stream order), then the LM again
     P->rc_seq = 0;
     int nf = 0;
@@ -691,6 +704,20 @@ int stage_ba(vg_ctx* ctx, int* iters_out) {
   return VG_OK;
 }
 
+// the device part of multi_margi (x_curr.R/p <- x_buf.back(), the window
+// view, the state publication, the margi kernels); gate: see ba_run
+static int margi_enqueue(vg_ctx* ctx, HostPipe* P, const int* gate, int* seq1, int* seq2) {
+  const vg_config& c = ctx->cfg;
+  const WinArg wa = make_winarg(P, 1);
+  *seq1 = ++ctx->pub_seq;
+  *seq2 = ++ctx->pub_seq;
+  if (!P->prefix) {
+    VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], c.thread_num, P->jour));
+    P->prefix = true;
+  }
+  return map_margi(ctx, P->mpd, wa, P->wp_n[P->mp[0]], c.thread_num, *seq1, *seq2, gate);
+}
+
 // x_curr.R/p <- x_buf.back(), multi_margi, jour, mp[] rotation and buffer slide
 // (local_mapping.cpp:499-546)
 int stage_margi_slide(vg_ctx* ctx) {
@@ -704,13 +731,17 @@ int stage_margi_slide(vg_ctx* ctx) {
   }
   VG_TRY(need_open(ctx, P, "vg_multi_margi"));
   VG_TRY(flush_deferred(ctx, P));
-  const WinArg wa = make_winarg(P, 1);
-  const int seq1 = ++ctx->pub_seq, seq2 = ++ctx->pub_seq;
-  prof_begin(ctx, kProfMargi);
-  if (!P->prefix) VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], c.thread_num, P->jour));
+  int seq1, seq2;
+  if (P->tail_queued) {  // already on the stream behind the LM (stage_ba)
+    seq1 = P->tail_seq1;
+    seq2 = P->tail_seq2;
+  } else {
+    prof_begin(ctx, kProfMargi);
+    VG_TRY(margi_enqueue(ctx, P, nullptr, &seq1, &seq2));
+    prof_end(ctx, kProfMargi);
+  }
   P->prefix = false;
-  VG_TRY(map_margi(ctx, P->mpd, wa, P->wp_n[P->mp[0]], c.thread_num, seq1, seq2));
-  prof_end(ctx, kProfMargi);
+  P->tail_queued = false;
   P->cur.seq1 = seq1;
   P->cur.seq2 = seq2;
   P->cur.shift = 1;
@@ -791,7 +822,7 @@ int host_step_deskew(vg_ctx* ctx, const float* dx, const float* dy, const float*
     VG_TRY(stage_recut(ctx, nullptr));
   }
   if (hp(ctx)->win_count >= c.win_size) {
-    if (c.if_BA == 1) VG_TRY(stage_ba(ctx, nullptr));
+    if (c.if_BA == 1) VG_TRY(stage_ba(ctx, nullptr, true));
     VG_TRY(stage_margi_slide(ctx));
   }
   return stage_finish(ctx);
@@ -816,7 +847,7 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
     VG_TRY(stage_recut(ctx, nullptr));
   }
   if (hp(ctx)->win_count >= c.win_size) {
-    if (c.if_BA == 1) VG_TRY(stage_ba(ctx, nullptr));
+    if (c.if_BA == 1) VG_TRY(stage_ba(ctx, nullptr, true));
     VG_TRY(stage_margi_slide(ctx));
   }
   return stage_finish(ctx);

@@ -85,7 +85,8 @@ __global__ void k_push_state(DState* __restrict__ st, PushArg pa) { push_state_b
 
 // window view for the map kernels: poses by ord, ring, per-ord counts / slots
 __global__ void k_make_win(DState* __restrict__ st, WinArg wa, const int* __restrict__ wpn, WinD* __restrict__ win,
-                           int* __restrict__ nper, int* __restrict__ slot_of) {
+                           int* __restrict__ nper, int* __restrict__ slot_of, const int* __restrict__ gate) {
+  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   const int t = threadIdx.x;
   const int wc = wa.win_count;
   if (wa.set_xc && wc > 0) {
@@ -142,7 +143,8 @@ __global__ void k_slide_state(DState* __restrict__ st, int win_count, int nimu) 
 // P1: x_curr, the post-IEKF pose, window states, IEKF / BA summary
 __global__ void k_publish_state(const DState* __restrict__ st, int win_count, int ba_iters_valid,
                                 const int* __restrict__ ba_iters, const int* __restrict__ ba_hess,
-                                Pub* __restrict__ pub, int seq) {
+                                Pub* __restrict__ pub, int seq, const int* __restrict__ gate) {
+  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   const int t = threadIdx.x;
   for (int e = t; e < kXC; e += blockDim.x) pub_store(&pub->xc[e], st->xc[e]);
   for (int e = t; e < 12; e += blockDim.x) pub_store(&pub->traj[e], st->traj[e]);
@@ -355,8 +357,8 @@ int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec) {
   return VG_OK;
 }
 
-int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot) {
-  k_make_win<<<1, 256, 0, ctx->stream>>>(ctx->st, wa, ctx->map.wpn, dwin, dnper, dslot);
+int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot, const int* gate) {
+  k_make_win<<<1, 256, 0, ctx->stream>>>(ctx->st, wa, ctx->map.wpn, dwin, dnper, dslot, gate);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }
@@ -371,9 +373,9 @@ int state_slide(vg_ctx* ctx, int win_count, int nimu) {
   return VG_OK;
 }
 
-int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq) {
+int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq, const int* gate) {
   k_publish_state<<<1, 256, 0, ctx->stream>>>(ctx->st, win_count, ba_iters_dev != nullptr, ba_iters_dev,
-                                              ba_iters_dev ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, seq);
+                                              ba_iters_dev ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, seq, gate);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }

@@ -166,6 +166,8 @@ struct HostPipe {
   int ins_slot = -1, ins_n = 0;
   bool published = false;
   bool prefix = false;     // map_margi_prefix enqueued for this scan
+  bool tail_queued = false;  // the margi tail went in behind the LM and its gate opened (ba_run)
+  int tail_seq1 = 0, tail_seq2 = 0;  // that tail's publication numbers
   int rc_seq = 0;          // > 0: this scan's recut ran asynchronously (status with Pub::seq_rc == rc_seq)
   std::deque<Pend> pend;   // enqueued scans awaiting absorption (oldest first)
   int sticky = VG_OK;      // deferred device error

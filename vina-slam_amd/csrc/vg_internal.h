@@ -293,7 +293,7 @@ struct vg_ctx {
   hipEvent_t ev_scan_ready = nullptr;  // deskew done (row f1)
   // the IEKF's 8 launches captured once and replayed (map.hip iekf_run)
   hipGraphExec_t g_iekf[3] = {nullptr, nullptr, nullptr};
-  hipGraphExec_t g_margi = nullptr;  // margi after the window view (map.hip map_margi)
+  hipGraphExec_t g_margi[2] = {};  // margi after the window view (map.hip map_margi): ungated, gated
   hipGraphExec_t g_ba = nullptr;     // one LM iteration (ba.hip ba_run)
   // steady state: the insert + recut of one scan, per ring position mp[0] (pipeline.cpp stage_insert_recut)
   hipGraphExec_t g_mid[vg::kMaxWin] = {};
@@ -512,7 +512,8 @@ const int* map_rc_status(vg_ctx* ctx);  // the asynchronous recut's status word 
 // multi_margi + the device-state slide; publishes the state (pub_seq, before
 // the margi kernels) and the end-of-scan counters (pub_seq2)
 int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, double jour);
-int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, int pub_seq, int pub_seq2);
+int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, int pub_seq, int pub_seq2,
+              const int* gate);
 // state.hip
 int state_alloc(vg_ctx* ctx);
 // x_curr / x_prop / IEKF flags; with x != nullptr also the scan the IEKF reads
@@ -520,9 +521,9 @@ int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x = nullptr,
                      const float* z = nullptr, int n = 0);
 int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n);
 int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec);  // imurec: kBaImuRec doubles (new_imu >= 0)
-int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot);
+int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot, const int* gate);
 int state_slide(vg_ctx* ctx, int win_count, int nimu);
-int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq);
+int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq, const int* gate = nullptr);
 int state_publish_counters(vg_ctx* ctx, int seq);
 int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq, int* flags, bool reset);
 int state_deskew(vg_ctx* ctx, const double* par, int npose, const float* x, const float* y, const float* z,
@@ -540,9 +541,15 @@ int ba_alloc(vg_ctx* ctx);
 // LM on the device state (window states, IMU_PRE records and bias records in
 // DState; the factor count in the map counters). Returns once the LM has
 // converged on the device (the flags are read without draining the stream).
+// before_first_wait: enqueued once the first iterations are; spec_tail (may
+// decline through its flag): the margi tail, enqueued right behind the
+// iteration count the previous run converged at and gated on the device by
+// ba_gate_dev; *tail_ok tells whether that copy is the one that runs
 int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
-           const std::function<int()>& before_first_wait = nullptr);
+           const std::function<int()>& before_first_wait = nullptr,
+           const std::function<int(bool*)>& spec_tail = nullptr, bool* tail_ok = nullptr);
 const int* ba_iters_dev(vg_ctx* ctx);
+const int* ba_gate_dev(vg_ctx* ctx);  // 1 once the LM run has finished (converged or 10 iterations)
 const int* ba_hess_dev(vg_ctx* ctx);  // Hessian passes of the last LM run (I_H of SURVEY 8(d))
 // LiDAR factor passes for a host-driven LM (initialisation): Hessian pass at
 // `poses` (lower 6W x 6W, gradient, residual into out) or residual pass at
@@ -580,7 +587,7 @@ int stage_iekf(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, i
 int stage_window_push(vg_ctx* ctx, const double* imu, int m);
 int stage_insert(vg_ctx* ctx);
 int stage_recut(vg_ctx* ctx, int* nf_out);
-int stage_ba(vg_ctx* ctx, int* iters_out);
+int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows = false);  // margi_follows: the fused step
 int stage_margi_slide(vg_ctx* ctx);
 int stage_finish(vg_ctx* ctx);
 }  // namespace vg
@@ -611,7 +618,16 @@ static __device__ unsigned long long g_probe[64];
       vg_probe_t = now_;                                  \
     }                                                     \
   } while (0)
+#define VG_PROBE_MARK_T(k, t)                             \
+  do {                                                    \
+    if (threadIdx.x == (t)) {                             \
+      const unsigned long long now_ = wall_clock64();     \
+      atomicAdd(&vg::g_probe[(k)], now_ - vg_probe_t);    \
+      vg_probe_t = now_;                                  \
+    }                                                     \
+  } while (0)
 #else
 #define VG_PROBE_BEGIN() (void)0
 #define VG_PROBE_MARK(k) (void)0
+#define VG_PROBE_MARK_T(k, t) (void)0
 #endif

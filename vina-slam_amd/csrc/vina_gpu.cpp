@@ -158,7 +158,8 @@ int vg_destroy(vg_ctx* ctx) {
       if (ctx->solve_ev[i][j]) (void)hipEventDestroy(ctx->solve_ev[i][j]);
   for (auto& g : ctx->g_iekf)
     if (g) (void)hipGraphExecDestroy(g);
-  if (ctx->g_margi) (void)hipGraphExecDestroy(ctx->g_margi);
+  for (auto& g : ctx->g_margi)
+    if (g) (void)hipGraphExecDestroy(g);
   if (ctx->g_ba) (void)hipGraphExecDestroy(ctx->g_ba);
   for (auto& g : ctx->g_mid)
     if (g) (void)hipGraphExecDestroy(g);
