@@ -27,7 +27,10 @@ TIGHT_M = 1e-9   # per-scan position bound (observed ~1e-14 m)
 ATE_M = 0.01     # north star: ATE within 1 cm of the CPU reference
 
 
-def run_pair(cfgname, lidar, nscan, seq_id=0, max_points=1_100_000):
+def run_pair(cfgname, lidar, nscan, seq_id=0, max_points=1_100_000, resident=False):
+    """resident: the scans go to the device first and the GPU side runs
+    vg_step_dev (no stream drain between scans, as in the bench), so the next
+    scan's IEKF overlaps the previous margi's remainder (map_margi)."""
     p = vgconfig.load(cfgname)
     g = p["General"]
     seq = synth.Sequence(lidar, seq_id, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
@@ -38,17 +41,31 @@ def run_pair(cfgname, lidar, nscan, seq_id=0, max_points=1_100_000):
     orc.seed(s0)
     gpu.seed(s0)
     so, sg = [], []
+    dev = []
+    if resident:
+        import torch
+        for k in range(nscan):
+            xyz, it, b, e = seq.scan(k)
+            dev.append(torch.from_numpy(np.ascontiguousarray(np.concatenate([xyz.T, it[None]], 0).astype(np.float32)))
+                       .to("cuda:0"))
     for k in range(nscan):
         xyz, it, b, e = seq.scan(k)
         imu = seq.imu(k)
         orc.step(xyz, it, b, e, imu)
-        gpu.step(xyz, it, b, e, imu)
+        if resident:
+            t = dev[k]
+            gpu.step_dev(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), xyz.shape[0], b, e, imu)
+        else:
+            gpu.step(xyz, it, b, e, imu)
         so.append(orc.stats())
-        sg.append(gpu.stats())
+        sg.append(gpu.stats() if not resident else None)
+    if resident:  # stats of every scan, read only now (no drain while stepping)
+        sg = gpu.stats_log()
     return seq, orc, gpu, so, sg
 
 
 def check_pair(so, sg, to, tg, wo, wg):
+    assert len(so) == len(sg)
     for k, (a, b) in enumerate(zip(so, sg)):
         for key in COUNTERS:
             assert a[key] == b[key], (k, key, a[key], b[key])
@@ -78,6 +95,17 @@ CASES = [
 @pytest.mark.parametrize("cfgname,lidar,nscan", CASES)
 def test_pipeline_matches_oracle(oracle_lib, cfgname, lidar, nscan):
     seq, orc, gpu, so, sg = run_pair(cfgname, lidar, nscan)
+    check_case(cfgname, lidar, nscan, orc, gpu, so, sg)
+
+
+def test_resident_pipeline_matches_oracle(oracle_lib):
+    """The bench's way of stepping (device-resident scans, vg_step_dev, no
+    drain): the overlapped IEKF / margi path, every counter exact."""
+    seq, orc, gpu, so, sg = run_pair("mid360", "64line", 30, resident=True)
+    check_case("mid360", "64line", 30, orc, gpu, so, sg)
+
+
+def check_case(cfgname, lidar, nscan, orc, gpu, so, sg):
     for k, b in enumerate(sg):
         print(k, {key: b[key] for key in COUNTERS})
     check_pair(so, sg, orc.trajectory(), gpu.trajectory(), orc.window_states(), gpu.window_states())
@@ -120,5 +148,19 @@ def test_gravity_scale_matches_oracle(oracle_lib):
     check_pair(so, sg, orc.trajectory(), tg, orc.window_states(), gpu.window_states())
     gt = np.array([seq.gt_pose(k)[1] for k in range(tg.shape[0])])
     assert np.linalg.norm(tg[:, 10:13] - gt, axis=1).max() < 0.05
+    gpu.close()
+    orc.close()
+
+
+def test_long_sequence_matches_oracle(oracle_lib):
+    """240 scans (24 window lengths) of the 16-line sequence: every counter
+    exact and poses tight at every scan, through the node pool's and the
+    point_fix arena's growth (reported), long after the window first filled."""
+    seq, orc, gpu, so, sg = run_pair("mid360", "16line", 240, seq_id=7, max_points=100_000)
+    check_pair(so, sg, orc.trajectory(), gpu.trajectory(), orc.window_states(), gpu.window_states())
+    for k in range(39, 240, 40):
+        print("scan %d: nodes %d, point_fix %d, slide %d" % (k, sg[k]["nodes_used"], sg[k]["fix_used"],
+                                                          sg[k]["n_slide"]))
+    assert sum(s["fix_full"] for s in sg) > 0
     gpu.close()
     orc.close()

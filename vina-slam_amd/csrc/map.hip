@@ -328,9 +328,9 @@ static int iekf_blocks(vg_ctx* ctx) {
 // one IEKF iteration: the point loop (block partials) and the update; the
 // optional event pair brackets k_iekf alone (vg_profile)
 int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
-                   hipEvent_t ev0, hipEvent_t ev1, int tag) {
+                   hipEvent_t ev0, hipEvent_t ev1, int tag, hipStream_t s) {
   Work& w = ctx->wk;
-  hipStream_t s = ctx->stream;
+  if (!s) s = ctx->stream;
   (void)x;
   (void)y;
   (void)z;
@@ -358,30 +358,31 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
 // node without the per-launch dispatch gap. The per-stage profiling pass
 // (vg_profile bit 1) launches directly, with an event pair around each k_iekf.
 int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank,
-             const double* begin_xc) {
-  if (begin_xc) VG_TRY(state_scan_begin(ctx, begin_xc, x, y, z, n));  // the scan opens here (pipeline.cpp)
-  else VG_TRY(state_set_scan(ctx, x, y, z, n));
+             const double* begin_xc, hipStream_t s) {
+  if (!s) s = ctx->stream;
+  if (begin_xc) VG_TRY(state_scan_begin(ctx, begin_xc, x, y, z, n, s));  // the scan opens here (pipeline.cpp)
+  else VG_TRY(state_set_scan(ctx, x, y, z, n, s));
   const bool graph = ctx->use_graphs && ctx->shard.world <= 1 && !ctx->prof_stages;
   const bool ev = ctx->prof_on && !graph;
   auto enqueue = [&]() -> int {
     for (int it = 0; it < 4; it++)
       VG_TRY(iekf_iteration(ctx, mp, x, y, z, n, it, ev ? ctx->iekf_ev[bank + it][0] : nullptr,
                             ev ? ctx->iekf_ev[bank + it][1] : nullptr,
-                            graph || !ctx->prof_stages ? 0 : ++ctx->plane_tag));
+                            graph || !ctx->prof_stages ? 0 : ++ctx->plane_tag, s));
     return VG_OK;
   };
   if (!graph) return enqueue();
   if (!ctx->g_iekf[0]) {
-    VG_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     const int r = enqueue();
     hipGraph_t g = nullptr;
-    const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+    const hipError_t e = hipStreamEndCapture(s, &g);
     if (r != VG_OK) return r;
     VG_HIP(e);
     VG_HIP(hipGraphInstantiate(&ctx->g_iekf[0], g, nullptr, nullptr, 0));
     VG_HIP(hipGraphDestroy(g));
   }
-  VG_HIP(hipGraphLaunch(ctx->g_iekf[0], ctx->stream));
+  VG_HIP(hipGraphLaunch(ctx->g_iekf[0], s));
   return VG_OK;
 }
 
@@ -2431,9 +2432,15 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   // the rest reads every per-scan value from the device (n_oldest: rc, the
   // publication number: the state), so it is captured once and replayed
   const int gl = 64;
+  // k_margi_leaf's plane updates are the last margi work the next scan's
+  // IEKF reads: ev_tail_a marks them, and the remainder (point_fix copies,
+  // isexist / erase marks, slide compaction, the device-state slide, the
+  // counter publication; nothing the IEKF reads) runs under the next IEKF
+  k_margi_leaf<<<gl, kBlock, 0, s>>>(m.counters + kCntLeaves, w.list0, mp, dwin, m, ctx->ba.fac_eig,
+                                     ctx->ba.fac_pcr, w.plan, gate);
+  VG_HIP(hipEventRecord(ctx->ev_tail_a, s));
+  ctx->tail_a_valid = true;
   auto body = [&]() -> int {
-    k_margi_leaf<<<gl, kBlock, 0, s>>>(m.counters + kCntLeaves, w.list0, mp, dwin, m, ctx->ba.fac_eig,
-                                       ctx->ba.fac_pcr, w.plan, gate);
     k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, w.k1, dwin, m, gate);
     for (int L = nlev - 1; L >= 1; L--)
       k_margi_internal<<<L == nlev - 1 ? 128 : gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc,

@@ -12,10 +12,13 @@
 // iteration ahead. The state the next scan's propagation needs is published to
 // host-mapped memory right after the BA, while the GPU still runs the margi;
 // the host mirror (x_curr, x_buf, trajectory, stats) absorbs it lazily.
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <vector>
+
 #include "vg_host.h"
 
 namespace vg {
@@ -342,7 +345,17 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   VG_TRY(flush_deferred_push(ctx, P));
   const bool begin = P->begin_pending;
   P->begin_pending = false;
-  return iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, begin ? P->begin_xc : nullptr);
+  // behind the previous margi's plane updates only (map_margi): its
+  // remainder on the main stream runs under this IEKF, and the main stream
+  // then waits for the IEKF. The opening (k_scan_begin) goes with it.
+  const bool split = ctx->tail_a_valid && ctx->use_graphs && !ctx->prof_stages && ctx->shard.world == 1;
+  ctx->tail_a_valid = false;
+  if (!split) return iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, begin ? P->begin_xc : nullptr);
+  VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->ev_tail_a, 0));
+  VG_TRY(iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, begin ? P->begin_xc : nullptr, ctx->stream_iekf));
+  VG_HIP(hipEventRecord(ctx->ev_iekf_done, ctx->stream_iekf));
+  VG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_iekf_done, 0));
+  return VG_OK;
 }
 
 static WinArg make_winarg(const HostPipe* P, int set_xc) {
@@ -800,6 +813,7 @@ int stage_deskew(vg_ctx* ctx, const float* x, const float* y, const float* z, co
   for (int i = 0; i < 3; i++) par[21 + i] = ctx->cfg.ext_t[i];
   if (!P->poses.empty()) memcpy(par.data() + 24, P->poses.data(), P->poses.size() * sizeof(double));
   VG_TRY(state_deskew(ctx, par.data(), npose, x, y, z, in, t, n));
+  ctx->tail_a_valid = false;  // the IEKF reads the deskewed scan: behind the whole main stream
   VG_HIP(hipEventRecord(ctx->ev_scan_ready, ctx->stream));  // the downsample stream reads the result
   return VG_OK;
 }
@@ -828,18 +842,37 @@ int host_step_deskew(vg_ctx* ctx, const float* dx, const float* dy, const float*
   return stage_finish(ctx);
 }
 
+// slack probe (scripts/slack_probe.sh): VG_HOST_DELAY="point,us" busy-waits
+// the host at one point of the step; ms/scan rises by the delay only where the
+// host is on the critical path (0: before the IEKF, 1: before the LM, 2: after
+// the LM wait, 3: before the insert)
+static void host_delay(int point) {
+  static int p = -2, us = 0;
+  if (p == -2) {
+    const char* e = getenv("VG_HOST_DELAY");
+    p = -1;
+    if (e && sscanf(e, "%d,%d", &p, &us) != 2) p = -1;
+  }
+  if (p != point) return;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() < us) {
+  }
+}
+
 // one scan of thd_odometry_localmapping's steady-state branch
 int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n, double beg,
               double end, const double* imu, int m) {
   const vg_config& c = ctx->cfg;
   if (init_active(hp(ctx))) return init_step(ctx, dx, dy, dz, di, nullptr, n, beg, end, imu, m);
   VG_TRY(stage_propagate(ctx, imu, m, beg, end));
+  host_delay(0);
   // both read only the raw scan (local_mapping.cpp:396-413); the IEKF opens
   // the main stream's critical path, the downsample (its count stays on the
   // device) runs beside it on its own stream
   VG_TRY(stage_iekf(ctx, dx, dy, dz, n, nullptr));
   VG_TRY(stage_downsample(ctx, dx, dy, dz, di, n, nullptr));
   VG_TRY(stage_window_push(ctx, imu, m));
+  host_delay(3);
   if (mid_graph_ok(ctx, hp(ctx))) {
     VG_TRY(stage_insert_recut(ctx));
   } else {
@@ -847,7 +880,9 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
     VG_TRY(stage_recut(ctx, nullptr));
   }
   if (hp(ctx)->win_count >= c.win_size) {
+    host_delay(1);
     if (c.if_BA == 1) VG_TRY(stage_ba(ctx, nullptr, true));
+    host_delay(2);
     VG_TRY(stage_margi_slide(ctx));
   }
   return stage_finish(ctx);

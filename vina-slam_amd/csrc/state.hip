@@ -332,16 +332,17 @@ int state_alloc(vg_ctx* ctx) {
   return VG_OK;
 }
 
-int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x, const float* y, const float* z, int n) {
+int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x, const float* y, const float* z, int n,
+                     hipStream_t s) {
   XcArg a;
   memcpy(a.x, xc249, sizeof(a.x));
-  k_scan_begin<<<1, 256, 0, ctx->stream>>>(a, ctx->st, x, y, z, n, x != nullptr ? 1 : 0);
+  k_scan_begin<<<1, 256, 0, s ? s : ctx->stream>>>(a, ctx->st, x, y, z, n, x != nullptr ? 1 : 0);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }
 
-int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n) {
-  k_set_scan<<<1, 64, 0, ctx->stream>>>(ctx->st, x, y, z, n);
+int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n, hipStream_t s) {
+  k_set_scan<<<1, 64, 0, s ? s : ctx->stream>>>(ctx->st, x, y, z, n);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }

@@ -290,6 +290,13 @@ struct vg_ctx {
   hipStream_t stream_ds = nullptr;
   hipEvent_t ev_ds_done = nullptr, ev_ds_free = nullptr;
   hipEvent_t ev_recut_done = nullptr, ev_prefix_done = nullptr;  // margi prefix on the second stream
+  // The next scan's IEKF overlaps the margi's map-only remainder: it runs on
+  // stream_iekf behind ev_tail_a (recorded after k_margi_leaf's plane updates,
+  // the last margi work the IEKF reads), and the main stream waits for it
+  // (ev_iekf_done) before anything else (map_margi, pipeline.cpp lio_state_estimation)
+  hipStream_t stream_iekf = nullptr;
+  hipEvent_t ev_tail_a = nullptr, ev_iekf_done = nullptr;
+  bool tail_a_valid = false;  // ev_tail_a marks the latest main-stream work the next IEKF depends on
   hipEvent_t ev_scan_ready = nullptr;  // deskew done (row f1)
   // the IEKF's 8 launches captured once and replayed (map.hip iekf_run)
   hipGraphExec_t g_iekf[3] = {nullptr, nullptr, nullptr};
@@ -484,12 +491,12 @@ int ds_enqueue(vg_ctx* ctx, hipStream_t s, const float* x, const float* y, const
 int map_alloc(vg_ctx* ctx);
 int map_reset(vg_ctx* ctx);
 int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
-                   hipEvent_t ev0, hipEvent_t ev1, int tag = 0);
+                   hipEvent_t ev0, hipEvent_t ev1, int tag = 0, hipStream_t s = nullptr);
 // all four iterations; replays the captured graph when possible
 // begin_xc != nullptr: open the scan on the device first (x_curr after
 // propagation, one launch with the scan binding)
 int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank,
-             const double* begin_xc = nullptr);
+             const double* begin_xc = nullptr, hipStream_t s = nullptr);
 constexpr int kNeedInsertReplay = 1;  // map_recut: the insert overflowed k_ins_alloc, replay it first
 // the initialisation's insert source (cut_voxel, initialization.cpp:229-246):
 // n fp64 body points, the kXC pose/covariance block of x_buf[i], both device
@@ -518,8 +525,8 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
 int state_alloc(vg_ctx* ctx);
 // x_curr / x_prop / IEKF flags; with x != nullptr also the scan the IEKF reads
 int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x = nullptr, const float* y = nullptr,
-                     const float* z = nullptr, int n = 0);
-int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n);
+                     const float* z = nullptr, int n = 0, hipStream_t s = nullptr);
+int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n, hipStream_t s = nullptr);
 int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec);  // imurec: kBaImuRec doubles (new_imu >= 0)
 int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot, const int* gate);
 int state_slide(vg_ctx* ctx, int win_count, int nimu);

@@ -46,7 +46,10 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
       (e = hipEventCreateWithFlags(&ctx->ev_ds_free, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&ctx->ev_recut_done, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&ctx->ev_prefix_done, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&ctx->ev_scan_ready, hipEventDisableTiming)) != hipSuccess) {
+      (e = hipEventCreateWithFlags(&ctx->ev_scan_ready, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&ctx->stream_iekf, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_tail_a, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_iekf_done, hipEventDisableTiming)) != hipSuccess) {
     ctx->err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
@@ -172,6 +175,10 @@ int vg_destroy(vg_ctx* ctx) {
   if (ctx->ev_recut_done) (void)hipEventDestroy(ctx->ev_recut_done);
   if (ctx->ev_prefix_done) (void)hipEventDestroy(ctx->ev_prefix_done);
   if (ctx->ev_scan_ready) (void)hipEventDestroy(ctx->ev_scan_ready);
+  if (ctx->stream_iekf) (void)hipStreamSynchronize(ctx->stream_iekf);
+  if (ctx->stream_iekf) (void)hipStreamDestroy(ctx->stream_iekf);
+  if (ctx->ev_tail_a) (void)hipEventDestroy(ctx->ev_tail_a);
+  if (ctx->ev_iekf_done) (void)hipEventDestroy(ctx->ev_iekf_done);
   delete ctx;
   return VG_OK;
 }
