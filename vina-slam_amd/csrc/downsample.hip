@@ -231,7 +231,7 @@ __device__ __forceinline__ uint32_t hds_hash(uint64_t k, int mask) {
   return (uint32_t)k & (uint32_t)mask;
 }
 constexpr int kHdsTile = 1024;  // points per tile (256 lanes x 4)
-constexpr int kHdsSmall = 32;   // a lane sorts a voxel's segment itself up to this many points
+constexpr int kHdsSmall = 16;   // a lane sorts a voxel's segment itself (in registers) up to this many points
 constexpr int kHdsEmptyFirst = 0x7f7f7f7f;  // above every point index (ds_reset's memset byte)
 
 __global__ void __launch_bounds__(256) k_hds_insert(int n, const float* __restrict__ x, const float* __restrict__ y,
@@ -376,6 +376,53 @@ __global__ void __launch_bounds__(256) k_hds_scatter(int n, DownsampleBufs d, co
   }
 }
 
+// A voxel's segment (N >= cnt point indices, padded with ~0u) back to input
+// order in registers — a static Batcher odd-even merge network, no memory
+// traffic — then the reference's float recurrence over the points in that
+// order (point_utils.hpp:34-37, evaluated exactly as written, no contraction).
+template <int N>
+__device__ __forceinline__ void hds_sorted_mean(const uint32_t* __restrict__ sg, int cnt, const float* __restrict__ x,
+                                                const float* __restrict__ y, const float* __restrict__ z,
+                                                float& px, float& py, float& pz, float& c) {
+  uint32_t u[N];
+#pragma unroll
+  for (int a = 0; a < N; a++) u[a] = a < cnt ? sg[a] : ~0u;
+#pragma unroll
+  for (int p = 1; p < N; p <<= 1)
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1)
+#pragma unroll
+      for (int j = k % p; j + k < N; j += 2 * k)
+#pragma unroll
+        for (int i = 0; i < k; i++)
+          if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+            const uint32_t lo = u[i + j] < u[i + j + k] ? u[i + j] : u[i + j + k];
+            const uint32_t hi = u[i + j] < u[i + j + k] ? u[i + j + k] : u[i + j];
+            u[i + j] = lo;
+            u[i + j + k] = hi;
+          }
+  float vx[N], vy[N], vz[N];  // the loads are independent of the recurrence: issue them all first
+#pragma unroll
+  for (int a = 0; a < N; a++)
+    if (a < cnt) {
+      vx[a] = x[u[a]];
+      vy[a] = y[u[a]];
+      vz[a] = z[u[a]];
+    }
+  px = vx[0];
+  py = vy[0];
+  pz = vz[0];
+  c = 1.0f;
+#pragma unroll
+  for (int a = 1; a < N; a++)
+    if (a < cnt) {
+      px = (px * c + vx[a]) / (c + 1);
+      py = (py * c + vy[a]) / (c + 1);
+      pz = (pz * c + vz[a]) / (c + 1);
+      c += 1;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_hds_mean(DownsampleBufs d, const float* __restrict__ x,
                                                   const float* __restrict__ y, const float* __restrict__ z,
                                                   const float* __restrict__ in, const int* __restrict__ need) {
@@ -389,25 +436,12 @@ __global__ void __launch_bounds__(256) k_hds_mean(DownsampleBufs d, const float*
       d.bigv[atomicAdd(&d.hflags[3], 1)] = v;
       continue;
     }
-    uint32_t* sg = d.pseg + b;
-    for (int a = 1; a < cnt; a++) {  // back to input order (short segments)
-      const uint32_t key = sg[a];
-      int q = a - 1;
-      while (q >= 0 && sg[q] > key) {
-        sg[q + 1] = sg[q];
-        q--;
-      }
-      sg[q + 1] = key;
-    }
-    float px = x[i], py = y[i], pz = z[i], c = 1.0f;
-    for (int a = 1; a < cnt; a++) {
-      const uint32_t j = sg[a];
-      // point_utils.hpp:34-37, evaluated exactly as written (no contraction)
-      px = (px * c + x[j]) / (c + 1);
-      py = (py * c + y[j]) / (c + 1);
-      pz = (pz * c + z[j]) / (c + 1);
-      c += 1;
-    }
+    const uint32_t* sg = d.pseg + b;
+    float px, py, pz, c;
+    if (cnt <= 2) hds_sorted_mean<2>(sg, cnt, x, y, z, px, py, pz, c);
+    else if (cnt <= 4) hds_sorted_mean<4>(sg, cnt, x, y, z, px, py, pz, c);
+    else if (cnt <= 8) hds_sorted_mean<8>(sg, cnt, x, y, z, px, py, pz, c);
+    else hds_sorted_mean<kHdsSmall>(sg, cnt, x, y, z, px, py, pz, c);
     d.ox[v] = px;
     d.oy[v] = py;
     d.oz[v] = pz;
