@@ -51,6 +51,9 @@ def main():
                                  max_fix_points=3_000_000, hash_log2=20) for _ in range(B)]
             for c in ctxs:
                 c.seed(seq.gt_state(0))
+                for key, env in ((7, "MP_OVERLAP"), (8, "MP_SPEC")):  # vgx_debug knobs, 0 = off
+                    if os.environ.get(env) is not None:
+                        vgpu.lib().vgx_debug(c.h, key, int(os.environ[env]))
             mv = vgpu.Multi(ctxs, spin, sleep)
 
             def step(k):
@@ -69,7 +72,9 @@ def main():
             same = all(np.array_equal(trajs[0], tr) for tr in trajs[1:])
             print(json.dumps({"lidar": lidar, "B": B, "spin_us": spin, "sleep_us": sleep,
                               "scans_per_s": round(B * steps / dt, 1), "ms_per_round": round(dt * 1e3 / steps, 3),
-                              "identical": same, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}), flush=True)
+                              "identical": same, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                              "overlap": os.environ.get("MP_OVERLAP", "1"), "spec": os.environ.get("MP_SPEC", "1")}),
+                  flush=True)
             mv.close()
             for c in ctxs:
                 c.close()

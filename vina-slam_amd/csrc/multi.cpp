@@ -79,7 +79,10 @@ vg_multi* vg_multi_create(vg_ctx** ctxs, int B, int spin_us, int sleep_us) {
   vg_multi* M = new vg_multi();
   M->ctx.assign(ctxs, ctxs + B);
   M->wk.resize(B);
-  for (int b = 0; b < B; b++) vg_set_wait_policy(ctxs[b], spin_us, sleep_us);
+  for (int b = 0; b < B; b++) {
+    vg_set_wait_policy(ctxs[b], spin_us, sleep_us);
+    if (B > 1) ctxs[b]->overlap_iekf = false;  // two streams per sequence (pipeline.cpp lio_state_estimation)
+  }
   for (int b = 0; b < B; b++) M->th.emplace_back(worker, M, b);
   return M;
 }

@@ -348,9 +348,14 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   // behind the previous margi's plane updates only (map_margi): its
   // remainder on the main stream runs under this IEKF, and the main stream
   // then waits for the IEKF. The opening (k_scan_begin) goes with it.
-  const bool split = ctx->tail_a_valid && ctx->use_graphs && !ctx->prof_stages && ctx->shard.world == 1;
+  const bool split = ctx->tail_a_valid && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages &&
+                     ctx->shard.world == 1;
   ctx->tail_a_valid = false;
   if (!split) return iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, begin ? P->begin_xc : nullptr);
+  // created on first use: a context of the multi-sequence mode never makes
+  // it (vg_multi_create), as a third stream per sequence makes sequences
+  // share hardware queues (B = 4: 2,742 -> 1,430 scans/s)
+  if (!ctx->stream_iekf) VG_HIP(hipStreamCreateWithFlags(&ctx->stream_iekf, hipStreamNonBlocking));
   VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->ev_tail_a, 0));
   VG_TRY(iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, begin ? P->begin_xc : nullptr, ctx->stream_iekf));
   VG_HIP(hipEventRecord(ctx->ev_iekf_done, ctx->stream_iekf));
@@ -686,7 +691,8 @@ int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows) {
     return VG_OK;
   };
   // the margi tail behind the LM (see ba_run): fused step, plain graph path
-  const bool spec_ok = margi_follows && ctx->use_graphs && !ctx->prof_stages && ctx->shard.world == 1;
+  const bool spec_ok = margi_follows && ctx->spec_tail && ctx->use_graphs && !ctx->prof_stages &&
+                       ctx->shard.world == 1;
   std::function<int(bool*)> spec = [&](bool* queued) -> int {
     if (rc_status || !P->prefix) return VG_OK;
     VG_TRY(margi_enqueue(ctx, P, ba_gate_dev(ctx), &P->tail_seq1, &P->tail_seq2));

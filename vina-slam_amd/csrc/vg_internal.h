@@ -310,6 +310,8 @@ struct vg_ctx {
   vg::HostIn* h_in = nullptr;  // host-mapped per-scan inputs of replayed graphs (host address)
   vg::HostIn* d_in = nullptr;  // its device address
   bool use_graphs = true;  // margi prefix on the second stream
+  bool overlap_iekf = true;  // the next IEKF under the margi remainder (lio_state_estimation)
+  bool spec_tail = true;     // the margi tail behind the predicted LM iterations (stage_ba)
   std::string err;
   vg::Arena arena;
   // raw scan staging (SoA)

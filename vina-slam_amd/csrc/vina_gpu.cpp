@@ -47,7 +47,6 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
       (e = hipEventCreateWithFlags(&ctx->ev_recut_done, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&ctx->ev_prefix_done, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&ctx->ev_scan_ready, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipStreamCreateWithFlags(&ctx->stream_iekf, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&ctx->ev_tail_a, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&ctx->ev_iekf_done, hipEventDisableTiming)) != hipSuccess) {
     ctx->err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
@@ -168,8 +167,8 @@ int vg_destroy(vg_ctx* ctx) {
     if (g) (void)hipGraphExecDestroy(g);
   if (ctx->h_in) (void)hipHostFree(ctx->h_in);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-  if (ctx->stream_ds) (void)hipStreamSynchronize(ctx->stream_ds);
-  if (ctx->stream_ds) (void)hipStreamDestroy(ctx->stream_ds);
+  if (ctx->stream_ds && ctx->stream_ds != ctx->stream) (void)hipStreamSynchronize(ctx->stream_ds);
+  if (ctx->stream_ds && ctx->stream_ds != ctx->stream) (void)hipStreamDestroy(ctx->stream_ds);
   if (ctx->ev_ds_done) (void)hipEventDestroy(ctx->ev_ds_done);
   if (ctx->ev_ds_free) (void)hipEventDestroy(ctx->ev_ds_free);
   if (ctx->ev_recut_done) (void)hipEventDestroy(ctx->ev_recut_done);
@@ -514,6 +513,14 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
   }
   if (key == 4) {
     ctx->dbg_fac_max = value;
+    return VG_OK;
+  }
+  if (key == 7) {  // 0: the IEKF waits for the whole margi (no cross-scan overlap)
+    ctx->overlap_iekf = value != 0;
+    return VG_OK;
+  }
+  if (key == 8) {  // 0: the margi tail is enqueued only after the LM is seen done
+    ctx->spec_tail = value != 0;
     return VG_OK;
   }
   if (key == 5) {  // arm: the next LM run copies its first Hessian pass (LiDAR hl + IMU blocks)
