@@ -889,7 +889,8 @@ __global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __re
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      for (int k = 0; k < nb; k++) acc += role_inc(E[wv][k], ri);
+#pragma unroll 8
+      for (int k = 0; k < nb; k++) acc += role_inc(E[wv][k], ri);  // unrolled: the LDS reads run ahead of the sum
       __builtin_amdgcn_wave_barrier();
     }
     if (acc_p) *acc_p = acc;
@@ -1615,6 +1616,7 @@ __global__ void __launch_bounds__(64 * kRcPushWaves) k_rc_push(int L, const uint
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 4
       for (int k = 0; k < nb; k++) {
         const int slot = s_slot[wv][k];
         const bool isfix = slot < 0;
