@@ -74,6 +74,10 @@ def iekf(nscan=40, lidar="64line"):
         print("  %-16s %8.2f us/call" % (name, buf[k] * 0.01 / n))
     for k, name in {28: "cov update", 29: "eig3/final"}.items():
         print("  %-16s %8.2f us/final" % (name, buf[k] * 0.01 / nf))
+    ni = max(buf[59], 1)
+    print("k_iekf block 0, thread 0:", buf[59], "launches")
+    for k, name in {30: "point loop", 31: "block reduction"}.items():
+        print("  %-16s %8.2f us/launch" % (name, buf[k] * 0.01 / ni))
 
 
 if __name__ == "__main__":

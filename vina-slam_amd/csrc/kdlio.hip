@@ -180,11 +180,12 @@ __global__ void __launch_bounds__(kKdBlock) k_kd_pass(int n, const float* __rest
   __shared__ double red[kKdSums][kKdBlock / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < kKdSums; k++) {
-    double v = acc[k];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    if (lane == 0) red[k][wv] = v;
-  }
+  for (int off = 32; off > 0; off >>= 1)  // every sum's level at once (independent exchanges overlap)
+#pragma unroll
+    for (int k = 0; k < kKdSums; k++) acc[k] += __shfl_down(acc[k], off, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < kKdSums; k++) red[k][wv] = acc[k];
   __syncthreads();
   if ((int)threadIdx.x < kKdSums) {
     double v = 0.0;

@@ -201,6 +201,7 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
                                               int* __restrict__ cache, double* __restrict__ partials,
                                               int* __restrict__ pk) {
   if (st->done) return;
+  VG_PROBE_BEGIN();
   const int n = st->sn;
   const float* __restrict__ x = st->sx;
   const float* __restrict__ y = st->sy;
@@ -229,26 +230,47 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
     var_init_pt(mp, x[i], y[i], z[i], pnt, var);
     M3 var_world = world_var(R, var, pnt, rot_var, tsl_var);
     V3 wld = rigid(R, pnt, p);
-    int leaf = it > 0 ? cache[i] : -1;
+    // cache[i]: the leaf of the point's last match (the reference's octos[i],
+    // odometry.cpp:124-131, reset per scan) or, after a failed match, the
+    // leaf the descent reached — a memo only (bit 30 tags it): while the
+    // point stays inside that leaf's box and its float voxel key still names
+    // the leaf's root (the lookup rounds in float, voxel_map.cpp:246-253), the
+    // lookup would reach the same leaf, so unmatched points skip the hash +
+    // descent too
+    const int cv = it > 0 ? cache[i] : -1;
+    int leaf = cv >= 0 ? (cv & 0x3fffffff) : -1;
     int flag = 0;
     double sigma = 0;
-    if (leaf >= 0 && inside(m.hdr[leaf], wld)) {
+    bool hit = leaf >= 0 && inside(m.hdr[leaf], wld);
+    if (hit && (cv & 0x40000000)) {
+      uint64_t kw, kl;
+      const NodeHdr& hl = m.hdr[leaf];
+      hit = pack_key(wld, mp.vs, kw) && pack_key(v3(hl.center[0], hl.center[1], hl.center[2]), mp.vs, kl) && kw == kl;
+    }
+    if (hit) {
       flag = match_leaf(m.hdr[leaf], m.pl[leaf], wld, var_world, sigma);
+      if (!flag && !(cv & 0x40000000)) leaf = -2;  // the reference's octos[i] stays: keep the cache
     } else {
+      leaf = -1;
       uint64_t key;
       if (pack_key(wld, mp.vs, key) && owns(m, key)) {  // another shard's tile: not matched here
         int root = hash_find(m.hkey, m.hval, m.hash_mask, key);
         int lf = root >= 0 ? descend(m.hdr, root, wld) : -1;
         if (lf >= 0) {
           flag = match_leaf(m.hdr[lf], m.pl[lf], wld, var_world, sigma);
-          if (flag) leaf = lf;
+          leaf = lf;
         }
       }
     }
-    if (!flag && it == 0) cache[i] = -1;  // the reference's fresh per-scan association
-    if (pk) pk[i] = flag ? leaf : -1;     // the leaf whose plane this iteration read (profiling pass)
+    if (pk) pk[i] = flag ? leaf : -1;  // the leaf whose plane this iteration read (profiling pass)
     if (flag) {
       cache[i] = leaf;
+    } else if (leaf >= 0) {
+      if (it == 0 || cv < 0 || (cv & 0x40000000)) cache[i] = leaf | 0x40000000;  // no octos[i] to keep
+    } else if (leaf == -1 && (it == 0 || cv < 0 || (cv & 0x40000000))) {
+      cache[i] = -1;
+    }
+    if (flag) {
       const PlaneRec& P = m.pl[leaf];
       V3 nn = ld_v3(P.normal), c = ld_v3(P.center);
       double R_inv = 1.0 / (0.0005 + sigma);
@@ -270,19 +292,28 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
       acc[33] += 1.0;
     }
   }
+  if (blockIdx.x == 0) VG_PROBE_MARK(30);  // the point loop (thread 0 of block 0)
   // block reduction: wave shuffles then LDS across the 4 waves (fixed tree)
   __shared__ double red[4][kIekfVals];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int j = 0; j < kIekfVals; j++) {
-    double v = acc[j];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    if (lane == 0) red[wv][j] = v;
-  }
+  // the same tree per value, but the 34 values step together: each level's
+  // exchanges are independent and overlap (34 chains of 6, not 204 in a row)
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int j = 0; j < kIekfVals; j++) acc[j] += __shfl_down(acc[j], off, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < kIekfVals; j++) red[wv][j] = acc[j];
   __syncthreads();
   if (threadIdx.x < kIekfVals) {
     int j = threadIdx.x;
     partials[(size_t)blockIdx.x * kIekfVals + j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
   }
+  if (blockIdx.x == 0) VG_PROBE_MARK(31);  // the block reduction
+#ifdef VG_PROBE
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_probe[59], 1ull);
+#endif
 }
 
 // P_k of SURVEY 8(d), the profiling pass only: distinct plane records the
