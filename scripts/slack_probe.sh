@@ -5,5 +5,5 @@ mkdir -p gpurun_out
 run() { timeout -k 10 200 python bench.py --no-cpu --stage-scans 0 --target-steps 0 --no-h2d --multi= > gpurun_out/slack.json 2>/dev/null || { echo "bench failed"; exit 1; }; python -c "import json; d=json.load(open('gpurun_out/slack.json')); print('$1', d['ms_per_step'])"; }
 for rep in 1 2; do
   unset VG_HOST_DELAY; run base
-  for pt in 0 3 1 2; do export VG_HOST_DELAY=$pt,40; run "pt$pt+40us"; done
+  for pt in 0 4 3 1 2; do export VG_HOST_DELAY=$pt,40; run "pt$pt+40us"; done
 done

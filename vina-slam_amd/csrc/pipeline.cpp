@@ -851,7 +851,7 @@ int host_step_deskew(vg_ctx* ctx, const float* dx, const float* dy, const float*
 // slack probe (scripts/slack_probe.sh): VG_HOST_DELAY="point,us" busy-waits
 // the host at one point of the step; ms/scan rises by the delay only where the
 // host is on the critical path (0: before the IEKF, 1: before the LM, 2: after
-// the LM wait, 3: before the insert)
+// the LM wait, 3: before the insert, 4: before the downsample)
 static void host_delay(int point) {
   static int p = -2, us = 0;
   if (p == -2) {
@@ -876,6 +876,7 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   // the main stream's critical path, the downsample (its count stays on the
   // device) runs beside it on its own stream
   VG_TRY(stage_iekf(ctx, dx, dy, dz, n, nullptr));
+  host_delay(4);
   VG_TRY(stage_downsample(ctx, dx, dy, dz, di, n, nullptr));
   VG_TRY(stage_window_push(ctx, imu, m));
   host_delay(3);
