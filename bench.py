@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--workers", type=int, default=0,
                     help="scan-generation processes (0: min(16, cpus); 1 under a profiler)")
     ap.add_argument("--no-h2d", action="store_true", help="skip the host-input (vg_step) rate")
+    ap.add_argument("--max-nodes", type=int, default=0, help="context capacity: octree nodes (0: product default)")
+    ap.add_argument("--max-fix", type=int, default=0, help="context capacity: point_fix points (0: default)")
+    ap.add_argument("--hash-log2", type=int, default=0, help="context capacity: root hash slots, log2 (0: default)")
     ap.add_argument("--multi", default="2,4,8",
                     help="multi-sequence mode (vg_multi_*): B values to time at N=1 (empty: skip)")
     return ap.parse_args()
@@ -80,8 +83,12 @@ def gen_scans(lidar, seq_id, general, n, workers):
         return pool.map(_gen, jobs, chunksize=1)
 
 
+CAP = {}  # context capacities (--max-nodes / --max-fix / --hash-log2; 0 = the product's defaults)
+
+
 def main():
     args = parse()
+    CAP.update(max_nodes=args.max_nodes, max_fix_points=args.max_fix, hash_log2=args.hash_log2)
     if args.multi and "GPU_MAX_HW_QUEUES" not in os.environ:
         # the multi-sequence leg runs two streams per sequence: let HIP map them
         # to separate hardware queues (HIP's default is 4; read at HIP start-up)
@@ -127,7 +134,7 @@ def main():
         scans.append((t, xyz.shape[0], b, e))
     imus = [h[4] for h in host_scans]
     npts = int(np.mean([s[1] for s in scans[warmup:total]]))
-    ctx = vgpu.Context(vgconfig.to_c(p), device=local, max_points=max(s[1] for s in scans) + 16)
+    ctx = vgpu.Context(vgconfig.to_c(p), device=local, max_points=max(s[1] for s in scans) + 16, **CAP)
     if tile:  # one RCCL communicator inside the library, id from rank 0
         obj = [vgpu.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
@@ -241,6 +248,7 @@ def main():
             "config": {"workload": "synthetic-%s@%s.yaml" % (args.lidar, args.config), "lidar": args.lidar,
                        "rays_per_scan": int(synth.LIDARS[args.lidar][0] * synth.LIDARS[args.lidar][1]),
                        "points_per_scan": npts, "downsampled_per_scan": int(np.mean([s["n_ds"] for s in stats])),
+                       "nodes_used_end": int(stats[-1]["nodes_used"]), "fix_used_end": int(stats[-1]["fix_used"]),
                        "factors_per_scan": int(np.mean([s["n_factors"] for s in stats])),
                        "lm_iters_per_scan": round(float(np.mean([s["ba_iters"] for s in stats])), 2),
                        "parallelism": ("tile-sharded x%d" if tile else "replica x%d") % world},
@@ -296,7 +304,7 @@ def multi_sequence(p, seq, scans, imus, warmup, total, dev, Bs):
            "wait_policy": "spin", "by_B": {}}
     npmax = max(s[1] for s in scans) + 16
     for B in Bs:
-        ctxs = [vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=npmax) for _ in range(B)]
+        ctxs = [vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=npmax, **CAP) for _ in range(B)]
         for c in ctxs:
             c.seed(seq.gt_state(0))
         mv = vgpu.Multi(ctxs, 0, 0)
@@ -331,7 +339,8 @@ def host_input_rate(p, seq, host_scans, imus, warmup, steps, dev):
     import vgconfig
     import vgpu
     n = min(warmup + steps, len(host_scans))
-    ctx = vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=max(h[0].shape[0] for h in host_scans) + 16)
+    ctx = vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=max(h[0].shape[0] for h in host_scans) + 16,
+                       **CAP)
     ctx.seed(seq.gt_state(0))
     xs = [np.ascontiguousarray(h[0]) for h in host_scans[:n]]
     its = [np.ascontiguousarray(h[1]) for h in host_scans[:n]]
@@ -367,7 +376,7 @@ def target_workload(args, cfg, host, warm, dev):
     for xyz, inten, b, e, _ in host:
         t = torch.from_numpy(np.ascontiguousarray(np.concatenate([xyz.T, inten[None]], 0))).to(dev)
         scans.append((t, xyz.shape[0], b, e))
-    ctx = vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=max(s[1] for s in scans) + 16)
+    ctx = vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=max(s[1] for s in scans) + 16, **CAP)
     ctx.seed(seq.gt_state(0))
 
     def run(k):

@@ -105,6 +105,27 @@ int map_alloc(vg_ctx* ctx) {
 int map_reset(vg_ctx* ctx) {
   DevMap& m = ctx->map;
   hipStream_t s = ctx->stream;
+  // Node records are handed out zeroed: the pool is cleared here (all of it
+  // the first time, afterwards the ids handed out since), so no allocation on
+  // the per-scan path writes a record it has not filled (ids are never reused
+  // between resets)
+  int used = m.cap_nodes;
+  if (ctx->pool_zeroed) {
+    VG_HIP(hipMemcpyAsync(ctx->h_pinned, m.counters, kCntN * sizeof(int), hipMemcpyDeviceToHost, s));
+    VG_HIP(hipStreamSynchronize(s));
+    used = ctx->h_pinned[kCntNodes] < m.cap_nodes ? ctx->h_pinned[kCntNodes] : m.cap_nodes;
+  }
+  if (used > 0) {
+    const size_t u = (size_t)used;
+    VG_HIP(hipMemsetAsync(m.pl, 0, u * sizeof(PlaneRec), s));
+    VG_HIP(hipMemsetAsync(m.pcr_add, 0, u * sizeof(Clu), s));
+    VG_HIP(hipMemsetAsync(m.pcr_fix, 0, u * sizeof(Clu), s));
+    VG_HIP(hipMemsetAsync(m.cov_add, 0, u * kCovN * sizeof(double), s));
+    VG_HIP(hipMemsetAsync(m.eig, 0, u * 12 * sizeof(double), s));
+    VG_HIP(hipMemsetAsync(m.jour, 0, u * sizeof(double), s));
+    VG_HIP(hipMemsetAsync(m.pcrs, 0, u * m.W * sizeof(Clu), s));
+  }
+  ctx->pool_zeroed = true;
   const size_t hs = (size_t)m.hash_mask + 1;
   VG_HIP(hipMemsetAsync(m.hkey, 0xff, hs * sizeof(uint64_t), s));
   VG_HIP(hipMemsetAsync(m.hval, 0xff, hs * sizeof(int), s));
@@ -121,26 +142,6 @@ int map_reset(vg_ctx* ctx) {
   return ds_reset(ctx);  // the pipeline downsample's voxel table
 }
 
-// Node records of freshly allocated nodes must be zero: the pool is zeroed
-// lazily per allocation range.
-__global__ void __launch_bounds__(256) k_zero_nodes(int first, const int* __restrict__ first_ptr,
-                                                   const int* __restrict__ cnt_after, int W, PlaneRec* pl, Clu* pcr_add,
-                                                   Clu* pcr_fix, double* cov, double* eig, double* jour, Clu* pcrs) {
-  if (first_ptr) first = *first_ptr;
-  const int last = cnt_after[0];
-  for (int id = first + blockIdx.x * blockDim.x + threadIdx.x; id < last; id += gridDim.x * blockDim.x) {
-    PlaneRec& p = pl[id];
-    for (int j = 0; j < 27; j++) (&p.center[0])[j] = 0.0;
-    p.radius = 0;
-    p.pad = 0;
-    clu_zero(pcr_add[id]);
-    clu_zero(pcr_fix[id]);
-    for (int j = 0; j < kCovN; j++) cov[(size_t)id * kCovN + j] = 0.0;
-    for (int j = 0; j < 12; j++) eig[(size_t)id * 12 + j] = 0.0;
-    jour[id] = 0.0;
-    for (int j = 0; j < W; j++) clu_zero(pcrs[(size_t)id * W + j]);
-  }
-}
 
 // ------------------------------------------------------------------ IEKF
 // One IEKF iteration's point loop (odometry.cpp:111-148): world covariance,
@@ -522,7 +523,6 @@ __global__ void __launch_bounds__(256) k_ins_newflag(int n, const uint32_t* __re
 // point's rank inside its tile. Ids and slide positions then follow point
 // index order: deterministic.
 constexpr int kRootTile = 1024;  // points per workgroup (256 threads x 4)
-__device__ __forceinline__ void zero_node(DevMap& m, int id);
 __device__ __forceinline__ int ins_root_code(const DevMap& m, const uint32_t* __restrict__ hslot, int i, int n) {
   // bit 0: first point of its root, bit 1: new root, bit 2: joins the slide map
   if (i >= n) return 0;
@@ -634,8 +634,7 @@ __global__ void __launch_bounds__(256) k_ins_roots_alloc(int n_arg, const int* _
       double c[3];
       const int64_t k[3] = {unpack_axis(key, 42), unpack_axis(key, 21), unpack_axis(key, 0)};
       for (int j = 0; j < 3; j++) c[j] = (0.5 + k[j]) * mp.vs;
-      init_node(m.hdr[r], c, (float)(mp.vs / 4.0), 0, -1);
-      zero_node(m, r);
+      init_node(m.hdr[r], c, (float)(mp.vs / 4.0), 0, -1);  // records zeroed by map_reset
       m.hval[s] = r;
     } else {
       r = m.hval[s];
@@ -936,21 +935,8 @@ __global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __re
 }
 
 // zero a freshly allocated node's records (the pool is zeroed lazily)
-__device__ __forceinline__ void zero_node(DevMap& m, int id) {
-  PlaneRec& p = m.pl[id];
-  for (int j = 0; j < 27; j++) (&p.center[0])[j] = 0.0;
-  p.radius = 0;
-  p.pad = 0;
-  clu_zero(m.pcr_add[id]);
-  clu_zero(m.pcr_fix[id]);
-  for (int j = 0; j < kCovN; j++) m.cov_add[(size_t)id * kCovN + j] = 0.0;
-  for (int j = 0; j < 12; j++) m.eig[(size_t)id * 12 + j] = 0.0;
-  m.jour[id] = 0.0;
-  for (int j = 0; j < m.W; j++) clu_zero(m.pcrs[(size_t)id * m.W + j]);
-}
-
 // children of parent p in octant order, ids id0, id0+1, ...; appended to next
-__device__ __forceinline__ void alloc_parent(DevMap& m, int p, int id0, int* next, int next_pos, bool zero) {
+__device__ __forceinline__ void alloc_parent(DevMap& m, int p, int id0, int* next, int next_pos) {
   NodeHdr& ph = m.hdr[p];
   int k = 0;
   for (int o = 0; o < 8; o++) {
@@ -966,7 +952,6 @@ __device__ __forceinline__ void alloc_parent(DevMap& m, int p, int id0, int* nex
     double c[3];
     for (int j = 0; j < 3; j++) c[j] = ph.center[j] + (float)((2 * xyz[j] - 1) * ph.qlen);
     init_node(m.hdr[id], c, ph.qlen / 2, ph.layer + 1, p);
-    if (zero) zero_node(m, id);
     ph.child[o] = id;
     if (next) next[next_pos + k - 1] = id;
   }
@@ -1060,10 +1045,9 @@ __global__ void __launch_bounds__(1024) k_ins_alloc(int thread_num, DevMap m, co
       for (int o = 0; o < 8; o++) cc += (m.cfirst[(size_t)p * 8 + o] == -5) ? 1 : 0;
     int tot;
     const int off = block_excl_scan(cc, s_w, &tot);
-    if (p >= 0) alloc_parent(m, p, base + carry + off, nullptr, 0, false);
+    if (p >= 0) alloc_parent(m, p, base + carry + off, nullptr, 0);
     carry += tot;
   }
-  for (int id = base + threadIdx.x; id < base + carry && id < m.cap_nodes; id += blockDim.x) zero_node(m, id);
   __syncthreads();
   if (threadIdx.x == 0) m.counters[kCntNodes] = base + carry;
 }
@@ -1139,9 +1123,6 @@ static int alloc_children(vg_ctx* ctx, int* plist, int np, int* next, int next_b
   VG_TRY(excl_scan(ctx, w.ac_cnt, w.ac_off, np));
   k_child_alloc<<<grid_for(np), kBlock, 0, s>>>(np, plist, w.ac_off, ctx->map, next, next_base);
   k_add_counter<<<1, 64, 0, s>>>(ctx->map.counters, kCntNodes, w.ac_cnt, w.ac_off, np);
-  k_zero_nodes<<<grid_for(1 << 16), kBlock, 0, s>>>(first, nullptr, ctx->map.counters + kCntNodes, ctx->map.W, ctx->map.pl,
-                                                  ctx->map.pcr_add, ctx->map.pcr_fix, ctx->map.cov_add, ctx->map.eig,
-                                                  ctx->map.jour, ctx->map.pcrs);
   VG_HIP(hipGetLastError());
   VG_TRY(read_counters(ctx));
   *n_created = ctx->h_pinned[kCntNodes] - first;
@@ -1346,7 +1327,7 @@ __global__ void __launch_bounds__(256) k_child_alloc(int np, const int* __restri
                               int* __restrict__ next, int next_base) {
   const int base = m.counters[kCntNodes];
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < np; q += gridDim.x * blockDim.x)
-    alloc_parent(m, parents[q], base + (int)off[q], next, next_base + (int)off[q], false);
+    alloc_parent(m, parents[q], base + (int)off[q], next, next_base + (int)off[q]);
 }
 
 // apply the sorted pushes of one child (keys[j, jend)), in the reference's
@@ -1498,8 +1479,7 @@ __global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int ev_cap, M
   const int base = m.counters[kCntNodes];
   const int nnext = rc[kRcLvl + L];
   __syncthreads();
-  if (p_t >= 0) alloc_parent(m, p_t, base + coff, next, nnext + coff, false);
-  for (int id = base + tid; id < base + ntot && id < m.cap_nodes; id += blockDim.x) zero_node(m, id);
+  if (p_t >= 0) alloc_parent(m, p_t, base + coff, next, nnext + coff);
   __syncthreads();
   if (tid == 0) {
     m.counters[kCntNodes] = base + ntot;

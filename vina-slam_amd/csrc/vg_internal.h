@@ -309,6 +309,7 @@ struct vg_ctx {
   int ba_last_iters = 2;   // LM iterations of the previous run (ba_run's enqueue-ahead policy)
   vg::HostIn* h_in = nullptr;  // host-mapped per-scan inputs of replayed graphs (host address)
   vg::HostIn* d_in = nullptr;  // its device address
+  bool pool_zeroed = false;  // map_reset has cleared the node records once (then only the used ids)
   bool use_graphs = true;  // margi prefix on the second stream
   bool overlap_iekf = true;  // the next IEKF under the margi remainder (lio_state_estimation)
   bool spec_tail = true;     // the margi tail behind the predicted LM iterations (stage_ba)
