@@ -81,7 +81,20 @@ vg_multi* vg_multi_create(vg_ctx** ctxs, int B, int spin_us, int sleep_us) {
   M->wk.resize(B);
   for (int b = 0; b < B; b++) {
     vg_set_wait_policy(ctxs[b], spin_us, sleep_us);
-    if (B > 1) ctxs[b]->overlap_iekf = false;  // two streams per sequence (pipeline.cpp lio_state_estimation)
+    if (B > 1) {
+      // one stream per sequence: the concurrency comes from the B sequences,
+      // and every stream beyond the hardware queues makes sequences share a
+      // queue (measured: B = 4 at 1,465-2,704 scans/s with two streams each,
+      // depending on how the queues fell); the downsample and the margi prefix
+      // then run in enqueue order on the context stream
+      vg_ctx* c = ctxs[b];
+      c->overlap_iekf = false;
+      if (c->stream_ds && c->stream_ds != c->stream) {
+        (void)hipStreamSynchronize(c->stream_ds);
+        (void)hipStreamDestroy(c->stream_ds);
+        c->stream_ds = c->stream;
+      }
+    }
   }
   for (int b = 0; b < B; b++) M->th.emplace_back(worker, M, b);
   return M;
