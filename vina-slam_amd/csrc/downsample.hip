@@ -234,10 +234,17 @@ constexpr int kHdsTile = 1024;  // points per tile (256 lanes x 4)
 constexpr int kHdsSmall = 16;   // a lane sorts a voxel's segment itself (in registers) up to this many points
 constexpr int kHdsEmptyFirst = 0x7f7f7f7f;  // above every point index (ds_reset's memset byte)
 
-__global__ void __launch_bounds__(256) k_hds_insert(int n, const float* __restrict__ x, const float* __restrict__ y,
-                                                    const float* __restrict__ z, double size, DownsampleBufs d,
-                                                    const int* __restrict__ need) {
+// the scan's input cloud as a kernel argument -> device memory, so that the
+// chain behind it (captured once as a graph) reads it from there
+__global__ void k_hds_args(HdsIn* __restrict__ dst, HdsIn a) {
+  if (threadIdx.x == 0) *dst = a;
+}
+
+__global__ void __launch_bounds__(256) k_hds_insert(double size, DownsampleBufs d, const int* __restrict__ need) {
   if (need && !*need) return;
+  const HdsIn a = *d.arg;
+  const float *x = a.x, *y = a.y, *z = a.z;
+  const int n = a.n;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int64_t kx = key_axis_f(x[i], size) + kKeyOff;
     int64_t ky = key_axis_f(y[i], size) + kKeyOff;
@@ -273,8 +280,10 @@ __device__ __forceinline__ void hds_code(const DownsampleBufs& d, int i, int n, 
   }
 }
 
-__global__ void __launch_bounds__(256) k_hds_tiles(int n, DownsampleBufs d, const int* __restrict__ need) {
+__global__ void __launch_bounds__(256) k_hds_tiles(DownsampleBufs d, const int* __restrict__ need) {
   if (need && !*need) return;
+  const int n = d.arg->n;
+  if ((int)blockIdx.x * kHdsTile >= n) return;  // the grid covers the capacity
   __shared__ int s_f[4], s_c[4];
   const int i0 = blockIdx.x * kHdsTile + threadIdx.x * 4;
   int F = 0, C = 0;
@@ -302,9 +311,11 @@ __global__ void __launch_bounds__(256) k_hds_tiles(int n, DownsampleBufs d, cons
 
 // need_in: this pass's predicate (nullptr: always); need_out: the fallback flag
 // this pass decides (nullptr: none)
-__global__ void __launch_bounds__(256) k_hds_rank(int n, int ntile, DownsampleBufs d, const int* __restrict__ need_in,
+__global__ void __launch_bounds__(256) k_hds_rank(DownsampleBufs d, const int* __restrict__ need_in,
                                                   int* __restrict__ need_out, int min_out) {
   if (need_in && !*need_in) return;
+  const int n = d.arg->n, ntile = (n + kHdsTile - 1) / kHdsTile;
+  if ((int)blockIdx.x >= ntile) return;  // the grid covers the capacity
   __shared__ unsigned long long s_w[4];
   __shared__ int s_b[2][4];
   // prefix of the earlier tiles (first points, points)
@@ -367,8 +378,9 @@ __global__ void __launch_bounds__(256) k_hds_rank(int n, int ntile, DownsampleBu
   }
 }
 
-__global__ void __launch_bounds__(256) k_hds_scatter(int n, DownsampleBufs d, const int* __restrict__ need) {
+__global__ void __launch_bounds__(256) k_hds_scatter(DownsampleBufs d, const int* __restrict__ need) {
   if (need && !*need) return;
+  const int n = d.arg->n;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t s = d.pslot[i];
     const int pos = atomicAdd(&d.hfill[s], 1);
@@ -423,10 +435,10 @@ __device__ __forceinline__ void hds_sorted_mean(const uint32_t* __restrict__ sg,
     }
 }
 
-__global__ void __launch_bounds__(256) k_hds_mean(DownsampleBufs d, const float* __restrict__ x,
-                                                  const float* __restrict__ y, const float* __restrict__ z,
-                                                  const float* __restrict__ in, const int* __restrict__ need) {
+__global__ void __launch_bounds__(256) k_hds_mean(DownsampleBufs d, const int* __restrict__ need) {
   if (need && !*need) return;
+  const HdsIn a = *d.arg;
+  const float *__restrict__ x = a.x, *__restrict__ y = a.y, *__restrict__ z = a.z, *__restrict__ in = a.in;
   const int nv = d.hflags[1];
   for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += gridDim.x * blockDim.x) {
     const int i = d.vfirst[v];
@@ -461,10 +473,10 @@ __global__ void __launch_bounds__(256) k_hds_mean(DownsampleBufs d, const float*
 // recurrences (the same arithmetic as k_hds_mean, bit for bit).
 constexpr int kHdsBits = 1 << 18;          // indices per bitmap window (32 KB of LDS)
 constexpr int kHdsWords = kHdsBits / 32;
-__global__ void __launch_bounds__(256) k_hds_big(DownsampleBufs d, const float* __restrict__ x,
-                                                 const float* __restrict__ y, const float* __restrict__ z,
-                                                 const float* __restrict__ in, const int* __restrict__ need) {
+__global__ void __launch_bounds__(256) k_hds_big(DownsampleBufs d, const int* __restrict__ need) {
   if (need && !*need) return;
+  const HdsIn a = *d.arg;
+  const float *x = a.x, *y = a.y, *z = a.z, *in = a.in;
   __shared__ uint32_t bm[kHdsWords];
   __shared__ int s_w[4], s_base;
   const int nbig = d.hflags[3];
@@ -552,21 +564,39 @@ int ds_enqueue_hashed(vg_ctx* ctx, hipStream_t s, const float* x, const float* y
     ctx->err = "scan larger than max_points_per_scan";
     return VG_E_CAPACITY;
   }
-  const int g = grid_for(n), ntile = (n + kHdsTile - 1) / kHdsTile;
   int* need = d.hflags + 2;
   if (n == 0) {
     VG_HIP(hipMemsetAsync(d.hflags + 1, 0, 2 * sizeof(int), s));
   } else {
-    for (int pass = 0; pass < (fallback ? 2 : 1); pass++) {
-      const int* pin = pass ? need : nullptr;
-      const double vs = pass ? voxel / 2 : voxel;
-      k_hds_insert<<<g, kBlock, 0, s>>>(n, x, y, z, vs, d, pin);
-      k_hds_tiles<<<ntile, kBlock, 0, s>>>(n, d, pin);
-      k_hds_rank<<<ntile, kBlock, 0, s>>>(n, ntile, d, pin, pass == 0 && fallback ? need : nullptr, 2000);
-      k_hds_scatter<<<g, kBlock, 0, s>>>(n, d, pin);
-      k_hds_mean<<<g, kBlock, 0, s>>>(d, x, y, z, in, pin);
-      k_hds_big<<<64, kBlock, 0, s>>>(d, x, y, z, in, pin);
+    k_hds_args<<<1, 64, 0, s>>>(d.arg, HdsIn{x, y, z, in, n, 0});
+    // every count and size below is read on the device (grids cover the
+    // context's capacity, surplus blocks exit), so the chain is one graph
+    // per (voxel, fallback), replayed for every scan: one launch instead of 12
+    const int cap = ctx->cap.max_points_per_scan;
+    const int g = grid_for(cap, kBlock, 1024), ntile = (cap + kHdsTile - 1) / kHdsTile;
+    auto chain = [&](hipStream_t st) {
+      for (int pass = 0; pass < (fallback ? 2 : 1); pass++) {
+        const int* pin = pass ? need : nullptr;
+        const double vs = pass ? voxel / 2 : voxel;
+        k_hds_insert<<<g, kBlock, 0, st>>>(vs, d, pin);
+        k_hds_tiles<<<ntile, kBlock, 0, st>>>(d, pin);
+        k_hds_rank<<<ntile, kBlock, 0, st>>>(d, pin, pass == 0 && fallback ? need : nullptr, 2000);
+        k_hds_scatter<<<g, kBlock, 0, st>>>(d, pin);
+        k_hds_mean<<<g, kBlock, 0, st>>>(d, pin);
+        k_hds_big<<<64, kBlock, 0, st>>>(d, pin);
+      }
+    };
+    const bool use_graph = ctx->use_graphs && fallback && voxel == ctx->cfg.down_size;
+    if (use_graph && !ctx->g_ds) {
+      VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      chain(s);
+      hipGraph_t gr = nullptr;
+      VG_HIP(hipStreamEndCapture(s, &gr));
+      VG_HIP(hipGraphInstantiate(&ctx->g_ds, gr, nullptr, nullptr, 0));
+      VG_HIP(hipGraphDestroy(gr));
     }
+    if (use_graph) VG_HIP(hipGraphLaunch(ctx->g_ds, s));
+    else chain(s);
   }
   if (pub_seq > 0) VG_TRY(state_publish_ds(ctx, s, pub_seq, d.hflags, false));
   VG_HIP(hipGetLastError());
@@ -589,6 +619,7 @@ int ds_alloc(vg_ctx* ctx) {
   d.oi = ctx->arena.take<float>(n);
   d.oc = ctx->arena.take<float>(n);
   d.flags = ctx->arena.take<int>(4);
+  d.arg = ctx->arena.take<HdsIn>(1);
   size_t b1 = 0, b2 = 0, b3 = 0;
   VG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, d.keys, d.keys_sorted, d.idx, d.idx_sorted, n, 0, 63,
                                             ctx->stream));

@@ -82,7 +82,12 @@ struct KdMap {
   size_t tmp_bytes = 0;
 };
 
+struct HdsIn {  // the per-scan downsample's input (k_hds_args -> device, read by every k_hds_* kernel)
+  const float *x, *y, *z, *in;
+  int n, pad;
+};
 struct DownsampleBufs {
+  HdsIn* arg = nullptr;       // the current scan's input cloud (device copy, see k_hds_args)
   uint64_t *keys = nullptr, *keys_sorted = nullptr;
   uint32_t *idx = nullptr, *idx_sorted = nullptr;
   uint32_t *head = nullptr, *pos = nullptr, *seg = nullptr;
@@ -302,6 +307,7 @@ struct vg_ctx {
   hipGraphExec_t g_iekf[3] = {nullptr, nullptr, nullptr};
   hipGraphExec_t g_margi[2] = {};  // margi after the window view (map.hip map_margi): ungated, gated
   hipGraphExec_t g_ba = nullptr;     // one LM iteration (ba.hip ba_run)
+  hipGraphExec_t g_ds = nullptr;     // the per-scan downsample chain (downsample.hip ds_enqueue_hashed)
   // steady state: the insert + recut of one scan, per ring position mp[0] (pipeline.cpp stage_insert_recut)
   hipGraphExec_t g_mid[vg::kMaxWin] = {};
   bool capturing = false;  // a stream capture is open (host-side steps that cannot be captured are deferred)

@@ -163,6 +163,7 @@ int vg_destroy(vg_ctx* ctx) {
   for (auto& g : ctx->g_margi)
     if (g) (void)hipGraphExecDestroy(g);
   if (ctx->g_ba) (void)hipGraphExecDestroy(ctx->g_ba);
+  if (ctx->g_ds) (void)hipGraphExecDestroy(ctx->g_ds);
   for (auto& g : ctx->g_mid)
     if (g) (void)hipGraphExecDestroy(g);
   if (ctx->h_in) (void)hipHostFree(ctx->h_in);

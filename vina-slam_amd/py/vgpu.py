@@ -186,6 +186,7 @@ class Context:
         r = lib().vg_create(ctypes.byref(cconfig), ctypes.byref(cap), device, ctypes.byref(self.h))
         if r != 0:
             raise VgError("vg_create failed (%d)" % r)
+        self._fn_step = lib().vg_step_dev
 
     def _chk(self, r, what):
         if r != 0:
@@ -261,6 +262,18 @@ class Context:
         imu = np.ascontiguousarray(imu, dtype=np.float64).reshape(-1, 7)
         self._chk(lib().vg_step_dev(self.h, ctypes.c_void_p(dx), ctypes.c_void_p(dy), ctypes.c_void_p(dz),
                                     ctypes.c_void_p(di), n, beg, end, _d(imu), imu.shape[0]), "vg_step_dev")
+
+    def prep_step_dev(self, dx, dy, dz, di, n, beg, end, imu):
+        """vg_step_dev's arguments converted once (a caller that holds its
+        scans resident passes them straight on, as a C++ caller would)."""
+        imu = np.ascontiguousarray(imu, dtype=np.float64).reshape(-1, 7)
+        return (imu, (ctypes.c_void_p(dx), ctypes.c_void_p(dy), ctypes.c_void_p(dz), ctypes.c_void_p(di),
+                      ctypes.c_int(n), ctypes.c_double(beg), ctypes.c_double(end), _d(imu), ctypes.c_int(imu.shape[0])))
+
+    def step_prepped(self, p):
+        r = self._fn_step(self.h, *p[1])
+        if r != 0:
+            self._chk(r, "vg_step_dev")
 
     def state(self):
         s = np.zeros(STATE_LEN)
