@@ -42,13 +42,13 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     return fail(VG_E_HIP);
   }
   if ((e = hipStreamCreateWithFlags(&ctx->stream_ds, hipStreamNonBlocking)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&ctx->ev_ds_done, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&ctx->ev_ds_free, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&ctx->ev_recut_done, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&ctx->ev_prefix_done, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&ctx->ev_scan_ready, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&ctx->ev_tail_a, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&ctx->ev_iekf_done, hipEventDisableTiming)) != hipSuccess) {
+      (e = hipEventCreateWithFlags(&ctx->ev_ds_done, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_ds_free, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_recut_done, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_prefix_done, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_scan_ready, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_tail_a, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&ctx->ev_iekf_done, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess) {
     ctx->err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
