@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--max-nodes", type=int, default=0, help="context capacity: octree nodes (0: product default)")
     ap.add_argument("--max-fix", type=int, default=0, help="context capacity: point_fix points (0: default)")
     ap.add_argument("--hash-log2", type=int, default=0, help="context capacity: root hash slots, log2 (0: default)")
-    ap.add_argument("--multi", default="2,4,8",
+    ap.add_argument("--multi", default="2,4,8,16",
                     help="multi-sequence mode (vg_multi_*): B values to time at N=1 (empty: skip); each B runs "
                          "in a child process of its own, before this one touches the GPU")
     ap.add_argument("--multi-child", type=int, default=0, help=argparse.SUPPRESS)
@@ -268,7 +268,7 @@ def main():
                        "parallelism": ("tile-sharded x%d" if tile else "replica x%d") % world},
             "roofline": roof, "roofline_k_ba_solve": roof_solve, "roofline_k_iekf": roof_iekf,
             "host_ms_per_scan": host_ms, "host_input": h2d, "cpu_baseline": cpu, "ate_vs_cpu": ate_cpu,
-            "target_128line": targets or None, "multi_sequence": multi,
+            "target_128line": targets or None, "multi_sequence": multi_roofline(multi, roof),
         }
         print(json.dumps(line))
     if world > 1:
@@ -302,6 +302,16 @@ def scan_roofline(stats, stage_stats, W, t_scan):
                               "P_k": round(p_mean, 1), "V_ins": mean("v_ins"), "V_slide": mean("n_slide"),
                               "F": mean("n_factors"), "I_H": mean("ba_hess"), "I_R": mean("ba_iters")},
             "note": "SURVEY 8(d) algorithmic bytes per scan / ms_per_step; P_k from the per-stage pass"}
+
+
+def multi_roofline(multi, roof):
+    """The whole-scan HBM fraction of each multi-sequence rate (the same scans,
+    so the same SURVEY 8(d) algorithmic bytes per scan as the metric's)."""
+    if not multi or not roof or not roof.get("bytes_per_scan"):
+        return multi
+    multi["roofline_frac_by_B"] = {B: round(v * roof["bytes_per_scan"] / (roof["peak"] * 1e9), 6)
+                                   for B, v in multi["by_B"].items()}
+    return multi
 
 
 def multi_children(args, host_scans, warmup, total):
