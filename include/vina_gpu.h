@@ -217,6 +217,11 @@ int vg_sync_push_scan(vg_sync* s, double header_time, double last_point_time, in
 int vg_sync_push_imu(vg_sync* s, const double* imu7);
 int vg_sync_pop(vg_sync* s, int* scan_id, double* beg, double* end, double* imu7, int cap, int* m, int* ready);
 int vg_get_state(vg_ctx* ctx, double* state);
+/* The last completed scan's downsampled cloud (body frame, after the deskew;
+ * the map path's pl_down, local_mapping.cpp:396-406) as n x 3 floats, up to
+ * cap copied, *n = its size: what pub_localtraj moves to the world and
+ * publishes on /map_scan (publishers.cpp:65-97). Completes outstanding work. */
+int vg_scan_points(vg_ctx* ctx, float* xyz, int cap, int* n);
 int vg_get_stats(vg_ctx* ctx, vg_stats* out);
 /* Per-scan counters of every completed scan since vg_create / vg_reset, in
  * order: copies min(n, cap) records, *n = total (out may be NULL to query). */

@@ -2,6 +2,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <vector>
 #include "vg_internal.h"
 
 using namespace vg;
@@ -342,6 +343,31 @@ int vg_step_deskew(vg_ctx* ctx, const float* xyz, const float* intensity, const 
 int vg_get_state(vg_ctx* ctx, double* state) {
   if (!ctx || !state) return VG_E_ARG;
   VG_TRY(host_state(ctx, state));
+  return VG_OK;
+}
+
+// the last completed scan's downsampled cloud (body frame after the deskew,
+// the map path's pl_down, local_mapping.cpp:396-406): the points
+// pub_localtraj publishes on /map_scan once moved to the world
+// (publishers.cpp:65-97). Completes the outstanding work first.
+int vg_scan_points(vg_ctx* ctx, float* xyz, int cap, int* n) {
+  if (!ctx || !n || cap < 0 || (cap > 0 && !xyz)) return VG_E_ARG;
+  VG_TRY(host_sync(ctx));
+  int cnt = 0;
+  VG_HIP(hipMemcpy(&cnt, ctx->ds.hflags + 1, sizeof(int), hipMemcpyDeviceToHost));
+  *n = cnt;
+  const int k = cnt < cap ? cnt : cap;
+  if (k > 0) {
+    std::vector<float> b((size_t)3 * k);
+    VG_HIP(hipMemcpy(b.data(), ctx->ds.ox, k * sizeof(float), hipMemcpyDeviceToHost));
+    VG_HIP(hipMemcpy(b.data() + k, ctx->ds.oy, k * sizeof(float), hipMemcpyDeviceToHost));
+    VG_HIP(hipMemcpy(b.data() + 2 * k, ctx->ds.oz, k * sizeof(float), hipMemcpyDeviceToHost));
+    for (int i = 0; i < k; i++) {
+      xyz[3 * i] = b[i];
+      xyz[3 * i + 1] = b[k + i];
+      xyz[3 * i + 2] = b[2 * k + i];
+    }
+  }
   return VG_OK;
 }
 
