@@ -1119,6 +1119,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   const int seq0 = ctx->pub_seq + 1;
   ctx->pub_seq += 10;
   k_ba_init<<<1, 256, 0, s>>>(d.st, d.hl, hl_part, nout, ring, d.mpring, W, map_rc_status(ctx), seq0);
+  VG_HIP(flush_insert_events(ctx));
   // factor count on the device (the recut's kCntFactors): fixed grids, so an
   // asynchronous recut needs no host round trip before the LM
   (void)nf;

@@ -2405,6 +2405,7 @@ int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thr
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream_ds;
   const int nlev = mp.max_layer + 1;
+  VG_HIP(flush_insert_events(ctx));
   VG_HIP(hipStreamWaitEvent(s, ctx->ev_recut_done, 0));  // recorded at the recut's end (map_recut)
   const int gl = 64;  // grid-stride over device-side counts
   k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour, w.rc, n_oldest);

@@ -460,6 +460,7 @@ int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float*
   P->n_raw = n;
   P->cur.st.n_raw = n;
   // own stream: waits only until the previous insert has read the ds buffers
+  VG_HIP(flush_insert_events(ctx));
   VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_ds_free, 0));
   VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_scan_ready, 0));  // a deskewed scan (no-op otherwise)
   prof_begin(ctx, kProfDownsample, ctx->stream_ds);
@@ -615,8 +616,9 @@ static int stage_insert_recut(vg_ctx* ctx) {
   prof_begin(ctx, kProfInsert);
   VG_HIP(hipGraphLaunch(ge, ctx->stream));
   prof_end(ctx, kProfInsert);
-  VG_HIP(hipEventRecord(ctx->ev_ds_free, ctx->stream));     // the insert has read the ds buffers
-  VG_HIP(hipEventRecord(ctx->ev_recut_done, ctx->stream));  // the margi prefix starts from here
+  // ev_ds_free (the insert has read the ds buffers) and ev_recut_done (the
+  // margi prefix starts from here): flush_insert_events
+  ctx->ins_ev_pending = true;
   P->wp_n[slot] = P->n_raw;  // an upper bound until the scan's counters are absorbed (absorb_p2)
   P->ins_slot = slot;
   P->cur.ins_slot = slot;

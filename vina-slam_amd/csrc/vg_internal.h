@@ -315,7 +315,8 @@ struct vg_ctx {
   int ba_last_iters = 2;   // LM iterations of the previous run (ba_run's enqueue-ahead policy)
   vg::HostIn* h_in = nullptr;  // host-mapped per-scan inputs of replayed graphs (host address)
   vg::HostIn* d_in = nullptr;  // its device address
-  bool pool_zeroed = false;  // map_reset has cleared the node records once (then only the used ids)
+  bool pool_zeroed = false;
+  bool ins_ev_pending = false;  // ev_ds_free / ev_recut_done of the last insert+recut graph not recorded yet  // map_reset has cleared the node records once (then only the used ids)
   bool use_graphs = true;  // margi prefix on the second stream
   bool overlap_iekf = true;  // the next IEKF under the margi remainder (lio_state_estimation)
   bool spec_tail = true;     // the margi tail behind the predicted LM iterations (stage_ba)
@@ -498,6 +499,17 @@ int ds_enqueue(vg_ctx* ctx, hipStream_t s, const float* x, const float* y, const
                double voxel, int pub_seq);
 // map.hip
 int map_alloc(vg_ctx* ctx);
+// The insert+recut graph's completion events are recorded lazily: right
+// behind the LM's k_ba_init when the LM follows (a marker packet straight
+// after the graph delays the next dispatch), else before their first waiter.
+// Recording later only makes the waiters wait longer.
+inline hipError_t flush_insert_events(vg_ctx* ctx) {
+  if (!ctx->ins_ev_pending) return hipSuccess;
+  ctx->ins_ev_pending = false;
+  hipError_t e = hipEventRecord(ctx->ev_ds_free, ctx->stream);
+  if (e == hipSuccess) e = hipEventRecord(ctx->ev_recut_done, ctx->stream);
+  return e;
+}
 int map_reset(vg_ctx* ctx);
 int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
                    hipEvent_t ev0, hipEvent_t ev1, int tag = 0, hipStream_t s = nullptr);
