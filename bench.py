@@ -431,7 +431,8 @@ def host_input_rate(p, seq, host_scans, imus, warmup, steps, dev):
     ctx.close()
     k = n - warmup
     return {"value": round(k / dt, 3), "unit": "scans/s", "ms_per_step": round(dt * 1e3 / k, 4), "steps": k,
-            "note": "vg_step: host xyz (AoS) + intensity, SoA conversion and H2D copy inside the timed region"}
+            "note": "vg_step: host xyz (AoS) + intensity inside the timed region: one copy into a pinned "
+                    "in-flight slot, DMA to HBM and AoS->SoA unpack on the device ahead of the scan's kernels"}
 
 
 def target_workload(args, cfg, host, warm, dev):

@@ -27,10 +27,14 @@ TIGHT_M = 1e-9   # per-scan position bound (observed ~1e-14 m)
 ATE_M = 0.01     # north star: ATE within 1 cm of the CPU reference
 
 
-def run_pair(cfgname, lidar, nscan, seq_id=0, max_points=1_100_000, resident=False):
+def run_pair(cfgname, lidar, nscan, seq_id=0, max_points=1_100_000, resident=False, nodrain=False, shrink=0):
     """resident: the scans go to the device first and the GPU side runs
     vg_step_dev (no stream drain between scans, as in the bench), so the next
-    scan's IEKF overlaps the previous margi's remainder (map_margi)."""
+    scan's IEKF overlaps the previous margi's remainder (map_margi).
+    nodrain: host buffers through vg_step without reading stats between scans
+    (the in-flight upload slots, vina_gpu.cpp upload_scan). shrink: the first
+    `shrink` scans keep only their first third of points (both sides), so the
+    upload slots grow mid-sequence."""
     p = vgconfig.load(cfgname)
     g = p["General"]
     seq = synth.Sequence(lidar, seq_id, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
@@ -50,6 +54,8 @@ def run_pair(cfgname, lidar, nscan, seq_id=0, max_points=1_100_000, resident=Fal
                        .to("cuda:0"))
     for k in range(nscan):
         xyz, it, b, e = seq.scan(k)
+        if k < shrink:
+            xyz, it = np.ascontiguousarray(xyz[: xyz.shape[0] // 3]), np.ascontiguousarray(it[: it.shape[0] // 3])
         imu = seq.imu(k)
         orc.step(xyz, it, b, e, imu)
         if resident:
@@ -58,8 +64,8 @@ def run_pair(cfgname, lidar, nscan, seq_id=0, max_points=1_100_000, resident=Fal
         else:
             gpu.step(xyz, it, b, e, imu)
         so.append(orc.stats())
-        sg.append(gpu.stats() if not resident else None)
-    if resident:  # stats of every scan, read only now (no drain while stepping)
+        sg.append(gpu.stats() if not (resident or nodrain) else None)
+    if resident or nodrain:  # stats of every scan, read only now (no drain while stepping)
         sg = gpu.stats_log()
     return seq, orc, gpu, so, sg
 
@@ -102,6 +108,15 @@ def test_resident_pipeline_matches_oracle(oracle_lib):
     """The bench's way of stepping (device-resident scans, vg_step_dev, no
     drain): the overlapped IEKF / margi path, every counter exact."""
     seq, orc, gpu, so, sg = run_pair("mid360", "64line", 30, resident=True)
+    check_case("mid360", "64line", 30, orc, gpu, so, sg)
+
+
+def test_host_input_nodrain_matches_oracle(oracle_lib):
+    """Host buffers through vg_step with nothing read back between scans: the
+    two in-flight upload slots (pinned copy, DMA, device unpack) are reused
+    every other scan and grow at scan 3, the IEKF of an uploaded scan overlaps
+    the previous margi remainder; every counter exact."""
+    seq, orc, gpu, so, sg = run_pair("mid360", "64line", 30, nodrain=True, shrink=3)
     check_case("mid360", "64line", 30, orc, gpu, so, sg)
 
 

@@ -357,6 +357,7 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   // share hardware queues (B = 4: 2,742 -> 1,430 scans/s)
   if (!ctx->stream_iekf) VG_HIP(hipStreamCreateWithFlags(&ctx->stream_iekf, hipStreamNonBlocking));
   VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->ev_tail_a, 0));
+  if (ctx->in_ev) VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->in_ev, 0));  // a host-input scan's unpack
   VG_TRY(iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, begin ? P->begin_xc : nullptr, ctx->stream_iekf));
   VG_HIP(hipEventRecord(ctx->ev_iekf_done, ctx->stream_iekf));
   VG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_iekf_done, 0));

@@ -407,6 +407,33 @@ int state_deskew(vg_ctx* ctx, const double* par, int npose, const float* x, cons
   return VG_OK;
 }
 
+// host-input scans: the DMA image of the caller's arrays (xyz AoS, intensity,
+// time, packed by n) -> the SoA planes every per-scan kernel reads; a missing
+// intensity reads as 0 (as the synchronous staging did)
+__global__ void __launch_bounds__(256) k_unpack_scan(int n, const float* __restrict__ img, int has_i, int has_t,
+                                                     float* __restrict__ x, float* __restrict__ y,
+                                                     float* __restrict__ z, float* __restrict__ in,
+                                                     float* __restrict__ t) {
+  const float* xyz = img;
+  const float* si = img + 3 * (size_t)n;
+  const float* st = si + (has_i ? n : 0);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    x[i] = xyz[3 * (size_t)i];
+    y[i] = xyz[3 * (size_t)i + 1];
+    z[i] = xyz[3 * (size_t)i + 2];
+    in[i] = has_i ? si[i] : 0.0f;
+    if (has_t) t[i] = st[i];
+  }
+}
+
+int state_unpack_scan(vg_ctx* ctx, hipStream_t s, int n, const float* img, bool has_i, bool has_t, float* x, float* y, float* z,
+                      float* in, float* t) {
+  if (n <= 0) return VG_OK;
+  k_unpack_scan<<<grid_for(n), 256, 0, s>>>(n, img, has_i ? 1 : 0, has_t ? 1 : 0, x, y, z, in, t);
+  VG_HIP(hipGetLastError());
+  return VG_OK;
+}
+
 int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq, int* flags, bool reset) {
   k_publish_ds<<<1, 64, 0, s>>>(flags, ctx->d_pub, seq, reset ? 1 : 0);
   VG_HIP(hipGetLastError());

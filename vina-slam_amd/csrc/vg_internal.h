@@ -342,6 +342,20 @@ struct vg_ctx {
   int wait_spin_us = 0, wait_sleep_us = 0;  // vg_set_wait_policy (0 sleep: spin)
   int plane_tag = 0;        // IEKF iteration tag of the P_k count (vg_profile stages)
   int* h_pinned = nullptr;  // small pinned host scratch for counters
+  // host-input scans (vg_step / vg_step_deskew): two slots in flight, each the
+  // caller's arrays copied once into pinned memory, one DMA to HBM and an
+  // AoS -> SoA unpack on stream_ds ahead of the scan's kernels, no host wait
+  // on the device (vina_gpu.cpp upload_scan)
+  struct InSlot {
+    char* h = nullptr;          // pinned: xyz AoS (12 B/pt) | intensity | time, packed by n
+    float* d = nullptr;         // HBM: the DMA image (5 cap floats), then the SoA planes x y z i t
+    hipEvent_t up = nullptr;    // unpack done (stream_ds): the DMA has read h
+    hipEvent_t done = nullptr;  // main stream past the scan that read the planes
+    bool live = false;
+  } in_slot[2];
+  size_t in_cap = 0;  // points per slot
+  int in_next = 0;
+  hipEvent_t in_ev = nullptr;  // the current scan's unpack (the split IEKF stream waits for it)
 
   vg_stats stats;
   void* host = nullptr;     // host-side pipeline state (pipeline.cpp)
@@ -556,6 +570,8 @@ int state_publish_counters(vg_ctx* ctx, int seq);
 int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq, int* flags, bool reset);
 int state_deskew(vg_ctx* ctx, const double* par, int npose, const float* x, const float* y, const float* z,
                  const float* in, const float* t, int n);
+int state_unpack_scan(vg_ctx* ctx, hipStream_t s, int n, const float* img, bool has_i, bool has_t, float* x, float* y, float* z,
+                      float* in, float* t);
 // initialisation: motion_blur's per-point part on a close-downsampled
 // cloud (pts, ascending time) -> nout fp64 body points; par (host): frame pose,
 // extrinsic, npose IMU pose records (descending start); synchronous

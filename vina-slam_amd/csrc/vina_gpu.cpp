@@ -1,4 +1,5 @@
 // vina_gpu.cpp — C-ABI entry points (include/vina_gpu.h) and context lifecycle.
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -168,6 +169,13 @@ int vg_destroy(vg_ctx* ctx) {
   for (auto& g : ctx->g_mid)
     if (g) (void)hipGraphExecDestroy(g);
   if (ctx->h_in) (void)hipHostFree(ctx->h_in);
+  if (ctx->stream_ds && ctx->stream_ds != ctx->stream) (void)hipStreamSynchronize(ctx->stream_ds);
+  for (auto& sl : ctx->in_slot) {
+    if (sl.h) (void)hipHostFree(sl.h);
+    if (sl.d) (void)hipFree(sl.d);
+    if (sl.up) (void)hipEventDestroy(sl.up);
+    if (sl.done) (void)hipEventDestroy(sl.done);
+  }
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->stream_ds && ctx->stream_ds != ctx->stream) (void)hipStreamSynchronize(ctx->stream_ds);
   if (ctx->stream_ds && ctx->stream_ds != ctx->stream) (void)hipStreamDestroy(ctx->stream_ds);
@@ -293,6 +301,78 @@ int vg_seed(vg_ctx* ctx, const double* state) {
   return VG_OK;
 }
 
+// A host-input scan into one of the two in-flight slots: the caller's arrays
+// are copied once into the slot's pinned block (the only host work per point),
+// one DMA takes them to HBM and k_unpack_scan writes the SoA planes, both on
+// stream_ds; the main stream waits for the unpack on the device. The slot is
+// reused two scans later: the host waits for its previous DMA (long done in
+// the steady state), the device for the main stream to pass the scan that read
+// it. *slot receives the index for upload_done.
+static int upload_scan(vg_ctx* ctx, const float* xyz, const float* inten, const float* time, int n, float* soa[5],
+                       int* slot) {
+  // slots sized to the largest scan so far (grown with headroom; the old ones
+  // are released once both streams have drained)
+  if ((size_t)n > ctx->in_cap) {
+    VG_HIP(hipStreamSynchronize(ctx->stream_ds));
+    VG_HIP(hipStreamSynchronize(ctx->stream));
+    for (auto& sl : ctx->in_slot) {
+      if (sl.h) VG_HIP(hipHostFree(sl.h));
+      if (sl.d) VG_HIP(hipFree(sl.d));
+      sl.h = nullptr;
+      sl.d = nullptr;
+      sl.live = false;
+    }
+    ctx->in_cap = std::min((size_t)ctx->cap.max_points_per_scan, ((size_t)n * 5 / 4 + 65535) & ~(size_t)65535);
+  }
+  const size_t cap = ctx->in_cap;
+  if (!ctx->in_slot[0].h) {
+    for (auto& sl : ctx->in_slot) {
+      VG_HIP(hipHostMalloc((void**)&sl.h, cap * 5 * sizeof(float), hipHostMallocDefault));
+      VG_HIP(hipMalloc((void**)&sl.d, cap * 10 * sizeof(float)));
+      if (!sl.up) VG_HIP(hipEventCreateWithFlags(&sl.up, hipEventDisableTiming | hipEventDisableSystemFence));
+      if (!sl.done) VG_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming | hipEventDisableSystemFence));
+    }
+  }
+  *slot = ctx->in_next;
+  vg_ctx::InSlot& sl = ctx->in_slot[ctx->in_next];
+  ctx->in_next ^= 1;
+  if (sl.live) VG_HIP(hipEventSynchronize(sl.up));
+  const size_t nn = (size_t)n;
+  size_t nf = 3 * nn;
+  memcpy(sl.h, xyz, nn * 3 * sizeof(float));
+  if (inten) {
+    memcpy(sl.h + nf * sizeof(float), inten, nn * sizeof(float));
+    nf += nn;
+  }
+  if (time) {
+    memcpy(sl.h + nf * sizeof(float), time, nn * sizeof(float));
+    nf += nn;
+  }
+  hipStream_t s = ctx->stream_ds;
+  if (sl.live) VG_HIP(hipStreamWaitEvent(s, sl.done, 0));
+  VG_HIP(hipMemcpyAsync(sl.d, sl.h, nf * sizeof(float), hipMemcpyHostToDevice, s));
+  float* pl = sl.d + 5 * cap;
+  for (int c = 0; c < 5; c++) soa[c] = pl + (size_t)c * cap;
+  VG_TRY(state_unpack_scan(ctx, s, n, sl.d, inten != nullptr, time != nullptr, soa[0], soa[1], soa[2], soa[3], soa[4]));
+  VG_HIP(hipEventRecord(sl.up, s));
+  if (s != ctx->stream) VG_HIP(hipStreamWaitEvent(ctx->stream, sl.up, 0));
+  ctx->in_ev = sl.up;
+  sl.live = true;
+  return VG_OK;
+}
+
+// after the scan's enqueue: the main stream has everything that reads the slot
+// (the IEKF stream and the downsample stream join it before the insert)
+static int upload_done(vg_ctx* ctx, int slot, int r) {
+  ctx->in_ev = nullptr;
+  const hipError_t e = hipEventRecord(ctx->in_slot[slot].done, ctx->stream);
+  if (r == VG_OK && e != hipSuccess) {
+    ctx->err = std::string("upload_done: ") + hipGetErrorString(e);
+    return VG_E_HIP;
+  }
+  return r;
+}
+
 int vg_step(vg_ctx* ctx, const float* xyz, const float* intensity, int n, double pcl_beg_time,
             double pcl_end_time, const double* imu, int m) {
   if (!ctx || (!xyz && n > 0) || n < 0 || m < 0 || (m > 0 && !imu)) return VG_E_ARG;
@@ -300,8 +380,11 @@ int vg_step(vg_ctx* ctx, const float* xyz, const float* intensity, int n, double
     ctx->err = "scan larger than max_points_per_scan";
     return VG_E_CAPACITY;
   }
-  if (n > 0) VG_TRY(upload_aos(ctx, xyz, intensity, n));
-  return host_step(ctx, ctx->d_x, ctx->d_y, ctx->d_z, ctx->d_i, n, pcl_beg_time, pcl_end_time, imu, m);
+  if (n == 0) return host_step(ctx, ctx->d_x, ctx->d_y, ctx->d_z, ctx->d_i, n, pcl_beg_time, pcl_end_time, imu, m);
+  float* p[5];
+  int slot = 0;
+  VG_TRY(upload_scan(ctx, xyz, intensity, nullptr, n, p, &slot));
+  return upload_done(ctx, slot, host_step(ctx, p[0], p[1], p[2], p[3], n, pcl_beg_time, pcl_end_time, imu, m));
 }
 
 int vg_step_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, const float* d_intensity, int n,
@@ -332,12 +415,14 @@ int vg_step_deskew(vg_ctx* ctx, const float* xyz, const float* intensity, const 
     ctx->err = "scan larger than max_points_per_scan";
     return VG_E_CAPACITY;
   }
-  if (n > 0) VG_TRY(upload_aos(ctx, xyz, intensity, n));
-  // times ride in the staging area's spare column block (after the 4 SoA planes)
-  float* d_t = ctx->d_t;
-  if (n > 0) VG_HIP(hipMemcpyAsync(d_t, time, n * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-  VG_HIP(hipStreamSynchronize(ctx->stream));
-  return host_step_deskew(ctx, ctx->d_x, ctx->d_y, ctx->d_z, ctx->d_i, d_t, n, pcl_beg_time, pcl_end_time, imu, m);
+  if (n == 0)
+    return host_step_deskew(ctx, ctx->d_x, ctx->d_y, ctx->d_z, ctx->d_i, ctx->d_t, n, pcl_beg_time, pcl_end_time, imu,
+                            m);
+  float* p[5];
+  int slot = 0;
+  VG_TRY(upload_scan(ctx, xyz, intensity, time, n, p, &slot));
+  return upload_done(ctx, slot,
+                     host_step_deskew(ctx, p[0], p[1], p[2], p[3], p[4], n, pcl_beg_time, pcl_end_time, imu, m));
 }
 
 int vg_get_state(vg_ctx* ctx, double* state) {
