@@ -354,6 +354,7 @@ struct vg_ctx {
     bool live = false;
   } in_slot[2];
   size_t in_cap = 0;  // points per slot
+  void* copy_pool = nullptr;  // helper threads of the pinned copy (vina_gpu.cpp CopyPool)
   int in_next = 0;
   hipEvent_t in_ev = nullptr;  // the current scan's unpack (the split IEKF stream waits for it)
 

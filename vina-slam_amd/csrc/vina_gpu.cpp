@@ -1,12 +1,93 @@
 // vina_gpu.cpp — C-ABI entry points (include/vina_gpu.h) and context lifecycle.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
+#include <mutex>
 #include <cstring>
 #include <new>
 #include <vector>
 #include "vg_internal.h"
 
 using namespace vg;
+
+// The pinned copy of a host-input scan split over the calling thread and a few
+// helper threads (VG_COPY_THREADS, default 4 in all): one core copies ~10 GB/s,
+// and this copy sits before the scan's first kernel. Helpers sleep on a
+// condition variable between scans (no spinning core in a ROS process).
+namespace {
+struct CopyPool {
+  struct Job {
+    char* dst;
+    const char* src;
+    size_t bytes;
+  };
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Job> jobs;
+  std::atomic<int> next{0}, left{0};
+  long gen = 0;
+  bool stop = false;
+  static constexpr size_t kChunk = 128 << 10;
+  explicit CopyPool(int nhelp) {
+    for (int i = 0; i < nhelp; i++) th.emplace_back([this] { loop(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+  void work() {
+    for (int j; (j = next.fetch_add(1)) < (int)jobs.size();) {
+      memcpy(jobs[j].dst, jobs[j].src, jobs[j].bytes);
+      left.fetch_sub(1, std::memory_order_release);
+    }
+  }
+  void loop() {
+    long seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+      }
+      work();
+    }
+  }
+  // copies every (dst, src, bytes) piece; returns when all are done
+  void run(const std::vector<Job>& pieces) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      jobs.clear();
+      for (const Job& p : pieces)
+        for (size_t o = 0; o < p.bytes; o += kChunk)
+          jobs.push_back({p.dst + o, p.src + o, std::min(kChunk, p.bytes - o)});
+      next.store(0);
+      left.store((int)jobs.size());
+      gen++;
+    }
+    if (!th.empty() && jobs.size() > 1) cv.notify_all();
+    work();
+    while (left.load(std::memory_order_acquire) > 0) std::this_thread::yield();
+  }
+};
+}  // namespace
+
+static void pinned_copy(vg_ctx* ctx, const std::vector<CopyPool::Job>& pieces) {
+  if (!ctx->copy_pool) {
+    const char* e = getenv("VG_COPY_THREADS");
+    const int n = std::max(1, std::min(16, e ? atoi(e) : 4));
+    ctx->copy_pool = new CopyPool(n - 1);
+  }
+  static_cast<CopyPool*>(ctx->copy_pool)->run(pieces);
+}
+
 
 static void fill_capacity(vg_capacity& c) {
   if (c.max_points_per_scan <= 0) c.max_points_per_scan = 2000000;
@@ -170,6 +251,7 @@ int vg_destroy(vg_ctx* ctx) {
     if (g) (void)hipGraphExecDestroy(g);
   if (ctx->h_in) (void)hipHostFree(ctx->h_in);
   if (ctx->stream_ds && ctx->stream_ds != ctx->stream) (void)hipStreamSynchronize(ctx->stream_ds);
+  delete static_cast<CopyPool*>(ctx->copy_pool);
   for (auto& sl : ctx->in_slot) {
     if (sl.h) (void)hipHostFree(sl.h);
     if (sl.d) (void)hipFree(sl.d);
@@ -339,15 +421,17 @@ static int upload_scan(vg_ctx* ctx, const float* xyz, const float* inten, const 
   if (sl.live) VG_HIP(hipEventSynchronize(sl.up));
   const size_t nn = (size_t)n;
   size_t nf = 3 * nn;
-  memcpy(sl.h, xyz, nn * 3 * sizeof(float));
+  std::vector<CopyPool::Job> pieces;
+  pieces.push_back({sl.h, (const char*)xyz, nn * 3 * sizeof(float)});
   if (inten) {
-    memcpy(sl.h + nf * sizeof(float), inten, nn * sizeof(float));
+    pieces.push_back({sl.h + nf * sizeof(float), (const char*)inten, nn * sizeof(float)});
     nf += nn;
   }
   if (time) {
-    memcpy(sl.h + nf * sizeof(float), time, nn * sizeof(float));
+    pieces.push_back({sl.h + nf * sizeof(float), (const char*)time, nn * sizeof(float)});
     nf += nn;
   }
+  pinned_copy(ctx, pieces);
   hipStream_t s = ctx->stream_ds;
   if (sl.live) VG_HIP(hipStreamWaitEvent(s, sl.done, 0));
   VG_HIP(hipMemcpyAsync(sl.d, sl.h, nf * sizeof(float), hipMemcpyHostToDevice, s));
