@@ -145,7 +145,12 @@ int vg_step_dev(vg_ctx* ctx, const float* d_x, const float* d_y, const float* d_
                 double pcl_beg_time, double pcl_end_time, const double* imu, int m);
 /* vg_step / vg_step_dev return once the scan is ENQUEUED: the device runs it
  * asynchronously (the host waits only for device-side counts it needs, without
- * draining the stream). Every query below completes the outstanding work first. */
+ * draining the stream). Every query below completes the outstanding work first.
+ * vg_step / vg_step_deskew copy the caller's host arrays into one of two pinned
+ * in-flight slots before returning (the caller may reuse them at once); the
+ * H2D copy and the SoA unpack run on the device ahead of the scan's kernels.
+ * vg_step_dev / vg_step_deskew_dev read the caller's device arrays while the
+ * scan runs: keep them unchanged until a later query (vg_get_state, vg_get_stats, ...) returns. */
 /* SURVEY row f1 — the same scan step with IMUEKF::motion_blur's per-point
  * deskew (imu_ekf.cpp:114-144) on the device first: `time` holds each point's
  * offset from pcl_beg_time in seconds (the reference's `curvature` field),
