@@ -64,3 +64,49 @@ def test_multi_sequences_match_lone_runs(lidar, B):
     mv.close()
     for c in ctxs:
         c.close()
+
+
+def test_host_input_threads_match_lone_runs():
+    """Two contexts fed host buffers through vg_step from two Python threads at
+    once (ctypes releases the GIL): each context's upload slots, pinned-copy
+    helpers and streams are its own, so both reproduce their device-resident
+    lone runs bit for bit."""
+    import threading
+
+    import torch
+    dev = torch.device("cuda", 0)
+    p = vgconfig.load("mid360")
+    g = p["General"]
+    nscan = 14
+    seqs = [synth.Sequence("16line", 21 + b, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
+            for b in range(2)]
+    lone = []
+    for s in seqs:
+        c = _ctx(p, s)
+        for t, n, b, e, imu in _scans(s, nscan, dev, torch):
+            c.step_dev(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), n, b, e, imu)
+        lone.append((c.trajectory(), c.window_states(), c.stats_log()))
+        c.close()
+    ctxs = [_ctx(p, s) for s in seqs]
+    errs = []
+
+    def run(c, s):
+        try:
+            for k in range(nscan):
+                xyz, it, b, e = s.scan(k)
+                c.step(np.ascontiguousarray(xyz, dtype=np.float32), np.ascontiguousarray(it, dtype=np.float32), b, e,
+                       s.imu(k))
+        except Exception as ex:  # surfaced below
+            errs.append(ex)
+
+    th = [threading.Thread(target=run, args=(c, s)) for c, s in zip(ctxs, seqs)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for c, (tr, ws, st) in zip(ctxs, lone):
+        assert np.array_equal(c.trajectory(), tr)
+        assert np.array_equal(c.window_states(), ws)
+        assert [x["n_factors"] for x in c.stats_log()] == [x["n_factors"] for x in st]
+        c.close()

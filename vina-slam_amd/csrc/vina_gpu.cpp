@@ -26,9 +26,11 @@ struct CopyPool {
   std::vector<std::thread> th;
   std::mutex mu;
   std::condition_variable cv;
-  std::vector<Job> jobs;
-  std::atomic<int> next{0}, left{0};
-  long gen = 0;
+  std::vector<Job> jobs;            // rewritten only once every job of the previous run is done
+  std::atomic<uint64_t> claim{0};   // (run << 32) | next job: a claim of a finished run cannot succeed
+  std::atomic<int> left{0};         // jobs of the current run not yet copied
+  uint32_t runs = 0;
+  int njobs = 0;
   bool stop = false;
   static constexpr size_t kChunk = 128 << 10;
   explicit CopyPool(int nhelp) {
@@ -42,38 +44,49 @@ struct CopyPool {
     cv.notify_all();
     for (auto& t : th) t.join();
   }
-  void work() {
-    for (int j; (j = next.fetch_add(1)) < (int)jobs.size();) {
-      memcpy(jobs[j].dst, jobs[j].src, jobs[j].bytes);
+  void work(uint32_t run, int n) {
+    uint64_t v = claim.load(std::memory_order_acquire);
+    for (;;) {
+      if ((uint32_t)(v >> 32) != run || (int)(uint32_t)v >= n) return;
+      if (!claim.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel)) continue;
+      const Job& jb = jobs[(uint32_t)v];
+      memcpy(jb.dst, jb.src, jb.bytes);
       left.fetch_sub(1, std::memory_order_release);
+      v = claim.load(std::memory_order_acquire);
     }
   }
   void loop() {
-    long seen = 0;
+    uint32_t seen = 0;
     for (;;) {
+      uint32_t run;
+      int n;
       {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return stop || gen != seen; });
+        cv.wait(g, [&] { return stop || runs != seen; });
         if (stop) return;
-        seen = gen;
+        seen = run = runs;
+        n = njobs;
       }
-      work();
+      work(run, n);
     }
   }
   // copies every (dst, src, bytes) piece; returns when all are done
   void run(const std::vector<Job>& pieces) {
+    uint32_t r;
+    int n;
     {
       std::lock_guard<std::mutex> g(mu);
       jobs.clear();
       for (const Job& p : pieces)
         for (size_t o = 0; o < p.bytes; o += kChunk)
           jobs.push_back({p.dst + o, p.src + o, std::min(kChunk, p.bytes - o)});
-      next.store(0);
-      left.store((int)jobs.size());
-      gen++;
+      r = ++runs;
+      n = njobs = (int)jobs.size();
+      left.store(n, std::memory_order_relaxed);
+      claim.store((uint64_t)r << 32, std::memory_order_release);
     }
-    if (!th.empty() && jobs.size() > 1) cv.notify_all();
-    work();
+    if (!th.empty() && n > 1) cv.notify_all();
+    work(r, n);
     while (left.load(std::memory_order_acquire) > 0) std::this_thread::yield();
   }
 };
