@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--lidar", default="64line")
     ap.add_argument("--config", default="mid360")
     ap.add_argument("--cpu-warmup", type=int, default=20, help="oracle warm-up scans (BASELINE.md: 20)")
-    ap.add_argument("--cpu-scans", type=int, default=40, help="oracle sample: timed scans after its warm-up")
+    ap.add_argument("--cpu-scans", type=int, default=200,
+                    help="oracle sample: timed scans after its warm-up (BASELINE.md: >= 200)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seq", type=int, default=0)
     ap.add_argument("--stage-scans", type=int, default=8, help="untimed profiled scans for the stage breakdown")
@@ -61,10 +62,30 @@ def parse():
     ap.add_argument("--hash-log2", type=int, default=0, help="context capacity: root hash slots, log2 (0: default)")
     ap.add_argument("--multi", default="2,4,8,16",
                     help="multi-sequence mode (vg_multi_*): B values to time at N=1 (empty: skip); each B runs "
-                         "in a child process of its own, before this one touches the GPU")
+                         "in a child process of its own, before this one touches the GPU; B distinct sequences")
+    ap.add_argument("--multi-1m", default="1,2,4",
+                    help="BASELINE config 5 (synthetic 1M-ray scans, batched): B values of the multi-sequence "
+                         "mode on the 1M workload at N=1 (empty: skip)")
+    ap.add_argument("--multi-1m-steps", type=int, default=10, help="timed scans per sequence of the 1M leg")
     ap.add_argument("--multi-child", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--multi-scans", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--multi-max-points", type=int, default=0, help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+T_START = time.perf_counter()
+
+
+def beat(msg):
+    """One stderr line per bench leg, so that a stalled run names its leg."""
+    print("[bench %7.1fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+
+def under_profiler():
+    """rocprofv3 hands its configuration to the preloaded tool library through
+    ROCPROF_* variables; a fork()ed pool inside such a process can deadlock on
+    the tool's threads, so scans are then generated in-process."""
+    return any(k.startswith("ROCPROF_") for k in os.environ)
 
 
 # ---- synthetic scans, generated before the GPU is touched (a process pool;
@@ -80,7 +101,7 @@ def _gen(job):
 def gen_scans(lidar, seq_id, general, n, workers):
     jobs = [(lidar, seq_id, general["blind"], general["extrinsic_rota"], general["extrinsic_tran"], k)
             for k in range(n)]
-    if workers <= 1 or n <= 2:
+    if workers <= 1 or n <= 2 or under_profiler():
         return [_gen(j) for j in jobs]
     with mproc.get_context("fork").Pool(min(workers, n)) as pool:
         return pool.map(_gen, jobs, chunksize=1)
@@ -92,10 +113,10 @@ CAP = {}  # context capacities (--max-nodes / --max-fix / --hash-log2; 0 = the p
 def main():
     args = parse()
     CAP.update(max_nodes=args.max_nodes, max_fix_points=args.max_fix, hash_log2=args.hash_log2)
-    if args.multi and "GPU_MAX_HW_QUEUES" not in os.environ:
-        # the multi-sequence leg runs one stream per sequence: let HIP map them
-        # to separate hardware queues (HIP's default is 4; read at HIP start-up)
-        os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    # recorded in the line: the headline leg runs with the environment's value
+    # (HIP's default is 4 hardware queues per process); only the multi-sequence
+    # children raise it (multi_children)
+    hwq = os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)")
     import synth
     import vgconfig
 
@@ -116,16 +137,23 @@ def main():
     if world > 1:
         workers = max(1, workers // world)
     seq_id = args.seq + (0 if tile else rank)
+    beat("generating %d %s scans (workers %d%s)" % (n_need, args.lidar, workers,
+                                                   ", in-process: profiler" if under_profiler() else ""))
     host_scans = gen_scans(args.lidar, seq_id, g, n_need, workers)
     tgt_scans = {}
     if world == 1 and args.target_steps > 0 and args.lidar != "128line":
         for cfg in ("mid360", "robosense"):
+            beat("generating the 128-line target scans (%s)" % cfg)
             gg = vgconfig.load(cfg)["General"]
-            tgt_scans[cfg] = gen_scans("128line", args.seq, gg, warmup + args.target_steps, workers)
+            tgt_scans[cfg] = gen_scans("128line", args.seq, gg, warmup + args.target_steps + TARGET_STAGE,
+                                       workers)
 
-    multi = None
+    multi, multi_1m = None, None
     if world == 1 and args.multi:
-        multi = multi_children(args, host_scans[:total], warmup, total)
+        multi = multi_children(args, args.lidar, args.multi, warmup, args.steps, workers,
+                               first=host_scans[:total])
+    if world == 1 and args.multi_1m:
+        multi_1m = multi_children(args, "1M", args.multi_1m, warmup, args.multi_1m_steps, workers)
 
     import torch
     import torch.distributed as dist
@@ -137,8 +165,9 @@ def main():
     dev = torch.device("cuda", local)
     seq = synth.Sequence(args.lidar, seq_id, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
 
+    beat("uploading scans, creating the context")
     scans = []
-    for xyz, inten, b, e, _ in host_scans[: total + args.stage_scans]:
+    for xyz, inten, b, e, _ in host_scans:
         t = torch.from_numpy(np.ascontiguousarray(np.concatenate([xyz.T, inten[None]], 0))).to(dev)
         scans.append((t, xyz.shape[0], b, e))
     imus = [h[4] for h in host_scans]
@@ -163,6 +192,7 @@ def main():
             return
         ctx.step_prepped(prepped[k])
 
+    beat("metric leg: %d warm-up + %d timed scans" % (warmup, args.steps))
     for k in range(warmup):
         run(k)
     # k_ba_solve launch events on every 4th scan's LM run: each event record
@@ -190,6 +220,7 @@ def main():
     stage_ms, stage_prof, stage_stats = {}, {}, []
     extra = min(args.stage_scans, len(scans) - total)
     if extra > 0:
+        beat("per-stage pass: %d scans" % extra)
         ctx.profile(True, stages=True)
         nlog1 = len(ctx.stats_log())
         for k in range(total, total + extra):
@@ -199,6 +230,10 @@ def main():
         stage_stats = ctx.stats_log()[nlog1:]
         stage_ms = {k: round(v["ms"] / extra, 4) for k, v in stage_prof.items() if not k.startswith("host_")}
         ctx.profile(False)
+    # the rest of the CPU baseline's sample, untimed: the ATE is taken over the
+    # same scans as the CPU timing (>= 200 after a 20-scan warm-up)
+    for k in range(total + max(extra, 0), len(scans)):
+        run(k)
     traj_gpu = ctx.trajectory()
     ctx.close()
     host_ms = {k[5:]: round(v["ms"] / args.steps, 4) for k, v in prof.items() if k.startswith("host_")}
@@ -241,17 +276,23 @@ def main():
 
     h2d = None
     if world == 1 and not args.no_h2d:
+        beat("host-input leg")
         h2d = host_input_rate(p, seq, host_scans, imus, warmup, args.steps, dev)
     cpu, ate_cpu = None, None
     if cpu_on:
+        beat("CPU baseline: %d + %d scans, 5 threads then 1" % (args.cpu_warmup, args.cpu_scans))
         cpu, traj_cpu = cpu_baseline(args, p, seq, host_scans)
-        lo, hi = warmup, min(total, traj_cpu.shape[0], traj_gpu.shape[0])
+        lo, hi = args.cpu_warmup, min(traj_cpu.shape[0], traj_gpu.shape[0])
         if hi > lo:
             d = np.linalg.norm(traj_cpu[lo:hi, 10:13] - traj_gpu[lo:hi, 10:13], axis=1)
             ate_cpu = {"ate_m": float("%.3e" % np.sqrt(np.mean(d ** 2))), "max_m": float("%.3e" % d.max()),
-                       "scans": hi - lo, "reference": "CPU restatement, 5 threads, same scans",
+                       "scans": hi - lo, "first_scan": lo,
+                       "reference": "CPU restatement, 5 threads, the CPU baseline's own scans",
                        "tolerance_m": 0.01}
-    targets = {cfg: target_workload(args, cfg, sc, warmup, dev) for cfg, sc in tgt_scans.items()}
+    targets = {}
+    for cfg, sc in tgt_scans.items():
+        beat("128-line target workload (%s)" % cfg)
+        targets[cfg] = target_workload(args, cfg, sc, warmup, dev)
 
     if rank == 0:
         line = {
@@ -269,6 +310,7 @@ def main():
             "roofline": roof, "roofline_k_ba_solve": roof_solve, "roofline_k_iekf": roof_iekf,
             "host_ms_per_scan": host_ms, "host_input": h2d, "cpu_baseline": cpu, "ate_vs_cpu": ate_cpu,
             "target_128line": targets or None, "multi_sequence": multi_roofline(multi, roof),
+            "multi_sequence_1M": multi_1m, "env": {"GPU_MAX_HW_QUEUES": hwq},
         }
         print(json.dumps(line))
     if world > 1:
@@ -314,96 +356,112 @@ def multi_roofline(multi, roof):
     return multi
 
 
-def multi_children(args, host_scans, warmup, total):
-    """The multi-sequence leg, one child process per B, started before this
-    process initialises the GPU: HIP keeps every hardware queue a process has
-    created, and once a process holds more queues than the sequences need,
-    sequences end up sharing queues (measured: the same B = 4 run at 1,100 or
-    3,300 scans/s depending on the streams created before it)."""
+def multi_children(args, lidar, Bs, warmup, steps, workers, first=None):
+    """A multi-sequence leg (vg_multi_*), one child process per B, started
+    before this process initialises the GPU: HIP keeps every hardware queue a
+    process has created, and once a process holds more queues than the
+    sequences need, sequences end up sharing queues (measured: the same B = 4
+    run at 1,100 or 3,300 scans/s depending on the streams created before it).
+    Every context runs a distinct synthetic sequence (seed args.seq + b; no two
+    contexts read the same scan). GPU_MAX_HW_QUEUES=16 is set for the children
+    only, one hardware queue per sequence stream."""
     import subprocess
     import tempfile
-    fd, path = tempfile.mkstemp(suffix=".npz", prefix="vg_multi_")
-    os.close(fd)
-    arrs = {}
-    for k, (xyz, inten, b, e, imu) in enumerate(host_scans):
-        arrs["x%d" % k], arrs["i%d" % k], arrs["m%d" % k] = xyz, inten, imu
-        arrs["t%d" % k] = np.array([b, e])
-    np.savez(path, **arrs)
-    out = {"unit": "scans/s", "steps": total - warmup, "workers": "one native thread + one stream per sequence",
-           "wait_policy": "spin", "process": "one per B, fresh HIP runtime", "by_B": {}}
+
+    import vgconfig
+    g = vgconfig.load(args.config)["General"]
+    Bs = [int(b) for b in Bs.split(",")]
+    total = warmup + steps
+    paths = []
+    out = {"lidar": lidar, "unit": "scans/s", "steps": steps, "warmup": warmup,
+           "workers": "one native thread + one stream per sequence", "inputs": "B distinct sequences",
+           "wait_policy": "spin", "process": "one per B, fresh HIP runtime", "env": {"GPU_MAX_HW_QUEUES": "16"},
+           "by_B": {}}
+    npmax = 0
     try:
-        for B in [int(b) for b in args.multi.split(",")]:
-            cmd = [sys.executable, os.path.abspath(__file__), "--multi-child", str(B), "--multi-scans", path,
-                   "--lidar", args.lidar, "--config", args.config, "--seq", str(args.seq), "--steps", str(args.steps),
-                   "--warmup", str(args.warmup), "--max-nodes", str(args.max_nodes), "--max-fix", str(args.max_fix),
+        for b in range(max(Bs)):
+            beat("multi-sequence %s: generating sequence %d of %d" % (lidar, b + 1, max(Bs)))
+            sc = first if (b == 0 and first is not None) else gen_scans(lidar, args.seq + b, g, total, workers)
+            fd, path = tempfile.mkstemp(suffix=".npz", prefix="vg_multi_")
+            os.close(fd)
+            arrs = {}
+            for k, (xyz, inten, tb, te, imu) in enumerate(sc[:total]):
+                arrs["x%d" % k], arrs["i%d" % k], arrs["m%d" % k] = xyz, inten, imu
+                arrs["t%d" % k] = np.array([tb, te])
+                npmax = max(npmax, xyz.shape[0])
+            np.savez(path, **arrs)
+            paths.append(path)
+            del sc, arrs
+        env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+        for B in Bs:
+            beat("multi-sequence %s: B = %d" % (lidar, B))
+            cmd = [sys.executable, os.path.abspath(__file__), "--multi-child", str(B),
+                   "--multi-scans", ",".join(paths[:B]), "--multi-max-points", str(npmax + 16),
+                   "--lidar", lidar, "--config", args.config, "--steps", str(steps), "--warmup", str(args.warmup),
+                   "--max-nodes", str(args.max_nodes), "--max-fix", str(args.max_fix),
                    "--hash-log2", str(args.hash_log2)]
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
             if r.returncode != 0:
                 raise RuntimeError("multi-sequence child B=%d failed (%d): %s" % (B, r.returncode, r.stderr[-2000:]))
-            out["by_B"][str(B)] = json.loads(r.stdout.strip().splitlines()[-1])["scans_per_s"]
+            res = json.loads(r.stdout.strip().splitlines()[-1])
+            out["by_B"][str(B)] = res["scans_per_s"]
+            out.setdefault("points_per_scan", res["points_per_scan"])
     finally:
-        os.unlink(path)
+        for path in paths:
+            os.unlink(path)
     return out
 
 
 def multi_child(args, p, g, warmup, total):
-    import torch
-
-    import synth
-    z = np.load(args.multi_scans)
-    dev = torch.device("cuda", 0)
-    seq = synth.Sequence(args.lidar, args.seq, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
-    scans, imus = [], []
-    for k in range(total):
-        xyz, inten = z["x%d" % k], z["i%d" % k]
-        t = torch.from_numpy(np.ascontiguousarray(np.concatenate([xyz.T, inten[None]], 0))).to(dev)
-        b, e = z["t%d" % k]
-        scans.append((t, xyz.shape[0], float(b), float(e)))
-        imus.append(z["m%d" % k])
-    r = multi_sequence(p, seq, scans, imus, warmup, total, dev, [args.multi_child])
-    print(json.dumps({"B": args.multi_child, "scans_per_s": r["by_B"][str(args.multi_child)]}))
-    return 0
-
-
-def multi_sequence(p, seq, scans, imus, warmup, total, dev, Bs):
-    """Multi-sequence mode (BASELINE config 5, vg_multi_*): B contexts on one
-    GPU, one native worker thread each, every context fed the same resident
-    scans (the throughput does not depend on the seed; tests/test_multi_gpu.py
-    checks distinct sequences bit for bit against lone runs). Whole-job
+    """One B of a multi-sequence leg: B contexts on one GPU, one native worker
+    thread each, context b stepping its own sequence's resident scans; whole-job
     scans/s over the timed scans after the warm-up."""
     import torch
 
+    import synth
     import vgconfig
     import vgpu
-    out = {"unit": "scans/s", "steps": total - warmup, "workers": "one native thread + one stream per sequence",
-           "wait_policy": "spin", "by_B": {}}
-    npmax = max(s[1] for s in scans) + 16
-    for B in Bs:
-        ctxs = [vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=npmax, **CAP) for _ in range(B)]
-        for c in ctxs:
-            c.seed(seq.gt_state(0))
-        mv = vgpu.Multi(ctxs, 0, 0)
+    B = args.multi_child
+    dev = torch.device("cuda", 0)
+    data = []
+    for path in args.multi_scans.split(",")[:B]:
+        z = np.load(path)
+        sc = []
+        for k in range(total):
+            xyz, inten = z["x%d" % k], z["i%d" % k]
+            t = torch.from_numpy(np.ascontiguousarray(np.concatenate([xyz.T, inten[None]], 0))).to(dev)
+            tb, te = z["t%d" % k]
+            sc.append((t, xyz.shape[0], float(tb), float(te), z["m%d" % k]))
+        data.append(sc)
+    seq = synth.Sequence(args.lidar, 0, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
+    ctxs = [vgpu.Context(vgconfig.to_c(p), device=0, max_points=args.multi_max_points, **CAP) for _ in range(B)]
+    for c in ctxs:
+        c.seed(seq.gt_state(0))  # every synthetic sequence follows the same trajectory (synth.Trajectory)
+    mv = vgpu.Multi(ctxs, 0, 0)
 
-        def step(k):
-            t, n, b, e = scans[k]
-            mv.step_dev([(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), 0, n, b, e,
-                          imus[k])] * B)
+    def step(k):
+        scans = []
+        for d in data:
+            t, n, tb, te, imu = d[k]
+            scans.append((t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), 0, n, tb, te, imu))
+        mv.step_dev(scans)
 
-        for k in range(warmup):
-            step(k)
-        mv.sync()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for k in range(warmup, total):
-            step(k)
-        mv.sync()
-        torch.cuda.synchronize(dev)
-        dt = time.perf_counter() - t0
-        out["by_B"][str(B)] = round(B * (total - warmup) / dt, 1)
-        mv.close()
-        for c in ctxs:
-            c.close()
-    return out
+    for k in range(warmup):
+        step(k)
+    mv.sync()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(warmup, total):
+        step(k)
+    mv.sync()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    mv.close()
+    for c in ctxs:
+        c.close()
+    npts = int(np.mean([d[k][1] for d in data for k in range(warmup, total)]))
+    print(json.dumps({"B": B, "scans_per_s": round(B * (total - warmup) / dt, 1), "points_per_scan": npts}))
+    return 0
 
 
 def host_input_rate(p, seq, host_scans, imus, warmup, steps, dev):
@@ -435,10 +493,15 @@ def host_input_rate(p, seq, host_scans, imus, warmup, steps, dev):
                     "in-flight slot, DMA to HBM and AoS->SoA unpack on the device ahead of the scan's kernels"}
 
 
+TARGET_STAGE = 4  # per-stage scans after the target workload's timed ones (P_k for its roofline)
+
+
 def target_workload(args, cfg, host, warm, dev):
     """The north star's target workload (synthetic 128-line clouds, 200,064
     rays) on one GPU, same pipeline and protocol as the metric, fewer scans:
-    reported beside the metric, never as `value`."""
+    reported beside the metric, never as `value`. Its whole-scan roofline uses
+    the same SURVEY 8(d) byte model (scan_roofline) with this workload's own
+    counters; P_k comes from TARGET_STAGE untimed per-stage scans after it."""
     import torch
 
     import synth
@@ -446,8 +509,9 @@ def target_workload(args, cfg, host, warm, dev):
     import vgpu
     p = vgconfig.load(cfg)
     g = p["General"]
+    W = p["LocalBA"]["win_size"]
     seq = synth.Sequence("128line", args.seq, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
-    steps = len(host) - warm
+    steps = len(host) - warm - TARGET_STAGE
     scans = []
     for xyz, inten, b, e, _ in host:
         t = torch.from_numpy(np.ascontiguousarray(np.concatenate([xyz.T, inten[None]], 0))).to(dev)
@@ -468,13 +532,22 @@ def target_workload(args, cfg, host, warm, dev):
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     st = ctx.stats_log()[warm:]
+    ctx.profile(True, stages=True)
+    for k in range(warm + steps, len(scans)):
+        run(k)
+    torch.cuda.synchronize(dev)
+    stage_st = ctx.stats_log()[warm + steps:]
+    ctx.profile(False)
     ctx.close()
+    roof = scan_roofline(st, stage_st, W, dt / steps)
     return {"workload": "synthetic-128line@%s.yaml" % cfg, "value": round(steps / dt, 3), "unit": "scans/s",
             "ms_per_step": round(dt * 1e3 / steps, 4), "steps": steps, "warmup": warm, "rays_per_scan": 200064,
-            "points_per_scan": int(np.mean([s[1] for s in scans[warm:]])),
+            "points_per_scan": int(np.mean([s[1] for s in scans[warm:warm + steps]])),
             "downsampled_per_scan": int(np.mean([x["n_ds"] for x in st])) if st else None,
             "factors_per_scan": int(np.mean([x["n_factors"] for x in st])) if st else None,
-            "lm": bool(p["General"]["if_BA"])}
+            "lm": bool(p["General"]["if_BA"]),
+            "bytes_per_scan": roof["bytes_per_scan"], "achieved": roof["achieved"], "peak": roof["peak"],
+            "unit_roofline": roof["unit"], "frac": roof["frac"], "counters_mean": roof["counters_mean"]}
 
 
 def pmc_traffic():

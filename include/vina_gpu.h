@@ -264,10 +264,41 @@ int vg_multi_margi(vg_ctx* ctx);
 int vg_step_end(vg_ctx* ctx);
 int vg_win_count(vg_ctx* ctx, int* n);
 
-/* Per-scan poses published after the IEKF (pub_localtraj / save_pose_tum,
- * local_mapping.cpp:427-430): n rows of 13 doubles [t, R row-major 9, p 3].
- * Copies min(n, cap) rows; *n = total rows. out may be NULL to query. */
+/* The TUM pose file's rows (FileReaderWriter::save_pose_tum, io.cpp:67-77,
+ * called at local_mapping.cpp:430): the pose right after the IEKF of every
+ * steady-state scan — none for the initialisation's scans (cold start).
+ * n rows of 13 doubles [t, R row-major 9, p 3]. Copies min(n, cap) rows;
+ * *n = total rows. out may be NULL to query. Completes outstanding work. */
 int vg_trajectory(vg_ctx* ctx, double* out, int cap, int* n);
+
+/* pub_localtraj / pub_localmap's path (pcl_path, publishers.cpp:65-131): one
+ * row per pub_localtraj call (every stepped scan, the initialisation's
+ * included, node.cpp:325 / local_mapping.cpp:427), n rows of 14 doubles
+ * [t, R row-major 9, p 3, jour]. After every window BA pub_localmap re-writes
+ * the positions of the window's rows with the refined x_buf[i].p
+ * (publishers.cpp:121-129, local_mapping.cpp:505); system_reset clears it
+ * (node.cpp:403). Completes outstanding work. */
+int vg_path(vg_ctx* ctx, double* out, int cap, int* n);
+
+/* Non-blocking: absorb every enqueued scan whose device results are already
+ * published (no stream drain, no wait), then report how many scans are
+ * complete and how many rows vg_poll_rows can copy. A node publishes from
+ * here instead of draining after every scan. Any out-pointer may be NULL. */
+int vg_poll(vg_ctx* ctx, int* n_scans, int* n_traj, int* n_path);
+/* The rows absorbed so far (after vg_poll; no wait): TUM rows from row
+ * traj_from on (at most traj_cap), and the first path_cap path rows. */
+int vg_poll_rows(vg_ctx* ctx, double* traj, int traj_from, int traj_cap, double* path, int path_cap);
+
+/* /map_cmap (pub_localmap, publishers.cpp:102-119,130): every third point of
+ * the oldest window frame's downsampled cloud at that frame's pose after the
+ * BA, x y z intensity per point, computed on the device after each window BA
+ * while enabled (vg_set_publish bit 0; off by default: no cost to the scan).
+ * Points follow the device's downsample order (first occurrence, DESIGN.md
+ * section 3), so "every third" selects from that order. Completes outstanding
+ * work; *n = points of the last window BA (0 if none ran while enabled). */
+int vg_local_map(vg_ctx* ctx, float* out_xyzi, int cap, int* n);
+/* Optional per-scan outputs: bit 0 = the /map_cmap cloud (vg_local_map). */
+int vg_set_publish(vg_ctx* ctx, int flags);
 
 /* ---- Spatial-tile sharding (north_star: the voxel map shards by spatial tile
  * across the GPUs of one node, with an all-reduce of the normal equations).
@@ -318,7 +349,12 @@ int vg_set_wait_policy(vg_ctx* ctx, int spin_us, int sleep_us);
  * until vg_multi_sync, the IMU samples are copied) and returns — it blocks
  * only when a sequence has 4 scans queued; the workers run free, in order per
  * sequence. vg_multi_sync completes every queued scan. Each sequence's
- * results are exactly those of a lone context. */
+ * results are exactly those of a lone context. vg_multi_step_dev queues all B
+ * scans or none: after a worker's error it returns that status without
+ * queuing (call vg_multi_sync before reading vg_last_error of the contexts).
+ * With B > 1 the contexts run on one stream each while the multi object
+ * exists; vg_multi_destroy gives each back its own downsample stream and the
+ * IEKF / margi overlap. */
 typedef struct vg_scan_dev {
   const float *d_x, *d_y, *d_z, *d_intensity, *d_time;
   int n;

@@ -8,7 +8,14 @@
 //   ResultOutput::pub_localtraj (publishers.cpp:65-97): the pose after the IEKF
 //     (the TF camera_init -> aft_mapped, pub_odom_func 42-63), the path point
 //     and the scan moved to the world (/map_scan) -> path() / scan_world();
-//   FileReaderWriter::save_pose_tum (io.cpp:67-77) -> tum_line / write_tum.
+//   ResultOutput::pub_localmap (publishers.cpp:99-131, local_mapping.cpp:505):
+//     the path's window rows re-written with the BA-refined positions (in
+//     path()) and the /map_cmap cloud -> local_map();
+//   FileReaderWriter::save_pose_tum (io.cpp:67-77) -> tum_rows() / tum_line /
+//     write_tum (steady-state scans only, as the reference's file).
+// Outputs are refreshed without draining the device pipeline (vg_poll): a
+// scan's rows appear once its results are published; scan_world(),
+// local_map() and write_tum() complete outstanding work first.
 // A ROS 2 wrapper (vina-slam_amd/ros2/vina_node.cpp, built when rclcpp is
 // found) only converts messages to these calls and these outputs to messages.
 #pragma once
@@ -26,6 +33,7 @@ struct PoseStamped {
   double R[9];  // row-major
   double p[3];
   double q[4];  // x, y, z, w
+  double jour = 0;  // path points only: the journey (the PointType's curvature, publishers.cpp:88-92)
 };
 
 // Eigen::Quaterniond(const Matrix3d&): the trace branch, else the largest
@@ -124,23 +132,54 @@ class NodeCore {
       scans_.erase(it);
       stepped++;
     }
-    if (stepped) refresh_path();
+    poll();
     return stepped;
   }
 
-  // pub_localtraj's path (pcl_path) and the TUM rows: one pose per scan after
-  // its IEKF, from the first scan past the initialisation
+  // Non-blocking refresh of the outputs from every scan whose results the
+  // device has published (vg_poll); returns true when something changed.
+  bool poll() {
+    int ns = 0, nt = 0, np = 0;
+    check(vg_poll(lio_.raw(), &ns, &nt, &np), "vg_poll");
+    return take_rows(ns, nt, np);
+  }
+  // Blocking: complete every enqueued scan, then refresh (end of a run).
+  void finish() {
+    int nt = 0;
+    check(vg_trajectory(lio_.raw(), nullptr, 0, &nt), "vg_trajectory");  // completes outstanding work
+    poll();
+  }
+
+  // save_pose_tum's rows: the pose after the IEKF of every steady-state scan
+  const std::vector<PoseStamped>& tum_rows() const { return tum_; }
+  // pcl_path (pub_localtraj's points, the initialisation's scans included,
+  // cleared by system_reset, the window's positions re-written by
+  // pub_localmap after each BA); R is the pose's rotation after its IEKF
   const std::vector<PoseStamped>& path() const { return path_; }
+
+  // /map_cmap (pub_localmap): switch the device-side cloud on (from the next
+  // window BA on) and read the last one: x y z intensity per point
+  void enable_local_map(bool on) { check(vg_set_publish(lio_.raw(), on ? 1 : 0), "vg_set_publish"); }
+  std::vector<float> local_map() {
+    int n = 0;
+    check(vg_local_map(lio_.raw(), nullptr, 0, &n), "vg_local_map");
+    std::vector<float> out((size_t)4 * n);
+    if (n > 0) check(vg_local_map(lio_.raw(), out.data(), n, &n), "vg_local_map");
+    return out;
+  }
 
   // the last scan's downsampled points in the world (pwld of pvec_update,
   // local_mapping.cpp:425-427): R (ext_R q + ext_t) + p at the scan's pose
   std::vector<float> scan_world() {
+    finish();
     int n = 0;
     check(vg_scan_points(lio_.raw(), nullptr, 0, &n), "vg_scan_points");
     std::vector<float> body((size_t)3 * n), out;
     if (n == 0 || path_.empty()) return out;
     check(vg_scan_points(lio_.raw(), body.data(), n, &n), "vg_scan_points");
-    const PoseStamped& s = path_.back();
+    // the pose pvec_update used: right after the IEKF (the TUM row; a path
+    // row's position may since have been re-written by pub_localmap)
+    const PoseStamped& s = (!tum_.empty() && tum_.back().t == path_.back().t) ? tum_.back() : path_.back();
     const double* E = cfg_.ext_R;
     out.resize((size_t)3 * n);
     for (int i = 0; i < n; i++) {
@@ -153,10 +192,11 @@ class NodeCore {
     return out;
   }
 
-  bool write_tum(const std::string& file) const {
+  bool write_tum(const std::string& file) {
+    finish();
     FILE* f = fopen(file.c_str(), "w");
     if (!f) return false;
-    for (const PoseStamped& s : path_) fputs(tum_line(s).c_str(), f);
+    for (const PoseStamped& s : tum_) fputs(tum_line(s).c_str(), f);
     return fclose(f) == 0;
   }
 
@@ -175,21 +215,30 @@ class NodeCore {
   void check(int r, const char* what) {
     if (r != VG_OK) throw Error(r, std::string(what) + ": " + vg_last_error(lio_.raw()));
   }
-  void refresh_path() {
-    int n = 0;
-    check(vg_trajectory(lio_.raw(), nullptr, 0, &n), "vg_trajectory");
-    if (n <= (int)path_.size()) return;
-    std::vector<double> rows((size_t)13 * n);
-    check(vg_trajectory(lio_.raw(), rows.data(), n, &n), "vg_trajectory");
-    for (int i = (int)path_.size(); i < n; i++) {
-      PoseStamped s;
-      const double* r = &rows[(size_t)13 * i];
-      s.t = r[0];
-      for (int k = 0; k < 9; k++) s.R[k] = r[1 + k];
-      for (int k = 0; k < 3; k++) s.p[k] = r[10 + k];
-      quat_from_R(s.R, s.q);
-      path_.push_back(s);
+  static PoseStamped row_pose(const double* r) {
+    PoseStamped s;
+    s.t = r[0];
+    for (int k = 0; k < 9; k++) s.R[k] = r[1 + k];
+    for (int k = 0; k < 3; k++) s.p[k] = r[10 + k];
+    quat_from_R(s.R, s.q);
+    return s;
+  }
+  // TUM rows only grow; the path is re-read whenever more scans completed
+  // (its window rows change after every BA, and a system_reset clears it)
+  bool take_rows(int ns, int nt, int np) {
+    if (ns == scans_done_ && nt == (int)tum_.size()) return false;
+    scans_done_ = ns;
+    const int nt_new = nt - (int)tum_.size();
+    std::vector<double> t((size_t)13 * (nt_new > 0 ? nt_new : 0)), pth((size_t)14 * np);
+    check(vg_poll_rows(lio_.raw(), t.data(), (int)tum_.size(), nt_new > 0 ? nt_new : 0, pth.data(), np),
+          "vg_poll_rows");
+    for (int i = 0; i < nt_new; i++) tum_.push_back(row_pose(&t[(size_t)13 * i]));
+    path_.resize(np);
+    for (int i = 0; i < np; i++) {
+      path_[i] = row_pose(&pth[(size_t)14 * i]);
+      path_[i].jour = pth[(size_t)14 * i + 13];
     }
+    return true;
   }
 
   vg_config cfg_;
@@ -198,7 +247,8 @@ class NodeCore {
   vg_sync* sync_ = nullptr;
   std::map<int, Scan> scans_;
   int next_id_ = 0;
-  std::vector<PoseStamped> path_;
+  int scans_done_ = 0;
+  std::vector<PoseStamped> tum_, path_;
 };
 
 }  // namespace vina_gpu

@@ -68,6 +68,9 @@ def lib():
         L.orc_deskew_only.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int]
         L.orc_traj_len.argtypes = [P]
         L.orc_get_traj.argtypes = [P, dp]
+        L.orc_path_len.argtypes = [P]
+        L.orc_get_path.argtypes = [P, dp]
+        L.orc_local_map.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
         L.orc_window_states.argtypes = [P, dp]
         L.orc_capture_arm.argtypes = [P]
         L.orc_kat_p2p.argtypes = [dp] * 7
@@ -278,9 +281,24 @@ class Pipeline:
         return {k: (list(getattr(s, k)) if k == "iekf_matches" else getattr(s, k)) for k, _ in Stats._fields_}
 
     def trajectory(self):
+        """save_pose_tum rows (steady-state scans): t, R(9), p(3)."""
         n = lib().orc_traj_len(self.h)
         out = np.zeros((n, 13))
         lib().orc_get_traj(self.h, _d(out))
+        return out
+
+    def path(self):
+        """pcl_path rows (pub_localtraj, re-written by pub_localmap): t, R(9), p(3), jour."""
+        n = lib().orc_path_len(self.h)
+        out = np.zeros((n, 14))
+        lib().orc_get_path(self.h, _d(out))
+        return out
+
+    def local_map(self, all_points=False):
+        """/map_cmap of the last window BA (x, y, z, intensity); all_points: every point of pvec_buf[0]."""
+        n = lib().orc_local_map(self.h, 1 if all_points else 0, None, 0)
+        out = np.zeros((n, 4), dtype=np.float32)
+        lib().orc_local_map(self.h, 1 if all_points else 0, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n)
         return out
 
     def window_states(self):

@@ -504,6 +504,7 @@ struct Pipeline {
     }
     x_curr.R = x_buf[win_count - 1].R;
     x_curr.p = x_buf[win_count - 1].p;
+    pub_localmap();
     *t5 = clk::now();
     mpar.cnt_plane_update = 0;
     mpar.cnt_fix_full = 0;
@@ -600,6 +601,7 @@ struct Pipeline {
     auto t2 = clk::now();
     pwld.clear();
     pvec_update(*pptr, x_curr, pwld);
+    path_push(jour);
     traj_push();
     win_count++;
     x_buf.push_back(x_curr);
@@ -636,11 +638,45 @@ struct Pipeline {
     return 0;
   }
 
-  std::vector<double> traj;  // per scan: t, R(9), p(3)
+  // save_pose_tum (io.cpp:67-77, local_mapping.cpp:430): steady-state scans
+  // only, per row t, R(9), p(3)
+  std::vector<double> traj;
   void traj_push() {
     traj.push_back(x_curr.t);
     for (int i = 0; i < 9; i++) traj.push_back(x_curr.R[i]);
     for (int i = 0; i < 3; i++) traj.push_back(x_curr.p[i]);
+  }
+  // pcl_path of pub_localtraj (publishers.cpp:65-97): per row t, R(9), p(3),
+  // jour (the path point's curvature); the initialisation's scans included
+  // (node.cpp:325, jour 0), cleared by system_reset (node.cpp:403)
+  std::vector<double> path;
+  void path_push(double j) {
+    path.push_back(x_curr.t);
+    for (int i = 0; i < 9; i++) path.push_back(x_curr.R[i]);
+    for (int i = 0; i < 3; i++) path.push_back(x_curr.p[i]);
+    path.push_back(j);
+  }
+  // pub_localmap (publishers.cpp:99-131, local_mapping.cpp:505, mgsize = 1):
+  // /map_cmap = every third point of pvec_buf[0] at x_buf[0]; the path rows
+  // [win_base, win_base + win_count) take x_buf[i].p. cmap_all keeps every
+  // point of pvec_buf[0] (the test compares sets: the device's point order
+  // differs)
+  std::vector<float> cmap, cmap_all;
+  void pub_localmap() {
+    cmap.clear();
+    cmap_all.clear();
+    const PVec& pv0 = *pvec_buf[0];
+    for (size_t j = 0; j < pv0.size(); j++) {
+      const V3 w = x_buf[0].R * pv0[j].pnt + x_buf[0].p;
+      const float f[4] = {(float)w[0], (float)w[1], (float)w[2], pv0[j].intensity};
+      cmap_all.insert(cmap_all.end(), f, f + 4);
+      if (j % 3 == 0) cmap.insert(cmap.end(), f, f + 4);
+    }
+    for (int i = 0; i < win_count; i++) {
+      const size_t r = (size_t)(i + win_base) * 14;
+      if (r + 14 > path.size()) break;
+      for (int k = 0; k < 3; k++) path[r + 10 + k] = x_buf[i].p[k];
+    }
   }
 };
 
@@ -859,6 +895,17 @@ void orc_shard(void* h, int rank, int world, int (*fn)(double*, int, void*), voi
   P->mpar.ar_user = user;
 }
 int orc_traj_len(void* h) { return (int)((Pipeline*)h)->traj.size() / 13; }
+int orc_path_len(void* h) { return (int)((Pipeline*)h)->path.size() / 14; }
+void orc_get_path(void* h, double* out) {
+  Pipeline* p = (Pipeline*)h;
+  memcpy(out, p->path.data(), p->path.size() * sizeof(double));
+}
+int orc_local_map(void* h, int all, float* out, int cap) {
+  const std::vector<float>& c = all ? ((Pipeline*)h)->cmap_all : ((Pipeline*)h)->cmap;
+  const int n = (int)c.size() / 4;
+  if (out) memcpy(out, c.data(), (size_t)(n < cap ? n : cap) * 4 * sizeof(float));
+  return n;
+}
 void orc_get_traj(void* h, double* out) {
   Pipeline* p = (Pipeline*)h;
   memcpy(out, p->traj.data(), p->traj.size() * sizeof(double));

@@ -77,6 +77,9 @@ int orc_deskew_only(void* h, float* xyz, const float* times, int n, double beg, 
 void orc_shard(void* h, int rank, int world, int (*fn)(double* buf, int n, void* user), void* user);
 int orc_traj_len(void* h);
 void orc_get_traj(void* h, double* out);
+int orc_path_len(void* h);
+void orc_get_path(void* h, double* out);
+int orc_local_map(void* h, int all, float* out, int cap);
 int orc_window_states(void* h, double* out);
 /* test hook: the next LM run's first divide_thread pass (optimizers.cpp:181-245)
  * as [6W x 6W LiDAR Hessian summed over the factors (row-major), 6W gradient,

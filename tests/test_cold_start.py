@@ -107,8 +107,9 @@ def _run_oracle(cfg="mid360", lidar="16line", nscan=16, scale=1.0, imu_in_g=Fals
         stats.append(orc.stats())
         states.append(orc.state())
     traj = orc.trajectory()
+    path = orc.path()
     orc.close()
-    return seq, stats, states, traj
+    return seq, stats, states, (traj, path)
 
 
 def test_cold_start_oracle_phases_and_motion(oracle_lib):
@@ -129,15 +130,19 @@ def test_cold_start_oracle_phases_and_motion(oracle_lib):
     # gravity along z (align_gravity, then one more gravity-LM round moves it slightly)
     gvec = states[-1][22:25]
     assert np.linalg.norm(gvec[:2]) < 0.01 * gn
-    # the trajectory's relative motion follows the ground truth (frames differ by a rigid transform)
+    # the TUM file holds the steady-state scans only (save_pose_tum, local_mapping.cpp:430); the path
+    # (pcl_path) every scan from the first window scan on, the last window's rows BA-refined
+    traj, path = traj
     ks = list(range(n1 + 1, 17))
-    assert traj.shape[0] == len(ks)
+    assert traj.shape[0] == phases.count(0) and path.shape[0] == len(ks)
+    assert np.array_equal(traj[:, 0], path[-traj.shape[0]:, 0])
+    # the path's relative motion follows the ground truth (frames differ by a rigid transform)
     gt = np.array([seq.gt_pose(k)[1] for k in ks])
-    est = traj[:, 10:13]
+    est = path[:, 10:13]
     d_gt = np.linalg.norm(np.diff(gt, axis=0), axis=1)
     d_est = np.linalg.norm(np.diff(est, axis=0), axis=1)
     err = np.abs(d_gt - d_est)
-    assert err.max() < 0.1, err  # init-window rows: kd-tree LIO poses before any BA
+    assert err.max() < 0.1, err  # init-window rows: kd-tree LIO poses, then re-written by pub_localmap
     assert err[W - 1:].max() < 0.01, err  # from the motion_init scan on
 
 
@@ -223,8 +228,13 @@ def test_cold_start_matches_oracle(oracle_lib, cfg, lidar, nscan, scale, in_g):
         assert np.abs(xo[22:25] - xg[22:25]).max() < 1e-9, k
         phases.append(so["init_phase"])
     to, tg = orc.trajectory(), gpu.trajectory()
-    assert to.shape == tg.shape
-    assert np.abs(to[:, 1:] - tg[:, 1:]).max() < 1e-9
+    assert to.shape == tg.shape and to.shape[0] == phases.count(0)  # TUM rows: steady-state scans only
+    if to.shape[0]:
+        assert np.array_equal(to[:, 0], tg[:, 0]) and np.abs(to[:, 1:] - tg[:, 1:]).max() < 1e-9
+    # pcl_path: the init scans since the last system_reset (node.cpp:403), then BA re-writes
+    po, pg = orc.path(), gpu.path()
+    assert po.shape == pg.shape and np.array_equal(po[:, 0], pg[:, 0])
+    assert np.abs(po[:, 1:13] - pg[:, 1:13]).max() < 1e-9 and np.array_equal(po[:, 13], pg[:, 13])
     assert (4 in phases) == (scale != 1.0) and (3 in phases) == (scale == 1.0)
     gpu.close()
     orc.close()

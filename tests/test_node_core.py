@@ -116,7 +116,7 @@ def _write_log(path, cfg, fmt, seed, events):
         f.write(struct.pack("<i", -1))
 
 
-def _oracle_tum(p, fmt, seed, events):
+def _oracle_tum(p, fmt, seed, events, extra=None):
     """The same events through the CPU restatement: decode at arrival, the
     Python statement of sync_packages (tests/test_decode.py), one deskewing
     step per package."""
@@ -138,6 +138,8 @@ def _oracle_tum(p, fmt, seed, events):
     for sid, beg, end, imu in pk:
         d = dec[sid]
         orc.step_deskew(d[:, :3].copy(), d[:, 3].copy(), d[:, 4].copy(), beg, end, imu)
+    if extra is not None:
+        extra.update(path=orc.path(), cmap=orc.local_map(), cmap_all=orc.local_map(all_points=True))
     return orc.trajectory(), len(pk)
 
 
@@ -152,13 +154,16 @@ def test_node_core_event_log_matches_oracle(oracle_lib, tmp_path):
     fmt = _fmt(g["blind"])
     seed = seq.gt_state(0)
     log, tum = tmp_path / "ev.bin", tmp_path / "out.tum"
+    pth, cmap = tmp_path / "path.txt", tmp_path / "cmap.bin"
     _write_log(log, vgconfig.to_c(p), fmt, seed, events)
     exe = os.path.join(REPO, "vina-slam_amd", "bin", "vg_node_replay")
-    r = subprocess.run([exe, str(log), str(tum)], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, str(log), str(tum), "0", str(pth), str(cmap)], capture_output=True, text=True,
+                       timeout=120)
     assert r.returncode == 0, r.stderr
     print(r.stdout.strip())
     rows = np.array([[float(x) for x in ln.split()] for ln in tum.read_text().splitlines()])
-    ref, npk = _oracle_tum(p, fmt, seed, events)
+    extra = {}
+    ref, npk = _oracle_tum(p, fmt, seed, events, extra)
     assert npk >= 14 and rows.shape == (ref.shape[0], 8), (rows.shape, ref.shape, npk)
     assert np.array_equal(rows[:, 0], [float("%.9f" % t) for t in ref[:, 0]])
     err = np.linalg.norm(rows[:, 1:4] - ref[:, 10:13], axis=1)
@@ -167,3 +172,24 @@ def test_node_core_event_log_matches_oracle(oracle_lib, tmp_path):
     import json
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     assert summary["stepped"] == npk and summary["last_scan_world_points"] > 1000
+    check_path_and_cmap(np.loadtxt(pth), np.fromfile(cmap, dtype=np.float32).reshape(-1, 4), extra, 1e-8)
+
+
+def check_path_and_cmap(path, cmap, ref, tol):
+    """pub_localmap's outputs against the oracle's (publishers.cpp:99-131):
+    the path rows (t exact, positions — BA re-writes included — within tol,
+    jour), and the /map_cmap cloud: the same size ceil(n / 3), every device
+    point one of the oracle's pvec_buf[0] points at x_buf[0] (the device takes
+    every third point in its own downsample order)."""
+    rp = ref["path"]
+    assert path.shape[0] == rp.shape[0], (path.shape, rp.shape)
+    assert np.array_equal(np.round(path[:, 0], 9), np.round(rp[:, 0], 9))
+    assert np.abs(path[:, 1:4] - rp[:, 10:13]).max() < tol
+    assert np.abs(path[:, 4] - rp[:, 13]).max() < 1e-6
+    allp = ref["cmap_all"]
+    assert cmap.shape == ref["cmap"].shape and cmap.shape[0] == (allp.shape[0] + 2) // 3 > 100
+    from scipy.spatial import cKDTree
+    d, j = cKDTree(allp[:, :3].astype(np.float64)).query(cmap[:, :3].astype(np.float64))
+    assert d.max() < 1e-4, d.max()
+    assert np.array_equal(cmap[:, 3], allp[j, 3])  # intensity of the voxel's first point
+    assert len(np.unique(j)) == cmap.shape[0]

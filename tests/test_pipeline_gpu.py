@@ -84,7 +84,7 @@ def check_pair(so, sg, to, tg, wo, wg):
     assert np.abs(wo[:, 1:25] - wg[:, 1:25]).max() < TIGHT_M  # window states R, p, v, bg, ba, g
 
 
-# (config, lidar, scans): BASELINE configs[1..4]'s parameter sets. The window
+# (config, lidar, scans): BASELINE configs[0..4]'s parameter sets. The window
 # fills at scan 9 (W = 10): the LM (mid360) and margi run from there, and the
 # IEKF matches against planes that margi's plane_update published.
 CASES = [
@@ -95,6 +95,8 @@ CASES = [
     ("robosense", "128line", 14),  # 128-line / 200 k rays (voxel 1.0, max_layer 2, BA off)
     ("mid360", "128line", 14),    # the north star's 128-line target on mid360 parameters
     ("mid360", "1M", 11),          # 1,000,064 rays (~870 k points after the blind filter)
+    ("velodyne", "16line", 16),   # configs[0]'s parameter set: voxel 1.0, max_layer 3, BA on, blind 0, rotated
+                                  # extrinsic (no VLP-16 bag exists here; the same loop the CPU path runs)
 ]
 
 
@@ -177,5 +179,41 @@ def test_long_sequence_matches_oracle(oracle_lib):
         print("scan %d: nodes %d, point_fix %d, slide %d" % (k, sg[k]["nodes_used"], sg[k]["fix_used"],
                                                           sg[k]["n_slide"]))
     assert sum(s["fix_full"] for s in sg) > 0
+    gpu.close()
+    orc.close()
+
+
+def test_path_and_local_map_match_oracle(oracle_lib):
+    """pub_localtraj / pub_localmap outputs (publishers.cpp:65-131,
+    local_mapping.cpp:427,505): the path with the window's BA re-writes, and the
+    /map_cmap cloud of the last window BA (vg_set_publish bit 0), against the
+    oracle; vg_poll never waits and ends at the full count once the device is
+    done."""
+    from test_node_core import check_path_and_cmap
+    p = vgconfig.load("mid360")
+    g = p["General"]
+    seq = synth.Sequence("16line", 5, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
+    orc = oracle.Pipeline(vgconfig.to_c(p, use_threads=0, vnc_prep=0))
+    gpu = vgpu.Context(vgconfig.to_c(p), max_points=100_000, max_nodes=500_000, max_fix_points=2_000_000,
+                       hash_log2=20)
+    gpu.set_publish(1)
+    orc.seed(seq.gt_state(0))
+    gpu.seed(seq.gt_state(0))
+    polled = []
+    for k in range(16):
+        xyz, it, b, e = seq.scan(k)
+        orc.step(xyz, it, b, e, seq.imu(k))
+        gpu.step(xyz, it, b, e, seq.imu(k))
+        polled.append(gpu.poll()[0])
+    assert all(0 <= n <= k + 1 for k, n in enumerate(polled)) and polled == sorted(polled)
+    path = gpu.path()
+    assert gpu.poll() == (16, 16, 16)
+    ref = dict(path=orc.path(), cmap=orc.local_map(), cmap_all=orc.local_map(all_points=True))
+    gp = np.concatenate([path[:, :1], path[:, 10:13], path[:, 13:14]], 1)
+    check_path_and_cmap(gp, gpu.local_map(), ref, TIGHT_M)
+    # the re-write moved the window's rows off the post-IEKF poses (the TUM rows)
+    tr = gpu.trajectory()
+    assert np.abs(path[-10:, 10:13] - tr[-10:, 10:13]).max() > 1e-6
+    assert np.array_equal(path[:-10, 1:10], tr[:-10, 1:10])
     gpu.close()
     orc.close()

@@ -597,6 +597,7 @@ static int system_reset(vg_ctx* ctx, HostPipe* P, InitState& I, const std::vecto
   for (int i = 0; i < ctx->cfg.win_size; i++) P->mp[i] = i;
   P->win_base = 0;
   P->win_count = 0;
+  P->path.clear();  // pcl_path.clear() (node.cpp:403)
   return VG_OK;
 }
 
@@ -698,9 +699,12 @@ int init_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   st.n_raw = n;
   st.n_ds = n_ds;
   st.init_valid = valid;
-  P->traj.push_back(end);
-  for (int k = 0; k < 9; k++) P->traj.push_back(P->x_curr.R.a[k]);
-  for (int k = 0; k < 3; k++) P->traj.push_back(P->x_curr.p.a[k]);
+  // pub_localtraj(pwld, 0, x_curr, 0, pcl_path) (node.cpp:325): a path point
+  // with jour 0; no save_pose_tum row during the initialisation
+  P->path.push_back(end);
+  for (int k = 0; k < 9; k++) P->path.push_back(P->x_curr.R.a[k]);
+  for (int k = 0; k < 3; k++) P->path.push_back(P->x_curr.p.a[k]);
+  P->path.push_back(0.0);
   // x_buf / imu_pre_buf (node.cpp:321-330)
   P->win_count++;
   P->x_buf.push_back(P->x_curr);

@@ -58,6 +58,9 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(m.wp_pnt = ctx->arena.take<double>(cw * W * 3));
   good &= ok(m.wp_var = ctx->arena.take<double>(cw * W * 9));
   good &= ok(m.wp_leaf = ctx->arena.take<int>(cw * W));
+  good &= ok(m.wp_int = ctx->arena.take<float>(cw * W));
+  good &= ok(ctx->d_cmap = ctx->arena.take<float4>((cw + 2) / 3));
+  good &= ok(ctx->d_cmap_n = ctx->arena.take<int>(4));
   good &= ok(m.counters = ctx->arena.take<int>(kCntN));
   good &= ok(m.stamp = ctx->arena.take<int>(cn));
   good &= ok(m.wpn = ctx->arena.take<int>(kMaxWin));
@@ -428,7 +431,7 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
 // on the body point + pvec_update.
 template <bool kPre>
 __global__ void __launch_bounds__(256) k_ins_prep(int n_arg, const int* __restrict__ nd, const float* __restrict__ ox, const float* __restrict__ oy,
-                           const float* __restrict__ oz, MP mp, DState* __restrict__ st, int slot,
+                           const float* __restrict__ oz, const float* __restrict__ oi, MP mp, DState* __restrict__ st, int slot,
                            DevMap m, double* __restrict__ pw, uint32_t* __restrict__ hslot,
                            const PushArg* __restrict__ pa, const double* __restrict__ pin, const double* __restrict__ xsrc,
                            int var_identity, int* __restrict__ dsf) {
@@ -483,6 +486,7 @@ __global__ void __launch_bounds__(256) k_ins_prep(int n_arg, const int* __restri
     for (int j = 0; j < 3; j++) m.wp_pnt[base * 3 + j] = pnt[j];
     for (int j = 0; j < 9; j++) m.wp_var[base * 9 + j] = vw[j];
     m.wp_leaf[base] = -1;
+    m.wp_int[base] = oi ? oi[i] : 0.f;
     for (int j = 0; j < 3; j++) pw[(size_t)i * 3 + j] = w[j];
     uint64_t key;
     if (!pack_key(w, mp.vs, key)) {
@@ -1166,13 +1170,15 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread
   // device count: n is an upper bound, the kernels stride over the real one
   const int g = nd ? grid_for(n, kBlock, 2048) : grid_for(n);
   if (pre)
-    k_ins_prep<true><<<g, kBlock, 0, s>>>(n, nullptr, nullptr, nullptr, nullptr, mp, ctx->st, slot, m, w.pw, w.u0,
+    k_ins_prep<true><<<g, kBlock, 0, s>>>(n, nullptr, nullptr, nullptr, nullptr, nullptr, mp, ctx->st, slot, m, w.pw,
+                                          w.u0,
                                           nullptr, pre->pnt, pre->pose, pre->var_identity, nullptr);
   else {
     // the push record goes through host-mapped memory, so a replayed graph
     // picks up each scan's record (the host writes it before the launch)
     if (push) ctx->h_in->push = *push;
-    k_ins_prep<false><<<g, kBlock, 0, s>>>(n, nd, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, mp, ctx->st, slot, m, w.pw,
+    k_ins_prep<false><<<g, kBlock, 0, s>>>(n, nd, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, ctx->ds.oi, mp, ctx->st, slot, m,
+                                           w.pw,
                                            w.u0, push ? &ctx->d_in->push : nullptr, nullptr, nullptr, 0,
                                            nd ? ctx->ds.hflags : nullptr);
   }
@@ -2423,6 +2429,25 @@ int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thr
   return VG_OK;
 }
 
+// pub_localmap's /map_cmap cloud (publishers.cpp:102-119): every third point
+// of the oldest window frame (mgsize = 1: pvec_buf[0]) at x_buf[0] after the
+// BA, R pnt + p in fp64, stored as float like the PointType it publishes
+__global__ void __launch_bounds__(256) k_local_map(const WinD* __restrict__ win, DevMap m, float4* __restrict__ out,
+                                                   int* __restrict__ nout, const int* __restrict__ gate) {
+  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
+  const int slot = win->mp[0];
+  const int n = m.wpn[slot];
+  const int nk = (n + 2) / 3;
+  if (blockIdx.x == 0 && threadIdx.x == 0) nout[0] = nk;
+  const M3 R = ld_m3(win->R[0]);
+  const V3 p = ld_v3(win->p[0]);
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nk; k += gridDim.x * blockDim.x) {
+    const size_t b = (size_t)slot * m.cap_wp + 3 * k;
+    const V3 w = rigid(R, ld_v3(&m.wp_pnt[b * 3]), p);
+    out[k] = make_float4((float)w[0], (float)w[1], (float)w[2], m.wp_int[b]);
+  }
+}
+
 int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, int pub_seq,
               int pub_seq2, const int* gate) {
   DevMap& m = ctx->map;
@@ -2442,6 +2467,7 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   wa2.seq2 = pub_seq2;
   VG_TRY(state_make_win(ctx, wa2, dwin, dn, dn + 32, gate));
   if (pub_seq > 0) VG_TRY(state_publish(ctx, wa.win_count, ba_iters_dev(ctx), pub_seq, gate));
+  if (ctx->pub_flags & 1) k_local_map<<<64, kBlock, 0, s>>>(dwin, m, ctx->d_cmap, ctx->d_cmap_n, gate);
   VG_HIP(hipStreamWaitEvent(s, ctx->ev_prefix_done, 0));  // map_margi_prefix
   // the rest reads every per-scan value from the device (n_oldest: rc, the
   // publication number: the state), so it is captured once and replayed

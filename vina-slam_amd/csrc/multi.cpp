@@ -40,6 +40,7 @@ struct vg_multi {
   bool quit = false;
   int depth = 4;  // scans queued per sequence before vg_multi_step_dev blocks
   int busy = 0;   // workers inside a step
+  std::vector<char> split;  // context b ran with its own downsample stream + IEKF overlap (restored on destroy)
 };
 
 static void worker(vg_multi* M, int b) {
@@ -79,6 +80,7 @@ vg_multi* vg_multi_create(vg_ctx** ctxs, int B, int spin_us, int sleep_us) {
   vg_multi* M = new vg_multi();
   M->ctx.assign(ctxs, ctxs + B);
   M->wk.resize(B);
+  M->split.assign(B, 0);
   for (int b = 0; b < B; b++) {
     vg_set_wait_policy(ctxs[b], spin_us, sleep_us);
     if (B > 1) {
@@ -88,6 +90,7 @@ vg_multi* vg_multi_create(vg_ctx** ctxs, int B, int spin_us, int sleep_us) {
       // depending on how the queues fell); the downsample and the margi prefix
       // then run in enqueue order on the context stream
       vg_ctx* c = ctxs[b];
+      M->split[b] = (char)((c->overlap_iekf ? 1 : 0) | (c->stream_ds && c->stream_ds != c->stream ? 2 : 0));
       c->overlap_iekf = false;
       if (c->stream_ds && c->stream_ds != c->stream) {
         (void)hipStreamSynchronize(c->stream_ds);
@@ -100,12 +103,19 @@ vg_multi* vg_multi_create(vg_ctx** ctxs, int B, int spin_us, int sleep_us) {
   return M;
 }
 
+// All-or-nothing: every queue has room and no worker has failed before any
+// scan is queued, so the sequences never go out of step on an error.
 int vg_multi_step_dev(vg_multi* M, const vg_scan_dev* scans) {
   if (!M || !scans) return VG_E_ARG;
   std::unique_lock<std::mutex> lk(M->mu);
+  M->cv_room.wait(lk, [&] {
+    for (const Worker& w : M->wk)
+      if (w.rc != VG_OK || (int)w.q.size() >= M->depth) return w.rc != VG_OK;
+    return true;
+  });
+  for (const Worker& w : M->wk)
+    if (w.rc != VG_OK) return w.rc;
   for (size_t b = 0; b < M->ctx.size(); b++) {
-    M->cv_room.wait(lk, [&] { return (int)M->wk[b].q.size() < M->depth; });
-    if (M->wk[b].rc != VG_OK) return M->wk[b].rc;
     Job j;
     j.sc = scans[b];
     if (scans[b].imu && scans[b].m > 0) j.imu.assign(scans[b].imu, scans[b].imu + 7 * (size_t)scans[b].m);
@@ -147,6 +157,17 @@ void vg_multi_destroy(vg_multi* M) {
   }
   M->cv_job.notify_all();
   for (auto& t : M->th) t.join();
+  // hand each context back as it came: its own downsample stream and the
+  // IEKF / margi overlap of the single-sequence path
+  for (size_t b = 0; b < M->ctx.size(); b++) {
+    vg_ctx* c = M->ctx[b];
+    (void)hipStreamSynchronize(c->stream);
+    if ((M->split[b] & 2) && c->stream_ds == c->stream) {
+      hipStream_t s = nullptr;
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) c->stream_ds = s;
+    }
+    if (M->split[b] & 1) c->overlap_iekf = c->stream_ds != c->stream;
+  }
   delete M;
 }
 

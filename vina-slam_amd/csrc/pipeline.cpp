@@ -130,9 +130,12 @@ static int absorb_p1(vg_ctx* ctx, HostPipe* P, Pend& q) {
     memcpy(h.g.a, o + 21, 24);
   }
   if (q.pushed >= 0 && q.pushed < (int)P->x_buf.size()) P->x_buf[q.pushed].cov = xc.cov;
-  if (!q.init_tail) {  // trajectory row (pub_localtraj / save_pose_tum, local_mapping.cpp:427-430)
+  if (!q.init_tail) {  // pub_localtraj's path point and save_pose_tum's row (local_mapping.cpp:427-430)
     P->traj.push_back(q.t);
     for (int i = 0; i < 12; i++) P->traj.push_back(pb.traj[i]);
+    P->path.push_back(q.t);
+    for (int i = 0; i < 12; i++) P->path.push_back(pb.traj[i]);
+    P->path.push_back(P->jour);
     q.st.iekf_iters = pb.iekf_iters;
     for (int i = 0; i < 4; i++) q.st.iekf_matches[i] = pb.matches[i];
     q.st.degenerate = degenerate_of(pb.nnt);
@@ -140,6 +143,13 @@ static int absorb_p1(vg_ctx* ctx, HostPipe* P, Pend& q) {
   q.st.ba_iters = pb.ba_iters1;
   q.st.ba_hess = pb.ba_hess1;
   for (int i = 0; i < 4; i++) q.st.iekf_planes[i] = pb.planes[i];
+  if (q.shift) {  // pub_localmap (publishers.cpp:121-129, local_mapping.cpp:505): the window's path rows
+                  // [win_base, win_base + win_count) take x_buf[i].p after the BA (pb.xs: the window before the slide)
+    const int W = ctx->cfg.win_size;
+    const int rows = (int)P->path.size() / kPathRow;
+    if (rows >= W)
+      for (int i = 0; i < W; i++) memcpy(&P->path[(size_t)(rows - W + i) * kPathRow + 10], pb.xs + (size_t)i * kXS + 9, 24);
+  }
   if (q.jour_check) {  // local_mapping.cpp:525-533 with x_curr.p = x_buf.back().p after the BA
     double spat = norm3(sub(xc.p, P->last_pos));
     if (spat > 0.5) {
@@ -212,6 +222,27 @@ int absorb(vg_ctx* ctx, HostPipe* P, bool full) {
   }
   if (r != VG_OK) P->sticky = r;
   return r;
+}
+
+// non-blocking: absorb, oldest first, every pending scan whose publications
+// (state and end-of-scan counters) have both arrived; stops at the first that
+// has not. Only the newest pending scan can be unpublished (the host absorbs a
+// scan's state before the next scan publishes), so the Pub block holds the
+// scan being absorbed.
+int absorb_ready(vg_ctx* ctx, HostPipe* P) {
+  if (P->sticky != VG_OK) return P->sticky;
+  while (!P->pend.empty()) {
+    Pend& q = P->pend.front();
+    if (q.seq1 != 0 && __atomic_load_n(&ctx->h_pub->seq1, __ATOMIC_ACQUIRE) < q.seq1) break;
+    if (__atomic_load_n(&ctx->h_pub->seq2, __ATOMIC_ACQUIRE) < q.seq2) break;
+    const int r = absorb_p2(ctx, P, q);
+    if (r != VG_OK) {
+      P->sticky = r;
+      return r;
+    }
+    P->pend.pop_front();
+  }
+  return VG_OK;
 }
 
 int host_sync(vg_ctx* ctx) {
@@ -1054,9 +1085,20 @@ int host_window(vg_ctx* ctx, double* out) {
 }
 int host_traj(vg_ctx* ctx, double* out, int cap) {
   HostPipe* P = hp(ctx);
-  int n = (int)P->traj.size() / 13;
-  if (out) memcpy(out, P->traj.data(), (size_t)(n < cap ? n : cap) * 13 * sizeof(double));
+  int n = (int)P->traj.size() / kTrajRow;
+  if (out) memcpy(out, P->traj.data(), (size_t)(n < cap ? n : cap) * kTrajRow * sizeof(double));
   return n;
+}
+int host_path(vg_ctx* ctx, double* out, int cap) {
+  HostPipe* P = hp(ctx);
+  int n = (int)P->path.size() / kPathRow;
+  if (out) memcpy(out, P->path.data(), (size_t)(n < cap ? n : cap) * kPathRow * sizeof(double));
+  return n;
+}
+int host_poll(vg_ctx* ctx) {
+  HostPipe* P = hp(ctx);
+  if (P->in_scan) return VG_OK;  // a stage-level scan is open: nothing to absorb mid-scan
+  return absorb_ready(ctx, P);
 }
 int host_stats_log(vg_ctx* ctx, vg_stats* out, int cap) {
   HostPipe* P = hp(ctx);

@@ -154,7 +154,9 @@ struct HostPipe {
   int wp_n[32] = {0};
   MP mpd;
   M6 noiseMeas = M6::Z(), noiseWalk = M6::Z();
-  std::vector<double> traj;
+  std::vector<double> traj;  // save_pose_tum rows (io.cpp:67-77): steady-state scans only, kTrajRow each
+  std::vector<double> path;  // pcl_path (publishers.cpp:65-131): every pub_localtraj, cleared by system_reset,
+                             // the window's rows re-written by pub_localmap after the BA; kPathRow each
   std::vector<vg_stats> stats_log;
   std::vector<double> poses;  // this scan's IMUEKF::imu_poses, 22 doubles each (deskew)
   int n_factors = 0;

@@ -154,6 +154,7 @@ struct DevMap {
   double* wp_pnt = nullptr;    // window points per physical slot: body pnt
   double* wp_var = nullptr;    // world var (after pvec_update), packed 6
   int* wp_leaf = nullptr;      // leaf holding the point in its list, -1 = not listed
+  float* wp_int = nullptr;     // intensity of the window point (pointVar::intensity; /map_cmap only)
   int* counters = nullptr;     // device counters (see kCnt*)
   int* stamp = nullptr;        // per-node tag of the last IEKF iteration that read its plane (P_k, profiling pass)
   int* wpn = nullptr;          // window points per physical slot (written by the insert, read by k_make_win)
@@ -319,6 +320,9 @@ struct vg_ctx {
   bool ins_ev_pending = false;  // ev_ds_free / ev_recut_done of the last insert+recut graph not recorded yet  // map_reset has cleared the node records once (then only the used ids)
   bool use_graphs = true;  // margi prefix on the second stream
   bool overlap_iekf = true;  // the next IEKF under the margi remainder (lio_state_estimation)
+  int pub_flags = 0;         // vg_set_publish: bit 0 = /map_cmap after each window BA (k_local_map)
+  float4* d_cmap = nullptr;  // the last /map_cmap cloud (x, y, z, intensity) and its size
+  int* d_cmap_n = nullptr;
   bool spec_tail = true;     // the margi tail behind the predicted LM iterations (stage_ba)
   std::string err;
   vg::Arena arena;
@@ -383,6 +387,8 @@ struct vg_ctx {
 };
 
 namespace vg {
+constexpr int kTrajRow = 13;  // vg_trajectory: t, R 9, p 3
+constexpr int kPathRow = 14;  // vg_path: t, R 9, p 3, jour (the path point's curvature)
 constexpr size_t kStageBytes = 1 << 17;
 constexpr size_t kStageDeskewOff = 8192;  // doubles: the deskew block's part of the staging area
 constexpr int kDeskewBuf = 4096;          // doubles (up to 180 IMU segments per scan)
@@ -609,6 +615,8 @@ void host_seed(vg_ctx* ctx, const double* s);
 int host_state(vg_ctx* ctx, double* s);
 int host_window(vg_ctx* ctx, double* out);
 int host_traj(vg_ctx* ctx, double* out, int cap);
+int host_path(vg_ctx* ctx, double* out, int cap);
+int host_poll(vg_ctx* ctx);
 int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n, double beg,
               double end, const double* imu, int m);
 int host_win_count(vg_ctx* ctx);

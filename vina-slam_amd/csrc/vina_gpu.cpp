@@ -581,6 +581,54 @@ int vg_trajectory(vg_ctx* ctx, double* out, int cap, int* n) {
   return VG_OK;
 }
 
+int vg_path(vg_ctx* ctx, double* out, int cap, int* n) {
+  if (!ctx || !n || cap < 0) return VG_E_ARG;
+  VG_TRY(host_sync(ctx));
+  *n = host_path(ctx, out, cap);
+  return VG_OK;
+}
+
+int vg_set_publish(vg_ctx* ctx, int flags) {
+  if (!ctx || (flags & ~1)) return VG_E_ARG;
+  VG_TRY(host_sync(ctx));
+  if ((flags & 1) && !(ctx->pub_flags & 1)) VG_HIP(hipMemset(ctx->d_cmap_n, 0, sizeof(int)));
+  ctx->pub_flags = flags;
+  return VG_OK;
+}
+
+int vg_local_map(vg_ctx* ctx, float* out_xyzi, int cap, int* n) {
+  if (!ctx || !n || cap < 0 || (cap > 0 && !out_xyzi)) return VG_E_ARG;
+  VG_TRY(host_sync(ctx));
+  int k = 0;
+  if (ctx->pub_flags & 1) VG_HIP(hipMemcpy(&k, ctx->d_cmap_n, sizeof(int), hipMemcpyDeviceToHost));
+  *n = k;
+  const int c = k < cap ? k : cap;
+  if (c > 0) VG_HIP(hipMemcpy(out_xyzi, ctx->d_cmap, (size_t)c * sizeof(float4), hipMemcpyDeviceToHost));
+  return VG_OK;
+}
+
+int vg_poll(vg_ctx* ctx, int* n_scans, int* n_traj, int* n_path) {
+  if (!ctx) return VG_E_ARG;
+  VG_TRY(host_poll(ctx));
+  if (n_scans) *n_scans = host_stats_log(ctx, nullptr, 0);
+  if (n_traj) *n_traj = host_traj(ctx, nullptr, 0);
+  if (n_path) *n_path = host_path(ctx, nullptr, 0);
+  return VG_OK;
+}
+
+int vg_poll_rows(vg_ctx* ctx, double* traj, int traj_from, int traj_cap, double* path, int path_cap) {
+  if (!ctx || traj_from < 0 || traj_cap < 0 || path_cap < 0) return VG_E_ARG;
+  const int nt = host_traj(ctx, nullptr, 0);
+  if (traj && traj_cap > 0 && traj_from < nt) {
+    std::vector<double> all((size_t)nt * vg::kTrajRow);
+    host_traj(ctx, all.data(), nt);
+    const int k = nt - traj_from < traj_cap ? nt - traj_from : traj_cap;
+    memcpy(traj, &all[(size_t)traj_from * vg::kTrajRow], (size_t)k * vg::kTrajRow * sizeof(double));
+  }
+  if (path && path_cap > 0) host_path(ctx, path, path_cap);
+  return VG_OK;
+}
+
 // ---- stage-level API (include/vina_gpu.h "Stage-level API") ----
 int vg_scan_load(vg_ctx* ctx, const float* xyz, const float* intensity, int n) {
   if (!ctx || n < 0 || (n > 0 && !xyz)) return VG_E_ARG;

@@ -22,7 +22,7 @@ static bool rd(FILE* f, void* p, size_t n) { return fread(p, 1, n, f) == n; }
 
 int main(int argc, char** argv) {
   if (argc < 3) {
-    fprintf(stderr, "usage: %s events.bin out_tum.txt [device]\n", argv[0]);
+    fprintf(stderr, "usage: %s events.bin out_tum.txt [device [out_path.txt [out_cmap.bin]]]\n", argv[0]);
     return 2;
   }
   FILE* f = fopen(argv[1], "rb");
@@ -46,6 +46,7 @@ int main(int argc, char** argv) {
     cap.max_points_per_scan = 400000;
     vina_gpu::NodeCore node(cfg, &cap, fmt, point_notime, argc > 3 ? atoi(argv[3]) : 0);
     if (has_seed) node.lio().seed(seed);
+    if (argc > 5) node.enable_local_map(true);  // /map_cmap after every window BA
     std::vector<unsigned char> rec;
     int n_imu = 0, n_msg = 0, n_step = 0;
     for (;;) {
@@ -72,8 +73,30 @@ int main(int argc, char** argv) {
       perror("tum");
       return 1;
     }
-    printf("{\"imu\": %d, \"scans\": %d, \"stepped\": %d, \"poses\": %zu, \"last_scan_world_points\": %zu}\n", n_imu,
-           n_msg, n_step, node.path().size(), w.size() / 3);
+    if (argc > 4) {  // pcl_path after the run: t x y z jour per row (the BA re-writes included)
+      FILE* fp = fopen(argv[4], "w");
+      if (!fp) {
+        perror("path");
+        return 1;
+      }
+      for (const vina_gpu::PoseStamped& s : node.path())
+        fprintf(fp, "%.9f %.12f %.12f %.12f %.12f\n", s.t, s.p[0], s.p[1], s.p[2], s.jour);
+      fclose(fp);
+    }
+    size_t ncmap = 0;
+    if (argc > 5) {  // the last /map_cmap cloud, float32 x y z intensity
+      const std::vector<float> c = node.local_map();
+      ncmap = c.size() / 4;
+      FILE* fc = fopen(argv[5], "wb");
+      if (!fc || fwrite(c.data(), sizeof(float), c.size(), fc) != c.size()) {
+        perror("cmap");
+        return 1;
+      }
+      fclose(fc);
+    }
+    printf("{\"imu\": %d, \"scans\": %d, \"stepped\": %d, \"poses\": %zu, \"path\": %zu, "
+           "\"last_scan_world_points\": %zu, \"cmap_points\": %zu}\n",
+           n_imu, n_msg, n_step, node.tum_rows().size(), node.path().size(), w.size() / 3, ncmap);
   } catch (const vina_gpu::Error& e) {
     fprintf(stderr, "vg_node_replay: %s (code %d)\n", e.what(), e.code);
     return 1;

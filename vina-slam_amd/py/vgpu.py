@@ -133,6 +133,11 @@ def lib():
         L.vg_stats_log.argtypes = [P, ctypes.POINTER(Stats), ctypes.c_int, ip]
         L.vg_window_states.argtypes = [P, dp, ip]
         L.vg_trajectory.argtypes = [P, dp, ctypes.c_int, ip]
+        L.vg_path.argtypes = [P, dp, ctypes.c_int, ip]
+        L.vg_poll.argtypes = [P, ip, ip, ip]
+        L.vg_poll_rows.argtypes = [P, dp, ctypes.c_int, ctypes.c_int, dp, ctypes.c_int]
+        L.vg_local_map.argtypes = [P, fp, ctypes.c_int, ip]
+        L.vg_set_publish.argtypes = [P, ctypes.c_int]
         L.vg_scan_load.argtypes = [P, fp, fp, ctypes.c_int]
         L.vg_scan_bind_dev.argtypes = [P, P, P, P, P, ctypes.c_int]
         L.vg_propagate.argtypes = [P, dp, ctypes.c_int, ctypes.c_double, ctypes.c_double]
@@ -338,6 +343,31 @@ class Context:
         self._chk(lib().vg_trajectory(self.h, _d(out), n.value, ctypes.byref(n)), "vg_trajectory")
         return out[: n.value]
 
+    def path(self):
+        """pcl_path rows (vg_path): t, R(9), p(3), jour; the window's positions re-written after each BA."""
+        n = ctypes.c_int(0)
+        self._chk(lib().vg_path(self.h, None, 0, ctypes.byref(n)), "vg_path")
+        out = np.zeros((max(n.value, 1), 14))
+        self._chk(lib().vg_path(self.h, _d(out), n.value, ctypes.byref(n)), "vg_path")
+        return out[: n.value]
+
+    def poll(self):
+        """Non-blocking (vg_poll): (scans complete, TUM rows, path rows) absorbed so far."""
+        a, b, c = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+        self._chk(lib().vg_poll(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "vg_poll")
+        return a.value, b.value, c.value
+
+    def set_publish(self, flags):
+        self._chk(lib().vg_set_publish(self.h, flags), "vg_set_publish")
+
+    def local_map(self):
+        """/map_cmap of the last window BA (vg_local_map): (n, 4) float32 x, y, z, intensity."""
+        n = ctypes.c_int(0)
+        self._chk(lib().vg_local_map(self.h, None, 0, ctypes.byref(n)), "vg_local_map")
+        out = np.zeros((max(n.value, 1), 4), dtype=np.float32)
+        self._chk(lib().vg_local_map(self.h, _f(out), n.value, ctypes.byref(n)), "vg_local_map")
+        return out[: n.value]
+
     # ---- stage-level API (reference call order, include/vina_gpu.h) ----
     def scan_load(self, xyz, inten):
         self._xyz = np.ascontiguousarray(xyz, dtype=np.float32)
@@ -495,6 +525,7 @@ class Multi:
             arr[b] = ScanDev(x, y, z, i, t or None, n, beg, end, _d(imu), imu.shape[0])
         r = lib().vg_multi_step_dev(self.h, arr)
         if r != 0:
+            lib().vg_multi_sync(self.h)  # the workers are idle before their error strings are read
             raise VgError("vg_multi_step_dev failed (%d): %s" % (
                 r, "; ".join(lib().vg_last_error(c.h).decode() for c in self.contexts)))
 

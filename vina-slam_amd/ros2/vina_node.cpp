@@ -114,6 +114,7 @@ class VinaNode : public rclcpp::Node {
           lid_topic, pcl_qos, [this](sensor_msgs::msg::PointCloud2::SharedPtr m) { on_cloud(*m); });
     pub_scan_ = create_publisher<sensor_msgs::msg::PointCloud2>("/map_scan", 100);
     pub_path_ = create_publisher<sensor_msgs::msg::PointCloud2>("/map_path", 100);
+    pub_cmap_ = create_publisher<sensor_msgs::msg::PointCloud2>("/map_cmap", 100);  // publishers.cpp:130
     tf_ = std::make_unique<tf2_ros::TransformBroadcaster>(*this);
   }
 
@@ -170,10 +171,17 @@ class VinaNode : public rclcpp::Node {
   }
 #endif
 
-  // sync_packages + the estimator, then pub_localtraj's outputs per new pose
+  // sync_packages + the estimator; then the outputs of every scan the device
+  // has finished (NodeCore::poll, no drain): the TF per new path point
+  // (pub_odom_func), the path (pub_localtraj / pub_localmap re-write), and —
+  // only while someone subscribes, since reading them completes the queued
+  // work — the last scan in the world (/map_scan) and /map_cmap
   void run() {
-    if (core_->spin() == 0) return;
+    const int stepped = core_->spin();
+    const bool changed = core_->poll();
+    if (stepped == 0 && !changed) return;
     const auto& path = core_->path();
+    if (path.size() < published_) published_ = 0;  // system_reset cleared pcl_path
     for (; published_ < path.size(); published_++) {
       const vina_gpu::PoseStamped& s = path[published_];
       geometry_msgs::msg::TransformStamped t;
@@ -189,11 +197,26 @@ class VinaNode : public rclcpp::Node {
       t.transform.rotation.w = s.q[3];
       tf_->sendTransform(t);
     }
-    publish_xyz(pub_scan_, core_->scan_world());
-    std::vector<float> pts;
-    for (const auto& s : path)
-      for (int k = 0; k < 3; k++) pts.push_back((float)s.p[k]);
-    publish_xyz(pub_path_, pts);
+    if (changed) {
+      path_xyz_.resize(3 * path.size());
+      for (size_t i = 0; i < path.size(); i++)
+        for (int k = 0; k < 3; k++) path_xyz_[3 * i + k] = (float)path[i].p[k];
+      publish_xyz(pub_path_, path_xyz_);
+    }
+    if (stepped > 0 && pub_scan_->get_subscription_count() > 0) publish_xyz(pub_scan_, core_->scan_world());
+    const bool want_cmap = pub_cmap_->get_subscription_count() > 0;
+    if (want_cmap != cmap_on_) {
+      core_->enable_local_map(want_cmap);
+      cmap_on_ = want_cmap;
+    }
+    if (cmap_on_ && stepped > 0) {
+      const std::vector<float> c = core_->local_map();
+      std::vector<float> xyz;
+      xyz.reserve(c.size() / 4 * 3);
+      for (size_t i = 0; i < c.size() / 4; i++)
+        for (int k = 0; k < 3; k++) xyz.push_back(c[4 * i + k]);
+      publish_xyz(pub_cmap_, xyz);
+    }
   }
 
   void publish_xyz(const rclcpp::Publisher<sensor_msgs::msg::PointCloud2>::SharedPtr& pub,
@@ -225,7 +248,9 @@ class VinaNode : public rclcpp::Node {
 #ifdef VG_HAVE_LIVOX
   rclcpp::Subscription<livox_ros_driver2::msg::CustomMsg>::SharedPtr sub_livox_;
 #endif
-  rclcpp::Publisher<sensor_msgs::msg::PointCloud2>::SharedPtr pub_scan_, pub_path_;
+  rclcpp::Publisher<sensor_msgs::msg::PointCloud2>::SharedPtr pub_scan_, pub_path_, pub_cmap_;
+  std::vector<float> path_xyz_;
+  bool cmap_on_ = false;
 };
 
 }  // namespace
