@@ -30,6 +30,10 @@ sys.path.insert(0, os.path.join(REPO, "vina-slam_amd", "py"))
 import numpy as np  # noqa: E402
 
 METRIC = "scans/sec (downsample+kNN+LM solve), 64-line LiDAR, 1/2/4/8 MI355X; ATE vs CPU"
+# one plane record as the correspondence gate reads it: SURVEY 8(d) prices it
+# at 112 B (fp32 c, n, radius, 21 sym plane_var); bit-faithful gating reads the
+# reference's fp64 record (PlaneRec, 224 B), so the byte model uses that
+PLANE_B = 224.0
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
 FP64_MFMA_TFLOPS = 78.6  # MI355X dense fp64 matrix peak
 
@@ -254,12 +258,12 @@ def main():
                   "unit": "TFLOP/s", "frac": round(s_ach / FP64_MFMA_TFLOPS, 7), "traffic": None,
                   "avg_launch_us": round(s_avg * 1e6, 3), "launches": sol["launches"], "flops_per_launch": int(flops)}
     # k_iekf (hot loop #1, HBM-bound gather): 16 B per raw point (fp32 xyz +
-    # cached leaf) + 112 B per distinct plane record (P_k) per launch; in the
+    # cached leaf) + PLANE_B per distinct plane record (P_k) per launch; in the
     # timed region the IEKF replays as one hipGraph, so its per-launch events
     # come from the per-stage pass (direct launches, same sequence)
     iek = stage_prof.get("iekf", {"ms": 0.0, "launches": 0})
     n_launch = iek["launches"]
-    bytes_tot = sum(s["iekf_iters"] * 16.0 * s["n_raw"] + 112.0 * sum(s["iekf_planes"][: s["iekf_iters"]])
+    bytes_tot = sum(s["iekf_iters"] * 16.0 * s["n_raw"] + PLANE_B * sum(s["iekf_planes"][: s["iekf_iters"]])
                     for s in stage_stats)
     avg_s = iek["ms"] * 1e-3 / max(n_launch, 1)
     achieved = (bytes_tot / max(n_launch, 1)) / avg_s / 1e9 if avg_s > 0 else 0.0
@@ -319,7 +323,7 @@ def main():
 
 def scan_roofline(stats, stage_stats, W, t_scan):
     """Whole-scan algorithmic bytes per timed scan / its wall time:
-    B = 16 N_raw + 16 N_ds + sum_k (12 N_raw + 4 N_raw + 112 P_k) + 12 N_ds
+    B = 16 N_raw + 16 N_ds + sum_k (12 N_raw + 4 N_raw + PLANE_B P_k) + 12 N_ds
         + 2 V_ins 440 + V_slide (80 W + 80) + (I_H + I_R) F (80 W + 176).
     Every counter is the timed scan's own (I_H = Hessian passes, I_R = LM
     iterations), except P_k, which is counted only in the per-stage pass
@@ -330,7 +334,7 @@ def scan_roofline(stats, stage_stats, W, t_scan):
     b = 0.0
     for s in stats:
         b += 16.0 * s["n_raw"] + 16.0 * s["n_ds"]
-        b += s["iekf_iters"] * (16.0 * s["n_raw"] + 112.0 * p_mean)
+        b += s["iekf_iters"] * (16.0 * s["n_raw"] + PLANE_B * p_mean)
         b += 12.0 * s["n_ds"] + 2.0 * s["v_ins"] * 440.0
         b += s["n_slide"] * (W * 80.0 + 80.0)
         b += (s["ba_hess"] + s["ba_iters"]) * s["n_factors"] * (W * 80.0 + 176.0)
@@ -343,7 +347,8 @@ def scan_roofline(stats, stage_stats, W, t_scan):
             "counters_mean": {"N_raw": mean("n_raw"), "N_ds": mean("n_ds"), "K": mean("iekf_iters"),
                               "P_k": round(p_mean, 1), "V_ins": mean("v_ins"), "V_slide": mean("n_slide"),
                               "F": mean("n_factors"), "I_H": mean("ba_hess"), "I_R": mean("ba_iters")},
-            "note": "SURVEY 8(d) algorithmic bytes per scan / ms_per_step; P_k from the per-stage pass"}
+            "note": "SURVEY 8(d) algorithmic bytes per scan / ms_per_step, plane records at %d B (fp64, as the "
+                    "gate reads them; SURVEY prices 112 B fp32); P_k from the per-stage pass" % PLANE_B}
 
 
 def multi_roofline(multi, roof):

@@ -234,7 +234,8 @@ def test_cold_start_matches_oracle(oracle_lib, cfg, lidar, nscan, scale, in_g):
     # pcl_path: the init scans since the last system_reset (node.cpp:403), then BA re-writes
     po, pg = orc.path(), gpu.path()
     assert po.shape == pg.shape and np.array_equal(po[:, 0], pg[:, 0])
-    assert np.abs(po[:, 1:13] - pg[:, 1:13]).max() < 1e-9 and np.array_equal(po[:, 13], pg[:, 13])
+    assert np.abs(po[:, 1:13] - pg[:, 1:13]).max() < 1e-9
+    assert np.abs(po[:, 13] - pg[:, 13]).max() < 1e-9  # jour: sums of |dp| of the BA-refined positions
     assert (4 in phases) == (scale != 1.0) and (3 in phases) == (scale == 1.0)
     gpu.close()
     orc.close()

@@ -120,3 +120,47 @@ def test_hashed_downsample_bit_exact(ctx, oracle_lib, case):
         got = [tuple(k) for k in np.where(loc < 0, (loc.astype(np.float64) - 1.0).astype(np.float32),
                                           loc).astype(np.int64)]
         assert got == order
+
+
+@pytest.mark.parametrize("case,size,halves", [("scan", 0.1, False), ("dense", 1.0, True), ("giant", 0.5, True),
+                                              ("clusters", 0.5, True)])
+def test_fallback_pass_matches_oracle(oracle_lib, case, size, halves):
+    """down_sampling_voxel's /2 fallback below 2000 voxels (local_mapping.cpp:
+    399-403) on the device: one workgroup redoes the pass at size / 2 when the
+    first kept fewer than 2000 voxels (k_hds_fallback), bit for bit the oracle's
+    set and the first-occurrence order; otherwise the first pass stands."""
+    import oracle
+    import vgpu
+    rng = np.random.default_rng(9)
+    p = vgconfig.load("mid360")
+    ctx = vgpu.Context(vgconfig.to_c(p), max_points=400_000, max_nodes=100_000, max_fix_points=100_000,
+                       hash_log2=16)
+    if case == "scan":
+        g_ = p["General"]
+        seq = synth.Sequence("64line", 1, blind=g_["blind"], ext_R=g_["extrinsic_rota"], ext_t=g_["extrinsic_tran"])
+        xyz, inten, _, _ = seq.scan(3)
+    elif case == "dense":  # ~300 voxels at 1 m, dense ones (> 16 points) at 0.5 m
+        c = rng.uniform(-5, 5, (300, 3))
+        xyz = (c[rng.integers(0, 300, 60_000)] + rng.normal(0, 0.01, (60_000, 3))).astype(np.float32)
+        inten = rng.uniform(0, 100, 60_000).astype(np.float32)
+    elif case == "giant":  # one voxel of 50 k points, ~1 at 0.25 m too
+        xyz = (rng.normal(0, 0.005, (50_000, 3)) + 3.05).astype(np.float32)
+        inten = np.arange(50_000, dtype=np.float32)
+    else:  # 1200 clusters at 0.5 m voxel centres: < 2000 voxels at 0.5 m, many more at 0.25 m (step 2 over
+        # 30 tiles of 1024 points)
+        c = (np.floor(rng.uniform(-40, 40, (1200, 3)) / 0.5) + 0.5) * 0.5
+        xyz = (c[rng.integers(0, 1200, 30_000)] + rng.normal(0, 0.04, (30_000, 3))).astype(np.float32)
+        inten = rng.uniform(0, 1, 30_000).astype(np.float32)
+    first = oracle.downsample(xyz, inten, size)
+    assert (first.shape[0] < 2000) == halves
+    used = size / 2 if halves else size
+    g = ctx.downsample_hashed(xyz, inten, size, fallback=True)
+    o = oracle.downsample(xyz, inten, used)
+    assert g.shape == o.shape
+    assert np.array_equal(_canon(g).view(np.uint32), _canon(o).view(np.uint32))
+    order = _first_occurrence_order(xyz, used)
+    loc = (g[:, :3].astype(np.float64) / used).astype(np.float32)
+    got = [tuple(k) for k in np.where(loc < 0, (loc.astype(np.float64) - 1.0).astype(np.float32),
+                                      loc).astype(np.int64)]
+    assert got == order
+    ctx.close()

@@ -42,7 +42,14 @@ def _run(cfgname, lidar, nscan, rank, world, q, port):
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
             dist.init_process_group("gloo", rank=rank, world_size=world)
 
+            log = os.environ.get("VG_AR_LOG")
+            seqn = [0]
+
             def allreduce(arr):
+                if log:  # debugging aid: every exchange of this rank, in order
+                    with open("%s.%d" % (log, rank), "a") as f:
+                        f.write("%d %d %s\n" % (seqn[0], arr.size, arr.dtype))
+                seqn[0] += 1
                 dist.all_reduce(torch.from_numpy(arr))
 
             ctx.shard_host(rank, world, allreduce)

@@ -473,84 +473,212 @@ __global__ void __launch_bounds__(256) k_hds_mean(DownsampleBufs d, const int* _
 // recurrences (the same arithmetic as k_hds_mean, bit for bit).
 constexpr int kHdsBits = 1 << 18;          // indices per bitmap window (32 KB of LDS)
 constexpr int kHdsWords = kHdsBits / 32;
-__global__ void __launch_bounds__(256) k_hds_big(DownsampleBufs d, const int* __restrict__ need) {
-  if (need && !*need) return;
-  const HdsIn a = *d.arg;
-  const float *x = a.x, *y = a.y, *z = a.z, *in = a.in;
-  __shared__ uint32_t bm[kHdsWords];
-  __shared__ int s_w[4], s_base;
-  const int nbig = d.hflags[3];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int q = blockIdx.x; q < nbig; q += gridDim.x) {
-    const int v = d.bigv[q];
-    const int i0 = d.vfirst[v];  // the voxel's smallest index
-    const uint32_t s = d.pslot[i0];
-    const int b = d.hoff[s], cnt = d.hcnt[s];
-    const uint32_t* sg = d.pseg + b;
-    uint32_t* out = d.pseg2 + b;
-    int hi = i0;
-    for (int e = tid; e < cnt; e += blockDim.x) hi = max(hi, (int)sg[e]);
-    for (int o = 32; o > 0; o >>= 1) hi = max(hi, __shfl_down(hi, o, 64));
-    if (lane == 0) s_w[wv] = hi;
+// one dense voxel v by the whole workgroup (any size, a multiple of 64 that
+// divides kHdsWords); bm: kHdsWords LDS words, s_w: one int per wave
+__device__ void hds_big_voxel(DownsampleBufs& d, int v, const float* x, const float* y, const float* z, const float* in,
+                              uint32_t* bm, int* s_w, int* s_base) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nt = blockDim.x, nw = nt >> 6;
+  const int i0 = d.vfirst[v];  // the voxel's smallest index
+  const uint32_t s = d.pslot[i0];
+  const int b = d.hoff[s], cnt = d.hcnt[s];
+  const uint32_t* sg = d.pseg + b;
+  uint32_t* out = d.pseg2 + b;
+  int hi = i0;
+  for (int e = tid; e < cnt; e += nt) hi = max(hi, (int)sg[e]);
+  for (int o = 32; o > 0; o >>= 1) hi = max(hi, __shfl_down(hi, o, 64));
+  if (lane == 0) s_w[wv] = hi;
+  __syncthreads();
+  hi = s_w[0];
+  for (int k = 1; k < nw; k++) hi = max(hi, s_w[k]);
+  if (tid == 0) *s_base = 0;
+  __syncthreads();
+  for (int w0 = i0; w0 <= hi; w0 += kHdsBits) {
+    for (int k = tid; k < kHdsWords; k += nt) bm[k] = 0u;
     __syncthreads();
-    hi = max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3]));
-    if (tid == 0) s_base = 0;
-    __syncthreads();
-    for (int w0 = i0; w0 <= hi; w0 += kHdsBits) {
-      for (int k = tid; k < kHdsWords; k += blockDim.x) bm[k] = 0u;
-      __syncthreads();
-      for (int e = tid; e < cnt; e += blockDim.x) {
-        const int off = (int)sg[e] - w0;
-        if (off >= 0 && off < kHdsBits) atomicOr(&bm[off >> 5], 1u << (off & 31));
-      }
-      __syncthreads();
-      constexpr int per = kHdsWords / 256;  // words per thread, contiguous
-      int mine = 0;
-      for (int k = 0; k < per; k++) mine += __popc(bm[tid * per + k]);
-      int xs = mine;  // block exclusive scan
-      for (int o = 1; o < 64; o <<= 1) {
-        const int yv = __shfl_up(xs, o, 64);
-        if (lane >= o) xs += yv;
-      }
-      __syncthreads();
-      if (lane == 63) s_w[wv] = xs;
-      __syncthreads();
-      int base = s_base;
-      for (int k = 0; k < wv; k++) base += s_w[k];
-      base += xs - mine;
-      for (int k = 0; k < per; k++) {
-        uint32_t m = bm[tid * per + k];
-        while (m) {
-          const int bit = __ffs(m) - 1;
-          m &= m - 1;
-          out[base++] = (uint32_t)(w0 + (tid * per + k) * 32 + bit);
-        }
-      }
-      __syncthreads();
-      if (tid == 0) s_base += s_w[0] + s_w[1] + s_w[2] + s_w[3];
-      __syncthreads();
+    for (int e = tid; e < cnt; e += nt) {
+      const int off = (int)sg[e] - w0;
+      if (off >= 0 && off < kHdsBits) atomicOr(&bm[off >> 5], 1u << (off & 31));
     }
-    if (tid < 3) {  // point_utils.hpp:34-37 per coordinate, as written
-      const float* a = tid == 0 ? x : (tid == 1 ? y : z);
-      float p = a[i0], c = 1.0f;
-      for (int e = 1; e < cnt; e++) {
-        p = (p * c + a[out[e]]) / (c + 1);
-        c += 1;
-      }
-      (tid == 0 ? d.ox : (tid == 1 ? d.oy : d.oz))[v] = p;
-      if (tid == 0) {
-        d.oi[v] = in ? in[i0] : 0.0f;
-        d.oc[v] = c;
+    __syncthreads();
+    const int per = kHdsWords / nt;  // words per thread, contiguous
+    int mine = 0;
+    for (int k = 0; k < per; k++) mine += __popc(bm[tid * per + k]);
+    int xs = mine;  // block exclusive scan
+    for (int o = 1; o < 64; o <<= 1) {
+      const int yv = __shfl_up(xs, o, 64);
+      if (lane >= o) xs += yv;
+    }
+    __syncthreads();
+    if (lane == 63) s_w[wv] = xs;
+    __syncthreads();
+    int base = *s_base;
+    for (int k = 0; k < wv; k++) base += s_w[k];
+    base += xs - mine;
+    for (int k = 0; k < per; k++) {
+      uint32_t m = bm[tid * per + k];
+      while (m) {
+        const int bit = __ffs(m) - 1;
+        m &= m - 1;
+        out[base++] = (uint32_t)(w0 + (tid * per + k) * 32 + bit);
       }
     }
     __syncthreads();
     if (tid == 0) {
-      d.hkey[s] = kKeyEmpty;
-      d.hfirst[s] = kHdsEmptyFirst;
-      d.hcnt[s] = 0;
-      d.hfill[s] = 0;
+      int t = 0;
+      for (int k = 0; k < nw; k++) t += s_w[k];
+      *s_base += t;
+    }
+    __syncthreads();
+  }
+  if (tid < 3) {  // point_utils.hpp:34-37 per coordinate, as written
+    const float* a = tid == 0 ? x : (tid == 1 ? y : z);
+    float p = a[i0], c = 1.0f;
+    for (int e = 1; e < cnt; e++) {
+      p = (p * c + a[out[e]]) / (c + 1);
+      c += 1;
+    }
+    (tid == 0 ? d.ox : (tid == 1 ? d.oy : d.oz))[v] = p;
+    if (tid == 0) {
+      d.oi[v] = in ? in[i0] : 0.0f;
+      d.oc[v] = c;
     }
   }
+  __syncthreads();
+  if (tid == 0) {
+    d.hkey[s] = kKeyEmpty;
+    d.hfirst[s] = kHdsEmptyFirst;
+    d.hcnt[s] = 0;
+    d.hfill[s] = 0;
+  }
+}
+
+// Dense voxels (more than kHdsSmall points): one workgroup each restores the
+// input order of the voxel's segment with an LDS bitmap over its index range
+// (windows of kHdsBits indices; set bits compacted by a block scan — O(points +
+// range/32), exact for any size), then three lanes run the x, y and z
+// recurrences (the same arithmetic as k_hds_mean, bit for bit).
+__global__ void __launch_bounds__(256) k_hds_big(DownsampleBufs d, const int* __restrict__ need) {
+  if (need && !*need) return;
+  const HdsIn a = *d.arg;
+  __shared__ uint32_t bm[kHdsWords];
+  __shared__ int s_w[4], s_base;
+  const int nbig = d.hflags[3];
+  for (int q = blockIdx.x; q < nbig; q += gridDim.x) hds_big_voxel(d, d.bigv[q], a.x, a.y, a.z, a.in, bm, s_w, &s_base);
+}
+
+// The /2 fallback pass of local_mapping.cpp:399-403 as ONE workgroup (it is
+// needed only when the first pass kept fewer than 2000 voxels): the same five
+// steps as k_hds_insert .. k_hds_big, separated by workgroup barriers instead
+// of kernel boundaries, the ranks by a block scan over the points in 1024-point
+// tiles, so the output (order, float means) is bit for bit the multi-kernel
+// pass's. On the common path it is one early-exiting launch instead of six.
+constexpr int kHdsFbThreads = 1024;
+__global__ void __launch_bounds__(kHdsFbThreads) k_hds_fallback(double size, DownsampleBufs d,
+                                                                const int* __restrict__ need) {
+  if (!*need) return;
+  __shared__ uint32_t bm[kHdsWords];
+  __shared__ unsigned long long s_w64[kHdsFbThreads / 64];
+  __shared__ int s_w[kHdsFbThreads / 64], s_base, s_nbig;
+  const HdsIn a = *d.arg;
+  const float *x = a.x, *y = a.y, *z = a.z, *in = a.in;
+  const int n = a.n, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = kHdsFbThreads / 64;
+  // 1. keys, insert-or-find, first index, count (k_hds_insert)
+  for (int i = tid; i < n; i += kHdsFbThreads) {
+    int64_t kx = key_axis_f(x[i], size) + kKeyOff;
+    int64_t ky = key_axis_f(y[i], size) + kKeyOff;
+    int64_t kz = key_axis_f(z[i], size) + kKeyOff;
+    const bool bad = (kx < 0) | (ky < 0) | (kz < 0) | (kx >= 2 * kKeyOff) | (ky >= 2 * kKeyOff) | (kz >= 2 * kKeyOff);
+    if (bad) {
+      atomicOr(&d.hflags[0], 1);
+      kx = ky = kz = 0;
+    }
+    const uint64_t key = ((uint64_t)kx << 42) | ((uint64_t)ky << 21) | (uint64_t)kz;
+    uint32_t s = hds_hash(key, d.hmask);
+    while (true) {
+      const unsigned long long prev =
+          atomicCAS((unsigned long long*)&d.hkey[s], (unsigned long long)kKeyEmpty, (unsigned long long)key);
+      if (prev == kKeyEmpty || prev == key) break;
+      s = (s + 1) & (uint32_t)d.hmask;
+    }
+    atomicMin(&d.hfirst[s], i);
+    atomicAdd(&d.hcnt[s], 1);
+    d.pslot[i] = s;
+  }
+  __syncthreads();
+  // 2. ranks in first-occurrence order and segment offsets (k_hds_tiles + k_hds_rank)
+  int bf = 0, bc = 0;  // first points / points of the earlier tiles
+  for (int t0 = 0; t0 < n; t0 += kHdsFbThreads) {
+    const int i = t0 + tid;
+    int f, c;
+    hds_code(d, i, n, f, c);
+    const unsigned long long v = ((unsigned long long)f << 32) | (unsigned long long)c;
+    unsigned long long xs = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long yv = __shfl_up(xs, o, 64);
+      if (lane >= o) xs += yv;
+    }
+    if (lane == 63) s_w64[wv] = xs;
+    __syncthreads();
+    unsigned long long base = 0, tot = 0;
+    for (int k = 0; k < nw; k++) {
+      if (k < wv) base += s_w64[k];
+      tot += s_w64[k];
+    }
+    const unsigned long long r = base + xs - v;
+    if (f) {
+      const uint32_t s = d.pslot[i];
+      const int rk = bf + (int)(r >> 32);
+      d.hrank[s] = rk;
+      d.hoff[s] = bc + (int)(r & 0xffffffffull);
+      d.vfirst[rk] = i;
+    }
+    bf += (int)(tot >> 32);
+    bc += (int)(tot & 0xffffffffull);
+    __syncthreads();
+  }
+  const int nv = bf;
+  if (tid == 0) {
+    d.hflags[1] = nv;
+    d.hflags[3] = 0;
+    s_nbig = 0;
+  }
+  __syncthreads();
+  // 3. point indices into their voxel's segment (k_hds_scatter)
+  for (int i = tid; i < n; i += kHdsFbThreads) {
+    const uint32_t s = d.pslot[i];
+    const int pos = atomicAdd(&d.hfill[s], 1);
+    d.pseg[d.hoff[s] + pos] = (uint32_t)i;
+  }
+  __syncthreads();
+  // 4. small voxels' means (k_hds_mean); dense ones listed for step 5
+  for (int v = tid; v < nv; v += kHdsFbThreads) {
+    const int i = d.vfirst[v];
+    const uint32_t s = d.pslot[i];
+    const int b = d.hoff[s], cnt = d.hcnt[s];
+    if (cnt > kHdsSmall) {
+      d.bigv[atomicAdd(&s_nbig, 1)] = v;
+      continue;
+    }
+    const uint32_t* sg = d.pseg + b;
+    float px, py, pz, c;
+    if (cnt <= 2) hds_sorted_mean<2>(sg, cnt, x, y, z, px, py, pz, c);
+    else if (cnt <= 4) hds_sorted_mean<4>(sg, cnt, x, y, z, px, py, pz, c);
+    else if (cnt <= 8) hds_sorted_mean<8>(sg, cnt, x, y, z, px, py, pz, c);
+    else hds_sorted_mean<kHdsSmall>(sg, cnt, x, y, z, px, py, pz, c);
+    d.ox[v] = px;
+    d.oy[v] = py;
+    d.oz[v] = pz;
+    d.oi[v] = in ? in[i] : 0.0f;
+    d.oc[v] = c;
+    d.hkey[s] = kKeyEmpty;
+    d.hfirst[s] = kHdsEmptyFirst;
+    d.hcnt[s] = 0;
+    d.hfill[s] = 0;
+  }
+  __syncthreads();
+  // 5. dense voxels, one after the other by the whole workgroup (k_hds_big)
+  const int nbig = s_nbig;
+  for (int q = 0; q < nbig; q++) hds_big_voxel(d, d.bigv[q], x, y, z, in, bm, s_w, &s_base);
 }
 
 // the pipeline's downsample, asynchronous on stream s; with `fallback`, the
@@ -575,16 +703,13 @@ int ds_enqueue_hashed(vg_ctx* ctx, hipStream_t s, const float* x, const float* y
     const int cap = ctx->cap.max_points_per_scan;
     const int g = grid_for(cap, kBlock, 1024), ntile = (cap + kHdsTile - 1) / kHdsTile;
     auto chain = [&](hipStream_t st) {
-      for (int pass = 0; pass < (fallback ? 2 : 1); pass++) {
-        const int* pin = pass ? need : nullptr;
-        const double vs = pass ? voxel / 2 : voxel;
-        k_hds_insert<<<g, kBlock, 0, st>>>(vs, d, pin);
-        k_hds_tiles<<<ntile, kBlock, 0, st>>>(d, pin);
-        k_hds_rank<<<ntile, kBlock, 0, st>>>(d, pin, pass == 0 && fallback ? need : nullptr, 2000);
-        k_hds_scatter<<<g, kBlock, 0, st>>>(d, pin);
-        k_hds_mean<<<g, kBlock, 0, st>>>(d, pin);
-        k_hds_big<<<64, kBlock, 0, st>>>(d, pin);
-      }
+      k_hds_insert<<<g, kBlock, 0, st>>>(voxel, d, nullptr);
+      k_hds_tiles<<<ntile, kBlock, 0, st>>>(d, nullptr);
+      k_hds_rank<<<ntile, kBlock, 0, st>>>(d, nullptr, fallback ? need : nullptr, 2000);
+      k_hds_scatter<<<g, kBlock, 0, st>>>(d, nullptr);
+      k_hds_mean<<<g, kBlock, 0, st>>>(d, nullptr);
+      k_hds_big<<<64, kBlock, 0, st>>>(d, nullptr);
+      if (fallback) k_hds_fallback<<<1, kHdsFbThreads, 0, st>>>(voxel / 2, d, need);
     };
     const bool use_graph = ctx->use_graphs && fallback && voxel == ctx->cfg.down_size;
     if (use_graph && !ctx->g_ds) {

@@ -59,6 +59,11 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(m.wp_var = ctx->arena.take<double>(cw * W * 9));
   good &= ok(m.wp_leaf = ctx->arena.take<int>(cw * W));
   good &= ok(m.wp_int = ctx->arena.take<float>(cw * W));
+  m.ord_stride = (int)(cw * (size_t)(ctx->cfg.max_layer + 1));
+  good &= ok(m.wp_ord = ctx->arena.take<int>((size_t)m.ord_stride * W));
+  good &= ok(m.lseg = ctx->arena.take<uint64_t>(cn * W));
+  good &= ok(m.slot_epoch = ctx->arena.take<int>(kMaxWin));
+  good &= ok(m.arena = ctx->arena.take<int>(kMaxWin));
   good &= ok(ctx->d_cmap = ctx->arena.take<float4>((cw + 2) / 3));
   good &= ok(ctx->d_cmap_n = ctx->arena.take<int>(4));
   good &= ok(m.counters = ctx->arena.take<int>(kCntN));
@@ -72,7 +77,6 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(w.v1 = ctx->arena.take<uint32_t>(w.cap));
   good &= ok(w.u0 = ctx->arena.take<uint32_t>(w.cap));
   good &= ok(w.u1 = ctx->arena.take<uint32_t>(w.cap));
-  good &= ok(w.evsrc = ctx->arena.take<uint32_t>(w.cap));
   good &= ok(w.ac_cnt = ctx->arena.take<uint32_t>(cn));
   good &= ok(w.ac_off = ctx->arena.take<uint32_t>(cn));
   good &= ok(w.cand = ctx->arena.take<int>(cn));
@@ -127,6 +131,7 @@ int map_reset(vg_ctx* ctx) {
     VG_HIP(hipMemsetAsync(m.eig, 0, u * 12 * sizeof(double), s));
     VG_HIP(hipMemsetAsync(m.jour, 0, u * sizeof(double), s));
     VG_HIP(hipMemsetAsync(m.pcrs, 0, u * m.W * sizeof(Clu), s));
+    VG_HIP(hipMemsetAsync(m.lseg, 0, u * m.W * sizeof(uint64_t), s));
   }
   ctx->pool_zeroed = true;
   const size_t hs = (size_t)m.hash_mask + 1;
@@ -136,6 +141,8 @@ int map_reset(vg_ctx* ctx) {
   VG_HIP(hipMemsetAsync(m.counters, 0, kCntN * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.stamp, 0, (size_t)m.cap_nodes * sizeof(int), s));
   VG_HIP(hipMemsetAsync(m.wpn, 0, kMaxWin * sizeof(int), s));
+  VG_HIP(hipMemsetAsync(m.slot_epoch, 0, kMaxWin * sizeof(int), s));
+  VG_HIP(hipMemsetAsync(m.arena, 0, kMaxWin * sizeof(int), s));
   VG_HIP(hipMemsetAsync(ctx->wk.cand_bits, 0, (ctx->cap.max_nodes / 32 + 1) * sizeof(uint32_t), s));
   VG_HIP(hipMemsetAsync(m.in_slide, 0, m.cap_nodes, s));
   VG_HIP(hipMemsetAsync(m.leaf_cnt, 0, (size_t)m.cap_nodes * sizeof(int), s));
@@ -460,6 +467,8 @@ __global__ void __launch_bounds__(256) k_ins_prep(int n_arg, const int* __restri
     m.counters[kCntFixFull] = 0;
     m.counters[kCntNds] = n;
     m.wpn[slot] = n;  // window points of this physical slot (k_make_win)
+    m.slot_epoch[slot] += 1;  // every leaf run of the slot's previous scan is stale now
+    m.arena[slot] = m.cap_wp;
     if (dsf && dsf[0]) {  // the downsample's key-range error (no host wait in between)
       atomicOr(&m.counters[kCntErr], 1);
       dsf[0] = 0;
@@ -902,6 +911,15 @@ __global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __re
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
     const bool listed = m.hdr[leaf].layer < mp.max_layer;
+    if (listed) {  // the leaf's run of this slot (index order), for the recut's subdivisions and the margi
+      int* ord = m.wp_ord + (size_t)slot * m.ord_stride + j0;
+      if (L <= 64) {
+        if (lane < L) ord[lane] = mine;
+      } else {
+        for (int e = lane; e < L; e += 64) ord[e] = order2[j0 + e];
+      }
+      if (lane == 0) m.lseg[(size_t)leaf * mp.W + slot] = lseg_pack(j0, L, m.slot_epoch[slot]);
+    }
     Clu* loc = &m.pcrs[(size_t)leaf * mp.W + slot];
     Clu* add = &m.pcr_add[leaf];
     double* acc_p = role < 0 ? nullptr
@@ -1075,12 +1093,6 @@ static int read_counters(vg_ctx* ctx) {
 // stable, so keys (leaf << 27 | index) generated in index order need only
 // their leaf bits sorted (3 passes instead of 7) to come out ordered by
 // (leaf, index).
-static int sort_keys(vg_ctx* ctx, const uint64_t* in, uint64_t* out, int n, int end_bit, int begin_bit = 0) {
-  size_t tb = ctx->wk.tmp_bytes;
-  if (n <= 0) return VG_OK;
-  VG_HIP(hipcub::DeviceRadixSort::SortKeys(ctx->wk.tmp, tb, in, out, n, begin_bit, end_bit, ctx->stream));
-  return VG_OK;
-}
 static int excl_scan(vg_ctx* ctx, const uint32_t* in, uint32_t* out, int n) {
   size_t tb = ctx->wk.tmp_bytes;
   if (n <= 0) return VG_OK;
@@ -1222,7 +1234,6 @@ int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num
 enum { kRcLvl = 0, kRcSub = 16, kRcWin = 32, kRcAbort = 48, kRcCh = 64, kRcChBase = 80, kRcStatus = 126, kRcNOld = 127,
        kRcN = 128 };
 constexpr int kApplyThreads = 1024;
-constexpr int kApplyEv = 4096;   // events sorted in LDS
 constexpr int kApplySub = kApplyThreads;  // subdividing leaves per level (one lane each)
 
 // visit one worklist entry; returns children / candidate / subdivide flags
@@ -1284,47 +1295,116 @@ __global__ void __launch_bounds__(256) k_rc_visit(int L, int thread_num, const i
   }
 }
 
-// window points of every frame that sit in a subdividing leaf (subdivide,
-// octree.cpp:279-300): event (leaf, octant, 1 + ord) with source index
-__device__ __forceinline__ bool win_event(int g, int cap_wp, const int* nper, const int* slot_of, const WinD* win,
-                                          DevMap& m, int& leaf, int& o, int& ord, int& i) {
-  ord = 0;
-  i = g;
-  while (ord < win->win_count && i >= nper[ord]) {
-    i -= nper[ord];
-    ord++;
+// The points of every subdividing leaf (subdivide / fix_divide, octree.cpp:
+// 257-300), one wave per leaf: its point_fix list, then its run of each
+// window slot (DevMap::lseg) in frame order. Pass 1 finds each point's octant
+// and counts per octant; pass 2 writes the events of each octant into their
+// own range of the leaf's block of the event list, in walk order, so a child's
+// events come out grouped and already in the reference's push order (point_fix
+// by index, then frame by frame, index ascending) — no sort. Event: phase << 21
+// | index (phase 0 point_fix, 1 + ord a window frame). rcinfo[17 q ..]: the
+// block's start, then per octant its offset and count; nscr[leaf*4+0] = q.
+constexpr int kRcWinWaves = 4;
+constexpr int kRcInfo = 17;
+// point e of the leaf's walk (fixed points, then the window's runs in
+// order), its phase located among the wave's per-phase run starts (lane ph
+// holds phase ph's exclusive start ex, run start st and slot)
+__device__ __forceinline__ int rc_walk_octant(const NodeHdr& h, int e, int wc, int ex, int st, int slot,
+                                              const WinD* win, const DevMap& m, int& ph, int& idx) {
+  ph = 0;
+#pragma unroll
+  for (int step = 32; step >= 1; step >>= 1) {
+    const int cand = ph + step;
+    const int v = __shfl(ex, cand <= wc ? cand : wc, 64);
+    if (cand <= wc && v <= e) ph = cand;
   }
-  if (ord >= win->win_count) return false;
-  const size_t b = (size_t)slot_of[ord] * cap_wp + i;
-  const int l = m.wp_leaf[b];
-  if (l < 0 || m.nscr[(size_t)l * 4 + 2] != 1) return false;
-  leaf = l;
-  const NodeHdr& h = m.hdr[leaf];
-  V3 pw = rigid(ld_m3(win->R[ord]), ld_v3(&m.wp_pnt[b * 3]), ld_v3(win->p[ord]));
-  o = octant(pw, h.center);
-  m.cfirst[(size_t)leaf * 8 + o] = -5;
-  return true;
+  const int loc = e - __shfl(ex, ph, 64);
+  const int pst = __shfl(st, ph, 64), psl = __shfl(slot, ph, 64);
+  if (ph == 0) {
+    idx = loc;
+    return octant(ld_v3(&m.fix_pnt[((size_t)h.fix_off + loc) * 3]), h.center);
+  }
+  idx = m.wp_ord[(size_t)psl * m.ord_stride + pst + loc];
+  const V3 pw = rigid(ld_m3(win->R[ph - 1]), ld_v3(&m.wp_pnt[((size_t)psl * m.cap_wp + idx) * 3]), ld_v3(win->p[ph - 1]));
+  return octant(pw, h.center);
 }
-
-__global__ void __launch_bounds__(256) k_rc_win(int L, const int* __restrict__ total_p, int cap_wp,
-                                                const int* __restrict__ nper,
-                                                const int* __restrict__ slot_of, const WinD* __restrict__ win,
-                                                DevMap m, uint64_t* __restrict__ ev, uint32_t* __restrict__ evsrc,
-                                                int cap, int* __restrict__ rc) {
-  if (rc[kRcAbort] || rc[kRcSub + L] == 0) return;
-  const int total = *total_p;  // k_make_win
-  for (int base = blockIdx.x * blockDim.x; base < total; base += gridDim.x * blockDim.x) {
-    const int g = base + threadIdx.x;
-    int leaf = -1, o = 0, ord = 0, i = 0;
-    const bool hit = g < total && win_event(g, cap_wp, nper, slot_of, win, m, leaf, o, ord, i);
-    const int pos = wave_append(&rc[kRcWin + L], hit ? 1 : 0);
-    if (hit) {
-      if (pos < cap) {
-        ev[pos] = ((uint64_t)leaf << 27) | ((uint64_t)o << 24) | (uint64_t)(1 + ord);
-        evsrc[pos] = (uint32_t)i;
-      } else {
-        atomicOr(&m.counters[kCntErr], 16);
+// one wave per subdividing leaf: the leaf's points are flattened across the
+// phases so each 64-point chunk costs one round of loads whatever the runs'
+// lengths; pass 1 counts the octants, pass 2 writes each octant's events
+// (ph << 21 | idx) at its running position, walk order kept
+__global__ void __launch_bounds__(64 * kRcWinWaves) k_rc_win(int L, const int* __restrict__ sub,
+                                                             const WinD* __restrict__ win, DevMap m,
+                                                             uint64_t* __restrict__ ev, int* __restrict__ rcinfo,
+                                                             int cap, int info_cap, int* __restrict__ rc) {
+  if (rc[kRcAbort]) return;
+  const int nsub = rc[kRcSub + L];
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int wc = win->win_count;
+  if (wc > 63) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) atomicOr(&m.counters[kCntErr], 16);
+    return;
+  }
+  const int my_slot = (lane >= 1 && lane <= wc) ? win->mp[lane - 1] : 0;
+  for (int q = blockIdx.x * kRcWinWaves + (threadIdx.x >> 6); q < nsub; q += gridDim.x * kRcWinWaves) {
+    const int leaf = sub[q];
+    const NodeHdr& h = m.hdr[leaf];
+    int len = 0, st = 0;
+    if (lane == 0) len = h.fix_cnt;
+    else if (lane <= wc && !lseg_get(m, leaf, my_slot, st, len)) len = 0;
+    int ex = len;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(ex, off, 64);
+      if (lane >= off) ex += y;
+    }
+    const int total = __shfl(ex, 63, 64);
+    ex -= len;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(&rc[kRcWin + L], total);
+    base = __shfl(base, 0, 64);
+    if ((size_t)q * kRcInfo + kRcInfo > (size_t)info_cap || base + total > cap) {
+      if (lane == 0) atomicOr(&m.counters[kCntErr], 16);
+      continue;
+    }
+    int cnt8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int e0 = 0; e0 < total; e0 += 64) {
+      const int e = e0 + lane;
+      int ph, idx;
+      int o = rc_walk_octant(h, e < total ? e : total - 1, wc, ex, st, my_slot, win, m, ph, idx);
+      if (e < total) m.cfirst[(size_t)leaf * 8 + o] = -5;
+      else o = -1;
+#pragma unroll
+      for (int k = 0; k < 8; k++) cnt8[k] += __popcll(__ballot(o == k));
+    }
+    int off8[8], run = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      off8[k] = run;
+      run += cnt8[k];
+    }
+    if (lane == 0) {
+      int* inf = rcinfo + (size_t)q * kRcInfo;
+      inf[0] = base;
+      for (int k = 0; k < 8; k++) {
+        inf[1 + k] = off8[k];
+        inf[9 + k] = cnt8[k];
       }
+      m.nscr[(size_t)leaf * 4 + 0] = q;
+    }
+    for (int e0 = 0; e0 < total; e0 += 64) {
+      const int e = e0 + lane;
+      int ph, idx;
+      int o = rc_walk_octant(h, e < total ? e : total - 1, wc, ex, st, my_slot, win, m, ph, idx);
+      if (e >= total) o = -1;
+      int pos = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint64_t bk = __ballot(o == k);
+        if (o == k) pos = base + off8[k] + __popcll(bk & below);
+        off8[k] += __popcll(bk);
+      }
+      if (o >= 0) ev[pos] = ((uint64_t)ph << 21) | (uint64_t)idx;
     }
   }
 }
@@ -1334,77 +1414,6 @@ __global__ void __launch_bounds__(256) k_child_alloc(int np, const int* __restri
   const int base = m.counters[kCntNodes];
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < np; q += gridDim.x * blockDim.x)
     alloc_parent(m, parents[q], base + (int)off[q], next, next_base + (int)off[q]);
-}
-
-// apply the sorted pushes of one child (keys[j, jend)), in the reference's
-// order: fix points first (push_fix, octree.cpp:179-188), then window points
-// frame by frame (push, octree.cpp:151-177)
-__device__ void push_child(const uint64_t* keys, int j, int jend, const MP& mp, const WinD* win, DevMap& m) {
-  const int child = (int)(keys[j] >> 27);
-  NodeHdr& h = m.hdr[child];
-  const NodeHdr& ph = m.hdr[h.parent];
-  const bool listed = h.layer < mp.max_layer;
-  int nfix = 0;
-  for (int jj = j; jj < jend; jj++)
-    if (((keys[jj] >> 21) & 63) == 0) nfix++;
-  if (nfix > 0 && listed) {
-    int off = atomicAdd(&m.counters[kCntFix], nfix);
-    if (off + nfix > m.cap_fix) {
-      atomicOr(&m.counters[kCntErr], 8);
-      return;
-    }
-    h.fix_off = off;
-    h.fix_cap = nfix;
-    h.fix_cnt = 0;
-  }
-  Clu add_ = m.pcr_add[child];
-  Clu fix_ = m.pcr_fix[child];
-  double cov[kCovN];
-  for (int t = 0; t < kCovN; t++) cov[t] = m.cov_add[(size_t)child * kCovN + t];
-  int cur_slot = -1;
-  Clu loc;
-  clu_zero(loc);
-  for (int jj = j; jj < jend; jj++) {
-    const uint64_t k = keys[jj];
-    const int phase = (int)((k >> 21) & 63);
-    const int idx = (int)(k & ((1u << 21) - 1));
-    if (phase == 0) {
-      const size_t f = (size_t)ph.fix_off + idx;
-      V3 pt = ld_v3(&m.fix_pnt[f * 3]);
-      M3 var = ld_m3(&m.fix_var[f * 9]);
-      if (listed) {
-        const size_t d = (size_t)h.fix_off + h.fix_cnt;
-        for (int t = 0; t < 3; t++) m.fix_pnt[d * 3 + t] = pt[t];
-        for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = var[t];
-        h.fix_cnt++;
-      }
-      clu_push(fix_, pt);
-      clu_push(add_, pt);
-      bf_var_acc(cov, var, pt);
-    } else {
-      const int ord = phase - 1;
-      const int slot = win->mp[ord];
-      if (slot != cur_slot) {
-        if (cur_slot >= 0) m.pcrs[(size_t)child * mp.W + cur_slot] = loc;
-        cur_slot = slot;
-        loc = m.pcrs[(size_t)child * mp.W + slot];
-      }
-      const size_t b = (size_t)slot * m.cap_wp + idx;
-      V3 pnt = ld_v3(&m.wp_pnt[b * 3]);
-      M3 var = ld_m3(&m.wp_var[b * 9]);
-      V3 pw = rigid(ld_m3(win->R[ord]), pnt, ld_v3(win->p[ord]));
-      h.has_sw = 1;
-      h.isexist = 1;
-      m.wp_leaf[b] = listed ? child : -1;
-      clu_push(loc, pnt);
-      clu_push(add_, pw);
-      bf_var_acc(cov, var, pw);
-    }
-  }
-  if (cur_slot >= 0) m.pcrs[(size_t)child * mp.W + cur_slot] = loc;
-  m.pcr_add[child] = add_;
-  m.pcr_fix[child] = fix_;
-  for (int t = 0; t < kCovN; t++) m.cov_add[(size_t)child * kCovN + t] = cov[t];
 }
 
 // finish a subdivided parent: release its SlideWindow, free point_fix,
@@ -1419,27 +1428,37 @@ __device__ __forceinline__ void sub_finish(DevMap& m, int p) {
   m.nscr[(size_t)p * 4 + 2] = -1;
 }
 
-__global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int ev_cap, MP mp, const WinD* __restrict__ win,
-                                                            DevMap m, int* __restrict__ next, const int* __restrict__ sub,
-                                                            const uint64_t* __restrict__ wev,
-                                                            const uint32_t* __restrict__ wsrc,
-                                                            uint64_t* __restrict__ keys_out, int* __restrict__ cseg,
+// one workgroup: the subdividing leaves in ascending id order (deterministic
+// child ids), their marked octants' children allocated as one block (base +
+// prefix), each child's event range from k_rc_win's per-octant blocks
+// (cseg), the parents finished. More subdividing leaves than the workgroup's
+// lanes (or than the test knob sub_cap) hand the level to the host-sized path.
+__device__ __forceinline__ void rc_child_segs(const DevMap& m, int p, int c0, const int* __restrict__ rcinfo,
+                                              int* __restrict__ cseg) {
+  const int* inf = rcinfo + (size_t)m.nscr[(size_t)p * 4 + 0] * kRcInfo;
+  int k = 0;
+  for (int o = 0; o < 8; o++) {
+    if (m.hdr[p].child[o] < 0 || inf[9 + o] == 0) continue;
+    cseg[2 * (c0 + k)] = inf[0] + inf[1 + o];
+    cseg[2 * (c0 + k) + 1] = inf[0] + inf[1 + o] + inf[9 + o];
+    k++;
+  }
+}
+__global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int sub_cap, DevMap m, int* __restrict__ next,
+                                                            const int* __restrict__ sub,
+                                                            const int* __restrict__ rcinfo, int* __restrict__ cseg,
                                                             int* __restrict__ rc) {
-  __shared__ uint64_t s_ev[kApplyEv];
-  __shared__ int s_sub[kApplySub], s_foff[kApplySub], s_coff[kApplySub];
+  __shared__ int s_sub[kApplySub];
   __shared__ int s_wsum[32];
-  __shared__ int s_meta[4];
   const int tid = threadIdx.x;
   if (rc[kRcAbort]) return;
   const int nsub = rc[kRcSub + L];
   if (nsub == 0) return;
   VG_PROBE_BEGIN();
-  const int nwin = rc[kRcWin + L];
-  if (nsub > kApplySub) {
+  if (nsub > sub_cap) {
     if (tid == 0) rc[kRcAbort] = L + 1;
     return;
   }
-  // sorted subdividing leaves (ascending id: deterministic child ids)
   int myp = tid < nsub ? sub[tid] : 0x7fffffff;
   {
     int rank = 0;
@@ -1449,95 +1468,30 @@ __global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int ev_cap, M
   }
   __syncthreads();
   const int p_t = tid < nsub ? s_sub[tid] : -1;
-  int nfix;
-  const int foff = block_excl_scan(p_t >= 0 ? m.hdr[p_t].fix_cnt : 0, s_wsum, &nfix);
-  if (tid < nsub) s_foff[tid] = foff;
-  if (nfix + nwin > ev_cap) {
-    if (tid == 0) rc[kRcAbort] = L + 1;  // uniform: every lane saw the same totals
-    return;
-  }
-  __syncthreads();
-  // fix events (fix_divide, octree.cpp:257-277): (parent, octant, j) at foff + j
-  for (int e = tid; e < nfix; e += blockDim.x) {
-    int lo = 0, hi = nsub - 1;  // last q with s_foff[q] <= e
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_foff[mid] <= e) lo = mid;
-      else hi = mid - 1;
-    }
-    const int p = s_sub[lo], j = e - s_foff[lo];
-    const NodeHdr& h = m.hdr[p];
-    V3 pt = ld_v3(&m.fix_pnt[((size_t)h.fix_off + j) * 3]);
-    const int o = octant(pt, h.center);
-    m.cfirst[(size_t)p * 8 + o] = -5;
-    s_ev[e] = ((uint64_t)p << 27) | ((uint64_t)o << 24) | (uint64_t)j;
-  }
-  for (int e = tid; e < nwin; e += blockDim.x) s_ev[nfix + e] = wev[e];
-  __syncthreads();
-  VG_PROBE_MARK(16);
-  // children: per parent the marked octants, ids base + prefix (k_child_count/alloc)
   int cc = 0;
   if (p_t >= 0)
     for (int o = 0; o < 8; o++) cc += (m.cfirst[(size_t)p_t * 8 + o] == -5) ? 1 : 0;
   int ntot;
   const int coff = block_excl_scan(cc, s_wsum, &ntot);
-  if (tid < nsub) s_coff[tid] = coff;
   const int base = m.counters[kCntNodes];
   const int nnext = rc[kRcLvl + L];
   __syncthreads();
-  if (p_t >= 0) alloc_parent(m, p_t, base + coff, next, nnext + coff);
+  if (p_t >= 0) {
+    alloc_parent(m, p_t, base + coff, next, nnext + coff);
+    rc_child_segs(m, p_t, coff, rcinfo, cseg);
+  }
   __syncthreads();
   if (tid == 0) {
     m.counters[kCntNodes] = base + ntot;
     rc[kRcLvl + L] = nnext + ntot;
-  }
-  VG_PROBE_MARK(17);
-  // sort keys (child << 27 | phase << 21 | idx)
-  const int ne = nfix + nwin;
-  int npad = 2;
-  while (npad < ne) npad <<= 1;
-  for (int e = tid; e < npad; e += blockDim.x) {
-    if (e >= ne) {
-      s_ev[e] = ~0ull;
-      continue;
-    }
-    const uint64_t v = s_ev[e];
-    const int p = (int)(v >> 27), o = (int)((v >> 24) & 7), lo = (int)(v & 0xffffff);
-    const int child = m.hdr[p].child[o];
-    uint64_t phase, idx;
-    if (e < nfix) {
-      phase = 0;
-      idx = (uint64_t)lo;
-    } else {
-      phase = (uint64_t)lo;  // 1 + ord
-      idx = wsrc[e - nfix];
-    }
-    s_ev[e] = ((uint64_t)child << 27) | (phase << 21) | idx;
-  }
-  __syncthreads();
-  VG_PROBE_MARK(18);
-  lds_bitonic(s_ev, npad);
-  VG_PROBE_MARK(19);
-  // sorted keys and the per-child segments [start, end) for k_rc_push
-  for (int e = tid; e < ne; e += blockDim.x) {
-    const uint64_t k = s_ev[e];
-    const int c = (int)(k >> 27) - base;
-    keys_out[e] = k;
-    if (e == 0 || (int)(s_ev[e - 1] >> 27) != c + base) cseg[2 * c] = e;
-    if (e == ne - 1 || (int)(s_ev[e + 1] >> 27) != c + base) cseg[2 * c + 1] = e + 1;
-  }
-  if (tid == 0) {
     rc[kRcCh + L] = ntot;
     rc[kRcChBase + L] = base;
   }
-  __syncthreads();
-  VG_PROBE_MARK(20);
   if (p_t >= 0) sub_finish(m, p_t);
-  VG_PROBE_MARK(21);
+  VG_PROBE_MARK(17);
 #ifdef VG_PROBE
   if (tid == 0) atomicAdd(&g_probe[62], 1ull);
 #endif
-  (void)s_meta;
 }
 
 // pushes of one level's children (push_fix then push per frame, octree.cpp:
@@ -1594,6 +1548,37 @@ __global__ void __launch_bounds__(64 * kRcPushWaves) k_rc_push(int L, const uint
       fix_off = __shfl(off, 0, 64);
       if (fix_off < 0) continue;
     }
+    // the child's run of each window slot (its events of phase 1 + ord are
+    // contiguous and in index order): lane p < win_count finds phase p + 1's
+    // range by binary search and takes the run from the slot's arena
+    int run_lo = 0, run_st = 0;
+    if (listed) {
+      const int wc = win->win_count;
+      if (lane < wc) {
+        const uint64_t base = 0;  // a child's events: phase << 21 | index, ascending
+        auto lower = [&](uint64_t key) {
+          int lo = j0, hi = j1;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (keys[mid] < key) lo = mid + 1;
+            else hi = mid;
+          }
+          return lo;
+        };
+        run_lo = lower(base | ((uint64_t)(lane + 1) << 21));
+        const int cnt = lower(base | ((uint64_t)(lane + 2) << 21)) - run_lo;
+        if (cnt > 0) {
+          const int slot = win->mp[lane];
+          run_st = atomicAdd(&m.arena[slot], cnt);
+          if (run_st + cnt > m.ord_stride) {
+            atomicOr(&m.counters[kCntErr], 16);
+            run_st = 0;
+          } else {
+            m.lseg[(size_t)child * mp.W + slot] = lseg_pack(run_st, cnt, m.slot_epoch[slot]);
+          }
+        }
+      }
+    }
     auto acc_ptr = [&](int r, int slot) -> double* {
       if (r < 9) return r < 6 ? &m.pcr_add[child].P[r] : &m.pcr_add[child].v[r - 6];
       if (r < 18) return r < 15 ? &m.pcr_fix[child].P[r - 9] : &m.pcr_fix[child].v[r - 15];
@@ -1628,6 +1613,13 @@ __global__ void __launch_bounds__(64 * kRcPushWaves) k_rc_push(int L, const uint
           s_slot[wv][lane] = slot;
           m.wp_leaf[bb] = listed ? child : -1;
         }
+      }
+      if (listed) {  // the point into the child's run (ds_bpermute of the run's lane; uniform call)
+        const int e = b0 + lane;
+        const int ph = e < j1 ? (int)((keys[e] >> 21) & 63) : 0;
+        const int src = ph > 0 ? ph - 1 : 0;
+        const int lo_p = __shfl(run_lo, src, 64), st_p = __shfl(run_st, src, 64);
+        if (ph > 0) m.wp_ord[(size_t)win->mp[ph - 1] * m.ord_stride + st_p + (e - lo_p)] = (int)(keys[e] & ((1u << 21) - 1));
       }
       const int nb = (j1 - b0) < 64 ? (j1 - b0) : 64;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1678,58 +1670,13 @@ __global__ void __launch_bounds__(64 * kRcPushWaves) k_rc_push(int L, const uint
 }
 
 // ---- host-sized path (overflow replay) ----------------------------------
-__global__ void __launch_bounds__(256) k_sub_fix_events(int ns, const int* __restrict__ sub, DevMap m,
-                                                        uint64_t* __restrict__ ev, int cap) {
-  for (int base = blockIdx.x * blockDim.x; base < ns; base += gridDim.x * blockDim.x) {
-    const int q = base + threadIdx.x;
-    const int p = q < ns ? sub[q] : -1;
-    const int cnt = p >= 0 ? m.hdr[p].fix_cnt : 0;
-    int pos = wave_append(&m.counters[kCntEvents], cnt);
-    if (p < 0) continue;
-    const NodeHdr& h = m.hdr[p];
-    for (int j = 0; j < cnt; j++, pos++) {
-      size_t f = (size_t)h.fix_off + j;
-      V3 pt = ld_v3(&m.fix_pnt[f * 3]);
-      int o = octant(pt, h.center);
-      m.cfirst[(size_t)p * 8 + o] = -5;
-      if (pos < cap) ev[pos] = ((uint64_t)p << 27) | ((uint64_t)o << 24) | (uint64_t)j;
-    }
-  }
+// the children's event ranges of the sorted parents (ids c0 + prefix, as
+// alloc_children handed them out)
+__global__ void __launch_bounds__(256) k_sub_cseg(int ns, const int* __restrict__ sub, const uint32_t* __restrict__ off,
+                                                  DevMap m, const int* __restrict__ rcinfo, int* __restrict__ cseg) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ns; q += gridDim.x * blockDim.x)
+    rc_child_segs(m, sub[q], (int)off[q], rcinfo, cseg);
 }
-
-// events at [0, fix_begin) come from the window, [fix_begin, ne) from point_fix
-__global__ void __launch_bounds__(256) k_sub_keys(int ne, const uint64_t* __restrict__ ev,
-                                                  const uint32_t* __restrict__ evsrc, DevMap m,
-                                                  uint64_t* __restrict__ keys, int fix_begin) {
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += gridDim.x * blockDim.x) {
-    uint64_t v = ev[e];
-    int p = (int)(v >> 27);
-    int o = (int)((v >> 24) & 7);
-    int lo = (int)(v & 0xffffff);
-    int child = m.hdr[p].child[o];
-    uint64_t phase, idx;
-    if (e >= fix_begin) {
-      phase = 0;
-      idx = (uint64_t)lo;
-    } else {
-      phase = (uint64_t)lo;  // 1 + ord
-      idx = evsrc[e];
-    }
-    keys[e] = ((uint64_t)child << 27) | (phase << 21) | idx;
-  }
-}
-
-__global__ void __launch_bounds__(256) k_push_events(int ne, const uint64_t* __restrict__ keys, MP mp,
-                                                     WinD* __restrict__ win, DevMap m) {
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < ne; j += gridDim.x * blockDim.x) {
-    int child = (int)(keys[j] >> 27);
-    if (j > 0 && (int)(keys[j - 1] >> 27) == child) continue;
-    int jend = j + 1;
-    while (jend < ne && (int)(keys[jend] >> 27) == child) jend++;
-    push_child(keys, j, jend, mp, win, m);
-  }
-}
-
 __global__ void __launch_bounds__(256) k_sub_finish(int ns, const int* __restrict__ sub, DevMap m) {
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ns; q += gridDim.x * blockDim.x) sub_finish(m, sub[q]);
 }
@@ -1751,32 +1698,25 @@ static int read_rc(vg_ctx* ctx, int* h) {
   return read_counters(ctx);  // synchronizes
 }
 
-// host-sized apply of level L (visit and window events already ran)
+// host-sized apply of level L (k_rc_visit and k_rc_win already ran): sorted
+// subdividing leaves, host-sized child allocation, the children's event
+// ranges, then the device pushes (k_rc_push) and the parents' finish
 static int recut_slow_apply(vg_ctx* ctx, int L, const MP& mp, WinD* dwin, int* next, int* hrc) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream;
-  const int nsub = hrc[kRcSub + L], nwin = hrc[kRcWin + L], nnext = hrc[kRcLvl + L];
+  const int nsub = hrc[kRcSub + L], nnext = hrc[kRcLvl + L];
   if (nsub <= 0) return VG_OK;
-  if (nwin > w.cap) {
-    ctx->err = "subdivision event buffer overflow";
-    return VG_E_CAPACITY;
-  }
   VG_TRY(sort_ids_inplace(ctx, w.list2, nsub));
-  VG_HIP(hipMemsetD32Async((hipDeviceptr_t)(m.counters + kCntEvents), nwin, 1, s));
-  k_sub_fix_events<<<grid_for(nsub), kBlock, 0, s>>>(nsub, w.list2, m, w.k0, w.cap);
   VG_TRY(read_counters(ctx));
-  const int ne = ctx->h_pinned[kCntEvents];
-  if (ne > w.cap) {
-    ctx->err = "subdivision event buffer overflow";
-    return VG_E_CAPACITY;
-  }
+  const int first = ctx->h_pinned[kCntNodes];
   int created = 0;
   VG_TRY(alloc_children(ctx, w.list2, nsub, next, nnext, true, &created));
+  k_sub_cseg<<<grid_for(nsub), kBlock, 0, s>>>(nsub, w.list2, w.ac_off, m, (const int*)w.v1, (int*)w.ac_cnt);
   VG_HIP(hipMemsetD32Async((hipDeviceptr_t)(w.rc + kRcLvl + L), nnext + created, 1, s));
-  k_sub_keys<<<grid_for(ne), kBlock, 0, s>>>(ne, w.k0, w.evsrc, m, w.k1, nwin);
-  VG_TRY(sort_keys(ctx, w.k1, w.k0, ne, 27 + bits_for(ctx->h_pinned[kCntNodes])));
-  k_push_events<<<grid_for(ne), kBlock, 0, s>>>(ne, w.k0, mp, dwin, m);
+  VG_HIP(hipMemsetD32Async((hipDeviceptr_t)(w.rc + kRcCh + L), created, 1, s));
+  VG_HIP(hipMemsetD32Async((hipDeviceptr_t)(w.rc + kRcChBase + L), first, 1, s));
+  k_rc_push<<<256, 64 * kRcPushWaves, 0, s>>>(L, w.k0, (const int*)w.ac_cnt, mp, dwin, m, w.rc);
   k_sub_finish<<<grid_for(nsub), kBlock, 0, s>>>(nsub, w.list2, m);
   VG_HIP(hipGetLastError());
   return read_counters(ctx);
@@ -1885,9 +1825,7 @@ static int recut_complete(vg_ctx* ctx, const MP& mp, int nlev, int* hrc, int* n_
     for (int L = L0 + 1; L < nlev; L++) {
       k_rc_visit<<<256, kBlock, 0, s>>>(L, ctx->rc_thread_num, list_of(L), mp, m, list_of(L + 1), w.list2, w.cand,
                                         w.rc, nullptr);
-      if (total > 0)
-        k_rc_win<<<grid_for(total), kBlock, 0, s>>>(L, dn + 64, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc,
-                                                     w.cap, w.rc);
+      k_rc_win<<<256, 64 * kRcWinWaves, 0, s>>>(L, w.list2, dwin, m, w.k0, (int*)w.v1, w.cap, w.cap, w.rc);
       VG_TRY(read_rc(ctx, hrc));
       VG_TRY(recut_slow_apply(ctx, L, mp, dwin, list_of(L + 1), hrc));
     }
@@ -1941,18 +1879,17 @@ static int map_recut_impl(vg_ctx* ctx, const MP& mp, const WinArg& wa, int threa
   const int nlev = mp.max_layer + 1;  // children sit one layer down; leaves at max_layer do not subdivide
   auto list_of = [&](int L) { return (L % 2 == 1) ? w.list0 : w.list1; };  // worklist of level L >= 1
   const int gv = 256, gw = grid_for(total > 0 ? total : 1, kBlock, 2048);  // grid-stride over the device total
-  const int ev_cap = (ctx->dbg_apply_cap >= 0 && ctx->dbg_apply_cap < kApplyEv) ? ctx->dbg_apply_cap : kApplyEv;
+  const int sub_cap = (ctx->dbg_apply_cap >= 0 && ctx->dbg_apply_cap < kApplySub) ? ctx->dbg_apply_cap : kApplySub;
   for (int L = 0; L < nlev; L++) {
     k_rc_visit<<<gv, kBlock, 0, s>>>(L, thread_num, L > 0 ? list_of(L) : nullptr, mp, m, list_of(L + 1), w.list2,
                                      w.cand, w.rc, pub_seq > 0 ? w.cand_bits : nullptr);
     // nodes at layer max_layer never subdivide (recut_visit_node, octree.cpp:371-372):
     // the deepest level has no window events, no apply and no pushes
     if (L == mp.max_layer) break;
-    if (total > 0)
-      k_rc_win<<<gw, kBlock, 0, s>>>(L, dn + 64, m.cap_wp, dn, dslot, dwin, m, w.k0, w.evsrc, w.cap, w.rc);
-    k_rc_apply<<<1, kApplyThreads, 0, s>>>(L, ev_cap, mp, dwin, m, list_of(L + 1), w.list2, w.k0, w.evsrc, w.k1,
-                                           (int*)w.ac_off, w.rc);
-    k_rc_push<<<64, 64 * kRcPushWaves, 0, s>>>(L, w.k1, (const int*)w.ac_off, mp, dwin, m, w.rc);
+    k_rc_win<<<256, 64 * kRcWinWaves, 0, s>>>(L, w.list2, dwin, m, w.k0, (int*)w.v1, w.cap, w.cap, w.rc);
+    k_rc_apply<<<1, kApplyThreads, 0, s>>>(L, sub_cap, m, list_of(L + 1), w.list2, (const int*)w.v1, (int*)w.ac_off,
+                                           w.rc);
+    k_rc_push<<<64, 64 * kRcPushWaves, 0, s>>>(L, w.k0, (const int*)w.ac_off, mp, dwin, m, w.rc);
   }
   VG_HIP(hipGetLastError());
   if (pub_seq > 0) {
@@ -2040,26 +1977,6 @@ __global__ void __launch_bounds__(256) k_collect_level(int L, int thread_num, De
   }
 }
 
-// oldest-slot point segments per leaf: seg start/count in nscr[.*4+0/1]
-__global__ void __launch_bounds__(256) k_margi_keys(int n, int slot, DevMap m, uint64_t* __restrict__ keys) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    int l = m.wp_leaf[(size_t)slot * m.cap_wp + i];
-    keys[i] = l >= 0 ? (((uint64_t)l << 27) | (uint64_t)i) : ~0ull;
-  }
-}
-__global__ void __launch_bounds__(256) k_margi_segs(int n, const uint64_t* __restrict__ keys, DevMap m) {
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-    uint64_t k = keys[j];
-    if (k == ~0ull) continue;
-    int l = (int)(k >> 27);
-    if (j > 0 && keys[j - 1] != ~0ull && (int)(keys[j - 1] >> 27) == l) continue;
-    int c = 0;
-    while (j + c < n && keys[j + c] != ~0ull && (int)(keys[j + c] >> 27) == l) c++;
-    m.nscr[(size_t)l * 4 + 0] = j;
-    m.nscr[(size_t)l * 4 + 1] = c;
-  }
-}
-
 __device__ void plane_update_dev(DevMap& m, int node, const Clu& pcr_add, const double* e) {
   PlaneRec& P = m.pl[node];
   V3 center = v3(pcr_add.v[0] / pcr_add.N, pcr_add.v[1] / pcr_add.N, pcr_add.v[2] / pcr_add.N);
@@ -2104,9 +2021,9 @@ __device__ void plane_update_dev(DevMap& m, int node, const Clu& pcr_add, const 
   P.radius = (float)e[2];
 }
 
-// OctoTree::margi leaf branch (octree.cpp:397-484), mgsize = 1. keys = the
-// oldest slot's listed points sorted by (leaf, index): each leaf's segment is
-// its sw->points[mp[0]] list in push order.
+// OctoTree::margi leaf branch (octree.cpp:397-484), mgsize = 1. A leaf's
+// run of the oldest slot (DevMap::lseg) is its sw->points[mp[0]] list in push
+// order.
 __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nleaves, const int* __restrict__ leaves,
                                                     MP mp, WinD* __restrict__ win, DevMap m,
                                                     const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
@@ -2120,12 +2037,11 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
     int* pq = &plan[(size_t)q * 8];
     pq[0] = -1;  // no point_fix copies (k_margi_copy)
     pq[4] = 0;
-    int seg = m.nscr[(size_t)node * 4 + 0], segn = m.nscr[(size_t)node * 4 + 1];
-    m.nscr[(size_t)node * 4 + 0] = -1;
-    m.nscr[(size_t)node * 4 + 1] = -1;
     if (!h.isexist || !h.has_sw) continue;
     const int W = mp.W;
     const int s0 = win->mp[0];
+    int seg = -1, segn = 0;  // the leaf's run of the oldest slot: its sw->points[mp[0]] in push order
+    if (!lseg_get(m, node, s0, seg, segn)) seg = -1;
     Clu* loc = &m.pcrs[(size_t)node * W];
     const M3 R0 = ld_m3(win->R[0]);
     const V3 p0 = ld_v3(win->p[0]);
@@ -2206,7 +2122,6 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
 constexpr int kCopyWaves = 4;
 __global__ void __launch_bounds__(64 * kCopyWaves) k_margi_copy(const int* __restrict__ nleaves,
                                                                 const int* __restrict__ plan,
-                                                                const uint64_t* __restrict__ keys,
                                                                 const WinD* __restrict__ win, DevMap m, const int* __restrict__ gate) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   const int lane = threadIdx.x & 63;
@@ -2228,7 +2143,7 @@ __global__ void __launch_bounds__(64 * kCopyWaves) k_margi_copy(const int* __res
     if (segn > 0) {
       const int seg = pq[3], dst = pq[5];
       for (int j = lane; j < segn; j += 64) {
-        const int i = (int)(keys[seg + j] & ((1u << 27) - 1));
+        const int i = m.wp_ord[(size_t)s0 * m.ord_stride + seg + j];
         const size_t b = (size_t)s0 * m.cap_wp + i;
         const V3 pt = rigid(R0, ld_v3(&m.wp_pnt[b * 3]), p0);
         const size_t d = (size_t)dst + j;
@@ -2250,17 +2165,8 @@ __device__ __forceinline__ void internal_exist(DevMap& m, int node) {
   h.isexist = e ? 1 : 0;
 }
 __global__ void __launch_bounds__(256) k_margi_internal(int L, int thread_num, DevMap m, int* __restrict__ lists,
-                                                        const int* __restrict__ rc, int nseg,
-                                                        const uint64_t* __restrict__ segkeys, const int* __restrict__ gate) {
+                                                        const int* __restrict__ rc, const int* __restrict__ gate) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
-  if (nseg < 0) nseg = rc[kRcNOld];  // the oldest slot's point count (k_set_jour)
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nseg; j += gridDim.x * blockDim.x) {
-    const uint64_t k = segkeys[j];
-    if (k == ~0ull) continue;
-    const int l = (int)(k >> 27);
-    m.nscr[(size_t)l * 4 + 0] = -1;
-    m.nscr[(size_t)l * 4 + 1] = -1;
-  }
   if (g_slide(m) < thread_num) return;
   int* work;
   const int nw = margi_level(L, m, rc, lists, &work);
@@ -2416,14 +2322,8 @@ int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thr
   const int gl = 64;  // grid-stride over device-side counts
   k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour, w.rc, n_oldest);
   for (int L = 0; L < nlev; L++) k_collect_level<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.list0, w.rc);
-  // oldest slot segments by leaf (the slot's point count is known on the host)
-  if (n_oldest > 0) {
-    k_margi_keys<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, slot0, m, w.k0);
-    size_t tb = w.tmp_bytes;
-    // stable LSD sort over the leaf bits only (keys generated in index order)
-    VG_HIP(hipcub::DeviceRadixSort::SortKeys(w.tmp2, tb, w.k0, w.k1, n_oldest, 27, 27 + bits_for(m.cap_nodes), s));
-    k_margi_segs<<<grid_for(n_oldest), kBlock, 0, s>>>(n_oldest, w.k1, m);
-  }
+  (void)slot0;  // the oldest slot's points per leaf are the leaves' runs (DevMap::lseg): no sort here
+  (void)n_oldest;
   VG_HIP(hipGetLastError());
   VG_HIP(hipEventRecord(ctx->ev_prefix_done, s));
   return VG_OK;
@@ -2476,16 +2376,16 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   // IEKF reads: ev_tail_a marks them, and the remainder (point_fix copies,
   // isexist / erase marks, slide compaction, the device-state slide, the
   // counter publication; nothing the IEKF reads) runs under the next IEKF
-  k_margi_leaf<<<gl, kBlock, 0, s>>>(m.counters + kCntLeaves, w.list0, mp, dwin, m, ctx->ba.fac_eig,
-                                     ctx->ba.fac_pcr, w.plan, gate);
+  // one lane per leaf (eigen-decomposition + plane_update in series on the lane):
+  // enough blocks that no lane takes two leaves, surplus blocks exit at once
+  k_margi_leaf<<<512, kBlock, 0, s>>>(m.counters + kCntLeaves, w.list0, mp, dwin, m, ctx->ba.fac_eig,
+                                      ctx->ba.fac_pcr, w.plan, gate);
   VG_HIP(hipEventRecord(ctx->ev_tail_a, s));
   ctx->tail_a_valid = true;
   auto body = [&]() -> int {
-    k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, w.k1, dwin, m, gate);
+    k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, dwin, m, gate);
     for (int L = nlev - 1; L >= 1; L--)
-      k_margi_internal<<<L == nlev - 1 ? 128 : gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc,
-                                                                  L == nlev - 1 ? -1 : 0, w.k1, gate);
-    if (nlev == 1) k_margi_internal<<<128, kBlock, 0, s>>>(-1, 1 << 30, m, w.list1, w.rc, -1, w.k1, gate);
+      k_margi_internal<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc, gate);
     for (int L = 0; L < nlev; L++)
       k_margi_erase_mark<<<gl, kBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc, gate);
     k_clear_mark<<<gl, kBlock, 0, s>>>(nlev - 2, nlev, thread_num, m, w.list1, w.rc, gate);

@@ -649,8 +649,11 @@ static int stage_insert_recut(vg_ctx* ctx) {
   VG_HIP(hipGraphLaunch(ge, ctx->stream));
   prof_end(ctx, kProfInsert);
   // ev_ds_free (the insert has read the ds buffers) and ev_recut_done (the
-  // margi prefix starts from here): flush_insert_events
+  // margi prefix starts from here), recorded right behind the graph: the next
+  // scan's downsample waits on ev_ds_free, and a record deferred to that
+  // point would make it wait for this scan's whole LM and margi as well
   ctx->ins_ev_pending = true;
+  VG_HIP(flush_insert_events(ctx));
   P->wp_n[slot] = P->n_raw;  // an upper bound until the scan's counters are absorbed (absorb_p2)
   P->ins_slot = slot;
   P->cur.ins_slot = slot;

@@ -155,6 +155,16 @@ struct DevMap {
   double* wp_var = nullptr;    // world var (after pvec_update), packed 6
   int* wp_leaf = nullptr;      // leaf holding the point in its list, -1 = not listed
   float* wp_int = nullptr;     // intensity of the window point (pointVar::intensity; /map_cmap only)
+  // SlideWindow::points per leaf (octree.cpp:151-177): per physical slot, the
+  // slot's listed point indices grouped by leaf, each leaf's run in index order
+  // — [0, cap_wp) written by the insert, then an arena the recut's children
+  // take their runs from (a point moves one layer down per subdivision, so
+  // max_layer arenas of cap_wp suffice); lseg locates a leaf's run per slot
+  int* wp_ord = nullptr;       // W * ord_stride
+  uint64_t* lseg = nullptr;    // cap_nodes * W: start 24 | count 21 | slot epoch 19 bits (lseg_pack)
+  int* slot_epoch = nullptr;   // per physical slot: inserts into it so far (a run of an older epoch is stale)
+  int* arena = nullptr;        // per physical slot: next free wp_ord entry of the children's arena
+  int ord_stride = 0;
   int* counters = nullptr;     // device counters (see kCnt*)
   int* stamp = nullptr;        // per-node tag of the last IEKF iteration that read its plane (P_k, profiling pass)
   int* wpn = nullptr;          // window points per physical slot (written by the insert, read by k_make_win)
@@ -175,7 +185,6 @@ struct Work {
   uint64_t *k0 = nullptr, *k1 = nullptr;
   uint32_t *v0 = nullptr, *v1 = nullptr;
   uint32_t *u0 = nullptr, *u1 = nullptr;
-  uint32_t* evsrc = nullptr;   // subdivision event source index
   uint32_t *ac_cnt = nullptr, *ac_off = nullptr;  // child allocation scratch
   int *list0 = nullptr, *list1 = nullptr, *list2 = nullptr, *cand = nullptr;
   int* leaf = nullptr;         // per ds point leaf / per event target

@@ -799,7 +799,9 @@ extern "C" int vgx_downsample_hashed(vg_ctx* ctx, const float* xyz, const float*
   VG_TRY(host_sync(ctx));
   VG_HIP(hipStreamSynchronize(ctx->stream_ds));
   VG_TRY(upload_aos(ctx, xyz, intensity, n));
-  VG_TRY(ds_enqueue_hashed(ctx, ctx->stream, ctx->d_x, ctx->d_y, ctx->d_z, ctx->d_i, n, voxel, false, 0));
+  const bool fallback = voxel < 0;  // test knob: a negative size runs the pipeline's /2 fallback pass as well
+  if (fallback) voxel = -voxel;
+  VG_TRY(ds_enqueue_hashed(ctx, ctx->stream, ctx->d_x, ctx->d_y, ctx->d_z, ctx->d_i, n, voxel, fallback, 0));
   hipStream_t s = ctx->stream;
   VG_HIP(hipMemcpyAsync(ctx->h_pinned, ctx->ds.hflags, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
   VG_HIP(hipStreamSynchronize(s));

@@ -217,8 +217,11 @@ class Context:
                   "vg_downsample")
         return out[: n.value]
 
-    def downsample_hashed(self, xyz, inten, size):
-        """The per-scan pipeline's downsample (test hook): (m,5) in first-occurrence order."""
+    def downsample_hashed(self, xyz, inten, size, fallback=False):
+        """The per-scan pipeline's downsample (test hook): (m,5) in first-occurrence order;
+        fallback: with the /2 pass below 2000 voxels (local_mapping.cpp:399-403)."""
+        if fallback:
+            size = -size
         xyz = np.ascontiguousarray(xyz, dtype=np.float32)
         inten = np.ascontiguousarray(inten, dtype=np.float32)
         out = np.zeros((max(xyz.shape[0], 1), 5), dtype=np.float32)
