@@ -397,7 +397,9 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None):
             np.savez(path, **arrs)
             paths.append(path)
             del sc, arrs
-        env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+        hwq = os.environ.get("VG_MULTI_HWQ", "16")  # experiments only; the line records what ran
+        out["env"]["GPU_MAX_HW_QUEUES"] = hwq
+        env = dict(os.environ, GPU_MAX_HW_QUEUES=hwq)
         for B in Bs:
             beat("multi-sequence %s: B = %d" % (lidar, B))
             cmd = [sys.executable, os.path.abspath(__file__), "--multi-child", str(B),

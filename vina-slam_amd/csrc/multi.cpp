@@ -90,8 +90,9 @@ vg_multi* vg_multi_create(vg_ctx** ctxs, int B, int spin_us, int sleep_us) {
       // depending on how the queues fell); the downsample and the margi prefix
       // then run in enqueue order on the context stream
       vg_ctx* c = ctxs[b];
-      M->split[b] = (char)((c->overlap_iekf ? 1 : 0) | (c->stream_ds && c->stream_ds != c->stream ? 2 : 0));
+      M->split[b] = (char)((c->overlap_iekf ? 1 : 0) | (c->want_ds_stream ? 2 : 0));
       c->overlap_iekf = false;
+      c->want_ds_stream = false;
       if (c->stream_ds && c->stream_ds != c->stream) {
         (void)hipStreamSynchronize(c->stream_ds);
         (void)hipStreamDestroy(c->stream_ds);
@@ -162,11 +163,8 @@ void vg_multi_destroy(vg_multi* M) {
   for (size_t b = 0; b < M->ctx.size(); b++) {
     vg_ctx* c = M->ctx[b];
     (void)hipStreamSynchronize(c->stream);
-    if ((M->split[b] & 2) && c->stream_ds == c->stream) {
-      hipStream_t s = nullptr;
-      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) c->stream_ds = s;
-    }
-    if (M->split[b] & 1) c->overlap_iekf = c->stream_ds != c->stream;
+    if (M->split[b] & 2) c->want_ds_stream = true;  // made again on the next scan (stage_downsample)
+    if (M->split[b] & 1) c->overlap_iekf = true;
   }
   delete M;
 }

@@ -492,6 +492,8 @@ int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float*
   P->n_raw = n;
   P->cur.st.n_raw = n;
   // own stream: waits only until the previous insert has read the ds buffers
+  if (ctx->want_ds_stream && ctx->stream_ds == ctx->stream)
+    VG_HIP(hipStreamCreateWithFlags(&ctx->stream_ds, hipStreamNonBlocking));
   VG_HIP(flush_insert_events(ctx));
   VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_ds_free, 0));
   VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_scan_ready, 0));  // a deskewed scan (no-op otherwise)

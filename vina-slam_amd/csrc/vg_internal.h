@@ -303,6 +303,10 @@ struct vg_ctx {
   // the downsample runs on its own stream: it reads only the raw scan, so it
   // overlaps the previous scan's recut/BA/margi and this scan's IEKF
   hipStream_t stream_ds = nullptr;
+  // the downsample / margi prefix get a stream of their own, created on the
+  // first scan; the multi-sequence mode turns it off before any scan, so its
+  // contexts never hold a second hardware queue (vg_multi_create)
+  bool want_ds_stream = true;
   hipEvent_t ev_ds_done = nullptr, ev_ds_free = nullptr;
   hipEvent_t ev_recut_done = nullptr, ev_prefix_done = nullptr;  // margi prefix on the second stream
   // The next scan's IEKF overlaps the margi's map-only remainder: it runs on

@@ -137,8 +137,7 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     ctx->err = std::string("hipSetDevice: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
-  if ((e = hipStreamCreateWithFlags(&ctx->stream_ds, hipStreamNonBlocking)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&ctx->ev_ds_done, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess ||
+  if ((e = hipEventCreateWithFlags(&ctx->ev_ds_done, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&ctx->ev_ds_free, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&ctx->ev_recut_done, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&ctx->ev_prefix_done, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess ||
@@ -152,6 +151,7 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     ctx->err = std::string("hipStreamCreate: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
+  ctx->stream_ds = ctx->stream;  // its own stream on the first scan (stage_downsample), unless multi-sequence
   if ((e = hipHostMalloc((void**)&ctx->h_pinned, 4096, hipHostMallocDefault)) != hipSuccess) {
     ctx->err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
