@@ -15,8 +15,8 @@ import synth  # noqa: E402
 import vgconfig  # noqa: E402
 import vgpu  # noqa: E402
 
-PHASES = {3: "load tiles", 9: "diag(0)", 5: "panel mfma", 6: "trailing || diag(K+1)", 7: "backward solve",
-          8: "trial/q1"}
+PHASES = {3: "load || inv(0)", 10: "wave0: L, tile, y", 11: "wave0: inv(K+1)", 6: "barrier wait",
+          5: "w(NB-1)", 7: "backward solve", 8: "trial/q1"}
 
 
 def main(nscan=40, lidar="64line"):

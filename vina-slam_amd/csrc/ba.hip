@@ -504,18 +504,101 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
   }
 }
 
-// LDL^T solve of the prepared system in one workgroup, trial state, IMU bias
-// trial. P A P^T is factored without further pivoting, 16 columns per panel:
-//   (1) wave 0 factors the diagonal tile in registers (4 lanes per row, the
-//       rank-1 vectors through LDS), inverts its unit-lower factor (stored in
-//       the tile's unused upper half) and forms M = L^-T D^-1 and the panel's
-//       share of z = D^+ L^-1 b (the right-hand side rides along as a
-//       bordered row, so the forward solve needs no separate pass);
-//   (2) the panel below, L_IK = A_IK M, one v_mfma_f64_16x16x4 wave per tile;
-//   (3) the trailing update A22 -= L21 D L21^T on MFMA and b -= L21 D z.
-// The backward solve runs blocked on wave 0. Rounding differs from Eigen's
-// sequential recurrences (tolerance-level; ties in |diag| may order
-// differently from its scan).
+// 4x4 symmetric sweep in registers, pivots in index order: b -> -b^-1. A
+// pivot with |d| <= DBL_MIN contributes nothing (Eigen's LDLT leaves such a
+// column undivided and its solve takes D^+, so that unknown's share is 0).
+__device__ __forceinline__ void sweep4(double (&b)[4][4]) {
+#pragma unroll
+  for (int p = 0; p < 4; p++) {
+    const double d = b[p][p];
+    double ip = __builtin_amdgcn_rcp(d);
+    ip = fma(ip, fma(-d, ip, 1.0), ip);
+    ip = fabs(d) > 2.2250738585072014e-308 ? ip : 0.0;
+    double c[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) c[i] = b[i][p] * ip;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j <= i; j++)
+        if (i != p && j != p) {
+          b[i][j] = fma(-c[i], b[p][j], b[i][j]);
+          b[j][i] = b[i][j];
+        }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (i != p) b[i][p] = b[p][i] = c[i];
+    b[p][p] = -ip;
+  }
+}
+// v_i for a lane-varying i in [0, 4): flat selects (no divergent branches)
+__device__ __forceinline__ double sel4(double v0, double v1, double v2, double v3, int i) {
+  double r = v3;
+  r = i == 2 ? v2 : r;
+  r = i == 1 ? v1 : r;
+  r = i == 0 ? v0 : r;
+  return r;
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <int C>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo32 = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), C, 0xf, 0xf, false);
+  const int hi32 = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), C, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi32 << 32) | (unsigned int)lo32);
+}
+// sum over the 16 lanes of each row (lanes with equal lane >> 4): DPP
+// quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror; every lane
+// adds the same pairs, so all 16 hold the same bits
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x141>(v);
+  v += dpp_f64<0x140>(v);
+  return v;
+}
+// sum over lanes l, l^16, l^32, l^48 (the four rows): gfx950's
+// v_permlane16_swap / v_permlane32_swap, (even + odd) then (low + high)
+__device__ __forceinline__ double xrow_sum(double v) {
+  long long b = __double_as_longlong(v);
+  auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+  auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  v = __longlong_as_double(((long long)hi[0] << 32) | lo[0]) + __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+  b = __double_as_longlong(v);
+  lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  return __longlong_as_double(((long long)hi[0] << 32) | lo[0]) + __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+}
+
+// Block LDL^T solve of the prepared system P A P^T y = P b in one workgroup
+// (the LDLT the reference runs at optimizers.cpp:466, pivot order from
+// k_ba_prep: Eigen's, descending |diag|). 16 x 16 tiles, no further pivoting:
+//   P A P^T = L D L^T with D = diag(S_KK) (the Schur-complement diagonal
+//   tiles) and L_IK = S_IK S_KK^-1, so
+//   forward  y_I -= L_IK y_K (rides along the trailing update),
+//   diagonal w_K  = S_KK^-1 y_K,
+//   backward x_K  = w_K - S_KK^-1 sum_{J>K} S_JK^T x_J.
+// A diagonal tile is inverted in registers by one wave as a 4-column block
+// sweep (Gauss-Jordan on the symmetric tile): each step inverts its 4 x 4
+// pivot block (sweep4, redundantly per lane), exchanges one 16 x 4 panel
+// through LDS and applies the rank-4 update with one v_mfma_f64_16x16x4; the
+// pivot rows/columns are written directly (not as the difference of two
+// rounded products). Tiles live in the D layout of that MFMA (lane (c, q)
+// holds rows q + 4g of column c), which is also the layout a tile has after a
+// trailing update, so the factor never leaves registers between the update
+// and the inversion.
+// Phase K (one workgroup barrier each): wave 0 computes -L_{K+1,K}^T, brings
+// tile (K+1, K+1) and y_{K+1} up to date and inverts the tile (the critical
+// chain); the twelve waves on the other three SIMDs take the rest of panel K's
+// trailing update, row pieces of up to four tiles that each compute their
+// row's -L_IK^T = S_KK^-1 S_IK^T once in registers (that transposed product
+// is exactly the MFMA A-operand layout of the update), plus w_K. The backward
+// substitution keeps acc_J in wave J's registers: one barrier per tile row.
+// Rounding differs from Eigen's sequential recurrences (tolerance level).
 __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double* __restrict__ timg,
                                                   const double* __restrict__ bvec, const double* __restrict__ dvec,
                                                   const double* __restrict__ jvec, const int* __restrict__ ipg,
@@ -525,228 +608,218 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
   if (st->done) return;
   extern __shared__ __attribute__((aligned(16))) double T[];
   constexpr int kN = kMaxNB * kTile;
-  __shared__ double Jv[kN], Dv[kN], xv[kN], col[kN], sMb[2][256], dKb[2][16], tb[16];
+  __shared__ double Jv[kN], Dv[kN], yv[kN], wv[kN], xv[kN], col[kN], sP[64], sG[64];
   __shared__ int ip[kN];
-  __shared__ unsigned char tI[kMaxNB * (kMaxNB + 1) / 2], tJ[kMaxNB * (kMaxNB + 1) / 2];
   const int n = 15 * W, m = n - 15;  // the gauge frame's unknowns are not factored (k_ba_prep)
   const int NB = (m + kTile - 1) / kTile, N = NB * kTile;
   const int ntile = NB * (NB + 1) / 2;
   const int tid = threadIdx.x, nt = blockDim.x;
-  const int lane = tid & 63, wave = tid >> 6, nwave = nt >> 6;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int cc = lane & 15, rq = lane >> 4;
   const double u = st->u;
   VG_PROBE_BEGIN();
-  {
+
+  // -S^-1 of a diagonal tile held in registers (D layout), on one wave
+  auto diag = [&](v4d a) __attribute__((always_inline)) {
+    const int cq = cc & 3, cb = cc >> 2;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      sP[rq * 16 + cc] = a[k];  // rows 4k..4k+3 of the tile
+      wave_lds_sync();
+      double b[4][4], p[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) b[i][j] = sP[i * 16 + 4 * k + j];
+        p[i] = sP[i * 16 + cc];  // A(4k+i, c) = A(c, 4k+i)
+      }
+      sweep4(b);  // -B^-1
+      double bc[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) bc[j] = sel4(b[j][0], b[j][1], b[j][2], b[j][3], rq);  // -B^-1(j, q)
+      double gq = 0.0;  // -G(c, q), G = A(:, K) B^-1
+#pragma unroll
+      for (int j = 0; j < 4; j++) gq = fma(p[j], bc[j], gq);
+      const bool inK = cb == k;
+      sG[cc * 4 + rq] = -gq;
+      a = __builtin_amdgcn_mfma_f64_16x16x4f64(inK ? 0.0 : gq, inK ? 0.0 : a[k], a, 0, 0, 0);  // A_OO -= G A_KO
+      wave_lds_sync();
+      double go[4];
+#pragma unroll
+      for (int g = 0; g < 4; g++) go[g] = sG[(rq + 4 * g) * 4 + cq];
+#pragma unroll
+      for (int g = 0; g < 4; g++)
+        if (g != k) a[g] = inK ? go[g] : a[g];  // A_OK <- G
+      a[k] = inK ? sel4(bc[0], bc[1], bc[2], bc[3], cq) : -gq;  // A_KK <- -B^-1, A_KO <- B^-1 A_KO = G^T
+    }
+    return a;
+  };
+  // -L_IK^T = S_KK^-1 S_IK^T as (-S_KK^-1) S_IK^T: lane (c, q) reg g =
+  // -L_IK(c, q + 4g). tv[ks] = (-S_KK^-1)(c, 4ks + q) (from the tile store, or
+  // wave 0's registers: the inverse is symmetric, so its D-layout register g
+  // is that A operand), sv[ks] = S_IK(c, 4ks + q). Two accumulation chains.
+  auto mk_gt = [&](const v4d& tv, const v4d& sv) __attribute__((always_inline)) {
+    const v4d z = v4d{0.0, 0.0, 0.0, 0.0};
+    v4d g1 = __builtin_amdgcn_mfma_f64_16x16x4f64(tv[0], sv[0], z, 0, 0, 0);
+    v4d g2 = __builtin_amdgcn_mfma_f64_16x16x4f64(tv[2], sv[2], z, 0, 0, 0);
+    g1 = __builtin_amdgcn_mfma_f64_16x16x4f64(tv[1], sv[1], g1, 0, 0, 0);
+    g2 = __builtin_amdgcn_mfma_f64_16x16x4f64(tv[3], sv[3], g2, 0, 0, 0);
+    return g1 + g2;
+  };
+  // operand columns of a tile: lane (c, q) reg ks = tile(c, 4ks + q)
+  auto ld_ops = [&](const double* t) __attribute__((always_inline)) {
+    v4d o;
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++) o[ks] = t[tel(cc, 4 * ks + rq)];
+    return o;
+  };
+  // acc -= L_IK S_JK^T, sj = ld_ops(S_JK); two accumulation chains
+  auto tile_upd = [&](v4d acc, const v4d& gt, const v4d& sj) __attribute__((always_inline)) {
+    v4d a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(gt[2], sj[2], v4d{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(gt[0], sj[0], acc, 0, 0, 0);
+    a2 = __builtin_amdgcn_mfma_f64_16x16x4f64(gt[3], sj[3], a2, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(gt[1], sj[1], acc, 0, 0, 0);
+    return acc + a2;
+  };
+  // y_I -= L_IK y_K
+  auto y_upd = [&](const v4d& gt, int K, int I) __attribute__((always_inline)) {
+    double s = 0.0;
+#pragma unroll
+    for (int g = 0; g < 4; g++) s = fma(gt[g], yv[16 * K + rq + 4 * g], s);
+    s = xrow_sum(s);
+    if (rq == 0) yv[16 * I + cc] += s;
+  };
+  // w_K = S_KK^-1 y_K (into wv, and into xv as well for the last tile row)
+  auto w_job = [&](int K, bool last) __attribute__((always_inline)) {
+    const double* Ti = &T[tix(K, K) * 256];
+    const double yk = yv[16 * K + cc];
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      const double s = -row16_sum(Ti[tel(rq + 4 * g, cc)] * yk);
+      if (cc == 0) {
+        wv[16 * K + rq + 4 * g] = s;
+        if (last) xv[16 * K + rq + 4 * g] = s;
+      }
+    }
+  };
+  auto ld_tile = [&](const double* t) __attribute__((always_inline)) {
+    v4d a;
+#pragma unroll
+    for (int g = 0; g < 4; g++) a[g] = t[tel(rq + 4 * g, cc)];
+    return a;
+  };
+  auto st_tile = [&](double* t, const v4d& a) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < 4; g++) t[tel(rq + 4 * g, cc)] = a[g];
+  };
+
+  // wave 0 takes tile (0, 0) straight from the image and inverts it while the
+  // other waves fill the tile store and the vectors
+  v4d tinv;  // wave 0: -S_KK^-1 of the current panel, kept in registers
+  if (wave == 0) {
+    tinv = diag(ld_tile(timg));
+    st_tile(T, tinv);
+  } else {
     const double2* src = reinterpret_cast<const double2*>(timg);
     double2* dst = reinterpret_cast<double2*>(T);
-    for (int t = tid; t < ntile * 128; t += nt) dst[t] = src[t];
-  }
-  for (int t = tid; t < N; t += nt) xv[t] = bvec[t];
-  for (int t = tid; t < n; t += nt) {
-    Dv[t] = dvec[t];
-    Jv[t] = jvec[t];
-    if (t < m) ip[t] = ipg[t];
-  }
-  if (tid < ntile) {
-    int I = 0;
-    while ((I + 1) * (I + 2) / 2 <= tid) I++;
-    tI[tid] = (unsigned char)I;
-    tJ[tid] = (unsigned char)(tid - I * (I + 1) / 2);
+    for (int t = 128 + tid - 64; t < ntile * 128; t += nt - 64) dst[t] = src[t];
+    for (int t = tid - 64; t < N; t += nt - 64) yv[t] = bvec[t];
+    for (int t = tid - 64; t < n; t += nt - 64) {
+      Dv[t] = dvec[t];
+      Jv[t] = jvec[t];
+      if (t < m) ip[t] = ipg[t];
+    }
   }
   __syncthreads();
   VG_PROBE_MARK(3);
 
-  // (1) diagonal tile K on wave 0 (see below); M and d go to parity buffer pb
-  auto diag = [&](int K, int pb) __attribute__((always_inline)) {
-    double* Tkk = &T[tix(K, K) * 256];
-    // (1) diagonal tile, lane (r = lane/4, q = lane%4) holds a(r, q + 4s)
-    //     and X(r, q + 4s) (X -> L^-1 by the same row operations):
-    //     column j: L(r,j) = a(r,j)/d_j; a(r,m) -= L(r,j) a(m,j);
-    //     X(r,:) -= L(r,j) X(j,:). The column's undivided values a(m,j)
-    //     (= d_j L(m,j)) and row X(j,:) do not wait for the reciprocal, so
-    //     their exchanges (DPP / ds_bpermute) overlap it; the reciprocal is
-    //     v_rcp_f64 plus one Newton step.
-    const int r = lane >> 2, q = lane & 3;
-    double a[4], X[4];
-#pragma unroll
-    for (int s4 = 0; s4 < 4; s4++) {
-      a[s4] = Tkk[tel(r, q + 4 * s4)];
-      X[s4] = (q + 4 * s4 == r) ? 1.0 : 0.0;
-    }
-    // Only blocks s4 >= j/4 of a change (entries right of column j; rows
-    // r <= j there are strictly upper and never read) and only blocks
-    // s4 <= j/4 of X (X(j,:) is zero right of j), so each column needs no
-    // per-element predicates and 5 block updates instead of 8.
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const int qj = j & 3, sj = j >> 2;
-      const double dj = bcast(a[sj], 4 * j + qj);
-      const double acol = quad_bcast(a[sj], qj);  // a(r, j) in every lane of row r
-      double tv[4], xj[4];
-#pragma unroll
-      for (int s4 = 0; s4 < 4; s4++) {
-        if (s4 >= sj) tv[s4] = __shfl(acol, 4 * (q + 4 * s4), 64);  // a(m, j), m = q + 4 s4
-        if (s4 <= sj) xj[s4] = __shfl(X[s4], 4 * j + q, 64);        // X(j, m)
-      }
-      double rdj = 1.0;  // Eigen leaves a zero pivot's column undivided
-      if (dj != 0.0) {
-        rdj = __builtin_amdgcn_rcp(dj);
-        rdj = fma(rdj, fma(-dj, rdj, 1.0), rdj);
-      }
-      const double l = acol * rdj;
-      const double lu = (dj != 0.0) ? l : 0.0;  // a zero pivot updates nothing (d_j L(m,j) = 0)
-      const double lx = (r > j) ? l : 0.0;
-#pragma unroll
-      for (int s4 = 0; s4 < 4; s4++) {
-        if (s4 > sj) a[s4] -= lu * tv[s4];
-        if (s4 <= sj) X[s4] -= lx * xj[s4];
-      }
-      if (q > qj) a[sj] -= lu * tv[sj];
-      else if (q == qj && r > j) a[sj] = l;
-    }
-    double myd = 0.0;
-#pragma unroll
-    for (int s4 = 0; s4 < 4; s4++)
-      if (q + 4 * s4 == r) myd = a[s4];
-    myd = __shfl(myd, 4 * r + (r & 3), 64);
-    const double rd = (myd != 0.0) ? 1.0 / myd : 1.0;
-    // z_r = D^+ (X b_K)_r (Eigen: |d| > DBL_MIN divides, else 0)
-    double zp = 0.0;
-#pragma unroll
-    for (int s4 = 0; s4 < 4; s4++) zp += X[s4] * xv[16 * K + q + 4 * s4];
-    zp += __shfl_xor(zp, 1, 64);
-    zp += __shfl_xor(zp, 2, 64);
-    const double zr = (fabs(myd) > 2.2250738585072014e-308) ? zp / myd : 0.0;
-#pragma unroll
-    for (int s4 = 0; s4 < 4; s4++) {
-      const int c = q + 4 * s4;
-      if (c <= r) Tkk[tel(r, c)] = a[s4];
-      if (c < r) Tkk[tel(c, r)] = X[s4];  // Linv(r, c) in the unused upper half
-      sMb[pb][c * 16 + r] = X[s4] * rd;  // M = L^-T D^-1
-    }
-    if (q == 0) dKb[pb][r] = myd;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (q == 0) xv[16 * K + r] = zr;
+  // -L_IK^T of a phase goes to tile (I, K) in the next phase, once no wave
+  // reads S_IK any more (the backward substitution needs L, not S): at most
+  // two rows per wave and phase (wave-uniform bookkeeping)
+  v4d pg0, pg1;
+  int pt0 = -1, pt1 = -1;
+  auto flush = [&]() __attribute__((always_inline)) {
+    if (pt0 >= 0) st_tile(&T[pt0 * 256], pg0);
+    if (pt1 >= 0) st_tile(&T[pt1 * 256], pg1);
+    pt0 = pt1 = -1;
   };
-  // (3) one trailing job of panel K on one wave: tile A_IJ -= L_IK diag(d)
-  //     L_JK^T, or (brow) the bordered right-hand side b_I -= L_IK diag(d) z_K
-  //     (column 0 of an MFMA tile)
-  auto tjob = [&](int K, int I, int J, bool brow, const double* dk) __attribute__((always_inline)) {
-    const double* Aik = &T[tix(I, K) * 256];
-    const double* Ajk = &T[tix(J, K) * 256];
-    double* Tij = &T[tix(I, J) * 256];
-    const int cc = lane & 15, rq = lane >> 4;
-    v4d acc;
-#pragma unroll
-    for (int g = 0; g < 4; g++) acc[g] = brow ? (cc == 0 ? xv[16 * I + rq + 4 * g] : 0.0) : Tij[tel(rq + 4 * g, cc)];
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) {
-      const int kk = 4 * ks + rq;
-      const double av = -(Aik[tel(cc, kk)] * dk[kk]);
-      const double bv = brow ? (cc == 0 ? xv[16 * K + kk] : 0.0) : Ajk[tel(cc, kk)];
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-    }
-    if (brow) {
-      if (cc == 0)
-#pragma unroll
-        for (int g = 0; g < 4; g++) xv[16 * I + rq + 4 * g] = acc[g];
+  auto pend = [&](const v4d& gt, int t) __attribute__((always_inline)) {
+    if (pt0 < 0) {
+      pg0 = gt;
+      pt0 = t;
     } else {
-#pragma unroll
-      for (int g = 0; g < 4; g++) Tij[tel(rq + 4 * g, cc)] = acc[g];
+      pg1 = gt;
+      pt1 = t;
     }
   };
-  // Right-looking with one panel of lookahead: after panel K, wave 0 brings
-  // tile (K+1, K+1) and b_{K+1} up to date and factors tile K+1 while the
-  // other waves run the rest of panel K's trailing update, so the trailing
-  // work leaves the critical path (two barriers per panel). M and d are
-  // double-buffered by panel parity.
-  if (wave == 0) diag(0, 0);
-  __syncthreads();
-  VG_PROBE_MARK(9);
-  for (int K = 0; K < NB; K++) {
-    const int pb = K & 1;
-    // (2) panel: L_IK = A_IK M (in place, one wave per tile)
-    for (int I = K + 1 + wave; I < NB; I += nwave) {
-      double* Tik = &T[tix(I, K) * 256];
-      const int cc = lane & 15, rq = lane >> 4;
-      v4d acc = v4d{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int ks = 0; ks < 4; ks++) {
-        const int kk = 4 * ks + rq;
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Tik[tel(cc, kk)], sMb[pb][kk * 16 + cc], acc, 0, 0, 0);
-      }
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int g = 0; g < 4; g++) Tik[tel(rq + 4 * g, cc)] = acc[g];
-    }
-    __syncthreads();
-    VG_PROBE_MARK(5);
-    if (K + 1 == NB) break;
-    const int Rm = NB - K - 1;
-    const int ntr = Rm * (Rm + 1) / 2;
+  for (int K = 0; K + 1 < NB; K++) {
+    flush();
     if (wave == 0) {
-      tjob(K, K + 1, K + 1, false, dKb[pb]);
-      tjob(K, K + 1, 0, true, dKb[pb]);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      diag(K + 1, pb ^ 1);
+      const v4d s1 = ld_ops(&T[tix(K + 1, K) * 256]);
+      v4d a = ld_tile(&T[tix(K + 1, K + 1) * 256]);
+      const v4d gt = mk_gt(tinv, s1);
+      a = tile_upd(a, gt, s1);
+      pend(gt, tix(K + 1, K));
+      VG_PROBE_MARK(10);
+      tinv = diag(a);
+      st_tile(&T[tix(K + 1, K + 1) * 256], tinv);
+      VG_PROBE_MARK(11);
     } else if (wave & 3) {
-      // jobs 0 (tile (K+1, K+1)) and ntr (b_{K+1}) belong to wave 0; the
-      // waves sharing its SIMD (wave % 4 == 0) stay idle so that its
-      // latency-bound column chain has the SIMD to itself
-      const int wk = wave - (wave >> 2) - 1, nwk = nwave - (nwave >> 2);
-      for (int q = 1 + wk; q < ntr + Rm; q += nwk) {
-        if (q == ntr) continue;
-        const bool brow = q > ntr;
-        tjob(K, brow ? K + 1 + (q - ntr) : K + 1 + tI[q], brow ? 0 : K + 1 + tJ[q], brow, dKb[pb]);
+      // the twelve waves off wave 0's SIMD: job 0 = w_K and y_{K+1}, then
+      // row pieces of up to four tiles
+      const int wk = wave - (wave >> 2) - 1;
+      constexpr int nwk = 12;
+      const v4d tv = ld_ops(&T[tix(K, K) * 256]);
+      int q = 0;
+      if (q++ == wk) {
+        w_job(K, false);
+        y_upd(mk_gt(tv, ld_ops(&T[tix(K + 1, K) * 256])), K, K + 1);
       }
+      for (int I = K + 2; I < NB; I++)
+        for (int J0 = K + 1; J0 <= I; J0 += 4) {
+          if (q++ % nwk != wk) continue;
+          const v4d gt = mk_gt(tv, ld_ops(&T[tix(I, K) * 256]));
+          const int J1 = J0 + 4 < I + 1 ? J0 + 4 : I + 1;
+          for (int J = J0; J < J1; J++) {
+            double* Tij = &T[tix(I, J) * 256];
+            st_tile(Tij, tile_upd(ld_tile(Tij), gt, ld_ops(&T[tix(J, K) * 256])));
+          }
+          if (J0 == K + 1) {
+            y_upd(gt, K, I);
+            pend(gt, tix(I, K));
+          }
+        }
     }
     __syncthreads();
     VG_PROBE_MARK(6);
   }
+  flush();
+  if (wave == 0) w_job(NB - 1, true);
+  __syncthreads();
+  VG_PROBE_MARK(5);
 
-  // backward solve on wave 0, lane (r = lane & 15, qd = lane >> 4):
-  // x_I = Linv_II^T (z_I - sum_{J>I} L_JI^T x_J), right-looking: once x_I is
-  // known its contributions to every earlier tile go into per-tile register
-  // accumulators (independent chains), so a step waits on 4 products only.
-  if (wave == 0) {
-    const int r = lane & 15, qd = lane >> 4;
-    double acc[kMaxNB];
+  // backward: x_J = w_J + sum_{I>J} (-L_IJ^T) x_I, tile (I, J) now holding
+  // -L_IJ^T; wave J keeps its lane shares pa[g] of rows q + 4g and completes
+  // x_J at step J+1 (one 16-lane DPP sum per row group)
+  {
+    double pa[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int I = NB - 1; I >= 1; I--) {
+      if (wave < I) {
+        const double* Lt = &T[tix(I, wave) * 256];
+        const double xi = xv[16 * I + cc];
 #pragma unroll
-    for (int J = 0; J < kMaxNB; J++) acc[J] = 0.0;
+        for (int g = 0; g < 4; g++) pa[g] = fma(Lt[tel(rq + 4 * g, cc)], xi, pa[g]);
+        if (wave == I - 1) {
 #pragma unroll
-    for (int I = kMaxNB - 1; I >= 0; I--) {
-      if (I >= NB) continue;
-      double sacc = acc[I];
-      sacc += __shfl_xor(sacc, 16, 64);
-      sacc += __shfl_xor(sacc, 32, 64);
-      const double z = xv[16 * I + r] - sacc;
-      if (qd == 0) tb[r] = z;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const double* Td = &T[tix(I, I) * 256];
-      double s2 = 0.0;
-#pragma unroll
-      for (int c = qd; c < 16; c += 4)
-        if (c > r) s2 += Td[tel(r, c)] * tb[c];
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (qd == 0) xv[16 * I + r] = z + s2;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-      for (int J = 0; J < I; J++) {
-        const double* Tt = &T[tix(I, J) * 256];
-#pragma unroll
-        for (int c = qd; c < 16; c += 4) acc[J] += Tt[tel(c, r)] * xv[16 * I + c];
+          for (int g = 0; g < 4; g++) {
+            const double t = row16_sum(pa[g]);
+            if (cc == 0) xv[16 * (I - 1) + rq + 4 * g] = wv[16 * (I - 1) + rq + 4 * g] + t;
+          }
+        }
       }
+      __syncthreads();
     }
   }
-  __syncthreads();
   VG_PROBE_MARK(7);
   for (int t = tid; t < n; t += nt) {
     if (t < m) col[ip[t]] = xv[t];
@@ -1283,6 +1356,49 @@ int ba_lidar_pass(vg_ctx* ctx, bool hessian, const double* poses, const int* mp_
   double r = 0.0;
   for (int b = 0; b < nrb; b++) r += h[b];
   *out = r;
+  return VG_OK;
+}
+
+// Test-only (vgx_ba_solve): k_ba_solve on a given m x m symmetric system
+// (m = 15W - 15, row-major A, right-hand side b) in identity pivot order;
+// x = the solution. Runs the kernel exactly as an LM iteration does (the
+// trial-state tail writes the context's scratch trial states and bias
+// records, so use a context that is not stepped afterwards).
+int ba_solve_test(vg_ctx* ctx, const double* A, const double* b, double* x) {
+  const int W = ctx->cfg.win_size, n = 15 * W, m = n - 15;
+  const int NB = (m + kTile - 1) / kTile, N = NB * kTile, ntile = NB * (NB + 1) / 2;
+  hipStream_t s = ctx->stream;
+  BaDev d = carve(ctx);
+  std::vector<double> img((size_t)ntile * 256), bv(N, 0.0), dv(n, 1.0), jv(n, 0.0);
+  std::vector<int> ipv(N, 0);
+  for (int I = 0; I < NB; I++)
+    for (int J = 0; J <= I; J++)
+      for (int r = 0; r < 16; r++)
+        for (int c = 0; c < 16; c++) {
+          const int R = I * 16 + r, C = J * 16 + c;
+          const double v = (R < m && C < m) ? A[(size_t)R * m + C] : (R == C ? 1.0 : 0.0);
+          img[(size_t)(I * (I + 1) / 2 + J) * 256 + r * 16 + (c ^ r)] = v;
+        }
+  for (int t = 0; t < m; t++) {
+    bv[t] = b[t];
+    ipv[t] = 15 + t;
+  }
+  BaState bs;
+  memset(&bs, 0, sizeof(bs));
+  VG_HIP(hipMemcpyAsync(d.timg, img.data(), img.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  VG_HIP(hipMemcpyAsync(d.bvec, bv.data(), N * sizeof(double), hipMemcpyHostToDevice, s));
+  VG_HIP(hipMemcpyAsync(d.dvec, dv.data(), n * sizeof(double), hipMemcpyHostToDevice, s));
+  VG_HIP(hipMemcpyAsync(d.jvec, jv.data(), n * sizeof(double), hipMemcpyHostToDevice, s));
+  VG_HIP(hipMemcpyAsync(d.ipg, ipv.data(), N * sizeof(int), hipMemcpyHostToDevice, s));
+  VG_HIP(hipMemcpyAsync(d.st, &bs, sizeof(bs), hipMemcpyHostToDevice, s));
+  VG_HIP(hipStreamSynchronize(s));
+  k_ba_solve<<<1, 1024, solve_lds_bytes(W), s>>>(W, W - 1, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias,
+                                                 d.dxi, d.st);
+  VG_HIP(hipGetLastError());
+  std::vector<double> out(n);
+  VG_HIP(hipMemcpyAsync(out.data(), d.dxi, n * sizeof(double), hipMemcpyDeviceToHost, s));
+  VG_HIP(hipStreamSynchronize(s));
+  for (int t = 0; t < m; t++) x[t] = out[15 + t];
   return VG_OK;
 }
 

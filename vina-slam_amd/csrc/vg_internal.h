@@ -619,7 +619,8 @@ const int* ba_hess_dev(vg_ctx* ctx);  // Hessian passes of the last LM run (I_H 
 // `poses` (lower 6W x 6W, gradient, residual into out) or residual pass at
 // `poses` (*out); synchronous
 int ba_lidar_pass(vg_ctx* ctx, bool hessian, const double* poses, const int* mp_ring, double* out);
-int ba_factor_normals(vg_ctx* ctx, std::vector<double>& normals);  // column 0 of each factor's eigenvectors
+int ba_factor_normals(vg_ctx* ctx, std::vector<double>& normals);
+int ba_solve_test(vg_ctx* ctx, const double* A, const double* b, double* x);  // vgx_ba_solve  // column 0 of each factor's eigenvectors
 // pipeline.cpp
 void host_init(vg_ctx* ctx);
 void host_free(vg_ctx* ctx);

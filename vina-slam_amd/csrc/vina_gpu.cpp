@@ -844,6 +844,14 @@ extern "C" int vgx_ba_capture(vg_ctx* ctx, double* out, int cap, int* n) {
   return VG_OK;
 }
 
+// Test-only: k_ba_solve on a given (15W-15)-unknown symmetric system (row-major
+// A, rhs b) in identity pivot order -> x. The context must not be stepped after.
+extern "C" int vgx_ba_solve(vg_ctx* ctx, const double* A, const double* b, double* x) {
+  if (!ctx || !A || !b || !x) return VG_E_ARG;
+  VG_TRY(vg::host_sync(ctx));
+  return vg::ba_solve_test(ctx, A, b, x);
+}
+
 int vg_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* valid, int* iters) {
   if (!ctx || (!xyz && n > 0) || n < 0 || !state || !valid || !iters) return VG_E_ARG;
   return host_lio_kdtree(ctx, xyz, n, state, valid, iters);

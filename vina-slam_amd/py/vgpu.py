@@ -166,6 +166,8 @@ def lib():
         L.vgx_debug.argtypes = [P, ctypes.c_int, ctypes.c_int]
         L.vgx_downsample_hashed.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, fp, ip]
         L.vgx_ba_capture.argtypes = [P, dp, ctypes.c_int, ip]
+        if hasattr(L, "vgx_ba_solve"):  # absent from builds older than the test entry (A/B runs)
+            L.vgx_ba_solve.argtypes = [P, dp, dp, dp]
         _lib = L
     return _lib
 
@@ -470,6 +472,14 @@ class Context:
         out = np.zeros(max(n.value, 1))
         self._chk(lib().vgx_ba_capture(self.h, _d(out), n.value, ctypes.byref(n)), "vgx_ba_capture")
         return out[: n.value]
+
+    def ba_solve(self, A, b):
+        """k_ba_solve on a (15W-15)-unknown symmetric system in identity pivot order."""
+        A = np.ascontiguousarray(A, dtype=np.float64)
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        x = np.zeros(b.shape[0])
+        self._chk(lib().vgx_ba_solve(self.h, _d(A), _d(b), _d(x)), "vgx_ba_solve")
+        return x
 
 
 class Sync:
