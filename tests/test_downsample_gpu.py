@@ -164,3 +164,21 @@ def test_fallback_pass_matches_oracle(oracle_lib, case, size, halves):
                                       loc).astype(np.int64)]
     assert got == order
     ctx.close()
+
+
+def test_hashed_downsample_1m_scan(oracle_lib):
+    """BASELINE config 5's scan (synthetic 1M rays, ~750 k points after the
+    blind filter): at 0.1 m about 13 k voxels hold 17-200 points (the
+    wave-per-voxel path, k_hds_mid) — bit for bit the oracle's set."""
+    seq = synth.Sequence("1M", seq_id=2, blind=3.0)
+    xyz, inten, _, _ = seq.scan(4)
+    c = vgpu.Context(vgconfig.to_c(vgconfig.load("mid360")), max_points=xyz.shape[0] + 16, max_nodes=100_000,
+                     max_fix_points=100_000, hash_log2=16)
+    try:
+        g = c.downsample_hashed(xyz, inten, 0.1)
+    finally:
+        c.close()
+    o = oracle.downsample(xyz, inten, 0.1)
+    assert g.shape == o.shape and g.shape[0] > 50_000
+    assert (o[:, 4] > 16).sum() > 5000
+    assert np.array_equal(_canon(g).view(np.uint32), _canon(o).view(np.uint32))

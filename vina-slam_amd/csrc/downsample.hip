@@ -29,6 +29,37 @@ __device__ __forceinline__ int64_t key_axis_f(float c, double size) {
   return (int64_t)l;
 }
 
+// 1/(k+1) in fp64, correctly rounded (constant-evaluated IEEE division)
+constexpr int kRcpN = 264;  // >= kHdsMid + 1
+struct RcpTable {
+  double v[kRcpN];
+  constexpr RcpTable() : v() {
+    for (int k = 0; k < kRcpN; k++) v[k] = 1.0 / (double)(k + 1);
+  }
+};
+__constant__ RcpTable kRcp = RcpTable();
+
+// One step of point_utils.hpp:34-37's running mean, p <- (p*c + v) / (c+1) in
+// float: the product and the sum rounded as written (no contraction), the
+// quotient as t * r in fp64 with r = RN64(1/(c+1)), rounded once to float.
+// That is the correctly rounded float quotient RN32(t/(c+1)) (for c+1 <=
+// 2^24): the fp64 value is within 2^-52 (relative) of t/b, while a float t
+// over an integer b <= 2^24 is either exact, or an exact rounding midpoint
+// only where r is exact too (b a power of two, or a subnormal quotient: taken
+// by the division below), or at least 2^-26/b >= 2^-50 (relative) away from
+// every midpoint between floats, so both round to the same float. It takes
+// the fp32 division's long correctly rounded sequence off the serial chain.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ float mean_step(float p, float c, float v, double r) {
+  const float t = p * c + v;
+  if (__builtin_expect(fabsf(t) < 0x1p-100f, 0)) return t / (c + 1);
+  return (float)((double)t * r);
+}
+
 __global__ void k_ds_keys(int n, const float* __restrict__ x, const float* __restrict__ y,
                           const float* __restrict__ z, double size, uint64_t* __restrict__ keys,
                           uint32_t* __restrict__ idx, int* __restrict__ flags) {
@@ -74,10 +105,12 @@ __global__ void k_ds_mean(const int* __restrict__ flags, const uint32_t* __restr
     float px = x[i0], py = y[i0], pz = z[i0], c = 1.0f;
     for (uint32_t j = b + 1; j < e; j++) {
       uint32_t i = order[j];
-      // point_utils.hpp:34-37, evaluated exactly as written (no contraction)
-      px = (px * c + x[i]) / (c + 1);
-      py = (py * c + y[i]) / (c + 1);
-      pz = (pz * c + z[i]) / (c + 1);
+      // point_utils.hpp:34-37 (mean_step: exactly the float recurrence as written)
+      const uint32_t jj = j - b;  // == c
+      const double r = jj < (uint32_t)kRcpN ? kRcp.v[jj] : 1.0 / (double)(jj + 1);
+      px = mean_step(px, c, x[i], r);
+      py = mean_step(py, c, y[i], r);
+      pz = mean_step(pz, c, z[i], r);
       c += 1;
     }
     ox[v] = px;
@@ -232,6 +265,8 @@ __device__ __forceinline__ uint32_t hds_hash(uint64_t k, int mask) {
 }
 constexpr int kHdsTile = 1024;  // points per tile (256 lanes x 4)
 constexpr int kHdsSmall = 16;   // a lane sorts a voxel's segment itself (in registers) up to this many points
+constexpr int kHdsMid = 256;    // a wave puts a voxel's segment back in order (LDS ranks) up to this many
+static_assert(kRcpN > kHdsMid, "the reciprocal table covers a mid-size voxel");
 constexpr int kHdsEmptyFirst = 0x7f7f7f7f;  // above every point index (ds_reset's memset byte)
 
 // the scan's input cloud as a kernel argument -> device memory, so that the
@@ -374,6 +409,7 @@ __global__ void __launch_bounds__(256) k_hds_rank(DownsampleBufs d, const int* _
     const int nv = bf + (int)(tot >> 32);
     d.hflags[1] = nv;
     d.hflags[3] = 0;  // dense voxels deferred by k_hds_mean
+    d.hflags[4] = 0;  // mid-size voxels deferred by k_hds_mean
     if (need_out) *need_out = nv < min_out ? 1 : 0;
   }
 }
@@ -428,9 +464,10 @@ __device__ __forceinline__ void hds_sorted_mean(const uint32_t* __restrict__ sg,
 #pragma unroll
   for (int a = 1; a < N; a++)
     if (a < cnt) {
-      px = (px * c + vx[a]) / (c + 1);
-      py = (py * c + vy[a]) / (c + 1);
-      pz = (pz * c + vz[a]) / (c + 1);
+      const double r = kRcp.v[a];  // c == a
+      px = mean_step(px, c, vx[a], r);
+      py = mean_step(py, c, vy[a], r);
+      pz = mean_step(pz, c, vz[a], r);
       c += 1;
     }
 }
@@ -444,8 +481,9 @@ __global__ void __launch_bounds__(256) k_hds_mean(DownsampleBufs d, const int* _
     const int i = d.vfirst[v];
     const uint32_t s = d.pslot[i];
     const int b = d.hoff[s], cnt = d.hcnt[s];
-    if (cnt > kHdsSmall) {  // a dense voxel: a workgroup puts it back in order (k_hds_big)
-      d.bigv[atomicAdd(&d.hflags[3], 1)] = v;
+    if (cnt > kHdsSmall) {  // mid-size: a wave puts it back in order (k_hds_mid); dense: a workgroup (k_hds_big)
+      if (cnt <= kHdsMid) d.bigv[d.cap - 1 - atomicAdd(&d.hflags[4], 1)] = v;
+      else d.bigv[atomicAdd(&d.hflags[3], 1)] = v;
       continue;
     }
     const uint32_t* sg = d.pseg + b;
@@ -466,6 +504,76 @@ __global__ void __launch_bounds__(256) k_hds_mean(DownsampleBufs d, const int* _
   }
 }
 
+// Mid-size voxels (kHdsSmall < points <= kHdsMid): one wave each. The
+// segment's point indices go to LDS, each lane ranks its (up to four) indices
+// against the whole segment (distinct indices: rank = input order), the
+// coordinates are gathered in that order into LDS, and lanes 0..2 run the x, y
+// and z recurrences (point_utils.hpp:34-37, mean_step).
+__global__ void __launch_bounds__(256) k_hds_mid(DownsampleBufs d, const int* __restrict__ need) {
+  if (need && !*need) return;
+  const HdsIn a = *d.arg;
+  __shared__ __attribute__((aligned(16))) uint32_t s_idx[4][kHdsMid];
+  __shared__ uint32_t s_ord[4][kHdsMid];
+  __shared__ float s_c[4][3][kHdsMid];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nmid = d.hflags[4];
+  for (int q = blockIdx.x * 4 + w; q < nmid; q += gridDim.x * 4) {
+    const int v = d.bigv[d.cap - 1 - q];
+    const int i0 = d.vfirst[v];
+    const uint32_t s = d.pslot[i0];
+    const int b = d.hoff[s], cnt = d.hcnt[s];
+    uint32_t u[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int e = lane + 64 * k;
+      u[k] = e < cnt ? d.pseg[b + e] : 0xffffffffu;
+      s_idx[w][e] = u[k];
+    }
+    wave_lds_sync();
+    int r[4] = {0, 0, 0, 0};
+    const uint4* s4 = reinterpret_cast<const uint4*>(s_idx[w]);
+    for (int j = 0; j < (cnt + 3) >> 2; j++) {
+      const uint4 t = s4[j];
+#pragma unroll
+      for (int k = 0; k < 4; k++) r[k] += (t.x < u[k]) + (t.y < u[k]) + (t.z < u[k]) + (t.w < u[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (lane + 64 * k < cnt) s_ord[w][r[k]] = u[k];
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int e = lane + 64 * k;
+      if (e < cnt) {
+        const uint32_t i = s_ord[w][e];
+        s_c[w][0][e] = a.x[i];
+        s_c[w][1][e] = a.y[i];
+        s_c[w][2][e] = a.z[i];
+      }
+    }
+    wave_lds_sync();
+    if (lane < 3) {
+      const float* cv = s_c[w][lane];
+      float p = cv[0], c = 1.0f;
+#pragma unroll 4
+      for (int e = 1; e < cnt; e++) {
+        p = mean_step(p, c, cv[e], kRcp.v[e]);  // c == e
+        c += 1.0f;
+      }
+      (lane == 0 ? d.ox : (lane == 1 ? d.oy : d.oz))[v] = p;
+      if (lane == 0) {
+        d.oi[v] = a.in ? a.in[i0] : 0.0f;
+        d.oc[v] = c;
+        d.hkey[s] = kKeyEmpty;
+        d.hfirst[s] = kHdsEmptyFirst;
+        d.hcnt[s] = 0;
+        d.hfill[s] = 0;
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
 // Dense voxels (more than kHdsSmall points): one workgroup each restores the
 // input order of the voxel's segment with an LDS bitmap over its index range
 // (windows of kHdsBits indices; set bits compacted by a block scan — O(points +
@@ -475,8 +583,9 @@ constexpr int kHdsBits = 1 << 18;          // indices per bitmap window (32 KB o
 constexpr int kHdsWords = kHdsBits / 32;
 // one dense voxel v by the whole workgroup (any size, a multiple of 64 that
 // divides kHdsWords); bm: kHdsWords LDS words, s_w: one int per wave
+constexpr int kHdsChunk = 2048;  // ordered points per LDS chunk of the recurrence
 __device__ void hds_big_voxel(DownsampleBufs& d, int v, const float* x, const float* y, const float* z, const float* in,
-                              uint32_t* bm, int* s_w, int* s_base) {
+                              uint32_t* bm, int* s_w, int* s_base, float* cb, double* rb) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nt = blockDim.x, nw = nt >> 6;
   const int i0 = d.vfirst[v];  // the voxel's smallest index
   const uint32_t s = d.pslot[i0];
@@ -530,13 +639,36 @@ __device__ void hds_big_voxel(DownsampleBufs& d, int v, const float* x, const fl
     }
     __syncthreads();
   }
-  if (tid < 3) {  // point_utils.hpp:34-37 per coordinate, as written
-    const float* a = tid == 0 ? x : (tid == 1 ? y : z);
-    float p = a[i0], c = 1.0f;
-    for (int e = 1; e < cnt; e++) {
-      p = (p * c + a[out[e]]) / (c + 1);
-      c += 1;
+  // point_utils.hpp:34-37 per coordinate (mean_step): the ordered points'
+  // coordinates and the fp64 reciprocals staged in LDS chunks by the whole
+  // workgroup, lanes 0..2 walking each chunk
+  float p = 0.0f, c = 1.0f;
+  for (int e0 = 0; e0 < cnt; e0 += kHdsChunk) {
+    const int m = cnt - e0 < kHdsChunk ? cnt - e0 : kHdsChunk;
+    for (int e = tid; e < m; e += nt) {
+      const uint32_t i = out[e0 + e];
+      cb[e] = x[i];
+      cb[kHdsChunk + e] = y[i];
+      cb[2 * kHdsChunk + e] = z[i];
+      rb[e] = 1.0 / (double)(e0 + e + 1);
     }
+    __syncthreads();
+    if (tid < 3) {
+      const float* cv = cb + tid * kHdsChunk;
+      int e = 0;
+      if (e0 == 0) {
+        p = cv[0];
+        e = 1;
+      }
+#pragma unroll 4
+      for (; e < m; e++) {
+        p = mean_step(p, c, cv[e], rb[e]);  // c == e0 + e
+        c += 1.0f;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < 3) {
     (tid == 0 ? d.ox : (tid == 1 ? d.oy : d.oz))[v] = p;
     if (tid == 0) {
       d.oi[v] = in ? in[i0] : 0.0f;
@@ -561,9 +693,12 @@ __global__ void __launch_bounds__(256) k_hds_big(DownsampleBufs d, const int* __
   if (need && !*need) return;
   const HdsIn a = *d.arg;
   __shared__ uint32_t bm[kHdsWords];
+  __shared__ float cb[3 * kHdsChunk];
+  __shared__ double rb[kHdsChunk];
   __shared__ int s_w[4], s_base;
   const int nbig = d.hflags[3];
-  for (int q = blockIdx.x; q < nbig; q += gridDim.x) hds_big_voxel(d, d.bigv[q], a.x, a.y, a.z, a.in, bm, s_w, &s_base);
+  for (int q = blockIdx.x; q < nbig; q += gridDim.x)
+    hds_big_voxel(d, d.bigv[q], a.x, a.y, a.z, a.in, bm, s_w, &s_base, cb, rb);
 }
 
 // The /2 fallback pass of local_mapping.cpp:399-403 as ONE workgroup (it is
@@ -577,6 +712,8 @@ __global__ void __launch_bounds__(kHdsFbThreads) k_hds_fallback(double size, Dow
                                                                 const int* __restrict__ need) {
   if (!*need) return;
   __shared__ uint32_t bm[kHdsWords];
+  __shared__ float cb[3 * kHdsChunk];
+  __shared__ double rb[kHdsChunk];
   __shared__ unsigned long long s_w64[kHdsFbThreads / 64];
   __shared__ int s_w[kHdsFbThreads / 64], s_base, s_nbig;
   const HdsIn a = *d.arg;
@@ -678,7 +815,7 @@ __global__ void __launch_bounds__(kHdsFbThreads) k_hds_fallback(double size, Dow
   __syncthreads();
   // 5. dense voxels, one after the other by the whole workgroup (k_hds_big)
   const int nbig = s_nbig;
-  for (int q = 0; q < nbig; q++) hds_big_voxel(d, d.bigv[q], x, y, z, in, bm, s_w, &s_base);
+  for (int q = 0; q < nbig; q++) hds_big_voxel(d, d.bigv[q], x, y, z, in, bm, s_w, &s_base, cb, rb);
 }
 
 // the pipeline's downsample, asynchronous on stream s; with `fallback`, the
@@ -708,7 +845,8 @@ int ds_enqueue_hashed(vg_ctx* ctx, hipStream_t s, const float* x, const float* y
       k_hds_rank<<<ntile, kBlock, 0, st>>>(d, nullptr, fallback ? need : nullptr, 2000);
       k_hds_scatter<<<g, kBlock, 0, st>>>(d, nullptr);
       k_hds_mean<<<g, kBlock, 0, st>>>(d, nullptr);
-      k_hds_big<<<64, kBlock, 0, st>>>(d, nullptr);
+      k_hds_mid<<<grid_for(cap / kHdsSmall + 1, kBlock / 64, 1024), kBlock, 0, st>>>(d, nullptr);
+      k_hds_big<<<256, kBlock, 0, st>>>(d, nullptr);
       if (fallback) k_hds_fallback<<<1, kHdsFbThreads, 0, st>>>(voxel / 2, d, need);
     };
     const bool use_graph = ctx->use_graphs && fallback && voxel == ctx->cfg.down_size;
@@ -768,7 +906,8 @@ int ds_alloc(vg_ctx* ctx) {
   d.bigv = ctx->arena.take<int>(n);
   d.pseg2 = ctx->arena.take<uint32_t>(n);
   d.tsum = ctx->arena.take<int>(2 * ((size_t)n / kHdsTile + 2));
-  d.hflags = ctx->arena.take<int>(4);
+  d.hflags = ctx->arena.take<int>(8);
+  d.cap = n;
   if (!d.keys || !d.seg || !d.oc || !d.tmp || !d.hkey || !d.hoff || !d.pseg || !d.tsum || !d.hflags) {
     ctx->err = "arena exhausted (downsample)";
     return VG_E_CAPACITY;
@@ -804,7 +943,7 @@ int ds_reset(vg_ctx* ctx) {
   VG_HIP(hipMemsetAsync(d.hfirst, 0x7f, hs * sizeof(int), s));  // 0x7f7f7f7f: above every point index
   VG_HIP(hipMemsetAsync(d.hcnt, 0, hs * sizeof(int), s));
   VG_HIP(hipMemsetAsync(d.hfill, 0, hs * sizeof(int), s));
-  VG_HIP(hipMemsetAsync(d.hflags, 0, 4 * sizeof(int), s));
+  VG_HIP(hipMemsetAsync(d.hflags, 0, 8 * sizeof(int), s));
   VG_HIP(hipStreamSynchronize(s));
   return VG_OK;
 }

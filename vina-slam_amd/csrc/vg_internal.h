@@ -100,13 +100,14 @@ struct DownsampleBufs {
   uint64_t* hkey = nullptr;
   int *hfirst = nullptr, *hcnt = nullptr, *hfill = nullptr, *hrank = nullptr, *hoff = nullptr;
   int hmask = 0;
+  int cap = 0;                // max points per scan (bigv's length: dense voxels from the front, mid-size from the back)
   uint32_t* pslot = nullptr;  // per point: its voxel's table slot
   uint32_t* pseg = nullptr;   // point indices grouped by voxel
   int* vfirst = nullptr;      // per voxel (output rank): its first point
   int* bigv = nullptr;        // dense voxels (output ranks) deferred to k_hds_big
   uint32_t* pseg2 = nullptr;  // dense voxels' segments back in input order
   int* tsum = nullptr;        // per 1024-point tile: first points, their points
-  int* hflags = nullptr;      // [0] range error (until the insert takes it), [1] n_out, [2] fallback needed, [3] dense voxels
+  int* hflags = nullptr;      // [0] range error (until the insert takes it), [1] n_out, [2] fallback needed, [3] dense voxels, [4] mid-size voxels
 };
 
 // ---- device-resident voxel map (replaces unordered_map<VOXEL_LOC, OctoTree*>
