@@ -66,11 +66,13 @@ def parse():
     ap.add_argument("--hash-log2", type=int, default=0, help="context capacity: root hash slots, log2 (0: default)")
     ap.add_argument("--multi", default="2,4,8,16",
                     help="multi-sequence mode (vg_multi_*): B values to time at N=1 (empty: skip); each B runs "
-                         "in a child process of its own, before this one touches the GPU; B distinct sequences")
-    ap.add_argument("--multi-1m", default="1,2,4",
+                         "in ceil(B / --multi-group) child processes started before this one touches the GPU and "
+                         "released together; B distinct sequences")
+    ap.add_argument("--multi-1m", default="1,2,4,8",
                     help="BASELINE config 5 (synthetic 1M-ray scans, batched): B values of the multi-sequence "
                          "mode on the 1M workload at N=1 (empty: skip)")
     ap.add_argument("--multi-1m-steps", type=int, default=10, help="timed scans per sequence of the 1M leg")
+    ap.add_argument("--multi-group", type=int, default=4, help="sequences per process in the multi-sequence legs")
     ap.add_argument("--multi-child", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--multi-scans", default="", help=argparse.SUPPRESS)
     ap.add_argument("--multi-max-points", type=int, default=0, help=argparse.SUPPRESS)
@@ -380,7 +382,10 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None):
     paths = []
     out = {"lidar": lidar, "unit": "scans/s", "steps": steps, "warmup": warmup,
            "workers": "one native thread + one stream per sequence", "inputs": "B distinct sequences",
-           "wait_policy": "spin", "process": "one per B, fresh HIP runtime", "env": {"GPU_MAX_HW_QUEUES": "16"},
+           "wait_policy": "spin", "process": "ceil(B/%d) concurrent processes of <= %d sequences, released together "
+                                                 "after their warm-up; rate = B x steps / (release -> last end)"
+                                                 % (args.multi_group, args.multi_group),
+           "env": {"GPU_MAX_HW_QUEUES": "16"},
            "by_B": {}}
     npmax = 0
     try:
@@ -400,19 +405,52 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None):
         hwq = os.environ.get("VG_MULTI_HWQ", "16")  # experiments only; the line records what ran
         out["env"]["GPU_MAX_HW_QUEUES"] = hwq
         env = dict(os.environ, GPU_MAX_HW_QUEUES=hwq)
+        wait = os.environ.get("VG_MULTI_WAIT", "")  # experiments: "spin_us,sleep_us" (the line records it)
+        if wait:
+            out["wait_policy"] = "spin %s us, then sleep %s us" % tuple(wait.split(","))
+        grp = args.multi_group
         for B in Bs:
             beat("multi-sequence %s: B = %d" % (lidar, B))
-            cmd = [sys.executable, os.path.abspath(__file__), "--multi-child", str(B),
-                   "--multi-scans", ",".join(paths[:B]), "--multi-max-points", str(npmax + 16),
-                   "--lidar", lidar, "--config", args.config, "--steps", str(steps), "--warmup", str(args.warmup),
-                   "--max-nodes", str(args.max_nodes), "--max-fix", str(args.max_fix),
-                   "--hash-log2", str(args.hash_log2)]
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
-            if r.returncode != 0:
-                raise RuntimeError("multi-sequence child B=%d failed (%d): %s" % (B, r.returncode, r.stderr[-2000:]))
-            res = json.loads(r.stdout.strip().splitlines()[-1])
-            out["by_B"][str(B)] = res["scans_per_s"]
-            out.setdefault("points_per_scan", res["points_per_scan"])
+            # ceil(B / grp) processes of at most grp sequences each (measured:
+            # one process stepping more than 4 sequences falls off a cliff,
+            # B = 6 at ~1,800 scans/s against ~3,000 for B = 4, while two
+            # processes of 4 run ~6,000), started together: each child warms
+            # up, reports READY and waits; the parent then releases all of
+            # them at once and times the job from GO to the last child's end
+            P = (B + grp - 1) // grp
+            sizes = [B // P + (1 if q < B % P else 0) for q in range(P)]
+            runs, first_seq = [], 0
+            for q in range(P):
+                cmd = [sys.executable, os.path.abspath(__file__), "--multi-child", str(sizes[q]),
+                       "--multi-scans", ",".join(paths[first_seq:first_seq + sizes[q]]),
+                       "--multi-max-points", str(npmax + 16),
+                       "--lidar", lidar, "--config", args.config, "--steps", str(steps), "--warmup", str(args.warmup),
+                       "--max-nodes", str(args.max_nodes), "--max-fix", str(args.max_fix),
+                       "--hash-log2", str(args.hash_log2)]
+                first_seq += sizes[q]
+                runs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env))
+            for r in runs:  # every child warmed up and idle
+                line = r.stdout.readline()
+                if line.strip() != "READY":
+                    for x in runs:
+                        x.kill()
+                    raise RuntimeError("multi-sequence child B=%d: %r" % (B, line[-500:]))
+            t0 = time.perf_counter()
+            for r in runs:
+                r.stdin.write("GO\n")
+                r.stdin.flush()
+            res = []
+            for r in runs:
+                res.append(json.loads(r.stdout.readline()))
+            wall = time.perf_counter() - t0
+            for r in runs:
+                r.stdin.close()
+                r.wait(timeout=60)
+                if r.returncode != 0:
+                    raise RuntimeError("multi-sequence child B=%d failed (%d)" % (B, r.returncode))
+            out["by_B"][str(B)] = round(B * steps / wall, 1)
+            out.setdefault("processes_by_B", {})[str(B)] = P
+            out.setdefault("points_per_scan", res[0]["points_per_scan"])
     finally:
         for path in paths:
             os.unlink(path)
@@ -444,7 +482,8 @@ def multi_child(args, p, g, warmup, total):
     ctxs = [vgpu.Context(vgconfig.to_c(p), device=0, max_points=args.multi_max_points, **CAP) for _ in range(B)]
     for c in ctxs:
         c.seed(seq.gt_state(0))  # every synthetic sequence follows the same trajectory (synth.Trajectory)
-    mv = vgpu.Multi(ctxs, 0, 0)
+    wait = os.environ.get("VG_MULTI_WAIT", "")
+    mv = vgpu.Multi(ctxs, *([int(v) for v in wait.split(",")] if wait else [0, 0]))
 
     def step(k):
         scans = []
@@ -457,17 +496,20 @@ def multi_child(args, p, g, warmup, total):
         step(k)
     mv.sync()
     torch.cuda.synchronize(dev)
+    print("READY", flush=True)  # the parent releases every child of this B at once
+    if sys.stdin.readline().strip() != "GO":
+        return 1
     t0 = time.perf_counter()
     for k in range(warmup, total):
         step(k)
     mv.sync()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    npts = int(np.mean([d[k][1] for d in data for k in range(warmup, total)]))
+    print(json.dumps({"B": B, "scans_per_s": round(B * (total - warmup) / dt, 1), "points_per_scan": npts}), flush=True)
     mv.close()
     for c in ctxs:
         c.close()
-    npts = int(np.mean([d[k][1] for d in data for k in range(warmup, total)]))
-    print(json.dumps({"B": B, "scans_per_s": round(B * (total - warmup) / dt, 1), "points_per_scan": npts}))
     return 0
 
 

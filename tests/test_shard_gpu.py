@@ -46,11 +46,13 @@ def _run(cfgname, lidar, nscan, rank, world, q, port):
             seqn = [0]
 
             def allreduce(arr):
-                if log:  # debugging aid: every exchange of this rank, in order
-                    with open("%s.%d" % (log, rank), "a") as f:
-                        f.write("%d %d %s\n" % (seqn[0], arr.size, arr.dtype))
-                seqn[0] += 1
+                pre = hash(arr.tobytes()) if log else 0
                 dist.all_reduce(torch.from_numpy(arr))
+                if log:  # debugging aid: every exchange of this rank, in order (input / result digests)
+                    with open("%s.%d" % (log, rank), "a") as f:
+                        f.write("%d %d %s %x %x\n" % (seqn[0], arr.size, arr.dtype, pre & 0xffffffff,
+                                                     hash(arr.tobytes()) & 0xffffffff))
+                seqn[0] += 1
 
             ctx.shard_host(rank, world, allreduce)
         ctx.seed(seq.gt_state(0))

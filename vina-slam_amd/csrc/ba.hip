@@ -1287,8 +1287,14 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
       if (queued) tail_at = enq;
     }
     VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ba, seq0 + k, "k_ba_control"));
+    // The flags may already come from iteration k+1 (queued ahead, possibly
+    // finished by now): decide on iteration k's outcome only — done at or
+    // before it (the device stops counting once done) — so the number of
+    // iterations enqueued never depends on timing (sharded mode: every
+    // enqueue is an exchange, all ranks must enqueue alike)
     done_iters = __atomic_load_n(&ctx->h_pub->ba_iters, __ATOMIC_ACQUIRE);
-    if (__atomic_load_n(&ctx->h_pub->ba_done, __ATOMIC_ACQUIRE)) break;
+    if (__atomic_load_n(&ctx->h_pub->ba_done, __ATOMIC_ACQUIRE) && done_iters <= k + 1) break;
+    done_iters = k + 1;
     if (enq == k + 1 && enq < 10) iteration(enq++);  // not queued ahead: now
   }
   if (tail_ok) *tail_ok = tail_at > 0 && done_iters <= tail_at;  // the gate opened for that copy

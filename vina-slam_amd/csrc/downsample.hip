@@ -845,7 +845,7 @@ int ds_enqueue_hashed(vg_ctx* ctx, hipStream_t s, const float* x, const float* y
       k_hds_rank<<<ntile, kBlock, 0, st>>>(d, nullptr, fallback ? need : nullptr, 2000);
       k_hds_scatter<<<g, kBlock, 0, st>>>(d, nullptr);
       k_hds_mean<<<g, kBlock, 0, st>>>(d, nullptr);
-      k_hds_mid<<<grid_for(cap / kHdsSmall + 1, kBlock / 64, 1024), kBlock, 0, st>>>(d, nullptr);
+      k_hds_mid<<<grid_for(cap / kHdsSmall + 1, kBlock / 64, 256), kBlock, 0, st>>>(d, nullptr);
       k_hds_big<<<256, kBlock, 0, st>>>(d, nullptr);
       if (fallback) k_hds_fallback<<<1, kHdsFbThreads, 0, st>>>(voxel / 2, d, need);
     };

@@ -204,6 +204,59 @@ __device__ __forceinline__ bool inside(const NodeHdr& h, const V3& w) {
 }
 
 
+// ---- wave sums without LDS: the partner across lane bit L (lane ^ L) via
+// gfx950's v_permlane32_swap / v_permlane16_swap and DPP (row_ror:8, row
+// shifts by 4, quad perms)
+__device__ __forceinline__ double pack_d(unsigned lo, unsigned hi) {
+  return __longlong_as_double(((long long)hi << 32) | lo);
+}
+template <int C>
+__device__ __forceinline__ unsigned dpp32(unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, C, 0xf, 0xf, false);
+}
+template <int L>
+__device__ __forceinline__ double xor_lane(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+  if constexpr (L == 32) {  // r[0] = x[lane % 32], r[1] = x[lane % 32 + 32]
+    auto l2 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    auto h2 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return (lane & 32) ? pack_d(l2[0], h2[0]) : pack_d(l2[1], h2[1]);
+  } else if constexpr (L == 16) {  // r[0] = the even row's x, r[1] = the odd row's
+    auto l2 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    auto h2 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return (lane & 16) ? pack_d(l2[0], h2[0]) : pack_d(l2[1], h2[1]);
+  } else if constexpr (L == 8) {
+    return pack_d(dpp32<0x128>(lo), dpp32<0x128>(hi));  // row_ror:8
+  } else if constexpr (L == 4) {
+    const double up = pack_d(dpp32<0x104>(lo), dpp32<0x104>(hi));  // row_shl:4 (lane i <- i + 4)
+    const double dn = pack_d(dpp32<0x114>(lo), dpp32<0x114>(hi));  // row_shr:4 (lane i <- i - 4)
+    return (lane & 4) ? dn : up;
+  } else if constexpr (L == 2) {
+    return pack_d(dpp32<0x4E>(lo), dpp32<0x4E>(hi));  // quad_perm [2,3,0,1]
+  } else {
+    return pack_d(dpp32<0xB1>(lo), dpp32<0xB1>(hi));  // quad_perm [1,0,3,2]
+  }
+}
+// one level of a halving wave sum: the lanes with bit L clear keep the first
+// ceil(N/2) values, the others the rest, each adding its partner's copy
+template <int L, int N>
+__device__ __forceinline__ void halve(const double (&v)[N], double (&w)[(N + 1) / 2], int lane, int& idx, int& n) {
+  constexpr int H = (N + 1) / 2;
+  const bool hi = (lane & L) != 0;
+#pragma unroll
+  for (int j = 0; j < H; j++) {
+    const double a = v[j], b = (H + j < N) ? v[H + j] : 0.0;
+    w[j] = (hi ? b : a) + xor_lane<L>(hi ? a : b, lane);
+  }
+  if (hi) {
+    idx += H;
+    n = n > H ? n - H : 0;
+  } else {
+    n = n < H ? n : H;
+  }
+}
+
 // The pose (x_curr R, p and the rotation / translation covariance blocks) is
 // read from the device state the previous k_iekf_update wrote; the kernel is a
 // no-op once the IEKF has finished (st->done). Iteration 0 ignores the leaf
@@ -304,18 +357,23 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
     }
   }
   if (blockIdx.x == 0) VG_PROBE_MARK(30);  // the point loop (thread 0 of block 0)
-  // block reduction: wave shuffles then LDS across the 4 waves (fixed tree)
+  // block reduction: a halving butterfly per wave, then LDS across the 4
+  // waves (fixed tree). Every level pairs lane ^ L for L = 32, 16, ..., 1, so
+  // each sum is bit for bit lane 0's of a shfl_down tree, but a lane hands
+  // over half of the values it carries at every level: 37 exchanges for the
+  // 34 sums instead of 204, through permlane / DPP instead of LDS
   __shared__ double red[4][kIekfVals];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // the same tree per value, but the 34 values step together: each level's
-  // exchanges are independent and overlap (34 chains of 6, not 204 in a row)
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-    for (int j = 0; j < kIekfVals; j++) acc[j] += __shfl_down(acc[j], off, 64);
-  if (lane == 0)
-#pragma unroll
-    for (int j = 0; j < kIekfVals; j++) red[wv][j] = acc[j];
+  static_assert(kIekfVals == 34, "the halving levels below are laid out for 34 sums");
+  int ridx = 0, rn = kIekfVals;
+  double h17[17], h9[9], h5[5], h3[3], h2[2], h1[1];
+  halve<32>(acc, h17, lane, ridx, rn);
+  halve<16>(h17, h9, lane, ridx, rn);
+  halve<8>(h9, h5, lane, ridx, rn);
+  halve<4>(h5, h3, lane, ridx, rn);
+  halve<2>(h3, h2, lane, ridx, rn);
+  halve<1>(h2, h1, lane, ridx, rn);
+  if (rn == 1) red[wv][ridx] = h1[0];
   __syncthreads();
   if (threadIdx.x < kIekfVals) {
     int j = threadIdx.x;
