@@ -17,6 +17,7 @@ import vgpu  # noqa: E402
 
 PHASES = {3: "load || inv(0)", 10: "wave0: L, tile, y", 11: "wave0: inv(K+1)", 6: "barrier wait",
           5: "w(NB-1)", 7: "backward solve", 8: "trial/q1"}
+EXTRA = {12: "(slowest trailing wave's jobs, summed over phases)"}
 
 
 def main(nscan=40, lidar="64line"):
@@ -42,6 +43,8 @@ def main(nscan=40, lidar="64line"):
         tot += us
         print("  %-16s %8.2f us/call" % (name, us))
     print("  %-16s %8.2f us/call" % ("total", tot))
+    for k, name in EXTRA.items():
+        print("  %8.2f us/call %s" % (buf[k] * 0.01 / calls, name))
     L.vg_probe_read_map(buf, 64)
     na = max(buf[62], 1)
     print("k_rc_apply calls:", buf[62])

@@ -6,11 +6,13 @@ CPU: the oracle's restatements are pinned by known answers — the
 ColPivHouseholderQR solve of A n = -1 against numpy's least squares, the exact
 kNN against a numpy brute force — and its kd-tree LIO registers init scans of
 the synthetic sequence to the true poses from perturbed priors.
-GPU (marked): vg_lio_kdtree (device hashed-grid kNN, plane fits, sums)
-reproduces the oracle on the same scans and priors: identical seeding, valid
-correspondence counts within 0.2 %, states within 1e-6 rad / 1e-6 m, the 0.5 m
-init maps equal as sets to 1e-5 m (different summation order of the normal
-equations, rounding-level). Parity of the kNN step itself is exact (same
+GPU (marked): vg_lio_kdtree (device hashed-grid kNN, plane fits, the normal
+equations summed in point order like the reference) reproduces the oracle on
+the same scans and priors: identical seeding, valid correspondence counts and
+iteration counts exact, states (pose, covariance) and the 0.5 m init maps
+(as sets) equal bit for bit. (Round 2 summed the normal equations in a block tree: a
+rounding-level difference that a later iteration's re-find turned into ±0.2 %
+of the correspondences and 1e-6 in the states.) The kNN step is exact (same
 neighbour sets) up to float distance ties, which the scans here do not hit.
 PCL/FLANN and Eigen are absent: parity unpinned on the reference
 side beyond these known answers."""
@@ -120,14 +122,19 @@ def test_gpu_kdtree_lio_matches_oracle(oracle_lib):
         sg, vg_, ig = ctx.lio_kdtree(ds, prior)
         assert (vg_ == -1) == (vo == -1), k
         if vo >= 0:
-            assert abs(vg_ - vo) <= max(2, int(0.002 * vo)), (k, vg_, vo)
+            # the normal equations are summed in point order as the reference
+            # does (k_kd_sum), so the correspondence sets, the counts and the
+            # states agree bit for bit
+            print(k, "valid", vg_, vo, "iters", ig, io, "dR %.1e dp %.1e dcov %.1e" % (
+                np.abs(sg[1:10] - so[1:10]).max(), np.abs(sg[10:13] - so[10:13]).max(),
+                np.abs(sg[25:] - so[25:]).max()))
+            assert vg_ == vo, (k, vg_, vo)
             assert ig == io, (k, ig, io)
-            assert np.abs(sg[1:10] - so[1:10]).max() < 1e-6, k
-            assert np.abs(sg[10:13] - so[10:13]).max() < 1e-6, k
-            assert np.abs(sg[25:] - so[25:]).max() < 1e-9, k
+            assert np.array_equal(sg, so), k  # observed: every state entry equal bit for bit
         mg, mo = ctx.kdmap(), orc.kdmap()
         assert mg.shape == mo.shape, (k, mg.shape, mo.shape)
         a = mg[np.lexsort(mg.T[::-1])]
         o = mo[np.lexsort(mo.T[::-1])]
-        assert np.abs(a - o).max() < 1e-5, k
+        print(k, "map", mg.shape[0], "max diff %.1e" % np.abs(a - o).max())
+        assert np.array_equal(a.view(np.uint32), o.view(np.uint32)), k
     ctx.close()

@@ -617,6 +617,10 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
   const int lane = tid & 63, wave = tid >> 6;
   const int cc = lane & 15, rq = lane >> 4;
   const double u = st->u;
+#ifdef VG_PROBE
+  __shared__ unsigned s_tmax;
+  if (tid == 0) s_tmax = 0;
+#endif
   VG_PROBE_BEGIN();
 
   // -S^-1 of a diagonal tile held in registers (D layout), on one wave
@@ -717,6 +721,7 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
   // other waves fill the tile store and the vectors
   v4d tinv;  // wave 0: -S_KK^-1 of the current panel, kept in registers
   if (wave == 0) {
+    __builtin_amdgcn_s_setprio(3);  // the critical chain issues first on its SIMD
     tinv = diag(ld_tile(timg));
     st_tile(T, tinv);
   } else {
@@ -765,8 +770,13 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
       st_tile(&T[tix(K + 1, K + 1) * 256], tinv);
       VG_PROBE_MARK(11);
     } else if (wave & 3) {
-      // the twelve waves off wave 0's SIMD: job 0 = w_K and y_{K+1}, then
-      // row pieces of up to four tiles
+      // the twelve waves off wave 0's SIMD: job 0 = w_K and y_{K+1}, then row
+      // pieces of up to four tiles (the three other waves on wave 0's SIMD
+      // stay idle: as helpers they slowed the critical chain more than they
+      // shortened the trailing update, phase clocks 34.1 -> 35.5 us)
+#ifdef VG_PROBE
+      const unsigned long long tj0 = wall_clock64();
+#endif
       const int wk = wave - (wave >> 2) - 1;
       constexpr int nwk = 12;
       const v4d tv = ld_ops(&T[tix(K, K) * 256]);
@@ -789,8 +799,17 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
             pend(gt, tix(I, K));
           }
         }
+#ifdef VG_PROBE
+      if (lane == 0) atomicMax(&s_tmax, (unsigned)(wall_clock64() - tj0));
+#endif
     }
     __syncthreads();
+#ifdef VG_PROBE
+    if (tid == 0) {
+      atomicAdd(&g_probe[12], (unsigned long long)s_tmax);  // the slowest trailing wave's job time
+      s_tmax = 0;
+    }
+#endif
     VG_PROBE_MARK(6);
   }
   flush();

@@ -129,69 +129,102 @@ struct KdPose {
   double R[9], p[3], eR[9], et[3];
 };
 
-// odometry.cpp:336-384 per point, then the block's 28 sums
+// odometry.cpp:342-381 per point with refind set: the 5 nearest map points,
+// the plane fit and its check -> ds[i] (-1: rejected) and the unit normal
 __global__ void __launch_bounds__(kKdBlock) k_kd_pass(int n, const float* __restrict__ px, const float* __restrict__ py,
-                                                      const float* __restrict__ pz, KdPose ps, int refind, KdMap kd) {
-  double acc[kKdSums];
-#pragma unroll
-  for (int k = 0; k < kKdSums; k++) acc[k] = 0.0;
+                                                      const float* __restrict__ pz, KdPose ps, KdMap kd) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    const M3 R = ld_m3(ps.R);
-    const V3 pnt = rigid(ld_m3(ps.eR), v3(px[i], py[i], pz[i]), ld_v3(ps.et));  // var_init (point_utils.cpp:36-52)
-    const V3 wld = rigid(R, pnt, ld_v3(ps.p));
-    if (refind) {
-      float bd[kNn];
-      int bi[kNn];
-      kd_knn(kd, (float)wld[0], (float)wld[1], (float)wld[2], bd, bi);
-      double A[kNn * 3], b[kNn];
-      for (int r = 0; r < kNn; r++) {
-        A[r * 3 + 0] = kd.x[bi[r]];
-        A[r * 3 + 1] = kd.y[bi[r]];
-        A[r * 3 + 2] = kd.z[bi[r]];
-        b[r] = -1.0;
+  if (i >= n) return;
+  const M3 R = ld_m3(ps.R);
+  const V3 pnt = rigid(ld_m3(ps.eR), v3(px[i], py[i], pz[i]), ld_v3(ps.et));  // var_init (point_utils.cpp:36-52)
+  const V3 wld = rigid(R, pnt, ld_v3(ps.p));
+  float bd[kNn];
+  int bi[kNn];
+  kd_knn(kd, (float)wld[0], (float)wld[1], (float)wld[2], bd, bi);
+  double A[kNn * 3], b[kNn];
+  for (int r = 0; r < kNn; r++) {
+    A[r * 3 + 0] = kd.x[bi[r]];
+    A[r * 3 + 1] = kd.y[bi[r]];
+    A[r * 3 + 2] = kd.z[bi[r]];
+    b[r] = -1.0;
+  }
+  double dir[3];
+  colpiv_qr_solve(A, kNn, b, dir);
+  bool off = false;
+  for (int r = 0; r < kNn; r++)
+    if (fabs(((dir[0] * A[r * 3] + dir[1] * A[r * 3 + 1]) + dir[2] * A[r * 3 + 2]) + 1.0) > 0.1) off = true;
+  if (off) {
+    kd.ds[i] = -1.0;
+  } else {
+    const double d = 1.0 / sqrt((dir[0] * dir[0] + dir[1] * dir[1]) + dir[2] * dir[2]);
+    kd.ds[i] = d;
+    for (int c = 0; c < 3; c++) kd.dir[(size_t)i * 3 + c] = dir[c] * d;
+  }
+}
+
+// the iteration's normal equations (odometry.cpp:367-378): HTH += jac jac^T,
+// HTz += jac (-pd2), valid++ over the scan's points IN POINT ORDER, as the
+// reference accumulates them — one workgroup: 1024 points at a time get their
+// Jacobian row in parallel (LDS), then lane k of wave 0 adds sum k's terms in
+// order (HTH upper 21, HTz 6, the count). The sums, and so the 15x15 update
+// on the host, are the reference's bit for bit.
+constexpr int kKdSumThreads = 1024;
+__global__ void __launch_bounds__(kKdSumThreads) k_kd_sum(int n, const float* __restrict__ px,
+                                                          const float* __restrict__ py, const float* __restrict__ pz,
+                                                          KdPose ps, KdMap kd) {
+  __shared__ double sj[7][kKdSumThreads];  // jac 0..5, -pd2
+  __shared__ unsigned char sv[kKdSumThreads];
+  const int tid = threadIdx.x;
+  const M3 R = ld_m3(ps.R);
+  const M3 Rt = tr(R);
+  double acc = 0.0;
+  int cnt = 0;
+  // sum k (wave 0, lane k < 27): HTH (r, c) upper row-major, then HTz r
+  int kr = 0, kc = 0;
+  if (tid < 21) {
+    int k = tid;
+    while (k >= 6 - kr) {
+      k -= 6 - kr;
+      kr++;
+    }
+    kc = kr + k;
+  } else if (tid < 27) {
+    kr = tid - 21;
+    kc = 6;
+  }
+  for (int c0 = 0; c0 < n; c0 += kKdSumThreads) {
+    const int i = c0 + tid;
+    unsigned char v = 0;
+    if (i < n) {
+      const double dsi = kd.ds[i];
+      if (dsi >= 0) {
+        const V3 pnt = rigid(ld_m3(ps.eR), v3(px[i], py[i], pz[i]), ld_v3(ps.et));
+        const V3 wld = rigid(R, pnt, ld_v3(ps.p));
+        const V3 nv = v3(kd.dir[(size_t)i * 3], kd.dir[(size_t)i * 3 + 1], kd.dir[(size_t)i * 3 + 2]);
+        const double pd2 = ((nv[0] * wld[0] + nv[1] * wld[1]) + nv[2] * wld[2]) + dsi;
+        const V3 j0 = mul(mul(hat(pnt), Rt), nv);
+        for (int c = 0; c < 3; c++) {
+          sj[c][tid] = j0[c];
+          sj[3 + c][tid] = nv[c];
+        }
+        sj[6][tid] = -pd2;
+        v = 1;
       }
-      double dir[3];
-      colpiv_qr_solve(A, kNn, b, dir);
-      bool off = false;
-      for (int r = 0; r < kNn; r++)
-        if (fabs(((dir[0] * A[r * 3] + dir[1] * A[r * 3 + 1]) + dir[2] * A[r * 3 + 2]) + 1.0) > 0.1) off = true;
-      if (off) {
-        kd.ds[i] = -1.0;
+    }
+    sv[tid] = v;
+    __syncthreads();
+    if (tid < kKdSums) {
+      const int m = n - c0 < kKdSumThreads ? n - c0 : kKdSumThreads;
+      if (tid == kKdSums - 1) {
+        for (int t = 0; t < m; t++) cnt += sv[t];
       } else {
-        const double d = 1.0 / sqrt((dir[0] * dir[0] + dir[1] * dir[1]) + dir[2] * dir[2]);
-        kd.ds[i] = d;
-        for (int c = 0; c < 3; c++) kd.dir[(size_t)i * 3 + c] = dir[c] * d;
+        for (int t = 0; t < m; t++)
+          if (sv[t]) acc += sj[kr][t] * sj[kc][t];
       }
     }
-    const double dsi = kd.ds[i];
-    if (dsi >= 0) {
-      const V3 nv = v3(kd.dir[(size_t)i * 3], kd.dir[(size_t)i * 3 + 1], kd.dir[(size_t)i * 3 + 2]);
-      const double pd2 = ((nv[0] * wld[0] + nv[1] * wld[1]) + nv[2] * wld[2]) + dsi;
-      const V3 j0 = mul(mul(hat(pnt), tr(R)), nv);
-      double jac[6] = {j0[0], j0[1], j0[2], nv[0], nv[1], nv[2]};
-      int k = 0;
-      for (int r = 0; r < 6; r++)
-        for (int c = r; c < 6; c++) acc[k++] = jac[r] * jac[c];
-      for (int r = 0; r < 6; r++) acc[21 + r] = jac[r] * (-pd2);
-      acc[27] = 1.0;
-    }
+    __syncthreads();
   }
-  __shared__ double red[kKdSums][kKdBlock / 64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1)  // every sum's level at once (independent exchanges overlap)
-#pragma unroll
-    for (int k = 0; k < kKdSums; k++) acc[k] += __shfl_down(acc[k], off, 64);
-  if (lane == 0)
-#pragma unroll
-    for (int k = 0; k < kKdSums; k++) red[k][wv] = acc[k];
-  __syncthreads();
-  if ((int)threadIdx.x < kKdSums) {
-    double v = 0.0;
-    for (int w = 0; w < kKdBlock / 64; w++) v += red[threadIdx.x][w];
-    kd.part[(size_t)blockIdx.x * kKdSums + threadIdx.x] = v;
-  }
+  if (tid < kKdSums) kd.part[tid] = tid == kKdSums - 1 ? (double)cnt : acc;
 }
 
 // the registered scan (world, float) appended to the map (odometry.cpp:427-435)
@@ -285,14 +318,12 @@ int kd_pass(vg_ctx* ctx, int n, const double* R, const double* p, int refind, do
     ctx->err = "kd pass: scan larger than max_points_per_scan";
     return VG_E_CAPACITY;
   }
-  const int nb = (n + kKdBlock - 1) / kKdBlock;
-  k_kd_pass<<<nb, kKdBlock, 0, s>>>(n, ctx->d_x, ctx->d_y, ctx->d_z, kd_pose(ctx, R, p), refind, kd);
+  const KdPose ps = kd_pose(ctx, R, p);
+  if (refind) k_kd_pass<<<(n + kKdBlock - 1) / kKdBlock, kKdBlock, 0, s>>>(n, ctx->d_x, ctx->d_y, ctx->d_z, ps, kd);
+  k_kd_sum<<<1, kKdSumThreads, 0, s>>>(n, ctx->d_x, ctx->d_y, ctx->d_z, ps, kd);
   VG_HIP(hipGetLastError());
-  std::vector<double> h((size_t)nb * kKdSums);
-  VG_HIP(hipMemcpyAsync(h.data(), kd.part, h.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  VG_HIP(hipMemcpyAsync(out28, kd.part, kKdSums * sizeof(double), hipMemcpyDeviceToHost, s));
   VG_HIP(hipStreamSynchronize(s));
-  for (int b = 0; b < nb; b++)  // ordered block sum (deterministic)
-    for (int k = 0; k < kKdSums; k++) out28[k] += h[(size_t)b * kKdSums + k];
   return VG_OK;
 }
 
