@@ -946,12 +946,15 @@ __global__ void __launch_bounds__(256) k_ins_scatter(int n_arg, const int* __res
 // lanes 0-8 own the frame cluster, 9-17 the accumulated cluster, 18-62
 // cov_add (see role_inc)
 constexpr int kPushWaves = 4;
+constexpr int kPwBits = 1 << 15;  // point indices per bitmap window of k_push_window (4 KB of LDS per wave)
+constexpr int kPwWords = kPwBits / 32;
 __global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __restrict__ seg_leaf,
                                                                  const int* __restrict__ seg_off,
                                                                  const int* __restrict__ order,
                                                                  int* __restrict__ order2, MP mp, int slot, DevMap m,
                                                                  const double* __restrict__ pw, int thread_num) {
   __shared__ double E[kPushWaves][64][kErec];
+  __shared__ uint32_t s_bm[kPushWaves][kPwWords];
   if (ins_skip(m, thread_num)) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int role = lane < 63 ? lane : -1;
@@ -974,15 +977,61 @@ __global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __re
           mine = (low == up) ? min(mine, other) : max(mine, other);
         }
     } else {
+      // longer segments: an LDS bitmap over the segment's index range, in
+      // windows of kPwBits indices (set bits compacted in order by a wave
+      // scan): O(L + range / 32) per leaf instead of ranking every point
+      // against every other (O(L^2 / 64) global loads per lane)
+      uint32_t* bm = s_bm[wv];
+      int lo = 0x7fffffff, hi = -1;
       for (int e = lane; e < L; e += 64) {
         const int x = order[j0 + e];
-        int r = 0;
-        for (int t = 0; t < L; t++) r += order[j0 + t] < x ? 1 : 0;
-        order2[j0 + r] = x;
+        lo = min(lo, x);
+        hi = max(hi, x);
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, __shfl_xor(lo, off, 64));
+        hi = max(hi, __shfl_xor(hi, off, 64));
+      }
+      int outpos = 0;
+      for (int w0 = lo; w0 <= hi; w0 += kPwBits) {
+        for (int k = lane; k < kPwWords; k += 64) bm[k] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (int e = lane; e < L; e += 64) {
+          const int off = order[j0 + e] - w0;
+          if (off >= 0 && off < kPwBits) atomicOr(&bm[off >> 5], 1u << (off & 31));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        constexpr int per = kPwWords / 64;  // contiguous words per lane
+        int cnt = 0;
+#pragma unroll
+        for (int k = 0; k < per; k++) cnt += __popc(bm[lane * per + k]);
+        int ex = cnt;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const int y = __shfl_up(ex, off, 64);
+          if (lane >= off) ex += y;
+        }
+        const int total = __shfl(ex, 63, 64);
+        int pos = outpos + ex - cnt;
+#pragma unroll
+        for (int k = 0; k < per; k++) {
+          uint32_t w = bm[lane * per + k];
+          while (w) {
+            const int b = __ffs(w) - 1;
+            w &= w - 1;
+            order2[j0 + pos++] = w0 + (lane * per + k) * 32 + b;
+          }
+        }
+        outpos += total;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      }
     }
     const bool listed = m.hdr[leaf].layer < mp.max_layer;
     if (listed) {  // the leaf's run of this slot (index order), for the recut's subdivisions and the margi
