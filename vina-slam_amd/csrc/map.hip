@@ -86,8 +86,6 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(w.leaf = ctx->arena.take<int>(cw));
   good &= ok(w.pw = ctx->arena.take<double>(cw * 3));
   good &= ok(w.iekf_cache = ctx->arena.take<int>(cw));
-  w.iekf_pv_stride = (cw + 63) / 64 * 64;
-  good &= ok(w.iekf_pv = ctx->arena.take<double>(w.iekf_pv_stride * 12));
   good &= ok(w.pk_leaf = ctx->arena.take<int>(cw));
   good &= ok(w.rc = ctx->arena.take<int>(128));
   good &= ok(w.cand_bits = ctx->arena.take<uint32_t>(ctx->cap.max_nodes / 32 + 1));
@@ -265,7 +263,7 @@ __device__ __forceinline__ void halve(const double (&v)[N], double (&w)[(N + 1) 
 // cache (no association yet, odometry.cpp:111-132).
 __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, int it, DevMap m,
                                               int* __restrict__ cache, double* __restrict__ partials,
-                                              int* __restrict__ pk, double* __restrict__ pv, size_t pvs) {
+                                              int* __restrict__ pk) {
   if (st->done) return;
   VG_PROBE_BEGIN();
   const int n = st->sn;
@@ -291,22 +289,9 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
   const int nb = gridDim.x;
   const int vb = (nb % 8 == 0) ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
   for (int i = vb * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    // var_init (calcBodyVar + the extrinsic) does not change between the
-    // iterations: the first one stores it, the others load it (same bits)
     V3 pnt;
     M3 var;
-    if (it == 0) {
-      var_init_pt(mp, x[i], y[i], z[i], pnt, var);
-#pragma unroll
-      for (int k = 0; k < 3; k++) pv[k * pvs + i] = pnt[k];
-#pragma unroll
-      for (int k = 0; k < 9; k++) pv[(3 + k) * pvs + i] = var[k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < 3; k++) pnt[k] = pv[k * pvs + i];
-#pragma unroll
-      for (int k = 0; k < 9; k++) var[k] = pv[(3 + k) * pvs + i];
-    }
+    var_init_pt(mp, x[i], y[i], z[i], pnt, var);
     M3 var_world = world_var(R, var, pnt, rot_var, tsl_var);
     V3 wld = rigid(R, pnt, p);
     // cache[i]: the leaf of the point's last match (the reference's octos[i],
@@ -419,7 +404,7 @@ __global__ void __launch_bounds__(256) k_iekf_planes(const DState* __restrict__ 
 // agent-scope release per workgroup, which on the multi-XCD MI355X writes back
 // the XCD's L2 each time: measured ~20 us per iteration, far more than the
 // launch it saves.)
-__global__ void __launch_bounds__(256) k_iekf_update(int nb, const double* __restrict__ partials,
+__global__ void __launch_bounds__(1024) k_iekf_update(int nb, const double* __restrict__ partials,
                                                      DState* __restrict__ st, int it) {
   __shared__ IekfLds L;
   if (st->done) return;
@@ -452,17 +437,16 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
   (void)n;  // the scan is read from the device state (state_set_scan)
   const int nb = iekf_blocks(ctx);
   if (ev0) VG_HIP(hipEventRecord(ev0, s));
-  k_iekf<<<nb, 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials, tag ? w.pk_leaf : nullptr, w.iekf_pv,
-                            w.iekf_pv_stride);
+  k_iekf<<<nb, 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials, tag ? w.pk_leaf : nullptr);
   if (ev1) VG_HIP(hipEventRecord(ev1, s));
   if (tag) k_iekf_planes<<<nb, 256, 0, s>>>(ctx->st, ctx->map, w.pk_leaf, tag, &ctx->st->planes[it]);
   if (ctx->shard.world > 1) {  // this shard's sums, all-reduced, then the (replicated) update
     double* sums = ctx->shard.d_buf;
     k_iekf_reduce<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, sums);
     VG_TRY(shard_allreduce(ctx, sums, sums + 64, kIekfVals, 0));
-    k_iekf_update<<<1, 256, 0, s>>>(-1, sums + 64, ctx->st, it);
+    k_iekf_update<<<1, 1024, 0, s>>>(-1, sums + 64, ctx->st, it);
   } else {
-    k_iekf_update<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, it);
+    k_iekf_update<<<1, 1024, 0, s>>>(nb, w.partials, ctx->st, it);
   }
   VG_HIP(hipGetLastError());
   return VG_OK;

@@ -18,8 +18,9 @@ namespace vg {
 constexpr int kIekfVals = 34;  // HTH upper 21, HTz 6, nnt upper 6, match count
 
 // LDS of iekf_update_block
+constexpr int kIekfGroups = 60;  // row groups of the partial sums (1024-lane update: 60 x 17 lanes)
 struct IekfLds {
-  double red[15][kIekfVals];
+  double red[kIekfGroups][kIekfVals];
   double o[kIekfVals], K6[15][6], G6[15][6], vec[15], sol[15], IG[15][15];
   int fin;
 };
@@ -28,15 +29,18 @@ struct IekfLds {
 // (row-major nb x kIekfVals; nb < 0: `partials` is the final 34 sums). Whole
 // workgroup (>= 256 threads), uniform.
 // ordered sum of nb block partials (row-major nb x kIekfVals) into L.o: row
-// group g = tid / 17 (rows g, g+15, ...), lane pair 2*(tid % 17); then the 15
-// groups in order (deterministic)
+// group g = tid / 17 (rows g, g+G, ...; G = blockDim / 17 groups, at most
+// kIekfGroups), lane pair 2*(tid % 17); then the G groups in order
+// (deterministic). A 1024-lane update runs 60 groups of ~9 rows each: the
+// dependent chains of L2 / cross-XCD loads are 4x shorter than with 15.
 __device__ __forceinline__ void iekf_reduce_block(int nb, const double* __restrict__ partials, IekfLds& L) {
   const int tid = threadIdx.x;
+  const int G = (int)blockDim.x / 17 < kIekfGroups ? (int)blockDim.x / 17 : kIekfGroups;
   const int g = tid / 17, j2 = 2 * (tid % 17);
-  if (g < 15) {
+  if (g < G) {
     double a0 = 0.0, a1 = 0.0;
-#pragma unroll 8
-    for (int b = g; b < nb; b += 15) {
+#pragma unroll 4
+    for (int b = g; b < nb; b += G) {
       const double2 v = *reinterpret_cast<const double2*>(&partials[(size_t)b * kIekfVals + j2]);
       a0 += v.x;
       a1 += v.y;
@@ -47,7 +51,7 @@ __device__ __forceinline__ void iekf_reduce_block(int nb, const double* __restri
   __syncthreads();
   if (tid < kIekfVals) {
     double s = L.red[0][tid];
-    for (int k = 1; k < 15; k++) s += L.red[k][tid];
+    for (int k = 1; k < G; k++) s += L.red[k][tid];
     L.o[tid] = s;
   }
   __syncthreads();

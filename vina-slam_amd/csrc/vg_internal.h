@@ -195,8 +195,6 @@ struct Work {
   size_t tmp_bytes = 0;
   double* partials = nullptr;  // reduction partials
   int* iekf_cache = nullptr;   // per raw point cached leaf
-  double* iekf_pv = nullptr;   // per raw point, SoA (stride iekf_pv_stride): body-frame point (3) + its covariance (9), from the scan's first IEKF iteration
-  size_t iekf_pv_stride = 0;
   int* pk_leaf = nullptr;      // per raw point leaf read by the profiled IEKF iteration (P_k count)
   int* rc = nullptr;           // device-side level counts (recut / margi, map.hip kRc*)
   uint32_t* cand_bits = nullptr;  // factor candidates of an asynchronous recut, one bit per node id
