@@ -1390,9 +1390,8 @@ __global__ void __launch_bounds__(256) k_rc_visit(int L, int thread_num, const i
     int kids[8], nchild, is_cand, is_sub;
     recut_visit_node(q < nw ? work[q] : -1, mp, m, kids, nchild, is_cand, is_sub);
     const int node = q < nw ? work[q] : -1;
-    int o1 = wave_append(&rc[kRcLvl + L], nchild);
-    int o2 = wave_append(&m.counters[kCntFactors], is_cand);
-    int o3 = wave_append(&rc[kRcSub + L], is_sub);
+    int o1, o2, o3;
+    wave_append3(&rc[kRcLvl + L], nchild, &m.counters[kCntFactors], is_cand, &rc[kRcSub + L], is_sub, o1, o2, o3);
     for (int j = 0; j < nchild; j++) next[o1 + j] = kids[j];
     if (is_cand) {
       cand[o2] = node;
@@ -1612,6 +1611,7 @@ __global__ void __launch_bounds__(64 * kRcPushWaves) k_rc_push(int L, const uint
                                                                const int* __restrict__ rc) {
   __shared__ double E[kRcPushWaves][64][kErec];
   __shared__ int s_slot[kRcPushWaves][64];  // window slot of the event, -1 for point_fix
+  __shared__ double s_pre[kRcPushWaves][32 * 9];  // the child's frame clusters, read ahead
   if (rc[kRcAbort]) return;
   const int nch = rc[kRcCh + L], cbase = rc[kRcChBase + L];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1693,6 +1693,14 @@ __global__ void __launch_bounds__(64 * kRcPushWaves) k_rc_push(int L, const uint
       Clu& lc = m.pcrs[(size_t)child * mp.W + slot];
       return r < 69 ? &lc.P[r - 63] : &lc.v[r - 69];
     };
+    // every slot's frame cluster in one round of independent loads (a slot's
+    // run is contiguous, so each is read once, before this wave writes it):
+    // a cluster switch then costs an LDS read, not a dependent HBM load
+    for (int t = lane; t < mp.W * 9; t += 64) {
+      const Clu& lc = m.pcrs[(size_t)child * mp.W + t / 9];
+      const int q = t % 9;
+      s_pre[wv][t] = q < 6 ? lc.P[q] : lc.v[q - 6];
+    }
     double a0 = r0 < 63 ? *acc_ptr(r0, 0) : 0.0, a1 = 0.0;
     int cur_slot = -1, loc_n = 0, nwin = 0;
     for (int b0 = j0; b0 < j1; b0 += 64) {
@@ -1743,8 +1751,8 @@ __global__ void __launch_bounds__(64 * kRcPushWaves) k_rc_push(int L, const uint
             if (lane == 63) m.pcrs[(size_t)child * mp.W + cur_slot].N += loc_n;
           }
           cur_slot = slot;
-          if (r0 >= 63) a0 = *acc_ptr(r0, cur_slot);
-          if (has1) a1 = *acc_ptr(r1, cur_slot);
+          if (r0 >= 63) a0 = s_pre[wv][cur_slot * 9 + r0 - 63];
+          if (has1) a1 = s_pre[wv][cur_slot * 9 + r1 - 63];
           loc_n = 0;
         }
         const double* Ek = E[wv][k];
@@ -1833,7 +1841,7 @@ static int recut_slow_apply(vg_ctx* ctx, int L, const MP& mp, WinD* dwin, int* n
 // child allocation overflowed (kCntMisc) blocks the whole recut (rc abort code
 // kInsAbort) until map_insert_replay has run
 constexpr int kInsAbort = 100;
-__global__ void k_recut_begin(DevMap m, int* __restrict__ rc, int thread_num) {
+__device__ __forceinline__ void recut_begin_block(DevMap& m, int* __restrict__ rc, int thread_num) {
   const int t = threadIdx.x;
   for (int i = t; i < kRcN; i += blockDim.x) rc[i] = 0;
   __syncthreads();
@@ -1842,6 +1850,15 @@ __global__ void k_recut_begin(DevMap m, int* __restrict__ rc, int thread_num) {
     m.counters[kCntGSlide] = m.counters[kCntSlide];  // all-reduced next in sharded mode
     if (m.counters[kCntMisc] != 0 && g_touched(m) >= thread_num) rc[kRcAbort] = kInsAbort;
   }
+}
+// the recut's head as one launch: the window view (poses from the device
+// state, ring, per-ord counts), then the level counters cleared
+__global__ void k_make_win_recut_begin(DState* __restrict__ st, WinArg wa, const int* __restrict__ wpn,
+                                       WinD* __restrict__ win, int* __restrict__ nper, int* __restrict__ slot_of,
+                                       DevMap m, int* __restrict__ rc, int thread_num) {
+  make_win_block(st, wa, wpn, win, nper, slot_of);
+  __syncthreads();
+  recut_begin_block(m, rc, thread_num);
 }
 
 // Asynchronous factor extraction (tras_opt, octree.cpp:491-516) sized on the
@@ -1971,12 +1988,11 @@ static int map_recut_impl(vg_ctx* ctx, const MP& mp, const WinArg& wa, int threa
   WinD* dwin = (WinD*)ctx->ba.xs;
   int* dn = (int*)((char*)ctx->ba.xs + sizeof(WinD));
   int* dslot = dn + 32;
-  VG_TRY(state_make_win(ctx, wa, dwin, dn, dslot, nullptr));
   int total = 0;
   for (int i = 0; i < wa.win_count; i++) total += wa.nper[i];
   ctx->rc_total = total;
   ctx->rc_thread_num = thread_num;
-  k_recut_begin<<<1, 128, 0, s>>>(m, w.rc, thread_num);
+  k_make_win_recut_begin<<<1, 256, 0, s>>>(ctx->st, wa, ctx->map.wpn, dwin, dn, dslot, m, w.rc, thread_num);
   if (m.shard_world > 1) {
     if (!replay) {  // the global slide count (a replay re-uses it: the insert replay does not change it)
       VG_TRY(shard_allreduce(ctx, m.counters + kCntGSlide, ctx->shard.d_buf + 512, 1, 1));
@@ -2472,8 +2488,8 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   // scan and is published before the margi kernels run
   WinArg wa2 = wa;
   wa2.seq2 = pub_seq2;
-  VG_TRY(state_make_win(ctx, wa2, dwin, dn, dn + 32, gate));
-  if (pub_seq > 0) VG_TRY(state_publish(ctx, wa.win_count, ba_iters_dev(ctx), pub_seq, gate));
+  if (pub_seq > 0) VG_TRY(state_make_win_publish(ctx, wa2, dwin, dn, dn + 32, ba_iters_dev(ctx), pub_seq, gate));
+  else VG_TRY(state_make_win(ctx, wa2, dwin, dn, dn + 32, gate));
   if (ctx->pub_flags & 1) k_local_map<<<64, kBlock, 0, s>>>(dwin, m, ctx->d_cmap, ctx->d_cmap_n, gate);
   VG_HIP(hipStreamWaitEvent(s, ctx->ev_prefix_done, 0));  // map_margi_prefix
   // the rest reads every per-scan value from the device (n_oldest: rc, the

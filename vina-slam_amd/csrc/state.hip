@@ -83,37 +83,11 @@ __global__ void k_set_scan(DState* __restrict__ st, const float* x, const float*
 // transfer on the stream
 __global__ void k_push_state(DState* __restrict__ st, PushArg pa) { push_state_block(st, pa); }
 
-// window view for the map kernels: poses by ord, ring, per-ord counts / slots
+// window view for the map kernels (make_win_block, vg_dev.h)
 __global__ void k_make_win(DState* __restrict__ st, WinArg wa, const int* __restrict__ wpn, WinD* __restrict__ win,
                            int* __restrict__ nper, int* __restrict__ slot_of, const int* __restrict__ gate) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
-  const int t = threadIdx.x;
-  const int wc = wa.win_count;
-  if (wa.set_xc && wc > 0) {
-    if (t < 12) st->xc[t] = st->xs[(wc - 1) * kXS + t];
-    __syncthreads();
-  }
-  for (int e = t; e < kMaxWin * 12; e += blockDim.x) {
-    const int i = e / 12, k = e % 12;
-    const double v = i < wc ? st->xs[i * kXS + k] : 0.0;
-    if (k < 9) win->R[i][k] = v;
-    else win->p[i][k - 9] = v;
-  }
-  if (t < kMaxWin) {
-    win->mp[t] = wa.mp[t];
-    nper[t] = t < wc ? wpn[wa.mp[t]] : 0;  // the inserts' counts (device: no host round trip)
-    slot_of[t] = wa.mp[t];
-  }
-  if (t == 0) {  // the window's point total (the recut's window-event grid reads it)
-    int tot = 0;
-    for (int k = 0; k < wc && k < kMaxWin; k++) tot += wpn[wa.mp[k]];
-    nper[64] = tot;
-  }
-  if (t == 0) {
-    win->win_count = wc;
-    win->pad = 0;
-    st->seq2 = wa.seq2;
-  }
+  make_win_block(st, wa, wpn, win, nper, slot_of);
 }
 
 // slide the window states and the IMU bias records by one
@@ -141,10 +115,9 @@ __global__ void k_slide_state(DState* __restrict__ st, int win_count, int nimu) 
 }
 
 // P1: x_curr, the post-IEKF pose, window states, IEKF / BA summary
-__global__ void k_publish_state(const DState* __restrict__ st, int win_count, int ba_iters_valid,
-                                const int* __restrict__ ba_iters, const int* __restrict__ ba_hess,
-                                Pub* __restrict__ pub, int seq, const int* __restrict__ gate) {
-  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
+__device__ __forceinline__ void publish_state_block(const DState* __restrict__ st, int win_count, int ba_iters_valid,
+                                                    const int* __restrict__ ba_iters, const int* __restrict__ ba_hess,
+                                                    Pub* __restrict__ pub, int seq) {
   const int t = threadIdx.x;
   for (int e = t; e < kXC; e += blockDim.x) pub_store(&pub->xc[e], st->xc[e]);
   for (int e = t; e < 12; e += blockDim.x) pub_store(&pub->traj[e], st->traj[e]);
@@ -159,6 +132,24 @@ __global__ void k_publish_state(const DState* __restrict__ st, int win_count, in
   }
   __syncthreads();
   if (t == 0) pub_flag(&pub->seq1, seq);
+}
+__global__ void k_publish_state(const DState* __restrict__ st, int win_count, int ba_iters_valid,
+                                const int* __restrict__ ba_iters, const int* __restrict__ ba_hess,
+                                Pub* __restrict__ pub, int seq, const int* __restrict__ gate) {
+  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
+  publish_state_block(st, win_count, ba_iters_valid, ba_iters, ba_hess, pub, seq);
+}
+// the margi tail's head as one launch: the window view, then the state (the
+// host's next IMU propagation waits for it) published
+__global__ void k_make_win_publish(DState* __restrict__ st, WinArg wa, const int* __restrict__ wpn,
+                                   WinD* __restrict__ win, int* __restrict__ nper, int* __restrict__ slot_of,
+                                   int ba_iters_valid, const int* __restrict__ ba_iters,
+                                   const int* __restrict__ ba_hess, Pub* __restrict__ pub, int seq,
+                                   const int* __restrict__ gate) {
+  if (gate && !*gate) return;
+  make_win_block(st, wa, wpn, win, nper, slot_of);
+  __syncthreads();  // x_curr (set_xc) and the window states, seen by the whole block
+  publish_state_block(st, wa.win_count, ba_iters_valid, ba_iters, ba_hess, pub, seq);
 }
 
 // P2: map counters at the end of the scan
@@ -370,6 +361,15 @@ int state_slide(vg_ctx* ctx, int win_count, int nimu) {
     return VG_E_ARG;
   }
   k_slide_state<<<1, 256, 0, ctx->stream>>>(ctx->st, win_count, nimu);
+  VG_HIP(hipGetLastError());
+  return VG_OK;
+}
+
+int state_make_win_publish(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot, const int* ba_iters_dev,
+                           int seq, const int* gate) {
+  k_make_win_publish<<<1, 256, 0, ctx->stream>>>(ctx->st, wa, ctx->map.wpn, dwin, dnper, dslot, ba_iters_dev != nullptr,
+                                                 ba_iters_dev, ba_iters_dev ? ba_hess_dev(ctx) : nullptr, ctx->d_pub,
+                                                 seq, gate);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }

@@ -296,6 +296,32 @@ __device__ __forceinline__ int wave_append(int* ctr, int count) {
   return base + x - count;
 }
 
+// three wave appends at once: one scan of the counts packed 21 bits each
+// (every count < 2^21 / 64), the three atomics issued back to back
+__device__ __forceinline__ void wave_append3(int* c0, int n0, int* c1, int n1, int* c2, int n2, int& o0, int& o1,
+                                             int& o2) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long v = (unsigned long long)n0 | ((unsigned long long)n1 << 21) | ((unsigned long long)n2 << 42);
+  unsigned long long x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  const unsigned long long tot = __shfl(x, 63, 64);
+  const int t0 = (int)(tot & 0x1fffff), t1 = (int)((tot >> 21) & 0x1fffff), t2 = (int)(tot >> 42);
+  int b0 = 0, b1 = 0, b2 = 0;
+  if (lane == 63) {
+    if (t0 > 0) b0 = atomicAdd(c0, t0);
+    if (t1 > 0) b1 = atomicAdd(c1, t1);
+    if (t2 > 0) b2 = atomicAdd(c2, t2);
+  }
+  const unsigned long long ex = x - v;
+  o0 = __shfl(b0, 63, 64) + (int)(ex & 0x1fffff);
+  o1 = __shfl(b1, 63, 64) + (int)((ex >> 21) & 0x1fffff);
+  o2 = __shfl(b2, 63, 64) + (int)(ex >> 42);
+}
+
 __device__ __forceinline__ M<9, 9> unpack9(const double* cov) {
   M<9, 9> m;
   int k = 0;
@@ -338,4 +364,36 @@ __device__ __forceinline__ void push_state_block(DState* __restrict__ st, const 
   }
 }
 
+// window view for the map kernels: poses by ord, ring, per-ord counts / slots
+__device__ __forceinline__ void make_win_block(DState* __restrict__ st, const WinArg& wa, const int* __restrict__ wpn,
+                                               WinD* __restrict__ win, int* __restrict__ nper,
+                                               int* __restrict__ slot_of) {
+  const int t = threadIdx.x;
+  const int wc = wa.win_count;
+  if (wa.set_xc && wc > 0) {
+    if (t < 12) st->xc[t] = st->xs[(wc - 1) * kXS + t];
+    __syncthreads();
+  }
+  for (int e = t; e < kMaxWin * 12; e += blockDim.x) {
+    const int i = e / 12, k = e % 12;
+    const double v = i < wc ? st->xs[i * kXS + k] : 0.0;
+    if (k < 9) win->R[i][k] = v;
+    else win->p[i][k - 9] = v;
+  }
+  if (t < kMaxWin) {
+    win->mp[t] = wa.mp[t];
+    nper[t] = t < wc ? wpn[wa.mp[t]] : 0;  // the inserts' counts (device: no host round trip)
+    slot_of[t] = wa.mp[t];
+  }
+  if (t == 0) {  // the window's point total (the recut's window-event grid reads it)
+    int tot = 0;
+    for (int k = 0; k < wc && k < kMaxWin; k++) tot += wpn[wa.mp[k]];
+    nper[64] = tot;
+  }
+  if (t == 0) {
+    win->win_count = wc;
+    win->pad = 0;
+    st->seq2 = wa.seq2;
+  }
+}
 }  // namespace vg

@@ -585,6 +585,8 @@ int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x = nullptr,
 int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n, hipStream_t s = nullptr);
 int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec);  // imurec: kBaImuRec doubles (new_imu >= 0)
 int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot, const int* gate);
+int state_make_win_publish(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot, const int* ba_iters_dev,
+                           int seq, const int* gate);  // the two above in one launch
 int state_slide(vg_ctx* ctx, int win_count, int nimu);
 int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq, const int* gate = nullptr);
 int state_publish_counters(vg_ctx* ctx, int seq);
