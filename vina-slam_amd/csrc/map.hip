@@ -930,15 +930,16 @@ __global__ void __launch_bounds__(256) k_ins_scatter(int n_arg, const int* __res
 // lanes 0-8 own the frame cluster, 9-17 the accumulated cluster, 18-62
 // cov_add (see role_inc)
 constexpr int kPushWaves = 4;
-constexpr int kPwBits = 1 << 15;  // point indices per bitmap window of k_push_window (4 KB of LDS per wave)
+constexpr int kPwBits = 1 << 16;  // point indices per bitmap window of k_push_window (8 KB, inside the wave's E)
 constexpr int kPwWords = kPwBits / 32;
-__global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __restrict__ seg_leaf,
+constexpr int kPwRankMax = 256;  // longest segment ordered by ranking (the bitmap's cost is its index range)
+static_assert(kPwWords * 4 <= 64 * kErec * 8, "the ordering bitmap lives in the wave's record buffer");
+__global__ void __launch_bounds__(64 * kPushWaves, 4) k_push_window(const int* __restrict__ seg_leaf,
                                                                  const int* __restrict__ seg_off,
                                                                  const int* __restrict__ order,
                                                                  int* __restrict__ order2, MP mp, int slot, DevMap m,
                                                                  const double* __restrict__ pw, int thread_num) {
   __shared__ double E[kPushWaves][64][kErec];
-  __shared__ uint32_t s_bm[kPushWaves][kPwWords];
   if (ins_skip(m, thread_num)) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int role = lane < 63 ? lane : -1;
@@ -960,12 +961,22 @@ __global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __re
           const bool up = (lane & k) == 0, low = (lane & j) == 0;
           mine = (low == up) ? min(mine, other) : max(mine, other);
         }
+    } else if (L <= kPwRankMax) {  // a few hundred points: each ranked against the (L1-resident) others
+      for (int e = lane; e < L; e += 64) {
+        const int x = order[j0 + e];
+        int r = 0;
+        for (int t = 0; t < L; t++) r += order[j0 + t] < x ? 1 : 0;
+        order2[j0 + r] = x;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     } else {
       // longer segments: an LDS bitmap over the segment's index range, in
       // windows of kPwBits indices (set bits compacted in order by a wave
       // scan): O(L + range / 32) per leaf instead of ranking every point
       // against every other (O(L^2 / 64) global loads per lane)
-      uint32_t* bm = s_bm[wv];
+      uint32_t* bm = reinterpret_cast<uint32_t*>(&E[wv][0][0]);  // free until the records are filled
       int lo = 0x7fffffff, hi = -1;
       for (int e = lane; e < L; e += 64) {
         const int x = order[j0 + e];
@@ -979,7 +990,8 @@ __global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __re
       }
       int outpos = 0;
       for (int w0 = lo; w0 <= hi; w0 += kPwBits) {
-        for (int k = lane; k < kPwWords; k += 64) bm[k] = 0u;
+        const int nw = min(kPwWords, ((hi - w0) >> 5) + 1);  // the words this window's range covers
+        for (int k = lane; k < nw; k += 64) bm[k] = 0u;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -990,28 +1002,26 @@ __global__ void __launch_bounds__(64 * kPushWaves) k_push_window(const int* __re
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        constexpr int per = kPwWords / 64;  // contiguous words per lane
-        int cnt = 0;
+        // 64 consecutive words per round, one per lane: a lane emits at
+        // most 32 indices per round however the points cluster
+        for (int r = 0; r < nw; r += 64) {
+          const int k = r + lane;
+          uint32_t w = k < nw ? bm[k] : 0u;
+          const int cnt = __popc(w);
+          int ex = cnt;
 #pragma unroll
-        for (int k = 0; k < per; k++) cnt += __popc(bm[lane * per + k]);
-        int ex = cnt;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          const int y = __shfl_up(ex, off, 64);
-          if (lane >= off) ex += y;
-        }
-        const int total = __shfl(ex, 63, 64);
-        int pos = outpos + ex - cnt;
-#pragma unroll
-        for (int k = 0; k < per; k++) {
-          uint32_t w = bm[lane * per + k];
+          for (int off = 1; off < 64; off <<= 1) {
+            const int y = __shfl_up(ex, off, 64);
+            if (lane >= off) ex += y;
+          }
+          int pos = outpos + ex - cnt;
           while (w) {
             const int b = __ffs(w) - 1;
             w &= w - 1;
-            order2[j0 + pos++] = w0 + (lane * per + k) * 32 + b;
+            order2[j0 + pos++] = w0 + k * 32 + b;
           }
+          outpos += __shfl(ex, 63, 64);
         }
-        outpos += total;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");

@@ -479,30 +479,42 @@ static int resolve_ds(vg_ctx* ctx, HostPipe* P) {
 // voxels (local_mapping.cpp:396-403), both decided on the device
 // (ds_enqueue_hashed): the host never waits for the count, the GPU runs the
 // IEKF meanwhile and the insert reads the count where it lands
-int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n,
-                     int* n_ds_out) {
-  HostTimer ht_(ctx, kHostDownsample);
-  HostPipe* P = hp(ctx);
-  VG_TRY(need_open(ctx, P, "vg_downsample_scan"));
-  const vg_config& c = ctx->cfg;
-  P->sx = dx;
-  P->sy = dy;
-  P->sz = dz;
-  P->si = di;
-  P->n_raw = n;
-  P->cur.st.n_raw = n;
-  // own stream: waits only until the previous insert has read the ds buffers
+// the downsample's device work on its own stream, which waits only until the
+// previous insert has read the ds buffers (and for a deskewed scan)
+static int ds_enqueue_scan(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n,
+                           int pub_seq) {
   if (ctx->want_ds_stream && ctx->stream_ds == ctx->stream)
     VG_HIP(hipStreamCreateWithFlags(&ctx->stream_ds, hipStreamNonBlocking));
   VG_HIP(flush_insert_events(ctx));
   VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_ds_free, 0));
   VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_scan_ready, 0));  // a deskewed scan (no-op otherwise)
   prof_begin(ctx, kProfDownsample, ctx->stream_ds);
-  P->ds_seq = n_ds_out ? ++ctx->pub_seq : -1;  // published only for a stage-level caller
-  P->ds_n = -1;
-  VG_TRY(ds_enqueue_hashed(ctx, ctx->stream_ds, dx, dy, dz, di, n, c.down_size, true, n_ds_out ? P->ds_seq : 0));
+  VG_TRY(ds_enqueue_hashed(ctx, ctx->stream_ds, dx, dy, dz, di, n, ctx->cfg.down_size, true, pub_seq));
   prof_end(ctx, kProfDownsample, ctx->stream_ds);
   VG_HIP(hipEventRecord(ctx->ev_ds_done, ctx->stream_ds));
+  return VG_OK;
+}
+
+// the scan's raw cloud as the insert's input; early: its downsample is already
+// enqueued (host_step)
+static void ds_adopt(HostPipe* P, const float* dx, const float* dy, const float* dz, const float* di, int n) {
+  P->sx = dx;
+  P->sy = dy;
+  P->sz = dz;
+  P->si = di;
+  P->n_raw = n;
+  P->cur.st.n_raw = n;
+  P->ds_n = -1;
+}
+
+int stage_downsample(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n,
+                     int* n_ds_out) {
+  HostTimer ht_(ctx, kHostDownsample);
+  HostPipe* P = hp(ctx);
+  VG_TRY(need_open(ctx, P, "vg_downsample_scan"));
+  ds_adopt(P, dx, dy, dz, di, n);
+  P->ds_seq = n_ds_out ? ++ctx->pub_seq : -1;  // published only for a stage-level caller
+  VG_TRY(ds_enqueue_scan(ctx, dx, dy, dz, di, n, n_ds_out ? P->ds_seq : 0));
   if (n_ds_out) {
     VG_TRY(resolve_ds(ctx, P));
     *n_ds_out = P->ds_n;
@@ -909,14 +921,27 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
               double end, const double* imu, int m) {
   const vg_config& c = ctx->cfg;
   if (init_active(hp(ctx))) return init_step(ctx, dx, dy, dz, di, nullptr, n, beg, end, imu, m);
+  // both read only the raw scan (local_mapping.cpp:396-413). The downsample
+  // (its count stays on the device) goes first, on its own stream, before the
+  // host waits for the previous scan's state: it runs under that scan's margi
+  // and this scan's IEKF instead of behind the IEKF's enqueue. The IEKF then
+  // opens the main stream's critical path.
+  HostPipe* P = hp(ctx);
+  const bool early = ctx->ds_early && ctx->want_ds_stream && !P->in_scan && P->sticky == VG_OK && !ctx->prof_stages;
+  if (early) {
+    HostTimer ht_(ctx, kHostDownsample);
+    VG_TRY(ds_enqueue_scan(ctx, dx, dy, dz, di, n, 0));
+  }
   VG_TRY(stage_propagate(ctx, imu, m, beg, end));
   host_delay(0);
-  // both read only the raw scan (local_mapping.cpp:396-413); the IEKF opens
-  // the main stream's critical path, the downsample (its count stays on the
-  // device) runs beside it on its own stream
   VG_TRY(stage_iekf(ctx, dx, dy, dz, n, nullptr));
   host_delay(4);
-  VG_TRY(stage_downsample(ctx, dx, dy, dz, di, n, nullptr));
+  if (early) {
+    ds_adopt(P, dx, dy, dz, di, n);
+    P->ds_seq = -1;
+  } else {
+    VG_TRY(stage_downsample(ctx, dx, dy, dz, di, n, nullptr));
+  }
   VG_TRY(stage_window_push(ctx, imu, m));
   host_delay(3);
   if (mid_graph_ok(ctx, hp(ctx))) {

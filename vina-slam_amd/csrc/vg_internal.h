@@ -337,6 +337,7 @@ struct vg_ctx {
   int pub_flags = 0;         // vg_set_publish: bit 0 = /map_cmap after each window BA (k_local_map)
   float4* d_cmap = nullptr;  // the last /map_cmap cloud (x, y, z, intensity) and its size
   int* d_cmap_n = nullptr;
+  bool ds_early = true;      // a fused step's downsample enqueued before the host waits for the previous state (host_step)
   bool spec_tail = true;     // the margi tail behind the predicted LM iterations (stage_ba)
   std::string err;
   vg::Arena arena;

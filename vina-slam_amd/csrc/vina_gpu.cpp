@@ -776,6 +776,10 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     ctx->overlap_iekf = value != 0;
     return VG_OK;
   }
+  if (key == 9) {  // 0: a fused step enqueues its downsample after the IEKF, not before the state wait
+    ctx->ds_early = value != 0;
+    return VG_OK;
+  }
   if (key == 8) {  // 0: the margi tail is enqueued only after the LM is seen done
     ctx->spec_tail = value != 0;
     return VG_OK;
