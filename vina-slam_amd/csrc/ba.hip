@@ -889,7 +889,7 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
 // them onto pcr_fix in frame order (the reference's order) and takes the 3x3
 // eigen-decomposition. Workgroup b < nrb takes chunks b, b + nrb, ... of the
 // device factor count *nfp; its residual partial goes to rpart[b].
-__global__ void __launch_bounds__(256) k_ba_resid(const int* __restrict__ nfp, int W, const int* __restrict__ fac_node,
+__global__ void __launch_bounds__(256, 2) k_ba_resid(const int* __restrict__ nfp, int W, const int* __restrict__ fac_node,
                                                   const Clu* __restrict__ pcr_fix, const Clu* __restrict__ pcrs,
                                                   const int* __restrict__ mpring, const double* __restrict__ xt,
                                                   double* __restrict__ fac_eig, Clu* __restrict__ fac_pcr,

@@ -1576,10 +1576,19 @@ __global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int sub_cap, 
     return;
   }
   int myp = tid < nsub ? sub[tid] : 0x7fffffff;
-  {
+  {  // rank among the level's leaves, read from LDS (ids are distinct)
+    __shared__ __attribute__((aligned(16))) int s_in[kApplySub];
+    s_in[tid] = myp;
+    __syncthreads();
     int rank = 0;
-    if (tid < nsub)
-      for (int q = 0; q < nsub; q++) rank += sub[q] < myp ? 1 : 0;
+    if (tid < nsub) {
+      const int4* v4 = reinterpret_cast<const int4*>(s_in);
+      for (int q = 0; q < (nsub + 3) / 4; q++) {
+        const int4 v = v4[q];
+        rank += (v.x < myp) + (v.y < myp) + (v.z < myp) + (v.w < myp);
+      }
+    }
+    __syncthreads();
     if (tid < nsub) s_sub[rank] = myp;
   }
   __syncthreads();

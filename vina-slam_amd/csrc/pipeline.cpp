@@ -663,11 +663,14 @@ static int stage_insert_recut(vg_ctx* ctx) {
   VG_HIP(hipGraphLaunch(ge, ctx->stream));
   prof_end(ctx, kProfInsert);
   // ev_ds_free (the insert has read the ds buffers) and ev_recut_done (the
-  // margi prefix starts from here), recorded right behind the graph: the next
-  // scan's downsample waits on ev_ds_free, and a record deferred to that
-  // point would make it wait for this scan's whole LM and margi as well
+  // margi prefix starts from here): recorded by their first waiter's flush,
+  // the LM's right behind k_ba_init (a record right behind the graph leaves
+  // the stream idle before k_ba_init). With the early downsample the next
+  // scan's downsample is enqueued after this LM anyway; without it the
+  // records stay right behind the graph, so that downsample does not wait
+  // for k_ba_init.
   ctx->ins_ev_pending = true;
-  VG_HIP(flush_insert_events(ctx));
+  if (!ctx->ds_early) VG_HIP(flush_insert_events(ctx));
   P->wp_n[slot] = P->n_raw;  // an upper bound until the scan's counters are absorbed (absorb_p2)
   P->ins_slot = slot;
   P->cur.ins_slot = slot;
