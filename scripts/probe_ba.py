@@ -81,11 +81,10 @@ def iekf(nscan=40, lidar="64line"):
     print("k_iekf block 0, thread 0:", buf[59], "launches")
     for k, name in {30: "point loop", 31: "block reduction"}.items():
         print("  %-16s %8.2f us/launch" % (name, buf[k] * 0.01 / ni))
-    nb = max(buf[44], 1)
-    print("k_margi_leaf, thread 0 of each block: %d block runs, %.2f leaves each" % (buf[44], buf[42] / nb))
-    print("  %-16s %8.2f us/block" % ("add_ (merge/eig)", buf[40] * 0.01 / nb))
-    print("  %-16s %8.2f us/block" % ("plane_update", buf[41] * 0.01 / nb))
-    print("  %-16s %8.2f us/block" % ("total", buf[43] * 0.01 / nb))
+    nb = max(buf[47], 1)
+    print("k_margi_leaf: %d working blocks, leaves (max) %d" % (buf[47], buf[50]))
+    print("  %-16s %8.2f us" % ("mean block span", buf[46] * 0.01 / nb))
+    print("  %-16s %8.2f us" % ("max block span", buf[45] * 0.01))
 
 
 if __name__ == "__main__":

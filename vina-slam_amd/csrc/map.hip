@@ -2172,90 +2172,124 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
                                                     int* __restrict__ plan, const int* __restrict__ gate) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   const int nl = *nleaves;
+#ifdef VG_PROBE
+  const unsigned long long pt0 = wall_clock64();
+  const bool pwork = (int)(blockIdx.x * blockDim.x) < nl;
+#endif
   int n_pu = 0, n_full = 0;  // plane_update calls / leaves past max_points (per-scan counters)
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nl; q += gridDim.x * blockDim.x) {
-    int node = leaves[q];
-    NodeHdr& h = m.hdr[node];
-    int* pq = &plan[(size_t)q * 8];
-    pq[0] = -1;  // no point_fix copies (k_margi_copy)
-    pq[4] = 0;
-    if (!h.isexist || !h.has_sw) continue;
+  // whole waves per round: the point_fix blocks that grow are carved with one
+  // atomic per wave (wave_append) instead of one per leaf on the shared counter
+  for (int base = blockIdx.x * blockDim.x; base < nl; base += gridDim.x * blockDim.x) {
+    const int q = base + threadIdx.x;
+    const int node = q < nl ? leaves[q] : -1;
+    int* pq = &plan[(size_t)(q < nl ? q : 0) * 8];
+    if (node >= 0) {
+      pq[0] = -1;  // no point_fix copies (k_margi_copy)
+      pq[4] = 0;
+    }
+    const bool live = node >= 0 && m.hdr[node].isexist && m.hdr[node].has_sw;
     const int W = mp.W;
     const int s0 = win->mp[0];
     int seg = -1, segn = 0;  // the leaf's run of the oldest slot: its sw->points[mp[0]] in push order
-    if (!lseg_get(m, node, s0, seg, segn)) seg = -1;
-    Clu* loc = &m.pcrs[(size_t)node * W];
-    const M3 R0 = ld_m3(win->R[0]);
-    const V3 p0 = ld_v3(win->p[0]);
-    Clu w0;
-    clu_zero(w0);
-    if (loc[s0].N != 0) w0 = clu_transform(loc[s0], R0, p0);
-    Clu add_;
-    double* e = &m.eig[(size_t)node * 12];
-    if (h.opt_state >= 0) {
-      add_ = fac_pcr[h.opt_state];
-      for (int j = 0; j < 12; j++) e[j] = fac_eig[(size_t)h.opt_state * 12 + j];
-      h.opt_state = -1;
-    } else {
-      add_ = m.pcr_fix[node];
-      for (int i = 0; i < win->win_count; i++) {
-        int si = win->mp[i];
-        if (loc[si].N != 0) {
-          Clu t = (i == 0) ? w0 : clu_transform(loc[si], ld_m3(win->R[i]), ld_v3(win->p[i]));
-          clu_add(add_, t);
+    Clu w0, add_, fix_;
+    int grow = 0;  // size of a new point_fix block (the live one is full)
+    bool append = false;
+    if (live) {
+      NodeHdr& h = m.hdr[node];
+      if (!lseg_get(m, node, s0, seg, segn)) seg = -1;
+      Clu* loc = &m.pcrs[(size_t)node * W];
+      const M3 R0 = ld_m3(win->R[0]);
+      const V3 p0 = ld_v3(win->p[0]);
+      clu_zero(w0);
+      if (loc[s0].N != 0) w0 = clu_transform(loc[s0], R0, p0);
+      double* e = &m.eig[(size_t)node * 12];
+      if (h.opt_state >= 0) {
+        add_ = fac_pcr[h.opt_state];
+        for (int j = 0; j < 12; j++) e[j] = fac_eig[(size_t)h.opt_state * 12 + j];
+        h.opt_state = -1;
+      } else {
+        add_ = m.pcr_fix[node];
+        for (int i = 0; i < win->win_count; i++) {
+          int si = win->mp[i];
+          if (loc[si].N != 0) {
+            Clu t = (i == 0) ? w0 : clu_transform(loc[si], ld_m3(win->R[i]), ld_v3(win->p[i]));
+            clu_add(add_, t);
+          }
+        }
+        if (h.is_plane) {
+          V3 ev;
+          M3 U;
+          eig3(clu_cov(add_), ev, U);
+          for (int j = 0; j < 3; j++) e[j] = ev[j];
+          for (int j = 0; j < 9; j++) e[3 + j] = U[j];
         }
       }
-      if (h.is_plane) {
-        V3 ev;
-        M3 U;
-        eig3(clu_cov(add_), ev, U);
-        for (int j = 0; j < 3; j++) e[j] = ev[j];
-        for (int j = 0; j < 9; j++) e[3 + j] = U[j];
+      fix_ = m.pcr_fix[node];
+      if (fix_.N < mp.max_points && h.is_plane)
+        if (add_.N - h.last_num >= 5 || h.last_num <= 10) {
+          plane_update_dev(m, node, add_, e);
+          h.last_num = add_.N;
+          n_pu++;
+        }
+      if (fix_.N >= mp.max_points) n_full++;
+      if (fix_.N < mp.max_points) {
+        if (w0.N != 0) {
+          clu_add(fix_, w0);
+          if (seg >= 0 && segn > 0) {
+            append = true;
+            const int need = h.fix_cnt + segn;
+            if (need > h.fix_cap) grow = need * 2 < 128 ? 128 : need * 2;
+          }
+        }
+      } else {
+        if (w0.N != 0) clu_sub(add_, w0);
+        h.fix_cnt = 0;
       }
     }
-    Clu fix_ = m.pcr_fix[node];
-    if (fix_.N < mp.max_points && h.is_plane)
-      if (add_.N - h.last_num >= 5 || h.last_num <= 10) {
-        plane_update_dev(m, node, add_, e);
-        h.last_num = add_.N;
-        n_pu++;
-      }
-    if (fix_.N >= mp.max_points) n_full++;
-    if (fix_.N < mp.max_points) {
-      if (w0.N != 0) {
-        clu_add(fix_, w0);
-        if (seg >= 0 && segn > 0) {
-          int need = h.fix_cnt + segn;
-          if (need > h.fix_cap) {  // grow the point_fix block (old block is abandoned)
-            int cap = need * 2 < 128 ? 128 : need * 2;
-            int off = atomicAdd(&m.counters[kCntFix], cap);
-            if (off + cap > m.cap_fix) {
-              atomicOr(&m.counters[kCntErr], 8);
-              continue;
-            }
+    const int off = wave_append(&m.counters[kCntFix], grow);
+    if (live) {
+      NodeHdr& h = m.hdr[node];
+      bool ok = true;
+      if (append) {
+        if (grow > 0) {  // grow the point_fix block (old block is abandoned)
+          if (off + grow > m.cap_fix) {
+            atomicOr(&m.counters[kCntErr], 8);
+            ok = false;
+          } else {
             pq[0] = h.fix_off;  // grow: move the live block first
             pq[1] = h.fix_cnt;
             pq[2] = off;
             h.fix_off = off;
-            h.fix_cap = cap;
+            h.fix_cap = grow;
           }
+        }
+        if (ok) {
           pq[3] = seg;  // then append the oldest frame's points of this leaf
           pq[4] = segn;
           pq[5] = h.fix_off + h.fix_cnt;
           h.fix_cnt += segn;
         }
       }
-    } else {
-      if (w0.N != 0) clu_sub(add_, w0);
-      h.fix_cnt = 0;
+      if (ok) {
+        clu_zero(m.pcrs[(size_t)node * W + s0]);
+        m.pcr_fix[node] = fix_;
+        m.pcr_add[node] = add_;
+        h.isexist = (fix_.N >= add_.N) ? 0 : 1;
+      }
     }
-    clu_zero(loc[s0]);
-    m.pcr_fix[node] = fix_;
-    m.pcr_add[node] = add_;
-    h.isexist = (fix_.N >= add_.N) ? 0 : 1;
   }
   wave_append(&m.counters[kCntPlaneUpd], n_pu);
   wave_append(&m.counters[kCntFixFull], n_full);
+#ifdef VG_PROBE
+  __syncthreads();
+  if (threadIdx.x == 0 && pwork) {  // per working block: summed span, longest span, count; leaves
+    const unsigned long long pt1 = wall_clock64();
+    atomicAdd(&g_probe[46], pt1 - pt0);
+    atomicMax(&g_probe[45], pt1 - pt0);
+    atomicAdd(&g_probe[47], 1ull);
+    atomicMax(&g_probe[50], (unsigned long long)nl);
+  }
+#endif
 }
 
 // the point_fix copies planned by k_margi_leaf, one wave per leaf: the live
