@@ -2175,19 +2175,31 @@ __device__ void plane_update_dev(DevMap& m, int node, const Clu& pcr_add, const 
 // run of the oldest slot (DevMap::lseg) is its sw->points[mp[0]] list in push
 // order.
 __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nleaves, const int* __restrict__ leaves,
-                                                    MP mp, WinD* __restrict__ win, DevMap m,
+                                                    MP mp, WinArg wa, DState* __restrict__ st, WinD* __restrict__ win,
+                                                    int* __restrict__ nper, int* __restrict__ slot_of, int ba_iters_valid,
+                                                    const int* __restrict__ ba_iters, const int* __restrict__ ba_hess,
+                                                    Pub* __restrict__ pub, int seq, DevMap m,
                                                     const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
                                                     int* __restrict__ plan, const int* __restrict__ gate) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
+  if (blockIdx.x == 0) {  // the margi head: x_curr <- x_buf.back(), the window view, the state publication
+    make_win_block(st, wa, m.wpn, win, nper, slot_of);
+    __syncthreads();  // x_curr (set_xc), seen by the whole block
+    if (seq > 0) publish_state_block(st, wa.win_count, ba_iters_valid, ba_iters, ba_hess, pub, seq);
+    return;
+  }
+  // the leaves read the refined window poses from the state (the view block
+  // above writes the same values into *win for the later margi kernels)
+  const double* xs = st->xs;
   const int nl = *nleaves;
 #ifdef VG_PROBE
   const unsigned long long pt0 = wall_clock64();
-  const bool pwork = (int)(blockIdx.x * blockDim.x) < nl;
+  const bool pwork = (int)((blockIdx.x - 1) * blockDim.x) < nl;
 #endif
   int n_pu = 0, n_full = 0;  // plane_update calls / leaves past max_points (per-scan counters)
   // whole waves per round: the point_fix blocks that grow are carved with one
   // atomic per wave (wave_append) instead of one per leaf on the shared counter
-  for (int base = blockIdx.x * blockDim.x; base < nl; base += gridDim.x * blockDim.x) {
+  for (int base = (blockIdx.x - 1) * blockDim.x; base < nl; base += (gridDim.x - 1) * blockDim.x) {
     const int q = base + threadIdx.x;
     const int node = q < nl ? leaves[q] : -1;
     int* pq = &plan[(size_t)(q < nl ? q : 0) * 8];
@@ -2197,7 +2209,7 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
     }
     const bool live = node >= 0 && m.hdr[node].isexist && m.hdr[node].has_sw;
     const int W = mp.W;
-    const int s0 = win->mp[0];
+    const int s0 = wa.mp[0];
     int seg = -1, segn = 0;  // the leaf's run of the oldest slot: its sw->points[mp[0]] in push order
     Clu w0, add_, fix_;
     int grow = 0;  // size of a new point_fix block (the live one is full)
@@ -2206,8 +2218,8 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
       NodeHdr& h = m.hdr[node];
       if (!lseg_get(m, node, s0, seg, segn)) seg = -1;
       Clu* loc = &m.pcrs[(size_t)node * W];
-      const M3 R0 = ld_m3(win->R[0]);
-      const V3 p0 = ld_v3(win->p[0]);
+      const M3 R0 = ld_m3(xs);
+      const V3 p0 = ld_v3(xs + 9);
       clu_zero(w0);
       if (loc[s0].N != 0) w0 = clu_transform(loc[s0], R0, p0);
       double* e = &m.eig[(size_t)node * 12];
@@ -2217,10 +2229,10 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
         h.opt_state = -1;
       } else {
         add_ = m.pcr_fix[node];
-        for (int i = 0; i < win->win_count; i++) {
-          int si = win->mp[i];
+        for (int i = 0; i < wa.win_count; i++) {
+          int si = wa.mp[i];
           if (loc[si].N != 0) {
-            Clu t = (i == 0) ? w0 : clu_transform(loc[si], ld_m3(win->R[i]), ld_v3(win->p[i]));
+            Clu t = (i == 0) ? w0 : clu_transform(loc[si], ld_m3(xs + (size_t)i * kXS), ld_v3(xs + (size_t)i * kXS + 9));
             clu_add(add_, t);
           }
         }
@@ -2544,14 +2556,11 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
     ctx->err = "win_size too large for the state slide";
     return VG_E_ARG;
   }
-  // x_curr.R/p <- x_buf.back() and the window view (k_make_win also stores
-  // the end-of-scan publication number); then the state is final for this
-  // scan and is published before the margi kernels run
+  // x_curr.R/p <- x_buf.back() and the window view (which also stores the
+  // end-of-scan publication number); the state is then final for this scan
+  // and is published — all by k_margi_leaf's workgroup 0, beside the leaves
   WinArg wa2 = wa;
   wa2.seq2 = pub_seq2;
-  if (pub_seq > 0) VG_TRY(state_make_win_publish(ctx, wa2, dwin, dn, dn + 32, ba_iters_dev(ctx), pub_seq, gate));
-  else VG_TRY(state_make_win(ctx, wa2, dwin, dn, dn + 32, gate));
-  if (ctx->pub_flags & 1) k_local_map<<<64, kBlock, 0, s>>>(dwin, m, ctx->d_cmap, ctx->d_cmap_n, gate);
   VG_HIP(hipStreamWaitEvent(s, ctx->ev_prefix_done, 0));  // map_margi_prefix
   // the rest reads every per-scan value from the device (n_oldest: rc, the
   // publication number: the state), so it is captured once and replayed
@@ -2562,9 +2571,14 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   // counter publication; nothing the IEKF reads) runs under the next IEKF
   // one lane per leaf (eigen-decomposition + plane_update in series on the lane):
   // enough blocks that no lane takes two leaves, surplus blocks exit at once
-  k_margi_leaf<<<512 * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(m.counters + kCntLeaves, w.list0, mp, dwin, m, ctx->ba.fac_eig,
-                                      ctx->ba.fac_pcr, w.plan, gate);
+  // workgroup 0 is the margi head (the window view and the state publication,
+  // k_make_win_publish's work) running beside the leaves
+  const int* bi = pub_seq > 0 ? ba_iters_dev(ctx) : nullptr;
+  k_margi_leaf<<<1 + 512 * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(
+      m.counters + kCntLeaves, w.list0, mp, wa2, ctx->st, dwin, dn, dn + 32, bi != nullptr, bi,
+      bi ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, pub_seq, m, ctx->ba.fac_eig, ctx->ba.fac_pcr, w.plan, gate);
   VG_HIP(hipEventRecord(ctx->ev_tail_a, s));
+  if (ctx->pub_flags & 1) k_local_map<<<64, kBlock, 0, s>>>(dwin, m, ctx->d_cmap, ctx->d_cmap_n, gate);
   ctx->tail_a_valid = true;
   auto body = [&]() -> int {
     k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, dwin, m, gate);

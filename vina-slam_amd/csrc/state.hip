@@ -13,9 +13,10 @@
 //                    cov = (I-G) cov and the degeneracy test (odometry.cpp:192-254)
 //   k_push_state     x_buf.push_back(x_curr) and a fresh IMU_PRE bias record
 //                    (local_mapping.cpp:434-441)
-//   k_make_win       the window view (poses by ord, mp ring, point counts) the
-//                    map kernels read; optionally x_curr.R/p <- x_buf.back()
-//                    first (local_mapping.cpp:501-502)
+//   make_win_block   (vg_dev.h) the window view (poses by ord, mp ring, point
+//                    counts) the map kernels read; optionally x_curr.R/p <-
+//                    x_buf.back() first (local_mapping.cpp:501-502): run by
+//                    k_make_win_recut_begin and by k_margi_leaf's workgroup 0
 //   k_slide_state    x_buf / imu_pre_buf slide by one (local_mapping.cpp:536-546)
 //   k_publish_*      copies to the host-mapped Pub block, closed by a sequence
 //                    flag (system-scope release), so the host reads results
@@ -29,17 +30,6 @@ namespace vg {
 struct XcArg {
   double x[kXC];
 };
-
-__device__ __forceinline__ void pub_store(double* dst, double v) {
-  __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void pub_store(int* dst, int v) {
-  __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void pub_flag(int* dst, int v) {
-  __threadfence_system();
-  __hip_atomic_store(dst, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 // x_curr after propagation; x_prop; cov_inv; IEKF flags; the scan the IEKF
 // reads (set_scan: one launch for both)
@@ -83,12 +73,6 @@ __global__ void k_set_scan(DState* __restrict__ st, const float* x, const float*
 // transfer on the stream
 __global__ void k_push_state(DState* __restrict__ st, PushArg pa) { push_state_block(st, pa); }
 
-// window view for the map kernels (make_win_block, vg_dev.h)
-__global__ void k_make_win(DState* __restrict__ st, WinArg wa, const int* __restrict__ wpn, WinD* __restrict__ win,
-                           int* __restrict__ nper, int* __restrict__ slot_of, const int* __restrict__ gate) {
-  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
-  make_win_block(st, wa, wpn, win, nper, slot_of);
-}
 
 // slide the window states and the IMU bias records by one
 __global__ void k_slide_state(DState* __restrict__ st, int win_count, int nimu) {
@@ -114,42 +98,11 @@ __global__ void k_slide_state(DState* __restrict__ st, int win_count, int nimu) 
   if (t == 0) st->imu_head = (st->imu_head + 1) % kMaxWin;
 }
 
-// P1: x_curr, the post-IEKF pose, window states, IEKF / BA summary
-__device__ __forceinline__ void publish_state_block(const DState* __restrict__ st, int win_count, int ba_iters_valid,
-                                                    const int* __restrict__ ba_iters, const int* __restrict__ ba_hess,
-                                                    Pub* __restrict__ pub, int seq) {
-  const int t = threadIdx.x;
-  for (int e = t; e < kXC; e += blockDim.x) pub_store(&pub->xc[e], st->xc[e]);
-  for (int e = t; e < 12; e += blockDim.x) pub_store(&pub->traj[e], st->traj[e]);
-  for (int e = t; e < 6; e += blockDim.x) pub_store(&pub->nnt[e], st->nnt[e]);
-  for (int e = t; e < win_count * kXS; e += blockDim.x) pub_store(&pub->xs[e], st->xs[e]);
-  if (t == 0) {
-    pub_store(&pub->iekf_iters, st->iters);
-    for (int k = 0; k < 4; k++) pub_store(&pub->matches[k], st->matches[k]);
-    pub_store(&pub->ba_iters1, ba_iters_valid ? *ba_iters : 0);
-    pub_store(&pub->ba_hess1, ba_iters_valid ? *ba_hess : 0);
-    for (int k = 0; k < 4; k++) pub_store(&pub->planes[k], st->planes[k]);
-  }
-  __syncthreads();
-  if (t == 0) pub_flag(&pub->seq1, seq);
-}
 __global__ void k_publish_state(const DState* __restrict__ st, int win_count, int ba_iters_valid,
                                 const int* __restrict__ ba_iters, const int* __restrict__ ba_hess,
                                 Pub* __restrict__ pub, int seq, const int* __restrict__ gate) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   publish_state_block(st, win_count, ba_iters_valid, ba_iters, ba_hess, pub, seq);
-}
-// the margi tail's head as one launch: the window view, then the state (the
-// host's next IMU propagation waits for it) published
-__global__ void k_make_win_publish(DState* __restrict__ st, WinArg wa, const int* __restrict__ wpn,
-                                   WinD* __restrict__ win, int* __restrict__ nper, int* __restrict__ slot_of,
-                                   int ba_iters_valid, const int* __restrict__ ba_iters,
-                                   const int* __restrict__ ba_hess, Pub* __restrict__ pub, int seq,
-                                   const int* __restrict__ gate) {
-  if (gate && !*gate) return;
-  make_win_block(st, wa, wpn, win, nper, slot_of);
-  __syncthreads();  // x_curr (set_xc) and the window states, seen by the whole block
-  publish_state_block(st, wa.win_count, ba_iters_valid, ba_iters, ba_hess, pub, seq);
 }
 
 // P2: map counters at the end of the scan
@@ -349,11 +302,6 @@ int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec) {
   return VG_OK;
 }
 
-int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot, const int* gate) {
-  k_make_win<<<1, 256, 0, ctx->stream>>>(ctx->st, wa, ctx->map.wpn, dwin, dnper, dslot, gate);
-  VG_HIP(hipGetLastError());
-  return VG_OK;
-}
 
 int state_slide(vg_ctx* ctx, int win_count, int nimu) {
   if (win_count * kXS > 4 * 256 || nimu * 12 > 2 * 256) {
@@ -365,14 +313,6 @@ int state_slide(vg_ctx* ctx, int win_count, int nimu) {
   return VG_OK;
 }
 
-int state_make_win_publish(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot, const int* ba_iters_dev,
-                           int seq, const int* gate) {
-  k_make_win_publish<<<1, 256, 0, ctx->stream>>>(ctx->st, wa, ctx->map.wpn, dwin, dnper, dslot, ba_iters_dev != nullptr,
-                                                 ba_iters_dev, ba_iters_dev ? ba_hess_dev(ctx) : nullptr, ctx->d_pub,
-                                                 seq, gate);
-  VG_HIP(hipGetLastError());
-  return VG_OK;
-}
 
 int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq, const int* gate) {
   k_publish_state<<<1, 256, 0, ctx->stream>>>(ctx->st, win_count, ba_iters_dev != nullptr, ba_iters_dev,

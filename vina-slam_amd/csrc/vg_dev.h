@@ -364,6 +364,37 @@ __device__ __forceinline__ void push_state_block(DState* __restrict__ st, const 
   }
 }
 
+// host-mapped publication stores (system scope; the flag last)
+__device__ __forceinline__ void pub_store(double* dst, double v) {
+  __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void pub_store(int* dst, int v) {
+  __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void pub_flag(int* dst, int v) {
+  __threadfence_system();
+  __hip_atomic_store(dst, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// P1: x_curr, the post-IEKF pose, window states, IEKF / BA summary
+__device__ __forceinline__ void publish_state_block(const DState* __restrict__ st, int win_count, int ba_iters_valid,
+                                                    const int* __restrict__ ba_iters, const int* __restrict__ ba_hess,
+                                                    Pub* __restrict__ pub, int seq) {
+  const int t = threadIdx.x;
+  for (int e = t; e < kXC; e += blockDim.x) pub_store(&pub->xc[e], st->xc[e]);
+  for (int e = t; e < 12; e += blockDim.x) pub_store(&pub->traj[e], st->traj[e]);
+  for (int e = t; e < 6; e += blockDim.x) pub_store(&pub->nnt[e], st->nnt[e]);
+  for (int e = t; e < win_count * kXS; e += blockDim.x) pub_store(&pub->xs[e], st->xs[e]);
+  if (t == 0) {
+    pub_store(&pub->iekf_iters, st->iters);
+    for (int k = 0; k < 4; k++) pub_store(&pub->matches[k], st->matches[k]);
+    pub_store(&pub->ba_iters1, ba_iters_valid ? *ba_iters : 0);
+    pub_store(&pub->ba_hess1, ba_iters_valid ? *ba_hess : 0);
+    for (int k = 0; k < 4; k++) pub_store(&pub->planes[k], st->planes[k]);
+  }
+  __syncthreads();
+  if (t == 0) pub_flag(&pub->seq1, seq);
+}
 // window view for the map kernels: poses by ord, ring, per-ord counts / slots
 __device__ __forceinline__ void make_win_block(DState* __restrict__ st, const WinArg& wa, const int* __restrict__ wpn,
                                                WinD* __restrict__ win, int* __restrict__ nper,

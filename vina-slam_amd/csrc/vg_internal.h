@@ -585,10 +585,6 @@ int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x = nullptr,
                      const float* z = nullptr, int n = 0, hipStream_t s = nullptr);
 int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n, hipStream_t s = nullptr);
 int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec);  // imurec: kBaImuRec doubles (new_imu >= 0)
-int state_make_win(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot, const int* gate);
-int state_make_win_publish(vg_ctx* ctx, const WinArg& wa, WinD* dwin, int* dnper, int* dslot, const int* ba_iters_dev,
-                           int seq, const int* gate);  // the two above in one launch
-int state_slide(vg_ctx* ctx, int win_count, int nimu);
 int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq, const int* gate = nullptr);
 int state_publish_counters(vg_ctx* ctx, int seq);
 int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq, int* flags, bool reset);
