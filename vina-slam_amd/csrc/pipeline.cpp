@@ -486,7 +486,7 @@ static int ds_enqueue_scan(vg_ctx* ctx, const float* dx, const float* dy, const 
   if (ctx->want_ds_stream && ctx->stream_ds == ctx->stream)
     VG_HIP(hipStreamCreateWithFlags(&ctx->stream_ds, hipStreamNonBlocking));
   VG_HIP(flush_insert_events(ctx));
-  VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_ds_free, 0));
+  VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ds_free_ev ? ctx->ds_free_ev : ctx->ev_ds_free, 0));
   VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_scan_ready, 0));  // a deskewed scan (no-op otherwise)
   prof_begin(ctx, kProfDownsample, ctx->stream_ds);
   VG_TRY(ds_enqueue_hashed(ctx, ctx->stream_ds, dx, dy, dz, di, n, ctx->cfg.down_size, true, pub_seq));
@@ -598,6 +598,7 @@ int stage_insert(vg_ctx* ctx) {
                     ctx->ds.hflags + 1));
   prof_end(ctx, kProfInsert);
   VG_HIP(hipEventRecord(ctx->ev_ds_free, ctx->stream));  // the insert has read the ds buffers
+  ctx->ds_free_ev = ctx->ev_ds_free;
   P->wp_n[slot] = P->n_raw;  // an upper bound until the scan's counters are absorbed (absorb_p2)
   P->ins_slot = slot;
   P->cur.ins_slot = slot;

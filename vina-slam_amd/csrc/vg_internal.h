@@ -309,6 +309,7 @@ struct vg_ctx {
   // contexts never hold a second hardware queue (vg_multi_create)
   bool want_ds_stream = true;
   hipEvent_t ev_ds_done = nullptr, ev_ds_free = nullptr;
+  hipEvent_t ds_free_ev = nullptr;  // what the next downsample waits for: ev_ds_free, or ev_recut_done when one record marks both
   hipEvent_t ev_recut_done = nullptr, ev_prefix_done = nullptr;  // margi prefix on the second stream
   // The next scan's IEKF overlaps the margi's map-only remainder: it runs on
   // stream_iekf behind ev_tail_a (recorded after k_margi_leaf's plane updates,
@@ -542,9 +543,8 @@ int map_alloc(vg_ctx* ctx);
 inline hipError_t flush_insert_events(vg_ctx* ctx) {
   if (!ctx->ins_ev_pending) return hipSuccess;
   ctx->ins_ev_pending = false;
-  hipError_t e = hipEventRecord(ctx->ev_ds_free, ctx->stream);
-  if (e == hipSuccess) e = hipEventRecord(ctx->ev_recut_done, ctx->stream);
-  return e;
+  ctx->ds_free_ev = ctx->ev_recut_done;  // one record marks both (each record is a gap in the stream)
+  return hipEventRecord(ctx->ev_recut_done, ctx->stream);
 }
 int map_reset(vg_ctx* ctx);
 int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
