@@ -154,12 +154,14 @@ def main():
             tgt_scans[cfg] = gen_scans("128line", args.seq, gg, warmup + args.target_steps + TARGET_STAGE,
                                        workers)
 
-    multi, multi_1m = None, None
+    multi, multi_1m, scans_1m = None, None, None
     if world == 1 and args.multi:
         multi = multi_children(args, args.lidar, args.multi, warmup, args.steps, workers,
                                first=host_scans[:total])
     if world == 1 and args.multi_1m:
-        multi_1m = multi_children(args, "1M", args.multi_1m, warmup, args.multi_1m_steps, workers)
+        keep = []  # sequence 0 of the leg, plus TARGET_STAGE scans: its single-context roofline (workload_roofline)
+        multi_1m = multi_children(args, "1M", args.multi_1m, warmup, args.multi_1m_steps, workers, keep=keep)
+        scans_1m = keep[0] if keep else None
 
     import torch
     import torch.distributed as dist
@@ -203,7 +205,9 @@ def main():
         run(k)
     # k_ba_solve launch events on every 4th scan's LM run: each event record
     # leaves a few-us gap in the stream
-    ctx.profile(True, every=4)
+    # host stage timers + the in-kernel clocks of k_iekf / k_ba_solve (no
+    # events in the stream: every graph replays as it does untimed)
+    ctx.profile(True, clock=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -247,32 +251,43 @@ def main():
     # ---- headline roofline: the whole scan against HBM -------
     roof = scan_roofline(stats, stage_stats, W, dt / args.steps)
     # ---- per-kernel rooflines ----------------------------------------------
+    # Kernel-only launch times from the in-kernel clocks (vg_profile bit 2:
+    # the device's constant-rate wall clock read inside the kernel, executed
+    # launches of the timed region, graph replays as untimed; rocprofv3's
+    # kernel average of the same command is the cross-check, profiles/).
     # k_ba_solve (the LM step's 15W x 15W LDL^T, one workgroup, fp64 MFMA
     # trailing updates): algorithmic flops per launch = n^3/3 + 2 n^2 with
-    # n = 15 W - 15 (the gauge frame is not factored) over its HIP-event launch
-    # time on the context stream in the timed region
+    # n = 15 W - 15 (the gauge frame is not factored)
     n_sys = 15 * W - 15
     flops = n_sys ** 3 / 3.0 + 2.0 * n_sys ** 2
-    sol = prof["ba_solve"]
+    sol = prof["k_ba_solve_clock"]
     s_avg = sol["ms"] * 1e-3 / max(sol["launches"], 1)
     s_ach = flops / s_avg / 1e12 if s_avg > 0 else 0.0
     roof_solve = {"kernel": "k_ba_solve", "bound": "mfma", "achieved": round(s_ach, 5), "peak": FP64_MFMA_TFLOPS,
                   "unit": "TFLOP/s", "frac": round(s_ach / FP64_MFMA_TFLOPS, 7), "traffic": None,
-                  "avg_launch_us": round(s_avg * 1e6, 3), "launches": sol["launches"], "flops_per_launch": int(flops)}
+                  "avg_launch_us": round(s_avg * 1e6, 3), "launches": sol["launches"], "flops_per_launch": int(flops),
+                  "timing": "in-kernel clock (wall_clock64), executed launches of the timed region"}
     # k_iekf (hot loop #1, HBM-bound gather): 16 B per raw point (fp32 xyz +
-    # cached leaf) + PLANE_B per distinct plane record (P_k) per launch; in the
-    # timed region the IEKF replays as one hipGraph, so its per-launch events
-    # come from the per-stage pass (direct launches, same sequence)
-    iek = stage_prof.get("iekf", {"ms": 0.0, "launches": 0})
+    # cached leaf) + PLANE_B per distinct plane record (P_k) per launch. The
+    # timed scans' own point counts and iteration counts; P_k (distinct plane
+    # records per executed iteration) from the per-stage pass, as its mean
+    iek = prof["k_iekf_clock"]
     n_launch = iek["launches"]
-    bytes_tot = sum(s["iekf_iters"] * 16.0 * s["n_raw"] + PLANE_B * sum(s["iekf_planes"][: s["iekf_iters"]])
-                    for s in stage_stats)
+    it_n = sum(s["iekf_iters"] for s in stage_stats)
+    p_mean = sum(sum(s["iekf_planes"][: s["iekf_iters"]]) for s in stage_stats) / it_n if it_n else 0.0
+    it_t = sum(s["iekf_iters"] for s in stats)
+    bytes_tot = sum(s["iekf_iters"] * 16.0 * s["n_raw"] for s in stats) + PLANE_B * p_mean * it_t
     avg_s = iek["ms"] * 1e-3 / max(n_launch, 1)
-    achieved = (bytes_tot / max(n_launch, 1)) / avg_s / 1e9 if avg_s > 0 else 0.0
+    bpl = bytes_tot / max(it_t, 1)
+    achieved = bpl / avg_s / 1e9 if avg_s > 0 else 0.0
+    ev = stage_prof.get("iekf", {"ms": 0.0, "launches": 0})
     roof_iekf = {"kernel": "k_iekf", "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                  "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
-                 "avg_launch_us": round(avg_s * 1e6, 3), "launches": n_launch,
-                 "bytes_per_launch": int(bytes_tot / max(n_launch, 1))}
+                 "avg_launch_us": round(avg_s * 1e6, 3), "launches": n_launch, "iterations_executed": it_t,
+                 "bytes_per_launch": int(bpl), "P_k_mean": round(p_mean, 1),
+                 "timing": "in-kernel clock (wall_clock64: first workgroup start -> last workgroup end), executed "
+                           "launches of the timed region",
+                 "event_interval_us": round(ev["ms"] * 1e3 / ev["launches"], 3) if ev["launches"] else None}
     pmc = pmc_traffic()
     for r in (roof_solve, roof_iekf):
         if r["kernel"] in pmc:
@@ -299,6 +314,16 @@ def main():
     for cfg, sc in tgt_scans.items():
         beat("128-line target workload (%s)" % cfg)
         targets[cfg] = target_workload(args, cfg, sc, warmup, dev)
+    if multi_1m and scans_1m:
+        beat("1M workload: single-context roofline")
+        w1 = target_workload(args, args.config, scans_1m, warmup, dev, lidar="1M")
+        multi_1m["bytes_per_scan"] = w1["bytes_per_scan"]
+        multi_1m["counters_mean"] = w1["counters_mean"]
+        multi_1m["single_context"] = {k: w1[k] for k in ("value", "ms_per_step", "steps", "achieved", "frac")}
+        multi_1m["roofline_frac_by_B"] = {B: round(v * w1["bytes_per_scan"] / (HBM_PEAK_GBPS * 1e9), 6)
+                                          for B, v in multi_1m["by_B"].items()}
+        multi_1m["roofline_note"] = ("SURVEY 8(d) algorithmic bytes per 1M-ray scan (sequence 0 of the leg, one "
+                                     "context, its own counters) x by_B / 8 TB/s")
 
     if rank == 0:
         line = {
@@ -363,7 +388,7 @@ def multi_roofline(multi, roof):
     return multi
 
 
-def multi_children(args, lidar, Bs, warmup, steps, workers, first=None):
+def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=None):
     """A multi-sequence leg (vg_multi_*), one child process per B, started
     before this process initialises the GPU: HIP keeps every hardware queue a
     process has created, and once a process holds more queues than the
@@ -391,7 +416,10 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None):
     try:
         for b in range(max(Bs)):
             beat("multi-sequence %s: generating sequence %d of %d" % (lidar, b + 1, max(Bs)))
-            sc = first if (b == 0 and first is not None) else gen_scans(lidar, args.seq + b, g, total, workers)
+            sc = first if (b == 0 and first is not None) else gen_scans(
+                lidar, args.seq + b, g, total + (TARGET_STAGE if b == 0 and keep is not None else 0), workers)
+            if b == 0 and keep is not None:
+                keep.append(sc)
             fd, path = tempfile.mkstemp(suffix=".npz", prefix="vg_multi_")
             os.close(fd)
             arrs = {}
@@ -545,7 +573,7 @@ def host_input_rate(p, seq, host_scans, imus, warmup, steps, dev):
 TARGET_STAGE = 4  # per-stage scans after the target workload's timed ones (P_k for its roofline)
 
 
-def target_workload(args, cfg, host, warm, dev):
+def target_workload(args, cfg, host, warm, dev, lidar="128line"):
     """The north star's target workload (synthetic 128-line clouds, 200,064
     rays) on one GPU, same pipeline and protocol as the metric, fewer scans:
     reported beside the metric, never as `value`. Its whole-scan roofline uses
@@ -559,7 +587,7 @@ def target_workload(args, cfg, host, warm, dev):
     p = vgconfig.load(cfg)
     g = p["General"]
     W = p["LocalBA"]["win_size"]
-    seq = synth.Sequence("128line", args.seq, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
+    seq = synth.Sequence(lidar, args.seq, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
     steps = len(host) - warm - TARGET_STAGE
     scans = []
     for xyz, inten, b, e, _ in host:
@@ -589,8 +617,9 @@ def target_workload(args, cfg, host, warm, dev):
     ctx.profile(False)
     ctx.close()
     roof = scan_roofline(st, stage_st, W, dt / steps)
-    return {"workload": "synthetic-128line@%s.yaml" % cfg, "value": round(steps / dt, 3), "unit": "scans/s",
-            "ms_per_step": round(dt * 1e3 / steps, 4), "steps": steps, "warmup": warm, "rays_per_scan": 200064,
+    return {"workload": "synthetic-%s@%s.yaml" % (lidar, cfg), "value": round(steps / dt, 3), "unit": "scans/s",
+            "ms_per_step": round(dt * 1e3 / steps, 4), "steps": steps, "warmup": warm,
+            "rays_per_scan": int(synth.LIDARS[lidar][0] * synth.LIDARS[lidar][1]),
             "points_per_scan": int(np.mean([s[1] for s in scans[warm:warm + steps]])),
             "downsampled_per_scan": int(np.mean([x["n_ds"] for x in st])) if st else None,
             "factors_per_scan": int(np.mean([x["n_factors"] for x in st])) if st else None,

@@ -327,7 +327,11 @@ int vg_shard_host(vg_ctx* ctx, int rank, int world, vg_host_allreduce_fn fn, voi
  * (k_ba_solve); 8..15 the HOST time of the stage calls (enqueue + waits):
  * propagate, downsample, IEKF, window push, insert, recut, BA, margi. `on`: 0 off, 1 the k_iekf and k_ba_solve launches only
  * (stages 1 and 7; cheap enough for a timed region), 3 every stage; bits 8-15
- * (n > 1) time k_ba_solve on every n-th BA run only.
+ * (n > 1) time k_ba_solve on every n-th BA run only; bit 2 (4): in-kernel
+ * clocks of k_iekf and k_ba_solve (the device's constant-rate wall clock read
+ * inside the kernels: kernel-only time of the executed launches, graph replays
+ * included, no events in the stream), read as stages 16 (k_iekf) and 17
+ * (k_ba_solve).
  * vg_profile resets the accumulators; vg_profile_read returns total ms and the
  * number of intervals. */
 int vg_profile(vg_ctx* ctx, int on);

@@ -123,7 +123,7 @@ def test_hashed_downsample_bit_exact(ctx, oracle_lib, case):
 
 
 @pytest.mark.parametrize("case,size,halves", [("scan", 0.1, False), ("dense", 1.0, True), ("giant", 0.5, True),
-                                              ("clusters", 0.5, True)])
+                                              ("clusters", 0.5, True), ("1m", 2.0, True)])
 def test_fallback_pass_matches_oracle(oracle_lib, case, size, halves):
     """down_sampling_voxel's /2 fallback below 2000 voxels (local_mapping.cpp:
     399-403) on the device: one workgroup redoes the pass at size / 2 when the
@@ -133,9 +133,11 @@ def test_fallback_pass_matches_oracle(oracle_lib, case, size, halves):
     import vgpu
     rng = np.random.default_rng(9)
     p = vgconfig.load("mid360")
-    ctx = vgpu.Context(vgconfig.to_c(p), max_points=400_000, max_nodes=100_000, max_fix_points=100_000,
-                       hash_log2=16)
-    if case == "scan":
+    ctx = vgpu.Context(vgconfig.to_c(p), max_points=1_100_000 if case == "1m" else 400_000, max_nodes=100_000,
+                       max_fix_points=100_000, hash_log2=16)
+    if case == "1m":  # a 1M-ray scan at 2 m: ~400 voxels, then ~1.5 k dense ones at 1 m (k_hds_big behind the pass)
+        xyz, inten, _, _ = synth.Sequence("1M", seq_id=2, blind=3.0).scan(4)
+    elif case == "scan":
         g_ = p["General"]
         seq = synth.Sequence("64line", 1, blind=g_["blind"], ext_R=g_["extrinsic_rota"], ext_t=g_["extrinsic_tran"])
         xyz, inten, _, _ = seq.scan(3)

@@ -604,8 +604,9 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
                                                   const double* __restrict__ jvec, const int* __restrict__ ipg,
                                                   const double* __restrict__ xs, double* __restrict__ xt,
                                                   double* __restrict__ bias, double* __restrict__ dxi_out,
-                                                  BaState* __restrict__ st) {
+                                                  BaState* __restrict__ st, KClock* __restrict__ clk) {
   if (st->done) return;
+  const unsigned long long clk0 = wall_clock64();  // vg_profile bit 2 (KClock)
   extern __shared__ __attribute__((aligned(16))) double T[];
   constexpr int kN = kMaxNB * kTile;
   __shared__ double Jv[kN], Dv[kN], yv[kN], wv[kN], xv[kN], col[kN], sP[64], sG[64];
@@ -876,6 +877,13 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) q1 += __shfl_xor(q1, off, 64);
     if (lane == 0) st->q1 = 0.5 * q1;
+  }
+  if (clk && clk->on) {
+    __syncthreads();
+    if (tid == 0) {
+      clk->solve_ticks += (unsigned long long)wall_clock64() - clk0;
+      clk->solve_n += 1;
+    }
   }
   VG_PROBE_MARK(8);
 #ifdef VG_PROBE
@@ -1224,7 +1232,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   int xerr = VG_OK;  // exchange errors (sharded mode)
   // k_ba_solve launch events (vg_profile): on every prof_every-th run only, so
   // that timing a long run costs the stream little (each record is a gap)
-  const bool solve_ev = ctx->prof_on && (ctx->prof_every <= 1 || ctx->prof_runs++ % ctx->prof_every == 0);
+  const bool solve_ev = ctx->prof_on && !ctx->prof_clock && (ctx->prof_every <= 1 || ctx->prof_runs++ % ctx->prof_every == 0);
   // one LM iteration (optimizers.cpp:449-516); kernels early-exit on the
   // device-side flags once converged. Every argument is fixed per context (the
   // factor count, the flags and the publication number live on the device),
@@ -1250,7 +1258,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
                                     d.dvec, d.jvec, d.ipg, d.st);
     if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][0], s);
     k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
-                                         d.st);
+                                         d.st, &ctx->st->clk);
     if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][1], s);
     k_ba_resid<<<nrb + 1, 256, 0, s>>>(nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
                                        ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, nimu, d.imurec, &ctx->st->imu_head, d.bias,
@@ -1418,7 +1426,7 @@ int ba_solve_test(vg_ctx* ctx, const double* A, const double* b, double* x) {
   VG_HIP(hipMemcpyAsync(d.st, &bs, sizeof(bs), hipMemcpyHostToDevice, s));
   VG_HIP(hipStreamSynchronize(s));
   k_ba_solve<<<1, 1024, solve_lds_bytes(W), s>>>(W, W - 1, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias,
-                                                 d.dxi, d.st);
+                                                 d.dxi, d.st, nullptr);
   VG_HIP(hipGetLastError());
   std::vector<double> out(n);
   VG_HIP(hipMemcpyAsync(out.data(), d.dxi, n * sizeof(double), hipMemcpyDeviceToHost, s));

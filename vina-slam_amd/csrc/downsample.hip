@@ -702,20 +702,18 @@ __global__ void __launch_bounds__(256) k_hds_big(DownsampleBufs d, const int* __
 }
 
 // The /2 fallback pass of local_mapping.cpp:399-403 as ONE workgroup (it is
-// needed only when the first pass kept fewer than 2000 voxels): the same five
-// steps as k_hds_insert .. k_hds_big, separated by workgroup barriers instead
+// needed only when the first pass kept fewer than 2000 voxels): the first four
+// steps of k_hds_insert .. k_hds_mean, separated by workgroup barriers instead
 // of kernel boundaries, the ranks by a block scan over the points in 1024-point
 // tiles, so the output (order, float means) is bit for bit the multi-kernel
-// pass's. On the common path it is one early-exiting launch instead of six.
+// pass's; its dense voxels go to the k_hds_big launch behind it (256
+// workgroups, not one after the other). On the common path it is two
+// early-exiting launches instead of seven.
 constexpr int kHdsFbThreads = 1024;
 __global__ void __launch_bounds__(kHdsFbThreads) k_hds_fallback(double size, DownsampleBufs d,
                                                                 const int* __restrict__ need) {
   if (!*need) return;
-  __shared__ uint32_t bm[kHdsWords];
-  __shared__ float cb[3 * kHdsChunk];
-  __shared__ double rb[kHdsChunk];
   __shared__ unsigned long long s_w64[kHdsFbThreads / 64];
-  __shared__ int s_w[kHdsFbThreads / 64], s_base, s_nbig;
   const HdsIn a = *d.arg;
   const float *x = a.x, *y = a.y, *z = a.z, *in = a.in;
   const int n = a.n, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = kHdsFbThreads / 64;
@@ -777,7 +775,6 @@ __global__ void __launch_bounds__(kHdsFbThreads) k_hds_fallback(double size, Dow
   if (tid == 0) {
     d.hflags[1] = nv;
     d.hflags[3] = 0;
-    s_nbig = 0;
   }
   __syncthreads();
   // 3. point indices into their voxel's segment (k_hds_scatter)
@@ -792,8 +789,8 @@ __global__ void __launch_bounds__(kHdsFbThreads) k_hds_fallback(double size, Dow
     const int i = d.vfirst[v];
     const uint32_t s = d.pslot[i];
     const int b = d.hoff[s], cnt = d.hcnt[s];
-    if (cnt > kHdsSmall) {
-      d.bigv[atomicAdd(&s_nbig, 1)] = v;
+    if (cnt > kHdsSmall) {  // dense: k_hds_big behind this launch, one workgroup each
+      d.bigv[atomicAdd(&d.hflags[3], 1)] = v;
       continue;
     }
     const uint32_t* sg = d.pseg + b;
@@ -812,10 +809,7 @@ __global__ void __launch_bounds__(kHdsFbThreads) k_hds_fallback(double size, Dow
     d.hcnt[s] = 0;
     d.hfill[s] = 0;
   }
-  __syncthreads();
-  // 5. dense voxels, one after the other by the whole workgroup (k_hds_big)
-  const int nbig = s_nbig;
-  for (int q = 0; q < nbig; q++) hds_big_voxel(d, d.bigv[q], x, y, z, in, bm, s_w, &s_base, cb, rb);
+  // 5. dense voxels: the k_hds_big launch behind this one (gated on the same flag)
 }
 
 // the pipeline's downsample, asynchronous on stream s; with `fallback`, the
@@ -847,7 +841,10 @@ int ds_enqueue_hashed(vg_ctx* ctx, hipStream_t s, const float* x, const float* y
       k_hds_mean<<<g, kBlock, 0, st>>>(d, nullptr);
       k_hds_mid<<<grid_for(cap / kHdsSmall + 1, kBlock / 64, 256), kBlock, 0, st>>>(d, nullptr);
       k_hds_big<<<256, kBlock, 0, st>>>(d, nullptr);
-      if (fallback) k_hds_fallback<<<1, kHdsFbThreads, 0, st>>>(voxel / 2, d, need);
+      if (fallback) {
+        k_hds_fallback<<<1, kHdsFbThreads, 0, st>>>(voxel / 2, d, need);
+        k_hds_big<<<256, kBlock, 0, st>>>(d, need);
+      }
     };
     const bool use_graph = ctx->use_graphs && fallback && voxel == ctx->cfg.down_size;
     if (use_graph && !ctx->g_ds) {

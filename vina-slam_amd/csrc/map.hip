@@ -265,6 +265,8 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
                                               int* __restrict__ cache, double* __restrict__ partials,
                                               int* __restrict__ pk) {
   if (st->done) return;
+  const bool clk_on = st->clk.on != 0;
+  if (clk_on && threadIdx.x == 0) atomicMin(&st->clk.iekf_t0, (unsigned long long)wall_clock64());
   VG_PROBE_BEGIN();
   const int n = st->sn;
   const float* __restrict__ x = st->sx;
@@ -379,6 +381,10 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
     int j = threadIdx.x;
     partials[(size_t)blockIdx.x * kIekfVals + j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
   }
+  if (clk_on) {  // the workgroup's end (its partials written)
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(&st->clk.iekf_t1, (unsigned long long)wall_clock64());
+  }
   if (blockIdx.x == 0) VG_PROBE_MARK(31);  // the block reduction
 #ifdef VG_PROBE
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_probe[59], 1ull);
@@ -408,6 +414,15 @@ __global__ void __launch_bounds__(1024) k_iekf_update(int nb, const double* __re
                                                      DState* __restrict__ st, int it) {
   __shared__ IekfLds L;
   if (st->done) return;
+  if (threadIdx.x == 0 && st->clk.on) {  // fold the k_iekf launch this update follows into the clock sums
+    KClock& c = st->clk;
+    if (c.iekf_t1 > c.iekf_t0) {
+      c.iekf_ticks += c.iekf_t1 - c.iekf_t0;
+      c.iekf_n += 1;
+    }
+    c.iekf_t0 = ~0ull;
+    c.iekf_t1 = 0;
+  }
   iekf_update_block(nb, partials, st, it, L);
 }
 // sharded mode: this shard's 34 sums (the update then runs on the all-reduced ones)

@@ -483,8 +483,14 @@ static int resolve_ds(vg_ctx* ctx, HostPipe* P) {
 // previous insert has read the ds buffers (and for a deskewed scan)
 static int ds_enqueue_scan(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n,
                            int pub_seq) {
-  if (ctx->want_ds_stream && ctx->stream_ds == ctx->stream)
+  if (ctx->want_ds_stream && ctx->stream_ds == ctx->stream) {
+    // the new stream starts behind everything already on the main stream: the
+    // scan's upload + unpack (upload_scan ran while the two were one stream)
+    // and the previous scans' inserts, none of which recorded an event it waits on
     VG_HIP(hipStreamCreateWithFlags(&ctx->stream_ds, hipStreamNonBlocking));
+    VG_HIP(hipEventRecord(ctx->ev_ds_done, ctx->stream));
+    VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_ds_done, 0));
+  }
   VG_HIP(flush_insert_events(ctx));
   VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ds_free_ev ? ctx->ds_free_ev : ctx->ev_ds_free, 0));
   VG_HIP(hipStreamWaitEvent(ctx->stream_ds, ctx->ev_scan_ready, 0));  // a deskewed scan (no-op otherwise)
@@ -1117,10 +1123,11 @@ int host_window(vg_ctx* ctx, double* out) {
   for (size_t i = 0; i < P->x_buf.size(); i++) state_out(P->x_buf[i], out + 250 * i);
   return (int)P->x_buf.size();
 }
-int host_traj(vg_ctx* ctx, double* out, int cap) {
+int host_traj(vg_ctx* ctx, double* out, int cap, int from) {
   HostPipe* P = hp(ctx);
   int n = (int)P->traj.size() / kTrajRow;
-  if (out) memcpy(out, P->traj.data(), (size_t)(n < cap ? n : cap) * kTrajRow * sizeof(double));
+  const int k = from < n ? (n - from < cap ? n - from : cap) : 0;
+  if (out && k > 0) memcpy(out, P->traj.data() + (size_t)from * kTrajRow, (size_t)k * kTrajRow * sizeof(double));
   return n;
 }
 int host_path(vg_ctx* ctx, double* out, int cap) {

@@ -224,6 +224,19 @@ constexpr int kXS = 24;             // per-frame state: R 9, p 3, v 3, bg 3, ba 
 constexpr int kXC = kXS + 225;      // x_curr: frame state + cov 15x15 (row-major)
 constexpr int kMaxWin = 32;
 constexpr int kBaImuRec = 64 + 225;  // IMU_PRE record (doubles): deltas, bias Jacobians, dtime, cov_inv
+// In-kernel clocks of the roofline kernels (vg_profile bit 2): s_memrealtime
+// ticks (wall_clock64, the device's constant-rate clock), kernel-only spans:
+// a k_iekf launch runs from its first workgroup's start to its last
+// workgroup's end (atomicMin / atomicMax here, folded into the sums by the
+// k_iekf_update behind it, which runs exactly when the point loop did);
+// k_ba_solve is one workgroup, timed by its thread 0.
+struct KClock {
+  unsigned long long iekf_t0, iekf_t1;     // the current k_iekf launch
+  unsigned long long iekf_ticks, iekf_n;   // executed k_iekf launches
+  unsigned long long solve_ticks, solve_n; // executed k_ba_solve launches
+  int on, pad;
+};
+
 struct DState {
   double xc[256];                   // x_curr (IMUST, types.hpp:43-113)
   double xp[256];                   // x_prop (odometry.cpp:67)
@@ -243,6 +256,7 @@ struct DState {
   // (imu_head + k) % kMaxWin, so the slide is one index step
   int imu_head, pad_h[3];
   double imurec[kMaxWin * kBaImuRec];
+  KClock clk;
 };
 // x_buf.push_back(x_curr) + a new IMU_PRE record, as kernel arguments (k_push_state,
 // or folded into the insert's first launch, map_insert)
@@ -386,6 +400,7 @@ struct vg_ctx {
   long prof_runs = 0;
   int rc_total = 0, rc_thread_num = 0;  // the last recut's window point total / thread_num (its resume)
   bool prof_stages = false;  // per-stage events (vg_profile bit 1)
+  bool prof_clock = false;   // in-kernel clocks instead of k_ba_solve events (vg_profile bit 2, KClock)
   hipEvent_t prof_ev[8][2] = {};
   hipEvent_t sync_ev = nullptr;  // host-spin synchronisation (vg::stream_wait)
   hipEvent_t iekf_ev[16][2] = {};  // k_iekf launches of the last two scans (vg_profile), 8 per scan
@@ -628,7 +643,7 @@ void host_reset(vg_ctx* ctx);
 void host_seed(vg_ctx* ctx, const double* s);
 int host_state(vg_ctx* ctx, double* s);
 int host_window(vg_ctx* ctx, double* out);
-int host_traj(vg_ctx* ctx, double* out, int cap);
+int host_traj(vg_ctx* ctx, double* out, int cap, int from = 0);  // rows [from, from + cap), returns the row count
 int host_path(vg_ctx* ctx, double* out, int cap);
 int host_poll(vg_ctx* ctx);
 int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n, double beg,

@@ -618,13 +618,7 @@ int vg_poll(vg_ctx* ctx, int* n_scans, int* n_traj, int* n_path) {
 
 int vg_poll_rows(vg_ctx* ctx, double* traj, int traj_from, int traj_cap, double* path, int path_cap) {
   if (!ctx || traj_from < 0 || traj_cap < 0 || path_cap < 0) return VG_E_ARG;
-  const int nt = host_traj(ctx, nullptr, 0);
-  if (traj && traj_cap > 0 && traj_from < nt) {
-    std::vector<double> all((size_t)nt * vg::kTrajRow);
-    host_traj(ctx, all.data(), nt);
-    const int k = nt - traj_from < traj_cap ? nt - traj_from : traj_cap;
-    memcpy(traj, &all[(size_t)traj_from * vg::kTrajRow], (size_t)k * vg::kTrajRow * sizeof(double));
-  }
+  if (traj && traj_cap > 0) host_traj(ctx, traj, traj_cap, traj_from);
   if (path && path_cap > 0) host_path(ctx, path, path_cap);
   return VG_OK;
 }
@@ -732,8 +726,17 @@ int vg_profile(vg_ctx* ctx, int on) {
   if (!ctx) return VG_E_ARG;
   ctx->prof_on = (on & 1) != 0;
   ctx->prof_stages = (on & 2) != 0;
+  ctx->prof_clock = (on & 4) != 0;
   ctx->prof_every = (on >> 8) & 0xff;  // k_ba_solve events on every prof_every-th BA run (0/1: every run)
   ctx->prof_runs = 0;
+  {  // bit 2: the in-kernel clocks (KClock), reset; set behind everything already enqueued
+    VG_TRY(host_sync(ctx));
+    vg::KClock k;
+    memset(&k, 0, sizeof(k));
+    k.iekf_t0 = ~0ull;
+    k.on = (on & 4) ? 1 : 0;
+    VG_HIP(hipMemcpy(&ctx->st->clk, &k, sizeof(k), hipMemcpyHostToDevice));
+  }
   ctx->iekf_ring_n = 0;
   for (int i = 0; i < vg::kProfAll; i++) {
     ctx->prof_ms[i] = 0;
@@ -744,7 +747,18 @@ int vg_profile(vg_ctx* ctx, int on) {
 }
 
 int vg_profile_read(vg_ctx* ctx, int stage, double* total_ms, int* count) {
-  if (!ctx || stage < 0 || stage >= vg::kProfAll || !total_ms || !count) return VG_E_ARG;
+  if (!ctx || stage < 0 || stage >= vg::kProfAll + 2 || !total_ms || !count) return VG_E_ARG;
+  if (stage >= vg::kProfAll) {  // 16 k_iekf, 17 k_ba_solve: kernel-only time from the in-kernel clocks
+    VG_TRY(host_sync(ctx));
+    vg::KClock k;
+    VG_HIP(hipMemcpy(&k, &ctx->st->clk, sizeof(k), hipMemcpyDeviceToHost));
+    int khz = 0;
+    VG_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
+    const unsigned long long t = stage == vg::kProfAll ? k.iekf_ticks : k.solve_ticks;
+    *total_ms = khz > 0 ? (double)t / (double)khz : 0.0;
+    *count = (int)(stage == vg::kProfAll ? k.iekf_n : k.solve_n);
+    return VG_OK;
+  }
   *total_ms = ctx->prof_ms[stage];
   *count = ctx->prof_n[stage];
   return VG_OK;

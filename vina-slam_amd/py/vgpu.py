@@ -418,12 +418,14 @@ class Context:
 
     PROFILE_STAGES = ["downsample", "iekf", "insert", "recut", "ba", "margi", "iekf_total", "ba_solve",
                       "host_propagate", "host_downsample", "host_iekf", "host_push", "host_insert", "host_recut",
-                      "host_ba", "host_margi"]
+                      "host_ba", "host_margi", "k_iekf_clock", "k_ba_solve_clock"]
 
-    def profile(self, on=True, stages=False, every=1):
+    def profile(self, on=True, stages=False, every=1, clock=False):
         """on: k_iekf / k_ba_solve launch events (the solve's on every `every`-th
-        BA run); stages: per-stage events as well."""
-        flags = (1 if on else 0) | (2 if stages else 0) | ((max(1, min(255, every)) & 0xff) << 8)
+        BA run) and host stage timers; stages: per-stage events as well; clock:
+        the in-kernel clocks of k_iekf / k_ba_solve (kernel-only time, graphs
+        kept; replaces the solve's events)."""
+        flags = (1 if on else 0) | (2 if stages else 0) | (4 if clock else 0) | ((max(1, min(255, every)) & 0xff) << 8)
         self._chk(lib().vg_profile(self.h, flags), "vg_profile")
 
     def profile_read(self):
