@@ -181,6 +181,12 @@ def main():
     imus = [h[4] for h in host_scans]
     npts = int(np.mean([s[1] for s in scans[warmup:total]]))
     ctx = vgpu.Context(vgconfig.to_c(p), device=local, max_points=max(s[1] for s in scans) + 16, **CAP)
+    # same-build A/B experiments only: VG_BENCH_DEBUG="key=value,..." sets test knobs (vgx_debug) on the
+    # metric leg's context; the line records them
+    dbg = os.environ.get("VG_BENCH_DEBUG", "")
+    for kv in filter(None, dbg.split(",")):
+        k, v = kv.split("=")
+        ctx.debug(int(k), int(v))
     if tile:  # one RCCL communicator inside the library, id from rank 0
         obj = [vgpu.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
@@ -341,7 +347,7 @@ def main():
             "roofline": roof, "roofline_k_ba_solve": roof_solve, "roofline_k_iekf": roof_iekf,
             "host_ms_per_scan": host_ms, "host_input": h2d, "cpu_baseline": cpu, "ate_vs_cpu": ate_cpu,
             "target_128line": targets or None, "multi_sequence": multi_roofline(multi, roof),
-            "multi_sequence_1M": multi_1m, "env": {"GPU_MAX_HW_QUEUES": hwq},
+            "multi_sequence_1M": multi_1m, "env": {"GPU_MAX_HW_QUEUES": hwq, "VG_BENCH_DEBUG": dbg or None},
         }
         print(json.dumps(line))
     if world > 1:

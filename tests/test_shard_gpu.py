@@ -106,3 +106,53 @@ def test_two_shards_match_one(cfgname, lidar, nscan):
     drot = np.abs(t1[:, 1:10] - ta[:, 1:10]).max()
     print("ATE sharded vs unsharded: %.3e m, max dpos %.3e m, max dR %.3e" % (err, dpos, drot))
     assert dpos < TIGHT_M and drot < TIGHT_M
+
+
+def _run_desync(rank, world, q, port):
+    """Rank 1's exchange counter is advanced by one before the first scan: its
+    exchanges carry another guard value than rank 0's (shard.hip), so both
+    ranks must get VG_E_STATE ("out of step") at their first exchange instead
+    of pairing different exchanges."""
+    import torch
+    import torch.distributed as dist
+    try:
+        p = vgconfig.load("mid360")
+        g = p["General"]
+        seq = synth.Sequence("16line", 2, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
+        ctx = vgpu.Context(vgconfig.to_c(p), **CAP["16line"])
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        ctx.shard_host(rank, world, lambda arr: dist.all_reduce(torch.from_numpy(arr)))
+        if rank == 1:
+            ctx.debug(12, 1)
+        ctx.seed(seq.gt_state(0))
+        msg = "no error"
+        for k in range(4):
+            xyz, it, b, e = seq.scan(k)
+            try:
+                ctx.step(xyz, it, b, e, seq.imu(k))
+                ctx.stats_log()
+            except vgpu.VgError as ex:
+                msg = "scan %d: %s" % (k, ex)
+                break
+        q.put((rank, msg))
+        ctx.close()
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, "exception: " + traceback.format_exc()))
+
+
+def test_desynchronised_rank_gets_an_error():
+    import torch.multiprocessing as mp
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _port()
+    procs = [ctxm.Process(target=_run_desync, args=(r, 2, q, port)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for pr in procs:
+        pr.join(timeout=60)
+    for r in (0, 1):
+        assert "out of step" in res[r] and "(-5)" in res[r], res[r]

@@ -1246,7 +1246,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
                                                        d.st);
     // sharded: every shard's factors -> one LiDAR Hessian / gradient / residual
     // (out of place: a rejected step re-reduces the unchanged partial)
-    if (sharded && xerr == VG_OK) xerr = shard_allreduce(ctx, hl_part, d.hl, nout, 0);
+    if (sharded && xerr == VG_OK) xerr = shard_allreduce(ctx, hl_part, d.hl, nout, 0, 3);
     if (k == 0 && ctx->dbg_capture == 1 && ctx->dbg_cap_buf) {  // test knob (vgx_debug 5): the first pass
       (void)hipMemcpyAsync(ctx->dbg_cap_buf, d.hl, nout * sizeof(double), hipMemcpyDeviceToDevice, s);
       (void)hipMemcpyAsync(ctx->dbg_cap_buf + nout, d.imuout, (size_t)nimu * 931 * sizeof(double),
@@ -1265,7 +1265,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
                                        d.imures);
     if (sharded) {  // the residual over every shard's factors
       k_ba_rsum<<<1, 64, 0, s>>>(nrb, d.rpart, rsum, d.st);
-      if (xerr == VG_OK) xerr = shard_allreduce(ctx, rsum, rsum + 1, 1, 0);
+      if (xerr == VG_OK) xerr = shard_allreduce(ctx, rsum, rsum + 1, 1, 0, 4);
     }
     k_ba_control<<<1, 256, 0, s>>>(W, nimu, sharded ? 1 : nrb, ctx->cfg.imu_coef, d.hl, nl + L,
                                    d.imuout, d.imures, sharded ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st,

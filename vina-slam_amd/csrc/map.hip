@@ -43,6 +43,7 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(m.cov_add = ctx->arena.take<double>(cn * kCovN));
   good &= ok(m.eig = ctx->arena.take<double>(cn * 12));
   good &= ok(m.jour = ctx->arena.take<double>(cn));
+  good &= ok(m.dbox = ctx->arena.take<double>(cn * 6));
   good &= ok(m.pcrs = ctx->arena.take<Clu>(cn * W));
   good &= ok(m.nscr = ctx->arena.take<int>(cn * 4));
   good &= ok(m.cfirst = ctx->arena.take<int>(cn * 8));
@@ -90,6 +91,9 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(w.rc = ctx->arena.take<int>(128));
   good &= ok(w.cand_bits = ctx->arena.take<uint32_t>(ctx->cap.max_nodes / 32 + 1));
   good &= ok(w.plan = ctx->arena.take<int>(cn * 8));
+  good &= ok(w.sub_odd = ctx->arena.take<int>(cn));
+  good &= ok(w.info_odd = ctx->arena.take<int>(w.cap));
+  good &= ok(w.ev_odd = ctx->arena.take<uint64_t>(w.cap));
   w.nparts = 1024;
   good &= ok(w.partials = ctx->arena.take<double>((size_t)w.nparts * 40));
   if (!good) {
@@ -307,7 +311,10 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
     int leaf = cv >= 0 ? (cv & 0x3fffffff) : -1;
     int flag = 0;
     double sigma = 0;
-    bool hit = leaf >= 0 && inside(m.hdr[leaf], wld);
+    // a matched leaf (octos[i]): OctoTree::inside's inclusive box; a memo: the
+    // descent's own region (dbox: strict where the descent is strict), so a
+    // point on a centre plane is never kept in the wrong sibling
+    bool hit = leaf >= 0 && ((cv & 0x40000000) ? in_dbox(m.dbox + (size_t)leaf * 6, wld) : inside(m.hdr[leaf], wld));
     if (hit && (cv & 0x40000000)) {
       uint64_t kw, kl;
       const NodeHdr& hl = m.hdr[leaf];
@@ -458,7 +465,7 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
   if (ctx->shard.world > 1) {  // this shard's sums, all-reduced, then the (replicated) update
     double* sums = ctx->shard.d_buf;
     k_iekf_reduce<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, sums);
-    VG_TRY(shard_allreduce(ctx, sums, sums + 64, kIekfVals, 0));
+    VG_TRY(shard_allreduce(ctx, sums, sums + 64, kIekfVals, 0, 0));
     k_iekf_update<<<1, 1024, 0, s>>>(-1, sums + 64, ctx->st, it);
   } else {
     k_iekf_update<<<1, 1024, 0, s>>>(nb, w.partials, ctx->st, it);
@@ -721,6 +728,7 @@ __global__ void __launch_bounds__(256) k_ins_roots_alloc(int n_arg, const int* _
       const int64_t k[3] = {unpack_axis(key, 42), unpack_axis(key, 21), unpack_axis(key, 0)};
       for (int j = 0; j < 3; j++) c[j] = (0.5 + k[j]) * mp.vs;
       init_node(m.hdr[r], c, (float)(mp.vs / 4.0), 0, -1);  // records zeroed by map_reset
+      dbox_root(m.dbox + (size_t)r * 6);
       m.hval[s] = r;
     } else {
       r = m.hval[s];
@@ -758,6 +766,7 @@ __global__ void __launch_bounds__(256) k_ins_newalloc(int n, const uint32_t* __r
     int64_t k[3] = {unpack_axis(key, 42), unpack_axis(key, 21), unpack_axis(key, 0)};
     for (int j = 0; j < 3; j++) c[j] = (0.5 + k[j]) * mp.vs;
     init_node(m.hdr[id], c, (float)(mp.vs / 4.0), 0, -1);
+    dbox_root(m.dbox + (size_t)id * 6);
     m.hval[s] = id;
     m.hfirst[s] = 0x7f7f7f7f;
     m.in_slide[id] = 1;
@@ -1114,6 +1123,7 @@ __device__ __forceinline__ void alloc_parent(DevMap& m, int p, int id0, int* nex
     double c[3];
     for (int j = 0; j < 3; j++) c[j] = ph.center[j] + (float)((2 * xyz[j] - 1) * ph.qlen);
     init_node(m.hdr[id], c, ph.qlen / 2, ph.layer + 1, p);
+    dbox_child(m.dbox + (size_t)id * 6, m.dbox + (size_t)p * 6, ph.center, o);
     ph.child[o] = id;
     if (next) next[next_pos + k - 1] = id;
   }
@@ -1340,7 +1350,7 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread
   k_ins_roots_alloc<<<ntile, kBlock, 0, s>>>(n, nd, ntile, w.u0, w.v1, (const int*)w.ac_cnt, mp, m);
   if (m.shard_world > 1) {  // the thread_num quirk counts distinct roots over all shards
     k_copy_int<<<1, 64, 0, s>>>(m.counters + kCntTouched, m.counters + kCntGTouched);
-    VG_TRY(shard_allreduce(ctx, m.counters + kCntGTouched, m.counters + kCntGTouched, 1, 1));
+    VG_TRY(shard_allreduce(ctx, m.counters + kCntGTouched, m.counters + kCntGTouched, 1, 1, 1));
   }
   k_ins_descend<<<g * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(n, nd, thread_num, w.pw, m, w.u0, w.leaf, w.list2);
   const int ins_cap = (ctx->dbg_ins_cap >= 0 && ctx->dbg_ins_cap < kInsAllocCap) ? ctx->dbg_ins_cap : kInsAllocCap;
@@ -1371,8 +1381,8 @@ int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num
 // k_rc_apply sets rc[kRcAbort]; the host then replays the rest of the recut
 // with the host-sized path (recut_slow_apply), which only happens while the
 // map is first built.
-enum { kRcLvl = 0, kRcSub = 16, kRcWin = 32, kRcAbort = 48, kRcCh = 64, kRcChBase = 80, kRcStatus = 126, kRcNOld = 127,
-       kRcN = 128 };
+enum { kRcLvl = 0, kRcSub = 16, kRcWin = 32, kRcAbort = 48, kRcCh = 64, kRcChBase = 80, kRcNch = 96, kRcTot = 104,
+       kRcNode0 = 112, kRcStatus = 126, kRcNOld = 127, kRcN = 128 };
 constexpr int kApplyThreads = 1024;
 constexpr int kApplySub = kApplyThreads;  // subdividing leaves per level (one lane each)
 
@@ -1441,10 +1451,11 @@ __global__ void __launch_bounds__(256) k_rc_visit(int L, int thread_num, const i
 // own range of the leaf's block of the event list, in walk order, so a child's
 // events come out grouped and already in the reference's push order (point_fix
 // by index, then frame by frame, index ascending) — no sort. Event: phase << 21
-// | index (phase 0 point_fix, 1 + ord a window frame). rcinfo[17 q ..]: the
-// block's start, then per octant its offset and count; nscr[leaf*4+0] = q.
+// | index (phase 0 point_fix, 1 + ord a window frame). rcinfo[18 q ..]: the
+// block's start, then per octant its offset and count, then the mask of
+// non-empty octants; nscr[leaf*4+0] = q.
 constexpr int kRcWinWaves = 4;
-constexpr int kRcInfo = 17;
+constexpr int kRcInfo = 18;  // event base, 8 octant offsets, 8 octant counts, octant mask
 // point e of the leaf's walk (fixed points, then the window's runs in
 // order), its phase located among the wave's per-phase run starts (lane ph
 // holds phase ph's exclusive start ex, run start st and slot)
@@ -1470,82 +1481,93 @@ __device__ __forceinline__ int rc_walk_octant(const NodeHdr& h, int e, int wc, i
 // one wave per subdividing leaf: the leaf's points are flattened across the
 // phases so each 64-point chunk costs one round of loads whatever the runs'
 // lengths; pass 1 counts the octants, pass 2 writes each octant's events
-// (ph << 21 | idx) at its running position, walk order kept
+// (ph << 21 | idx) at its running position, walk order kept. The leaf's
+// children-to-be are counted into rc[kRcNch + L] (the fused level kernel
+// sizes its pushes from it).
+__device__ __forceinline__ void rc_win_leaf(int L, int leaf, int q, const WinD* __restrict__ win, DevMap& m,
+                                            uint64_t* __restrict__ ev, int* __restrict__ rcinfo, int cap,
+                                            int info_cap, int* __restrict__ rc) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int wc = win->win_count;
+  const int my_slot = (lane >= 1 && lane <= wc) ? win->mp[lane - 1] : 0;
+  const NodeHdr& h = m.hdr[leaf];
+  int len = 0, st = 0;
+  if (lane == 0) len = h.fix_cnt;
+  else if (lane <= wc && !lseg_get(m, leaf, my_slot, st, len)) len = 0;
+  int ex = len;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(ex, off, 64);
+    if (lane >= off) ex += y;
+  }
+  const int total = __shfl(ex, 63, 64);
+  ex -= len;
+  int base = 0;
+  if (lane == 0) base = atomicAdd(&rc[kRcWin + L], total);
+  base = __shfl(base, 0, 64);
+  if ((size_t)q * kRcInfo + kRcInfo > (size_t)info_cap || base + total > cap) {
+    if (lane == 0) {
+      atomicOr(&m.counters[kCntErr], 16);
+      if ((size_t)q * kRcInfo + kRcInfo <= (size_t)info_cap) rcinfo[(size_t)q * kRcInfo + 17] = 0;  // no children
+    }
+    return;
+  }
+  int cnt8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int e0 = 0; e0 < total; e0 += 64) {
+    const int e = e0 + lane;
+    int ph, idx;
+    int o = rc_walk_octant(h, e < total ? e : total - 1, wc, ex, st, my_slot, win, m, ph, idx);
+    if (e < total) m.cfirst[(size_t)leaf * 8 + o] = -5;
+    else o = -1;
+#pragma unroll
+    for (int k = 0; k < 8; k++) cnt8[k] += __popcll(__ballot(o == k));
+  }
+  int off8[8], run = 0, mask = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    off8[k] = run;
+    run += cnt8[k];
+    mask |= (cnt8[k] > 0) << k;
+  }
+  if (lane == 0) {
+    int* inf = rcinfo + (size_t)q * kRcInfo;
+    inf[0] = base;
+    for (int k = 0; k < 8; k++) {
+      inf[1 + k] = off8[k];
+      inf[9 + k] = cnt8[k];
+    }
+    inf[17] = mask;
+    m.nscr[(size_t)leaf * 4 + 0] = q;
+    atomicAdd(&rc[kRcNch + L], __popc(mask));
+  }
+  for (int e0 = 0; e0 < total; e0 += 64) {
+    const int e = e0 + lane;
+    int ph, idx;
+    int o = rc_walk_octant(h, e < total ? e : total - 1, wc, ex, st, my_slot, win, m, ph, idx);
+    if (e >= total) o = -1;
+    int pos = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint64_t bk = __ballot(o == k);
+      if (o == k) pos = base + off8[k] + __popcll(bk & below);
+      off8[k] += __popcll(bk);
+    }
+    if (o >= 0) ev[pos] = ((uint64_t)ph << 21) | (uint64_t)idx;
+  }
+}
 __global__ void __launch_bounds__(64 * kRcWinWaves) k_rc_win(int L, const int* __restrict__ sub,
                                                              const WinD* __restrict__ win, DevMap m,
                                                              uint64_t* __restrict__ ev, int* __restrict__ rcinfo,
                                                              int cap, int info_cap, int* __restrict__ rc) {
   if (rc[kRcAbort]) return;
   const int nsub = rc[kRcSub + L];
-  const int lane = threadIdx.x & 63;
-  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int wc = win->win_count;
-  if (wc > 63) {
+  if (win->win_count > 63) {
     if (threadIdx.x == 0 && blockIdx.x == 0) atomicOr(&m.counters[kCntErr], 16);
     return;
   }
-  const int my_slot = (lane >= 1 && lane <= wc) ? win->mp[lane - 1] : 0;
-  for (int q = blockIdx.x * kRcWinWaves + (threadIdx.x >> 6); q < nsub; q += gridDim.x * kRcWinWaves) {
-    const int leaf = sub[q];
-    const NodeHdr& h = m.hdr[leaf];
-    int len = 0, st = 0;
-    if (lane == 0) len = h.fix_cnt;
-    else if (lane <= wc && !lseg_get(m, leaf, my_slot, st, len)) len = 0;
-    int ex = len;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(ex, off, 64);
-      if (lane >= off) ex += y;
-    }
-    const int total = __shfl(ex, 63, 64);
-    ex -= len;
-    int base = 0;
-    if (lane == 0) base = atomicAdd(&rc[kRcWin + L], total);
-    base = __shfl(base, 0, 64);
-    if ((size_t)q * kRcInfo + kRcInfo > (size_t)info_cap || base + total > cap) {
-      if (lane == 0) atomicOr(&m.counters[kCntErr], 16);
-      continue;
-    }
-    int cnt8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int e0 = 0; e0 < total; e0 += 64) {
-      const int e = e0 + lane;
-      int ph, idx;
-      int o = rc_walk_octant(h, e < total ? e : total - 1, wc, ex, st, my_slot, win, m, ph, idx);
-      if (e < total) m.cfirst[(size_t)leaf * 8 + o] = -5;
-      else o = -1;
-#pragma unroll
-      for (int k = 0; k < 8; k++) cnt8[k] += __popcll(__ballot(o == k));
-    }
-    int off8[8], run = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      off8[k] = run;
-      run += cnt8[k];
-    }
-    if (lane == 0) {
-      int* inf = rcinfo + (size_t)q * kRcInfo;
-      inf[0] = base;
-      for (int k = 0; k < 8; k++) {
-        inf[1 + k] = off8[k];
-        inf[9 + k] = cnt8[k];
-      }
-      m.nscr[(size_t)leaf * 4 + 0] = q;
-    }
-    for (int e0 = 0; e0 < total; e0 += 64) {
-      const int e = e0 + lane;
-      int ph, idx;
-      int o = rc_walk_octant(h, e < total ? e : total - 1, wc, ex, st, my_slot, win, m, ph, idx);
-      if (e >= total) o = -1;
-      int pos = 0;
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint64_t bk = __ballot(o == k);
-        if (o == k) pos = base + off8[k] + __popcll(bk & below);
-        off8[k] += __popcll(bk);
-      }
-      if (o >= 0) ev[pos] = ((uint64_t)ph << 21) | (uint64_t)idx;
-    }
-  }
+  for (int q = blockIdx.x * kRcWinWaves + (threadIdx.x >> 6); q < nsub; q += gridDim.x * kRcWinWaves)
+    rc_win_leaf(L, sub[q], q, win, m, ev, rcinfo, cap, info_cap, rc);
 }
 
 __global__ void __launch_bounds__(256) k_child_alloc(int np, const int* __restrict__ parents, const uint32_t* __restrict__ off, DevMap m,
@@ -1642,11 +1664,185 @@ __global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int sub_cap, 
 #endif
 }
 
-// pushes of one level's children (push_fix then push per frame, octree.cpp:
-// 151-188), one wave per child; role layout: 0-8 accumulated cluster, 9-17
-// fixed cluster (point_fix events), 18-62 cov_add, 63-71 the frame cluster of
-// the current window slot (lanes 0-7 carry a second role)
 constexpr int kRcPushWaves = 4;
+// the pushes of one child (push_fix then push per frame, octree.cpp:151-188)
+// by one wave: its events keys[j0, j1) (point_fix first, then frame by
+// frame), its parent and layer given (the caller may have initialised the
+// header in this same wave); E / s_slot / s_pre: the wave's LDS slices. Role
+// layout: 0-8 accumulated cluster, 9-17 fixed cluster (point_fix events),
+// 18-62 cov_add, 63-71 the frame cluster of the current window slot (lanes
+// 0-7 carry a second role)
+__device__ __forceinline__ void rc_push_child(int child, int parent, int layer, int j0, int j1,
+                                              const uint64_t* __restrict__ keys, const MP& mp,
+                                              const WinD* __restrict__ win, DevMap& m, double (*E)[kErec],
+                                              int* s_slot, double* s_pre, const RoleIdx& ri0, const RoleIdx& ri1) {
+  const int lane = threadIdx.x & 63;
+  const int r0 = lane, r1 = lane + 64;
+  const bool has1 = r1 < 72;
+  NodeHdr& h = m.hdr[child];
+  const NodeHdr& ph = m.hdr[parent];
+  const bool listed = layer < mp.max_layer;
+  // leading point_fix events (phase 0 sorts first)
+  int nfix = 0;
+  for (int b0 = j0; b0 < j1; b0 += 64) {
+    const int e = b0 + lane;
+    const bool f = e < j1 && ((keys[e] >> 21) & 63) == 0;
+    const int k = __popcll(__ballot(f));
+    nfix += k;
+    if (k < 64) break;
+  }
+  int fix_off = 0;
+  if (nfix > 0 && listed) {
+    int off = 0;
+    if (lane == 0) {
+      off = atomicAdd(&m.counters[kCntFix], nfix);
+      if (off + nfix > m.cap_fix) {
+        atomicOr(&m.counters[kCntErr], 8);
+        off = -1;
+      } else {
+        h.fix_off = off;
+        h.fix_cap = nfix;
+        h.fix_cnt = nfix;
+      }
+    }
+    fix_off = __shfl(off, 0, 64);
+    if (fix_off < 0) return;
+  }
+  // the child's run of each window slot (its events of phase 1 + ord are
+  // contiguous and in index order): lane p < win_count finds phase p + 1's
+  // range by binary search and takes the run from the slot's arena
+  int run_lo = 0, run_st = 0;
+  if (listed) {
+    const int wc = win->win_count;
+    if (lane < wc) {
+      const uint64_t base = 0;  // a child's events: phase << 21 | index, ascending
+      auto lower = [&](uint64_t key) {
+        int lo = j0, hi = j1;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (keys[mid] < key) lo = mid + 1;
+          else hi = mid;
+        }
+        return lo;
+      };
+      run_lo = lower(base | ((uint64_t)(lane + 1) << 21));
+      const int cnt = lower(base | ((uint64_t)(lane + 2) << 21)) - run_lo;
+      if (cnt > 0) {
+        const int slot = win->mp[lane];
+        run_st = atomicAdd(&m.arena[slot], cnt);
+        if (run_st + cnt > m.ord_stride) {
+          atomicOr(&m.counters[kCntErr], 16);
+          run_st = 0;
+        } else {
+          m.lseg[(size_t)child * mp.W + slot] = lseg_pack(run_st, cnt, m.slot_epoch[slot]);
+        }
+      }
+    }
+  }
+  auto acc_ptr = [&](int r, int slot) -> double* {
+    if (r < 9) return r < 6 ? &m.pcr_add[child].P[r] : &m.pcr_add[child].v[r - 6];
+    if (r < 18) return r < 15 ? &m.pcr_fix[child].P[r - 9] : &m.pcr_fix[child].v[r - 15];
+    if (r < 63) return &m.cov_add[(size_t)child * kCovN + r - 18];
+    Clu& lc = m.pcrs[(size_t)child * mp.W + slot];
+    return r < 69 ? &lc.P[r - 63] : &lc.v[r - 69];
+  };
+  // every slot's frame cluster in one round of independent loads (a slot's
+  // run is contiguous, so each is read once, before this wave writes it):
+  // a cluster switch then costs an LDS read, not a dependent HBM load
+  for (int t = lane; t < mp.W * 9; t += 64) {
+    const Clu& lc = m.pcrs[(size_t)child * mp.W + t / 9];
+    const int q = t % 9;
+    s_pre[t] = q < 6 ? lc.P[q] : lc.v[q - 6];
+  }
+  double a0 = r0 < 63 ? *acc_ptr(r0, 0) : 0.0, a1 = 0.0;
+  int cur_slot = -1, loc_n = 0, nwin = 0;
+  for (int b0 = j0; b0 < j1; b0 += 64) {
+    const int e = b0 + lane;
+    if (e < j1) {
+      const uint64_t k = keys[e];
+      const int phase = (int)((k >> 21) & 63), idx = (int)(k & ((1u << 21) - 1));
+      if (phase == 0) {
+        const size_t f = (size_t)ph.fix_off + idx;
+        const V3 pt = ld_v3(&m.fix_pnt[f * 3]);
+        const M3 var = ld_m3(&m.fix_var[f * 9]);
+        fill_record(E[lane], pt, pt, var);
+        s_slot[lane] = -1;
+        if (listed) {
+          const size_t d = (size_t)fix_off + (e - j0);
+          for (int t = 0; t < 3; t++) m.fix_pnt[d * 3 + t] = pt[t];
+          for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = var[t];
+        }
+      } else {
+        const int ord = phase - 1, slot = win->mp[ord];
+        const size_t bb = (size_t)slot * m.cap_wp + idx;
+        const V3 pnt = ld_v3(&m.wp_pnt[bb * 3]);
+        fill_record(E[lane], pnt, rigid(ld_m3(win->R[ord]), pnt, ld_v3(win->p[ord])),
+                    ld_m3(&m.wp_var[bb * 9]));
+        s_slot[lane] = slot;
+        m.wp_leaf[bb] = listed ? child : -1;
+      }
+    }
+    if (listed) {  // the point into the child's run (ds_bpermute of the run's lane; uniform call)
+      const int e = b0 + lane;
+      const int ph = e < j1 ? (int)((keys[e] >> 21) & 63) : 0;
+      const int src = ph > 0 ? ph - 1 : 0;
+      const int lo_p = __shfl(run_lo, src, 64), st_p = __shfl(run_st, src, 64);
+      if (ph > 0) m.wp_ord[(size_t)win->mp[ph - 1] * m.ord_stride + st_p + (e - lo_p)] = (int)(keys[e] & ((1u << 21) - 1));
+    }
+    const int nb = (j1 - b0) < 64 ? (j1 - b0) : 64;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 4
+    for (int k = 0; k < nb; k++) {
+      const int slot = s_slot[k];
+      const bool isfix = slot < 0;
+      if (!isfix && slot != cur_slot) {  // frame cluster switch (uniform)
+        if (cur_slot >= 0) {
+          if (r0 >= 63) *acc_ptr(r0, cur_slot) = a0;
+          if (has1) *acc_ptr(r1, cur_slot) = a1;
+          if (lane == 63) m.pcrs[(size_t)child * mp.W + cur_slot].N += loc_n;
+        }
+        cur_slot = slot;
+        if (r0 >= 63) a0 = s_pre[cur_slot * 9 + r0 - 63];
+        if (has1) a1 = s_pre[cur_slot * 9 + r1 - 63];
+        loc_n = 0;
+      }
+      const double* Ek = E[k];
+      const bool use0 = r0 < 9 || (r0 >= 18 && r0 < 63) || (r0 < 18 ? isfix : !isfix);
+      const double i0 = role_inc(Ek, ri0);
+      if (use0) a0 += i0;
+      if (has1 && !isfix) a1 += role_inc(Ek, ri1);
+      if (!isfix) {
+        loc_n++;
+        nwin++;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (r0 < 63) *acc_ptr(r0, 0) = a0;
+  if (cur_slot >= 0) {
+    if (r0 >= 63) *acc_ptr(r0, cur_slot) = a0;
+    if (has1) *acc_ptr(r1, cur_slot) = a1;
+    if (lane == 63) m.pcrs[(size_t)child * mp.W + cur_slot].N += loc_n;
+  }
+  if (lane == 0) {
+    m.pcr_add[child].N += j1 - j0;
+    m.pcr_fix[child].N += nfix;
+    if (nwin > 0) {
+      h.has_sw = 1;
+      h.isexist = 1;
+    }
+  }
+}
+__device__ __forceinline__ RoleIdx rc_push_role(int r) {
+  if (r < 9) return role_clu(r, kEp);
+  if (r < 18) return role_clu(r - 9, kEp);
+  if (r < 63) return role_cov(r - 18);
+  return role_clu(r - 63, kEq);
+}
+
+// pushes of one level's children, one wave per child (rc_push_child)
 __global__ void __launch_bounds__(64 * kRcPushWaves) k_rc_push(int L, const uint64_t* __restrict__ keys,
                                                                const int* __restrict__ cseg, MP mp,
                                                                const WinD* __restrict__ win, DevMap m,
@@ -1657,173 +1853,230 @@ __global__ void __launch_bounds__(64 * kRcPushWaves) k_rc_push(int L, const uint
   if (rc[kRcAbort]) return;
   const int nch = rc[kRcCh + L], cbase = rc[kRcChBase + L];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  auto make = [](int r) -> RoleIdx {
-    if (r < 9) return role_clu(r, kEp);
-    if (r < 18) return role_clu(r - 9, kEp);
-    if (r < 63) return role_cov(r - 18);
-    return role_clu(r - 63, kEq);
-  };
-  const int r0 = lane, r1 = lane + 64;
-  const bool has1 = r1 < 72;
-  const RoleIdx ri0 = make(r0), ri1 = make(has1 ? r1 : 0);
+  const RoleIdx ri0 = rc_push_role(lane), ri1 = rc_push_role(lane + 64 < 72 ? lane + 64 : 0);
   for (int c = blockIdx.x * kRcPushWaves + wv; c < nch; c += gridDim.x * kRcPushWaves) {
-    const int child = cbase + c, j0 = cseg[2 * c], j1 = cseg[2 * c + 1];
-    NodeHdr& h = m.hdr[child];
-    const NodeHdr& ph = m.hdr[h.parent];
-    const bool listed = h.layer < mp.max_layer;
-    // leading point_fix events (phase 0 sorts first)
-    int nfix = 0;
-    for (int b0 = j0; b0 < j1; b0 += 64) {
-      const int e = b0 + lane;
-      const bool f = e < j1 && ((keys[e] >> 21) & 63) == 0;
-      const int k = __popcll(__ballot(f));
-      nfix += k;
-      if (k < 64) break;
-    }
-    int fix_off = 0;
-    if (nfix > 0 && listed) {
-      int off = 0;
-      if (lane == 0) {
-        off = atomicAdd(&m.counters[kCntFix], nfix);
-        if (off + nfix > m.cap_fix) {
-          atomicOr(&m.counters[kCntErr], 8);
-          off = -1;
-        } else {
-          h.fix_off = off;
-          h.fix_cap = nfix;
-          h.fix_cnt = nfix;
-        }
+    const int child = cbase + c;
+    const NodeHdr& h = m.hdr[child];
+    rc_push_child(child, h.parent, h.layer, cseg[2 * c], cseg[2 * c + 1], keys, mp, win, m, E[wv], s_slot[wv],
+                  s_pre[wv], ri0, ri1);
+  }
+}
+
+// ---- the fused recut levels -------------------------------------------
+// The level loop above costs four dependent launches per level (visit, win,
+// apply, push). The fused form runs one launch per level boundary:
+//   k_rc_level0   visit(0) + win(0): the slide roots, 64 per wave; each wave
+//                 then splits the subdividing leaves its lanes found;
+//   k_rc_level(L) apply(L) + push(L) + visit(L+1) + win(L+1): the level's
+//                 subdividing leaves are sorted and their children counted in
+//                 LDS by every workgroup that pushes (redundantly: the same
+//                 ids k_rc_apply hands out, base + prefix in ascending parent
+//                 id order, so node ids and every order derived from them are
+//                 unchanged); one wave per child initialises it, pushes its
+//                 events, visits it and, when it subdivides, splits its
+//                 points for level L+1; the grid's last waves visit (and
+//                 split) the level's other nodes, the children of internal
+//                 nodes listed by visit(L).
+// Level L's sub list / rcinfo / events and level L+1's live in alternate
+// buffers (sub_of / info_of / ev_of), so one launch reads the first and
+// writes the second. The node counter's value before the level is carried in
+// rc (kRcNode0, then kRcChBase + kRcCh of the previous level), so no
+// workgroup reads a counter another one advances. Abort and overflow
+// semantics are the level loop's (rc[kRcAbort] = L + 1; the host-sized path
+// replays from there).
+
+// one wave: visit the list entries [64 j, 64 j + 64) of level L; appends the
+// internal nodes' children to next, the candidates, the subdividing leaves
+// to sub; then (do_win) splits each subdividing leaf (rc_win_leaf)
+__device__ __forceinline__ void rc_visit_chunk(int L, const int* __restrict__ work, int nw, int j, const MP& mp,
+                                               DevMap& m, int* __restrict__ next, int* __restrict__ sub,
+                                               int* __restrict__ cand, int* __restrict__ rc,
+                                               uint32_t* __restrict__ cand_bits, bool do_win,
+                                               const WinD* __restrict__ win, uint64_t* __restrict__ ev,
+                                               int* __restrict__ rcinfo, int cap) {
+  const int q = j * 64 + (threadIdx.x & 63);
+  const int node = q < nw ? work[q] : -1;
+  int kids[8], nchild, is_cand, is_sub;
+  recut_visit_node(node, mp, m, kids, nchild, is_cand, is_sub);
+  int o1, o2, o3;
+  wave_append3(&rc[kRcLvl + L], nchild, &m.counters[kCntFactors], is_cand, &rc[kRcSub + L], is_sub, o1, o2, o3);
+  for (int k = 0; k < nchild; k++) next[o1 + k] = kids[k];
+  if (is_cand) {
+    cand[o2] = node;
+    if (cand_bits) atomicOr(&cand_bits[node >> 5], 1u << (node & 31));  // k_fac_sort's id order
+  }
+  if (is_sub) sub[o3] = node;
+  if (!do_win) return;
+  uint64_t bs = __ballot(is_sub);
+  while (bs) {
+    const int l = __ffsll((unsigned long long)bs) - 1;
+    bs &= bs - 1;
+    rc_win_leaf(L, __shfl(node, l, 64), __shfl(o3, l, 64), win, m, ev, rcinfo, cap, cap, rc);
+  }
+}
+
+constexpr int kRcFusedWaves = 4;
+__global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level0(int thread_num, MP mp, DevMap m,
+                                                                  int* __restrict__ next, int* __restrict__ sub,
+                                                                  int* __restrict__ cand, int* __restrict__ rc,
+                                                                  uint32_t* __restrict__ cand_bits,
+                                                                  const WinD* __restrict__ win,
+                                                                  uint64_t* __restrict__ ev,
+                                                                  int* __restrict__ rcinfo, int cap) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) rc[kRcNode0] = m.counters[kCntNodes];  // k_rc_level(0)'s id base
+  if (rc[kRcAbort]) return;
+  if (g_slide(m) < thread_num) return;  // local_mapping.cpp:150-154 (global count)
+  const int nw = m.counters[kCntSlide];
+  const bool wide = win->win_count > 63;
+  if (wide && mp.max_layer > 0) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) atomicOr(&m.counters[kCntErr], 16);
+  }
+  const bool do_win = mp.max_layer > 0 && !wide;
+  const int nwv = gridDim.x * kRcFusedWaves;
+  for (int j = blockIdx.x * kRcFusedWaves + (threadIdx.x >> 6); j * 64 < nw; j += nwv)
+    rc_visit_chunk(0, m.slide, nw, j, mp, m, next, sub, cand, rc, cand_bits, do_win, win, ev, rcinfo, cap);
+}
+
+__global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level(
+    int L, int sub_cap, MP mp, DevMap m, const int* __restrict__ sub_in, const int* __restrict__ info_in,
+    const uint64_t* __restrict__ ev_in, int* __restrict__ next, int* __restrict__ next2, int* __restrict__ sub_out,
+    int* __restrict__ cand, int* __restrict__ rc, uint32_t* __restrict__ cand_bits, const WinD* __restrict__ win,
+    uint64_t* __restrict__ ev_out, int* __restrict__ info_out, int cap) {
+  __shared__ __attribute__((aligned(16))) int s_in[kApplySub];
+  __shared__ int s_sub[kApplySub], s_q[kApplySub], s_mask[kApplySub], s_coff[kApplySub];
+  __shared__ int s_ws[kRcFusedWaves];
+  __shared__ double E[kRcFusedWaves][64][kErec];
+  __shared__ int s_slot[kRcFusedWaves][64];
+  __shared__ double s_pre[kRcFusedWaves][32 * 9];
+  if (rc[kRcAbort]) return;
+  const int nsub = rc[kRcSub + L];
+  if (nsub > sub_cap) {  // the host-sized path replays from this level
+    if (blockIdx.x == 0 && threadIdx.x == 0) rc[kRcAbort] = L + 1;
+    return;
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ntot = rc[kRcNch + L];  // children of this level's subdividing leaves (rc_win_leaf)
+  const int A = rc[kRcLvl + L];     // level L+1's other nodes (visit(L))
+  const int base = (L == 0) ? rc[kRcNode0] : rc[kRcChBase + L - 1] + rc[kRcCh + L - 1];
+  if (blockIdx.x == 0 && tid == 0) {
+    rc[kRcCh + L] = ntot;
+    rc[kRcChBase + L] = base;
+    rc[kRcTot + L] = A + ntot;
+    m.counters[kCntNodes] = base + ntot;
+  }
+  const bool wide = win->win_count > 63;
+  const bool do_win = (L + 1 < mp.max_layer) && !wide;
+  if (wide && L + 1 < mp.max_layer && blockIdx.x == 0 && tid == 0) atomicOr(&m.counters[kCntErr], 16);
+  // every subdividing leaf becomes internal (alloc_parent's mark, sub_finish), children or not; the
+  // pushes below read only the parents' fix_off and geometry, which this leaves alone
+  for (int i = blockIdx.x * blockDim.x + tid; i < nsub; i += gridDim.x * blockDim.x) {
+    const int p = sub_in[i];
+    m.nscr[(size_t)p * 4 + 1] = -1;
+    sub_finish(m, p);
+  }
+  if ((int)blockIdx.x * kRcFusedWaves < ntot) {
+    // apply(L): the subdividing leaves in ascending id order (rank among distinct ids, from LDS)
+    for (int t = tid; t < kApplySub; t += blockDim.x) s_in[t] = t < nsub ? sub_in[t] : 0x7fffffff;
+    __syncthreads();
+    for (int t = tid; t < nsub; t += blockDim.x) {
+      const int myp = s_in[t];
+      int rank = 0;
+      const int4* v4 = reinterpret_cast<const int4*>(s_in);
+      for (int u = 0; u < (nsub + 3) / 4; u++) {
+        const int4 v = v4[u];
+        rank += (v.x < myp) + (v.y < myp) + (v.z < myp) + (v.w < myp);
       }
-      fix_off = __shfl(off, 0, 64);
-      if (fix_off < 0) continue;
+      s_sub[rank] = myp;
     }
-    // the child's run of each window slot (its events of phase 1 + ord are
-    // contiguous and in index order): lane p < win_count finds phase p + 1's
-    // range by binary search and takes the run from the slot's arena
-    int run_lo = 0, run_st = 0;
-    if (listed) {
-      const int wc = win->win_count;
-      if (lane < wc) {
-        const uint64_t base = 0;  // a child's events: phase << 21 | index, ascending
-        auto lower = [&](uint64_t key) {
-          int lo = j0, hi = j1;
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (keys[mid] < key) lo = mid + 1;
-            else hi = mid;
-          }
-          return lo;
-        };
-        run_lo = lower(base | ((uint64_t)(lane + 1) << 21));
-        const int cnt = lower(base | ((uint64_t)(lane + 2) << 21)) - run_lo;
-        if (cnt > 0) {
-          const int slot = win->mp[lane];
-          run_st = atomicAdd(&m.arena[slot], cnt);
-          if (run_st + cnt > m.ord_stride) {
-            atomicOr(&m.counters[kCntErr], 16);
-            run_st = 0;
-          } else {
-            m.lseg[(size_t)child * mp.W + slot] = lseg_pack(run_st, cnt, m.slot_epoch[slot]);
-          }
-        }
+    __syncthreads();
+    // per parent: its rcinfo slot and non-empty octants; exclusive prefix of their counts (4 per thread)
+    int c4[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int t = 4 * tid + k;
+      c4[k] = 0;
+      if (t < nsub) {
+        const int p = s_sub[t], q = m.nscr[(size_t)p * 4 + 0];
+        const int mk = info_in[(size_t)q * kRcInfo + 17];
+        s_q[t] = q;
+        s_mask[t] = mk;
+        c4[k] = __popc(mk);
       }
+      sum += c4[k];
     }
-    auto acc_ptr = [&](int r, int slot) -> double* {
-      if (r < 9) return r < 6 ? &m.pcr_add[child].P[r] : &m.pcr_add[child].v[r - 6];
-      if (r < 18) return r < 15 ? &m.pcr_fix[child].P[r - 9] : &m.pcr_fix[child].v[r - 15];
-      if (r < 63) return &m.cov_add[(size_t)child * kCovN + r - 18];
-      Clu& lc = m.pcrs[(size_t)child * mp.W + slot];
-      return r < 69 ? &lc.P[r - 63] : &lc.v[r - 69];
-    };
-    // every slot's frame cluster in one round of independent loads (a slot's
-    // run is contiguous, so each is read once, before this wave writes it):
-    // a cluster switch then costs an LDS read, not a dependent HBM load
-    for (int t = lane; t < mp.W * 9; t += 64) {
-      const Clu& lc = m.pcrs[(size_t)child * mp.W + t / 9];
-      const int q = t % 9;
-      s_pre[wv][t] = q < 6 ? lc.P[q] : lc.v[q - 6];
+    int x = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
     }
-    double a0 = r0 < 63 ? *acc_ptr(r0, 0) : 0.0, a1 = 0.0;
-    int cur_slot = -1, loc_n = 0, nwin = 0;
-    for (int b0 = j0; b0 < j1; b0 += 64) {
-      const int e = b0 + lane;
-      if (e < j1) {
-        const uint64_t k = keys[e];
-        const int phase = (int)((k >> 21) & 63), idx = (int)(k & ((1u << 21) - 1));
-        if (phase == 0) {
-          const size_t f = (size_t)ph.fix_off + idx;
-          const V3 pt = ld_v3(&m.fix_pnt[f * 3]);
-          const M3 var = ld_m3(&m.fix_var[f * 9]);
-          fill_record(E[wv][lane], pt, pt, var);
-          s_slot[wv][lane] = -1;
-          if (listed) {
-            const size_t d = (size_t)fix_off + (e - j0);
-            for (int t = 0; t < 3; t++) m.fix_pnt[d * 3 + t] = pt[t];
-            for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = var[t];
-          }
-        } else {
-          const int ord = phase - 1, slot = win->mp[ord];
-          const size_t bb = (size_t)slot * m.cap_wp + idx;
-          const V3 pnt = ld_v3(&m.wp_pnt[bb * 3]);
-          fill_record(E[wv][lane], pnt, rigid(ld_m3(win->R[ord]), pnt, ld_v3(win->p[ord])),
-                      ld_m3(&m.wp_var[bb * 9]));
-          s_slot[wv][lane] = slot;
-          m.wp_leaf[bb] = listed ? child : -1;
-        }
-      }
-      if (listed) {  // the point into the child's run (ds_bpermute of the run's lane; uniform call)
-        const int e = b0 + lane;
-        const int ph = e < j1 ? (int)((keys[e] >> 21) & 63) : 0;
-        const int src = ph > 0 ? ph - 1 : 0;
-        const int lo_p = __shfl(run_lo, src, 64), st_p = __shfl(run_st, src, 64);
-        if (ph > 0) m.wp_ord[(size_t)win->mp[ph - 1] * m.ord_stride + st_p + (e - lo_p)] = (int)(keys[e] & ((1u << 21) - 1));
-      }
-      const int nb = (j1 - b0) < 64 ? (j1 - b0) : 64;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll 4
-      for (int k = 0; k < nb; k++) {
-        const int slot = s_slot[wv][k];
-        const bool isfix = slot < 0;
-        if (!isfix && slot != cur_slot) {  // frame cluster switch (uniform)
-          if (cur_slot >= 0) {
-            if (r0 >= 63) *acc_ptr(r0, cur_slot) = a0;
-            if (has1) *acc_ptr(r1, cur_slot) = a1;
-            if (lane == 63) m.pcrs[(size_t)child * mp.W + cur_slot].N += loc_n;
-          }
-          cur_slot = slot;
-          if (r0 >= 63) a0 = s_pre[wv][cur_slot * 9 + r0 - 63];
-          if (has1) a1 = s_pre[wv][cur_slot * 9 + r1 - 63];
-          loc_n = 0;
-        }
-        const double* Ek = E[wv][k];
-        const bool use0 = r0 < 9 || (r0 >= 18 && r0 < 63) || (r0 < 18 ? isfix : !isfix);
-        const double i0 = role_inc(Ek, ri0);
-        if (use0) a0 += i0;
-        if (has1 && !isfix) a1 += role_inc(Ek, ri1);
-        if (!isfix) {
-          loc_n++;
-          nwin++;
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
+    if (lane == 63) s_ws[wv] = x;
+    __syncthreads();
+    int run = x - sum;
+    for (int k = 0; k < wv; k++) run += s_ws[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int t = 4 * tid + k;
+      if (t < nsub) s_coff[t] = run;
+      run += c4[k];
     }
-    if (r0 < 63) *acc_ptr(r0, 0) = a0;
-    if (cur_slot >= 0) {
-      if (r0 >= 63) *acc_ptr(r0, cur_slot) = a0;
-      if (has1) *acc_ptr(r1, cur_slot) = a1;
-      if (lane == 63) m.pcrs[(size_t)child * mp.W + cur_slot].N += loc_n;
-    }
-    if (lane == 0) {
-      m.pcr_add[child].N += j1 - j0;
-      m.pcr_fix[child].N += nfix;
-      if (nwin > 0) {
-        h.has_sw = 1;
-        h.isexist = 1;
+    __syncthreads();
+    const RoleIdx ri0 = rc_push_role(lane), ri1 = rc_push_role(lane + 64 < 72 ? lane + 64 : 0);
+    for (int c = blockIdx.x * kRcFusedWaves + wv; c < ntot; c += gridDim.x * kRcFusedWaves) {
+      int lo = 0, hi = nsub - 1;  // the parent: the last t with s_coff[t] <= c
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_coff[mid] <= c) lo = mid;
+        else hi = mid - 1;
       }
+      const int t = lo, p = s_sub[t], k = c - s_coff[t];
+      int mk = s_mask[t];
+      for (int i = 0; i < k; i++) mk &= mk - 1;
+      const int o = __ffs(mk) - 1;  // the parent's k-th non-empty octant
+      if (o < 0) continue;
+      const int* inf = info_in + (size_t)s_q[t] * kRcInfo;
+      const int j0 = inf[0] + inf[1 + o], j1 = j0 + inf[9 + o];
+      const int child = base + c;
+      if (child >= m.cap_nodes) {
+        if (lane == 0) atomicOr(&m.counters[kCntErr], 4);
+        continue;
+      }
+      NodeHdr& ph = m.hdr[p];
+      const int layer = ph.layer + 1;
+      if (lane == 0) {  // alloc_parent for this octant
+        const int xyz[3] = {(o >> 2) & 1, (o >> 1) & 1, o & 1};
+        double cc[3];
+        for (int jj = 0; jj < 3; jj++) cc[jj] = ph.center[jj] + (float)((2 * xyz[jj] - 1) * ph.qlen);
+        init_node(m.hdr[child], cc, ph.qlen / 2, layer, p);
+        dbox_child(m.dbox + (size_t)child * 6, m.dbox + (size_t)p * 6, ph.center, o);
+        ph.child[o] = child;
+        m.cfirst[(size_t)p * 8 + o] = 0x7f7f7f7f;
+        next[A + c] = child;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      rc_push_child(child, p, layer, j0, j1, ev_in, mp, win, m, E[wv], s_slot[wv], s_pre[wv], ri0, ri1);
+      // visit(L+1) of the new child (its cluster, counts and flags: this wave's stores just above)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      int kids[8], nchild, is_cand, is_sub;
+      recut_visit_node(lane == 0 ? child : -1, mp, m, kids, nchild, is_cand, is_sub);
+      int o1, o2, o3;
+      wave_append3(&rc[kRcLvl + L + 1], 0, &m.counters[kCntFactors], is_cand, &rc[kRcSub + L + 1], is_sub, o1, o2,
+                   o3);
+      if (is_cand) {
+        cand[o2] = child;
+        if (cand_bits) atomicOr(&cand_bits[child >> 5], 1u << (child & 31));
+      }
+      if (is_sub) sub_out[o3] = child;
+      if (do_win && __shfl(is_sub, 0, 64)) rc_win_leaf(L + 1, child, __shfl(o3, 0, 64), win, m, ev_out, info_out,
+                                                      cap, cap, rc);
     }
   }
+  // visit(L+1) (+ win(L+1)) of the level's other nodes, from the grid's last waves
+  const int nwv = gridDim.x * kRcFusedWaves;
+  for (int j = nwv - 1 - ((int)blockIdx.x * kRcFusedWaves + wv); j * 64 < A; j += nwv)
+    rc_visit_chunk(L + 1, next, A, j, mp, m, next2, sub_out, cand, rc, cand_bits, do_win, win, ev_out, info_out, cap);
 }
 
 // ---- host-sized path (overflow replay) ----------------------------------
@@ -1850,6 +2103,11 @@ __global__ void __launch_bounds__(256) k_factor_finish(int nf, const int* __rest
   }
 }
 
+// a recut level's subdividing leaves, rcinfo and events (alternate buffers per level)
+static int* sub_of(Work& w, int L) { return (L % 2 == 0) ? w.list2 : w.sub_odd; }
+static int* info_of(Work& w, int L) { return (L % 2 == 0) ? (int*)w.v1 : w.info_odd; }
+static uint64_t* ev_of(Work& w, int L) { return (L % 2 == 0) ? w.k0 : w.ev_odd; }
+
 static int read_rc(vg_ctx* ctx, int* h) {
   VG_HIP(hipMemcpyAsync(h, ctx->wk.rc, kRcN * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   return read_counters(ctx);  // synchronizes
@@ -1864,17 +2122,18 @@ static int recut_slow_apply(vg_ctx* ctx, int L, const MP& mp, WinD* dwin, int* n
   hipStream_t s = ctx->stream;
   const int nsub = hrc[kRcSub + L], nnext = hrc[kRcLvl + L];
   if (nsub <= 0) return VG_OK;
-  VG_TRY(sort_ids_inplace(ctx, w.list2, nsub));
+  int* sub = sub_of(w, L);
+  VG_TRY(sort_ids_inplace(ctx, sub, nsub));
   VG_TRY(read_counters(ctx));
   const int first = ctx->h_pinned[kCntNodes];
   int created = 0;
-  VG_TRY(alloc_children(ctx, w.list2, nsub, next, nnext, true, &created));
-  k_sub_cseg<<<grid_for(nsub), kBlock, 0, s>>>(nsub, w.list2, w.ac_off, m, (const int*)w.v1, (int*)w.ac_cnt);
+  VG_TRY(alloc_children(ctx, sub, nsub, next, nnext, true, &created));
+  k_sub_cseg<<<grid_for(nsub), kBlock, 0, s>>>(nsub, sub, w.ac_off, m, info_of(w, L), (int*)w.ac_cnt);
   VG_HIP(hipMemsetD32Async((hipDeviceptr_t)(w.rc + kRcLvl + L), nnext + created, 1, s));
   VG_HIP(hipMemsetD32Async((hipDeviceptr_t)(w.rc + kRcCh + L), created, 1, s));
   VG_HIP(hipMemsetD32Async((hipDeviceptr_t)(w.rc + kRcChBase + L), first, 1, s));
-  k_rc_push<<<256, 64 * kRcPushWaves, 0, s>>>(L, w.k0, (const int*)w.ac_cnt, mp, dwin, m, w.rc);
-  k_sub_finish<<<grid_for(nsub), kBlock, 0, s>>>(nsub, w.list2, m);
+  k_rc_push<<<256, 64 * kRcPushWaves, 0, s>>>(L, ev_of(w, L), (const int*)w.ac_cnt, mp, dwin, m, w.rc);
+  k_sub_finish<<<grid_for(nsub), kBlock, 0, s>>>(nsub, sub, m);
   VG_HIP(hipGetLastError());
   return read_counters(ctx);
 }
@@ -1963,6 +2222,61 @@ __global__ void __launch_bounds__(256) k_factor_finish_dev(const int* __restrict
   }
 }
 const int* map_rc_status(vg_ctx* ctx) { return ctx->wk.rc + kRcStatus; }
+
+// Test-only (vgx_memo_probe): the IEKF memo at centre planes. For every
+// internal node, points exactly on its centre plane along each axis (the
+// other two coordinates at +-hl/2) are looked up afresh (hash + descent, the
+// reference's path: voxel_map.cpp:241-266, octree.cpp:586) and through the
+// memo of the same point one ulp above / below the plane (the previous
+// iteration's leaf). out: [0] samples, [1] memo != descent with the
+// inclusive box (OctoTree::inside), [2] memo != descent with the descent's
+// region (dbox, what k_iekf uses), [3] samples whose memo leaf differs from
+// the fresh one (the plane really separates two leaves).
+__global__ void __launch_bounds__(256) k_memo_probe(MP mp, DevMap m, int* __restrict__ out) {
+  const int nn = m.counters[kCntNodes];
+  int cnt[4] = {0, 0, 0, 0};
+  for (int node = blockIdx.x * blockDim.x + threadIdx.x; node < nn; node += gridDim.x * blockDim.x) {
+    const NodeHdr& h = m.hdr[node];
+    if (h.octo != 1) continue;
+    const double hl = h.qlen * 2;
+    for (int j = 0; j < 3; j++)
+      for (int sgn = 0; sgn < 4; sgn++)
+        for (int side = 0; side < 2; side++) {
+          V3 w = v3(h.center[0], h.center[1], h.center[2]);
+          int k1 = (j + 1) % 3, k2 = (j + 2) % 3;
+          w[k1] += ((sgn & 1) ? 0.5 : -0.5) * hl;
+          w[k2] += ((sgn & 2) ? 0.5 : -0.5) * hl;
+          V3 w2 = w;
+          w2[j] = nextafter(w[j], side ? 1e300 : -1e300);
+          uint64_t key, key2;
+          if (!pack_key(w, mp.vs, key) || !pack_key(w2, mp.vs, key2) || key != key2) continue;
+          const int root = hash_find(m.hkey, m.hval, m.hash_mask, key);
+          if (root < 0) continue;
+          const int fresh = descend(m.hdr, root, w), memo = descend(m.hdr, root, w2);
+          if (fresh < 0 || memo < 0) continue;
+          uint64_t kl;
+          const NodeHdr& hm = m.hdr[memo];
+          const bool same_root = pack_key(v3(hm.center[0], hm.center[1], hm.center[2]), mp.vs, kl) && kl == key;
+          const int p_old = (same_root && inside(hm, w)) ? memo : fresh;
+          const int p_new = (same_root && in_dbox(m.dbox + (size_t)memo * 6, w)) ? memo : fresh;
+          cnt[0]++;
+          cnt[1] += p_old != fresh;
+          cnt[2] += p_new != fresh;
+          cnt[3] += memo != fresh;
+        }
+  }
+  for (int k = 0; k < 4; k++)
+    if (cnt[k]) atomicAdd(&out[k], cnt[k]);
+}
+int map_memo_probe(vg_ctx* ctx, const MP& mp, int* out) {
+  int* dout = reinterpret_cast<int*>(ctx->wk.partials);  // scratch: the probe runs between scans
+  VG_HIP(hipMemsetAsync(dout, 0, 4 * sizeof(int), ctx->stream));
+  k_memo_probe<<<256, 256, 0, ctx->stream>>>(mp, ctx->map, dout);
+  VG_HIP(hipGetLastError());
+  VG_HIP(hipMemcpyAsync(out, dout, 4 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  VG_HIP(hipStreamSynchronize(ctx->stream));
+  return VG_OK;
+}
 int map_set_attrs(vg_ctx* ctx) {
   (void)ctx;
   return VG_OK;
@@ -1989,9 +2303,9 @@ static int recut_complete(vg_ctx* ctx, const MP& mp, int nlev, int* hrc, int* n_
     int* dslot = dn + 32;
     const int total = ctx->rc_total;
     for (int L = L0 + 1; L < nlev; L++) {
-      k_rc_visit<<<256 * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(L, ctx->rc_thread_num, list_of(L), mp, m, list_of(L + 1), w.list2, w.cand,
+      k_rc_visit<<<256 * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(L, ctx->rc_thread_num, list_of(L), mp, m, list_of(L + 1), sub_of(w, L), w.cand,
                                         w.rc, nullptr);
-      k_rc_win<<<256, 64 * kRcWinWaves, 0, s>>>(L, w.list2, dwin, m, w.k0, (int*)w.v1, w.cap, w.cap, w.rc);
+      k_rc_win<<<256, 64 * kRcWinWaves, 0, s>>>(L, sub_of(w, L), dwin, m, ev_of(w, L), info_of(w, L), w.cap, w.cap, w.rc);
       VG_TRY(read_rc(ctx, hrc));
       VG_TRY(recut_slow_apply(ctx, L, mp, dwin, list_of(L + 1), hrc));
     }
@@ -2037,7 +2351,7 @@ static int map_recut_impl(vg_ctx* ctx, const MP& mp, const WinArg& wa, int threa
   k_make_win_recut_begin<<<1, 256, 0, s>>>(ctx->st, wa, ctx->map.wpn, dwin, dn, dslot, m, w.rc, thread_num);
   if (m.shard_world > 1) {
     if (!replay) {  // the global slide count (a replay re-uses it: the insert replay does not change it)
-      VG_TRY(shard_allreduce(ctx, m.counters + kCntGSlide, ctx->shard.d_buf + 512, 1, 1));
+      VG_TRY(shard_allreduce(ctx, m.counters + kCntGSlide, ctx->shard.d_buf + 512, 1, 1, 2));
     }
     k_copy_int<<<1, 64, 0, s>>>((const int*)(ctx->shard.d_buf + 512), m.counters + kCntGSlide);
   }
@@ -2045,16 +2359,27 @@ static int map_recut_impl(vg_ctx* ctx, const MP& mp, const WinArg& wa, int threa
   auto list_of = [&](int L) { return (L % 2 == 1) ? w.list0 : w.list1; };  // worklist of level L >= 1
   const int gv = 256, gw = grid_for(total > 0 ? total : 1, kBlock, 2048);  // grid-stride over the device total
   const int sub_cap = (ctx->dbg_apply_cap >= 0 && ctx->dbg_apply_cap < kApplySub) ? ctx->dbg_apply_cap : kApplySub;
-  for (int L = 0; L < nlev; L++) {
-    k_rc_visit<<<gv * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(L, thread_num, L > 0 ? list_of(L) : nullptr, mp, m, list_of(L + 1), w.list2,
-                                     w.cand, w.rc, pub_seq > 0 ? w.cand_bits : nullptr);
-    // nodes at layer max_layer never subdivide (recut_visit_node, octree.cpp:371-372):
-    // the deepest level has no window events, no apply and no pushes
-    if (L == mp.max_layer) break;
-    k_rc_win<<<256, 64 * kRcWinWaves, 0, s>>>(L, w.list2, dwin, m, w.k0, (int*)w.v1, w.cap, w.cap, w.rc);
-    k_rc_apply<<<1, kApplyThreads, 0, s>>>(L, sub_cap, m, list_of(L + 1), w.list2, (const int*)w.v1, (int*)w.ac_off,
-                                           w.rc);
-    k_rc_push<<<64, 64 * kRcPushWaves, 0, s>>>(L, w.k0, (const int*)w.ac_off, mp, dwin, m, w.rc);
+  uint32_t* bits = pub_seq > 0 ? w.cand_bits : nullptr;
+  if (ctx->rc_fused) {  // one launch per level boundary (k_rc_level0, k_rc_level)
+    k_rc_level0<<<gv, 64 * kRcFusedWaves, 0, s>>>(thread_num, mp, m, list_of(1), sub_of(w, 0), w.cand, w.rc, bits,
+                                                 dwin, ev_of(w, 0), info_of(w, 0), w.cap);
+    for (int L = 0; L < mp.max_layer; L++)
+      k_rc_level<<<gv, 64 * kRcFusedWaves, 0, s>>>(L, sub_cap, mp, m, sub_of(w, L), info_of(w, L), ev_of(w, L),
+                                                  list_of(L + 1), list_of(L + 2), sub_of(w, L + 1), w.cand, w.rc,
+                                                  bits, dwin, ev_of(w, L + 1), info_of(w, L + 1), w.cap);
+  } else {
+    for (int L = 0; L < nlev; L++) {
+      k_rc_visit<<<gv * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(L, thread_num, L > 0 ? list_of(L) : nullptr, mp, m,
+                                                                     list_of(L + 1), sub_of(w, L), w.cand, w.rc, bits);
+      // nodes at layer max_layer never subdivide (recut_visit_node, octree.cpp:371-372):
+      // the deepest level has no window events, no apply and no pushes
+      if (L == mp.max_layer) break;
+      k_rc_win<<<256, 64 * kRcWinWaves, 0, s>>>(L, sub_of(w, L), dwin, m, ev_of(w, L), info_of(w, L), w.cap, w.cap,
+                                                w.rc);
+      k_rc_apply<<<1, kApplyThreads, 0, s>>>(L, sub_cap, m, list_of(L + 1), sub_of(w, L), info_of(w, L),
+                                             (int*)w.ac_off, w.rc);
+      k_rc_push<<<64, 64 * kRcPushWaves, 0, s>>>(L, ev_of(w, L), (const int*)w.ac_off, mp, dwin, m, w.rc);
+    }
   }
   VG_HIP(hipGetLastError());
   if (pub_seq > 0) {

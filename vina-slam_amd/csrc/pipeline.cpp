@@ -86,7 +86,9 @@ void host_reset(vg_ctx* ctx) {
 static int map_error(vg_ctx* ctx, int e) {
   ctx->err = std::string("device map error flags=") + std::to_string(e) + ((e & 4) ? " (node pool full)" : "") +
              ((e & 8) ? " (point_fix arena full)" : "") + ((e & 1) ? " (voxel key out of packed range)" : "") +
-             ((e & 2) ? " (root hash full)" : "") + ((e & 16) ? " (subdivision event buffer full)" : "");
+             ((e & 2) ? " (root hash full)" : "") + ((e & 16) ? " (subdivision event buffer full)" : "") +
+             ((e & 32) ? " (sharded exchange out of step: the ranks' exchange sequences differ)" : "");
+  if (e & 32) return VG_E_STATE;
   return (e & 1) ? VG_E_RANGE : VG_E_CAPACITY;
 }
 
@@ -862,6 +864,7 @@ int stage_finish(vg_ctx* ctx) {
 }
 
 int host_win_count(vg_ctx* ctx) { return hp(ctx)->win_count; }
+int host_memo_probe(vg_ctx* ctx, int* out) { return map_memo_probe(ctx, hp(ctx)->mpd, out); }
 
 // IMUEKF::motion_blur's per-point deskew (imu_ekf.cpp:114-144), SURVEY row
 // f1: after the propagation (which recorded the IMU poses), the scan is moved

@@ -333,6 +333,29 @@ __device__ __forceinline__ M<9, 9> unpack9(const double* cov) {
   return m;
 }
 
+// The region the correspondence descent (octant(): w > centre takes the upper
+// child, octree.cpp:586) assigns to a node: lo < w <= hi per axis, the bounds
+// being ancestors' centres (roots unbounded: their membership is the float
+// voxel key). The IEKF's memo of an unmatched point's leaf is valid exactly
+// while the point stays in it (k_iekf); OctoTree::inside's inclusive box
+// (octree.cpp:732-737) is the test for the reference's own octos[i] only.
+__device__ __forceinline__ void dbox_root(double* b) {
+  for (int j = 0; j < 3; j++) {
+    b[j] = -__builtin_huge_val();
+    b[3 + j] = __builtin_huge_val();
+  }
+}
+__device__ __forceinline__ void dbox_child(double* b, const double* pb, const double* pc, int o) {
+  for (int j = 0; j < 3; j++) {
+    const bool up = (o >> (2 - j)) & 1;
+    b[j] = up ? pc[j] : pb[j];
+    b[3 + j] = up ? pb[3 + j] : pc[j];
+  }
+}
+__device__ __forceinline__ bool in_dbox(const double* b, const V3& w) {
+  return w[0] > b[0] && w[0] <= b[3] && w[1] > b[1] && w[1] <= b[4] && w[2] > b[2] && w[2] <= b[5];
+}
+
 __device__ __forceinline__ void init_node(NodeHdr& h, const double c[3], float qlen, int layer, int parent) {
   for (int j = 0; j < 3; j++) h.center[j] = c[j];
   for (int j = 0; j < 8; j++) h.child[j] = -1;

@@ -140,6 +140,7 @@ struct DevMap {
   double* cov_add = nullptr;   // cap_nodes * 45
   double* eig = nullptr;       // cap_nodes * 12 (eig_value 3, eig_vector 9 row-major)
   double* jour = nullptr;
+  double* dbox = nullptr;      // cap_nodes * 6: the descent's region per node (lo[3] exclusive, hi[3] inclusive; vg_dev.h dbox_*)
   Clu* pcrs = nullptr;         // cap_nodes * W (SlideWindow::pcrs_local, physical slot)
   int* nscr = nullptr;         // per-node scratch (cap_nodes * 4)
   int* cfirst = nullptr;       // per-node per-octant first-event scratch (cap_nodes * 8)
@@ -199,6 +200,10 @@ struct Work {
   int* rc = nullptr;           // device-side level counts (recut / margi, map.hip kRc*)
   uint32_t* cand_bits = nullptr;  // factor candidates of an asynchronous recut, one bit per node id
   int* plan = nullptr;         // per-leaf point_fix copy plan (margi)
+  // the recut's odd levels: subdividing leaves, rcinfo, events (even levels: list2, v1, k0)
+  int* sub_odd = nullptr;
+  int* info_odd = nullptr;
+  uint64_t* ev_odd = nullptr;
   int nparts = 0;
 };
 
@@ -282,6 +287,9 @@ struct Shard {
   void* user = nullptr;
   double* h_buf = nullptr;   // pinned staging (host mode)
   double* d_buf = nullptr;   // device scratch for the exchanged sums (4096 doubles)
+  int frame_n = 0;           // doubles per exchange (shard.hip: payload + guard pair)
+  double* d_frame = nullptr; // the exchange frame (+ this rank's guard value)
+  unsigned* d_seq = nullptr; // the device's count of exchanges (the guard's sequence number)
 };
 
 // Host-mapped publication block (written by the device with system-scope
@@ -400,6 +408,7 @@ struct vg_ctx {
   long prof_runs = 0;
   int rc_total = 0, rc_thread_num = 0;  // the last recut's window point total / thread_num (its resume)
   bool prof_stages = false;  // per-stage events (vg_profile bit 1)
+  bool rc_fused = true;      // the fused recut levels (vgx_debug 11: 0 = the four-launch level loop)
   bool prof_clock = false;   // in-kernel clocks instead of k_ba_solve events (vg_profile bit 2, KClock)
   hipEvent_t prof_ev[8][2] = {};
   hipEvent_t sync_ev = nullptr;  // host-spin synchronisation (vg::stream_wait)
@@ -588,6 +597,7 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* 
 int map_recut_resume(vg_ctx* ctx, const MP& mp, int* n_factors);
 int map_set_attrs(vg_ctx* ctx);
 const int* map_rc_status(vg_ctx* ctx);  // the asynchronous recut's status word (k_fac_sort)
+int map_memo_probe(vg_ctx* ctx, const MP& mp, int* out);  // test-only (vgx_memo_probe)
 // multi_margi + the device-state slide; publishes the state (pub_seq, before
 // the margi kernels) and the end-of-scan counters (pub_seq2)
 int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, double jour);
@@ -649,10 +659,11 @@ int host_poll(vg_ctx* ctx);
 int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di, int n, double beg,
               double end, const double* imu, int m);
 int host_win_count(vg_ctx* ctx);
+int host_memo_probe(vg_ctx* ctx, int* out);  // map_memo_probe with the context's map parameters
 // shard.cpp
 int shard_alloc(vg_ctx* ctx);
 void shard_free(vg_ctx* ctx);
-int shard_allreduce(vg_ctx* ctx, const void* send, void* recv, int count, int dtype);
+int shard_allreduce(vg_ctx* ctx, const void* send, void* recv, int count, int dtype, int site);
 int host_sync(vg_ctx* ctx);
 int host_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* valid, int* iters);
 int decode_scan(vg_ctx* ctx, const void* records, int n, const vg_lidar_format* fmt, float* xyz, float* inten,

@@ -786,6 +786,18 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     ctx->dbg_fac_max = value;
     return VG_OK;
   }
+  if (key == 12) {  // sharded: add `value` to this context's exchange counter (desynchronises the guard)
+    if (!ctx->shard.d_seq) return VG_E_STATE;
+    unsigned s = 0;
+    VG_HIP(hipMemcpy(&s, ctx->shard.d_seq, sizeof(s), hipMemcpyDeviceToHost));
+    s += (unsigned)value;
+    VG_HIP(hipMemcpy(ctx->shard.d_seq, &s, sizeof(s), hipMemcpyHostToDevice));
+    return VG_OK;
+  }
+  if (key == 11) {  // 0: the recut's four-launch level loop instead of the fused levels
+    ctx->rc_fused = value != 0;
+    return VG_OK;
+  }
   if (key == 7) {  // 0: the IEKF waits for the whole margi (no cross-scan overlap)
     ctx->overlap_iekf = value != 0;
     return VG_OK;
@@ -806,6 +818,15 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     return VG_OK;
   }
   return VG_E_ARG;
+}
+
+// Test-only: the IEKF memo against fresh descents at internal nodes' centre
+// planes (map.hip k_memo_probe); out[4]: samples, mismatches of the inclusive
+// box, mismatches of the descent region k_iekf uses, samples split by the plane
+extern "C" int vgx_memo_probe(vg_ctx* ctx, int* out) {
+  if (!ctx || !out) return VG_E_ARG;
+  VG_TRY(host_sync(ctx));
+  return host_memo_probe(ctx, out);
 }
 
 // Test-only: the per-scan pipeline's hashed downsample (ds_enqueue_hashed,

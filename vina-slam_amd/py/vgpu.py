@@ -168,6 +168,8 @@ def lib():
         L.vgx_ba_capture.argtypes = [P, dp, ctypes.c_int, ip]
         if hasattr(L, "vgx_ba_solve"):  # absent from builds older than the test entry (A/B runs)
             L.vgx_ba_solve.argtypes = [P, dp, dp, dp]
+        if hasattr(L, "vgx_memo_probe"):
+            L.vgx_memo_probe.argtypes = [P, ip]
         _lib = L
     return _lib
 
@@ -463,6 +465,14 @@ class Context:
     # ---- test-only knobs (vgx_*, not part of include/vina_gpu.h)
     def debug(self, key, value):
         self._chk(lib().vgx_debug(self.h, key, value), "vgx_debug")
+
+    def memo_probe(self):
+        """The IEKF memo at internal nodes' centre planes (vgx_memo_probe):
+        samples, mismatches of OctoTree::inside's box, mismatches of the descent
+        region k_iekf uses, samples whose plane separates two leaves."""
+        out = np.zeros(4, np.int32)
+        self._chk(lib().vgx_memo_probe(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int))), "vgx_memo_probe")
+        return [int(v) for v in out]
 
     def capture_arm(self):
         """Capture the next LM run's first Hessian pass (vgx_debug 5)."""
