@@ -480,9 +480,10 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
 // node without the per-launch dispatch gap. The per-stage profiling pass
 // (vg_profile bit 1) launches directly, with an event pair around each k_iekf.
 int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank,
-             const double* begin_xc, hipStream_t s) {
+             const double* begin_xc, hipStream_t s, const PropArg* begin_prop) {
   if (!s) s = ctx->stream;
-  if (begin_xc) VG_TRY(state_scan_begin(ctx, begin_xc, x, y, z, n, s));  // the scan opens here (pipeline.cpp)
+  if (begin_xc || begin_prop)  // the scan opens here (pipeline.cpp)
+    VG_TRY(state_scan_begin(ctx, begin_xc, x, y, z, n, s, begin_prop));
   else VG_TRY(state_set_scan(ctx, x, y, z, n, s));
   const bool graph = ctx->use_graphs && ctx->shard.world <= 1 && !ctx->prof_stages;
   const bool ev = ctx->prof_on && !graph;

@@ -27,7 +27,8 @@ namespace vg {
 static int flush_begin(vg_ctx* ctx, HostPipe* P) {
   if (!P->begin_pending) return VG_OK;
   P->begin_pending = false;
-  return state_scan_begin(ctx, P->begin_xc);
+  return P->begin_prop ? state_scan_begin(ctx, nullptr, nullptr, nullptr, nullptr, 0, nullptr, &P->prop)
+                       : state_scan_begin(ctx, P->begin_xc);
 }
 static int flush_deferred(vg_ctx* ctx, HostPipe* P) {
   VG_TRY(flush_begin(ctx, P));
@@ -384,14 +385,16 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   const bool split = ctx->tail_a_valid && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages &&
                      ctx->shard.world == 1;
   ctx->tail_a_valid = false;
-  if (!split) return iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, begin ? P->begin_xc : nullptr);
+  const double* bxc = begin && !P->begin_prop ? P->begin_xc : nullptr;
+  const PropArg* bprop = begin && P->begin_prop ? &P->prop : nullptr;
+  if (!split) return iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, bxc, nullptr, bprop);
   // created on first use: a context of the multi-sequence mode never makes
   // it (vg_multi_create), as a third stream per sequence makes sequences
   // share hardware queues (B = 4: 2,742 -> 1,430 scans/s)
   if (!ctx->stream_iekf) VG_HIP(hipStreamCreateWithFlags(&ctx->stream_iekf, hipStreamNonBlocking));
   VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->ev_tail_a, 0));
   if (ctx->in_ev) VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->in_ev, 0));  // a host-input scan's unpack
-  VG_TRY(iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, begin ? P->begin_xc : nullptr, ctx->stream_iekf));
+  VG_TRY(iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, bxc, ctx->stream_iekf, bprop));
   VG_HIP(hipEventRecord(ctx->ev_iekf_done, ctx->stream_iekf));
   VG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_iekf_done, 0));
   return VG_OK;
@@ -420,7 +423,7 @@ static int need_open(vg_ctx* ctx, HostPipe* P, const char* what) {
 
 // odom_ekf.process -> motion_blur state/covariance part (local_mapping.cpp:389);
 // opens the scan on the device (x_curr, x_prop, cov_inv)
-int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double end) {
+int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double end, bool dev) {
   HostTimer ht_(ctx, kHostPropagate);
   HostPipe* P = hp(ctx);
   if (P->in_scan) {
@@ -431,23 +434,45 @@ int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double en
     ctx->err = "vg_propagate: cold-start initialisation in progress (use vg_step* until init_phase 3)";
     return VG_E_STATE;
   }
-  VG_TRY(absorb(ctx, P, false));  // x_curr / x_buf of the previous scan
-  P->poses.clear();
-  if (!P->first) {
-    propagate(ctx, P, to_imus(imu, m), beg, end);
-  } else {
+  // device propagation (k_scan_prop): from the device's x_curr, so the host
+  // does not wait for the previous scan's state here (the window push absorbs
+  // it, behind the IEKF's enqueue); the first scan has nothing to propagate
+  P->begin_prop = dev && ctx->dev_prop && !P->first && m <= kPropMax && P->sticky == VG_OK;
+  if (P->begin_prop) {
+    PropArg& a = P->prop;
+    const vg_config& c = ctx->cfg;
+    a.n = m;
+    a.last_end = P->last_pcl_end_time;
+    a.beg = beg;
+    a.end = end;
+    a.sg = P->sg;
+    a.cov_gyr = c.odo_cov_gyr;
+    a.cov_acc = c.odo_cov_acc;
+    a.rdw_gyr = c.odo_rdw_gyr;
+    a.rdw_acc = c.odo_rdw_acc;
+    if (m > 0) memcpy(a.imu, imu, (size_t)m * 7 * sizeof(double));
+    P->poses.clear();
     P->x_curr.t = end;
     P->last_pcl_end_time = end;
+  } else {
+    VG_TRY(absorb(ctx, P, false));  // x_curr / x_buf of the previous scan
+    P->poses.clear();
+    if (!P->first) {
+      propagate(ctx, P, to_imus(imu, m), beg, end);
+    } else {
+      P->x_curr.t = end;
+      P->last_pcl_end_time = end;
+    }
+    double* xc = P->begin_xc;  // opened on the device with the IEKF's first launch (flush_begin otherwise)
+    const HX& h = P->x_curr;
+    memcpy(xc, h.R.a, 72);
+    memcpy(xc + 9, h.p.a, 24);
+    memcpy(xc + 12, h.v.a, 24);
+    memcpy(xc + 15, h.bg.a, 24);
+    memcpy(xc + 18, h.ba.a, 24);
+    memcpy(xc + 21, h.g.a, 24);
+    memcpy(xc + kXS, h.cov.a, 225 * sizeof(double));
   }
-  double* xc = P->begin_xc;  // opened on the device with the IEKF's first launch (flush_begin otherwise)
-  const HX& h = P->x_curr;
-  memcpy(xc, h.R.a, 72);
-  memcpy(xc + 9, h.p.a, 24);
-  memcpy(xc + 12, h.v.a, 24);
-  memcpy(xc + 15, h.bg.a, 24);
-  memcpy(xc + 18, h.ba.a, 24);
-  memcpy(xc + 21, h.g.a, 24);
-  memcpy(xc + kXS, h.cov.a, 225 * sizeof(double));
   P->begin_pending = true;
   P->push_pending = false;
   P->cur = Pend();
@@ -552,6 +577,9 @@ int stage_window_push(vg_ctx* ctx, const double* imu, int m) {
   HostTimer ht_(ctx, kHostPush);
   HostPipe* P = hp(ctx);
   VG_TRY(need_open(ctx, P, "vg_window_push"));
+  // the previous scan's window after its BA (the IMU_PRE bias below); already
+  // absorbed unless this scan propagated on the device
+  VG_TRY(absorb(ctx, P, false));
   if (P->win_count >= 32) {
     ctx->err = "vg_window_push: window full";
     return VG_E_STATE;
@@ -945,7 +973,7 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
     HostTimer ht_(ctx, kHostDownsample);
     VG_TRY(ds_enqueue_scan(ctx, dx, dy, dz, di, n, 0));
   }
-  VG_TRY(stage_propagate(ctx, imu, m, beg, end));
+  VG_TRY(stage_propagate(ctx, imu, m, beg, end, true));
   host_delay(0);
   VG_TRY(stage_iekf(ctx, dx, dy, dz, n, nullptr));
   host_delay(4);

@@ -58,6 +58,176 @@ __global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict
   }
 }
 
+// IMUEKF::process's state / covariance propagation (imu_ekf.cpp:13-86, the
+// host's propagate() in pipeline.cpp, same expression trees) from the device's
+// x_curr, then the scan opening (k_scan_begin). One workgroup: the per-sample
+// rotations (Exp, the sin / cos) in parallel, the rotation / velocity /
+// position chain on thread 0, the F / noise blocks of each sample in
+// parallel, then cov <- F cov F^T + Q sample by sample, one lane per entry,
+// each sum in ascending column order over F's non-zeros (the host's
+// sandwich()).
+__global__ void __launch_bounds__(256) k_scan_prop(PropArg a, DState* __restrict__ st, const float* x, const float* y,
+                                                   const float* z, int n, int set_scan) {
+  __shared__ double sExp[kPropMax][9], sF00[kPropMax][9], sRi[kPropMax][9], sAsk[kPropMax][9];
+  __shared__ double sF60[kPropMax][9], sF612[kPropMax][9], sCw[kPropMax][9], sDt[kPropMax];
+  __shared__ int sOk[kPropMax];
+  __shared__ double C[225], A[225];
+  const int tid = threadIdx.x;
+  const double* xc = st->xc;
+  const V3 bg = v3(xc[15], xc[16], xc[17]), ba = v3(xc[18], xc[19], xc[20]);
+  const int ns = a.n > 1 ? a.n - 1 : 0;  // sample pairs
+  // 1. per pair: skip rule, angvel, acc_avr, dt, Exp(angvel, dt), F00 = Exp(angvel, -dt), hat(acc_avr)
+  if (tid < ns) {
+    const double* h = &a.imu[7 * tid];
+    const double* t = &a.imu[7 * (tid + 1)];
+    const bool ok = !(h[0] < a.last_end);
+    V3 angvel, acc_avr;
+    for (int j = 0; j < 3; j++) {
+      angvel[j] = 0.5 * (h[1 + j] + t[1 + j]);
+      acc_avr[j] = 0.5 * (h[4 + j] + t[4 + j]);
+    }
+    angvel = sub(angvel, bg);
+    acc_avr = sub(scl(acc_avr, a.sg), ba);
+    double cur = h[0];
+    if (cur < a.last_end) cur = a.last_end;
+    const double dt = t[0] - cur;
+    const M3 e = Exp(angvel, dt), f = Exp(angvel, -dt), k = hat(acc_avr);
+    for (int q = 0; q < 9; q++) {
+      sExp[tid][q] = e[q];
+      sF00[tid][q] = f[q];
+      sAsk[tid][q] = k[q];
+    }
+    sDt[tid] = dt;
+    sOk[tid] = ok ? 1 : 0;
+  }
+  __syncthreads();
+  // 2. the rotation / velocity / position chain (thread 0), the final pose
+  if (tid == 0) {
+    M3 R_imu = ld_m3(xc);
+    V3 vel = v3(xc[12], xc[13], xc[14]), pos = v3(xc[9], xc[10], xc[11]);
+    const V3 g = v3(xc[21], xc[22], xc[23]);
+    V3 acc_imu = V3::Z(), angvel = V3::Z();
+    for (int k = 0; k < ns; k++) {
+      if (!sOk[k]) continue;
+      const double* h = &a.imu[7 * k];
+      const double* t = &a.imu[7 * (k + 1)];
+      V3 av, acc_avr;
+      for (int j = 0; j < 3; j++) {
+        av[j] = 0.5 * (h[1 + j] + t[1 + j]);
+        acc_avr[j] = 0.5 * (h[4 + j] + t[4 + j]);
+      }
+      angvel = sub(av, bg);
+      acc_avr = sub(scl(acc_avr, a.sg), ba);
+      acc_imu = add(mul(R_imu, acc_avr), g);
+      for (int q = 0; q < 9; q++) sRi[k][q] = R_imu[q];
+      const double dt = sDt[k];
+      pos = add(add(pos, scl(vel, dt)), scl(acc_imu, 0.5 * dt * dt));
+      vel = add(vel, scl(acc_imu, dt));
+      R_imu = mul(R_imu, ld_m3(sExp[k]));
+    }
+    if (a.n > 0) {  // imu_ekf.cpp:81-86
+      const double tb = a.imu[7 * (a.n - 1)];
+      const double note = a.end > tb ? 1.0 : -1.0;
+      const double dt = note * (a.end - tb);
+      const V3 v = add(vel, scl(acc_imu, note * dt));
+      const M3 R = mul(R_imu, Exp(scl(angvel, note), dt));
+      const V3 p = add(add(pos, scl(vel, note * dt)), scl(acc_imu, note * 0.5 * dt * dt));
+      for (int q = 0; q < 9; q++) st->xc[q] = R[q];
+      for (int j = 0; j < 3; j++) {
+        st->xc[9 + j] = p[j];
+        st->xc[12 + j] = v[j];
+      }
+    }
+  }
+  __syncthreads();
+  // 3. per pair: F60, F612 and the acceleration noise block
+  if (tid < ns && sOk[tid]) {
+    const M3 Ri = ld_m3(sRi[tid]);
+    const double dt = sDt[tid];
+    M3 ca = M3::Z();
+    for (int j = 0; j < 3; j++) ca(j, j) = a.cov_acc;
+    const M3 f60 = scl(mul(Ri, ld_m3(sAsk[tid])), -dt), f612 = scl(Ri, -dt);
+    const M3 cw = scl(mul(mul(Ri, ca), tr(Ri)), dt * dt);
+    for (int q = 0; q < 9; q++) {
+      sF60[tid][q] = f60[q];
+      sF612[tid][q] = f612[q];
+      sCw[tid][q] = cw[q];
+    }
+  }
+  const int r = tid / 15, c = tid % 15;
+  if (tid < 225) C[tid] = xc[kXS + tid];
+  __syncthreads();
+  // 4. cov = F cov F^T + Q per pair, F's non-zero columns ascending (sandwich())
+  auto frow = [&](int k, int i, int* kk, double* vv) -> int {
+    const double dt = sDt[k];
+    if (i < 3) {
+      kk[0] = 0, kk[1] = 1, kk[2] = 2, kk[3] = 9 + i;
+      vv[0] = sF00[k][i * 3], vv[1] = sF00[k][i * 3 + 1], vv[2] = sF00[k][i * 3 + 2], vv[3] = -dt;
+      return 4;
+    }
+    if (i < 6) {
+      kk[0] = i, kk[1] = i + 3;
+      vv[0] = 1.0, vv[1] = dt;
+      return 2;
+    }
+    if (i < 9) {
+      const int q = i - 6;
+      kk[0] = 0, kk[1] = 1, kk[2] = 2, kk[3] = i, kk[4] = 12, kk[5] = 13, kk[6] = 14;
+      vv[0] = sF60[k][q * 3], vv[1] = sF60[k][q * 3 + 1], vv[2] = sF60[k][q * 3 + 2], vv[3] = 1.0;
+      vv[4] = sF612[k][q * 3], vv[5] = sF612[k][q * 3 + 1], vv[6] = sF612[k][q * 3 + 2];
+      return 7;
+    }
+    kk[0] = i;
+    vv[0] = 1.0;
+    return 1;
+  };
+  for (int k = 0; k < ns; k++) {
+    if (!sOk[k]) continue;  // uniform
+    int kk[7];
+    double vv[7];
+    if (tid < 225) {  // A = F C
+      const int nn = frow(k, r, kk, vv);
+      double s = vv[0] * C[kk[0] * 15 + c];
+      for (int t = 1; t < nn; t++) s += vv[t] * C[kk[t] * 15 + c];
+      A[tid] = s;
+    }
+    __syncthreads();
+    if (tid < 225) {  // C = A F^T + Q
+      const int nn = frow(k, c, kk, vv);
+      double s = A[r * 15 + kk[0]] * vv[0];
+      for (int t = 1; t < nn; t++) s += A[r * 15 + kk[t]] * vv[t];
+      const double dt = sDt[k];
+      double q = 0.0;
+      if (r >= 6 && r < 9 && c >= 6 && c < 9) q = sCw[k][(r - 6) * 3 + (c - 6)];
+      else if (r == c && r < 3) q = a.cov_gyr * dt * dt;
+      else if (r == c && r >= 9 && r < 12) q = a.rdw_gyr * dt * dt;
+      else if (r == c && r >= 12) q = a.rdw_acc * dt * dt;
+      C[tid] = s + q;
+    }
+    __syncthreads();
+  }
+  // 5. the scan opening (k_scan_begin) with the propagated state
+  if (tid < 225) st->xc[kXS + tid] = C[tid];
+  __syncthreads();
+  for (int t = tid; t < kXC; t += blockDim.x) st->xp[t] = st->xc[t];
+  if (set_scan && tid == 64) {
+    st->sx = x;
+    st->sy = y;
+    st->sz = z;
+    st->sn = n;
+  }
+  if (tid == 0) {
+    st->it = 0;
+    st->rematch = 0;
+    st->done = 0;
+    st->iters = 0;
+    st->degenerate = 0;
+    st->ticket = 0;
+    for (int k = 0; k < 4; k++) st->matches[k] = 0;
+    for (int k = 0; k < 4; k++) st->planes[k] = 0;
+  }
+}
+
 __global__ void k_set_scan(DState* __restrict__ st, const float* x, const float* y, const float* z, int n) {
   if (threadIdx.x == 0) {
     st->sx = x;
@@ -277,7 +447,12 @@ int state_alloc(vg_ctx* ctx) {
 }
 
 int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x, const float* y, const float* z, int n,
-                     hipStream_t s) {
+                     hipStream_t s, const PropArg* prop) {
+  if (prop) {
+    k_scan_prop<<<1, 256, 0, s ? s : ctx->stream>>>(*prop, ctx->st, x, y, z, n, x != nullptr ? 1 : 0);
+    VG_HIP(hipGetLastError());
+    return VG_OK;
+  }
   XcArg a;
   memcpy(a.x, xc249, sizeof(a.x));
   k_scan_begin<<<1, 256, 0, s ? s : ctx->stream>>>(a, ctx->st, x, y, z, n, x != nullptr ? 1 : 0);

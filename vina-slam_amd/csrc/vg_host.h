@@ -178,6 +178,8 @@ struct HostPipe {
   // window push with the insert's first kernel
   bool begin_pending = false;
   double begin_xc[kXC];
+  bool begin_prop = false;  // the opening propagates on the device (k_scan_prop) from `prop`
+  PropArg prop;
   bool push_pending = false;
   PushArg push;
   // IMUEKF::scale_gravity as used by the propagation and the preintegration

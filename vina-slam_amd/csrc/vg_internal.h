@@ -269,6 +269,17 @@ struct PushArg {
   int ord, new_imu;
   double rec[kBaImuRec];
 };
+// IMUEKF::process's propagation (imu_ekf.cpp:13-86) on the device: the scan's
+// IMU samples and times as kernel arguments; the state it starts from is the
+// device's x_curr (the previous scan's, after its BA), so the host never waits
+// for that state before opening the next scan (state.hip k_scan_prop)
+constexpr int kPropMax = 48;  // IMU samples per scan in the arguments (more: the host path)
+struct PropArg {
+  int n, pad;
+  double last_end, beg, end, sg;                 // last_pcl_end_time, pcl_beg/end, imupre_scale_gravity
+  double cov_gyr, cov_acc, rdw_gyr, rdw_acc;     // Odometry.* (node.cpp:211-214)
+  double imu[kPropMax * 7];                      // t, gyr[3], acc[3] per sample
+};
 // per-scan inputs of the replayed graphs, in host-mapped memory: the host
 // writes them before the launch, the kernels read them in place
 struct HostIn {
@@ -408,6 +419,7 @@ struct vg_ctx {
   long prof_runs = 0;
   int rc_total = 0, rc_thread_num = 0;  // the last recut's window point total / thread_num (its resume)
   bool prof_stages = false;  // per-stage events (vg_profile bit 1)
+  bool dev_prop = true;      // host_step propagates on the device (k_scan_prop; vgx_debug 13: 0 = on the host)
   bool rc_fused = true;      // the fused recut levels (vgx_debug 11: 0 = the four-launch level loop)
   bool prof_clock = false;   // in-kernel clocks instead of k_ba_solve events (vg_profile bit 2, KClock)
   hipEvent_t prof_ev[8][2] = {};
@@ -577,7 +589,7 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
 // begin_xc != nullptr: open the scan on the device first (x_curr after
 // propagation, one launch with the scan binding)
 int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank,
-             const double* begin_xc = nullptr, hipStream_t s = nullptr);
+             const double* begin_xc = nullptr, hipStream_t s = nullptr, const PropArg* begin_prop = nullptr);
 constexpr int kNeedInsertReplay = 1;  // map_recut: the insert overflowed k_ins_alloc, replay it first
 // the initialisation's insert source (cut_voxel, initialization.cpp:229-246):
 // n fp64 body points, the kXC pose/covariance block of x_buf[i], both device
@@ -607,7 +619,7 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
 int state_alloc(vg_ctx* ctx);
 // x_curr / x_prop / IEKF flags; with x != nullptr also the scan the IEKF reads
 int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x = nullptr, const float* y = nullptr,
-                     const float* z = nullptr, int n = 0, hipStream_t s = nullptr);
+                     const float* z = nullptr, int n = 0, hipStream_t s = nullptr, const PropArg* prop = nullptr);
 int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n, hipStream_t s = nullptr);
 int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec);  // imurec: kBaImuRec doubles (new_imu >= 0)
 int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq, const int* gate = nullptr);
@@ -669,7 +681,7 @@ int host_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* va
 int decode_scan(vg_ctx* ctx, const void* records, int n, const vg_lidar_format* fmt, float* xyz, float* inten,
                 float* time, int* n_out);  // decode.hip
 int host_stats_log(vg_ctx* ctx, vg_stats* out, int cap);
-int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double end);
+int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double end, bool dev = false);  // dev: k_scan_prop
 int stage_deskew(vg_ctx* ctx, const float* x, const float* y, const float* z, const float* in, const float* t,
                  int n);
 int host_step_deskew(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, const float* di,
