@@ -1035,10 +1035,9 @@ __global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, do
     st->fin = (st->done || st->iters >= 10) ? 1 : 0;
     const int seq = st->seq;  // one publication per launch, numbered on the device (graph replays)
     st->seq = seq + 1;
-    __hip_atomic_store(&pub->ba_done, st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&pub->ba_iters, st->iters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __threadfence_system();
-    __hip_atomic_store(&pub->seq_ba, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    pub_store(&pub->ba_done, st->done);
+    pub_store(&pub->ba_iters, st->iters);
+    pub_flag(&pub->seq_ba, seq);
   }
 }
 

@@ -2204,10 +2204,9 @@ __global__ void __launch_bounds__(1024) k_fac_sort(DevMap m, int* __restrict__ r
     const int seq = *seq_ctr + 1;  // the device's count of asynchronous recuts (the host mirrors it)
     *seq_ctr = seq;
     rc[kRcStatus] = status;
-    __hip_atomic_store(&pub->rc_status, status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&pub->rc_nf, nf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __threadfence_system();
-    __hip_atomic_store(&pub->seq_rc, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    pub_store(&pub->rc_status, status);
+    pub_store(&pub->rc_nf, nf);
+    pub_flag(&pub->seq_rc, seq);
   }
 }
 __global__ void __launch_bounds__(256) k_factor_finish_dev(const int* __restrict__ rc, DevMap m,
@@ -2822,12 +2821,10 @@ __global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m
   if (seq2 < 0) seq2 = st->seq2;  // set by k_make_win (replayed graph)
   if (seq2 > 0) {
     __syncthreads();
-    if (t < kCntN) __hip_atomic_store(&pub->counters[t], m.counters[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t < kCntN) pub_store(&pub->counters[t], m.counters[t]);
+    pub_drain();
     __syncthreads();
-    if (t == 0) {
-      __threadfence_system();
-      __hip_atomic_store(&pub->seq2, seq2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (t == 0) pub_flag(&pub->seq2, seq2);
   }
 }
 __global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, double j, int* __restrict__ rc,

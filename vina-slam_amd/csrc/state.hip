@@ -279,6 +279,7 @@ __global__ void k_publish_state(const DState* __restrict__ st, int win_count, in
 __global__ void k_publish_counters(const int* __restrict__ counters, Pub* __restrict__ pub, int seq) {
   const int t = threadIdx.x;
   if (t < kCntN) pub_store(&pub->counters[t], counters[t]);
+  pub_drain();
   __syncthreads();
   if (t == 0) pub_flag(&pub->seq2, seq);
 }

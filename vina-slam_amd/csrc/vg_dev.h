@@ -387,16 +387,23 @@ __device__ __forceinline__ void push_state_block(DState* __restrict__ st, const 
   }
 }
 
-// host-mapped publication stores (system scope; the flag last)
+// host-mapped publication stores. Every payload word is a system-scope store
+// (written through the L2 to host memory), so ordering them before the flag
+// needs no L2 write-back: each storing wave drains its stores (pub_drain, an
+// s_waitcnt vmcnt(0), before the workgroup barrier), then one lane stores
+// the flag, also system scope. (A system-scope release or __threadfence_system
+// would write back every dirty line of the XCD's L2 first: nothing the host
+// reads lives there.)
 __device__ __forceinline__ void pub_store(double* dst, double v) {
   __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void pub_store(int* dst, int v) {
   __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ void pub_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void pub_flag(int* dst, int v) {
-  __threadfence_system();
-  __hip_atomic_store(dst, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  pub_drain();  // this wave's own payload stores
+  __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // P1: x_curr, the post-IEKF pose, window states, IEKF / BA summary
@@ -415,6 +422,7 @@ __device__ __forceinline__ void publish_state_block(const DState* __restrict__ s
     pub_store(&pub->ba_hess1, ba_iters_valid ? *ba_hess : 0);
     for (int k = 0; k < 4; k++) pub_store(&pub->planes[k], st->planes[k]);
   }
+  pub_drain();
   __syncthreads();
   if (t == 0) pub_flag(&pub->seq1, seq);
 }
