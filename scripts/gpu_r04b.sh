@@ -8,7 +8,6 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -1 gpurun_out/gputest_$TAG.log
 timeout -k 10 420 python -u bench.py ${BENCH_ARGS} > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { echo "bench failed"; tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 head -c 400 gpurun_out/bench_$TAG.json; echo
-[ "$AB_DEBUG" = "11=0" ] && AB_DEBUG="11=0;13=0"
 [ -n "$AB_DEBUG" ] && { timeout -k 10 900 bash scripts/ab_env.sh || exit 1; }
 TAG=$TAG bash scripts/gpu_trace.sh > gpurun_out/trace_$TAG.out 2>&1 || { tail -5 gpurun_out/trace_$TAG.out; exit 1; }
 python3 scripts/scan_timeline.py gpurun_out/trace_$TAG/run_kernel_trace.csv 4 > gpurun_out/scan_timeline_$TAG.txt && tail -1 gpurun_out/scan_timeline_$TAG.txt

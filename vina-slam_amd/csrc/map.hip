@@ -2916,6 +2916,9 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
       m.counters + kCntLeaves, w.list0, mp, wa2, ctx->st, dwin, dn, dn + 32, bi != nullptr, bi,
       bi ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, pub_seq, m, ctx->ba.fac_eig, ctx->ba.fac_pcr, w.plan, gate);
   VG_HIP(hipEventRecord(ctx->ev_tail_a, s));
+  if (ctx->flag_sync && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages && ctx->shard.world == 1) {
+    VG_TRY(sync_set(ctx, s, 0, (unsigned)pub_seq, gate));  // the margi's publication number (stage_margi_slide)
+  }
   if (ctx->pub_flags & 1) k_local_map<<<64, kBlock, 0, s>>>(dwin, m, ctx->d_cmap, ctx->d_cmap_n, gate);
   ctx->tail_a_valid = true;
   auto body = [&]() -> int {

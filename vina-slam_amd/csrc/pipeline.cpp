@@ -88,7 +88,8 @@ static int map_error(vg_ctx* ctx, int e) {
   ctx->err = std::string("device map error flags=") + std::to_string(e) + ((e & 4) ? " (node pool full)" : "") +
              ((e & 8) ? " (point_fix arena full)" : "") + ((e & 1) ? " (voxel key out of packed range)" : "") +
              ((e & 2) ? " (root hash full)" : "") + ((e & 16) ? " (subdivision event buffer full)" : "") +
-             ((e & 32) ? " (sharded exchange out of step: the ranks' exchange sequences differ)" : "");
+             ((e & 32) ? " (sharded exchange out of step: the ranks' exchange sequences differ)" : "") +
+             ((e & 64) ? " (cross-stream hand-off timed out)" : "");
   if (e & 32) return VG_E_STATE;
   return (e & 1) ? VG_E_RANGE : VG_E_CAPACITY;
 }
@@ -392,11 +393,20 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   // it (vg_multi_create), as a third stream per sequence makes sequences
   // share hardware queues (B = 4: 2,742 -> 1,430 scans/s)
   if (!ctx->stream_iekf) VG_HIP(hipStreamCreateWithFlags(&ctx->stream_iekf, hipStreamNonBlocking));
-  VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->ev_tail_a, 0));
+  const bool flags = ctx->flag_sync && ctx->sync_tail_armed;  // state.hip k_sync_*: no late-released event waits
+  ctx->sync_tail_armed = false;
+  if (flags) VG_TRY(sync_wait(ctx, ctx->stream_iekf, 0, ctx->sync_tail_value));
+  else VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->ev_tail_a, 0));
   if (ctx->in_ev) VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->in_ev, 0));  // a host-input scan's unpack
   VG_TRY(iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, bxc, ctx->stream_iekf, bprop));
-  VG_HIP(hipEventRecord(ctx->ev_iekf_done, ctx->stream_iekf));
-  VG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_iekf_done, 0));
+  if (flags) {
+    const unsigned v = ++ctx->sync_iekf_value;
+    VG_TRY(sync_set(ctx, ctx->stream_iekf, 1, v));
+    VG_TRY(sync_wait(ctx, ctx->stream, 1, v));
+  } else {
+    VG_HIP(hipEventRecord(ctx->ev_iekf_done, ctx->stream_iekf));
+    VG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_iekf_done, 0));
+  }
   return VG_OK;
 }
 
@@ -852,6 +862,11 @@ int stage_margi_slide(vg_ctx* ctx) {
   }
   P->prefix = false;
   P->tail_queued = false;
+  // the margi that stands (the speculative tail or the one just enqueued) stores seq1 into the
+  // IEKF hand-off flag (map_margi), which the next scan's IEKF stream polls (lio_state_estimation)
+  ctx->sync_tail_armed = ctx->flag_sync && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages &&
+                         ctx->shard.world == 1;
+  ctx->sync_tail_value = (unsigned)seq1;
   P->cur.seq1 = seq1;
   P->cur.seq2 = seq2;
   P->cur.shift = 1;

@@ -23,6 +23,8 @@
 //                    without draining the stream
 // The fp64 expression trees are the host code's (vg_la.h, -ffp-contract=off),
 // so the device update is the same arithmetic the host update was.
+#include <cstddef>
+
 #include "vg_iekf.h"
 
 namespace vg {
@@ -66,8 +68,18 @@ __global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict
 // parallel, then cov <- F cov F^T + Q sample by sample, one lane per entry,
 // each sum in ascending column order over F's non-zeros (the host's
 // sandwich()).
-__global__ void __launch_bounds__(256) k_scan_prop(PropArg a, DState* __restrict__ st, const float* x, const float* y,
+__global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restrict__ st, const float* x, const float* y,
                                                    const float* z, int n, int set_scan) {
+  // the arguments once into LDS, by all lanes (the kernel-argument block is
+  // host memory: the serial chain below would pay a round trip per sample)
+  __shared__ PropArg a;
+  {
+    const int words = (int)((offsetof(PropArg, imu) + (size_t)(arg.n > 0 ? arg.n : 0) * 7 * sizeof(double)) / 8);
+    const double* src = reinterpret_cast<const double*>(&arg);
+    double* dst = reinterpret_cast<double*>(&a);
+    for (int i = threadIdx.x; i < words; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
   __shared__ double sExp[kPropMax][9], sF00[kPropMax][9], sRi[kPropMax][9], sAsk[kPropMax][9];
   __shared__ double sF60[kPropMax][9], sF612[kPropMax][9], sCw[kPropMax][9], sDt[kPropMax];
   __shared__ int sOk[kPropMax];
@@ -226,6 +238,46 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg a, DState* __restrict
     for (int k = 0; k < 4; k++) st->matches[k] = 0;
     for (int k = 0; k < 4; k++) st->planes[k] = 0;
   }
+}
+
+// ---- cross-stream hand-offs on the critical path (vg_ctx::flag_sync)
+// A hipStreamWaitEvent whose event is still pending when the waiting queue
+// reaches it releases late: measured ~18 us after the event on an idle GPU,
+// and not before the producer's queue drained when that queue stays busy (the
+// next scan's IEKF behind the margi remainder: ~97 us). So the two waits the
+// scan's critical path crosses — the IEKF stream on k_margi_leaf, the main
+// stream on the IEKF — are a counter instead: the producer's stream bumps it
+// (k_sync_set, one lane, behind the producing kernel, so that kernel's
+// end-of-kernel release has made its writes visible), a one-lane kernel on
+// the consumer's stream polls it (k_sync_wait) and ends; the consumer's
+// kernels then start with the usual kernel-start acquire. The flag carries a
+// host-chosen increasing number (the margi's publication number, a count of
+// split IEKFs), so a gated-off producer (a speculative margi tail the LM did
+// not reach) simply does not store it; a poll gives up after ~1 s (error bit
+// 64) instead of hanging.
+__global__ void k_sync_set(unsigned* __restrict__ flag, const int* __restrict__ gate, unsigned value) {
+  if (threadIdx.x != 0 || (gate && !*gate)) return;
+  __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void k_sync_wait(const unsigned* __restrict__ flag, unsigned target, int* __restrict__ err) {
+  if (threadIdx.x != 0) return;
+  for (long it = 0; (int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0; it++) {
+    __builtin_amdgcn_s_sleep(4);
+    if (it > (1l << 24)) {
+      atomicOr(err, 64);
+      return;
+    }
+  }
+}
+int sync_set(vg_ctx* ctx, hipStream_t s, int k, unsigned value, const int* gate) {
+  k_sync_set<<<1, 64, 0, s>>>(ctx->d_sync + k, gate, value);
+  VG_HIP(hipGetLastError());
+  return VG_OK;
+}
+int sync_wait(vg_ctx* ctx, hipStream_t s, int k, unsigned target) {
+  k_sync_wait<<<1, 64, 0, s>>>(ctx->d_sync + k, target, ctx->map.counters + kCntErr);
+  VG_HIP(hipGetLastError());
+  return VG_OK;
 }
 
 __global__ void k_set_scan(DState* __restrict__ st, const float* x, const float* y, const float* z, int n) {
@@ -440,7 +492,8 @@ int state_load(vg_ctx* ctx, const double* xs, int nw, const double* xc, const do
 int state_alloc(vg_ctx* ctx) {
   ctx->st = ctx->arena.take<DState>(1);
   ctx->d_deskew = ctx->arena.take<double>(kDeskewBuf);
-  if (!ctx->st || !ctx->d_deskew) {
+  ctx->d_sync = ctx->arena.take<unsigned>(8);
+  if (!ctx->st || !ctx->d_deskew || !ctx->d_sync) {
     ctx->err = "arena exhausted (state)";
     return VG_E_CAPACITY;
   }

@@ -419,6 +419,10 @@ struct vg_ctx {
   long prof_runs = 0;
   int rc_total = 0, rc_thread_num = 0;  // the last recut's window point total / thread_num (its resume)
   bool prof_stages = false;  // per-stage events (vg_profile bit 1)
+  bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)
+  unsigned* d_sync = nullptr;  // hand-off flags: [0] margi leaf -> next IEKF, [1] IEKF -> insert
+  bool sync_tail_armed = false;  // the last margi's leaf pass stores sync_tail_value into d_sync[0]
+  unsigned sync_tail_value = 0, sync_iekf_value = 0;
   bool dev_prop = true;      // host_step propagates on the device (k_scan_prop; vgx_debug 13: 0 = on the host)
   bool rc_fused = true;      // the fused recut levels (vgx_debug 11: 0 = the four-launch level loop)
   bool prof_clock = false;   // in-kernel clocks instead of k_ba_solve events (vg_profile bit 2, KClock)
@@ -610,6 +614,8 @@ int map_recut_resume(vg_ctx* ctx, const MP& mp, int* n_factors);
 int map_set_attrs(vg_ctx* ctx);
 const int* map_rc_status(vg_ctx* ctx);  // the asynchronous recut's status word (k_fac_sort)
 int map_memo_probe(vg_ctx* ctx, const MP& mp, int* out);  // test-only (vgx_memo_probe)
+int sync_set(vg_ctx* ctx, hipStream_t s, int k, unsigned value, const int* gate = nullptr);  // state.hip: cross-stream flags
+int sync_wait(vg_ctx* ctx, hipStream_t s, int k, unsigned target);
 // multi_margi + the device-state slide; publishes the state (pub_seq, before
 // the margi kernels) and the end-of-scan counters (pub_seq2)
 int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, double jour);

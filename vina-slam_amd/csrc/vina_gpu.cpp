@@ -794,6 +794,10 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     VG_HIP(hipMemcpy(ctx->shard.d_seq, &s, sizeof(s), hipMemcpyHostToDevice));
     return VG_OK;
   }
+  if (key == 14) {  // 0: event waits for the margi leaf -> IEKF and IEKF -> insert hand-offs
+    ctx->flag_sync = value != 0;
+    return VG_OK;
+  }
   if (key == 13) {  // 0: host_step propagates on the host (waits for the previous scan's state)
     ctx->dev_prop = value != 0;
     return VG_OK;
