@@ -244,7 +244,8 @@ def main():
         torch.cuda.synchronize(dev)
         stage_prof = ctx.profile_read()
         stage_stats = ctx.stats_log()[nlog1:]
-        stage_ms = {k: round(v["ms"] / extra, 4) for k, v in stage_prof.items() if not k.startswith("host_")}
+        stage_ms = {k: round(v["ms"] / extra, 4) for k, v in stage_prof.items()
+                    if not k.startswith("host_") and not k.endswith("_clock")}
         ctx.profile(False)
     # the rest of the CPU baseline's sample, untimed: the ATE is taken over the
     # same scans as the CPU timing (>= 200 after a 20-scan warm-up)
@@ -299,6 +300,23 @@ def main():
         if r["kernel"] in pmc:
             r["traffic"] = pmc[r["kernel"]]["traffic_bytes"]
             r["traffic_source"] = pmc["_file"]
+    # FETCH_SIZE calibrated per access shape (scripts/micro/fetch_cal.hip ->
+    # profiles/<round>/fetch_calibration.json): the counter k_iekf's
+    # algorithmic bytes would produce (its 4 B/lane SoA planes + leaf cache at
+    # the SoA ratio, its 224 B plane-record gathers at the record ratio) beside
+    # the measured counter; their quotient is the traffic ratio the x2
+    # correction cannot give for these shapes
+    cal = fetch_calibration()
+    if cal and "k_iekf" in pmc and "fetch_raw_bytes" in pmc["k_iekf"]:
+        it_n = max(it_t, 1)
+        n_mean = sum(s["iekf_iters"] * s["n_raw"] for s in stats) / it_n
+        exp_fetch = cal["k_soa4"] * 16.0 * n_mean + cal["k_rec224"] * PLANE_B * p_mean
+        roof_iekf["fetch_calibrated"] = {
+            "measured_fetch_raw": pmc["k_iekf"]["fetch_raw_bytes"], "expected_fetch_raw": int(exp_fetch),
+            "ratio": round(pmc["k_iekf"]["fetch_raw_bytes"] / exp_fetch, 3) if exp_fetch else None,
+            "shape_ratios": {"soa4": cal["k_soa4"], "rec224": cal["k_rec224"]}, "source": cal["_file"],
+            "note": "measured FETCH_SIZE bytes (no x2) / the FETCH the algorithmic bytes produce at the calibrated "
+                    "per-shape ratios (same workload, PMC pass of the same build)"}
     roof["stage_ms_per_scan"] = stage_ms
 
     h2d = None
@@ -643,6 +661,18 @@ def pmc_traffic():
     if not files:
         return {}
     d = json.load(open(files[-1]))["kernels"]
+    d["_file"] = os.path.relpath(files[-1], REPO)
+    return d
+
+
+def fetch_calibration():
+    """FETCH_SIZE bytes / algorithmic bytes per access shape, newest
+    profiles/<round>/fetch_calibration.json (scripts/gpu_fetch_cal.sh)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "fetch_calibration.json")))
+    if not files:
+        return {}
+    d = {k: v["fetch_ratio"] for k, v in json.load(open(files[-1]))["shapes"].items() if "fetch_ratio" in v}
     d["_file"] = os.path.relpath(files[-1], REPO)
     return d
 

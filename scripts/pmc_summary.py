@@ -37,7 +37,7 @@ def main(src, dst):
         fb = 2.0 * 1024.0 * sum(f) / len(f)
         wb = 1024.0 * sum(w) / max(len(w), 1)
         out["kernels"][k.split("::")[-1]] = {"launches": len(f), "fetch_bytes": round(fb), "write_bytes": round(wb),
-                                             "traffic_bytes": round(fb + wb)}
+                                             "traffic_bytes": round(fb + wb), "fetch_raw_bytes": round(fb / 2.0)}
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 

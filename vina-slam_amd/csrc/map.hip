@@ -270,7 +270,11 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
                                               int* __restrict__ pk) {
   if (st->done) return;
   const bool clk_on = st->clk.on != 0;
-  if (clk_on && threadIdx.x == 0) atomicMin(&st->clk.iekf_t0, (unsigned long long)wall_clock64());
+  const int clk_slot = (st->clk.scan * 4 + it) & (kClkRing - 1);
+  if (clk_on && blockIdx.x == 0 && threadIdx.x == 0) {
+    st->clk.t0[clk_slot] = (unsigned long long)wall_clock64();
+    st->clk.exec[clk_slot] = 1;
+  }
   VG_PROBE_BEGIN();
   const int n = st->sn;
   const float* __restrict__ x = st->sx;
@@ -388,9 +392,9 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
     int j = threadIdx.x;
     partials[(size_t)blockIdx.x * kIekfVals + j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
   }
-  if (clk_on) {  // the workgroup's end (its partials written)
+  if (clk_on && blockIdx.x < kClkBlocks) {  // the workgroup's end (its partials written)
     __syncthreads();
-    if (threadIdx.x == 0) atomicMax(&st->clk.iekf_t1, (unsigned long long)wall_clock64());
+    if (threadIdx.x == 0) st->clk.tend[clk_slot][blockIdx.x] = (unsigned long long)wall_clock64();
   }
   if (blockIdx.x == 0) VG_PROBE_MARK(31);  // the block reduction
 #ifdef VG_PROBE
@@ -421,15 +425,6 @@ __global__ void __launch_bounds__(1024) k_iekf_update(int nb, const double* __re
                                                      DState* __restrict__ st, int it) {
   __shared__ IekfLds L;
   if (st->done) return;
-  if (threadIdx.x == 0 && st->clk.on) {  // fold the k_iekf launch this update follows into the clock sums
-    KClock& c = st->clk;
-    if (c.iekf_t1 > c.iekf_t0) {
-      c.iekf_ticks += c.iekf_t1 - c.iekf_t0;
-      c.iekf_n += 1;
-    }
-    c.iekf_t0 = ~0ull;
-    c.iekf_t1 = 0;
-  }
   iekf_update_block(nb, partials, st, it, L);
 }
 // sharded mode: this shard's 34 sums (the update then runs on the all-reduced ones)
@@ -446,6 +441,7 @@ __global__ void __launch_bounds__(256) k_iekf_reduce(int nb, const double* __res
 static int iekf_blocks(vg_ctx* ctx) {
   return ((grid_for(ctx->cap.max_points_per_scan, 256, 512) + 7) / 8) * 8;
 }
+int iekf_grid(vg_ctx* ctx) { return iekf_blocks(ctx); }
 
 // one IEKF iteration: the point loop (block partials) and the update; the
 // optional event pair brackets k_iekf alone (vg_profile)

@@ -57,6 +57,11 @@ __global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict
     st->ticket = 0;
     for (int k = 0; k < 4; k++) st->matches[k] = 0;
     for (int k = 0; k < 4; k++) st->planes[k] = 0;
+    if (st->clk.on) {  // this scan's k_iekf clock slots (KClock)
+      const int sc = st->clk.scan + 1;
+      st->clk.scan = sc;
+      for (int k = 0; k < 4; k++) st->clk.exec[(sc * 4 + k) & (kClkRing - 1)] = 0;
+    }
   }
 }
 
@@ -237,6 +242,11 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
     st->ticket = 0;
     for (int k = 0; k < 4; k++) st->matches[k] = 0;
     for (int k = 0; k < 4; k++) st->planes[k] = 0;
+    if (st->clk.on) {  // this scan's k_iekf clock slots (KClock)
+      const int sc = st->clk.scan + 1;
+      st->clk.scan = sc;
+      for (int k = 0; k < 4; k++) st->clk.exec[(sc * 4 + k) & (kClkRing - 1)] = 0;
+    }
   }
 }
 

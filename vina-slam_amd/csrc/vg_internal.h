@@ -229,17 +229,22 @@ constexpr int kXS = 24;             // per-frame state: R 9, p 3, v 3, bg 3, ba 
 constexpr int kXC = kXS + 225;      // x_curr: frame state + cov 15x15 (row-major)
 constexpr int kMaxWin = 32;
 constexpr int kBaImuRec = 64 + 225;  // IMU_PRE record (doubles): deltas, bias Jacobians, dtime, cov_inv
-// In-kernel clocks of the roofline kernels (vg_profile bit 2): s_memrealtime
-// ticks (wall_clock64, the device's constant-rate clock), kernel-only spans:
-// a k_iekf launch runs from its first workgroup's start to its last
-// workgroup's end (atomicMin / atomicMax here, folded into the sums by the
-// k_iekf_update behind it, which runs exactly when the point loop did);
-// k_ba_solve is one workgroup, timed by its thread 0.
+// In-kernel clocks of the roofline kernels (vg_profile bit 2): the device's
+// constant-rate wall clock (wall_clock64), kernel-only spans, no atomics on
+// the timed kernels' paths (a hot atomic from every workgroup cost k_iekf
+// ~3 us per launch). A k_iekf launch runs from workgroup 0's start to the
+// last workgroup's end: workgroup 0 stores the start, every workgroup its end,
+// into a ring slot per (scan, iteration); the host takes the maximum when it
+// reads the clock (vg_profile_read). k_ba_solve is one workgroup, timed by its
+// thread 0.
+constexpr int kClkRing = 256;    // k_iekf launch slots: the last 64 scans x 4 iterations
+constexpr int kClkBlocks = 512;  // >= the IEKF grid (iekf_blocks)
 struct KClock {
-  unsigned long long iekf_t0, iekf_t1;     // the current k_iekf launch
-  unsigned long long iekf_ticks, iekf_n;   // executed k_iekf launches
-  unsigned long long solve_ticks, solve_n; // executed k_ba_solve launches
-  int on, pad;
+  unsigned long long solve_ticks, solve_n;  // executed k_ba_solve launches
+  int on, scan;                             // scans opened since vg_profile (k_scan_begin / k_scan_prop)
+  int exec[kClkRing];                       // the slot's k_iekf ran (not a no-op after convergence)
+  unsigned long long t0[kClkRing];
+  unsigned long long tend[kClkRing][kClkBlocks];
 };
 
 struct DState {
@@ -614,6 +619,7 @@ int map_recut_resume(vg_ctx* ctx, const MP& mp, int* n_factors);
 int map_set_attrs(vg_ctx* ctx);
 const int* map_rc_status(vg_ctx* ctx);  // the asynchronous recut's status word (k_fac_sort)
 int map_memo_probe(vg_ctx* ctx, const MP& mp, int* out);  // test-only (vgx_memo_probe)
+int iekf_grid(vg_ctx* ctx);  // k_iekf's workgroups (map.hip iekf_blocks)
 int sync_set(vg_ctx* ctx, hipStream_t s, int k, unsigned value, const int* gate = nullptr);  // state.hip: cross-stream flags
 int sync_wait(vg_ctx* ctx, hipStream_t s, int k, unsigned target);
 // multi_margi + the device-state slide; publishes the state (pub_seq, before

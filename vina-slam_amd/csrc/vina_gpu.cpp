@@ -731,11 +731,9 @@ int vg_profile(vg_ctx* ctx, int on) {
   ctx->prof_runs = 0;
   {  // bit 2: the in-kernel clocks (KClock), reset; set behind everything already enqueued
     VG_TRY(host_sync(ctx));
-    vg::KClock k;
-    memset(&k, 0, sizeof(k));
-    k.iekf_t0 = ~0ull;
-    k.on = (on & 4) ? 1 : 0;
-    VG_HIP(hipMemcpy(&ctx->st->clk, &k, sizeof(k), hipMemcpyHostToDevice));
+    VG_HIP(hipMemset(&ctx->st->clk, 0, sizeof(vg::KClock)));
+    const int clk_on = (on & 4) ? 1 : 0;
+    VG_HIP(hipMemcpy(&ctx->st->clk.on, &clk_on, sizeof(int), hipMemcpyHostToDevice));
   }
   ctx->iekf_ring_n = 0;
   for (int i = 0; i < vg::kProfAll; i++) {
@@ -750,13 +748,31 @@ int vg_profile_read(vg_ctx* ctx, int stage, double* total_ms, int* count) {
   if (!ctx || stage < 0 || stage >= vg::kProfAll + 2 || !total_ms || !count) return VG_E_ARG;
   if (stage >= vg::kProfAll) {  // 16 k_iekf, 17 k_ba_solve: kernel-only time from the in-kernel clocks
     VG_TRY(host_sync(ctx));
-    vg::KClock k;
+    std::vector<vg::KClock> kv(1);
+    vg::KClock& k = kv[0];
     VG_HIP(hipMemcpy(&k, &ctx->st->clk, sizeof(k), hipMemcpyDeviceToHost));
     int khz = 0;
     VG_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
-    const unsigned long long t = stage == vg::kProfAll ? k.iekf_ticks : k.solve_ticks;
+    unsigned long long t = k.solve_ticks, nl = k.solve_n;
+    if (stage == vg::kProfAll) {  // k_iekf: the executed launches of the last <= 64 scans
+      t = 0;
+      nl = 0;
+      const int nb = vg::iekf_grid(ctx) < vg::kClkBlocks ? vg::iekf_grid(ctx) : vg::kClkBlocks;
+      const int s1 = k.scan, s0 = k.scan - vg::kClkRing / 4 + 1 > 1 ? k.scan - vg::kClkRing / 4 + 1 : 1;
+      for (int sc = s0; sc <= s1; sc++)
+        for (int it = 0; it < 4; it++) {
+          const int slot = (sc * 4 + it) & (vg::kClkRing - 1);
+          if (!k.exec[slot]) continue;
+          unsigned long long e = 0;
+          for (int b = 0; b < nb; b++) e = k.tend[slot][b] > e ? k.tend[slot][b] : e;
+          if (e > k.t0[slot]) {
+            t += e - k.t0[slot];
+            nl++;
+          }
+        }
+    }
     *total_ms = khz > 0 ? (double)t / (double)khz : 0.0;
-    *count = (int)(stage == vg::kProfAll ? k.iekf_n : k.solve_n);
+    *count = (int)nl;
     return VG_OK;
   }
   *total_ms = ctx->prof_ms[stage];
