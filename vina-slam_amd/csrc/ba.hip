@@ -1270,7 +1270,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
                                    d.imuout, d.imures, sharded ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st,
                                    ctx->d_pub);
   };
-  const bool graph = ctx->use_graphs && !sharded && !solve_ev && ctx->dbg_capture != 1;
+  const bool graph = ctx->use_graphs && ctx->ba_graph && !sharded && !solve_ev && ctx->dbg_capture != 1;
   if (graph && !ctx->g_ba) {
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     enqueue(0);

@@ -424,6 +424,7 @@ struct vg_ctx {
   long prof_runs = 0;
   int rc_total = 0, rc_thread_num = 0;  // the last recut's window point total / thread_num (its resume)
   bool prof_stages = false;  // per-stage events (vg_profile bit 1)
+  bool ba_graph = true;      // LM iterations replay one captured graph each (vgx_debug 15: 0 = direct launches)
   bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)
   unsigned* d_sync = nullptr;  // hand-off flags: [0] margi leaf -> next IEKF, [1] IEKF -> insert
   bool sync_tail_armed = false;  // the last margi's leaf pass stores sync_tail_value into d_sync[0]
