@@ -84,7 +84,9 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
     double* dst = reinterpret_cast<double*>(&a);
     for (int i = threadIdx.x; i < words; i += blockDim.x) dst[i] = src[i];
   }
+  VG_PROBE_BEGIN();
   __syncthreads();
+  VG_PROBE_MARK(1);
   __shared__ double sExp[kPropMax][9], sF00[kPropMax][9], sRi[kPropMax][9], sAsk[kPropMax][9];
   __shared__ double sF60[kPropMax][9], sF612[kPropMax][9], sCw[kPropMax][9], sDt[kPropMax];
   __shared__ int sOk[kPropMax];
@@ -118,6 +120,7 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
     sOk[tid] = ok ? 1 : 0;
   }
   __syncthreads();
+  VG_PROBE_MARK(2);
   // 2. the rotation / velocity / position chain (thread 0), the final pose
   if (tid == 0) {
     M3 R_imu = ld_m3(xc);
@@ -157,6 +160,7 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
     }
   }
   __syncthreads();
+  VG_PROBE_MARK(3);
   // 3. per pair: F60, F612 and the acceleration noise block
   if (tid < ns && sOk[tid]) {
     const M3 Ri = ld_m3(sRi[tid]);
@@ -174,6 +178,7 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
   const int r = tid / 15, c = tid % 15;
   if (tid < 225) C[tid] = xc[kXS + tid];
   __syncthreads();
+  VG_PROBE_MARK(4);
   // 4. cov = F cov F^T + Q per pair, F's non-zero columns ascending (sandwich())
   auto frow = [&](int k, int i, int* kk, double* vv) -> int {
     const double dt = sDt[k];
@@ -223,6 +228,7 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
     }
     __syncthreads();
   }
+  VG_PROBE_MARK(5);
   // 5. the scan opening (k_scan_begin) with the propagated state
   if (tid < 225) st->xc[kXS + tid] = C[tid];
   __syncthreads();
@@ -248,6 +254,10 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
       for (int k = 0; k < 4; k++) st->clk.exec[(sc * 4 + k) & (kClkRing - 1)] = 0;
     }
   }
+  VG_PROBE_MARK(6);
+#ifdef VG_PROBE
+  if (tid == 0) atomicAdd(&g_probe[63], 1ull);
+#endif
 }
 
 // ---- cross-stream hand-offs on the critical path (vg_ctx::flag_sync)
@@ -620,3 +630,7 @@ int state_publish_ds(vg_ctx* ctx, hipStream_t s, int seq, int* flags, bool reset
 }
 
 }  // namespace vg
+
+#ifdef VG_PROBE
+VG_PROBE_READER(vg_probe_read_state)
+#endif

@@ -429,7 +429,7 @@ struct vg_ctx {
   unsigned* d_sync = nullptr;  // hand-off flags: [0] margi leaf -> next IEKF, [1] IEKF -> insert
   bool sync_tail_armed = false;  // the last margi's leaf pass stores sync_tail_value into d_sync[0]
   unsigned sync_tail_value = 0, sync_iekf_value = 0;
-  bool dev_prop = true;      // host_step propagates on the device (k_scan_prop; vgx_debug 13: 0 = on the host)
+  bool dev_prop = false;     // host_step propagates on the device (k_scan_prop; vgx_debug 13: 1 = on the device)
   bool rc_fused = true;      // the fused recut levels (vgx_debug 11: 0 = the four-launch level loop)
   bool prof_clock = false;   // in-kernel clocks instead of k_ba_solve events (vg_profile bit 2, KClock)
   hipEvent_t prof_ev[8][2] = {};
