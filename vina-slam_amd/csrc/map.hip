@@ -91,6 +91,8 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(w.rc = ctx->arena.take<int>(128));
   good &= ok(w.cand_bits = ctx->arena.take<uint32_t>(ctx->cap.max_nodes / 32 + 1));
   good &= ok(w.plan = ctx->arena.take<int>(cn * 8));
+  w.ngran = (int)(cw / 1024 + 64);
+  good &= ok(w.gran = ctx->arena.take<unsigned long long>(w.ngran));
   good &= ok(w.sub_odd = ctx->arena.take<int>(cn));
   good &= ok(w.info_odd = ctx->arena.take<int>(w.cap));
   good &= ok(w.ev_odd = ctx->arena.take<uint64_t>(w.cap));
@@ -518,8 +520,12 @@ __global__ void __launch_bounds__(256) k_ins_prep(int n_arg, const int* __restri
                            const float* __restrict__ oz, const float* __restrict__ oi, MP mp, DState* __restrict__ st, int slot,
                            DevMap m, double* __restrict__ pw, uint32_t* __restrict__ hslot,
                            const PushArg* __restrict__ pa, const double* __restrict__ pin, const double* __restrict__ xsrc,
-                           int var_identity, int* __restrict__ dsf) {
+                           int var_identity, int* __restrict__ dsf, unsigned long long* __restrict__ gran, int ngran) {
   const int n = nd ? *nd : n_arg;  // the downsampled count on the device (ds_enqueue_hashed)
+  {  // the root registration's look-back granules (k_ins_roots_lb, the next launch) start empty
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gran && g < ngran) gran[g] = 0ull;
+  }
   // the window push (local_mapping.cpp:434-441) rides in block 0: it copies
   // x_curr into x_buf[ord], which this kernel only reads
   if (!kPre && pa && blockIdx.x == 0) push_state_block(st, *pa);  // pa: host-mapped (vg_ctx::d_in)
@@ -742,6 +748,118 @@ __global__ void __launch_bounds__(256) k_ins_roots_alloc(int n_arg, const int* _
     m.counters[kCntRoots] = tot[1];
     m.counters[kCntTouched] = tot[0];
     m.counters[kCntSlide] = sbase + tot[2];
+  }
+}
+
+// Root registration in ONE launch (k_ins_flags + k_ins_roots_alloc): each
+// 1024-point tile publishes its three counts (first points, new roots, slide
+// joiners) as one 64-bit granule {valid bit, 3 x 21-bit counts} with an
+// agent-scope store, then sums the granules of the tiles before it (decoupled
+// look-back: tiles are dispatched in order per XCD, so a tile only ever waits
+// for tiles already dispatched) and allocates its own roots at base + prefix —
+// the same ids and slide positions as the two-launch form. The granules are
+// zeroed by k_ins_prep, the launch before. The last tile writes the totals.
+__global__ void __launch_bounds__(256) k_ins_roots_lb(int n_arg, const int* __restrict__ nd, int ntile,
+                                                      const uint32_t* __restrict__ hslot, MP mp, DevMap m,
+                                                      unsigned long long* __restrict__ gran) {
+  const int n = nd ? *nd : n_arg;
+  __shared__ u64 s_w[4];
+  __shared__ int s_off[3], s_tot[3];
+  const int tid = threadIdx.x, lane = tid & 63, b = blockIdx.x;
+  const int i0 = b * kRootTile + tid * 4;
+  int code[4];
+  u64 v = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    code[k] = ins_root_code(m, hslot, i0 + k, n);
+    v += pack3(code[k]);
+  }
+  u64 tot;
+  u64 r = block_excl_scan3(v, s_w, &tot);
+  constexpr u64 kF = (1ull << 21) - 1;
+  if (tid == 0) __hip_atomic_store(&gran[b], tot | (1ull << 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < 64) {  // wave 0: the earlier tiles' counts (and, in the last tile, everyone's)
+    const bool last = b == ntile - 1;
+    const int upto = last ? ntile : b;
+    int a0 = 0, a1 = 0, a2 = 0, t0 = 0, t1 = 0, t2 = 0;
+    for (int k = lane; k < upto; k += 64) {
+      u64 g;
+      for (long it = 0;; it++) {
+        g = __hip_atomic_load(&gran[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (g >> 63) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (it > (1l << 24)) {  // never: a tile that never publishes (bounded, not a hang)
+          atomicOr(&m.counters[kCntErr], 64);
+          g = 1ull << 63;
+          break;
+        }
+      }
+      const int c0 = (int)(g & kF), c1 = (int)((g >> 21) & kF), c2 = (int)((g >> 42) & kF);
+      if (k < b) {
+        a0 += c0;
+        a1 += c1;
+        a2 += c2;
+      }
+      t0 += c0;
+      t1 += c1;
+      t2 += c2;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      a0 += __shfl_down(a0, o, 64);
+      a1 += __shfl_down(a1, o, 64);
+      a2 += __shfl_down(a2, o, 64);
+      t0 += __shfl_down(t0, o, 64);
+      t1 += __shfl_down(t1, o, 64);
+      t2 += __shfl_down(t2, o, 64);
+    }
+    if (lane == 0) {
+      s_off[0] = a0;
+      s_off[1] = a1;
+      s_off[2] = a2;
+      s_tot[0] = t0;
+      s_tot[1] = t1;
+      s_tot[2] = t2;
+    }
+  }
+  __syncthreads();
+  const int base = m.counters[kCntNew], sbase = m.counters[kCntSlideBase];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int i = i0 + k;
+    const int cd = code[k];
+    const u64 rk = r;
+    r += pack3(cd);
+    if (i >= n || !(cd & 1)) continue;
+    const uint32_t s = hslot[i];
+    int rt;
+    if (cd & 2) {  // a new root (voxel_map.cpp:77-83): centre, quater_length, empty records
+      rt = base + s_off[1] + (int)((rk >> 21) & kF);
+      if (rt >= m.cap_nodes) {
+        atomicOr(&m.counters[kCntErr], 4);
+        continue;
+      }
+      const uint64_t key = m.hkey[s];
+      double c[3];
+      const int64_t kk[3] = {unpack_axis(key, 42), unpack_axis(key, 21), unpack_axis(key, 0)};
+      for (int j = 0; j < 3; j++) c[j] = (0.5 + kk[j]) * mp.vs;
+      init_node(m.hdr[rt], c, (float)(mp.vs / 4.0), 0, -1);  // records zeroed by map_reset
+      dbox_root(m.dbox + (size_t)rt * 6);
+      m.hval[s] = rt;
+    } else {
+      rt = m.hval[s];
+      m.hdr[rt].isexist = 1;
+    }
+    if (cd & 4) {
+      m.in_slide[rt] = 1;
+      m.slide[sbase + s_off[2] + (int)((rk >> 42) & kF)] = rt;
+    }
+    m.hfirst[s] = 0x7f7f7f7f;
+  }
+  if (b == ntile - 1 && tid == 0) {
+    m.counters[kCntNodes] = min(base + s_tot[1], m.cap_nodes);
+    m.counters[kCntRoots] = s_tot[1];
+    m.counters[kCntTouched] = s_tot[0];
+    m.counters[kCntSlide] = sbase + s_tot[2];
   }
 }
 
@@ -1331,7 +1449,7 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread
   if (pre)
     k_ins_prep<true><<<g, kBlock, 0, s>>>(n, nullptr, nullptr, nullptr, nullptr, nullptr, mp, ctx->st, slot, m, w.pw,
                                           w.u0,
-                                          nullptr, pre->pnt, pre->pose, pre->var_identity, nullptr);
+                                          nullptr, pre->pnt, pre->pose, pre->var_identity, nullptr, w.gran, w.ngran);
   else {
     // the push record goes through host-mapped memory, so a replayed graph
     // picks up each scan's record (the host writes it before the launch)
@@ -1339,12 +1457,16 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread
     k_ins_prep<false><<<g, kBlock, 0, s>>>(n, nd, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, ctx->ds.oi, mp, ctx->st, slot, m,
                                            w.pw,
                                            w.u0, push ? &ctx->d_in->push : nullptr, nullptr, nullptr, 0,
-                                           nd ? ctx->ds.hflags : nullptr);
+                                           nd ? ctx->ds.hflags : nullptr, w.gran, w.ngran);
   }
   const int ntile = (n + kRootTile - 1) / kRootTile;
   (void)epoch;
-  k_ins_flags<<<ntile, kBlock, 0, s>>>(n, nd, w.u0, m, w.v1, (int*)w.ac_cnt);
-  k_ins_roots_alloc<<<ntile, kBlock, 0, s>>>(n, nd, ntile, w.u0, w.v1, (const int*)w.ac_cnt, mp, m);
+  if (ctx->roots_lb && ntile <= w.ngran) {  // one launch (decoupled look-back)
+    k_ins_roots_lb<<<ntile, kBlock, 0, s>>>(n, nd, ntile, w.u0, mp, m, w.gran);
+  } else {
+    k_ins_flags<<<ntile, kBlock, 0, s>>>(n, nd, w.u0, m, w.v1, (int*)w.ac_cnt);
+    k_ins_roots_alloc<<<ntile, kBlock, 0, s>>>(n, nd, ntile, w.u0, w.v1, (const int*)w.ac_cnt, mp, m);
+  }
   if (m.shard_world > 1) {  // the thread_num quirk counts distinct roots over all shards
     k_copy_int<<<1, 64, 0, s>>>(m.counters + kCntTouched, m.counters + kCntGTouched);
     VG_TRY(shard_allreduce(ctx, m.counters + kCntGTouched, m.counters + kCntGTouched, 1, 1, 1));

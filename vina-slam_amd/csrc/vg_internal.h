@@ -201,6 +201,8 @@ struct Work {
   uint32_t* cand_bits = nullptr;  // factor candidates of an asynchronous recut, one bit per node id
   int* plan = nullptr;         // per-leaf point_fix copy plan (margi)
   // the recut's odd levels: subdividing leaves, rcinfo, events (even levels: list2, v1, k0)
+  unsigned long long* gran = nullptr;  // per 1024-point tile: the root registration's look-back granules
+  int ngran = 0;
   int* sub_odd = nullptr;
   int* info_odd = nullptr;
   uint64_t* ev_odd = nullptr;
@@ -424,6 +426,7 @@ struct vg_ctx {
   long prof_runs = 0;
   int rc_total = 0, rc_thread_num = 0;  // the last recut's window point total / thread_num (its resume)
   bool prof_stages = false;  // per-stage events (vg_profile bit 1)
+  bool roots_lb = true;      // root registration in one look-back launch (vgx_debug 16: 0 = two launches)
   bool ba_graph = true;      // LM iterations replay one captured graph each (vgx_debug 15: 0 = direct launches)
   bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)
   unsigned* d_sync = nullptr;  // hand-off flags: [0] margi leaf -> next IEKF, [1] IEKF -> insert

@@ -810,6 +810,10 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     VG_HIP(hipMemcpy(ctx->shard.d_seq, &s, sizeof(s), hipMemcpyHostToDevice));
     return VG_OK;
   }
+  if (key == 16) {  // 0: root registration as k_ins_flags + k_ins_roots_alloc
+    ctx->roots_lb = value != 0;
+    return VG_OK;
+  }
   if (key == 15) {  // 0: the LM iterations as direct launches (no graph per iteration)
     ctx->ba_graph = value != 0;
     return VG_OK;
