@@ -363,6 +363,7 @@ struct vg_ctx {
   hipGraphExec_t g_iekf[3] = {nullptr, nullptr, nullptr};
   hipGraphExec_t g_margi[2] = {};  // margi after the window view (map.hip map_margi): ungated, gated
   hipGraphExec_t g_ba = nullptr;     // one LM iteration (ba.hip ba_run)
+  hipGraphExec_t g_ba2 = nullptr;    // the first two LM iterations
   hipGraphExec_t g_ds = nullptr;     // the per-scan downsample chain (downsample.hip ds_enqueue_hashed)
   // steady state: the insert + recut of one scan, per ring position mp[0] (pipeline.cpp stage_insert_recut)
   hipGraphExec_t g_mid[vg::kMaxWin] = {};
@@ -427,6 +428,7 @@ struct vg_ctx {
   int rc_total = 0, rc_thread_num = 0;  // the last recut's window point total / thread_num (its resume)
   bool prof_stages = false;  // per-stage events (vg_profile bit 1)
   bool roots_lb = true;      // root registration in one look-back launch (vgx_debug 16: 0 = two launches)
+  bool ba_graph2 = true;     // the first two LM iterations as one graph (vgx_debug 17: 0 = one graph each)
   bool ba_graph = true;      // LM iterations replay one captured graph each (vgx_debug 15: 0 = direct launches)
   bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)
   unsigned* d_sync = nullptr;  // hand-off flags: [0] margi leaf -> next IEKF, [1] IEKF -> insert

@@ -259,6 +259,7 @@ int vg_destroy(vg_ctx* ctx) {
   for (auto& g : ctx->g_margi)
     if (g) (void)hipGraphExecDestroy(g);
   if (ctx->g_ba) (void)hipGraphExecDestroy(ctx->g_ba);
+  if (ctx->g_ba2) (void)hipGraphExecDestroy(ctx->g_ba2);
   if (ctx->g_ds) (void)hipGraphExecDestroy(ctx->g_ds);
   for (auto& g : ctx->g_mid)
     if (g) (void)hipGraphExecDestroy(g);
@@ -808,6 +809,10 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     VG_HIP(hipMemcpy(&s, ctx->shard.d_seq, sizeof(s), hipMemcpyDeviceToHost));
     s += (unsigned)value;
     VG_HIP(hipMemcpy(ctx->shard.d_seq, &s, sizeof(s), hipMemcpyHostToDevice));
+    return VG_OK;
+  }
+  if (key == 17) {  // 0: one graph per LM iteration (no two-iteration graph)
+    ctx->ba_graph2 = value != 0;
     return VG_OK;
   }
   if (key == 16) {  // 0: root registration as k_ins_flags + k_ins_roots_alloc
