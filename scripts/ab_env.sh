@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 IFS=';' read -ra CFGS <<< "$AB_DEBUG"
-for i in 1 2 3; do
+for i in $(seq 1 ${AB_ROUNDS:-3}); do
   for v in A "${CFGS[@]}"; do
     if [ "$v" = A ]; then unset VG_BENCH_DEBUG; tag=A; else export VG_BENCH_DEBUG=$v; tag=B_${v//[=,]/_}; fi
     timeout -k 10 200 python bench.py --no-cpu --stage-scans 0 --target-steps 0 --no-h2d --multi= --multi-1m= > gpurun_out/ab_$tag$i.json 2>/dev/null || { echo "bench $v failed"; exit 1; }

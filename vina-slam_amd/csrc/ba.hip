@@ -409,10 +409,40 @@ __device__ __forceinline__ double quad_bcast(double v, int qd) {
   }
 }
 
+// the LiDAR Hessian / gradient / residual (k_ba_hess's outputs) as k_ba_prep
+// reads them: summed already (hl, k_ba_hfinal ran), or summed here from the
+// chunk partials in k_ba_hfinal's order (8 strided lane sums, then the fixed
+// shuffle tree), so each entry is formed where it is used and the separate
+// reduction launch goes (every lower entry is read by one tile, once)
+struct HlSrc {
+  const double* hl;
+  const double* part;  // non-null: sum the partials
+  int nchunk, nout;
+  __device__ __forceinline__ double operator[](int e) const {
+    if (!part) return hl[e];
+    double s[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) s[j] = 0.0;
+    int b0 = 0;
+    for (; b0 + 8 <= nchunk; b0 += 8) {
+      double v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) v[j] = part[(size_t)(b0 + j) * nout + e];
+#pragma unroll
+      for (int j = 0; j < 8; j++) s[j] += v[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (b0 + j < nchunk) s[j] += part[(size_t)(b0 + j) * nout + e];
+    const double t0 = s[0] + s[4], t1 = s[1] + s[5], t2 = s[2] + s[6], t3 = s[3] + s[7];
+    return (t0 + t2) + (t1 + t3);
+  }
+};
+
 // one assembled lower entry (R >= C) of the 15W x 15W system in the host
 // loop's accumulation order (divide_thread 215-222: IMU factors k ascending,
 // x imu_coef, then hess_plus 171-179 adds the LiDAR 6x6 blocks)
-__device__ __forceinline__ double asm_entry(int R, int C, int nimu, double imu_coef, const double* hl,
+__device__ __forceinline__ double asm_entry(int R, int C, int nimu, double imu_coef, const HlSrc& hl,
                                             const double* imuout, int L) {
   const int bR = R / 15, bC = C / 15, rR = R % 15, rC = C % 15;
   double v = 0.0;
@@ -425,7 +455,7 @@ __device__ __forceinline__ double asm_entry(int R, int C, int nimu, double imu_c
   }
   return v;
 }
-__device__ __forceinline__ double asm_grad(int t, int nimu, double imu_coef, const double* hl, const double* imuout,
+__device__ __forceinline__ double asm_grad(int t, int nimu, double imu_coef, const HlSrc& hl, const double* imuout,
                                            int L) {
   const int b = t / 15, r = t % 15;
   double v = 0.0;
@@ -447,7 +477,8 @@ __device__ __forceinline__ double asm_grad(int t, int nimu, double imu_coef, con
 // columns, zero gradient) are decoupled from the rest, so wherever Eigen's
 // pivot order puts them their elimination changes nothing and their solution
 // is 0: they are left out of the factored system (n - 15 unknowns).
-__global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coef, const double* __restrict__ hl,
+__global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coef, double* __restrict__ hl,
+                                                 const double* __restrict__ part, const int* __restrict__ nfp, int chunk,
                                                  const double* __restrict__ imuout, double* __restrict__ Hcalc,
                                                  double* __restrict__ Jcalc, double* __restrict__ timg,
                                                  double* __restrict__ bvec, double* __restrict__ dvec,
@@ -461,8 +492,10 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
   const int tid = threadIdx.x, q = blockIdx.x;
   const bool calc = st->calc_hess != 0;
   const double u = st->u;
+  const int nl = L * (L + 1) / 2, nout = nl + L + 1;
+  const HlSrc hs{hl, part, part ? (*nfp + chunk - 1) / chunk : 0, nout};
   for (int t = tid; t < n; t += blockDim.x)
-    Dv[t] = t < 15 ? 1.0 : (calc ? asm_entry(t, t, nimu, imu_coef, hl, imuout, L) : Hcalc[lo(t, t)]);
+    Dv[t] = t < 15 ? 1.0 : (calc ? asm_entry(t, t, nimu, imu_coef, hs, imuout, L) : Hcalc[lo(t, t)]);
   __syncthreads();
   for (int i = 15 + tid; i < n; i += blockDim.x) {  // rank of |D + u D| descending, index ascending on ties
     const unsigned long long ki = (unsigned long long)__double_as_longlong(fabs(Dv[i] + u * Dv[i]));
@@ -484,7 +517,7 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
       v = (R == C) ? 1.0 : 0.0;
     } else {
       const int pr = ip[R], pc = ip[C], a = pr > pc ? pr : pc, bb = pr > pc ? pc : pr;
-      const double raw = calc ? asm_entry(a, bb, nimu, imu_coef, hl, imuout, L) : Hcalc[lo(a, bb)];
+      const double raw = calc ? asm_entry(a, bb, nimu, imu_coef, hs, imuout, L) : Hcalc[lo(a, bb)];
       if (calc && R >= C) Hcalc[lo(a, bb)] = raw;
       v = (pr == pc) ? Dv[pr] + u * Dv[pr] : raw;
     }
@@ -492,8 +525,9 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
   }
   if (q == 0) {
     for (int t = tid; t < n; t += blockDim.x) {
-      const double raw = calc ? asm_grad(t, nimu, imu_coef, hl, imuout, L) : Jcalc[t];
+      const double raw = calc ? asm_grad(t, nimu, imu_coef, hs, imuout, L) : Jcalc[t];
       if (calc) Jcalc[t] = raw;
+      if (calc && part && t < L + 1) hl[nl + t] = hs[nl + t];  // gradient + residual for k_ba_control
       Jg[t] = t < 15 ? 0.0 : raw;
       dvec[t] = Dv[t];
       if (t < m) ipg[t] = ip[t];
@@ -891,6 +925,131 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
 #endif
 }
 
+// LM bookkeeping (optimizers.cpp:480-515): k_ba_control, or
+// k_ba_resid's IMU workgroup (CtlArg::err set, unsharded; resid_bookkeeping)
+struct CtlArg {
+  int W, nimu, nrb, nl;
+  double imu_coef;
+  const double* hl;
+  const double* imuout;
+  const double* imures;
+  const double* rpart;
+  double* xs;
+  const double* xt;
+  double* bias;
+  BaState* st;
+  Pub* pub;
+  int* err;   // k_ba_resid runs the bookkeeping (nullptr: k_ba_control follows); error bit 64 on a stalled hand-off
+};
+// `pre`: the lane's strided sum of the residual partials, already formed (k_ba_resid)
+__device__ __forceinline__ void ba_control_body(const CtlArg& c, const double* pre = nullptr) {
+  __shared__ int accept;
+  __shared__ double s_r[256];
+  {  // residual partials: lane-strided sums, then a fixed tree (deterministic)
+    double part = 0.0;
+    if (pre) part = *pre;
+    else if (!c.st->done)
+      for (int b = threadIdx.x; b < c.nrb; b += blockDim.x) part += c.rpart[b];
+    s_r[threadIdx.x] = part;
+    __syncthreads();
+    for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) s_r[threadIdx.x] += s_r[threadIdx.x + w];
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) {
+    accept = -1;
+    if (!c.st->done) {
+      if (c.st->calc_hess) c.st->nhess += 1;
+      if (c.st->calc_hess) {  // residual1 of divide_thread at the current state
+        double r = 0.0;
+        for (int k = 0; k < c.nimu; k++) r += c.imuout[(size_t)k * 931 + 930];
+        r *= c.imu_coef * 0.5;
+        r += c.hl[c.nl];
+        c.st->res1 = r;
+      }
+      double r1 = 0.0;
+      for (int k = 0; k < c.nimu; k++) r1 += c.imures[k];
+      r1 *= c.imu_coef * 0.5;
+      const double r2 = s_r[0];
+      const double residual2 = r1 + r2;
+      c.st->res2 = residual2;
+      const double residual1 = c.st->res1;
+      double q = residual1 - residual2;
+      if (q > 0) {
+        accept = 1;
+        const double one_three = 1.0 / 3;
+        q = q / c.st->q1;
+        c.st->v = 2;
+        q = 1 - pow(2 * q - 1, 3);
+        c.st->u *= (q < one_three ? one_three : q);
+        c.st->calc_hess = 1;
+      } else {
+        accept = 0;
+        c.st->u = c.st->u * c.st->v;
+        c.st->v = 2 * c.st->v;
+        c.st->calc_hess = 0;
+      }
+      c.st->iters += 1;
+      if (fabs((residual1 - residual2) / residual1) < 1e-6) c.st->done = 1;
+    }
+  }
+  __syncthreads();
+  if (accept == 1) {
+    for (int t = threadIdx.x; t < c.W * kX; t += blockDim.x) c.xs[t] = c.xt[t];
+  } else if (accept == 0) {
+    for (int t = threadIdx.x; t < c.nimu * 6; t += blockDim.x) {
+      int k = t / 6, j = t % 6;
+      c.bias[k * 12 + j] = c.bias[k * 12 + 6 + j];
+    }
+  }
+  if (threadIdx.x == 0) {  // LM flags -> host (read without draining the stream)
+    c.st->fin = (c.st->done || c.st->iters >= 10) ? 1 : 0;
+    const int seq = c.st->seq;  // one publication per launch, numbered on the device (graph replays)
+    c.st->seq = seq + 1;
+    pub_store(&c.pub->ba_done, c.st->done);
+    pub_store(&c.pub->ba_iters, c.st->iters);
+    pub_flag(&c.pub->seq_ba, seq);
+  }
+}
+__global__ void __launch_bounds__(256) k_ba_control(CtlArg c) { ba_control_body(c); }
+
+// The LM bookkeeping inside k_ba_resid, without a fence per workgroup (an
+// agent-scope release writes back the XCD's L2): every residual slot starts
+// as a sentinel NaN (k_ba_init, and the reader re-arms it), each workgroup
+// stores its partial with one relaxed agent-scope 64-bit store, and the IMU
+// workgroup (the last dispatched) polls the slots until none holds the
+// sentinel, then runs k_ba_control's body on the values it read.
+constexpr unsigned long long kRpartEmpty = 0x7ff4deadbeef0001ull;  // a NaN payload arithmetic never produces
+__device__ __forceinline__ void rpart_put(double* slot, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(slot), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void resid_bookkeeping(const CtlArg& c) {
+  __shared__ int s_late;
+  if (threadIdx.x == 0) s_late = 0;
+  __syncthreads();
+  double part = 0.0;  // k_ba_control's lane-strided order: slots t, t + 256, ...
+  for (int b = threadIdx.x; b < c.nrb; b += blockDim.x) {
+    unsigned long long* p = reinterpret_cast<unsigned long long*>(const_cast<double*>(c.rpart) + b);
+    unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int spin = 0; v == kRpartEmpty; spin++) {
+      if (spin > (1 << 22)) {  // ~seconds: a workgroup never stored (should not happen)
+        s_late = 1;
+        v = 0ull;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __hip_atomic_store(p, kRpartEmpty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next launch
+    part += __longlong_as_double((long long)v);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && s_late) atomicOr(c.err, 64);
+  ba_control_body(c, &part);
+}
+
 // evaluate_only_residual (factors.cpp:128-158) at the trial poses. A chunk of
 // 256/W factors per workgroup step: lane (f, i) moves factor f's frame-i
 // cluster to the trial pose (independent work, in parallel), then lane f merges
@@ -901,13 +1060,21 @@ __global__ void __launch_bounds__(256, 2) k_ba_resid(const int* __restrict__ nfp
                                                   const Clu* __restrict__ pcr_fix, const Clu* __restrict__ pcrs,
                                                   const int* __restrict__ mpring, const double* __restrict__ xt,
                                                   double* __restrict__ fac_eig, Clu* __restrict__ fac_pcr,
-                                                  double* __restrict__ rpart, const BaState* __restrict__ st, int nrb,
+                                                  double* __restrict__ rpart, const BaState* st, int nrb,
                                                   int nimu, const double* __restrict__ imurec,
                                                   const int* __restrict__ imu_head,
-                                                  const double* __restrict__ bias, double* __restrict__ imures) {
-  if (st->done) return;
+                                                  const double* __restrict__ bias, double* __restrict__ imures,
+                                                  CtlArg ctl) {
+  if (st->done) {  // converged: the bookkeeping still publishes the flags
+    if (ctl.err && (int)blockIdx.x == nrb) ba_control_body(ctl);
+    return;
+  }
   if ((int)blockIdx.x >= nrb) {  // IMU residuals at the trial state in the same launch
     if ((int)threadIdx.x < nimu) imu_residual_lane(threadIdx.x, imurec, *imu_head, bias, xt, imures);
+    if (ctl.err) {
+      __syncthreads();  // imures, read by thread 0 of this workgroup
+      resid_bookkeeping(ctl);
+    }
     return;
   }
   __shared__ Clu s_t[256];
@@ -952,7 +1119,7 @@ __global__ void __launch_bounds__(256, 2) k_ba_resid(const int* __restrict__ nfp
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) rpart[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+  if (threadIdx.x == 0) rpart_put(&rpart[blockIdx.x], ((red[0] + red[1]) + red[2]) + red[3]);
 }
 
 // sharded mode: this shard's factor residual (ordered sum of the block partials)
@@ -966,88 +1133,17 @@ __global__ void k_ba_rsum(int nrb, const double* __restrict__ rpart, double* __r
   }
 }
 
-// LM bookkeeping (optimizers.cpp:480-515)
-__global__ void __launch_bounds__(256) k_ba_control(int W, int nimu, int nrb, double imu_coef, const double* __restrict__ hl, int nl,
-                             const double* __restrict__ imuout, const double* __restrict__ imures,
-                             const double* __restrict__ rpart, double* __restrict__ xs,
-                             const double* __restrict__ xt, double* __restrict__ bias, BaState* __restrict__ st,
-                             Pub* __restrict__ pub) {
-  __shared__ int accept;
-  __shared__ double s_r[256];
-  {  // residual partials: lane-strided sums, then a fixed tree (deterministic)
-    double part = 0.0;
-    if (!st->done)
-      for (int b = threadIdx.x; b < nrb; b += blockDim.x) part += rpart[b];
-    s_r[threadIdx.x] = part;
-    __syncthreads();
-    for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
-      if ((int)threadIdx.x < w) s_r[threadIdx.x] += s_r[threadIdx.x + w];
-      __syncthreads();
-    }
-  }
-  if (threadIdx.x == 0) {
-    accept = -1;
-    if (!st->done) {
-      if (st->calc_hess) st->nhess += 1;
-      if (st->calc_hess) {  // residual1 of divide_thread at the current state
-        double r = 0.0;
-        for (int k = 0; k < nimu; k++) r += imuout[(size_t)k * 931 + 930];
-        r *= imu_coef * 0.5;
-        r += hl[nl];
-        st->res1 = r;
-      }
-      double r1 = 0.0;
-      for (int k = 0; k < nimu; k++) r1 += imures[k];
-      r1 *= imu_coef * 0.5;
-      const double r2 = s_r[0];
-      const double residual2 = r1 + r2;
-      st->res2 = residual2;
-      const double residual1 = st->res1;
-      double q = residual1 - residual2;
-      if (q > 0) {
-        accept = 1;
-        const double one_three = 1.0 / 3;
-        q = q / st->q1;
-        st->v = 2;
-        q = 1 - pow(2 * q - 1, 3);
-        st->u *= (q < one_three ? one_three : q);
-        st->calc_hess = 1;
-      } else {
-        accept = 0;
-        st->u = st->u * st->v;
-        st->v = 2 * st->v;
-        st->calc_hess = 0;
-      }
-      st->iters += 1;
-      if (fabs((residual1 - residual2) / residual1) < 1e-6) st->done = 1;
-    }
-  }
-  __syncthreads();
-  if (accept == 1) {
-    for (int t = threadIdx.x; t < W * kX; t += blockDim.x) xs[t] = xt[t];
-  } else if (accept == 0) {
-    for (int t = threadIdx.x; t < nimu * 6; t += blockDim.x) {
-      int k = t / 6, j = t % 6;
-      bias[k * 12 + j] = bias[k * 12 + 6 + j];
-    }
-  }
-  if (threadIdx.x == 0) {  // LM flags -> host (read without draining the stream)
-    st->fin = (st->done || st->iters >= 10) ? 1 : 0;
-    const int seq = st->seq;  // one publication per launch, numbered on the device (graph replays)
-    st->seq = seq + 1;
-    pub_store(&pub->ba_done, st->done);
-    pub_store(&pub->ba_iters, st->iters);
-    pub_flag(&pub->seq_ba, seq);
-  }
-}
-
 struct MpRing {
   int mp[kMaxW];
 };
 // LM state (optimizers.cpp:436-441), the reduced-Hessian accumulator, the ring
 __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict__ hl, double* __restrict__ hl_part,
                                                  int nout, MpRing ring, int* __restrict__ mpring, int W,
-                                                 const int* __restrict__ rc_status, int seq0) {
+                                                 const int* __restrict__ rc_status, int seq0, double* __restrict__ rpart,
+                                                 int nrb) {
+  for (int b = threadIdx.x; b < nrb; b += blockDim.x)  // empty residual slots (resid_bookkeeping)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(rpart + b), kRpartEmpty, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   for (int t = threadIdx.x; t < nout; t += blockDim.x) {
     hl[t] = 0.0;
     hl_part[t] = 0.0;
@@ -1217,7 +1313,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   double* rsum = ctx->shard.d_buf + 256;  // [0]: this shard's residual, [1]: all-reduced
   const int seq0 = ctx->pub_seq + 1;
   ctx->pub_seq += 10;
-  k_ba_init<<<1, 256, 0, s>>>(d.st, d.hl, hl_part, nout, ring, d.mpring, W, map_rc_status(ctx), seq0);
+  k_ba_init<<<1, 256, 0, s>>>(d.st, d.hl, hl_part, nout, ring, d.mpring, W, map_rc_status(ctx), seq0, d.rpart, kResidBlocks);
   VG_HIP(flush_insert_events(ctx));
   // factor count on the device (the recut's kCntFactors): fixed grids, so an
   // asynchronous recut needs no host round trip before the LM
@@ -1237,12 +1333,19 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   // factor count, the flags and the publication number live on the device),
   // so an unsharded run replays one captured graph per iteration; the sampled
   // solve-timing runs launch directly (events around k_ba_solve).
+  CtlArg ctl{W, nimu, sharded ? 1 : nrb, nl + L, ctx->cfg.imu_coef, d.hl, d.imuout, d.imures,
+             sharded ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st, ctx->d_pub, nullptr};
+  CtlArg ctl_fused = ctl;  // unsharded: the bookkeeping rides in k_ba_resid's IMU workgroup
+  if (!sharded && ctx->ba_fuse_ctl) ctl_fused.err = ctx->map.counters + kCntErr;
   auto enqueue = [&](int k) {
     k_ba_hess<<<G + nimu, kHessThreads, hess_lds, s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
                                                       ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, nimu, d.imurec, &ctx->st->imu_head,
                                                       d.bias, d.imuout);
-    k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, sharded ? hl_part : d.hl,
-                                                       d.st);
+    // unsharded, k_ba_prep sums the chunk partials itself (HlSrc)
+    const bool fuse = ctx->ba_fuse_final && !sharded && !(k == 0 && ctx->dbg_capture == 1);
+    if (!fuse)
+      k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, sharded ? hl_part : d.hl,
+                                                         d.st);
     // sharded: every shard's factors -> one LiDAR Hessian / gradient / residual
     // (out of place: a rejected step re-reduces the unchanged partial)
     if (sharded && xerr == VG_OK) xerr = shard_allreduce(ctx, hl_part, d.hl, nout, 0, 3);
@@ -1253,7 +1356,8 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
       ctx->dbg_cap_n = nout + nimu * 931;
       ctx->dbg_capture = 2;
     }
-    k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
+    k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, fuse ? d.part : nullptr, nfp, hess_chunk(W),
+                                    d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
                                     d.dvec, d.jvec, d.ipg, d.st);
     if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][0], s);
     k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
@@ -1261,14 +1365,12 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
     if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][1], s);
     k_ba_resid<<<nrb + 1, 256, 0, s>>>(nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
                                        ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, nimu, d.imurec, &ctx->st->imu_head, d.bias,
-                                       d.imures);
+                                       d.imures, ctl_fused);
     if (sharded) {  // the residual over every shard's factors
       k_ba_rsum<<<1, 64, 0, s>>>(nrb, d.rpart, rsum, d.st);
       if (xerr == VG_OK) xerr = shard_allreduce(ctx, rsum, rsum + 1, 1, 0, 4);
     }
-    k_ba_control<<<1, 256, 0, s>>>(W, nimu, sharded ? 1 : nrb, ctx->cfg.imu_coef, d.hl, nl + L,
-                                   d.imuout, d.imures, sharded ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st,
-                                   ctx->d_pub);
+    if (!ctl_fused.err) k_ba_control<<<1, 256, 0, s>>>(ctl);
   };
   const bool graph = ctx->use_graphs && ctx->ba_graph && !sharded && !solve_ev && ctx->dbg_capture != 1;
   if (graph && !ctx->g_ba) {
@@ -1403,7 +1505,7 @@ int ba_lidar_pass(vg_ctx* ctx, bool hessian, const double* poses, const int* mp_
   const int nrb = kResidBlocks;
   k_ba_resid<<<nrb, 256, 0, s>>>(nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
                                  ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, 0, d.imurec, &ctx->st->imu_head,
-                                 d.bias, d.imures);
+                                 d.bias, d.imures, CtlArg{});
   VG_HIP(hipGetLastError());
   VG_HIP(hipMemcpyAsync(h, d.rpart, nrb * sizeof(double), hipMemcpyDeviceToHost, s));
   VG_HIP(hipStreamSynchronize(s));

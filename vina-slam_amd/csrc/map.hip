@@ -46,6 +46,7 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(m.dbox = ctx->arena.take<double>(cn * 6));
   good &= ok(m.pcrs = ctx->arena.take<Clu>(cn * W));
   good &= ok(m.nscr = ctx->arena.take<int>(cn * 4));
+  good &= ok(m.pend = ctx->arena.take<unsigned long long>(cn));
   good &= ok(m.cfirst = ctx->arena.take<int>(cn * 8));
   good &= ok(m.hkey = ctx->arena.take<uint64_t>(hs));
   good &= ok(m.hval = ctx->arena.take<int>(hs));
@@ -98,6 +99,7 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(w.ev_odd = ctx->arena.take<uint64_t>(w.cap));
   w.nparts = 1024;
   good &= ok(w.partials = ctx->arena.take<double>((size_t)w.nparts * 40));
+  good &= ok(w.islots = ctx->arena.take<double>((size_t)4 * kIekfAllMax * kIekfVals));
   if (!good) {
     ctx->err = "arena exhausted (map)";
     return VG_E_CAPACITY;
@@ -267,40 +269,37 @@ __device__ __forceinline__ void halve(const double (&v)[N], double (&w)[(N + 1) 
 // read from the device state the previous k_iekf_update wrote; the kernel is a
 // no-op once the IEKF has finished (st->done). Iteration 0 ignores the leaf
 // cache (no association yet, odometry.cpp:111-132).
-__global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, int it, DevMap m,
-                                              int* __restrict__ cache, double* __restrict__ partials,
-                                              int* __restrict__ pk) {
-  if (st->done) return;
-  const bool clk_on = st->clk.on != 0;
-  const int clk_slot = (st->clk.scan * 4 + it) & (kClkRing - 1);
-  if (clk_on && blockIdx.x == 0 && threadIdx.x == 0) {
-    st->clk.t0[clk_slot] = (unsigned long long)wall_clock64();
-    st->clk.exec[clk_slot] = 1;
-  }
-  VG_PROBE_BEGIN();
+// Fused form (npt < gridDim.x): workgroup npt, dispatched last, runs the
+// update itself: it takes the point-loop workgroups' partials from their
+// slots as they land (iekf_reduce_spin: relaxed agent-scope stores and
+// loads, no fence per workgroup) — no separate k_iekf_update launch.
+__device__ __forceinline__ void iekf_fused_update(DState* __restrict__ st, int it, int npt, double* partials,
+                                               int* __restrict__ err) {
+  __shared__ IekfLds L;
+  __shared__ int s_late;
+  if (threadIdx.x == 0) s_late = 0;
+  __syncthreads();
+  int late = 0;
+  const int n = st->sn;
+  iekf_reduce_spin(npt, n < npt * 256 ? (n + 255) / 256 : npt, partials, L, &late);
+  if (late) s_late = 1;
+  __syncthreads();
+  if (threadIdx.x == 0 && s_late) atomicOr(err, 64);
+  iekf_update_tail(st, it, L);
+}
+// one IEKF iteration's point loop over the workgroup's chunk vb (k_iekf,
+// k_iekf_all): the 34 sums of this lane's points
+__device__ __forceinline__ void iekf_points(const MP& mp, const DState* __restrict__ st, const DevMap& m,
+                                            int* __restrict__ cache, int* __restrict__ pk, int it, int nb, int vb,
+                                            const M3& R, const V3& p, const M3& rot_var, const M3& tsl_var,
+                                            double (&acc)[kIekfVals]) {
   const int n = st->sn;
   const float* __restrict__ x = st->sx;
   const float* __restrict__ y = st->sy;
   const float* __restrict__ z = st->sz;
-  double acc[kIekfVals];
-  for (int j = 0; j < kIekfVals; j++) acc[j] = 0.0;
-  const double* xc = st->xc;
-  M3 R, rot_var, tsl_var;
-  for (int r = 0; r < 3; r++)
-    for (int c = 0; c < 3; c++) {
-      R(r, c) = xc[r * 3 + c];
-      rot_var(r, c) = xc[kXS + r * 15 + c];
-      tsl_var(r, c) = xc[kXS + (3 + r) * 15 + 3 + c];
-    }
-  const V3 p = ld_v3(xc + 9);
   const M3 Rt = tr(R);
-  // XCD-aware chunking (cdna_hip_programming.md T1): blocks are dealt
-  // round-robin over the 8 XCDs, so block b works on chunk (b % 8) * (nb / 8)
-  // + b / 8 — each XCD sweeps a contiguous run of the scan and the plane /
-  // node records of neighbouring points stay in its own L2 (nb % 8 == 0)
-  const int nb = gridDim.x;
-  const int vb = (nb % 8 == 0) ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
-  for (int i = vb * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  for (int j = 0; j < kIekfVals; j++) acc[j] = 0.0;
+  for (int i = vb * blockDim.x + threadIdx.x; i < n; i += nb * blockDim.x) {
     V3 pnt;
     M3 var;
     var_init_pt(mp, x[i], y[i], z[i], pnt, var);
@@ -371,13 +370,13 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
       acc[33] += 1.0;
     }
   }
-  if (blockIdx.x == 0) VG_PROBE_MARK(30);  // the point loop (thread 0 of block 0)
-  // block reduction: a halving butterfly per wave, then LDS across the 4
-  // waves (fixed tree). Every level pairs lane ^ L for L = 32, 16, ..., 1, so
-  // each sum is bit for bit lane 0's of a shfl_down tree, but a lane hands
-  // over half of the values it carries at every level: 37 exchanges for the
-  // 34 sums instead of 204, through permlane / DPP instead of LDS
-  __shared__ double red[4][kIekfVals];
+}
+// the workgroup's 34 sums (threads < 34 hold one each): a halving butterfly
+// per wave, then LDS across the 4 waves (fixed tree). Every level pairs lane ^
+// L for L = 32, 16, ..., 1, so each sum is bit for bit lane 0's of a shfl_down
+// tree, but a lane hands over half of the values it carries at every level:
+// 37 exchanges for the 34 sums instead of 204, through permlane / DPP
+__device__ __forceinline__ double iekf_wg_sum(double (&acc)[kIekfVals], double (*red)[kIekfVals]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   static_assert(kIekfVals == 34, "the halving levels below are laid out for 34 sums");
   int ridx = 0, rn = kIekfVals;
@@ -390,9 +389,64 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
   halve<1>(h2, h1, lane, ridx, rn);
   if (rn == 1) red[wv][ridx] = h1[0];
   __syncthreads();
+  const int j = threadIdx.x < kIekfVals ? threadIdx.x : 0;
+  return ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+}
+// the pose words an iteration's point loop reads from x_curr: R 9, p 3, the
+// rotation and translation covariance blocks 9 + 9
+__device__ __forceinline__ double pose_word(const double* xc, int t) {
+  if (t < 12) return xc[t];
+  if (t < 21) return xc[kXS + ((t - 12) / 3) * 15 + (t - 12) % 3];
+  return xc[kXS + (3 + (t - 21) / 3) * 15 + 3 + (t - 21) % 3];
+}
+__device__ __forceinline__ void pose_of(const double* w, M3& R, V3& p, M3& rot_var, M3& tsl_var) {
+  for (int q = 0; q < 9; q++) {
+    R[q] = w[q];
+    rot_var[q] = w[12 + q];
+    tsl_var[q] = w[21 + q];
+  }
+  p = v3(w[9], w[10], w[11]);
+}
+
+__global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, int it, DevMap m,
+                                              int* __restrict__ cache, double* __restrict__ partials,
+                                              int* __restrict__ pk, int npt) {
+  if (st->done) return;
+  if ((int)blockIdx.x >= npt) {
+    iekf_fused_update(st, it, npt, partials, m.counters + kCntErr);
+    return;
+  }
+  const bool clk_on = st->clk.on != 0;
+  const int clk_slot = (st->clk.scan * 4 + it) & (kClkRing - 1);
+  if (clk_on && blockIdx.x == 0 && threadIdx.x == 0) {
+    st->clk.t0[clk_slot] = (unsigned long long)wall_clock64();
+    st->clk.exec[clk_slot] = 1;
+  }
+  VG_PROBE_BEGIN();
+  const int n = st->sn;
+  double w[30];
+  for (int t = 0; t < 30; t++) w[t] = pose_word(st->xc, t);
+  M3 R, rot_var, tsl_var;
+  V3 p;
+  pose_of(w, R, p, rot_var, tsl_var);
+  // XCD-aware chunking (cdna_hip_programming.md T1): blocks are dealt
+  // round-robin over the 8 XCDs, so block b works on chunk (b % 8) * (nb / 8)
+  // + b / 8 — each XCD sweeps a contiguous run of the scan and the plane /
+  // node records of neighbouring points stay in its own L2 (nb % 8 == 0)
+  const int nb = npt;
+  const int vb = iekf_chunk(blockIdx.x, nb);
+  if ((int)gridDim.x > npt && vb * (int)blockDim.x >= n) {  // no points (fused form: no partial either)
+    if (clk_on && blockIdx.x < kClkBlocks && threadIdx.x == 0) st->clk.tend[clk_slot][blockIdx.x] = (unsigned long long)wall_clock64();
+    return;
+  }
+  double acc[kIekfVals];
+  iekf_points(mp, st, m, cache, pk, it, nb, vb, R, p, rot_var, tsl_var, acc);
+  if (blockIdx.x == 0) VG_PROBE_MARK(30);  // the point loop (thread 0 of block 0)
+  __shared__ double red[4][kIekfVals];
+  const double v = iekf_wg_sum(acc, red);
   if (threadIdx.x < kIekfVals) {
-    int j = threadIdx.x;
-    partials[(size_t)blockIdx.x * kIekfVals + j] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+    if ((int)gridDim.x > npt) slot_put(&partials[(size_t)blockIdx.x * kIekfVals + threadIdx.x], v);  // the fused update reads it
+    else partials[(size_t)blockIdx.x * kIekfVals + threadIdx.x] = v;
   }
   if (clk_on && blockIdx.x < kClkBlocks) {  // the workgroup's end (its partials written)
     __syncthreads();
@@ -402,6 +456,94 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
 #ifdef VG_PROBE
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_probe[59], 1ull);
 #endif
+}
+
+// The four IEKF iterations in one launch (odometry.cpp:98-230): npt point
+// workgroups and one update workgroup (the last dispatched), all resident at
+// once (npt + 1 <= 2 per CU: kIekfAllMax). Iteration it's partials go to slot
+// set it (iekf_reduce_spin takes and re-arms them); the update then stores the
+// next iteration's pose and the finished flag into DState::islot[it], which
+// every point workgroup polls before its next pass (relaxed agent-scope
+// stores and loads: no fence, no launch between iterations). Every wait is
+// bounded (error bit 64), so a workgroup that never became resident cannot
+// hang the GPU. Results equal k_iekf + update launches bit for bit.
+__device__ __forceinline__ void iekf_all_update(DState* __restrict__ st, int npt, double* pslots,
+                                                int* __restrict__ err) {
+  __shared__ IekfLds L;
+  __shared__ int s_late;
+  const int n = st->sn;
+  const int nact = n < npt * 256 ? (n + 255) / 256 : npt;
+  for (int it = 0; it < 4; it++) {
+    if (threadIdx.x == 0) s_late = 0;
+    __syncthreads();
+    int late = 0;
+    iekf_reduce_spin(npt, nact, pslots + (size_t)it * npt * kIekfVals, L, &late);
+    if (late) s_late = 1;
+    __syncthreads();
+    if (s_late) {  // a point workgroup never delivered: stop them all
+      if (threadIdx.x == 0) atomicOr(err, 64);
+      if (it < 3 && threadIdx.x < 31) slot_put(&st->islot[it][threadIdx.x], 1.0);
+      return;
+    }
+    iekf_update_tail(st, it, L);
+    __syncthreads();  // x_curr (thread 0 of the tail) seen by the block
+    const bool fin = L.fin != 0;
+    if (it < 3 && threadIdx.x < 31)
+      slot_put(&st->islot[it][threadIdx.x], threadIdx.x < 30 ? pose_word(st->xc, threadIdx.x) : (fin ? 1.0 : 0.0));
+    if (fin) return;
+  }
+}
+__global__ void __launch_bounds__(256) k_iekf_all(MP mp, DState* __restrict__ st, DevMap m, int* __restrict__ cache,
+                                                  double* __restrict__ pslots, int npt) {
+  if (st->done) return;
+  if ((int)blockIdx.x >= npt) {
+    iekf_all_update(st, npt, pslots, m.counters + kCntErr);
+    return;
+  }
+  const int n = st->sn;
+  const int vb = iekf_chunk(blockIdx.x, npt);
+  if (vb * (int)blockDim.x >= n) return;  // no points in any iteration (the update skips the row)
+  __shared__ double red[4][kIekfVals];
+  __shared__ double s_pose[32];
+  __shared__ int s_late;
+  const bool clk_on = st->clk.on != 0;
+  for (int it = 0; it < 4; it++) {
+    if (threadIdx.x == 0) s_late = 0;
+    __syncthreads();  // the previous pass is done with s_pose / red
+    if (threadIdx.x < 31) {
+      double v;
+      if (it == 0) {
+        v = threadIdx.x < 30 ? pose_word(st->xc, threadIdx.x) : 0.0;
+      } else {
+        int late = 0;
+        v = slot_wait(&st->islot[it - 1][threadIdx.x], &late);
+        if (late) s_late = 1;
+      }
+      s_pose[threadIdx.x] = v;
+    }
+    __syncthreads();
+    if (s_late) {
+      if (threadIdx.x == 0) atomicOr(m.counters + kCntErr, 64);
+      return;
+    }
+    if (s_pose[30] != 0.0) return;  // the update finished the IEKF
+    M3 R, rot_var, tsl_var;
+    V3 p;
+    pose_of(s_pose, R, p, rot_var, tsl_var);
+    const int clk_slot = (st->clk.scan * 4 + it) & (kClkRing - 1);
+    if (clk_on && blockIdx.x == 0 && threadIdx.x == 0) {
+      st->clk.t0[clk_slot] = (unsigned long long)wall_clock64();
+      st->clk.exec[clk_slot] = 1;
+    }
+    double acc[kIekfVals];
+    iekf_points(mp, st, m, cache, nullptr, it, npt, vb, R, p, rot_var, tsl_var, acc);
+    const double v = iekf_wg_sum(acc, red);
+    if (threadIdx.x < kIekfVals) slot_put(&pslots[((size_t)it * npt + blockIdx.x) * kIekfVals + threadIdx.x], v);
+    if (clk_on && blockIdx.x < kClkBlocks) {
+      __syncthreads();
+      if (threadIdx.x == 0) st->clk.tend[clk_slot][blockIdx.x] = (unsigned long long)wall_clock64();
+    }
+  }
 }
 
 // P_k of SURVEY 8(d), the profiling pass only: distinct plane records the
@@ -456,9 +598,22 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
   (void)z;
   (void)n;  // the scan is read from the device state (state_set_scan)
   const int nb = iekf_blocks(ctx);
+  // the update inside k_iekf (one more workgroup) unless the sums are
+  // exchanged, k_iekf is timed alone, or the plane count runs in between
+  const bool fused = ctx->iekf_fused && ctx->shard.world <= 1 && !ev0 && !tag;
+  if (fused && !ctx->iekf_armed) {  // iekf_run arms the slots before a fused iteration
+    ctx->err = "fused IEKF update: partial slots not armed";
+    return VG_E_STATE;
+  }
+  if (!fused) ctx->iekf_armed = false;  // plain partials from here on
   if (ev0) VG_HIP(hipEventRecord(ev0, s));
-  k_iekf<<<nb, 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials, tag ? w.pk_leaf : nullptr);
+  k_iekf<<<nb + (fused ? 1 : 0), 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials,
+                                             tag ? w.pk_leaf : nullptr, nb);
   if (ev1) VG_HIP(hipEventRecord(ev1, s));
+  if (fused) {
+    VG_HIP(hipGetLastError());
+    return VG_OK;
+  }
   if (tag) k_iekf_planes<<<nb, 256, 0, s>>>(ctx->st, ctx->map, w.pk_leaf, tag, &ctx->st->planes[it]);
   if (ctx->shard.world > 1) {  // this shard's sums, all-reduced, then the (replicated) update
     double* sums = ctx->shard.d_buf;
@@ -485,6 +640,58 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
   else VG_TRY(state_set_scan(ctx, x, y, z, n, s));
   const bool graph = ctx->use_graphs && ctx->shard.world <= 1 && !ctx->prof_stages;
   const bool ev = ctx->prof_on && !graph;
+  // the fused update's slots start empty (iekf_reduce_spin re-arms what it
+  // reads, so this runs only after something else used the buffer); outside
+  // the captured graph
+  if (ctx->iekf_fused && ctx->shard.world <= 1 && !ev && !ctx->prof_stages && !ctx->iekf_armed) {
+    VG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctx->wk.partials), (int)kSlotEmpty32,
+                             (size_t)iekf_blocks(ctx) * kIekfVals * 2, s));
+    ctx->iekf_armed = true;
+  }
+  // the four iterations as one launch (k_iekf_all): not with another context's
+  // IEKF possibly resident beside it (multi-sequence mode turns overlap_iekf
+  // off), not when k_iekf is timed alone or the sums are exchanged
+  if (ctx->iekf_persist && ctx->iekf_fused && ctx->overlap_iekf && ctx->shard.world <= 1 && !ev && !ctx->prof_stages &&
+      ctx->iekf_all_cap >= 0) {
+    Work& w = ctx->wk;
+    if (ctx->iekf_all_cap == 0) {  // workgroups the device holds at once (a partitioned GPU holds fewer)
+      int per_cu = 0, cus = 0;
+      VG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_iekf_all, 256, 0));
+      VG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+      ctx->iekf_all_cap = per_cu * cus;
+    }
+    // at least 8 workgroups to spare (the other streams' kernels, the poll of the
+    // IEKF hand-off)
+    int npt = iekf_blocks(ctx) < kIekfAllMax ? iekf_blocks(ctx) : kIekfAllMax;
+    if (npt > ctx->iekf_all_cap - 9) npt = ctx->iekf_all_cap - 9;
+    npt = npt / 8 * 8;
+    if (npt < 64) {  // too small a device for the resident form: per-iteration launches from now on
+      ctx->iekf_all_cap = -1;
+      return iekf_run(ctx, mp, x, y, z, n, bank, nullptr, s, nullptr);
+    }
+    if (!w.islots_armed) {  // iekf_reduce_spin re-arms what it reads
+      VG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.islots), (int)kSlotEmpty32,
+                               (size_t)4 * kIekfAllMax * kIekfVals * 2, s));
+      w.islots_armed = true;
+    }
+    if (!graph || !ctx->g_iekf[1]) {
+      if (graph) VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      k_iekf_all<<<npt + 1, 256, 0, s>>>(mp, ctx->st, ctx->map, w.iekf_cache, w.islots, npt);
+      const hipError_t le = hipGetLastError();
+      if (!graph) {
+        VG_HIP(le);
+        return VG_OK;
+      }
+      hipGraph_t g = nullptr;
+      const hipError_t e = hipStreamEndCapture(s, &g);
+      VG_HIP(le);
+      VG_HIP(e);
+      VG_HIP(hipGraphInstantiate(&ctx->g_iekf[1], g, nullptr, nullptr, 0));
+      VG_HIP(hipGraphDestroy(g));
+    }
+    VG_HIP(hipGraphLaunch(ctx->g_iekf[1], s));
+    return VG_OK;
+  }
   auto enqueue = [&]() -> int {
     for (int it = 0; it < 4; it++)
       VG_TRY(iekf_iteration(ctx, mp, x, y, z, n, it, ev ? ctx->iekf_ev[bank + it][0] : nullptr,
@@ -2388,6 +2595,7 @@ __global__ void __launch_bounds__(256) k_memo_probe(MP mp, DevMap m, int* __rest
 }
 int map_memo_probe(vg_ctx* ctx, const MP& mp, int* out) {
   int* dout = reinterpret_cast<int*>(ctx->wk.partials);  // scratch: the probe runs between scans
+  ctx->iekf_armed = false;                                // (the fused update's slots are re-armed)
   VG_HIP(hipMemsetAsync(dout, 0, 4 * sizeof(int), ctx->stream));
   k_memo_probe<<<256, 256, 0, ctx->stream>>>(mp, ctx->map, dout);
   VG_HIP(hipGetLastError());
@@ -2552,6 +2760,25 @@ __device__ __forceinline__ int margi_level(int L, const DevMap& m, const int* rc
   return rc[L - 1];
 }
 
+// OctoTree::margi's bottom-up isexist (octree.cpp:485-494) without a launch
+// per level: a node whose isexist is final reports it to its parent with one
+// 64-bit atomic (children still to report in the high word, minus one; the
+// existing ones in the low word, plus its bit); the child that reports last
+// has every sibling's bit in the returned word, so it sets the parent's
+// isexist = OR(children) and reports for the parent in turn. The payload is
+// the atomic itself: no fence. Roots (parent -1) end the chain.
+__device__ __forceinline__ void margi_exist_up(DevMap& m, int node, int ex) {
+  for (int hop = 0; hop < 16; hop++) {
+    const int par = m.hdr[node].parent;
+    if (par < 0) return;
+    const unsigned long long old = atomicAdd(&m.pend[par], (unsigned long long)ex - (1ull << 32));
+    if ((old >> 32) != 1ull) return;  // a sibling reports later
+    ex = ((unsigned)(old & 0xffffffffull) + (unsigned)ex) > 0u ? 1 : 0;
+    m.hdr[par].isexist = (int8_t)ex;
+    node = par;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_collect_level(int L, int thread_num, DevMap m, int* __restrict__ lists,
                                                        int* __restrict__ leaves, int* __restrict__ rc) {
   if (g_slide(m) < thread_num) return;
@@ -2566,10 +2793,15 @@ __global__ void __launch_bounds__(256) k_collect_level(int L, int thread_num, De
     int nchild = 0, is_leaf = 0;
     int kids[8];
     if (node >= 0) {
-      const NodeHdr& h = m.hdr[node];
+      NodeHdr& h = m.hdr[node];
       if (h.octo == 1) {
         for (int o = 0; o < 8; o++)
           if (h.child[o] >= 0) kids[nchild++] = h.child[o];
+        m.pend[node] = (unsigned long long)nchild << 32;  // margi_exist_up: children still to report
+        if (nchild == 0) {  // internal_exist of a childless node: 0, reported now
+          h.isexist = 0;
+          margi_exist_up(m, node, 0);
+        }
       } else {
         is_leaf = 1;
       }
@@ -2774,12 +3006,20 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
 // block moves when it grows, then the leaf's points of the oldest frame are
 // appended in push order (octree.cpp:450-458)
 constexpr int kCopyWaves = 4;
+// exist_up: the leaves also report their isexist up the tree (margi_exist_up,
+// k_margi_erase_all follows); each leaf's report rides on a lane of its own
 __global__ void __launch_bounds__(64 * kCopyWaves) k_margi_copy(const int* __restrict__ nleaves,
                                                                 const int* __restrict__ plan,
-                                                                const WinD* __restrict__ win, DevMap m, const int* __restrict__ gate) {
+                                                                const WinD* __restrict__ win, DevMap m, const int* __restrict__ gate,
+                                                                const int* __restrict__ leaves, int exist_up) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   const int lane = threadIdx.x & 63;
   const int nl = *nleaves;
+  if (exist_up)
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nl; q += gridDim.x * blockDim.x) {
+      const int node = leaves[q];
+      margi_exist_up(m, node, m.hdr[node].isexist ? 1 : 0);
+    }
   const int s0 = win->mp[0];
   const M3 R0 = ld_m3(win->R[0]);
   const V3 p0 = ld_v3(win->p[0]);
@@ -2872,6 +3112,41 @@ __global__ void __launch_bounds__(256) k_clear_mark(int L0, int nlev, int thread
       m.nscr[(size_t)work[q] * 4 + 2] = -1;
   }
 }
+// local_mapping.cpp:67-78 + clear_slwd (octree.cpp:739-756) in one launch: a
+// node of the slide subtrees is erased with its root, so every node of every
+// level looks its root up (L parent hops) — the roots' isexist is final
+// (margi_exist_up) — instead of a top-down launch per level with dead marks
+__global__ void __launch_bounds__(256) k_margi_erase_all(int nlev, int thread_num, DevMap m, const int* __restrict__ lists,
+                                                         const int* __restrict__ rc, const int* __restrict__ gate) {
+  if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
+  if (g_slide(m) < thread_num) return;
+  const int n0 = m.counters[kCntSlide];
+  int total = n0;
+  for (int l = 1; l < nlev; l++) total += rc[l - 1];
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+    int L = 0, node;
+    if (q < n0) {
+      node = m.slide[q];
+    } else {
+      int r = q - n0, off = 0;
+      L = 1;
+      while (L < nlev - 1 && r >= rc[L - 1]) {
+        r -= rc[L - 1];
+        off += rc[L - 1];
+        L++;
+      }
+      node = lists[off + r];
+    }
+    int root = node;
+    for (int k = 0; k < L; k++) root = m.hdr[root].parent;
+    if (!m.hdr[root].isexist) {
+      m.hdr[node].has_sw = 0;
+      for (int j = 0; j < m.W; j++) clu_zero(m.pcrs[(size_t)node * m.W + j]);
+      if (L == 0) m.in_slide[node] = 0;
+    }
+  }
+}
+
 // single block, order-preserving in-place compaction of the slide list (a
 // chunk is read completely before any of it is written; writes never pass
 // the read position)
@@ -3040,12 +3315,17 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   if (ctx->pub_flags & 1) k_local_map<<<64, kBlock, 0, s>>>(dwin, m, ctx->d_cmap, ctx->d_cmap_n, gate);
   ctx->tail_a_valid = true;
   auto body = [&]() -> int {
-    k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, dwin, m, gate);
-    for (int L = nlev - 1; L >= 1; L--)
-      k_margi_internal<<<gl * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc, gate);
-    for (int L = 0; L < nlev; L++)
-      k_margi_erase_mark<<<gl * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc, gate);
-    k_clear_mark<<<gl, kBlock, 0, s>>>(nlev - 2, nlev, thread_num, m, w.list1, w.rc, gate);
+    const bool fused = ctx->margi_fused;
+    k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, dwin, m, gate, w.list0, fused ? 1 : 0);
+    if (fused) {
+      k_margi_erase_all<<<gl * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(nlev, thread_num, m, w.list1, w.rc, gate);
+    } else {
+      for (int L = nlev - 1; L >= 1; L--)
+        k_margi_internal<<<gl * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc, gate);
+      for (int L = 0; L < nlev; L++)
+        k_margi_erase_mark<<<gl * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc, gate);
+      k_clear_mark<<<gl, kBlock, 0, s>>>(nlev - 2, nlev, thread_num, m, w.list1, w.rc, gate);
+    }
     // slide list compaction, the device-state slide, the counter publication
     k_slide_compact<<<1, 1024, 0, s>>>(thread_num, m, ctx->st, wa.win_count, mp.W - 1, ctx->d_pub, -1, gate);
     VG_HIP(hipGetLastError());

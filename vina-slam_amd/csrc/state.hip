@@ -48,6 +48,10 @@ __global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict
     st->xc[t] = xa.x[t];
     st->xp[t] = xa.x[t];
   }
+  {
+    for (int t = tid; t < 3 * 32; t += blockDim.x)  // k_iekf_all's pose slots start empty
+      reinterpret_cast<unsigned long long*>(&st->islot[0][0])[t] = kSlotEmpty;
+  }
   if (tid == 0) {
     st->it = 0;
     st->rematch = 0;
@@ -69,10 +73,12 @@ __global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict
 // host's propagate() in pipeline.cpp, same expression trees) from the device's
 // x_curr, then the scan opening (k_scan_begin). One workgroup: the per-sample
 // rotations (Exp, the sin / cos) in parallel, the rotation / velocity /
-// position chain on thread 0, the F / noise blocks of each sample in
-// parallel, then cov <- F cov F^T + Q sample by sample, one lane per entry,
-// each sum in ascending column order over F's non-zeros (the host's
-// sandwich()).
+// position chain on wave 0 (one lane per matrix / vector entry, rows by
+// shuffle), the F / noise blocks of each sample in parallel, then
+// cov <- F cov F^T + Q sample by sample, one lane per entry, each sum in
+// ascending column order over F's non-zeros (the host's sandwich()). The
+// round-4 first form (the chain on one lane, per-lane index arrays for F's
+// rows) took 54 us: 11 us chain, 37 us covariance (scripts/probe_prop.py).
 __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restrict__ st, const float* x, const float* y,
                                                    const float* z, int n, int set_scan) {
   // the arguments once into LDS, by all lanes (the kernel-argument block is
@@ -121,31 +127,60 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
   }
   __syncthreads();
   VG_PROBE_MARK(2);
-  // 2. the rotation / velocity / position chain (thread 0), the final pose
-  if (tid == 0) {
-    M3 R_imu = ld_m3(xc);
-    V3 vel = v3(xc[12], xc[13], xc[14]), pos = v3(xc[9], xc[10], xc[11]);
-    const V3 g = v3(xc[21], xc[22], xc[23]);
-    V3 acc_imu = V3::Z(), angvel = V3::Z();
+  // 2. the rotation / velocity / position chain on wave 0: lane 3r+c holds
+  // R_imu(r, c), lanes 9-11 the position, 12-14 the velocity; each lane forms
+  // the acceleration component it needs from its row (the host's mul() tree)
+  __shared__ double sTail[24];
+  if (tid < 64) {
+    const int l = tid;
+    const bool isR = l < 9;
+    const int rr = isR ? l / 3 : 0, cc = l % 3;
+    const int ci = l < 9 ? rr : (l < 12 ? l - 9 : (l < 15 ? l - 12 : 0));  // its component of acc_imu / angvel
+    double Rv = isR ? xc[l] : 0.0;
+    double pv = (l >= 9 && l < 12) ? xc[9 + l - 9] : 0.0;
+    double vv = (l >= 12 && l < 15) ? xc[12 + l - 12] : 0.0;
+    const double gci = xc[21 + ci], bgc = bg[ci];
+    double acc_last = 0.0, ang_last = 0.0;
     for (int k = 0; k < ns; k++) {
-      if (!sOk[k]) continue;
+      if (!sOk[k]) continue;  // uniform
       const double* h = &a.imu[7 * k];
       const double* t = &a.imu[7 * (k + 1)];
-      V3 av, acc_avr;
-      for (int j = 0; j < 3; j++) {
-        av[j] = 0.5 * (h[1 + j] + t[1 + j]);
-        acc_avr[j] = 0.5 * (h[4 + j] + t[4 + j]);
-      }
-      angvel = sub(av, bg);
-      acc_avr = sub(scl(acc_avr, a.sg), ba);
-      acc_imu = add(mul(R_imu, acc_avr), g);
-      for (int q = 0; q < 9; q++) sRi[k][q] = R_imu[q];
+      double aa[3];
+      for (int j2 = 0; j2 < 3; j2++) aa[j2] = 0.5 * (h[4 + j2] + t[4 + j2]) * a.sg - ba[j2];
+      const double r0 = __shfl(Rv, 3 * ci, 64), r1 = __shfl(Rv, 3 * ci + 1, 64), r2 = __shfl(Rv, 3 * ci + 2, 64);
+      double s = r0 * aa[0];
+      s += r1 * aa[1];
+      s += r2 * aa[2];
+      const double acc = s + gci;  // acc_imu[ci] = (R_imu acc_avr)[ci] + g[ci]
+      if (isR) sRi[k][l] = Rv;
       const double dt = sDt[k];
-      pos = add(add(pos, scl(vel, dt)), scl(acc_imu, 0.5 * dt * dt));
-      vel = add(vel, scl(acc_imu, dt));
-      R_imu = mul(R_imu, ld_m3(sExp[k]));
+      const double velc = __shfl(vv, 12 + ci, 64);  // vel[ci] before this pair's update
+      if (l >= 9 && l < 12) pv = (pv + velc * dt) + acc * (0.5 * dt * dt);
+      if (l >= 12 && l < 15) vv = vv + acc * dt;
+      const double q0 = __shfl(Rv, 3 * rr, 64), q1 = __shfl(Rv, 3 * rr + 1, 64), q2 = __shfl(Rv, 3 * rr + 2, 64);
+      if (isR) {  // R_imu <- R_imu Exp(angvel, dt)
+        double s2 = q0 * sExp[k][cc];
+        s2 += q1 * sExp[k][3 + cc];
+        s2 += q2 * sExp[k][6 + cc];
+        Rv = s2;
+      }
+      ang_last = 0.5 * (h[1 + ci] + t[1 + ci]) - bgc;
+      acc_last = acc;
     }
-    if (a.n > 0) {  // imu_ekf.cpp:81-86
+    if (isR) sTail[l] = Rv;
+    if (l >= 9 && l < 12) sTail[l] = pv;
+    if (l >= 12 && l < 15) sTail[l] = vv;
+    if (l < 3) {
+      sTail[15 + l] = acc_last;
+      sTail[18 + l] = ang_last;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (l == 0 && a.n > 0) {  // imu_ekf.cpp:81-86
+      const M3 R_imu = ld_m3(sTail);
+      const V3 pos = v3(sTail[9], sTail[10], sTail[11]), vel = v3(sTail[12], sTail[13], sTail[14]);
+      const V3 acc_imu = v3(sTail[15], sTail[16], sTail[17]), angvel = v3(sTail[18], sTail[19], sTail[20]);
       const double tb = a.imu[7 * (a.n - 1)];
       const double note = a.end > tb ? 1.0 : -1.0;
       const double dt = note * (a.end - tb);
@@ -153,9 +188,9 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
       const M3 R = mul(R_imu, Exp(scl(angvel, note), dt));
       const V3 p = add(add(pos, scl(vel, note * dt)), scl(acc_imu, note * 0.5 * dt * dt));
       for (int q = 0; q < 9; q++) st->xc[q] = R[q];
-      for (int j = 0; j < 3; j++) {
-        st->xc[9 + j] = p[j];
-        st->xc[12 + j] = v[j];
+      for (int j2 = 0; j2 < 3; j2++) {
+        st->xc[9 + j2] = p[j2];
+        st->xc[12 + j2] = v[j2];
       }
     }
   }
@@ -179,53 +214,71 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
   if (tid < 225) C[tid] = xc[kXS + tid];
   __syncthreads();
   VG_PROBE_MARK(4);
-  // 4. cov = F cov F^T + Q per pair, F's non-zero columns ascending (sandwich())
-  auto frow = [&](int k, int i, int* kk, double* vv) -> int {
+  // 4. cov = F cov F^T + Q per pair, F's non-zero columns ascending (sandwich()),
+  // the four row shapes of F written out (no per-lane index arrays)
+  auto a_ent = [&](int k, int i, int j) -> double {  // (F C)(i, j)
     const double dt = sDt[k];
     if (i < 3) {
-      kk[0] = 0, kk[1] = 1, kk[2] = 2, kk[3] = 9 + i;
-      vv[0] = sF00[k][i * 3], vv[1] = sF00[k][i * 3 + 1], vv[2] = sF00[k][i * 3 + 2], vv[3] = -dt;
-      return 4;
+      double s = sF00[k][i * 3] * C[j];
+      s += sF00[k][i * 3 + 1] * C[15 + j];
+      s += sF00[k][i * 3 + 2] * C[30 + j];
+      s += (-dt) * C[(9 + i) * 15 + j];
+      return s;
     }
     if (i < 6) {
-      kk[0] = i, kk[1] = i + 3;
-      vv[0] = 1.0, vv[1] = dt;
-      return 2;
+      double s = 1.0 * C[i * 15 + j];
+      s += dt * C[(i + 3) * 15 + j];
+      return s;
     }
     if (i < 9) {
       const int q = i - 6;
-      kk[0] = 0, kk[1] = 1, kk[2] = 2, kk[3] = i, kk[4] = 12, kk[5] = 13, kk[6] = 14;
-      vv[0] = sF60[k][q * 3], vv[1] = sF60[k][q * 3 + 1], vv[2] = sF60[k][q * 3 + 2], vv[3] = 1.0;
-      vv[4] = sF612[k][q * 3], vv[5] = sF612[k][q * 3 + 1], vv[6] = sF612[k][q * 3 + 2];
-      return 7;
+      double s = sF60[k][q * 3] * C[j];
+      s += sF60[k][q * 3 + 1] * C[15 + j];
+      s += sF60[k][q * 3 + 2] * C[30 + j];
+      s += 1.0 * C[i * 15 + j];
+      s += sF612[k][q * 3] * C[180 + j];
+      s += sF612[k][q * 3 + 1] * C[195 + j];
+      s += sF612[k][q * 3 + 2] * C[210 + j];
+      return s;
     }
-    kk[0] = i;
-    vv[0] = 1.0;
-    return 1;
+    return 1.0 * C[i * 15 + j];
+  };
+  auto o_ent = [&](int k, int i, int j) -> double {  // (A F^T)(i, j) + Q(i, j)
+    const double dt = sDt[k];
+    const double* Ai = &A[i * 15];
+    double s;
+    if (j < 3) {
+      s = Ai[0] * sF00[k][j * 3];
+      s += Ai[1] * sF00[k][j * 3 + 1];
+      s += Ai[2] * sF00[k][j * 3 + 2];
+      s += Ai[9 + j] * (-dt);
+    } else if (j < 6) {
+      s = Ai[j] * 1.0;
+      s += Ai[j + 3] * dt;
+    } else if (j < 9) {
+      const int q = j - 6;
+      s = Ai[0] * sF60[k][q * 3];
+      s += Ai[1] * sF60[k][q * 3 + 1];
+      s += Ai[2] * sF60[k][q * 3 + 2];
+      s += Ai[j] * 1.0;
+      s += Ai[12] * sF612[k][q * 3];
+      s += Ai[13] * sF612[k][q * 3 + 1];
+      s += Ai[14] * sF612[k][q * 3 + 2];
+    } else {
+      s = Ai[j] * 1.0;
+    }
+    double q = 0.0;
+    if (i >= 6 && i < 9 && j >= 6 && j < 9) q = sCw[k][(i - 6) * 3 + (j - 6)];
+    else if (i == j && i < 3) q = a.cov_gyr * dt * dt;
+    else if (i == j && i >= 9 && i < 12) q = a.rdw_gyr * dt * dt;
+    else if (i == j && i >= 12) q = a.rdw_acc * dt * dt;
+    return s + q;
   };
   for (int k = 0; k < ns; k++) {
     if (!sOk[k]) continue;  // uniform
-    int kk[7];
-    double vv[7];
-    if (tid < 225) {  // A = F C
-      const int nn = frow(k, r, kk, vv);
-      double s = vv[0] * C[kk[0] * 15 + c];
-      for (int t = 1; t < nn; t++) s += vv[t] * C[kk[t] * 15 + c];
-      A[tid] = s;
-    }
+    if (tid < 225) A[tid] = a_ent(k, r, c);
     __syncthreads();
-    if (tid < 225) {  // C = A F^T + Q
-      const int nn = frow(k, c, kk, vv);
-      double s = A[r * 15 + kk[0]] * vv[0];
-      for (int t = 1; t < nn; t++) s += A[r * 15 + kk[t]] * vv[t];
-      const double dt = sDt[k];
-      double q = 0.0;
-      if (r >= 6 && r < 9 && c >= 6 && c < 9) q = sCw[k][(r - 6) * 3 + (c - 6)];
-      else if (r == c && r < 3) q = a.cov_gyr * dt * dt;
-      else if (r == c && r >= 9 && r < 12) q = a.rdw_gyr * dt * dt;
-      else if (r == c && r >= 12) q = a.rdw_acc * dt * dt;
-      C[tid] = s + q;
-    }
+    if (tid < 225) C[tid] = o_ent(k, r, c);
     __syncthreads();
   }
   VG_PROBE_MARK(5);
@@ -233,6 +286,8 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
   if (tid < 225) st->xc[kXS + tid] = C[tid];
   __syncthreads();
   for (int t = tid; t < kXC; t += blockDim.x) st->xp[t] = st->xc[t];
+  for (int t = tid; t < 3 * 32; t += blockDim.x)  // k_iekf_all's pose slots start empty
+    reinterpret_cast<unsigned long long*>(&st->islot[0][0])[t] = kSlotEmpty;
   if (set_scan && tid == 64) {
     st->sx = x;
     st->sy = y;
@@ -301,6 +356,11 @@ int sync_wait(vg_ctx* ctx, hipStream_t s, int k, unsigned target) {
 }
 
 __global__ void k_set_scan(DState* __restrict__ st, const float* x, const float* y, const float* z, int n) {
+  {
+    const int tid = threadIdx.x;
+    for (int t = tid; t < 3 * 32; t += blockDim.x)  // k_iekf_all's pose slots start empty
+      reinterpret_cast<unsigned long long*>(&st->islot[0][0])[t] = kSlotEmpty;
+  }
   if (threadIdx.x == 0) {
     st->sx = x;
     st->sy = y;

@@ -143,6 +143,7 @@ struct DevMap {
   double* dbox = nullptr;      // cap_nodes * 6: the descent's region per node (lo[3] exclusive, hi[3] inclusive; vg_dev.h dbox_*)
   Clu* pcrs = nullptr;         // cap_nodes * W (SlideWindow::pcrs_local, physical slot)
   int* nscr = nullptr;         // per-node scratch (cap_nodes * 4)
+  unsigned long long* pend = nullptr;  // margi: per internal node, children still to report (high 32) | existing ones (low 32)
   int* cfirst = nullptr;       // per-node per-octant first-event scratch (cap_nodes * 8)
   uint64_t* hkey = nullptr;    // root hash
   int* hval = nullptr;
@@ -195,6 +196,8 @@ struct Work {
   void* tmp2 = nullptr;        // sort workspace of the second stream
   size_t tmp_bytes = 0;
   double* partials = nullptr;  // reduction partials
+  double* islots = nullptr;    // k_iekf_all's partial slots: 4 iterations x kIekfAllMax workgroups x 34
+  bool islots_armed = false;
   int* iekf_cache = nullptr;   // per raw point cached leaf
   int* pk_leaf = nullptr;      // per raw point leaf read by the profiled IEKF iteration (P_k count)
   int* rc = nullptr;           // device-side level counts (recut / margi, map.hip kRc*)
@@ -269,6 +272,10 @@ struct DState {
   int imu_head, pad_h[3];
   double imurec[kMaxWin * kBaImuRec];
   KClock clk;
+  // k_iekf_all: the pose each IEKF iteration 1-3 starts from (R 9, p 3, rot / tsl
+  // covariance blocks 9 + 9, finished flag), stored by its update workgroup, empty
+  // (kSlotEmpty) from the scan opening on
+  double islot[3][32];
 };
 // x_buf.push_back(x_curr) + a new IMU_PRE record, as kernel arguments (k_push_state,
 // or folded into the insert's first launch, map_insert)
@@ -429,6 +436,13 @@ struct vg_ctx {
   bool prof_stages = false;  // per-stage events (vg_profile bit 1)
   bool roots_lb = true;      // root registration in one look-back launch (vgx_debug 16: 0 = two launches)
   bool ba_graph2 = true;     // the first two LM iterations as one graph (vgx_debug 17: 0 = one graph each)
+  bool margi_fused = true;    // margi isexist bottom-up in k_margi_copy, erase in one launch (vgx_debug 21: 0 = per-level launches)
+  int iekf_all_cap = 0;       // k_iekf_all: workgroups resident at once (0: not yet asked, -1: too few)
+  bool iekf_persist = true;   // the four IEKF iterations as one launch, k_iekf_all (vgx_debug 22: 0 = a launch each)
+  bool iekf_fused = true;     // the IEKF update inside k_iekf (vgx_debug 20: 0 = k_iekf_update launch)
+  bool iekf_armed = false;    // wk.partials holds empty slots (kSlotEmpty)
+  bool ba_fuse_ctl = true;    // the LM bookkeeping in k_ba_resid's last workgroup (vgx_debug 19: 0 = k_ba_control launch)
+  bool ba_fuse_final = true;  // k_ba_prep sums k_ba_hess's chunk partials (vgx_debug 18: 0 = k_ba_hfinal launch)
   bool ba_graph = true;      // LM iterations replay one captured graph each (vgx_debug 15: 0 = direct launches)
   bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)
   unsigned* d_sync = nullptr;  // hand-off flags: [0] margi leaf -> next IEKF, [1] IEKF -> insert

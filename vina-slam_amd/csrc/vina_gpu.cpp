@@ -811,6 +811,26 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     VG_HIP(hipMemcpy(ctx->shard.d_seq, &s, sizeof(s), hipMemcpyHostToDevice));
     return VG_OK;
   }
+  if (key == 22) {  // 0: the IEKF iterations as one launch each (k_iekf)
+    ctx->iekf_persist = value != 0;
+    return VG_OK;
+  }
+  if (key == 21) {  // 0: margi's isexist / erase passes as per-level launches
+    ctx->margi_fused = value != 0;
+    return VG_OK;
+  }
+  if (key == 20) {  // 0: the IEKF update as its own k_iekf_update launch
+    ctx->iekf_fused = value != 0;
+    return VG_OK;
+  }
+  if (key == 19) {  // 0: the LM bookkeeping as its own k_ba_control launch
+    ctx->ba_fuse_ctl = value != 0;
+    return VG_OK;
+  }
+  if (key == 18) {  // 0: the chunk partials summed by a k_ba_hfinal launch (not inside k_ba_prep)
+    ctx->ba_fuse_final = value != 0;
+    return VG_OK;
+  }
   if (key == 17) {  // 0: one graph per LM iteration (no two-iteration graph)
     ctx->ba_graph2 = value != 0;
     return VG_OK;
