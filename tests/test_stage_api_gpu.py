@@ -107,3 +107,41 @@ def test_recut_replay_path_equals_fast_path(knob):
         assert sa == sb, (k, sa, sb)
     assert np.array_equal(a.trajectory(), b.trajectory())
     assert np.array_equal(a.window_states(), b.window_states())
+
+
+@pytest.mark.parametrize("ka,kb,exact", [({}, {18: 1}, True), ({}, {19: 1}, True), ({21: 0}, {}, True),
+                                         ({20: 1}, {20: 1, 22: 1}, True), ({}, {20: 1}, False)],
+                         ids=["lm-chunk-sums-in-prep", "lm-bookkeeping-in-resid", "margi-exist-up",
+                              "iekf-resident-iterations", "iekf-update-in-kernel"])
+def test_fused_launches_equal_separate(ka, kb, exact):
+    """Every launch fusion of the scan chain against its separate-launch form
+    (vgx_debug knobs; r04e's A/B kept only margi's): k_ba_hfinal's ordered
+    sums inside k_ba_prep (18), k_ba_control inside k_ba_resid's IMU workgroup
+    (19), margi's bottom-up isexist by atomic reports + one erase launch (21),
+    the four IEKF iterations as one resident launch (22 against 20 alone) —
+    all bit-identical. The IEKF update inside k_iekf (20) reduces the block
+    partials in 15 row groups where the 1024-lane k_iekf_update uses 60, so
+    only its rounding may differ: counters exact, poses within 1e-12 m."""
+    p = vgconfig.load("mid360")
+    seq = _seq(p, seq_id=7)
+    a = vgpu.Context(vgconfig.to_c(p), **CAP)
+    b = vgpu.Context(vgconfig.to_c(p), **CAP)
+    for c, kv in ((a, ka), (b, kb)):
+        for key, val in kv.items():
+            assert vgpu.lib().vgx_debug(c.h, key, val) == 0
+    a.seed(seq.gt_state(0))
+    b.seed(seq.gt_state(0))
+    for k in range(15):
+        xyz, it, beg, end = seq.scan(k)
+        imu = seq.imu(k)
+        a.step(xyz, it, beg, end, imu)
+        b.step(xyz, it, beg, end, imu)
+        sa, sb = a.stats(), b.stats()
+        assert sa == sb, (k, sa, sb)
+    ta, tb = a.trajectory(), b.trajectory()
+    if not exact:
+        assert np.abs(ta - tb).max() < 1e-12
+        assert np.abs(a.window_states() - b.window_states()).max() < 1e-9
+    else:
+        assert np.array_equal(ta, tb)
+        assert np.array_equal(a.window_states(), b.window_states())

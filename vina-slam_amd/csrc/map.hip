@@ -467,8 +467,17 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
 // stores and loads: no fence, no launch between iterations). Every wait is
 // bounded (error bit 64), so a workgroup that never became resident cannot
 // hang the GPU. Results equal k_iekf + update launches bit for bit.
+// the IEKF's end to the insert's stream (vg_ctx::d_sync[1]): every thread's
+// state writes released at agent scope (one workgroup: one L2 write-back),
+// then the flag advances by one
+__device__ __forceinline__ void iekf_signal_done(unsigned* flag) {
+  if (!flag) return;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void iekf_all_update(DState* __restrict__ st, int npt, double* pslots,
-                                                int* __restrict__ err) {
+                                                int* __restrict__ err, unsigned* done_flag) {
   __shared__ IekfLds L;
   __shared__ int s_late;
   const int n = st->sn;
@@ -483,6 +492,7 @@ __device__ __forceinline__ void iekf_all_update(DState* __restrict__ st, int npt
     if (s_late) {  // a point workgroup never delivered: stop them all
       if (threadIdx.x == 0) atomicOr(err, 64);
       if (it < 3 && threadIdx.x < 31) slot_put(&st->islot[it][threadIdx.x], 1.0);
+      iekf_signal_done(done_flag);
       return;
     }
     iekf_update_tail(st, it, L);
@@ -490,14 +500,20 @@ __device__ __forceinline__ void iekf_all_update(DState* __restrict__ st, int npt
     const bool fin = L.fin != 0;
     if (it < 3 && threadIdx.x < 31)
       slot_put(&st->islot[it][threadIdx.x], threadIdx.x < 30 ? pose_word(st->xc, threadIdx.x) : (fin ? 1.0 : 0.0));
-    if (fin) return;
+    if (fin) {
+      iekf_signal_done(done_flag);
+      return;
+    }
   }
 }
 __global__ void __launch_bounds__(256) k_iekf_all(MP mp, DState* __restrict__ st, DevMap m, int* __restrict__ cache,
-                                                  double* __restrict__ pslots, int npt) {
-  if (st->done) return;
+                                                  double* __restrict__ pslots, int npt, unsigned* done_flag) {
+  if (st->done) {  // (not within a scan: the opening clears it)
+    if ((int)blockIdx.x == npt) iekf_signal_done(done_flag);
+    return;
+  }
   if ((int)blockIdx.x >= npt) {
-    iekf_all_update(st, npt, pslots, m.counters + kCntErr);
+    iekf_all_update(st, npt, pslots, m.counters + kCntErr, done_flag);
     return;
   }
   const int n = st->sn;
@@ -633,11 +649,13 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
 // node without the per-launch dispatch gap. The per-stage profiling pass
 // (vg_profile bit 1) launches directly, with an event pair around each k_iekf.
 int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank,
-             const double* begin_xc, hipStream_t s, const PropArg* begin_prop) {
+             const double* begin_xc, hipStream_t s, const PropArg* begin_prop, bool signal, bool* signalled,
+             bool opened) {
   if (!s) s = ctx->stream;
+  if (signalled) *signalled = false;
   if (begin_xc || begin_prop)  // the scan opens here (pipeline.cpp)
     VG_TRY(state_scan_begin(ctx, begin_xc, x, y, z, n, s, begin_prop));
-  else VG_TRY(state_set_scan(ctx, x, y, z, n, s));
+  else if (!opened) VG_TRY(state_set_scan(ctx, x, y, z, n, s));
   const bool graph = ctx->use_graphs && ctx->shard.world <= 1 && !ctx->prof_stages;
   const bool ev = ctx->prof_on && !graph;
   // the fused update's slots start empty (iekf_reduce_spin re-arms what it
@@ -660,36 +678,47 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
       VG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
       ctx->iekf_all_cap = per_cu * cus;
     }
-    // at least 8 workgroups to spare (the other streams' kernels, the poll of the
-    // IEKF hand-off)
+    // Every active point workgroup, the update one and whatever else is
+    // resident for good must fit at once, per XCD: workgroups are dealt to
+    // the 8 XCDs in turn, so XCD 0 holds npt / 8 point workgroups plus the
+    // update one (the last dispatched), and the main stream's poll of the
+    // IEKF hand-off (k_sync_wait, resident until the IEKF ends) may sit on
+    // it too. Four slots per XCD stay spare (kIekfAllMax = 8 x (64 - 4) on a
+    // 256-CU part at two workgroups per CU).
     int npt = iekf_blocks(ctx) < kIekfAllMax ? iekf_blocks(ctx) : kIekfAllMax;
-    if (npt > ctx->iekf_all_cap - 9) npt = ctx->iekf_all_cap - 9;
+    if (npt > 8 * (ctx->iekf_all_cap / 8 - 4)) npt = 8 * (ctx->iekf_all_cap / 8 - 4);
     npt = npt / 8 * 8;
     if (npt < 64) {  // too small a device for the resident form: per-iteration launches from now on
       ctx->iekf_all_cap = -1;
-      return iekf_run(ctx, mp, x, y, z, n, bank, nullptr, s, nullptr);
+      return iekf_run(ctx, mp, x, y, z, n, bank, nullptr, s, nullptr, false, nullptr, true);
     }
     if (!w.islots_armed) {  // iekf_reduce_spin re-arms what it reads
       VG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.islots), (int)kSlotEmpty32,
                                (size_t)4 * kIekfAllMax * kIekfVals * 2, s));
       w.islots_armed = true;
     }
-    if (!graph || !ctx->g_iekf[1]) {
+    // the update workgroup advances the IEKF -> insert flag itself when asked
+    // (one release by one workgroup), so no k_sync_set launch follows the IEKF
+    unsigned* flag = signal ? ctx->d_sync + 1 : nullptr;
+    hipGraphExec_t& ge = ctx->g_iekf[signal ? 2 : 1];
+    if (!graph || !ge) {
       if (graph) VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-      k_iekf_all<<<npt + 1, 256, 0, s>>>(mp, ctx->st, ctx->map, w.iekf_cache, w.islots, npt);
+      k_iekf_all<<<npt + 1, 256, 0, s>>>(mp, ctx->st, ctx->map, w.iekf_cache, w.islots, npt, flag);
       const hipError_t le = hipGetLastError();
       if (!graph) {
         VG_HIP(le);
+        if (signalled) *signalled = signal;
         return VG_OK;
       }
       hipGraph_t g = nullptr;
       const hipError_t e = hipStreamEndCapture(s, &g);
       VG_HIP(le);
       VG_HIP(e);
-      VG_HIP(hipGraphInstantiate(&ctx->g_iekf[1], g, nullptr, nullptr, 0));
+      VG_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
       VG_HIP(hipGraphDestroy(g));
     }
-    VG_HIP(hipGraphLaunch(ctx->g_iekf[1], s));
+    VG_HIP(hipGraphLaunch(ge, s));
+    if (signalled) *signalled = signal;
     return VG_OK;
   }
   auto enqueue = [&]() -> int {
@@ -2870,12 +2899,18 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
                                                     const int* __restrict__ ba_iters, const int* __restrict__ ba_hess,
                                                     Pub* __restrict__ pub, int seq, DevMap m,
                                                     const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
-                                                    int* __restrict__ plan, const int* __restrict__ gate) {
+                                                    int* __restrict__ plan, const int* __restrict__ gate,
+                                                    unsigned* __restrict__ head_flag) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   if (blockIdx.x == 0) {  // the margi head: x_curr <- x_buf.back(), the window view, the state publication
     make_win_block(st, wa, m.wpn, win, nper, slot_of);
     __syncthreads();  // x_curr (set_xc), seen by the whole block
     if (seq > 0) publish_state_block(st, wa.win_count, ba_iters_valid, ba_iters, ba_hess, pub, seq);
+    if (head_flag) {  // x_curr is final: the next scan's propagation may start (vg_ctx::d_sync[2])
+      __threadfence();
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(head_flag, (unsigned)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return;
   }
   // the leaves read the refined window poses from the state (the view block
@@ -3305,11 +3340,16 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   // workgroup 0 is the margi head (the window view and the state publication,
   // k_make_win_publish's work) running beside the leaves
   const int* bi = pub_seq > 0 ? ba_iters_dev(ctx) : nullptr;
+  // the hand-off flags to the next scan's IEKF stream: the margi head's
+  // x_curr (d_sync[2], the device propagation starts from it) and the leaves'
+  // plane updates (d_sync[0], the IEKF reads them)
+  const bool flags = ctx->flag_sync && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages && ctx->shard.world == 1;
   k_margi_leaf<<<1 + 512 * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(
       m.counters + kCntLeaves, w.list0, mp, wa2, ctx->st, dwin, dn, dn + 32, bi != nullptr, bi,
-      bi ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, pub_seq, m, ctx->ba.fac_eig, ctx->ba.fac_pcr, w.plan, gate);
+      bi ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, pub_seq, m, ctx->ba.fac_eig, ctx->ba.fac_pcr, w.plan, gate,
+      flags ? ctx->d_sync + 2 : nullptr);
   VG_HIP(hipEventRecord(ctx->ev_tail_a, s));
-  if (ctx->flag_sync && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages && ctx->shard.world == 1) {
+  if (flags) {
     VG_TRY(sync_set(ctx, s, 0, (unsigned)pub_seq, gate));  // the margi's publication number (stage_margi_slide)
   }
   if (ctx->pub_flags & 1) k_local_map<<<64, kBlock, 0, s>>>(dwin, m, ctx->d_cmap, ctx->d_cmap_n, gate);

@@ -395,13 +395,28 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   if (!ctx->stream_iekf) VG_HIP(hipStreamCreateWithFlags(&ctx->stream_iekf, hipStreamNonBlocking));
   const bool flags = ctx->flag_sync && ctx->sync_tail_armed;  // state.hip k_sync_*: no late-released event waits
   ctx->sync_tail_armed = false;
-  if (flags) VG_TRY(sync_wait(ctx, ctx->stream_iekf, 0, ctx->sync_tail_value));
-  else VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->ev_tail_a, 0));
-  if (ctx->in_ev) VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->in_ev, 0));  // a host-input scan's unpack
-  VG_TRY(iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, bxc, ctx->stream_iekf, bprop));
+  bool opened = false;
+  if (flags && bprop) {
+    // the device propagation needs only x_curr, final once the margi head
+    // (k_margi_leaf's workgroup 0) stored it: it runs under the leaves'
+    // plane updates, and the IEKF waits for those alone
+    VG_TRY(sync_wait(ctx, ctx->stream_iekf, 2, ctx->sync_tail_value));
+    if (ctx->in_ev) VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->in_ev, 0));  // a host-input scan's unpack
+    VG_TRY(state_scan_begin(ctx, nullptr, x, y, z, n, ctx->stream_iekf, bprop));
+    VG_TRY(sync_wait(ctx, ctx->stream_iekf, 0, ctx->sync_tail_value));
+    bprop = nullptr;
+    opened = true;
+  } else {
+    if (flags) VG_TRY(sync_wait(ctx, ctx->stream_iekf, 0, ctx->sync_tail_value));
+    else VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->ev_tail_a, 0));
+    if (ctx->in_ev) VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->in_ev, 0));  // a host-input scan's unpack
+  }
+  bool signalled = false;  // k_iekf_all advanced the flag itself (no k_sync_set launch)
+  VG_TRY(iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, bxc, ctx->stream_iekf, bprop, flags, &signalled,
+                  opened));
   if (flags) {
     const unsigned v = ++ctx->sync_iekf_value;
-    VG_TRY(sync_set(ctx, ctx->stream_iekf, 1, v));
+    if (!signalled) VG_TRY(sync_set(ctx, ctx->stream_iekf, 1, v));
     VG_TRY(sync_wait(ctx, ctx->stream, 1, v));
   } else {
     VG_HIP(hipEventRecord(ctx->ev_iekf_done, ctx->stream_iekf));

@@ -16,7 +16,7 @@
 namespace vg {
 
 constexpr int kIekfVals = 34;  // HTH upper 21, HTz 6, nnt upper 6, match count
-constexpr int kIekfAllMax = 504;  // k_iekf_all point workgroups: with the update one, <= 2 per CU on 256 CUs (253 VGPRs)
+constexpr int kIekfAllMax = 480;  // k_iekf_all point workgroups (see iekf_run: co-residency per XCD)
 
 // LDS of iekf_update_block
 constexpr int kIekfGroups = 60;  // row groups of the partial sums (1024-lane update: 60 x 17 lanes)

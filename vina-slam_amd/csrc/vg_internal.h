@@ -438,14 +438,14 @@ struct vg_ctx {
   bool ba_graph2 = true;     // the first two LM iterations as one graph (vgx_debug 17: 0 = one graph each)
   bool margi_fused = true;    // margi isexist bottom-up in k_margi_copy, erase in one launch (vgx_debug 21: 0 = per-level launches)
   int iekf_all_cap = 0;       // k_iekf_all: workgroups resident at once (0: not yet asked, -1: too few)
-  bool iekf_persist = true;   // the four IEKF iterations as one launch, k_iekf_all (vgx_debug 22: 0 = a launch each)
-  bool iekf_fused = true;     // the IEKF update inside k_iekf (vgx_debug 20: 0 = k_iekf_update launch)
+  bool iekf_persist = false;  // vgx_debug 22 (with 20): the four IEKF iterations as one launch, k_iekf_all (r04e A/B: slower)
+  bool iekf_fused = false;    // vgx_debug 20: the IEKF update as k_iekf's last workgroup (r04e A/B: -23 %)
   bool iekf_armed = false;    // wk.partials holds empty slots (kSlotEmpty)
-  bool ba_fuse_ctl = true;    // the LM bookkeeping in k_ba_resid's last workgroup (vgx_debug 19: 0 = k_ba_control launch)
-  bool ba_fuse_final = true;  // k_ba_prep sums k_ba_hess's chunk partials (vgx_debug 18: 0 = k_ba_hfinal launch)
+  bool ba_fuse_ctl = false;   // vgx_debug 19: the LM bookkeeping in k_ba_resid's IMU workgroup (r04e A/B: neutral)
+  bool ba_fuse_final = false; // vgx_debug 18: k_ba_prep sums k_ba_hess's chunk partials itself (r04e A/B: -6 %)
   bool ba_graph = true;      // LM iterations replay one captured graph each (vgx_debug 15: 0 = direct launches)
   bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)
-  unsigned* d_sync = nullptr;  // hand-off flags: [0] margi leaf -> next IEKF, [1] IEKF -> insert
+  unsigned* d_sync = nullptr;  // hand-off flags: [0] margi leaf -> next IEKF, [1] IEKF -> insert, [2] margi head -> propagation
   bool sync_tail_armed = false;  // the last margi's leaf pass stores sync_tail_value into d_sync[0]
   unsigned sync_tail_value = 0, sync_iekf_value = 0;
   bool dev_prop = false;     // host_step propagates on the device (k_scan_prop; vgx_debug 13: 1 = on the device)
@@ -617,8 +617,12 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
 // all four iterations; replays the captured graph when possible
 // begin_xc != nullptr: open the scan on the device first (x_curr after
 // propagation, one launch with the scan binding)
+// *signalled: the run itself advanced the IEKF -> insert hand-off flag
+// (d_sync[1], by one; k_iekf_all's update workgroup after a release), so the
+// caller need not enqueue k_sync_set (signal: the caller wants it)
 int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int bank,
-             const double* begin_xc = nullptr, hipStream_t s = nullptr, const PropArg* begin_prop = nullptr);
+             const double* begin_xc = nullptr, hipStream_t s = nullptr, const PropArg* begin_prop = nullptr,
+             bool signal = false, bool* signalled = nullptr, bool opened = false);  // opened: scan already bound
 constexpr int kNeedInsertReplay = 1;  // map_recut: the insert overflowed k_ins_alloc, replay it first
 // the initialisation's insert source (cut_voxel, initialization.cpp:229-246):
 // n fp64 body points, the kXC pose/covariance block of x_buf[i], both device
