@@ -73,6 +73,9 @@ def parse():
                          "mode on the 1M workload at N=1 (empty: skip)")
     ap.add_argument("--multi-1m-steps", type=int, default=10, help="timed scans per sequence of the 1M leg")
     ap.add_argument("--multi-group", type=int, default=4, help="sequences per process in the multi-sequence legs")
+    ap.add_argument("--multi-active", type=int, default=0,
+                    help="at most this many sequences on the device at once (vg_multi_set_active; 0: no cap); "
+                         "with a cap, every B runs in ONE process")
     ap.add_argument("--multi-child", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--multi-scans", default="", help=argparse.SUPPRESS)
     ap.add_argument("--multi-max-points", type=int, default=0, help=argparse.SUPPRESS)
@@ -431,9 +434,11 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=Non
     paths = []
     out = {"lidar": lidar, "unit": "scans/s", "steps": steps, "warmup": warmup,
            "workers": "one native thread + one stream per sequence", "inputs": "B distinct sequences",
-           "wait_policy": "spin", "process": "ceil(B/%d) concurrent processes of <= %d sequences, released together "
-                                                 "after their warm-up; rate = B x steps / (release -> last end)"
-                                                 % (args.multi_group, args.multi_group),
+           "wait_policy": "spin",
+           "process": ("one process per B, at most %d sequences on the device at once (vg_multi_set_active); "
+                       "rate = B x steps / (release -> end)" % args.multi_active) if args.multi_active > 0 else
+                      ("ceil(B/%d) concurrent processes of <= %d sequences, released together after their warm-up; "
+                       "rate = B x steps / (release -> last end)" % (args.multi_group, args.multi_group)),
            "env": {"GPU_MAX_HW_QUEUES": "16"},
            "by_B": {}}
     npmax = 0
@@ -469,7 +474,7 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=Non
             # processes of 4 run ~6,000), started together: each child warms
             # up, reports READY and waits; the parent then releases all of
             # them at once and times the job from GO to the last child's end
-            P = (B + grp - 1) // grp
+            P = 1 if args.multi_active > 0 else (B + grp - 1) // grp  # a cap applies within one process
             sizes = [B // P + (1 if q < B % P else 0) for q in range(P)]
             runs, first_seq = [], 0
             for q in range(P):
@@ -478,7 +483,7 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=Non
                        "--multi-max-points", str(npmax + 16),
                        "--lidar", lidar, "--config", args.config, "--steps", str(steps), "--warmup", str(args.warmup),
                        "--max-nodes", str(args.max_nodes), "--max-fix", str(args.max_fix),
-                       "--hash-log2", str(args.hash_log2)]
+                       "--hash-log2", str(args.hash_log2), "--multi-active", str(args.multi_active)]
                 first_seq += sizes[q]
                 runs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env))
             for r in runs:  # every child warmed up and idle
@@ -536,6 +541,8 @@ def multi_child(args, p, g, warmup, total):
         c.seed(seq.gt_state(0))  # every synthetic sequence follows the same trajectory (synth.Trajectory)
     wait = os.environ.get("VG_MULTI_WAIT", "")
     mv = vgpu.Multi(ctxs, *([int(v) for v in wait.split(",")] if wait else [0, 0]))
+    if 0 < args.multi_active < B:
+        mv.set_active(args.multi_active)
 
     def step(k):
         scans = []

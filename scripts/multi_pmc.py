@@ -24,7 +24,7 @@ import vgconfig  # noqa: E402
 
 def main():
     B = int(sys.argv[1])
-    lidar = sys.argv[2] if len(sys.argv) > 2 else "64line"
+    lidar = sys.argv[2] if len(sys.argv) > 2 else "64line"  # argv[3]: vg_multi_set_active cap (0: none)
     p = vgconfig.load("mid360")
     g = p["General"]
     warm, steps = 12, 16
@@ -47,6 +47,9 @@ def main():
     for c in ctxs:
         c.seed(seq.gt_state(0))
     mv = vgpu.Multi(ctxs, 0, 0)
+    cap = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    if cap:
+        mv.set_active(cap)  # at most `cap` sequences on the device at once
 
     def step(k):
         mv.step_dev([(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), 0, n, b, e, imu)
@@ -62,7 +65,7 @@ def main():
     mv.sync()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    print(json.dumps({"B": B, "scans_per_s": round(B * steps / dt, 1)}), flush=True)
+    print(json.dumps({"B": B, "active_cap": cap, "scans_per_s": round(B * steps / dt, 1)}), flush=True)
     mv.close()
     for c in ctxs:
         c.close()

@@ -109,10 +109,11 @@ def test_recut_replay_path_equals_fast_path(knob):
     assert np.array_equal(a.window_states(), b.window_states())
 
 
-@pytest.mark.parametrize("ka,kb,exact", [({}, {18: 1}, True), ({}, {19: 1}, True), ({21: 0}, {}, True),
-                                         ({20: 1}, {20: 1, 22: 1}, True), ({}, {20: 1}, False)],
+@pytest.mark.parametrize("ka,kb,exact", [({}, {18: 1}, True), ({19: 0}, {}, True), ({21: 0}, {}, True),
+                                         ({20: 1}, {20: 1, 22: 1}, True), ({}, {20: 1}, False),
+                                         ({}, {13: 1}, True)],
                          ids=["lm-chunk-sums-in-prep", "lm-bookkeeping-in-resid", "margi-exist-up",
-                              "iekf-resident-iterations", "iekf-update-in-kernel"])
+                              "iekf-resident-iterations", "iekf-update-in-kernel", "device-propagation"])
 def test_fused_launches_equal_separate(ka, kb, exact):
     """Every launch fusion of the scan chain against its separate-launch form
     (vgx_debug knobs; r04e's A/B kept only margi's): k_ba_hfinal's ordered
@@ -121,7 +122,9 @@ def test_fused_launches_equal_separate(ka, kb, exact):
     the four IEKF iterations as one resident launch (22 against 20 alone) —
     all bit-identical. The IEKF update inside k_iekf (20) reduces the block
     partials in 15 row groups where the 1024-lane k_iekf_update uses 60, so
-    only its rounding may differ: counters exact, poses within 1e-12 m."""
+    only its rounding may differ: counters exact, poses within 1e-12 m. The
+    device IMU propagation (13: k_scan_prop, from the margi head's flag)
+    keeps the host's expression trees: bit-identical to host propagation."""
     p = vgconfig.load("mid360")
     seq = _seq(p, seq_id=7)
     a = vgpu.Context(vgconfig.to_c(p), **CAP)

@@ -41,6 +41,14 @@ struct vg_multi {
   int depth = 4;  // scans queued per sequence before vg_multi_step_dev blocks
   int busy = 0;   // workers inside a step
   std::vector<char> split;  // context b ran with its own downsample stream + IEKF overlap (restored on destroy)
+  // At most `cap` sequences on the device at once (0: no cap). Measured
+  // (profiles/r04/multi_pmc_r04g.json): at B = 8 every kernel's L2 hit rate and
+  // request count equal B = 4's, yet every kernel takes >= ~47 us — the
+  // hardware queues are oversubscribed and time-sliced, not the caches. So a
+  // worker takes a slot, runs its scan, waits for that scan's device work,
+  // and gives the slot back: never more than `cap` queues busy.
+  int cap = 0, active = 0;
+  std::condition_variable cv_slot;
 };
 
 static void worker(vg_multi* M, int b) {
@@ -58,12 +66,27 @@ static void worker(vg_multi* M, int b) {
     vg_ctx* c = M->ctx[b];
     const vg_scan_dev& sc = j.sc;
     const double* imu = j.imu.empty() ? nullptr : j.imu.data();
+    const bool capped = M->cap > 0;
+    if (capped) {
+      std::unique_lock<std::mutex> lk(M->mu);
+      M->cv_slot.wait(lk, [&] { return M->active < M->cap; });
+      M->active++;
+    }
     int r;
     if (sc.d_time)
       r = vg_step_deskew_dev(c, sc.d_x, sc.d_y, sc.d_z, sc.d_intensity, sc.d_time, sc.n, sc.pcl_beg_time,
                              sc.pcl_end_time, imu, sc.m);
     else
       r = vg_step_dev(c, sc.d_x, sc.d_y, sc.d_z, sc.d_intensity, sc.n, sc.pcl_beg_time, sc.pcl_end_time, imu, sc.m);
+    if (capped) {  // the scan's device work done before the slot goes to another sequence
+      const int r2 = vg::host_sync(c);
+      if (r == VG_OK) r = r2;
+      {
+        std::lock_guard<std::mutex> lk(M->mu);
+        M->active--;
+      }
+      M->cv_slot.notify_one();
+    }
     {
       std::lock_guard<std::mutex> lk(M->mu);
       if (r != VG_OK && M->wk[b].rc == VG_OK) M->wk[b].rc = r;
@@ -125,6 +148,16 @@ int vg_multi_step_dev(vg_multi* M, const vg_scan_dev* scans) {
   }
   lk.unlock();
   M->cv_job.notify_all();
+  return VG_OK;
+}
+
+int vg_multi_set_active(vg_multi* M, int cap) {
+  if (!M || cap < 0) return VG_E_ARG;
+  std::lock_guard<std::mutex> lk(M->mu);
+  if (M->busy || M->active) return VG_E_STATE;  // between steps only
+  for (const Worker& w : M->wk)
+    if (!w.q.empty()) return VG_E_STATE;
+  M->cap = cap >= (int)M->ctx.size() ? 0 : cap;
   return VG_OK;
 }
 

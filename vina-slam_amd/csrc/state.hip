@@ -274,23 +274,17 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
     else if (i == j && i >= 12) q = a.rdw_acc * dt * dt;
     return s + q;
   };
-  // on wave 0 alone, four entries per lane: the two half-steps of a sample
-  // meet at wave barriers, not workgroup barriers (r04e probe: 15.7 us for the
-  // chain with two workgroup barriers per sample)
-  if (tid < 64) {
-    for (int k = 0; k < ns; k++) {
-      if (!sOk[k]) continue;  // uniform
-      for (int e = tid; e < 225; e += 64) A[e] = a_ent(k, e / 15, e % 15);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      for (int e = tid; e < 225; e += 64) C[e] = o_ent(k, e / 15, e % 15);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
+  // one lane per entry, two workgroup barriers per sample (15.7 us for ~18
+  // samples, r04e probe); the same chain on wave 0 alone, four entries per
+  // lane meeting at wave barriers, took 56.8 us (r04g: the lanes of one wave
+  // then take different row shapes and every shape's code runs for all)
+  for (int k = 0; k < ns; k++) {
+    if (!sOk[k]) continue;  // uniform
+    if (tid < 225) A[tid] = a_ent(k, r, c);
+    __syncthreads();
+    if (tid < 225) C[tid] = o_ent(k, r, c);
+    __syncthreads();
   }
-  __syncthreads();
   VG_PROBE_MARK(5);
   // 5. the scan opening (k_scan_begin) with the propagated state
   if (tid < 225) st->xc[kXS + tid] = C[tid];

@@ -441,7 +441,7 @@ struct vg_ctx {
   bool iekf_persist = false;  // vgx_debug 22 (with 20): the four IEKF iterations as one launch, k_iekf_all (r04e A/B: slower)
   bool iekf_fused = false;    // vgx_debug 20: the IEKF update as k_iekf's last workgroup (r04e A/B: -23 %)
   bool iekf_armed = false;    // wk.partials holds empty slots (kSlotEmpty)
-  bool ba_fuse_ctl = false;   // vgx_debug 19: the LM bookkeeping in k_ba_resid's IMU workgroup (r04e A/B: neutral)
+  bool ba_fuse_ctl = true;    // vgx_debug 19: the LM bookkeeping in k_ba_resid's IMU workgroup (A/Bs r04e 0, r04g/h +0.8-0.9 %)
   bool ba_fuse_final = false; // vgx_debug 18: k_ba_prep sums k_ba_hess's chunk partials itself (r04e A/B: -6 %)
   bool ba_graph = true;      // LM iterations replay one captured graph each (vgx_debug 15: 0 = direct launches)
   bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)

@@ -162,6 +162,7 @@ def lib():
         L.vg_multi_create.restype = P
         L.vg_multi_step_dev.argtypes = [P, ctypes.POINTER(ScanDev)]
         L.vg_multi_sync.argtypes = [P]
+        L.vg_multi_set_active.argtypes = [P, ctypes.c_int]
         L.vg_multi_destroy.argtypes = [P]
         L.vgx_debug.argtypes = [P, ctypes.c_int, ctypes.c_int]
         L.vgx_downsample_hashed.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, fp, ip]
@@ -553,6 +554,12 @@ class Multi:
             lib().vg_multi_sync(self.h)  # the workers are idle before their error strings are read
             raise VgError("vg_multi_step_dev failed (%d): %s" % (
                 r, "; ".join(lib().vg_last_error(c.h).decode() for c in self.contexts)))
+
+    def set_active(self, cap):
+        """At most `cap` sequences on the device at once (vg_multi_set_active)."""
+        r = lib().vg_multi_set_active(self.h, int(cap))
+        if r != 0:
+            raise VgError("vg_multi_set_active failed (%d)" % r)
 
     def sync(self):
         r = lib().vg_multi_sync(self.h)
