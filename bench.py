@@ -422,8 +422,11 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=Non
     sequences need, sequences end up sharing queues (measured: the same B = 4
     run at 1,100 or 3,300 scans/s depending on the streams created before it).
     Every context runs a distinct synthetic sequence (seed args.seq + b; no two
-    contexts read the same scan). GPU_MAX_HW_QUEUES=16 is set for the children
-    only, one hardware queue per sequence stream."""
+    contexts read the same scan). GPU_MAX_HW_QUEUES (children only): 16 for
+    B <= --multi-group (a hardware queue per sequence stream), --multi-group
+    for larger B (the streams share that many queues: more busy queues are
+    time-sliced by the GPU).
+    """
     import subprocess
     import tempfile
 
@@ -435,10 +438,11 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=Non
     out = {"lidar": lidar, "unit": "scans/s", "steps": steps, "warmup": warmup,
            "workers": "one native thread + one stream per sequence", "inputs": "B distinct sequences",
            "wait_policy": "spin",
-           "process": ("one process per B, at most %d sequences on the device at once (vg_multi_set_active); "
-                       "rate = B x steps / (release -> end)" % args.multi_active) if args.multi_active > 0 else
-                      ("ceil(B/%d) concurrent processes of <= %d sequences, released together after their warm-up; "
-                       "rate = B x steps / (release -> last end)" % (args.multi_group, args.multi_group)),
+           "process": "one process per B, released after its warm-up; B > %d: the B streams share %d hardware "
+                      "queues (GPU_MAX_HW_QUEUES)%s; rate = B x steps / (release -> end)"
+                      % (args.multi_group, args.multi_group,
+                         ", at most %d sequences on the device at once (vg_multi_set_active)" % args.multi_active
+                         if args.multi_active > 0 else ""),
            "env": {"GPU_MAX_HW_QUEUES": "16"},
            "by_B": {}}
     npmax = 0
@@ -468,13 +472,17 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=Non
         grp = args.multi_group
         for B in Bs:
             beat("multi-sequence %s: B = %d" % (lidar, B))
-            # ceil(B / grp) processes of at most grp sequences each (measured:
-            # one process stepping more than 4 sequences falls off a cliff,
-            # B = 6 at ~1,800 scans/s against ~3,000 for B = 4, while two
-            # processes of 4 run ~6,000), started together: each child warms
-            # up, reports READY and waits; the parent then releases all of
-            # them at once and times the job from GO to the last child's end
-            P = 1 if args.multi_active > 0 else (B + grp - 1) // grp  # a cap applies within one process
+            # the child warms up, reports READY and waits; the parent then
+            # releases it and times the job from GO to its end.
+            # B > grp: ONE process whose B streams share grp hardware queues
+            # (GPU_MAX_HW_QUEUES = grp): past ~4 hardware queues the GPU
+            # time-slices them (profiles/r04/multi_pmc_r04g.json: same L2 hit
+            # rates, a ~47 us floor per kernel at B = 8), and B = 8 / 16 over
+            # 4 shared queues ran 2,839 / 3,140 scans/s against 2,565 / ~2,250
+            # over private queues (profiles/r04/multi_hwq_r04.json)
+            P = 1
+            benv = dict(env, GPU_MAX_HW_QUEUES=str(grp)) if B > grp else env
+            out.setdefault("hw_queues_by_B", {})[str(B)] = int(benv["GPU_MAX_HW_QUEUES"])
             sizes = [B // P + (1 if q < B % P else 0) for q in range(P)]
             runs, first_seq = [], 0
             for q in range(P):
@@ -485,7 +493,7 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=Non
                        "--max-nodes", str(args.max_nodes), "--max-fix", str(args.max_fix),
                        "--hash-log2", str(args.hash_log2), "--multi-active", str(args.multi_active)]
                 first_seq += sizes[q]
-                runs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env))
+                runs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=benv))
             for r in runs:  # every child warmed up and idle
                 line = r.stdout.readline()
                 if line.strip() != "READY":

@@ -370,10 +370,12 @@ typedef struct vg_multi vg_multi;
 vg_multi* vg_multi_create(vg_ctx** ctxs, int B, int spin_us, int sleep_us);
 int vg_multi_step_dev(vg_multi* mv, const vg_scan_dev* scans);
 /* At most `cap` sequences with device work in flight at once (0 or >= B: no
- * cap); a worker then waits for its scan's device work before the next
- * sequence takes its slot. Past four busy hardware queues the GPU
- * time-slices them (every kernel >= ~47 us at B = 8, same L2 hit rates as
- * B = 4), so B > 4 runs best capped at 4. Between steps only (VG_E_STATE). */
+ * cap): sequence b runs in slot b % cap, one sequence per slot at a time, and
+ * waits for its scan's device work before the slot passes on. Past about four
+ * hardware queues per process the GPU time-slices them (every kernel >= ~47
+ * us at B = 8, same L2 hit rates as B = 4), idle ones included, so pair the
+ * cap with GPU_MAX_HW_QUEUES = cap (the B streams then share cap queues, slot
+ * by slot). Between steps only (VG_E_STATE). */
 int vg_multi_set_active(vg_multi* mv, int cap);
 int vg_multi_sync(vg_multi* mv);
 void vg_multi_destroy(vg_multi* mv);

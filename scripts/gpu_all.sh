@@ -18,7 +18,7 @@ D=gpurun_out/pmc_$TAG
 mkdir -p $D
 ARGS="--no-cpu --steps 12 --warmup 12 --stage-scans 0 --target-steps 0 --workers 1 --no-h2d --multi= --multi-1m="
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/stats -o run -- python3 bench.py --no-cpu --target-steps 0 --workers 1 --no-h2d --multi= --multi-1m= > $D/stats.log 2>&1 || { echo "stats pass failed"; tail -20 $D/stats.log; exit 1; }
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $D/fetch -o run -- python3 bench.py $ARGS > $D/fetch.log 2>&1 || { echo "fetch pass failed"; tail -20 $D/fetch.log; exit 1; }
-timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $D/write -o run -- python3 bench.py $ARGS > $D/write.log 2>&1 || { echo "write pass failed"; tail -20 $D/write.log; exit 1; }
+VG_BENCH_DEBUG=14=0 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $D/fetch -o run -- python3 bench.py $ARGS > $D/fetch.log 2>&1 || { echo "fetch pass failed"; tail -20 $D/fetch.log; exit 1; }
+VG_BENCH_DEBUG=14=0 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $D/write -o run -- python3 bench.py $ARGS > $D/write.log 2>&1 || { echo "write pass failed"; tail -20 $D/write.log; exit 1; }
 python3 scripts/pmc_summary.py $D $D/pmc_traffic.json > /dev/null
 find $D -name '*stats*.csv'

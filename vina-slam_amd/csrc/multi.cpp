@@ -44,10 +44,15 @@ struct vg_multi {
   // At most `cap` sequences on the device at once (0: no cap). Measured
   // (profiles/r04/multi_pmc_r04g.json): at B = 8 every kernel's L2 hit rate and
   // request count equal B = 4's, yet every kernel takes >= ~47 us — the
-  // hardware queues are oversubscribed and time-sliced, not the caches. So a
-  // worker takes a slot, runs its scan, waits for that scan's device work,
-  // and gives the slot back: never more than `cap` queues busy.
+  // hardware queues are oversubscribed and time-sliced, not the caches; idle
+  // queues count too (a cap of 4 busy sequences over 8 queues changes
+  // nothing). So with GPU_MAX_HW_QUEUES = cap the B streams share cap
+  // queues, and sequence b runs only while no other sequence of its slot
+  // b % cap does: a worker takes its slot, runs its scan, waits for that
+  // scan's device work and gives the slot back.
   int cap = 0, active = 0;
+  std::vector<char> slot_busy;  // sequence b runs in slot b % cap (its stream shares a hardware queue with
+                                // the other sequences of that slot when GPU_MAX_HW_QUEUES = cap)
   std::condition_variable cv_slot;
 };
 
@@ -67,9 +72,11 @@ static void worker(vg_multi* M, int b) {
     const vg_scan_dev& sc = j.sc;
     const double* imu = j.imu.empty() ? nullptr : j.imu.data();
     const bool capped = M->cap > 0;
+    const int slot = capped ? b % M->cap : 0;
     if (capped) {
       std::unique_lock<std::mutex> lk(M->mu);
-      M->cv_slot.wait(lk, [&] { return M->active < M->cap; });
+      M->cv_slot.wait(lk, [&] { return !M->slot_busy[slot]; });
+      M->slot_busy[slot] = 1;
       M->active++;
     }
     int r;
@@ -83,9 +90,10 @@ static void worker(vg_multi* M, int b) {
       if (r == VG_OK) r = r2;
       {
         std::lock_guard<std::mutex> lk(M->mu);
+        M->slot_busy[slot] = 0;
         M->active--;
       }
-      M->cv_slot.notify_one();
+      M->cv_slot.notify_all();
     }
     {
       std::lock_guard<std::mutex> lk(M->mu);
@@ -158,6 +166,7 @@ int vg_multi_set_active(vg_multi* M, int cap) {
   for (const Worker& w : M->wk)
     if (!w.q.empty()) return VG_E_STATE;
   M->cap = cap >= (int)M->ctx.size() ? 0 : cap;
+  M->slot_busy.assign(M->cap > 0 ? M->cap : 0, 0);
   return VG_OK;
 }
 
