@@ -12,7 +12,7 @@ path = sys.argv[1]
 name = sys.argv[2] if len(sys.argv) > 2 else "k_ba_solve"
 min_us = float(sys.argv[3]) if len(sys.argv) > 3 else 10.0
 d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in csv.DictReader(open(path))
-     if r["Kernel_Name"].startswith("vg::" + name + "(")]
+     if r["Kernel_Name"].replace("void ", "").startswith(("vg::" + name + "(", "vg::" + name + "<"))]
 ex = [x for x in d if x >= min_us]
 out = {"kernel": name, "launches": len(d), "executed": len(ex),
        "executed_avg_us": round(sum(ex) / max(1, len(ex)), 3),

@@ -20,7 +20,7 @@ KERNELS = {"vg::k_ba_solve": 16.0, "vg::k_iekf": 256.0}  # name -> min KiB of an
 def load(path):
     d = defaultdict(list)
     for r in csv.DictReader(open(path)):
-        d[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+        d[r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0]].append(float(r["Counter_Value"]))
     return d
 
 

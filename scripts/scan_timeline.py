@@ -21,7 +21,7 @@ def main():
     back = int(sys.argv[2]) if len(sys.argv) > 2 else 4
     rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), int(r["Queue_Id"]))
                   for r in csv.DictReader(open(path)))
-    iekf = [i for i, r in enumerate(rows) if r[2] in ("k_iekf", "k_iekf_all")]
+    iekf = [i for i, r in enumerate(rows) if r[2].split("<")[0] in ("k_iekf", "k_iekf_all")]
     scans, last = [], -1e18
     for i in iekf:
         if rows[i][0] - last > 300000:

@@ -111,9 +111,10 @@ def test_recut_replay_path_equals_fast_path(knob):
 
 @pytest.mark.parametrize("ka,kb,exact", [({}, {18: 1}, True), ({19: 0}, {}, True), ({21: 0}, {}, True),
                                          ({20: 1}, {20: 1, 22: 1}, True), ({}, {20: 1}, False),
-                                         ({}, {13: 1}, True)],
+                                         ({}, {13: 1}, True), ({23: 0}, {}, True)],
                          ids=["lm-chunk-sums-in-prep", "lm-bookkeeping-in-resid", "margi-exist-up",
-                              "iekf-resident-iterations", "iekf-update-in-kernel", "device-propagation"])
+                              "iekf-resident-iterations", "iekf-update-in-kernel", "device-propagation",
+                              "iekf-plane-prefetch"])
 def test_fused_launches_equal_separate(ka, kb, exact):
     """Every launch fusion of the scan chain against its separate-launch form
     (vgx_debug knobs; r04e's A/B kept only margi's): k_ba_hfinal's ordered
@@ -124,7 +125,8 @@ def test_fused_launches_equal_separate(ka, kb, exact):
     partials in 15 row groups where the 1024-lane k_iekf_update uses 60, so
     only its rounding may differ: counters exact, poses within 1e-12 m. The
     device IMU propagation (13: k_scan_prop, from the margi head's flag)
-    keeps the host's expression trees: bit-identical to host propagation."""
+    keeps the host's expression trees: bit-identical to host propagation; so
+    does k_iekf's early touch of a cached match's plane record (23)."""
     p = vgconfig.load("mid360")
     seq = _seq(p, seq_id=7)
     a = vgpu.Context(vgconfig.to_c(p), **CAP)

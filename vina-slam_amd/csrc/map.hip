@@ -289,6 +289,10 @@ __device__ __forceinline__ void iekf_fused_update(DState* __restrict__ st, int i
 }
 // one IEKF iteration's point loop over the workgroup's chunk vb (k_iekf,
 // k_iekf_all): the 34 sums of this lane's points
+// kPf: a point whose cached leaf matched last iteration (octos[i]) touches its
+// plane record's 128 B lines right away, beside the header load, so the
+// gate's record reads hit in cache instead of a second dependent miss
+template <bool kPf = false>
 __device__ __forceinline__ void iekf_points(const MP& mp, const DState* __restrict__ st, const DevMap& m,
                                             int* __restrict__ cache, int* __restrict__ pk, int it, int nb, int vb,
                                             const M3& R, const V3& p, const M3& rot_var, const M3& tsl_var,
@@ -316,6 +320,13 @@ __device__ __forceinline__ void iekf_points(const MP& mp, const DState* __restri
     int leaf = cv >= 0 ? (cv & 0x3fffffff) : -1;
     int flag = 0;
     double sigma = 0;
+    double pf0 = 0.0, pf1 = 0.0, pf2 = 0.0;
+    if (kPf && cv >= 0 && !(cv & 0x40000000)) {  // bytes 0, 112, 216: every 128 B line the 224 B record spans
+      const double* rec = reinterpret_cast<const double*>(&m.pl[leaf]);
+      pf0 = rec[0];
+      pf1 = rec[14];
+      pf2 = rec[27];
+    }
     // a matched leaf (octos[i]): OctoTree::inside's inclusive box; a memo: the
     // descent's own region (dbox: strict where the descent is strict), so a
     // point on a centre plane is never kept in the wrong sibling
@@ -326,6 +337,7 @@ __device__ __forceinline__ void iekf_points(const MP& mp, const DState* __restri
       hit = pack_key(wld, mp.vs, kw) && pack_key(v3(hl.center[0], hl.center[1], hl.center[2]), mp.vs, kl) && kw == kl;
     }
     if (hit) {
+      if (kPf) asm volatile("" ::"v"(pf0), "v"(pf1), "v"(pf2));  // the touches complete here, not before
       flag = match_leaf(m.hdr[leaf], m.pl[leaf], wld, var_world, sigma);
       if (!flag && !(cv & 0x40000000)) leaf = -2;  // the reference's octos[i] stays: keep the cache
     } else {
@@ -408,6 +420,7 @@ __device__ __forceinline__ void pose_of(const double* w, M3& R, V3& p, M3& rot_v
   p = v3(w[9], w[10], w[11]);
 }
 
+template <bool kPf>
 __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, int it, DevMap m,
                                               int* __restrict__ cache, double* __restrict__ partials,
                                               int* __restrict__ pk, int npt) {
@@ -440,7 +453,7 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
     return;
   }
   double acc[kIekfVals];
-  iekf_points(mp, st, m, cache, pk, it, nb, vb, R, p, rot_var, tsl_var, acc);
+  iekf_points<kPf>(mp, st, m, cache, pk, it, nb, vb, R, p, rot_var, tsl_var, acc);
   if (blockIdx.x == 0) VG_PROBE_MARK(30);  // the point loop (thread 0 of block 0)
   __shared__ double red[4][kIekfVals];
   const double v = iekf_wg_sum(acc, red);
@@ -581,18 +594,23 @@ __global__ void __launch_bounds__(256) k_iekf_planes(const DState* __restrict__ 
 // agent-scope release per workgroup, which on the multi-XCD MI355X writes back
 // the XCD's L2 each time: measured ~20 us per iteration, far more than the
 // launch it saves.)
+// done_flag: the update that finishes the IEKF also advances the IEKF ->
+// insert hand-off flag (one workgroup: one release), so no k_sync_set launch
+// follows the IEKF graph
 __global__ void __launch_bounds__(1024) k_iekf_update(int nb, const double* __restrict__ partials,
-                                                     DState* __restrict__ st, int it) {
+                                                     DState* __restrict__ st, int it, unsigned* done_flag) {
   __shared__ IekfLds L;
   if (st->done) return;
   iekf_update_block(nb, partials, st, it, L);
+  if (done_flag && L.fin) iekf_signal_done(done_flag);
 }
 // sharded mode: this shard's 34 sums (the update then runs on the all-reduced ones)
 __global__ void __launch_bounds__(256) k_iekf_reduce(int nb, const double* __restrict__ partials,
                                                      const DState* __restrict__ st, double* __restrict__ out) {
   __shared__ IekfLds L;
   if (st->done) return;
-  iekf_reduce_block(nb, partials, L);
+  const int n = st->sn;
+  iekf_reduce_block(nb, partials, L, n < nb * 256 ? (n + 255) / 256 : nb);
   if (threadIdx.x < kIekfVals) out[threadIdx.x] = L.o[threadIdx.x];
 }
 
@@ -606,7 +624,7 @@ int iekf_grid(vg_ctx* ctx) { return iekf_blocks(ctx); }
 // one IEKF iteration: the point loop (block partials) and the update; the
 // optional event pair brackets k_iekf alone (vg_profile)
 int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
-                   hipEvent_t ev0, hipEvent_t ev1, int tag, hipStream_t s) {
+                   hipEvent_t ev0, hipEvent_t ev1, int tag, hipStream_t s, unsigned* done_flag) {
   Work& w = ctx->wk;
   if (!s) s = ctx->stream;
   (void)x;
@@ -623,7 +641,8 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
   }
   if (!fused) ctx->iekf_armed = false;  // plain partials from here on
   if (ev0) VG_HIP(hipEventRecord(ev0, s));
-  k_iekf<<<nb + (fused ? 1 : 0), 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials,
+  auto kern = ctx->iekf_prefetch ? k_iekf<true> : k_iekf<false>;
+  kern<<<nb + (fused ? 1 : 0), 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials,
                                              tag ? w.pk_leaf : nullptr, nb);
   if (ev1) VG_HIP(hipEventRecord(ev1, s));
   if (fused) {
@@ -635,9 +654,9 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
     double* sums = ctx->shard.d_buf;
     k_iekf_reduce<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, sums);
     VG_TRY(shard_allreduce(ctx, sums, sums + 64, kIekfVals, 0, 0));
-    k_iekf_update<<<1, 1024, 0, s>>>(-1, sums + 64, ctx->st, it);
+    k_iekf_update<<<1, 1024, 0, s>>>(-1, sums + 64, ctx->st, it, nullptr);
   } else {
-    k_iekf_update<<<1, 1024, 0, s>>>(nb, w.partials, ctx->st, it);
+    k_iekf_update<<<1, 1024, 0, s>>>(nb, w.partials, ctx->st, it, done_flag);
   }
   VG_HIP(hipGetLastError());
   return VG_OK;
@@ -721,25 +740,35 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
     if (signalled) *signalled = signal;
     return VG_OK;
   }
+  // the separate-update form signals the hand-off from its last update
+  // (k_iekf_update; not with the update inside k_iekf, nor when sharded)
+  const bool self_signal = signal && !ctx->iekf_fused && ctx->shard.world <= 1;
+  unsigned* flag = self_signal ? ctx->d_sync + 1 : nullptr;
   auto enqueue = [&]() -> int {
     for (int it = 0; it < 4; it++)
       VG_TRY(iekf_iteration(ctx, mp, x, y, z, n, it, ev ? ctx->iekf_ev[bank + it][0] : nullptr,
                             ev ? ctx->iekf_ev[bank + it][1] : nullptr,
-                            graph || !ctx->prof_stages ? 0 : ++ctx->plane_tag, s));
+                            graph || !ctx->prof_stages ? 0 : ++ctx->plane_tag, s, flag));
     return VG_OK;
   };
-  if (!graph) return enqueue();
-  if (!ctx->g_iekf[0]) {
+  if (!graph) {
+    VG_TRY(enqueue());
+    if (signalled) *signalled = self_signal;
+    return VG_OK;
+  }
+  hipGraphExec_t& ge = ctx->g_iekf[self_signal ? 3 : 0];
+  if (!ge) {
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     const int r = enqueue();
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(s, &g);
     if (r != VG_OK) return r;
     VG_HIP(e);
-    VG_HIP(hipGraphInstantiate(&ctx->g_iekf[0], g, nullptr, nullptr, 0));
+    VG_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     VG_HIP(hipGraphDestroy(g));
   }
-  VG_HIP(hipGraphLaunch(ctx->g_iekf[0], s));
+  VG_HIP(hipGraphLaunch(ge, s));
+  if (signalled) *signalled = self_signal;
   return VG_OK;
 }
 

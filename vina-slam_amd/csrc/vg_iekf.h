@@ -34,7 +34,11 @@ struct IekfLds {
 // kIekfGroups), lane pair 2*(tid % 17); then the G groups in order
 // (deterministic). A 1024-lane update runs 60 groups of ~9 rows each: the
 // dependent chains of L2 / cross-XCD loads are 4x shorter than with 15.
-__device__ __forceinline__ void iekf_reduce_block(int nb, const double* __restrict__ partials, IekfLds& L) {
+// (nact: the workgroups whose chunk holds points, iekf_chunk below; the
+// others' rows are +0 and skipped — the same sums)
+__device__ __forceinline__ int iekf_chunk(int b, int nb);
+__device__ __forceinline__ void iekf_reduce_block(int nb, const double* __restrict__ partials, IekfLds& L,
+                                                  int nact) {
   const int tid = threadIdx.x;
   const int G = (int)blockDim.x / 17 < kIekfGroups ? (int)blockDim.x / 17 : kIekfGroups;
   const int g = tid / 17, j2 = 2 * (tid % 17);
@@ -42,6 +46,7 @@ __device__ __forceinline__ void iekf_reduce_block(int nb, const double* __restri
     double a0 = 0.0, a1 = 0.0;
 #pragma unroll 4
     for (int b = g; b < nb; b += G) {
+      if (iekf_chunk(b, nb) >= nact) continue;
       const double2 v = *reinterpret_cast<const double2*>(&partials[(size_t)b * kIekfVals + j2]);
       a0 += v.x;
       a1 += v.y;
@@ -179,7 +184,8 @@ __device__ void iekf_update_block(int nb, const double* __restrict__ partials, D
                                   IekfLds& L) {
   const int tid = threadIdx.x;
   if (nb >= 0) {
-    iekf_reduce_block(nb, partials, L);
+    const int n = st->sn;
+    iekf_reduce_block(nb, partials, L, n < nb * 256 ? (n + 255) / 256 : nb);
   } else {  // sharded mode: `partials` holds the all-reduced sums
     if (tid < kIekfVals) L.o[tid] = partials[tid];
     __syncthreads();

@@ -367,7 +367,7 @@ struct vg_ctx {
   bool tail_a_valid = false;  // ev_tail_a marks the latest main-stream work the next IEKF depends on
   hipEvent_t ev_scan_ready = nullptr;  // deskew done (row f1)
   // the IEKF's 8 launches captured once and replayed (map.hip iekf_run)
-  hipGraphExec_t g_iekf[3] = {nullptr, nullptr, nullptr};
+  hipGraphExec_t g_iekf[4] = {nullptr, nullptr, nullptr, nullptr};  // [0] per-iteration launches, [1] k_iekf_all, [2] k_iekf_all signalling, [3] [0] signalling
   hipGraphExec_t g_margi[2] = {};  // margi after the window view (map.hip map_margi): ungated, gated
   hipGraphExec_t g_ba = nullptr;     // one LM iteration (ba.hip ba_run)
   hipGraphExec_t g_ba2 = nullptr;    // the first two LM iterations
@@ -437,6 +437,7 @@ struct vg_ctx {
   bool roots_lb = true;      // root registration in one look-back launch (vgx_debug 16: 0 = two launches)
   bool ba_graph2 = true;     // the first two LM iterations as one graph (vgx_debug 17: 0 = one graph each)
   bool margi_fused = true;    // margi isexist bottom-up in k_margi_copy, erase in one launch (vgx_debug 21: 0 = per-level launches)
+  bool iekf_prefetch = true;  // vgx_debug 23: k_iekf touches a cached match's plane record beside its header (r04i A/B +0.9 %)
   int iekf_all_cap = 0;       // k_iekf_all: workgroups resident at once (0: not yet asked, -1: too few)
   bool iekf_persist = false;  // vgx_debug 22 (with 20): the four IEKF iterations as one launch, k_iekf_all (r04e A/B: slower)
   bool iekf_fused = false;    // vgx_debug 20: the IEKF update as k_iekf's last workgroup (r04e A/B: -23 %)
@@ -613,7 +614,8 @@ inline hipError_t flush_insert_events(vg_ctx* ctx) {
 }
 int map_reset(vg_ctx* ctx);
 int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const float* z, int n, int it,
-                   hipEvent_t ev0, hipEvent_t ev1, int tag = 0, hipStream_t s = nullptr);
+                   hipEvent_t ev0, hipEvent_t ev1, int tag = 0, hipStream_t s = nullptr,
+                   unsigned* done_flag = nullptr);
 // all four iterations; replays the captured graph when possible
 // begin_xc != nullptr: open the scan on the device first (x_curr after
 // propagation, one launch with the scan binding)
