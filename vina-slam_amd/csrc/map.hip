@@ -2935,6 +2935,7 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
     make_win_block(st, wa, m.wpn, win, nper, slot_of);
     __syncthreads();  // x_curr (set_xc), seen by the whole block
     if (seq > 0) publish_state_block(st, wa.win_count, ba_iters_valid, ba_iters, ba_hess, pub, seq);
+    if (threadIdx.x == 0) st->margi_seq = seq;  // k_margi_copy hands it to the next IEKF
     if (head_flag) {  // x_curr is final: the next scan's propagation may start (vg_ctx::d_sync[2])
       __threadfence();
       __syncthreads();
@@ -3075,8 +3076,15 @@ constexpr int kCopyWaves = 4;
 __global__ void __launch_bounds__(64 * kCopyWaves) k_margi_copy(const int* __restrict__ nleaves,
                                                                 const int* __restrict__ plan,
                                                                 const WinD* __restrict__ win, DevMap m, const int* __restrict__ gate,
-                                                                const int* __restrict__ leaves, int exist_up) {
+                                                                const int* __restrict__ leaves, int exist_up,
+                                                                unsigned* __restrict__ tail_flag,
+                                                                const DState* __restrict__ st) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
+  // k_margi_leaf (the plane updates the next IEKF reads) has ended: its writes
+  // are released, so the hand-off flag to the IEKF stream goes up now, with
+  // the margi head's number (no k_sync_set launch between the two kernels)
+  if (tail_flag && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(tail_flag, (unsigned)st->margi_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int lane = threadIdx.x & 63;
   const int nl = *nleaves;
   if (exist_up)
@@ -3378,14 +3386,17 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
       bi ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, pub_seq, m, ctx->ba.fac_eig, ctx->ba.fac_pcr, w.plan, gate,
       flags ? ctx->d_sync + 2 : nullptr);
   VG_HIP(hipEventRecord(ctx->ev_tail_a, s));
-  if (flags) {
-    VG_TRY(sync_set(ctx, s, 0, (unsigned)pub_seq, gate));  // the margi's publication number (stage_margi_slide)
-  }
+  // the margi's publication number into the IEKF hand-off flag: by the margi
+  // graph's first kernel (k_margi_copy) — or k_sync_set when the local map
+  // publication sits in between
+  const bool copy_signals = flags && !(ctx->pub_flags & 1);
+  if (flags && !copy_signals) VG_TRY(sync_set(ctx, s, 0, (unsigned)pub_seq, gate));
   if (ctx->pub_flags & 1) k_local_map<<<64, kBlock, 0, s>>>(dwin, m, ctx->d_cmap, ctx->d_cmap_n, gate);
   ctx->tail_a_valid = true;
   auto body = [&]() -> int {
     const bool fused = ctx->margi_fused;
-    k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, dwin, m, gate, w.list0, fused ? 1 : 0);
+    k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, dwin, m, gate, w.list0, fused ? 1 : 0,
+                                                  copy_signals ? ctx->d_sync : nullptr, ctx->st);
     if (fused) {
       k_margi_erase_all<<<gl * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(nlev, thread_num, m, w.list1, w.rc, gate);
     } else {
@@ -3402,7 +3413,7 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   };
   (void)n_oldest;
   if (!ctx->use_graphs || ctx->prof_stages) return body();
-  hipGraphExec_t& ge = ctx->g_margi[gate ? 1 : 0];
+  hipGraphExec_t& ge = ctx->g_margi[(gate ? 1 : 0) + (copy_signals ? 2 : 0)];
   if (!ge) {
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     const int r = body();

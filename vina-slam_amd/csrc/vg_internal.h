@@ -269,7 +269,7 @@ struct DState {
   // IMU_PRE records of the window factors (preintegrated deltas, bias
   // Jacobians, cov_inv; constant once pushed): a ring, factor k at slot
   // (imu_head + k) % kMaxWin, so the slide is one index step
-  int imu_head, pad_h[3];
+  int imu_head, margi_seq, pad_h[2];  // margi_seq: the last margi head's publication number (k_margi_copy signals it)
   double imurec[kMaxWin * kBaImuRec];
   KClock clk;
   // k_iekf_all: the pose each IEKF iteration 1-3 starts from (R 9, p 3, rot / tsl
@@ -368,7 +368,7 @@ struct vg_ctx {
   hipEvent_t ev_scan_ready = nullptr;  // deskew done (row f1)
   // the IEKF's 8 launches captured once and replayed (map.hip iekf_run)
   hipGraphExec_t g_iekf[4] = {nullptr, nullptr, nullptr, nullptr};  // [0] per-iteration launches, [1] k_iekf_all, [2] k_iekf_all signalling, [3] [0] signalling
-  hipGraphExec_t g_margi[2] = {};  // margi after the window view (map.hip map_margi): ungated, gated
+  hipGraphExec_t g_margi[4] = {};  // margi after the window view (map.hip map_margi): [gated + 2 * signalling]
   hipGraphExec_t g_ba = nullptr;     // one LM iteration (ba.hip ba_run)
   hipGraphExec_t g_ba2 = nullptr;    // the first two LM iterations
   hipGraphExec_t g_ds = nullptr;     // the per-scan downsample chain (downsample.hip ds_enqueue_hashed)
