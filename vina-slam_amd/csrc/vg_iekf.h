@@ -183,6 +183,7 @@ __device__ __forceinline__ void iekf_update_tail(DState* __restrict__ st, int it
 __device__ void iekf_update_block(int nb, const double* __restrict__ partials, DState* __restrict__ st, int it,
                                   IekfLds& L) {
   const int tid = threadIdx.x;
+  VG_PROBE_BEGIN();
   if (nb >= 0) {
     const int n = st->sn;
     iekf_reduce_block(nb, partials, L, n < nb * 256 ? (n + 255) / 256 : nb);
@@ -190,6 +191,7 @@ __device__ void iekf_update_block(int nb, const double* __restrict__ partials, D
     if (tid < kIekfVals) L.o[tid] = partials[tid];
     __syncthreads();
   }
+  VG_PROBE_MARK(23);  // the ordered sum of the block partials
   iekf_update_tail(st, it, L);
 }
 // the update once L.o holds the 34 sums
