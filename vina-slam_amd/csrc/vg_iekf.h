@@ -43,13 +43,29 @@ __device__ __forceinline__ void iekf_reduce_block(int nb, const double* __restri
   const int G = (int)blockDim.x / 17 < kIekfGroups ? (int)blockDim.x / 17 : kIekfGroups;
   const int g = tid / 17, j2 = 2 * (tid % 17);
   if (g < G) {
+    // the group's first kRows rows loaded at once (one memory round trip, not
+    // one per row), then summed in the same row order
+    constexpr int kRows = 9;  // ceil(512 / 60): a 512-workgroup grid in one batch
+    double2 v[kRows];
+    bool ok[kRows];
+#pragma unroll
+    for (int k = 0; k < kRows; k++) {
+      const int b = g + k * G;
+      ok[k] = b < nb && iekf_chunk(b, nb) < nact;
+      v[k] = ok[k] ? *reinterpret_cast<const double2*>(&partials[(size_t)b * kIekfVals + j2]) : make_double2(0.0, 0.0);
+    }
     double a0 = 0.0, a1 = 0.0;
-#pragma unroll 4
-    for (int b = g; b < nb; b += G) {
+#pragma unroll
+    for (int k = 0; k < kRows; k++)
+      if (ok[k]) {
+        a0 += v[k].x;
+        a1 += v[k].y;
+      }
+    for (int b = g + kRows * G; b < nb; b += G) {
       if (iekf_chunk(b, nb) >= nact) continue;
-      const double2 v = *reinterpret_cast<const double2*>(&partials[(size_t)b * kIekfVals + j2]);
-      a0 += v.x;
-      a1 += v.y;
+      const double2 w = *reinterpret_cast<const double2*>(&partials[(size_t)b * kIekfVals + j2]);
+      a0 += w.x;
+      a1 += w.y;
     }
     L.red[g][j2] = a0;
     L.red[g][j2 + 1] = a1;
@@ -179,11 +195,28 @@ __device__ __forceinline__ void iekf_reduce_spin(int nb, int nact, double* parti
   __syncthreads();
 }
 
-__device__ __forceinline__ void iekf_update_tail(DState* __restrict__ st, int it, IekfLds& L);
+__device__ __forceinline__ void iekf_update_tail(DState* __restrict__ st, int it, IekfLds& L, bool vec_done = false);
+// vec = x_prop ⊟ x_curr (IMUST::operator-, types.hpp:80-86), one thread
+__device__ __forceinline__ void iekf_vec(const DState* __restrict__ st, IekfLds& L) {
+  const double* xp = st->xp;
+  const double* xc = st->xc;
+  const V3 rr = Log(mul(tr(ld_m3(xc)), ld_m3(xp)));
+  for (int k = 0; k < 3; k++) {
+    L.vec[k] = rr[k];
+    L.vec[3 + k] = xp[9 + k] - xc[9 + k];
+    L.vec[6 + k] = xp[12 + k] - xc[12 + k];
+    L.vec[9 + k] = xp[15 + k] - xc[15 + k];
+    L.vec[12 + k] = xp[18 + k] - xc[18 + k];
+  }
+}
 __device__ void iekf_update_block(int nb, const double* __restrict__ partials, DState* __restrict__ st, int it,
                                   IekfLds& L) {
   const int tid = threadIdx.x;
   VG_PROBE_BEGIN();
+  // x_curr does not change before the update's end: vec on a lane the
+  // ordered sum leaves idle (17 x 60 = 1020 of 1024), beside the sum
+  const bool vec_early = (int)blockDim.x > 17 * kIekfGroups;
+  if (vec_early && tid == (int)blockDim.x - 1) iekf_vec(st, L);
   if (nb >= 0) {
     const int n = st->sn;
     iekf_reduce_block(nb, partials, L, n < nb * 256 ? (n + 255) / 256 : nb);
@@ -192,10 +225,10 @@ __device__ void iekf_update_block(int nb, const double* __restrict__ partials, D
     __syncthreads();
   }
   VG_PROBE_MARK(23);  // the ordered sum of the block partials
-  iekf_update_tail(st, it, L);
+  iekf_update_tail(st, it, L, vec_early);
 }
 // the update once L.o holds the 34 sums
-__device__ __forceinline__ void iekf_update_tail(DState* __restrict__ st, int it, IekfLds& L) {
+__device__ __forceinline__ void iekf_update_tail(DState* __restrict__ st, int it, IekfLds& L, bool vec_done) {
   const int tid = threadIdx.x;
   VG_PROBE_BEGIN();
   const double* o = L.o;
@@ -268,18 +301,7 @@ __device__ __forceinline__ void iekf_update_tail(DState* __restrict__ st, int it
     L.G6[r][c] = s;
     st->G6[r * 6 + c] = s;
   }
-  if (tid == 128) {  // vec = x_prop ⊟ x_curr (IMUST::operator-, types.hpp:80-86)
-    const double* xp = st->xp;
-    const double* xc = st->xc;
-    const V3 rr = Log(mul(tr(ld_m3(xc)), ld_m3(xp)));
-    for (int k = 0; k < 3; k++) {
-      L.vec[k] = rr[k];
-      L.vec[3 + k] = xp[9 + k] - xc[9 + k];
-      L.vec[6 + k] = xp[12 + k] - xc[12 + k];
-      L.vec[9 + k] = xp[15 + k] - xc[15 + k];
-      L.vec[12 + k] = xp[18 + k] - xc[18 + k];
-    }
-  }
+  if (tid == 128 && !vec_done) iekf_vec(st, L);  // (iekf_update_block: computed beside the sum)
   __syncthreads();
   if (tid < 15) {  // sol = (K6 HTz + vec) - G6 v6
     double s1 = L.K6[tid][0] * o[21];
