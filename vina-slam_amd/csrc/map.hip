@@ -2929,7 +2929,7 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
                                                     Pub* __restrict__ pub, int seq, DevMap m,
                                                     const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
                                                     int* __restrict__ plan, const int* __restrict__ gate,
-                                                    unsigned* __restrict__ head_flag) {
+                                                    unsigned* __restrict__ head_flag, int batch) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   if (blockIdx.x == 0) {  // the margi head: x_curr <- x_buf.back(), the window view, the state publication
     make_win_block(st, wa, m.wpn, win, nper, slot_of);
@@ -2984,11 +2984,28 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
         h.opt_state = -1;
       } else {
         add_ = m.pcr_fix[node];
-        for (int i = 0; i < wa.win_count; i++) {
-          int si = wa.mp[i];
-          if (loc[si].N != 0) {
-            Clu t = (i == 0) ? w0 : clu_transform(loc[si], ld_m3(xs + (size_t)i * kXS), ld_v3(xs + (size_t)i * kXS + 9));
-            clu_add(add_, t);
+        if (batch) {  // the frame clusters read four at a time (one round trip each four), merged in frame order
+          for (int i0 = 0; i0 < wa.win_count; i0 += 4) {
+            Clu c[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+              if (i0 + k < wa.win_count) c[k] = loc[wa.mp[i0 + k]];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              const int i = i0 + k;
+              if (i < wa.win_count && c[k].N != 0) {
+                Clu t = (i == 0) ? w0 : clu_transform(c[k], ld_m3(xs + (size_t)i * kXS), ld_v3(xs + (size_t)i * kXS + 9));
+                clu_add(add_, t);
+              }
+            }
+          }
+        } else {
+          for (int i = 0; i < wa.win_count; i++) {
+            int si = wa.mp[i];
+            if (loc[si].N != 0) {
+              Clu t = (i == 0) ? w0 : clu_transform(loc[si], ld_m3(xs + (size_t)i * kXS), ld_v3(xs + (size_t)i * kXS + 9));
+              clu_add(add_, t);
+            }
           }
         }
         if (h.is_plane) {
@@ -3384,7 +3401,7 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   k_margi_leaf<<<1 + 512 * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(
       m.counters + kCntLeaves, w.list0, mp, wa2, ctx->st, dwin, dn, dn + 32, bi != nullptr, bi,
       bi ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, pub_seq, m, ctx->ba.fac_eig, ctx->ba.fac_pcr, w.plan, gate,
-      flags ? ctx->d_sync + 2 : nullptr);
+      flags ? ctx->d_sync + 2 : nullptr, ctx->margi_batch ? 1 : 0);
   VG_HIP(hipEventRecord(ctx->ev_tail_a, s));
   // the margi's publication number into the IEKF hand-off flag: by the margi
   // graph's first kernel (k_margi_copy) — or k_sync_set when the local map
