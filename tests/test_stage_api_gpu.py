@@ -111,10 +111,11 @@ def test_recut_replay_path_equals_fast_path(knob):
 
 @pytest.mark.parametrize("ka,kb,exact", [({}, {18: 1}, True), ({19: 0}, {}, True), ({21: 0}, {}, True),
                                          ({20: 1}, {20: 1, 22: 1}, True), ({}, {20: 1}, False),
-                                         ({}, {13: 1}, True), ({23: 0}, {}, True), ({24: 0}, {}, True)],
+                                         ({}, {13: 1}, True), ({23: 0}, {}, True), ({24: 0}, {}, True),
+                                         ({}, {25: 1}, True)],
                          ids=["lm-chunk-sums-in-prep", "lm-bookkeeping-in-resid", "margi-exist-up",
                               "iekf-resident-iterations", "iekf-update-in-kernel", "device-propagation",
-                              "iekf-plane-prefetch", "margi-batched-cluster-loads"])
+                              "iekf-plane-prefetch", "margi-batched-cluster-loads", "lm-solve-dataflow"])
 def test_fused_launches_equal_separate(ka, kb, exact):
     """Every launch fusion of the scan chain against its separate-launch form
     (vgx_debug knobs; r04e's A/B kept only margi's): k_ba_hfinal's ordered

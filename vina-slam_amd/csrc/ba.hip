@@ -648,7 +648,7 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
                                                   const double* __restrict__ jvec, const int* __restrict__ ipg,
                                                   const double* __restrict__ xs, double* __restrict__ xt,
                                                   double* __restrict__ bias, double* __restrict__ dxi_out,
-                                                  BaState* __restrict__ st, KClock* __restrict__ clk) {
+                                                  BaState* __restrict__ st, KClock* __restrict__ clk, int df) {
   if (st->done) return;
   const unsigned long long clk0 = wall_clock64();  // vg_profile bit 2 (KClock)
   extern __shared__ __attribute__((aligned(16))) double T[];
@@ -802,6 +802,103 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
       pt1 = t;
     }
   };
+  if (df) {
+    // Dataflow form: no workgroup barrier per phase. Wave 0 starts phase K as
+    // soon as row K+1's first two tiles carry panels 0..K-1 (the trailing
+    // piece that updates them raises s_rowv[K+1]); the twelve trailing waves
+    // keep phase order among themselves (arrival counter -> s_tdone) and start
+    // phase K once -S_KK^-1 is stored (s_tinv). Wave 0 keeps its -L^T tiles
+    // until every reader of the S tile they replace (trailing phase K) is done.
+    __shared__ int s_tinv, s_tdone, s_arr[kMaxNB], s_rowv[kMaxNB];
+    if (tid == 0) {
+      s_tinv = 0;
+      s_tdone = 0;
+    }
+    if (tid < kMaxNB) {
+      s_arr[tid] = 0;
+      s_rowv[tid] = 0;
+    }
+    __syncthreads();
+    auto wait_ge = [&](int* p, int target) __attribute__((always_inline)) {  // bounded: never a hung GPU
+      for (int spin = 0; __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target &&
+                         spin < (1 << 22);
+           spin++)
+        __builtin_amdgcn_s_sleep(1);
+    };
+    auto done_phases = [&]() __attribute__((always_inline)) {
+      return __hip_atomic_load(&s_tdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    if (wave == 0) {
+      v4d q0 = v4d{0.0, 0.0, 0.0, 0.0}, q1 = q0;
+      int k0 = -1, k1 = -1;  // phases of the queued -L^T(K+1, K) tiles, oldest first
+      for (int K = 0; K + 1 < NB; K++) {
+        if (K > 0) wait_ge(&s_rowv[K + 1], K);
+        while (k0 >= 0 && k0 < done_phases()) {  // readers of S(k0+1, k0) are done
+          st_tile(&T[tix(k0 + 1, k0) * 256], q0);
+          k0 = k1;
+          q0 = q1;
+          k1 = -1;
+        }
+        const v4d s1 = ld_ops(&T[tix(K + 1, K) * 256]);
+        v4d a = ld_tile(&T[tix(K + 1, K + 1) * 256]);
+        const v4d gt = mk_gt(tinv, s1);
+        a = tile_upd(a, gt, s1);
+        if (k0 < 0) {
+          k0 = K;
+          q0 = gt;
+        } else if (k1 < 0) {
+          k1 = K;
+          q1 = gt;
+        } else {  // two queued already: the oldest's readers must finish first
+          wait_ge(&s_tdone, k0 + 1);
+          st_tile(&T[tix(k0 + 1, k0) * 256], q0);
+          k0 = k1;
+          q0 = q1;
+          k1 = K;
+          q1 = gt;
+        }
+        tinv = diag(a);
+        st_tile(&T[tix(K + 1, K + 1) * 256], tinv);
+        __hip_atomic_store(&s_tinv, K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      wait_ge(&s_tdone, NB - 1);
+      if (k0 >= 0) st_tile(&T[tix(k0 + 1, k0) * 256], q0);
+      if (k1 >= 0) st_tile(&T[tix(k1 + 1, k1) * 256], q1);
+    } else if (wave & 3) {
+      const int wk = wave - (wave >> 2) - 1;
+      constexpr int nwk = 12;
+      for (int K = 0; K + 1 < NB; K++) {
+        wait_ge(&s_tinv, K);
+        wait_ge(&s_tdone, K);
+        flush();  // this wave's -L^T of phase K-1 (every reader finished phase K-1)
+        const v4d tv = ld_ops(&T[tix(K, K) * 256]);
+        int q = 0;
+        if (q++ == wk) {
+          w_job(K, false);
+          y_upd(mk_gt(tv, ld_ops(&T[tix(K + 1, K) * 256])), K, K + 1);
+        }
+        for (int I = K + 2; I < NB; I++)
+          for (int J0 = K + 1; J0 <= I; J0 += 4) {
+            if (q++ % nwk != wk) continue;
+            const v4d gt = mk_gt(tv, ld_ops(&T[tix(I, K) * 256]));
+            const int J1 = J0 + 4 < I + 1 ? J0 + 4 : I + 1;
+            for (int J = J0; J < J1; J++) {
+              double* Tij = &T[tix(I, J) * 256];
+              st_tile(Tij, tile_upd(ld_tile(Tij), gt, ld_ops(&T[tix(J, K) * 256])));
+            }
+            if (J0 == K + 1) {
+              y_upd(gt, K, I);
+              pend(gt, tix(I, K));
+              if (I == K + 2) __hip_atomic_store(&s_rowv[I], K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+          }
+        if (lane == 0 && __hip_atomic_fetch_add(&s_arr[K], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == nwk - 1)
+          __hip_atomic_store(&s_tdone, K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      flush();
+    }
+    __syncthreads();
+  } else
   for (int K = 0; K + 1 < NB; K++) {
     flush();
     if (wave == 0) {
@@ -1371,7 +1468,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
                                     d.dvec, d.jvec, d.ipg, d.st);
     if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][0], s);
     k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
-                                         d.st, &ctx->st->clk);
+                                         d.st, &ctx->st->clk, ctx->ba_dataflow ? 1 : 0);
     if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][1], s);
     k_ba_resid<<<nrb + 1, 256, 0, s>>>(nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
                                        ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, nimu, d.imurec, &ctx->st->imu_head, d.bias,
@@ -1559,7 +1656,7 @@ int ba_solve_test(vg_ctx* ctx, const double* A, const double* b, double* x) {
   VG_HIP(hipMemcpyAsync(d.st, &bs, sizeof(bs), hipMemcpyHostToDevice, s));
   VG_HIP(hipStreamSynchronize(s));
   k_ba_solve<<<1, 1024, solve_lds_bytes(W), s>>>(W, W - 1, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias,
-                                                 d.dxi, d.st, nullptr);
+                                                 d.dxi, d.st, nullptr, ctx->ba_dataflow ? 1 : 0);
   VG_HIP(hipGetLastError());
   std::vector<double> out(n);
   VG_HIP(hipMemcpyAsync(out.data(), d.dxi, n * sizeof(double), hipMemcpyDeviceToHost, s));

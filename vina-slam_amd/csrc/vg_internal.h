@@ -436,6 +436,7 @@ struct vg_ctx {
   bool prof_stages = false;  // per-stage events (vg_profile bit 1)
   bool roots_lb = true;      // root registration in one look-back launch (vgx_debug 16: 0 = two launches)
   bool ba_graph2 = true;     // the first two LM iterations as one graph (vgx_debug 17: 0 = one graph each)
+  bool ba_dataflow = false;   // vgx_debug 25: k_ba_solve without a workgroup barrier per phase (flags in LDS)
   bool margi_batch = true;    // vgx_debug 24: k_margi_leaf reads a leaf's frame clusters four at a time (r04k +0.4 %)
   bool margi_fused = true;    // margi isexist bottom-up in k_margi_copy, erase in one launch (vgx_debug 21: 0 = per-level launches)
   bool iekf_prefetch = true;  // vgx_debug 23: k_iekf touches a cached match's plane record beside its header (r04i A/B +0.9 %)

@@ -811,6 +811,10 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     VG_HIP(hipMemcpy(ctx->shard.d_seq, &s, sizeof(s), hipMemcpyHostToDevice));
     return VG_OK;
   }
+  if (key == 25) {  // 1: the LM solve's phases meet at LDS flags, not workgroup barriers
+    ctx->ba_dataflow = value != 0;
+    return VG_OK;
+  }
   if (key == 24) {  // 1: k_margi_leaf batches a leaf's frame-cluster loads
     ctx->margi_batch = value != 0;
     return VG_OK;
