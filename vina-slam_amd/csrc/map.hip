@@ -2049,6 +2049,9 @@ __global__ void __launch_bounds__(kApplyThreads) k_rc_apply(int L, int sub_cap, 
 }
 
 constexpr int kRcPushWaves = 4;
+constexpr int kPushScan = 4;    // event batches a push scans in one round (rc_push_child)
+constexpr int kPreN = 32 * 9;   // s_pre: the frame clusters' P/v, then their point counts
+constexpr int kPreV = 5;        // s_pre values per lane (32 slots * 10 / 64)
 // the pushes of one child (push_fix then push per frame, octree.cpp:151-188)
 // by one wave: its events keys[j0, j1) (point_fix first, then frame by
 // frame), its parent and layer given (the caller may have initialised the
@@ -2066,14 +2069,98 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
   NodeHdr& h = m.hdr[child];
   const NodeHdr& ph = m.hdr[parent];
   const bool listed = layer < mp.max_layer;
-  // leading point_fix events (phase 0 sorts first)
-  int nfix = 0;
-  for (int b0 = j0; b0 < j1; b0 += 64) {
-    const int e = b0 + lane;
-    const bool f = e < j1 && ((keys[e] >> 21) & 63) == 0;
-    const int k = __popcll(__ballot(f));
-    nfix += k;
-    if (k < 64) break;
+#ifdef VG_PROBE
+  const bool pr = blockIdx.x == 0 && threadIdx.x == 0;  // workgroup 0's wave 0: 40 pushes, 41 events,
+  unsigned long long pt0 = wall_clock64();              // 42 prologue, 43 batch loads, 44 serial sums
+  if (pr) {
+    atomicAdd(&g_probe[40], 1ull);
+    atomicAdd(&g_probe[41], (unsigned long long)(j1 - j0));
+  }
+#define PUSH_MARK(k)                                    \
+  do {                                                  \
+    if (pr) {                                           \
+      const unsigned long long n_ = wall_clock64();     \
+      atomicAdd(&g_probe[(k)], n_ - pt0);               \
+      pt0 = n_;                                         \
+    }                                                   \
+  } while (0)
+#else
+#define PUSH_MARK(k) (void)0
+#endif
+  // the child's events are phase << 21 | index, ascending: point_fix
+  // (phase 0) first, then one contiguous run per window slot (phase 1 + ord).
+  // Up to kPushScan batches are read in one round of loads and the runs are
+  // counted with ballots; longer children binary-search the keys.
+  const int nev = j1 - j0, wc = listed ? win->win_count : 0;
+  // the prologue's other loads go out with the keys' (one round): each
+  // lane's window slot and its epoch, the frame clusters (s_pre, stored
+  // below) and the accumulators' starting values
+  const int my_slot = lane < win->win_count ? win->mp[lane] : 0;  // listed or not (the batches read it)
+  const int my_epoch = lane < wc ? m.slot_epoch[my_slot] : 0;
+  double pv[kPreV];
+#pragma unroll
+  for (int i = 0; i < kPreV; i++) {
+    const int t = lane + 64 * i;
+    pv[i] = 0.0;
+    if (t < mp.W * 10) {
+      const int sl = t < mp.W * 9 ? t / 9 : t - mp.W * 9, q = t < mp.W * 9 ? t % 9 : 9;
+      const Clu& lc = m.pcrs[(size_t)child * mp.W + sl];
+      pv[i] = q < 6 ? lc.P[q] : (q < 9 ? lc.v[q - 6] : (double)lc.N);
+    }
+  }
+  auto acc_ptr = [&](int r, int slot) -> double* {
+    if (r < 9) return r < 6 ? &m.pcr_add[child].P[r] : &m.pcr_add[child].v[r - 6];
+    if (r < 18) return r < 15 ? &m.pcr_fix[child].P[r - 9] : &m.pcr_fix[child].v[r - 15];
+    if (r < 63) return &m.cov_add[(size_t)child * kCovN + r - 18];
+    Clu& lc = m.pcrs[(size_t)child * mp.W + slot];
+    return r < 69 ? &lc.P[r - 63] : &lc.v[r - 69];
+  };
+  double a0 = r0 < 63 ? *acc_ptr(r0, 0) : 0.0, a1 = 0.0;
+  const int n_add0 = lane == 0 ? m.pcr_add[child].N : 0, n_fix0 = lane == 0 ? m.pcr_fix[child].N : 0;
+  int nfix = 0, run_lo = 0, run_n = 0;
+  const bool short_ev = nev <= 64 * kPushScan;  // the keys stay in registers (kv) for the batches below
+  uint64_t kv[kPushScan];
+  if (short_ev) {
+    int phv[kPushScan];
+#pragma unroll
+    for (int b = 0; b < kPushScan; b++) {
+      const int e = 64 * b + lane;
+      kv[b] = e < nev ? keys[j0 + e] : 0ull;
+      phv[b] = e < nev ? (int)((kv[b] >> 21) & 63) : 64;
+    }
+#pragma unroll
+    for (int b = 0; b < kPushScan; b++) nfix += __popcll(__ballot(phv[b] == 0));
+    for (int q = 1, acc = nfix; q <= wc && acc < nev; q++) {
+      int c = 0;
+#pragma unroll
+      for (int b = 0; b < kPushScan; b++) c += __popcll(__ballot(phv[b] == q));
+      if (lane == q - 1) {
+        run_lo = j0 + acc;
+        run_n = c;
+      }
+      acc += c;
+    }
+  } else {
+    for (int b0 = j0; b0 < j1; b0 += 64) {
+      const int e = b0 + lane;
+      const bool f = e < j1 && ((keys[e] >> 21) & 63) == 0;
+      const int k = __popcll(__ballot(f));
+      nfix += k;
+      if (k < 64) break;
+    }
+    if (lane < wc) {
+      auto lower = [&](uint64_t key) {
+        int lo = j0, hi = j1;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (keys[mid] < key) lo = mid + 1;
+          else hi = mid;
+        }
+        return lo;
+      };
+      run_lo = lower((uint64_t)(lane + 1) << 21);
+      run_n = lower((uint64_t)(lane + 2) << 21) - run_lo;
+    }
   }
   int fix_off = 0;
   if (nfix > 0 && listed) {
@@ -2092,59 +2179,36 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
     fix_off = __shfl(off, 0, 64);
     if (fix_off < 0) return;
   }
-  // the child's run of each window slot (its events of phase 1 + ord are
-  // contiguous and in index order): lane p < win_count finds phase p + 1's
-  // range by binary search and takes the run from the slot's arena
-  int run_lo = 0, run_st = 0;
-  if (listed) {
-    const int wc = win->win_count;
-    if (lane < wc) {
-      const uint64_t base = 0;  // a child's events: phase << 21 | index, ascending
-      auto lower = [&](uint64_t key) {
-        int lo = j0, hi = j1;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (keys[mid] < key) lo = mid + 1;
-          else hi = mid;
-        }
-        return lo;
-      };
-      run_lo = lower(base | ((uint64_t)(lane + 1) << 21));
-      const int cnt = lower(base | ((uint64_t)(lane + 2) << 21)) - run_lo;
-      if (cnt > 0) {
-        const int slot = win->mp[lane];
-        run_st = atomicAdd(&m.arena[slot], cnt);
-        if (run_st + cnt > m.ord_stride) {
-          atomicOr(&m.counters[kCntErr], 16);
-          run_st = 0;
-        } else {
-          m.lseg[(size_t)child * mp.W + slot] = lseg_pack(run_st, cnt, m.slot_epoch[slot]);
-        }
-      }
+  // lane p < win_count takes phase p + 1's run from the slot's arena
+  int run_st = 0;
+  if (lane < wc && run_n > 0) {
+    run_st = atomicAdd(&m.arena[my_slot], run_n);
+    if (run_st + run_n > m.ord_stride) {
+      atomicOr(&m.counters[kCntErr], 16);
+      run_st = 0;
+    } else {
+      m.lseg[(size_t)child * mp.W + my_slot] = lseg_pack(run_st, run_n, my_epoch);
     }
   }
-  auto acc_ptr = [&](int r, int slot) -> double* {
-    if (r < 9) return r < 6 ? &m.pcr_add[child].P[r] : &m.pcr_add[child].v[r - 6];
-    if (r < 18) return r < 15 ? &m.pcr_fix[child].P[r - 9] : &m.pcr_fix[child].v[r - 15];
-    if (r < 63) return &m.cov_add[(size_t)child * kCovN + r - 18];
-    Clu& lc = m.pcrs[(size_t)child * mp.W + slot];
-    return r < 69 ? &lc.P[r - 63] : &lc.v[r - 69];
-  };
-  // every slot's frame cluster in one round of independent loads (a slot's
-  // run is contiguous, so each is read once, before this wave writes it):
-  // a cluster switch then costs an LDS read, not a dependent HBM load
-  for (int t = lane; t < mp.W * 9; t += 64) {
-    const Clu& lc = m.pcrs[(size_t)child * mp.W + t / 9];
-    const int q = t % 9;
-    s_pre[t] = q < 6 ? lc.P[q] : lc.v[q - 6];
+  // every slot's frame cluster, loaded above in one round (a slot's run is
+  // contiguous, so each is read once, before this wave writes it): a cluster
+  // switch then costs an LDS read, not a dependent HBM load; their point
+  // counts sit at s_pre[kPreN + slot], so the count update at a switch is a
+  // plain store
+#pragma unroll
+  for (int i = 0; i < kPreV; i++) {
+    const int t = lane + 64 * i;
+    if (t < mp.W * 10) s_pre[t < mp.W * 9 ? t : kPreN + t - mp.W * 9] = pv[i];
   }
-  double a0 = r0 < 63 ? *acc_ptr(r0, 0) : 0.0, a1 = 0.0;
   int cur_slot = -1, loc_n = 0, nwin = 0;
+  PUSH_MARK(42);
   for (int b0 = j0; b0 < j1; b0 += 64) {
-    const int e = b0 + lane;
+    const int e = b0 + lane, bi = (b0 - j0) >> 6;
+    const uint64_t k = !short_ev ? (e < j1 ? keys[e] : 0ull)
+                                 : (bi == 0 ? kv[0] : bi == 1 ? kv[1] : bi == 2 ? kv[2] : kv[3]);
+    const int phase = (int)((k >> 21) & 63), idx = (int)(k & ((1u << 21) - 1));
+    const int slot_e = __shfl(my_slot, phase > 0 ? phase - 1 : 0, 64);  // win->mp[phase - 1]
     if (e < j1) {
-      const uint64_t k = keys[e];
-      const int phase = (int)((k >> 21) & 63), idx = (int)(k & ((1u << 21) - 1));
       if (phase == 0) {
         const size_t f = (size_t)ph.fix_off + idx;
         const V3 pt = ld_v3(&m.fix_pnt[f * 3]);
@@ -2157,7 +2221,7 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
           for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = var[t];
         }
       } else {
-        const int ord = phase - 1, slot = win->mp[ord];
+        const int ord = phase - 1, slot = slot_e;
         const size_t bb = (size_t)slot * m.cap_wp + idx;
         const V3 pnt = ld_v3(&m.wp_pnt[bb * 3]);
         fill_record(E[lane], pnt, rigid(ld_m3(win->R[ord]), pnt, ld_v3(win->p[ord])),
@@ -2167,16 +2231,16 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
       }
     }
     if (listed) {  // the point into the child's run (ds_bpermute of the run's lane; uniform call)
-      const int e = b0 + lane;
-      const int ph = e < j1 ? (int)((keys[e] >> 21) & 63) : 0;
+      const int ph = e < j1 ? phase : 0;
       const int src = ph > 0 ? ph - 1 : 0;
       const int lo_p = __shfl(run_lo, src, 64), st_p = __shfl(run_st, src, 64);
-      if (ph > 0) m.wp_ord[(size_t)win->mp[ph - 1] * m.ord_stride + st_p + (e - lo_p)] = (int)(keys[e] & ((1u << 21) - 1));
+      if (ph > 0) m.wp_ord[(size_t)slot_e * m.ord_stride + st_p + (e - lo_p)] = idx;
     }
     const int nb = (j1 - b0) < 64 ? (j1 - b0) : 64;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    PUSH_MARK(43);
 #pragma unroll 4
     for (int k = 0; k < nb; k++) {
       const int slot = s_slot[k];
@@ -2185,7 +2249,7 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
         if (cur_slot >= 0) {
           if (r0 >= 63) *acc_ptr(r0, cur_slot) = a0;
           if (has1) *acc_ptr(r1, cur_slot) = a1;
-          if (lane == 63) m.pcrs[(size_t)child * mp.W + cur_slot].N += loc_n;
+          if (lane == 63) m.pcrs[(size_t)child * mp.W + cur_slot].N = (int)s_pre[kPreN + cur_slot] + loc_n;
         }
         cur_slot = slot;
         if (r0 >= 63) a0 = s_pre[cur_slot * 9 + r0 - 63];
@@ -2203,16 +2267,18 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
       }
     }
     __builtin_amdgcn_wave_barrier();
+    PUSH_MARK(44);
   }
+#undef PUSH_MARK
   if (r0 < 63) *acc_ptr(r0, 0) = a0;
   if (cur_slot >= 0) {
     if (r0 >= 63) *acc_ptr(r0, cur_slot) = a0;
     if (has1) *acc_ptr(r1, cur_slot) = a1;
-    if (lane == 63) m.pcrs[(size_t)child * mp.W + cur_slot].N += loc_n;
+    if (lane == 63) m.pcrs[(size_t)child * mp.W + cur_slot].N = (int)s_pre[kPreN + cur_slot] + loc_n;
   }
   if (lane == 0) {
-    m.pcr_add[child].N += j1 - j0;
-    m.pcr_fix[child].N += nfix;
+    m.pcr_add[child].N = n_add0 + nev;
+    m.pcr_fix[child].N = n_fix0 + nfix;
     if (nwin > 0) {
       h.has_sw = 1;
       h.isexist = 1;
@@ -2233,7 +2299,7 @@ __global__ void __launch_bounds__(64 * kRcPushWaves) k_rc_push(int L, const uint
                                                                const int* __restrict__ rc) {
   __shared__ double E[kRcPushWaves][64][kErec];
   __shared__ int s_slot[kRcPushWaves][64];  // window slot of the event, -1 for point_fix
-  __shared__ double s_pre[kRcPushWaves][32 * 9];  // the child's frame clusters, read ahead
+  __shared__ double s_pre[kRcPushWaves][32 * 10];  // the child's frame clusters, read ahead
   if (rc[kRcAbort]) return;
   const int nch = rc[kRcCh + L], cbase = rc[kRcChBase + L];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2331,7 +2397,7 @@ __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level(
   __shared__ int s_ws[kRcFusedWaves];
   __shared__ double E[kRcFusedWaves][64][kErec];
   __shared__ int s_slot[kRcFusedWaves][64];
-  __shared__ double s_pre[kRcFusedWaves][32 * 9];
+  __shared__ double s_pre[kRcFusedWaves][32 * 10];
   if (rc[kRcAbort]) return;
   const int nsub = rc[kRcSub + L];
   if (nsub > sub_cap) {  // the host-sized path replays from this level
@@ -2341,6 +2407,22 @@ __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level(
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int ntot = rc[kRcNch + L];  // children of this level's subdividing leaves (rc_win_leaf)
   const int A = rc[kRcLvl + L];     // level L+1's other nodes (visit(L))
+#ifdef VG_PROBE
+  const int pb = L < 2 ? 8 * L : 32;  // per level: calls, sort, prefix, push, tail, nsub, ntot, A (block 0)
+  VG_PROBE_BEGIN();
+  if (blockIdx.x == 0 && tid == 0 && L < 3) {
+    atomicAdd(&g_probe[pb], 1ull);
+    atomicAdd(&g_probe[pb + 5], (unsigned long long)nsub);
+    atomicAdd(&g_probe[pb + 6], (unsigned long long)ntot);
+    atomicAdd(&g_probe[pb + 7], (unsigned long long)A);
+  }
+#define RC_MARK(k) \
+  do {             \
+    if (blockIdx.x == 0 && L < 3) VG_PROBE_MARK(pb + (k)); \
+  } while (0)
+#else
+#define RC_MARK(k) (void)0
+#endif
   const int base = (L == 0) ? rc[kRcNode0] : rc[kRcChBase + L - 1] + rc[kRcCh + L - 1];
   if (blockIdx.x == 0 && tid == 0) {
     rc[kRcCh + L] = ntot;
@@ -2373,6 +2455,7 @@ __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level(
       s_sub[rank] = myp;
     }
     __syncthreads();
+    RC_MARK(1);
     // per parent: its rcinfo slot and non-empty octants; exclusive prefix of their counts (4 per thread)
     int c4[4], sum = 0;
 #pragma unroll
@@ -2405,6 +2488,7 @@ __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level(
       run += c4[k];
     }
     __syncthreads();
+    RC_MARK(2);
     const RoleIdx ri0 = rc_push_role(lane), ri1 = rc_push_role(lane + 64 < 72 ? lane + 64 : 0);
     for (int c = blockIdx.x * kRcFusedWaves + wv; c < ntot; c += gridDim.x * kRcFusedWaves) {
       int lo = 0, hi = nsub - 1;  // the parent: the last t with s_coff[t] <= c
@@ -2418,6 +2502,20 @@ __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level(
       for (int i = 0; i < k; i++) mk &= mk - 1;
       const int o = __ffs(mk) - 1;  // the parent's k-th non-empty octant
       if (o < 0) continue;
+#ifdef VG_PROBE
+      unsigned long long qt = wall_clock64();  // workgroup 0's wave 0: 48 init, 49 push, 51 visit, 52 win, 53 wins
+      const bool qpr = blockIdx.x == 0 && tid == 0;
+#define Q_MARK(k)                                   \
+  do {                                              \
+    if (qpr) {                                      \
+      const unsigned long long n_ = wall_clock64(); \
+      atomicAdd(&g_probe[(k)], n_ - qt);            \
+      qt = n_;                                      \
+    }                                               \
+  } while (0)
+#else
+#define Q_MARK(k) (void)0
+#endif
       const int* inf = info_in + (size_t)s_q[t] * kRcInfo;
       const int j0 = inf[0] + inf[1 + o], j1 = j0 + inf[9 + o];
       const int child = base + c;
@@ -2439,7 +2537,9 @@ __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level(
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      Q_MARK(48);
       rc_push_child(child, p, layer, j0, j1, ev_in, mp, win, m, E[wv], s_slot[wv], s_pre[wv], ri0, ri1);
+      Q_MARK(49);
       // visit(L+1) of the new child (its cluster, counts and flags: this wave's stores just above)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -2453,14 +2553,24 @@ __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level(
         if (cand_bits) atomicOr(&cand_bits[child >> 5], 1u << (child & 31));
       }
       if (is_sub) sub_out[o3] = child;
-      if (do_win && __shfl(is_sub, 0, 64)) rc_win_leaf(L + 1, child, __shfl(o3, 0, 64), win, m, ev_out, info_out,
-                                                      cap, cap, rc);
+      Q_MARK(51);
+      if (do_win && __shfl(is_sub, 0, 64)) {
+        rc_win_leaf(L + 1, child, __shfl(o3, 0, 64), win, m, ev_out, info_out, cap, cap, rc);
+#ifdef VG_PROBE
+        if (qpr) atomicAdd(&g_probe[53], 1ull);
+#endif
+      }
+      Q_MARK(52);
+#undef Q_MARK
     }
+    RC_MARK(3);
   }
   // visit(L+1) (+ win(L+1)) of the level's other nodes, from the grid's last waves
   const int nwv = gridDim.x * kRcFusedWaves;
   for (int j = nwv - 1 - ((int)blockIdx.x * kRcFusedWaves + wv); j * 64 < A; j += nwv)
     rc_visit_chunk(L + 1, next, A, j, mp, m, next2, sub_out, cand, rc, cand_bits, do_win, win, ev_out, info_out, cap);
+  RC_MARK(4);
+#undef RC_MARK
 }
 
 // ---- host-sized path (overflow replay) ----------------------------------
