@@ -2441,10 +2441,22 @@ __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level(
     sub_finish(m, p);
   }
   if ((int)blockIdx.x * kRcFusedWaves < ntot) {
-    // apply(L): the subdividing leaves in ascending id order (rank among distinct ids, from LDS)
-    for (int t = tid; t < kApplySub; t += blockDim.x) s_in[t] = t < nsub ? sub_in[t] : 0x7fffffff;
+    // apply(L): the subdividing leaves in ascending id order (rank among distinct ids, from LDS),
+    // each with its rcinfo slot (its index in sub_in, rc_win_leaf's q) and octant mask, read in
+    // the same round as the ids
+    constexpr int kPer = kApplySub / (64 * kRcFusedWaves);
+    int mk_t[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const int t = tid + k * 64 * kRcFusedWaves;
+      s_in[t] = t < nsub ? sub_in[t] : 0x7fffffff;
+      mk_t[k] = (t < nsub && (size_t)t * kRcInfo + kRcInfo <= (size_t)cap) ? info_in[(size_t)t * kRcInfo + 17] : 0;
+    }
     __syncthreads();
-    for (int t = tid; t < nsub; t += blockDim.x) {
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const int t = tid + k * 64 * kRcFusedWaves;
+      if (t >= nsub) break;
       const int myp = s_in[t];
       int rank = 0;
       const int4* v4 = reinterpret_cast<const int4*>(s_in);
@@ -2453,6 +2465,8 @@ __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level(
         rank += (v.x < myp) + (v.y < myp) + (v.z < myp) + (v.w < myp);
       }
       s_sub[rank] = myp;
+      s_q[rank] = t;
+      s_mask[rank] = mk_t[k];
     }
     __syncthreads();
     RC_MARK(1);
@@ -2462,13 +2476,7 @@ __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level(
     for (int k = 0; k < 4; k++) {
       const int t = 4 * tid + k;
       c4[k] = 0;
-      if (t < nsub) {
-        const int p = s_sub[t], q = m.nscr[(size_t)p * 4 + 0];
-        const int mk = info_in[(size_t)q * kRcInfo + 17];
-        s_q[t] = q;
-        s_mask[t] = mk;
-        c4[k] = __popc(mk);
-      }
+      if (t < nsub) c4[k] = __popc(s_mask[t]);
       sum += c4[k];
     }
     int x = sum;
