@@ -2162,11 +2162,15 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
       run_n = lower((uint64_t)(lane + 2) << 21) - run_lo;
     }
   }
+  // the point_fix block and the slots' runs are allocated in one round (an
+  // overflow of either fails the scan with VG_E_CAPACITY, so a run taken
+  // beside a point_fix overflow is never used)
+  int off = 0, run_st = 0;
+  if (lane == 0 && nfix > 0 && listed) off = atomicAdd(&m.counters[kCntFix], nfix);
+  if (lane < wc && run_n > 0) run_st = atomicAdd(&m.arena[my_slot], run_n);
   int fix_off = 0;
   if (nfix > 0 && listed) {
-    int off = 0;
     if (lane == 0) {
-      off = atomicAdd(&m.counters[kCntFix], nfix);
       if (off + nfix > m.cap_fix) {
         atomicOr(&m.counters[kCntErr], 8);
         off = -1;
@@ -2179,10 +2183,8 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
     fix_off = __shfl(off, 0, 64);
     if (fix_off < 0) return;
   }
-  // lane p < win_count takes phase p + 1's run from the slot's arena
-  int run_st = 0;
+  // lane p < win_count holds phase p + 1's run in the slot's arena
   if (lane < wc && run_n > 0) {
-    run_st = atomicAdd(&m.arena[my_slot], run_n);
     if (run_st + run_n > m.ord_stride) {
       atomicOr(&m.counters[kCntErr], 16);
       run_st = 0;
