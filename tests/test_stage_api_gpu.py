@@ -109,25 +109,28 @@ def test_recut_replay_path_equals_fast_path(knob):
     assert np.array_equal(a.window_states(), b.window_states())
 
 
-@pytest.mark.parametrize("ka,kb,exact", [({}, {18: 1}, True), ({19: 0}, {}, True), ({21: 0}, {}, True),
-                                         ({20: 1}, {20: 1, 22: 1}, True), ({}, {20: 1}, False),
-                                         ({}, {13: 1}, True), ({23: 0}, {}, True), ({24: 0}, {}, True),
-                                         ({}, {25: 1}, True)],
-                         ids=["lm-chunk-sums-in-prep", "lm-bookkeeping-in-resid", "margi-exist-up",
-                              "iekf-resident-iterations", "iekf-update-in-kernel", "device-propagation",
-                              "iekf-plane-prefetch", "margi-batched-cluster-loads", "lm-solve-dataflow"])
+@pytest.mark.parametrize("ka,kb,exact", [({19: 0}, {}, True), ({21: 0}, {}, True), ({}, {13: 1}, True),
+                                         ({23: 0}, {}, True), ({24: 0}, {}, True), ({11: 0}, {}, True),
+                                         ({16: 0}, {}, True), ({17: 0}, {}, True), ({14: 0}, {}, True),
+                                         ({26: 0}, {}, True)],
+                         ids=["lm-bookkeeping-in-resid", "margi-exist-up", "device-propagation",
+                              "iekf-plane-prefetch", "margi-batched-cluster-loads", "recut-fused-levels",
+                              "root-registration-lookback", "lm-two-iteration-graph", "flag-hand-offs",
+                              "lm-outcome-deferred"])
 def test_fused_launches_equal_separate(ka, kb, exact):
-    """Every launch fusion of the scan chain against its separate-launch form
-    (vgx_debug knobs; r04e's A/B kept only margi's): k_ba_hfinal's ordered
-    sums inside k_ba_prep (18), k_ba_control inside k_ba_resid's IMU workgroup
-    (19), margi's bottom-up isexist by atomic reports + one erase launch (21),
-    the four IEKF iterations as one resident launch (22 against 20 alone) —
-    all bit-identical. The IEKF update inside k_iekf (20) reduces the block
-    partials in 15 row groups where the 1024-lane k_iekf_update uses 60, so
-    only its rounding may differ: counters exact, poses within 1e-12 m. The
-    device IMU propagation (13: k_scan_prop, from the margi head's flag)
-    keeps the host's expression trees: bit-identical to host propagation; so
-    does k_iekf's early touch of a cached match's plane record (23)."""
+    """Every default-on launch fusion or hand-off of the scan chain against its
+    separate-launch form (vgx_debug knobs), bit for bit: k_ba_control inside
+    k_ba_resid's IMU workgroup (19), margi's bottom-up isexist by atomic
+    reports + one erase launch (21), the device IMU propagation (13:
+    k_scan_prop keeps the host's expression trees), k_iekf's early touch of a
+    cached match's plane record (23), k_margi_leaf's batched cluster loads
+    (24), the fused recut levels against the four-launch level loop (11, same
+    node ids), root registration by decoupled look-back against two launches
+    (16), the first two LM iterations as one graph (17), the device-flag
+    hand-offs against event waits (14) and a step that returns before its
+    LM's outcome (26: the next step enqueues its IEKF first, then resolves it;
+    the first window-full scans need more LM iterations than predicted, so
+    the real margi tail replaces a speculative one there)."""
     p = vgconfig.load("mid360")
     seq = _seq(p, seq_id=7)
     a = vgpu.Context(vgconfig.to_c(p), **CAP)

@@ -419,40 +419,10 @@ __device__ __forceinline__ double quad_bcast(double v, int qd) {
   }
 }
 
-// the LiDAR Hessian / gradient / residual (k_ba_hess's outputs) as k_ba_prep
-// reads them: summed already (hl, k_ba_hfinal ran), or summed here from the
-// chunk partials in k_ba_hfinal's order (8 strided lane sums, then the fixed
-// shuffle tree), so each entry is formed where it is used and the separate
-// reduction launch goes (every lower entry is read by one tile, once)
-struct HlSrc {
-  const double* hl;
-  const double* part;  // non-null: sum the partials
-  int nchunk, nout;
-  __device__ __forceinline__ double operator[](int e) const {
-    if (!part) return hl[e];
-    double s[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) s[j] = 0.0;
-    int b0 = 0;
-    for (; b0 + 8 <= nchunk; b0 += 8) {
-      double v[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) v[j] = part[(size_t)(b0 + j) * nout + e];
-#pragma unroll
-      for (int j = 0; j < 8; j++) s[j] += v[j];
-    }
-#pragma unroll
-    for (int j = 0; j < 8; j++)
-      if (b0 + j < nchunk) s[j] += part[(size_t)(b0 + j) * nout + e];
-    const double t0 = s[0] + s[4], t1 = s[1] + s[5], t2 = s[2] + s[6], t3 = s[3] + s[7];
-    return (t0 + t2) + (t1 + t3);
-  }
-};
-
 // one assembled lower entry (R >= C) of the 15W x 15W system in the host
 // loop's accumulation order (divide_thread 215-222: IMU factors k ascending,
 // x imu_coef, then hess_plus 171-179 adds the LiDAR 6x6 blocks)
-__device__ __forceinline__ double asm_entry(int R, int C, int nimu, double imu_coef, const HlSrc& hl,
+__device__ __forceinline__ double asm_entry(int R, int C, int nimu, double imu_coef, const double* hl,
                                             const double* imuout, int L) {
   const int bR = R / 15, bC = C / 15, rR = R % 15, rC = C % 15;
   double v = 0.0;
@@ -465,7 +435,7 @@ __device__ __forceinline__ double asm_entry(int R, int C, int nimu, double imu_c
   }
   return v;
 }
-__device__ __forceinline__ double asm_grad(int t, int nimu, double imu_coef, const HlSrc& hl, const double* imuout,
+__device__ __forceinline__ double asm_grad(int t, int nimu, double imu_coef, const double* hl, const double* imuout,
                                            int L) {
   const int b = t / 15, r = t % 15;
   double v = 0.0;
@@ -487,8 +457,7 @@ __device__ __forceinline__ double asm_grad(int t, int nimu, double imu_coef, con
 // columns, zero gradient) are decoupled from the rest, so wherever Eigen's
 // pivot order puts them their elimination changes nothing and their solution
 // is 0: they are left out of the factored system (n - 15 unknowns).
-__global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coef, double* __restrict__ hl,
-                                                 const double* __restrict__ part, const int* __restrict__ nfp, int chunk,
+__global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coef, const double* __restrict__ hl,
                                                  const double* __restrict__ imuout, double* __restrict__ Hcalc,
                                                  double* __restrict__ Jcalc, double* __restrict__ timg,
                                                  double* __restrict__ bvec, double* __restrict__ dvec,
@@ -502,10 +471,8 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
   const int tid = threadIdx.x, q = blockIdx.x;
   const bool calc = st->calc_hess != 0;
   const double u = st->u;
-  const int nl = L * (L + 1) / 2, nout = nl + L + 1;
-  const HlSrc hs{hl, part, part ? (*nfp + chunk - 1) / chunk : 0, nout};
   for (int t = tid; t < n; t += blockDim.x)
-    Dv[t] = t < 15 ? 1.0 : (calc ? asm_entry(t, t, nimu, imu_coef, hs, imuout, L) : Hcalc[lo(t, t)]);
+    Dv[t] = t < 15 ? 1.0 : (calc ? asm_entry(t, t, nimu, imu_coef, hl, imuout, L) : Hcalc[lo(t, t)]);
   __syncthreads();
   for (int i = 15 + tid; i < n; i += blockDim.x) {  // rank of |D + u D| descending, index ascending on ties
     const unsigned long long ki = (unsigned long long)__double_as_longlong(fabs(Dv[i] + u * Dv[i]));
@@ -527,7 +494,7 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
       v = (R == C) ? 1.0 : 0.0;
     } else {
       const int pr = ip[R], pc = ip[C], a = pr > pc ? pr : pc, bb = pr > pc ? pc : pr;
-      const double raw = calc ? asm_entry(a, bb, nimu, imu_coef, hs, imuout, L) : Hcalc[lo(a, bb)];
+      const double raw = calc ? asm_entry(a, bb, nimu, imu_coef, hl, imuout, L) : Hcalc[lo(a, bb)];
       if (calc && R >= C) Hcalc[lo(a, bb)] = raw;
       v = (pr == pc) ? Dv[pr] + u * Dv[pr] : raw;
     }
@@ -535,9 +502,8 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
   }
   if (q == 0) {
     for (int t = tid; t < n; t += blockDim.x) {
-      const double raw = calc ? asm_grad(t, nimu, imu_coef, hs, imuout, L) : Jcalc[t];
+      const double raw = calc ? asm_grad(t, nimu, imu_coef, hl, imuout, L) : Jcalc[t];
       if (calc) Jcalc[t] = raw;
-      if (calc && part && t < L + 1) hl[nl + t] = hs[nl + t];  // gradient + residual for k_ba_control
       Jg[t] = t < 15 ? 0.0 : raw;
       dvec[t] = Dv[t];
       if (t < m) ipg[t] = ip[t];
@@ -648,7 +614,7 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
                                                   const double* __restrict__ jvec, const int* __restrict__ ipg,
                                                   const double* __restrict__ xs, double* __restrict__ xt,
                                                   double* __restrict__ bias, double* __restrict__ dxi_out,
-                                                  BaState* __restrict__ st, KClock* __restrict__ clk, int df) {
+                                                  BaState* __restrict__ st, KClock* __restrict__ clk) {
   if (st->done) return;
   const unsigned long long clk0 = wall_clock64();  // vg_profile bit 2 (KClock)
   extern __shared__ __attribute__((aligned(16))) double T[];
@@ -802,103 +768,6 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
       pt1 = t;
     }
   };
-  if (df) {
-    // Dataflow form: no workgroup barrier per phase. Wave 0 starts phase K as
-    // soon as row K+1's first two tiles carry panels 0..K-1 (the trailing
-    // piece that updates them raises s_rowv[K+1]); the twelve trailing waves
-    // keep phase order among themselves (arrival counter -> s_tdone) and start
-    // phase K once -S_KK^-1 is stored (s_tinv). Wave 0 keeps its -L^T tiles
-    // until every reader of the S tile they replace (trailing phase K) is done.
-    __shared__ int s_tinv, s_tdone, s_arr[kMaxNB], s_rowv[kMaxNB];
-    if (tid == 0) {
-      s_tinv = 0;
-      s_tdone = 0;
-    }
-    if (tid < kMaxNB) {
-      s_arr[tid] = 0;
-      s_rowv[tid] = 0;
-    }
-    __syncthreads();
-    auto wait_ge = [&](int* p, int target) __attribute__((always_inline)) {  // bounded: never a hung GPU
-      for (int spin = 0; __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target &&
-                         spin < (1 << 22);
-           spin++)
-        __builtin_amdgcn_s_sleep(1);
-    };
-    auto done_phases = [&]() __attribute__((always_inline)) {
-      return __hip_atomic_load(&s_tdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    if (wave == 0) {
-      v4d q0 = v4d{0.0, 0.0, 0.0, 0.0}, q1 = q0;
-      int k0 = -1, k1 = -1;  // phases of the queued -L^T(K+1, K) tiles, oldest first
-      for (int K = 0; K + 1 < NB; K++) {
-        if (K > 0) wait_ge(&s_rowv[K + 1], K);
-        while (k0 >= 0 && k0 < done_phases()) {  // readers of S(k0+1, k0) are done
-          st_tile(&T[tix(k0 + 1, k0) * 256], q0);
-          k0 = k1;
-          q0 = q1;
-          k1 = -1;
-        }
-        const v4d s1 = ld_ops(&T[tix(K + 1, K) * 256]);
-        v4d a = ld_tile(&T[tix(K + 1, K + 1) * 256]);
-        const v4d gt = mk_gt(tinv, s1);
-        a = tile_upd(a, gt, s1);
-        if (k0 < 0) {
-          k0 = K;
-          q0 = gt;
-        } else if (k1 < 0) {
-          k1 = K;
-          q1 = gt;
-        } else {  // two queued already: the oldest's readers must finish first
-          wait_ge(&s_tdone, k0 + 1);
-          st_tile(&T[tix(k0 + 1, k0) * 256], q0);
-          k0 = k1;
-          q0 = q1;
-          k1 = K;
-          q1 = gt;
-        }
-        tinv = diag(a);
-        st_tile(&T[tix(K + 1, K + 1) * 256], tinv);
-        __hip_atomic_store(&s_tinv, K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      wait_ge(&s_tdone, NB - 1);
-      if (k0 >= 0) st_tile(&T[tix(k0 + 1, k0) * 256], q0);
-      if (k1 >= 0) st_tile(&T[tix(k1 + 1, k1) * 256], q1);
-    } else if (wave & 3) {
-      const int wk = wave - (wave >> 2) - 1;
-      constexpr int nwk = 12;
-      for (int K = 0; K + 1 < NB; K++) {
-        wait_ge(&s_tinv, K);
-        wait_ge(&s_tdone, K);
-        flush();  // this wave's -L^T of phase K-1 (every reader finished phase K-1)
-        const v4d tv = ld_ops(&T[tix(K, K) * 256]);
-        int q = 0;
-        if (q++ == wk) {
-          w_job(K, false);
-          y_upd(mk_gt(tv, ld_ops(&T[tix(K + 1, K) * 256])), K, K + 1);
-        }
-        for (int I = K + 2; I < NB; I++)
-          for (int J0 = K + 1; J0 <= I; J0 += 4) {
-            if (q++ % nwk != wk) continue;
-            const v4d gt = mk_gt(tv, ld_ops(&T[tix(I, K) * 256]));
-            const int J1 = J0 + 4 < I + 1 ? J0 + 4 : I + 1;
-            for (int J = J0; J < J1; J++) {
-              double* Tij = &T[tix(I, J) * 256];
-              st_tile(Tij, tile_upd(ld_tile(Tij), gt, ld_ops(&T[tix(J, K) * 256])));
-            }
-            if (J0 == K + 1) {
-              y_upd(gt, K, I);
-              pend(gt, tix(I, K));
-              if (I == K + 2) __hip_atomic_store(&s_rowv[I], K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-          }
-        if (lane == 0 && __hip_atomic_fetch_add(&s_arr[K], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == nwk - 1)
-          __hip_atomic_store(&s_tdone, K + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      flush();
-    }
-    __syncthreads();
-  } else
   for (int K = 0; K + 1 < NB; K++) {
     flush();
     if (wave == 0) {
@@ -1402,7 +1271,8 @@ const int* ba_gate_dev(vg_ctx* ctx) { return &carve(ctx).st->fin; }
 // (pinned staging, uploaded asynchronously). The window states and the IMU
 // bias records are read and written in DState.
 int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::function<int()>& before_first_wait,
-           const std::function<int(bool*)>& spec_tail, bool* tail_ok) {
+           const std::function<int(bool*)>& spec_tail, bool* tail_ok, bool* pending) {
+  if (pending) *pending = false;
   const int W = ctx->cfg.win_size;
   if (15 * W > kMaxNB * kTile) {
     ctx->err = "win_size > 11 unsupported by the BA solve (LDS-resident 15W x 15W tile store)";
@@ -1448,10 +1318,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
     k_ba_hess<<<G + nimu, kHessThreads, hess_lds, s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
                                                       ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, nimu, d.imurec, &ctx->st->imu_head,
                                                       d.bias, d.imuout);
-    // unsharded, k_ba_prep sums the chunk partials itself (HlSrc)
-    const bool fuse = ctx->ba_fuse_final && !sharded && !(k == 0 && ctx->dbg_capture == 1);
-    if (!fuse)
-      k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, sharded ? hl_part : d.hl,
+    k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, sharded ? hl_part : d.hl,
                                                          d.st);
     // sharded: every shard's factors -> one LiDAR Hessian / gradient / residual
     // (out of place: a rejected step re-reduces the unchanged partial)
@@ -1463,12 +1330,11 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
       ctx->dbg_cap_n = nout + nimu * 931;
       ctx->dbg_capture = 2;
     }
-    k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, fuse ? d.part : nullptr, nfp, hess_chunk(W),
-                                    d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
+    k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
                                     d.dvec, d.jvec, d.ipg, d.st);
     if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][0], s);
     k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
-                                         d.st, &ctx->st->clk, ctx->ba_dataflow ? 1 : 0);
+                                         d.st, &ctx->st->clk);
     if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][1], s);
     k_ba_resid<<<nrb + 1, 256, 0, s>>>(nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
                                        ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, nimu, d.imurec, &ctx->st->imu_head, d.bias,
@@ -1543,6 +1409,19 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
       VG_TRY(spec_tail(&queued));
       if (queued) tail_at = enq;
     }
+    // the outcome is read later (ba_resolve): the tail is queued, every
+    // further iteration is a replay of the same graph
+    if (pending && tail_at > 0 && graph) {
+      ctx->ba_loop.seq0 = seq0;
+      ctx->ba_loop.enq = enq;
+      ctx->ba_loop.tail_at = tail_at;
+      ctx->ba_loop.k = k;
+      ctx->ba_loop.active = true;
+      *pending = true;
+      *iters = -1;
+      if (tail_ok) *tail_ok = true;
+      return VG_OK;
+    }
     VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_ba, seq0 + k, "k_ba_control"));
     // The flags may already come from iteration k+1 (queued ahead, possibly
     // finished by now): decide on iteration k's outcome only — done at or
@@ -1566,6 +1445,49 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
       }
     }
   (void)g_dummy;
+  return VG_OK;
+}
+
+// The rest of ba_run's loop for a run it left pending: the same decisions on
+// the same flags (iteration k's own outcome), every iteration a replay of the
+// one-iteration graph.
+int ba_resolve(vg_ctx* ctx, bool block, bool* finished, int* iters, bool* tail_ok) {
+  BaLoop& L = ctx->ba_loop;
+  *finished = true;
+  if (!L.active) return VG_OK;
+  hipStream_t s = ctx->stream;
+  auto launch = [&]() -> int {
+    const hipError_t e = hipGraphLaunch(ctx->g_ba, s);
+    if (e != hipSuccess) {
+      L.active = false;
+      ctx->err = std::string("hipGraphLaunch (LM iteration): ") + hipGetErrorString(e);
+      return VG_E_HIP;
+    }
+    L.enq++;
+    return VG_OK;
+  };
+  int done_iters = 0;
+  for (int k = L.k; k < 10; k++) {
+    L.k = k;
+    if (L.enq == k + 1 && L.enq < 10 && L.enq < ctx->ba_last_iters) VG_TRY(launch());  // one ahead
+    if (!block && __atomic_load_n(&ctx->h_pub->seq_ba, __ATOMIC_ACQUIRE) < L.seq0 + k) {
+      *finished = false;
+      return VG_OK;
+    }
+    const int r = pub_wait(ctx, &ctx->h_pub->seq_ba, L.seq0 + k, "k_ba_control");
+    if (r != VG_OK) {
+      L.active = false;
+      return r;
+    }
+    done_iters = __atomic_load_n(&ctx->h_pub->ba_iters, __ATOMIC_ACQUIRE);
+    if (__atomic_load_n(&ctx->h_pub->ba_done, __ATOMIC_ACQUIRE) && done_iters <= k + 1) break;
+    done_iters = k + 1;
+    if (L.enq == k + 1 && L.enq < 10) VG_TRY(launch());  // not queued ahead: now
+  }
+  L.active = false;
+  *tail_ok = L.tail_at > 0 && done_iters <= L.tail_at;
+  *iters = done_iters;
+  ctx->ba_last_iters = done_iters > 0 ? done_iters : 2;
   return VG_OK;
 }
 
@@ -1656,7 +1578,7 @@ int ba_solve_test(vg_ctx* ctx, const double* A, const double* b, double* x) {
   VG_HIP(hipMemcpyAsync(d.st, &bs, sizeof(bs), hipMemcpyHostToDevice, s));
   VG_HIP(hipStreamSynchronize(s));
   k_ba_solve<<<1, 1024, solve_lds_bytes(W), s>>>(W, W - 1, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias,
-                                                 d.dxi, d.st, nullptr, ctx->ba_dataflow ? 1 : 0);
+                                                 d.dxi, d.st, nullptr);
   VG_HIP(hipGetLastError());
   std::vector<double> out(n);
   VG_HIP(hipMemcpyAsync(out.data(), d.dxi, n * sizeof(double), hipMemcpyDeviceToHost, s));

@@ -99,7 +99,6 @@ int map_alloc(vg_ctx* ctx) {
   good &= ok(w.ev_odd = ctx->arena.take<uint64_t>(w.cap));
   w.nparts = 1024;
   good &= ok(w.partials = ctx->arena.take<double>((size_t)w.nparts * 40));
-  good &= ok(w.islots = ctx->arena.take<double>((size_t)4 * kIekfAllMax * kIekfVals));
   if (!good) {
     ctx->err = "arena exhausted (map)";
     return VG_E_CAPACITY;
@@ -269,26 +268,8 @@ __device__ __forceinline__ void halve(const double (&v)[N], double (&w)[(N + 1) 
 // read from the device state the previous k_iekf_update wrote; the kernel is a
 // no-op once the IEKF has finished (st->done). Iteration 0 ignores the leaf
 // cache (no association yet, odometry.cpp:111-132).
-// Fused form (npt < gridDim.x): workgroup npt, dispatched last, runs the
-// update itself: it takes the point-loop workgroups' partials from their
-// slots as they land (iekf_reduce_spin: relaxed agent-scope stores and
-// loads, no fence per workgroup) — no separate k_iekf_update launch.
-__device__ __forceinline__ void iekf_fused_update(DState* __restrict__ st, int it, int npt, double* partials,
-                                               int* __restrict__ err) {
-  __shared__ IekfLds L;
-  __shared__ int s_late;
-  if (threadIdx.x == 0) s_late = 0;
-  __syncthreads();
-  int late = 0;
-  const int n = st->sn;
-  iekf_reduce_spin(npt, n < npt * 256 ? (n + 255) / 256 : npt, partials, L, &late);
-  if (late) s_late = 1;
-  __syncthreads();
-  if (threadIdx.x == 0 && s_late) atomicOr(err, 64);
-  iekf_update_tail(st, it, L);
-}
-// one IEKF iteration's point loop over the workgroup's chunk vb (k_iekf,
-// k_iekf_all): the 34 sums of this lane's points
+// one IEKF iteration's point loop over the workgroup's chunk vb (k_iekf): the
+// 34 sums of this lane's points
 // kPf: a point whose cached leaf matched last iteration (octos[i]) touches its
 // plane record's 128 B lines right away, beside the header load, so the
 // gate's record reads hit in cache instead of a second dependent miss
@@ -423,12 +404,8 @@ __device__ __forceinline__ void pose_of(const double* w, M3& R, V3& p, M3& rot_v
 template <bool kPf>
 __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, int it, DevMap m,
                                               int* __restrict__ cache, double* __restrict__ partials,
-                                              int* __restrict__ pk, int npt) {
+                                              int* __restrict__ pk) {
   if (st->done) return;
-  if ((int)blockIdx.x >= npt) {
-    iekf_fused_update(st, it, npt, partials, m.counters + kCntErr);
-    return;
-  }
   const bool clk_on = st->clk.on != 0;
   const int clk_slot = (st->clk.scan * 4 + it) & (kClkRing - 1);
   if (clk_on && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -446,21 +423,14 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
   // round-robin over the 8 XCDs, so block b works on chunk (b % 8) * (nb / 8)
   // + b / 8 — each XCD sweeps a contiguous run of the scan and the plane /
   // node records of neighbouring points stay in its own L2 (nb % 8 == 0)
-  const int nb = npt;
+  const int nb = gridDim.x;
   const int vb = iekf_chunk(blockIdx.x, nb);
-  if ((int)gridDim.x > npt && vb * (int)blockDim.x >= n) {  // no points (fused form: no partial either)
-    if (clk_on && blockIdx.x < kClkBlocks && threadIdx.x == 0) st->clk.tend[clk_slot][blockIdx.x] = (unsigned long long)wall_clock64();
-    return;
-  }
   double acc[kIekfVals];
   iekf_points<kPf>(mp, st, m, cache, pk, it, nb, vb, R, p, rot_var, tsl_var, acc);
   if (blockIdx.x == 0) VG_PROBE_MARK(30);  // the point loop (thread 0 of block 0)
   __shared__ double red[4][kIekfVals];
   const double v = iekf_wg_sum(acc, red);
-  if (threadIdx.x < kIekfVals) {
-    if ((int)gridDim.x > npt) slot_put(&partials[(size_t)blockIdx.x * kIekfVals + threadIdx.x], v);  // the fused update reads it
-    else partials[(size_t)blockIdx.x * kIekfVals + threadIdx.x] = v;
-  }
+  if (threadIdx.x < kIekfVals) partials[(size_t)blockIdx.x * kIekfVals + threadIdx.x] = v;
   if (clk_on && blockIdx.x < kClkBlocks) {  // the workgroup's end (its partials written)
     __syncthreads();
     if (threadIdx.x == 0) st->clk.tend[clk_slot][blockIdx.x] = (unsigned long long)wall_clock64();
@@ -471,15 +441,6 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
 #endif
 }
 
-// The four IEKF iterations in one launch (odometry.cpp:98-230): npt point
-// workgroups and one update workgroup (the last dispatched), all resident at
-// once (npt + 1 <= 2 per CU: kIekfAllMax). Iteration it's partials go to slot
-// set it (iekf_reduce_spin takes and re-arms them); the update then stores the
-// next iteration's pose and the finished flag into DState::islot[it], which
-// every point workgroup polls before its next pass (relaxed agent-scope
-// stores and loads: no fence, no launch between iterations). Every wait is
-// bounded (error bit 64), so a workgroup that never became resident cannot
-// hang the GPU. Results equal k_iekf + update launches bit for bit.
 // the IEKF's end to the insert's stream (vg_ctx::d_sync[1]): every thread's
 // state writes released at agent scope (one workgroup: one L2 write-back),
 // then the flag advances by one
@@ -488,91 +449,6 @@ __device__ __forceinline__ void iekf_signal_done(unsigned* flag) {
   __threadfence();
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void iekf_all_update(DState* __restrict__ st, int npt, double* pslots,
-                                                int* __restrict__ err, unsigned* done_flag) {
-  __shared__ IekfLds L;
-  __shared__ int s_late;
-  const int n = st->sn;
-  const int nact = n < npt * 256 ? (n + 255) / 256 : npt;
-  for (int it = 0; it < 4; it++) {
-    if (threadIdx.x == 0) s_late = 0;
-    __syncthreads();
-    int late = 0;
-    iekf_reduce_spin(npt, nact, pslots + (size_t)it * npt * kIekfVals, L, &late);
-    if (late) s_late = 1;
-    __syncthreads();
-    if (s_late) {  // a point workgroup never delivered: stop them all
-      if (threadIdx.x == 0) atomicOr(err, 64);
-      if (it < 3 && threadIdx.x < 31) slot_put(&st->islot[it][threadIdx.x], 1.0);
-      iekf_signal_done(done_flag);
-      return;
-    }
-    iekf_update_tail(st, it, L);
-    __syncthreads();  // x_curr (thread 0 of the tail) seen by the block
-    const bool fin = L.fin != 0;
-    if (it < 3 && threadIdx.x < 31)
-      slot_put(&st->islot[it][threadIdx.x], threadIdx.x < 30 ? pose_word(st->xc, threadIdx.x) : (fin ? 1.0 : 0.0));
-    if (fin) {
-      iekf_signal_done(done_flag);
-      return;
-    }
-  }
-}
-__global__ void __launch_bounds__(256) k_iekf_all(MP mp, DState* __restrict__ st, DevMap m, int* __restrict__ cache,
-                                                  double* __restrict__ pslots, int npt, unsigned* done_flag) {
-  if (st->done) {  // (not within a scan: the opening clears it)
-    if ((int)blockIdx.x == npt) iekf_signal_done(done_flag);
-    return;
-  }
-  if ((int)blockIdx.x >= npt) {
-    iekf_all_update(st, npt, pslots, m.counters + kCntErr, done_flag);
-    return;
-  }
-  const int n = st->sn;
-  const int vb = iekf_chunk(blockIdx.x, npt);
-  if (vb * (int)blockDim.x >= n) return;  // no points in any iteration (the update skips the row)
-  __shared__ double red[4][kIekfVals];
-  __shared__ double s_pose[32];
-  __shared__ int s_late;
-  const bool clk_on = st->clk.on != 0;
-  for (int it = 0; it < 4; it++) {
-    if (threadIdx.x == 0) s_late = 0;
-    __syncthreads();  // the previous pass is done with s_pose / red
-    if (threadIdx.x < 31) {
-      double v;
-      if (it == 0) {
-        v = threadIdx.x < 30 ? pose_word(st->xc, threadIdx.x) : 0.0;
-      } else {
-        int late = 0;
-        v = slot_wait(&st->islot[it - 1][threadIdx.x], &late);
-        if (late) s_late = 1;
-      }
-      s_pose[threadIdx.x] = v;
-    }
-    __syncthreads();
-    if (s_late) {
-      if (threadIdx.x == 0) atomicOr(m.counters + kCntErr, 64);
-      return;
-    }
-    if (s_pose[30] != 0.0) return;  // the update finished the IEKF
-    M3 R, rot_var, tsl_var;
-    V3 p;
-    pose_of(s_pose, R, p, rot_var, tsl_var);
-    const int clk_slot = (st->clk.scan * 4 + it) & (kClkRing - 1);
-    if (clk_on && blockIdx.x == 0 && threadIdx.x == 0) {
-      st->clk.t0[clk_slot] = (unsigned long long)wall_clock64();
-      st->clk.exec[clk_slot] = 1;
-    }
-    double acc[kIekfVals];
-    iekf_points(mp, st, m, cache, nullptr, it, npt, vb, R, p, rot_var, tsl_var, acc);
-    const double v = iekf_wg_sum(acc, red);
-    if (threadIdx.x < kIekfVals) slot_put(&pslots[((size_t)it * npt + blockIdx.x) * kIekfVals + threadIdx.x], v);
-    if (clk_on && blockIdx.x < kClkBlocks) {
-      __syncthreads();
-      if (threadIdx.x == 0) st->clk.tend[clk_slot][blockIdx.x] = (unsigned long long)wall_clock64();
-    }
-  }
 }
 
 // P_k of SURVEY 8(d), the profiling pass only: distinct plane records the
@@ -632,23 +508,10 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
   (void)z;
   (void)n;  // the scan is read from the device state (state_set_scan)
   const int nb = iekf_blocks(ctx);
-  // the update inside k_iekf (one more workgroup) unless the sums are
-  // exchanged, k_iekf is timed alone, or the plane count runs in between
-  const bool fused = ctx->iekf_fused && ctx->shard.world <= 1 && !ev0 && !tag;
-  if (fused && !ctx->iekf_armed) {  // iekf_run arms the slots before a fused iteration
-    ctx->err = "fused IEKF update: partial slots not armed";
-    return VG_E_STATE;
-  }
-  if (!fused) ctx->iekf_armed = false;  // plain partials from here on
   if (ev0) VG_HIP(hipEventRecord(ev0, s));
   auto kern = ctx->iekf_prefetch ? k_iekf<true> : k_iekf<false>;
-  kern<<<nb + (fused ? 1 : 0), 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials,
-                                             tag ? w.pk_leaf : nullptr, nb);
+  kern<<<nb, 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials, tag ? w.pk_leaf : nullptr);
   if (ev1) VG_HIP(hipEventRecord(ev1, s));
-  if (fused) {
-    VG_HIP(hipGetLastError());
-    return VG_OK;
-  }
   if (tag) k_iekf_planes<<<nb, 256, 0, s>>>(ctx->st, ctx->map, w.pk_leaf, tag, &ctx->st->planes[it]);
   if (ctx->shard.world > 1) {  // this shard's sums, all-reduced, then the (replicated) update
     double* sums = ctx->shard.d_buf;
@@ -677,72 +540,8 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
   else if (!opened) VG_TRY(state_set_scan(ctx, x, y, z, n, s));
   const bool graph = ctx->use_graphs && ctx->shard.world <= 1 && !ctx->prof_stages;
   const bool ev = ctx->prof_on && !graph;
-  // the fused update's slots start empty (iekf_reduce_spin re-arms what it
-  // reads, so this runs only after something else used the buffer); outside
-  // the captured graph
-  if (ctx->iekf_fused && ctx->shard.world <= 1 && !ev && !ctx->prof_stages && !ctx->iekf_armed) {
-    VG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctx->wk.partials), (int)kSlotEmpty32,
-                             (size_t)iekf_blocks(ctx) * kIekfVals * 2, s));
-    ctx->iekf_armed = true;
-  }
-  // the four iterations as one launch (k_iekf_all): not with another context's
-  // IEKF possibly resident beside it (multi-sequence mode turns overlap_iekf
-  // off), not when k_iekf is timed alone or the sums are exchanged
-  if (ctx->iekf_persist && ctx->iekf_fused && ctx->overlap_iekf && ctx->shard.world <= 1 && !ev && !ctx->prof_stages &&
-      ctx->iekf_all_cap >= 0) {
-    Work& w = ctx->wk;
-    if (ctx->iekf_all_cap == 0) {  // workgroups the device holds at once (a partitioned GPU holds fewer)
-      int per_cu = 0, cus = 0;
-      VG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_iekf_all, 256, 0));
-      VG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
-      ctx->iekf_all_cap = per_cu * cus;
-    }
-    // Every active point workgroup, the update one and whatever else is
-    // resident for good must fit at once, per XCD: workgroups are dealt to
-    // the 8 XCDs in turn, so XCD 0 holds npt / 8 point workgroups plus the
-    // update one (the last dispatched), and the main stream's poll of the
-    // IEKF hand-off (k_sync_wait, resident until the IEKF ends) may sit on
-    // it too. Four slots per XCD stay spare (kIekfAllMax = 8 x (64 - 4) on a
-    // 256-CU part at two workgroups per CU).
-    int npt = iekf_blocks(ctx) < kIekfAllMax ? iekf_blocks(ctx) : kIekfAllMax;
-    if (npt > 8 * (ctx->iekf_all_cap / 8 - 4)) npt = 8 * (ctx->iekf_all_cap / 8 - 4);
-    npt = npt / 8 * 8;
-    if (npt < 64) {  // too small a device for the resident form: per-iteration launches from now on
-      ctx->iekf_all_cap = -1;
-      return iekf_run(ctx, mp, x, y, z, n, bank, nullptr, s, nullptr, false, nullptr, true);
-    }
-    if (!w.islots_armed) {  // iekf_reduce_spin re-arms what it reads
-      VG_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.islots), (int)kSlotEmpty32,
-                               (size_t)4 * kIekfAllMax * kIekfVals * 2, s));
-      w.islots_armed = true;
-    }
-    // the update workgroup advances the IEKF -> insert flag itself when asked
-    // (one release by one workgroup), so no k_sync_set launch follows the IEKF
-    unsigned* flag = signal ? ctx->d_sync + 1 : nullptr;
-    hipGraphExec_t& ge = ctx->g_iekf[signal ? 2 : 1];
-    if (!graph || !ge) {
-      if (graph) VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-      k_iekf_all<<<npt + 1, 256, 0, s>>>(mp, ctx->st, ctx->map, w.iekf_cache, w.islots, npt, flag);
-      const hipError_t le = hipGetLastError();
-      if (!graph) {
-        VG_HIP(le);
-        if (signalled) *signalled = signal;
-        return VG_OK;
-      }
-      hipGraph_t g = nullptr;
-      const hipError_t e = hipStreamEndCapture(s, &g);
-      VG_HIP(le);
-      VG_HIP(e);
-      VG_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-      VG_HIP(hipGraphDestroy(g));
-    }
-    VG_HIP(hipGraphLaunch(ge, s));
-    if (signalled) *signalled = signal;
-    return VG_OK;
-  }
-  // the separate-update form signals the hand-off from its last update
-  // (k_iekf_update; not with the update inside k_iekf, nor when sharded)
-  const bool self_signal = signal && !ctx->iekf_fused && ctx->shard.world <= 1;
+  // the last update signals the hand-off itself (k_iekf_update; not when sharded)
+  const bool self_signal = signal && ctx->shard.world <= 1;
   unsigned* flag = self_signal ? ctx->d_sync + 1 : nullptr;
   auto enqueue = [&]() -> int {
     for (int it = 0; it < 4; it++)
@@ -2773,7 +2572,6 @@ __global__ void __launch_bounds__(256) k_memo_probe(MP mp, DevMap m, int* __rest
 }
 int map_memo_probe(vg_ctx* ctx, const MP& mp, int* out) {
   int* dout = reinterpret_cast<int*>(ctx->wk.partials);  // scratch: the probe runs between scans
-  ctx->iekf_armed = false;                                // (the fused update's slots are re-armed)
   VG_HIP(hipMemsetAsync(dout, 0, 4 * sizeof(int), ctx->stream));
   k_memo_probe<<<256, 256, 0, ctx->stream>>>(mp, ctx->map, dout);
   VG_HIP(hipGetLastError());

@@ -90,7 +90,7 @@ static int map_error(vg_ctx* ctx, int e) {
              ((e & 2) ? " (root hash full)" : "") + ((e & 16) ? " (subdivision event buffer full)" : "") +
              ((e & 32) ? " (sharded exchange out of step: the ranks' exchange sequences differ)" : "") +
              ((e & 64) ? " (cross-stream hand-off timed out)" : "");
-  if (e & 32) return VG_E_STATE;
+  if (e & (32 | 64)) return VG_E_STATE;  // out-of-step exchange, or a hand-off that timed out: not a capacity limit
   return (e & 1) ? VG_E_RANGE : VG_E_CAPACITY;
 }
 
@@ -209,10 +209,31 @@ static int absorb_p2(vg_ctx* ctx, HostPipe* P, Pend& q) {
   return VG_OK;
 }
 
+// The outcome of the previous fused step's LM (stage_ba left it pending):
+// ba_resolve waits for its flags and enqueues any further iteration; if the
+// speculative margi tail did not run, the real one follows with the same
+// publication numbers and window view, so every wait already enqueued on
+// those numbers (the next IEKF's hand-off flags, the host's P1 / P2) holds.
+// block = false: returns without waiting when a flag is not published yet.
+static int resolve_lm(vg_ctx* ctx, HostPipe* P, bool block = true) {
+  if (!P->lmp.active) return VG_OK;
+  HostTimer ht_(ctx, kHostBA);
+  bool fin = true, tail_ok = true;
+  int iters = 0;
+  int r = ba_resolve(ctx, block, &fin, &iters, &tail_ok);
+  if (r == VG_OK && !fin) return VG_OK;
+  P->lmp.active = false;
+  if (r == VG_OK && !tail_ok)
+    r = map_margi(ctx, P->mpd, P->lmp.wa, 0, ctx->cfg.thread_num, P->lmp.seq1, P->lmp.seq2, nullptr);
+  if (r != VG_OK) P->sticky = r;
+  return r;
+}
+
 // absorb every pending scan whose results are needed (all of P1, and P2 when
 // `full`); blocking
 int absorb(vg_ctx* ctx, HostPipe* P, bool full) {
   if (P->sticky != VG_OK) return P->sticky;
+  VG_TRY(resolve_lm(ctx, P));
   int r = VG_OK;
   while (!P->pend.empty()) {
     Pend& q = P->pend.front();
@@ -235,6 +256,8 @@ int absorb(vg_ctx* ctx, HostPipe* P, bool full) {
 // scan being absorbed.
 int absorb_ready(vg_ctx* ctx, HostPipe* P) {
   if (P->sticky != VG_OK) return P->sticky;
+  VG_TRY(resolve_lm(ctx, P, false));
+  if (P->lmp.active) return VG_OK;  // the LM is still running: nothing of that scan is published
   while (!P->pend.empty()) {
     Pend& q = P->pend.front();
     if (q.seq1 != 0 && __atomic_load_n(&ctx->h_pub->seq1, __ATOMIC_ACQUIRE) < q.seq1) break;
@@ -255,6 +278,7 @@ int host_sync(vg_ctx* ctx) {
     ctx->err = "host_sync inside a scan";
     return VG_E_STATE;
   }
+  VG_TRY(resolve_lm(ctx, P));  // before the drain: it may enqueue work
   VG_HIP(stream_wait(ctx));
   return absorb(ctx, P, true);
 }
@@ -388,12 +412,17 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   ctx->tail_a_valid = false;
   const double* bxc = begin && !P->begin_prop ? P->begin_xc : nullptr;
   const PropArg* bprop = begin && P->begin_prop ? &P->prop : nullptr;
+  // a pending LM is resolved before this IEKF is enqueued unless the IEKF
+  // stream waits for the margi on device flags (the numbers the real tail
+  // stores as well) and starts from the device's state
+  if (!(split && ctx->flag_sync && ctx->sync_tail_armed && bprop)) VG_TRY(resolve_lm(ctx, P));
   if (!split) return iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, bxc, nullptr, bprop);
   // created on first use: a context of the multi-sequence mode never makes
   // it (vg_multi_create), as a third stream per sequence makes sequences
   // share hardware queues (B = 4: 2,742 -> 1,430 scans/s)
   if (!ctx->stream_iekf) VG_HIP(hipStreamCreateWithFlags(&ctx->stream_iekf, hipStreamNonBlocking));
   const bool flags = ctx->flag_sync && ctx->sync_tail_armed;  // state.hip k_sync_*: no late-released event waits
+  // (flag_sync is off when kernels run serialised: vg_create, VG_SERIAL_KERNELS)
   ctx->sync_tail_armed = false;
   bool opened = false;
   if (flags && bprop) {
@@ -417,6 +446,9 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   if (flags) {
     const unsigned v = ++ctx->sync_iekf_value;
     if (!signalled) VG_TRY(sync_set(ctx, ctx->stream_iekf, 1, v));
+    // the previous LM's further iterations and real margi tail, if any, go
+    // onto the main stream ahead of its wait for this IEKF
+    VG_TRY(resolve_lm(ctx, P));
     VG_TRY(sync_wait(ctx, ctx->stream, 1, v));
   } else {
     VG_HIP(hipEventRecord(ctx->ev_iekf_done, ctx->stream_iekf));
@@ -462,7 +494,9 @@ int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double en
   // device propagation (k_scan_prop): from the device's x_curr, so the host
   // does not wait for the previous scan's state here (the window push absorbs
   // it, behind the IEKF's enqueue); the first scan has nothing to propagate
-  P->begin_prop = dev && ctx->dev_prop && !P->first && m <= kPropMax && P->sticky == VG_OK;
+  // A pending LM (the previous fused step returned before its outcome):
+  // only the device has that scan's state, so it propagates there
+  P->begin_prop = dev && (ctx->dev_prop || P->lmp.active) && !P->first && m <= kPropMax && P->sticky == VG_OK;
   if (P->begin_prop) {
     PropArg& a = P->prop;
     const vg_config& c = ctx->cfg;
@@ -786,6 +820,7 @@ int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows) {
     ctx->err = "vg_ba: window not full";
     return VG_E_STATE;
   }
+  VG_TRY(resolve_lm(ctx, P));  // (resolved by the IEKF's enqueue already)
   int iters = 0;
   prof_begin(ctx, kProfBA);
   // margi's BA-independent part goes onto the second stream once the first LM
@@ -816,8 +851,27 @@ int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows) {
     return VG_OK;
   };
   bool tail_ok = false;
-  VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), &iters, prefix, spec_ok ? spec : std::function<int(bool*)>(), &tail_ok));
+  // The outcome may stay pending (ba_run returns once the speculative tail is
+  // queued): the next fused step enqueues its downsample, device propagation
+  // and IEKF first — all behind the margi on device flags — and reads it then
+  // (resolve_lm). Needs the flag hand-offs and the IEKF stream.
+  const bool defer = spec_ok && ctx->lm_defer && ctx->flag_sync && !ctx->serial_kernels && ctx->overlap_iekf &&
+                     ctx->want_ds_stream;
+  bool pending = false;
+  VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), &iters, prefix, spec_ok ? spec : std::function<int(bool*)>(), &tail_ok,
+                defer ? &pending : nullptr));
   P->tail_queued = tail_ok;
+  if (pending) {
+    P->lmp.active = true;
+    P->lmp.seq1 = P->tail_seq1;
+    P->lmp.seq2 = P->tail_seq2;
+    P->lmp.wa = P->tail_wa;
+    P->rc_seq = 0;
+    prof_end(ctx, kProfBA);
+    P->cur.st.ba_iters = 0;  // absorb_p1 takes the device's count
+    if (iters_out) *iters_out = -1;
+    return VG_OK;
+  }
   if (rc_status) {  // complete the recut on the host (stream order), then the LM again
     P->rc_seq = 0;
     int nf = 0;
@@ -844,6 +898,7 @@ int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows) {
 static int margi_enqueue(vg_ctx* ctx, HostPipe* P, const int* gate, int* seq1, int* seq2) {
   const vg_config& c = ctx->cfg;
   const WinArg wa = make_winarg(P, 1);
+  P->tail_wa = wa;
   *seq1 = ++ctx->pub_seq;
   *seq2 = ++ctx->pub_seq;
   if (!P->prefix) {

@@ -48,10 +48,6 @@ __global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict
     st->xc[t] = xa.x[t];
     st->xp[t] = xa.x[t];
   }
-  {
-    for (int t = tid; t < 3 * 32; t += blockDim.x)  // k_iekf_all's pose slots start empty
-      reinterpret_cast<unsigned long long*>(&st->islot[0][0])[t] = kSlotEmpty;
-  }
   if (tid == 0) {
     st->it = 0;
     st->rematch = 0;
@@ -290,8 +286,6 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
   if (tid < 225) st->xc[kXS + tid] = C[tid];
   __syncthreads();
   for (int t = tid; t < kXC; t += blockDim.x) st->xp[t] = st->xc[t];
-  for (int t = tid; t < 3 * 32; t += blockDim.x)  // k_iekf_all's pose slots start empty
-    reinterpret_cast<unsigned long long*>(&st->islot[0][0])[t] = kSlotEmpty;
   if (set_scan && tid == 64) {
     st->sx = x;
     st->sy = y;
@@ -360,11 +354,6 @@ int sync_wait(vg_ctx* ctx, hipStream_t s, int k, unsigned target) {
 }
 
 __global__ void k_set_scan(DState* __restrict__ st, const float* x, const float* y, const float* z, int n) {
-  {
-    const int tid = threadIdx.x;
-    for (int t = tid; t < 3 * 32; t += blockDim.x)  // k_iekf_all's pose slots start empty
-      reinterpret_cast<unsigned long long*>(&st->islot[0][0])[t] = kSlotEmpty;
-  }
   if (threadIdx.x == 0) {
     st->sx = x;
     st->sy = y;

@@ -400,6 +400,11 @@ __device__ __forceinline__ void pub_store(double* dst, double v) {
 __device__ __forceinline__ void pub_store(int* dst, int v) {
   __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// (gfx9 counts stores in vmcnt; gfx10+ counts them in vscnt, where this wait
+// would not order the payload before the flag)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "pub_drain orders stores with vmcnt: gfx9 (gfx950) only"
+#endif
 __device__ __forceinline__ void pub_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void pub_flag(int* dst, int v) {
   pub_drain();  // this wave's own payload stores

@@ -170,6 +170,15 @@ struct HostPipe {
   bool prefix = false;     // map_margi_prefix enqueued for this scan
   bool tail_queued = false;  // the margi tail went in behind the LM and its gate opened (ba_run)
   int tail_seq1 = 0, tail_seq2 = 0;  // that tail's publication numbers
+  WinArg tail_wa;                    // and its window view (before the host's slide)
+  // the previous fused step's LM, not resolved yet (stage_ba, ctx->ba_loop):
+  // if its speculative tail turns out not to run, the real one is enqueued
+  // with the same publication numbers and window view (resolve_lm)
+  struct LmPend {
+    bool active = false;
+    int seq1 = 0, seq2 = 0;
+    WinArg wa;
+  } lmp;
   int rc_seq = 0;          // > 0: this scan's recut ran asynchronously (status with Pub::seq_rc == rc_seq)
   std::deque<Pend> pend;   // enqueued scans awaiting absorption (oldest first)
   int sticky = VG_OK;      // deferred device error

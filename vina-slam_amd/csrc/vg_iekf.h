@@ -16,7 +16,6 @@
 namespace vg {
 
 constexpr int kIekfVals = 34;  // HTH upper 21, HTz 6, nnt upper 6, match count
-constexpr int kIekfAllMax = 480;  // k_iekf_all point workgroups (see iekf_run: co-residency per XCD)
 
 // LDS of iekf_update_block
 constexpr int kIekfGroups = 60;  // row groups of the partial sums (1024-lane update: 60 x 17 lanes)
@@ -87,113 +86,10 @@ __device__ __forceinline__ double bcast_lane(double v, int ln) {
   return __longlong_as_double(((long long)hi32 << 32) | (unsigned int)lo32);
 }
 
-// Empty partial slot of the fused update (k_iekf's update workgroup): a NaN
-// payload with equal 32-bit halves (hipMemsetD32 arms a buffer), never an
-// arithmetic result
-constexpr unsigned kSlotEmpty32 = 0x7ff5a5a5u;
-constexpr unsigned long long kSlotEmpty = ((unsigned long long)kSlotEmpty32 << 32) | kSlotEmpty32;
-__device__ __forceinline__ void slot_put(double* slot, double v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(slot), (unsigned long long)__double_as_longlong(v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// take a slot's value once it is stored (relaxed agent-scope loads, no fence),
-// and re-arm it; *late is set if it never arrives (bounded wait)
-__device__ __forceinline__ double slot_take(double* slot, int* late) {
-  unsigned long long* p = reinterpret_cast<unsigned long long*>(slot);
-  unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int spin = 0; v == kSlotEmpty; spin++) {
-    if (spin > (1 << 22)) {
-      *late = 1;
-      v = 0ull;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-    v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __hip_atomic_store(p, kSlotEmpty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return __longlong_as_double((long long)v);
-}
-// wait for a slot several readers share (not re-armed: the scan opening does)
-__device__ __forceinline__ double slot_wait(const double* slot, int* late) {
-  const unsigned long long* p = reinterpret_cast<const unsigned long long*>(slot);
-  unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int spin = 0; v == kSlotEmpty; spin++) {
-    if (spin > (1 << 22)) {
-      *late = 1;
-      v = 0ull;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-    v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  return __longlong_as_double((long long)v);
-}
-// iekf_reduce_block's order on slots the point-loop workgroups of the same
-// launch are still filling: row group g = tid / 17 sums rows g, g + G, ...
-// (lane pair 2 (tid % 17)), then the G groups in order. Eight rows' loads are
-// issued before any is waited for.
 // The point loop's chunk of workgroup b (XCD-aware: consecutive chunks on one
-// XCD) and whether it holds points: a workgroup without points stores no
-// partial in the fused form, and the reduction skips its row (an exact no-op:
-// its sums are +0)
+// XCD); the reduction skips the rows of chunks without points (an exact no-op:
+// their sums are +0)
 __device__ __forceinline__ int iekf_chunk(int b, int nb) { return (nb % 8 == 0) ? (b % 8) * (nb / 8) + b / 8 : b; }
-__device__ __forceinline__ void iekf_reduce_spin(int nb, int nact, double* partials, IekfLds& L, int* late) {
-  const int tid = threadIdx.x;
-  const int G = (int)blockDim.x / 17 < kIekfGroups ? (int)blockDim.x / 17 : kIekfGroups;
-  const int g = tid / 17, j2 = 2 * (tid % 17);
-  if (g < G && nact < nb) {  // a partly empty grid: the active rows one by one
-    double a0 = 0.0, a1 = 0.0;
-    for (int b = g; b < nb; b += G)
-      if (iekf_chunk(b, nb) < nact) {
-        a0 += slot_take(&partials[(size_t)b * kIekfVals + j2], late);
-        a1 += slot_take(&partials[(size_t)b * kIekfVals + j2 + 1], late);
-      }
-    L.red[g][j2] = a0;
-    L.red[g][j2 + 1] = a1;
-  } else if (g < G) {
-    double a0 = 0.0, a1 = 0.0;
-    int b = g;
-    for (; b + 7 * G < nb; b += 8 * G) {
-      unsigned long long v[16];
-#pragma unroll
-      for (int r = 0; r < 8; r++)
-#pragma unroll
-        for (int h = 0; h < 2; h++)
-          v[2 * r + h] = __hip_atomic_load(reinterpret_cast<unsigned long long*>(&partials[(size_t)(b + r * G) * kIekfVals + j2 + h]),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-      for (int r = 0; r < 8; r++) {
-        double x[2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          double* sl = &partials[(size_t)(b + r * G) * kIekfVals + j2 + h];
-          if (v[2 * r + h] == kSlotEmpty) {
-            x[h] = slot_take(sl, late);
-          } else {
-            x[h] = __longlong_as_double((long long)v[2 * r + h]);
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(sl), kSlotEmpty, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-        a0 += x[0];
-        a1 += x[1];
-      }
-    }
-    for (; b < nb; b += G) {
-      a0 += slot_take(&partials[(size_t)b * kIekfVals + j2], late);
-      a1 += slot_take(&partials[(size_t)b * kIekfVals + j2 + 1], late);
-    }
-    L.red[g][j2] = a0;
-    L.red[g][j2 + 1] = a1;
-  }
-  __syncthreads();
-  if (tid < kIekfVals) {
-    double s = L.red[0][tid];
-    for (int k = 1; k < G; k++) s += L.red[k][tid];
-    L.o[tid] = s;
-  }
-  __syncthreads();
-}
 
 __device__ __forceinline__ void iekf_update_tail(DState* __restrict__ st, int it, IekfLds& L, bool vec_done = false);
 // vec = x_prop ⊟ x_curr (IMUST::operator-, types.hpp:80-86), one thread

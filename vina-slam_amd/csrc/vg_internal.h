@@ -196,8 +196,6 @@ struct Work {
   void* tmp2 = nullptr;        // sort workspace of the second stream
   size_t tmp_bytes = 0;
   double* partials = nullptr;  // reduction partials
-  double* islots = nullptr;    // k_iekf_all's partial slots: 4 iterations x kIekfAllMax workgroups x 34
-  bool islots_armed = false;
   int* iekf_cache = nullptr;   // per raw point cached leaf
   int* pk_leaf = nullptr;      // per raw point leaf read by the profiled IEKF iteration (P_k count)
   int* rc = nullptr;           // device-side level counts (recut / margi, map.hip kRc*)
@@ -272,10 +270,6 @@ struct DState {
   int imu_head, margi_seq, pad_h[2];  // margi_seq: the last margi head's publication number (k_margi_copy signals it)
   double imurec[kMaxWin * kBaImuRec];
   KClock clk;
-  // k_iekf_all: the pose each IEKF iteration 1-3 starts from (R 9, p 3, rot / tsl
-  // covariance blocks 9 + 9, finished flag), stored by its update workgroup, empty
-  // (kSlotEmpty) from the scan opening on
-  double islot[3][32];
 };
 // x_buf.push_back(x_curr) + a new IMU_PRE record, as kernel arguments (k_push_state,
 // or folded into the insert's first launch, map_insert)
@@ -331,6 +325,14 @@ struct Pub {
   double nnt[8];
   double xs[kMaxWin * kXS];
 };
+// An LM run whose outcome the host has not read yet (ba_run's loop state,
+// continued by ba_resolve): the fused step returns once the LM iterations and
+// the speculative margi tail are enqueued, and the next step enqueues its
+// downsample, propagation and IEKF before it waits for that outcome
+struct BaLoop {
+  int seq0 = 0, enq = 0, tail_at = 0, k = 0;  // first iteration flag number, iterations enqueued, ahead of the tail, next k
+  bool active = false;
+};
 // window view for the map kernels, built on the device from DState::xs
 struct WinArg {
   int mp[kMaxWin];      // mp[] ring (octree.cpp:75)
@@ -367,7 +369,7 @@ struct vg_ctx {
   bool tail_a_valid = false;  // ev_tail_a marks the latest main-stream work the next IEKF depends on
   hipEvent_t ev_scan_ready = nullptr;  // deskew done (row f1)
   // the IEKF's 8 launches captured once and replayed (map.hip iekf_run)
-  hipGraphExec_t g_iekf[4] = {nullptr, nullptr, nullptr, nullptr};  // [0] per-iteration launches, [1] k_iekf_all, [2] k_iekf_all signalling, [3] [0] signalling
+  hipGraphExec_t g_iekf[4] = {nullptr, nullptr, nullptr, nullptr};  // [0] the four iterations, [3] the same, signalling the insert ([1], [2] unused)
   hipGraphExec_t g_margi[4] = {};  // margi after the window view (map.hip map_margi): [gated + 2 * signalling]
   hipGraphExec_t g_ba = nullptr;     // one LM iteration (ba.hip ba_run)
   hipGraphExec_t g_ba2 = nullptr;    // the first two LM iterations
@@ -377,6 +379,11 @@ struct vg_ctx {
   bool capturing = false;  // a stream capture is open (host-side steps that cannot be captured are deferred)
   int rc_pub = 0;          // asynchronous recuts enqueued (mirrors DState::rc_ctr, k_fac_sort)
   int ba_last_iters = 2;   // LM iterations of the previous run (ba_run's enqueue-ahead policy)
+  vg::BaLoop ba_loop;      // a deferred LM run (ba_run / ba_resolve)
+  bool lm_defer = true;    // the fused step returns before the LM outcome (vgx_debug 26: 0 = waits for it)
+  // kernels do not run concurrently (AMD_SERIALIZE_KERNEL, or VG_SERIAL_KERNELS=1 as rocprofv3 --pmc
+  // runs set): no device-flag hand-offs (a polling kernel would wait for a producer queued behind it)
+  bool serial_kernels = false;
   vg::HostIn* h_in = nullptr;  // host-mapped per-scan inputs of replayed graphs (host address)
   vg::HostIn* d_in = nullptr;  // its device address
   bool pool_zeroed = false;
@@ -436,16 +443,10 @@ struct vg_ctx {
   bool prof_stages = false;  // per-stage events (vg_profile bit 1)
   bool roots_lb = true;      // root registration in one look-back launch (vgx_debug 16: 0 = two launches)
   bool ba_graph2 = true;     // the first two LM iterations as one graph (vgx_debug 17: 0 = one graph each)
-  bool ba_dataflow = false;   // vgx_debug 25: k_ba_solve without a workgroup barrier per phase (flags in LDS)
   bool margi_batch = true;    // vgx_debug 24: k_margi_leaf reads a leaf's frame clusters four at a time (r04k +0.4 %)
   bool margi_fused = true;    // margi isexist bottom-up in k_margi_copy, erase in one launch (vgx_debug 21: 0 = per-level launches)
   bool iekf_prefetch = true;  // vgx_debug 23: k_iekf touches a cached match's plane record beside its header (r04i A/B +0.9 %)
-  int iekf_all_cap = 0;       // k_iekf_all: workgroups resident at once (0: not yet asked, -1: too few)
-  bool iekf_persist = false;  // vgx_debug 22 (with 20): the four IEKF iterations as one launch, k_iekf_all (r04e A/B: slower)
-  bool iekf_fused = false;    // vgx_debug 20: the IEKF update as k_iekf's last workgroup (r04e A/B: -23 %)
-  bool iekf_armed = false;    // wk.partials holds empty slots (kSlotEmpty)
   bool ba_fuse_ctl = true;    // vgx_debug 19: the LM bookkeeping in k_ba_resid's IMU workgroup (A/Bs r04e 0, r04g/h +0.8-0.9 %)
-  bool ba_fuse_final = false; // vgx_debug 18: k_ba_prep sums k_ba_hess's chunk partials itself (r04e A/B: -6 %)
   bool ba_graph = true;      // LM iterations replay one captured graph each (vgx_debug 15: 0 = direct launches)
   bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)
   unsigned* d_sync = nullptr;  // hand-off flags: [0] margi leaf -> next IEKF, [1] IEKF -> insert, [2] margi head -> propagation
@@ -686,9 +687,17 @@ int ba_alloc(vg_ctx* ctx);
 // decline through its flag): the margi tail, enqueued right behind the
 // iteration count the previous run converged at and gated on the device by
 // ba_gate_dev; *tail_ok tells whether that copy is the one that runs
+// pending != nullptr: the run may return once the speculative tail is queued
+// (*pending = true, *iters = -1); ba_resolve then continues it
 int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
            const std::function<int()>& before_first_wait = nullptr,
-           const std::function<int(bool*)>& spec_tail = nullptr, bool* tail_ok = nullptr);
+           const std::function<int(bool*)>& spec_tail = nullptr, bool* tail_ok = nullptr, bool* pending = nullptr);
+// the rest of a deferred run (ctx->ba_loop): waits for the iteration flags and
+// enqueues further iterations as ba_run would have. block = false: returns
+// with *finished = false as soon as a flag it needs is not published yet.
+// *tail_ok: the speculative tail is the copy that runs (else the caller
+// enqueues the real one)
+int ba_resolve(vg_ctx* ctx, bool block, bool* finished, int* iters, bool* tail_ok);
 const int* ba_iters_dev(vg_ctx* ctx);
 const int* ba_gate_dev(vg_ctx* ctx);  // 1 once the LM run has finished (converged or 10 iterations)
 const int* ba_hess_dev(vg_ctx* ctx);  // Hessian passes of the last LM run (I_H of SURVEY 8(d))

@@ -122,6 +122,18 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
   fill_capacity(ctx->cap);
   ctx->device = device;
   memset(&ctx->stats, 0, sizeof(ctx->stats));
+  // Kernels serialised (AMD_SERIALIZE_KERNEL, or a counter-collection run:
+  // rocprofv3 --pmc dispatches one kernel at a time; VG_SERIAL_KERNELS=1 says
+  // so): a polling hand-off kernel would wait for a producer queued behind it,
+  // so the context uses event waits and waits for each LM's outcome in its step
+  {
+    const char* a = getenv("AMD_SERIALIZE_KERNEL");
+    const char* v = getenv("VG_SERIAL_KERNELS");
+    if ((a && atoi(a) != 0) || (v && atoi(v) != 0)) {
+      ctx->serial_kernels = true;
+      ctx->flag_sync = false;
+    }
+  }
   auto fail = [&](int code) {
     fprintf(stderr, "vg_create: %s\n", ctx->err.c_str());
     vg_destroy(ctx);
@@ -236,7 +248,12 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
 
 int vg_destroy(vg_ctx* ctx) {
   if (!ctx) return VG_OK;
+  // a pending LM (vg_step returned before its outcome) needs nothing more:
+  // its speculative tail either ran or ran as no-ops, and nothing waits on it
+  ctx->ba_loop.active = false;
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream_ds && ctx->stream_ds != ctx->stream) (void)hipStreamSynchronize(ctx->stream_ds);
+  if (ctx->stream_iekf) (void)hipStreamSynchronize(ctx->stream_iekf);
   if (ctx->arena.base) (void)hipFree(ctx->arena.base);
   if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
   if (ctx->dbg_cap_buf) (void)hipFree(ctx->dbg_cap_buf);
@@ -296,6 +313,8 @@ int vg_reset(vg_ctx* ctx) {
   if (!ctx) return VG_E_ARG;
   VG_HIP(hipStreamSynchronize(ctx->stream_ds));
   VG_HIP(hipStreamSynchronize(ctx->stream));
+  if (ctx->stream_iekf) VG_HIP(hipStreamSynchronize(ctx->stream_iekf));
+  ctx->ba_loop.active = false;  // the HostPipe's record of it goes with host_reset
   VG_TRY(map_reset(ctx));
   VG_TRY(kd_reset(ctx));
   host_reset(ctx);
@@ -811,10 +830,6 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     VG_HIP(hipMemcpy(ctx->shard.d_seq, &s, sizeof(s), hipMemcpyHostToDevice));
     return VG_OK;
   }
-  if (key == 25) {  // 1: the LM solve's phases meet at LDS flags, not workgroup barriers
-    ctx->ba_dataflow = value != 0;
-    return VG_OK;
-  }
   if (key == 24) {  // 1: k_margi_leaf batches a leaf's frame-cluster loads
     ctx->margi_batch = value != 0;
     return VG_OK;
@@ -823,24 +838,12 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     ctx->iekf_prefetch = value != 0;
     return VG_OK;
   }
-  if (key == 22) {  // 0: the IEKF iterations as one launch each (k_iekf)
-    ctx->iekf_persist = value != 0;
-    return VG_OK;
-  }
   if (key == 21) {  // 0: margi's isexist / erase passes as per-level launches
     ctx->margi_fused = value != 0;
     return VG_OK;
   }
-  if (key == 20) {  // 0: the IEKF update as its own k_iekf_update launch
-    ctx->iekf_fused = value != 0;
-    return VG_OK;
-  }
   if (key == 19) {  // 0: the LM bookkeeping as its own k_ba_control launch
     ctx->ba_fuse_ctl = value != 0;
-    return VG_OK;
-  }
-  if (key == 18) {  // 0: the chunk partials summed by a k_ba_hfinal launch (not inside k_ba_prep)
-    ctx->ba_fuse_final = value != 0;
     return VG_OK;
   }
   if (key == 17) {  // 0: one graph per LM iteration (no two-iteration graph)
@@ -859,7 +862,11 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     ctx->flag_sync = value != 0;
     return VG_OK;
   }
-  if (key == 13) {  // 0: host_step propagates on the host (waits for the previous scan's state)
+  if (key == 26) {  // 0: a fused step waits for its LM's outcome (no deferral to the next step)
+    ctx->lm_defer = value != 0;
+    return VG_OK;
+  }
+  if (key == 13) {  // 1: host_step always propagates on the device (0: only while an LM is pending)
     ctx->dev_prop = value != 0;
     return VG_OK;
   }
