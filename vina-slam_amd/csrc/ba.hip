@@ -42,8 +42,9 @@ struct BaState {             // device-resident LM state
   int calc_hess, done, iters, seq;  // seq: the next LM publication number (k_ba_control)
   int nhess;                        // Hessian passes executed (I_H, SURVEY 8(d) byte model)
   int fin;                          // the run has finished (converged or 10 iterations): the margi tail's gate
+  int skip, pad_[3];                // the recut needs the host (k_ba_init): the run is skipped, the gate stays shut
 };
-static_assert(sizeof(BaState) <= 8 * sizeof(double), "BaState is carved as 8 doubles");
+static_assert(sizeof(BaState) <= 16 * sizeof(double), "BaState is carved as 16 doubles");
 
 typedef double v4d __attribute__((ext_vector_type(4)));
 
@@ -980,7 +981,7 @@ __device__ __forceinline__ void ba_control_body(const CtlArg& c, const double* p
     }
   }
   if (threadIdx.x == 0) {  // LM flags -> host (read without draining the stream)
-    c.st->fin = (c.st->done || c.st->iters >= 10) ? 1 : 0;
+    c.st->fin = ((c.st->done || c.st->iters >= 10) && !c.st->skip) ? 1 : 0;
     const int seq = c.st->seq;  // one publication per launch, numbered on the device (graph replays)
     c.st->seq = seq + 1;
     pub_store(&c.pub->ba_done, c.st->done);
@@ -1112,11 +1113,15 @@ __global__ void k_ba_rsum(int nrb, const double* __restrict__ rpart, double* __r
 struct MpRing {
   int mp[kMaxW];
 };
-// LM state (optimizers.cpp:436-441), the reduced-Hessian accumulator, the ring
+// LM state (optimizers.cpp:436-441), the reduced-Hessian accumulator, the ring.
+// ph (the scan graph, pipeline.cpp): the per-scan numbers k_ins_prep copied
+// from host-mapped memory into DState::ph — the LM's first flag number
+// replaces seq0, and the recut-done flag the margi prefix waits for
+// (vg_ctx::d_sync[3]) is raised here (the recut's kernels have ended)
 __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict__ hl, double* __restrict__ hl_part,
                                                  int nout, MpRing ring, int* __restrict__ mpring, int W,
                                                  const int* __restrict__ rc_status, int seq0, double* __restrict__ rpart,
-                                                 int nrb) {
+                                                 int nrb, const int* __restrict__ ph, unsigned* __restrict__ rc_flag) {
   for (int b = threadIdx.x; b < nrb; b += blockDim.x)  // empty residual slots (resid_bookkeeping)
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(rpart + b), kRpartEmpty, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -1126,15 +1131,18 @@ __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict
   }
   if ((int)threadIdx.x < W) mpring[threadIdx.x] = ring.mp[threadIdx.x];
   if (threadIdx.x == 0) {
+    const int skip = (rc_status && *rc_status) ? 1 : 0;  // an asynchronous recut that needs the host: skip
     st->u = 0.01;
     st->v = 2;
     st->res1 = st->res2 = st->q1 = 0.0;
     st->calc_hess = 1;
-    st->done = (rc_status && *rc_status) ? 1 : 0;  // an asynchronous recut that needs the host: skip
+    st->done = skip;
+    st->skip = skip;
     st->iters = 0;
     st->nhess = 0;
-    st->seq = seq0;
+    st->seq = ph ? ph[0] : seq0;
     st->fin = 0;
+    if (ph) __hip_atomic_store(rc_flag, (unsigned)ph[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1254,7 +1262,7 @@ static BaDev carve(vg_ctx* ctx) {
   d.imures = p;
   p += kMaxW;
   d.st = (BaState*)p;
-  p += 8;
+  p += 16;
   d.mpring = (int*)p;
   p += 16;
   d.part = b.hpart;
@@ -1267,11 +1275,96 @@ const int* ba_iters_dev(vg_ctx* ctx) { return &carve(ctx).st->iters; }
 const int* ba_hess_dev(vg_ctx* ctx) { return &carve(ctx).st->nhess; }
 const int* ba_gate_dev(vg_ctx* ctx) { return &carve(ctx).st->fin; }
 
+// one LM iteration (optimizers.cpp:449-516); kernels early-exit on the
+// device-side flags once converged. Every argument is fixed per context (the
+// factor count, the flags and the publication number live on the device), so
+// an unsharded run replays one captured graph per iteration; the sampled
+// solve-timing runs launch directly (events around k_ba_solve).
+static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr) {
+  const int W = ctx->cfg.win_size;
+  hipStream_t s = ctx->stream;
+  BaDev d = carve(ctx);
+  const int nimu = W - 1;
+  const int L = 6 * W, nl = L * (L + 1) / 2, nout = nl + L + 1;
+  const bool sharded = ctx->shard.world > 1;
+  double* hl_part = ctx->ba.hout_part;  // this shard's LiDAR Hessian (sharded mode)
+  double* rsum = ctx->shard.d_buf + 256;  // [0]: this shard's residual, [1]: all-reduced
+  // factor count on the device (the recut's kCntFactors): fixed grids, so an
+  // asynchronous recut needs no host round trip before the LM
+  const int* nfp = ctx->map.counters + kCntFactors;
+  const int G = std::min(kHessGridMax, ctx->ba.cap_f / hess_chunk(W) + 1);
+  const int nrb = kResidBlocks;
+  const size_t hess_lds = hess_lds_bytes(W);
+  const size_t solve_lds = solve_lds_bytes(W);
+  const int NBt = (15 * W - 15 + kTile - 1) / kTile, ntile = NBt * (NBt + 1) / 2;
+  CtlArg ctl{W, nimu, sharded ? 1 : nrb, nl + L, ctx->cfg.imu_coef, d.hl, d.imuout, d.imures,
+             sharded ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st, ctx->d_pub, nullptr};
+  CtlArg ctl_fused = ctl;  // unsharded: the bookkeeping rides in k_ba_resid's IMU workgroup
+  if (!sharded && ctx->ba_fuse_ctl) ctl_fused.err = ctx->map.counters + kCntErr;
+  k_ba_hess<<<G + nimu, kHessThreads, hess_lds, s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
+                                                    ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, nimu, d.imurec, &ctx->st->imu_head,
+                                                    d.bias, d.imuout);
+  k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, sharded ? hl_part : d.hl,
+                                                       d.st);
+  // sharded: every shard's factors -> one LiDAR Hessian / gradient / residual
+  // (out of place: a rejected step re-reduces the unchanged partial)
+  if (sharded && xerr == VG_OK) xerr = shard_allreduce(ctx, hl_part, d.hl, nout, 0, 3);
+  if (k == 0 && ctx->dbg_capture == 1 && ctx->dbg_cap_buf) {  // test knob (vgx_debug 5): the first pass
+    (void)hipMemcpyAsync(ctx->dbg_cap_buf, d.hl, nout * sizeof(double), hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(ctx->dbg_cap_buf + nout, d.imuout, (size_t)nimu * 931 * sizeof(double),
+                         hipMemcpyDeviceToDevice, s);
+    ctx->dbg_cap_n = nout + nimu * 931;
+    ctx->dbg_capture = 2;
+  }
+  k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
+                                  d.dvec, d.jvec, d.ipg, d.st);
+  if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][0], s);
+  k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
+                                       d.st, &ctx->st->clk);
+  if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][1], s);
+  k_ba_resid<<<nrb + 1, 256, 0, s>>>(nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
+                                     ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, nimu, d.imurec, &ctx->st->imu_head, d.bias,
+                                     d.imures, ctl_fused);
+  if (sharded) {  // the residual over every shard's factors
+    k_ba_rsum<<<1, 64, 0, s>>>(nrb, d.rpart, rsum, d.st);
+    if (xerr == VG_OK) xerr = shard_allreduce(ctx, rsum, rsum + 1, 1, 0, 4);
+  }
+  if (!ctl_fused.err) k_ba_control<<<1, 256, 0, s>>>(ctl);
+}
+
+// k_ba_init: seq0 > 0 the LM's first flag number, else (the scan graph) read
+// on the device from DState::ph
+static void ba_init_kernel(vg_ctx* ctx, const int* mp_ring, int seq0) {
+  const int W = ctx->cfg.win_size;
+  BaDev d = carve(ctx);
+  const int L = 6 * W, nout = L * (L + 1) / 2 + L + 1;
+  // the IMU records are in DState's ring (k_push_state), the mp ring rides in k_ba_init's arguments
+  MpRing ring;
+  for (int i = 0; i < kMaxW; i++) ring.mp[i] = i < W ? mp_ring[i] : 0;
+  k_ba_init<<<1, 256, 0, ctx->stream>>>(d.st, d.hl, ctx->ba.hout_part, nout, ring, d.mpring, W, map_rc_status(ctx),
+                                        seq0, d.rpart, kResidBlocks, seq0 > 0 ? nullptr : ctx->st->ph, ctx->d_sync + 3);
+}
+
+// the scan graph's LM part (pipeline.cpp stage_insert_recut), captured on the
+// context stream: k_ba_init reading its per-scan numbers from the device,
+// then the first two iterations
+int ba_capture_scan_lm(vg_ctx* ctx, const int* mp_ring) {
+  ba_init_kernel(ctx, mp_ring, 0);
+  int xerr = VG_OK;
+  ba_iter_kernels(ctx, 0, false, xerr);
+  ba_iter_kernels(ctx, 1, false, xerr);
+  VG_HIP(hipGetLastError());
+  return xerr;
+}
+
 // Run damping_iter on the device state. imurec: (W-1) x kImuRec host records
 // (pinned staging, uploaded asynchronously). The window states and the IMU
 // bias records are read and written in DState.
+// pre > 0: k_ba_init, the first `pre` iterations and the gated margi tail are
+// already on the stream (the scan graph), with the flag numbers from
+// ctx->ba_seq0_pre
 int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::function<int()>& before_first_wait,
-           const std::function<int(bool*)>& spec_tail, bool* tail_ok, bool* pending) {
+           const std::function<int(bool*)>& spec_tail, bool* tail_ok, bool* pending, int pre) {
   if (pending) *pending = false;
   const int W = ctx->cfg.win_size;
   if (15 * W > kMaxNB * kTile) {
@@ -1279,72 +1372,23 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
     return VG_E_ARG;
   }
   hipStream_t s = ctx->stream;
-  BaDev d = carve(ctx);
-  const int nimu = W - 1;
-  const int L = 6 * W, nl = L * (L + 1) / 2, nout = nl + L + 1;
-  // the IMU records are in DState's ring (k_push_state), the mp ring rides in k_ba_init's arguments
-  MpRing ring;
-  for (int i = 0; i < kMaxW; i++) ring.mp[i] = i < W ? mp_ring[i] : 0;
-  const bool sharded = ctx->shard.world > 1;
-  double* hl_part = ctx->ba.hout_part;  // this shard's LiDAR Hessian (sharded mode)
-  double* rsum = ctx->shard.d_buf + 256;  // [0]: this shard's residual, [1]: all-reduced
-  const int seq0 = ctx->pub_seq + 1;
-  ctx->pub_seq += 10;
-  k_ba_init<<<1, 256, 0, s>>>(d.st, d.hl, hl_part, nout, ring, d.mpring, W, map_rc_status(ctx), seq0, d.rpart, kResidBlocks);
-  VG_HIP(flush_insert_events(ctx));
-  // factor count on the device (the recut's kCntFactors): fixed grids, so an
-  // asynchronous recut needs no host round trip before the LM
   (void)nf;
-  const int* nfp = ctx->map.counters + kCntFactors;
-  const int G = std::min(kHessGridMax, ctx->ba.cap_f / hess_chunk(W) + 1);
-  const int nrb = kResidBlocks;
-  const size_t hess_lds = hess_lds_bytes(W);
-  const size_t solve_lds = solve_lds_bytes(W);
-  const int NBt = (15 * W - 15 + kTile - 1) / kTile, ntile = NBt * (NBt + 1) / 2;
+  const bool sharded = ctx->shard.world > 1;
+  int seq0;
+  if (pre > 0) {
+    seq0 = ctx->ba_seq0_pre;
+  } else {
+    seq0 = ctx->pub_seq + 1;
+    ctx->pub_seq += 10;
+    ba_init_kernel(ctx, mp_ring, seq0);
+    VG_HIP(flush_insert_events(ctx));
+  }
   int xerr = VG_OK;  // exchange errors (sharded mode)
   // k_ba_solve launch events (vg_profile): on every prof_every-th run only, so
   // that timing a long run costs the stream little (each record is a gap)
-  const bool solve_ev = ctx->prof_on && !ctx->prof_clock && (ctx->prof_every <= 1 || ctx->prof_runs++ % ctx->prof_every == 0);
-  // one LM iteration (optimizers.cpp:449-516); kernels early-exit on the
-  // device-side flags once converged. Every argument is fixed per context (the
-  // factor count, the flags and the publication number live on the device),
-  // so an unsharded run replays one captured graph per iteration; the sampled
-  // solve-timing runs launch directly (events around k_ba_solve).
-  CtlArg ctl{W, nimu, sharded ? 1 : nrb, nl + L, ctx->cfg.imu_coef, d.hl, d.imuout, d.imures,
-             sharded ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st, ctx->d_pub, nullptr};
-  CtlArg ctl_fused = ctl;  // unsharded: the bookkeeping rides in k_ba_resid's IMU workgroup
-  if (!sharded && ctx->ba_fuse_ctl) ctl_fused.err = ctx->map.counters + kCntErr;
-  auto enqueue = [&](int k) {
-    k_ba_hess<<<G + nimu, kHessThreads, hess_lds, s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
-                                                      ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, nimu, d.imurec, &ctx->st->imu_head,
-                                                      d.bias, d.imuout);
-    k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, sharded ? hl_part : d.hl,
-                                                         d.st);
-    // sharded: every shard's factors -> one LiDAR Hessian / gradient / residual
-    // (out of place: a rejected step re-reduces the unchanged partial)
-    if (sharded && xerr == VG_OK) xerr = shard_allreduce(ctx, hl_part, d.hl, nout, 0, 3);
-    if (k == 0 && ctx->dbg_capture == 1 && ctx->dbg_cap_buf) {  // test knob (vgx_debug 5): the first pass
-      (void)hipMemcpyAsync(ctx->dbg_cap_buf, d.hl, nout * sizeof(double), hipMemcpyDeviceToDevice, s);
-      (void)hipMemcpyAsync(ctx->dbg_cap_buf + nout, d.imuout, (size_t)nimu * 931 * sizeof(double),
-                           hipMemcpyDeviceToDevice, s);
-      ctx->dbg_cap_n = nout + nimu * 931;
-      ctx->dbg_capture = 2;
-    }
-    k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
-                                    d.dvec, d.jvec, d.ipg, d.st);
-    if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][0], s);
-    k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
-                                         d.st, &ctx->st->clk);
-    if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][1], s);
-    k_ba_resid<<<nrb + 1, 256, 0, s>>>(nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
-                                       ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, nimu, d.imurec, &ctx->st->imu_head, d.bias,
-                                       d.imures, ctl_fused);
-    if (sharded) {  // the residual over every shard's factors
-      k_ba_rsum<<<1, 64, 0, s>>>(nrb, d.rpart, rsum, d.st);
-      if (xerr == VG_OK) xerr = shard_allreduce(ctx, rsum, rsum + 1, 1, 0, 4);
-    }
-    if (!ctl_fused.err) k_ba_control<<<1, 256, 0, s>>>(ctl);
-  };
+  const bool solve_ev = pre == 0 && ctx->prof_on && !ctx->prof_clock &&
+                        (ctx->prof_every <= 1 || ctx->prof_runs++ % ctx->prof_every == 0);
+  auto enqueue = [&](int k) { ba_iter_kernels(ctx, k, solve_ev, xerr); };
   const bool graph = ctx->use_graphs && ctx->ba_graph && !sharded && !solve_ev && ctx->dbg_capture != 1;
   if (graph && !ctx->g_ba) {
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
@@ -1357,7 +1401,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   }
   // the two iterations of the steady state as ONE graph (no graph boundary
   // between them: each boundary left the stream idle ~9 us)
-  const bool graph2 = graph && ctx->ba_graph2 && ctx->ba_last_iters >= 2;
+  const bool graph2 = pre == 0 && graph && ctx->ba_graph2 && ctx->ba_last_iters >= 2;
   if (graph2 && !ctx->g_ba2) {
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     enqueue(0);
@@ -1389,7 +1433,10 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   // last iteration. So the tail starts as soon as the LM ends instead of one
   // host round trip later.
   int enq = 1, done_iters = 0, tail_at = 0;  // iterations enqueued so far / ahead of the speculative tail
-  if (graph2) {
+  if (pre > 0) {
+    enq = pre;
+    tail_at = pre;
+  } else if (graph2) {
     const hipError_t e = hipGraphLaunch(ctx->g_ba2, s);
     if (e != hipSuccess) {
       ctx->err = std::string("hipGraphLaunch (LM iterations 0-1): ") + hipGetErrorString(e);
@@ -1411,7 +1458,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
     }
     // the outcome is read later (ba_resolve): the tail is queued, every
     // further iteration is a replay of the same graph
-    if (pending && tail_at > 0 && graph) {
+    if (pending && tail_at > 0 && graph && !ctx->ba_no_defer) {
       ctx->ba_loop.seq0 = seq0;
       ctx->ba_loop.enq = enq;
       ctx->ba_loop.tail_at = tail_at;

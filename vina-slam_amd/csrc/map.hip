@@ -584,7 +584,8 @@ __global__ void __launch_bounds__(256) k_ins_prep(int n_arg, const int* __restri
                            const float* __restrict__ oz, const float* __restrict__ oi, MP mp, DState* __restrict__ st, int slot,
                            DevMap m, double* __restrict__ pw, uint32_t* __restrict__ hslot,
                            const PushArg* __restrict__ pa, const double* __restrict__ pin, const double* __restrict__ xsrc,
-                           int var_identity, int* __restrict__ dsf, unsigned long long* __restrict__ gran, int ngran) {
+                           int var_identity, int* __restrict__ dsf, unsigned long long* __restrict__ gran, int ngran,
+                           const int* __restrict__ ph_in) {
   const int n = nd ? *nd : n_arg;  // the downsampled count on the device (ds_enqueue_hashed)
   {  // the root registration's look-back granules (k_ins_roots_lb, the next launch) start empty
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -593,6 +594,8 @@ __global__ void __launch_bounds__(256) k_ins_prep(int n_arg, const int* __restri
   // the window push (local_mapping.cpp:434-441) rides in block 0: it copies
   // x_curr into x_buf[ord], which this kernel only reads
   if (!kPre && pa && blockIdx.x == 0) push_state_block(st, *pa);  // pa: host-mapped (vg_ctx::d_in)
+  // the scan graph's per-scan numbers (HostIn::ph, host-mapped) into the device state, beside the push
+  if (ph_in && blockIdx.x == 0 && threadIdx.x < 6) st->ph[threadIdx.x] = ph_in[threadIdx.x];
   // pose of x_buf[ord] = x_curr after the IEKF (device state)
   const double* xc = kPre ? xsrc : st->xc;
   M3 R, rot_var, tsl_var;
@@ -1513,15 +1516,20 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread
   if (pre)
     k_ins_prep<true><<<g, kBlock, 0, s>>>(n, nullptr, nullptr, nullptr, nullptr, nullptr, mp, ctx->st, slot, m, w.pw,
                                           w.u0,
-                                          nullptr, pre->pnt, pre->pose, pre->var_identity, nullptr, w.gran, w.ngran);
+                                          nullptr, pre->pnt, pre->pose, pre->var_identity, nullptr, w.gran, w.ngran,
+                                          nullptr);
   else {
     // the push record goes through host-mapped memory, so a replayed graph
     // picks up each scan's record (the host writes it before the launch)
-    if (push) ctx->h_in->push = *push;
+    // (slot in_sel: a scan graph's ring position, whose per-scan numbers ride along)
+    HostIn* hin = ctx->h_in + ctx->in_sel;
+    HostIn* din = ctx->d_in + ctx->in_sel;
+    if (push) hin->push = *push;
     k_ins_prep<false><<<g, kBlock, 0, s>>>(n, nd, ctx->ds.ox, ctx->ds.oy, ctx->ds.oz, ctx->ds.oi, mp, ctx->st, slot, m,
                                            w.pw,
-                                           w.u0, push ? &ctx->d_in->push : nullptr, nullptr, nullptr, 0,
-                                           nd ? ctx->ds.hflags : nullptr, w.gran, w.ngran);
+                                           w.u0, push ? &din->push : nullptr, nullptr, nullptr, 0,
+                                           nd ? ctx->ds.hflags : nullptr, w.gran, w.ngran,
+                                           ctx->in_ph ? din->ph : nullptr);
   }
   const int ntile = (n + kRootTile - 1) / kRootTile;
   (void)epoch;
@@ -2847,18 +2855,20 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
                                                     Pub* __restrict__ pub, int seq, DevMap m,
                                                     const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
                                                     int* __restrict__ plan, const int* __restrict__ gate,
-                                                    unsigned* __restrict__ head_flag, int batch) {
+                                                    unsigned* __restrict__ head_flag, int batch,
+                                                    const int* __restrict__ dseq) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
   if (blockIdx.x == 0) {  // the margi head: x_curr <- x_buf.back(), the window view, the state publication
+    if (dseq) {  // the scan graph: this scan's publication numbers from the device state (DState::ph)
+      seq = dseq[0];
+      wa.seq2 = dseq[1];
+    }
     make_win_block(st, wa, m.wpn, win, nper, slot_of);
     __syncthreads();  // x_curr (set_xc), seen by the whole block
-    if (seq > 0) publish_state_block(st, wa.win_count, ba_iters_valid, ba_iters, ba_hess, pub, seq);
     if (threadIdx.x == 0) st->margi_seq = seq;  // k_margi_copy hands it to the next IEKF
-    if (head_flag) {  // x_curr is final: the next scan's propagation may start (vg_ctx::d_sync[2])
-      __threadfence();
-      __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_store(head_flag, (unsigned)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    // x_curr is final: the next scan's propagation may start (vg_ctx::d_sync[2]) as soon as
+    // the publication has read what that propagation overwrites
+    publish_state_block(st, wa.win_count, ba_iters_valid, ba_iters, ba_hess, pub, seq, head_flag, (unsigned)seq);
     return;
   }
   // the leaves read the refined window poses from the state (the view block
@@ -3246,19 +3256,25 @@ __global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, doub
 // The part of multi_margi that does not depend on the BA (jour stamps, the
 // slide-tree levels, the oldest slot's points grouped by leaf), enqueued right
 // after the recut on the second stream so it runs under the LM iterations.
-int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, double jour) {
+int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, double jour,
+                     const unsigned* flags) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream_ds;
   const int nlev = mp.max_layer + 1;
-  VG_HIP(flush_insert_events(ctx));
-  VG_HIP(hipStreamWaitEvent(s, ctx->ev_recut_done, 0));  // recorded at the recut's end (map_recut)
+  if (flags) {  // the scan graph: k_ba_init raises d_sync[3] once the recut has ended (no event inside a graph)
+    VG_TRY(sync_wait(ctx, s, 3, flags[0]));
+  } else {
+    VG_HIP(flush_insert_events(ctx));
+    VG_HIP(hipStreamWaitEvent(s, ctx->ev_recut_done, 0));  // recorded at the recut's end (map_recut)
+  }
   const int gl = 64;  // grid-stride over device-side counts
   k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour, w.rc, n_oldest);
   for (int L = 0; L < nlev; L++) k_collect_level<<<gl * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(L, thread_num, m, w.list1, w.list0, w.rc);
   (void)slot0;  // the oldest slot's points per leaf are the leaves' runs (DevMap::lseg): no sort here
   (void)n_oldest;
   VG_HIP(hipGetLastError());
+  if (flags) VG_TRY(sync_set(ctx, s, 4, flags[1]));  // the scan graph's margi tail waits for it
   VG_HIP(hipEventRecord(ctx->ev_prefix_done, s));
   return VG_OK;
 }
@@ -3319,7 +3335,7 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   k_margi_leaf<<<1 + 512 * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(
       m.counters + kCntLeaves, w.list0, mp, wa2, ctx->st, dwin, dn, dn + 32, bi != nullptr, bi,
       bi ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, pub_seq, m, ctx->ba.fac_eig, ctx->ba.fac_pcr, w.plan, gate,
-      flags ? ctx->d_sync + 2 : nullptr, ctx->margi_batch ? 1 : 0);
+      flags ? ctx->d_sync + 2 : nullptr, ctx->margi_batch ? 1 : 0, nullptr);
   VG_HIP(hipEventRecord(ctx->ev_tail_a, s));
   // the margi's publication number into the IEKF hand-off flag: by the margi
   // graph's first kernel (k_margi_copy) — or k_sync_set when the local map
@@ -3361,6 +3377,41 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   }
   VG_HIP(hipGraphLaunch(ge, s));
   return VG_OK;  // device error flags reach the host with the end-of-scan counters
+}
+
+// The margi tail inside the scan graph (pipeline.cpp stage_insert_recut),
+// captured on the context stream behind the first two LM iterations: gated on
+// the LM's `fin` like a speculative tail; the margi prefix (second stream) is
+// waited for on a device flag (d_sync[4] >= DState::ph[4]); the publication
+// numbers come from DState::ph; the ring (wa) is the graph's own.
+int map_margi_tail_capture(vg_ctx* ctx, const MP& mp, const WinArg& wa) {
+  DevMap& m = ctx->map;
+  Work& w = ctx->wk;
+  hipStream_t s = ctx->stream;
+  const int nlev = mp.max_layer + 1;
+  WinD* dwin = (WinD*)ctx->ba.xs;
+  int* dn = (int*)((char*)ctx->ba.xs + sizeof(WinD));
+  const int* gate = ba_gate_dev(ctx);
+  const int thread_num = ctx->cfg.thread_num;
+  VG_TRY(sync_wait_dev(ctx, s, 4, &ctx->st->ph[4], gate));
+  k_margi_leaf<<<1 + 512 * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(
+      m.counters + kCntLeaves, w.list0, mp, wa, ctx->st, dwin, dn, dn + 32, 1, ba_iters_dev(ctx), ba_hess_dev(ctx),
+      ctx->d_pub, 0, m, ctx->ba.fac_eig, ctx->ba.fac_pcr, w.plan, gate, ctx->d_sync + 2, ctx->margi_batch ? 1 : 0,
+      &ctx->st->ph[1]);
+  k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, dwin, m, gate, w.list0,
+                                                ctx->margi_fused ? 1 : 0, ctx->d_sync, ctx->st);
+  if (ctx->margi_fused) {
+    k_margi_erase_all<<<64 * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(nlev, thread_num, m, w.list1, w.rc, gate);
+  } else {
+    for (int L = nlev - 1; L >= 1; L--)
+      k_margi_internal<<<64 * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc, gate);
+    for (int L = 0; L < nlev; L++)
+      k_margi_erase_mark<<<64 * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(L, thread_num, m, w.list1, w.rc, gate);
+    k_clear_mark<<<64, kBlock, 0, s>>>(nlev - 2, nlev, thread_num, m, w.list1, w.rc, gate);
+  }
+  k_slide_compact<<<1, 1024, 0, s>>>(thread_num, m, ctx->st, wa.win_count, mp.W - 1, ctx->d_pub, -1, gate);
+  VG_HIP(hipGetLastError());
+  return VG_OK;
 }
 
 }  // namespace vg

@@ -429,10 +429,10 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
     // the device propagation needs only x_curr, final once the margi head
     // (k_margi_leaf's workgroup 0) stored it: it runs under the leaves'
     // plane updates, and the IEKF waits for those alone
-    VG_TRY(sync_wait(ctx, ctx->stream_iekf, 2, ctx->sync_tail_value));
+    // (both waits inside k_scan_prop: no polling kernels, no launch gap)
     if (ctx->in_ev) VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->in_ev, 0));  // a host-input scan's unpack
-    VG_TRY(state_scan_begin(ctx, nullptr, x, y, z, n, ctx->stream_iekf, bprop));
-    VG_TRY(sync_wait(ctx, ctx->stream_iekf, 0, ctx->sync_tail_value));
+    VG_TRY(state_scan_begin(ctx, nullptr, x, y, z, n, ctx->stream_iekf, bprop, ctx->d_sync + 2, ctx->sync_tail_value,
+                            ctx->d_sync, ctx->sync_tail_value));
     bprop = nullptr;
     opened = true;
   } else {
@@ -724,6 +724,24 @@ static bool mid_graph_ok(vg_ctx* ctx, const HostPipe* P) {
          P->win_count == c.win_size && P->push_pending && P->push.ord == c.win_size - 1 && !P->begin_pending &&
          ctx->dbg_apply_cap < 0 && ctx->dbg_ins_cap < 0 && ctx->dbg_fac_max < 0 && P->ds_seq != 0;
 }
+// The scan graph: the same insert + recut, then k_ba_init, the first two LM
+// iterations and the margi tail gated on the LM's end (a speculative tail
+// inside the graph), one launch per scan on the main stream — no graph
+// boundaries between the recut, the LM and the margi (each left the stream
+// idle 5-14 us). Per-scan numbers (the LM's flag numbers, the tail's
+// publication numbers, two hand-off values) go through the ring position's
+// host-mapped slot into DState::ph (k_ins_prep). Events cannot be recorded
+// inside it, so the margi prefix waits for the recut on a device flag
+// (k_ba_init raises d_sync[3]) and the tail for the prefix on another
+// (d_sync[4]); the next downsample follows the prefix on its stream.
+// Conditions: the steady state predicted 2 LM iterations (the graph holds 2),
+// the flag hand-offs, no /map_cmap publication in the tail.
+static bool scan_graph_ok(vg_ctx* ctx, const HostPipe* P) {
+  return ctx->scan_graph && ctx->spec_tail && ctx->ba_graph && ctx->ba_graph2 && ctx->ba_last_iters == 2 &&
+         ctx->flag_sync && !ctx->serial_kernels && ctx->overlap_iekf && ctx->want_ds_stream &&
+         !(ctx->prof_on && !ctx->prof_clock) &&
+         ctx->dbg_capture != 1 && !(ctx->pub_flags & 1) && !P->lmp.active;
+}
 static int stage_insert_recut(vg_ctx* ctx) {
   HostTimer ht_(ctx, kHostInsert);
   HostPipe* P = hp(ctx);
@@ -735,8 +753,24 @@ static int stage_insert_recut(vg_ctx* ctx) {
   P->epoch++;
   VG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_ds_done, 0));
   P->push_pending = false;
-  ctx->h_in->push = P->push;  // this scan's record, read by the replay
-  hipGraphExec_t& ge = ctx->g_mid[ring0];
+  const bool sg = scan_graph_ok(ctx, P);
+  P->scan_g = sg;
+  ctx->in_sel = ring0;  // this ring position's host-mapped inputs
+  HostIn& hin = ctx->h_in[ring0];
+  hin.push = P->push;  // this scan's record, read by the replay
+  if (sg) {
+    const int seq0 = ctx->pub_seq + 1;  // the LM's flag numbers (ba_run's)
+    ctx->pub_seq += 10;
+    ctx->ba_seq0_pre = seq0;
+    P->tail_seq1 = ++ctx->pub_seq;  // the tail's publication numbers (margi_enqueue's)
+    P->tail_seq2 = ++ctx->pub_seq;
+    P->tail_wa = make_winarg(P, 1);
+    P->sg_flags[0] = ++ctx->rc_flag_ctr;
+    P->sg_flags[1] = ++ctx->pre_flag_ctr;
+    const int ph[6] = {seq0, P->tail_seq1, P->tail_seq2, (int)P->sg_flags[0], (int)P->sg_flags[1], 0};
+    memcpy(hin.ph, ph, sizeof(ph));
+  }
+  hipGraphExec_t& ge = sg ? ctx->g_scan[ring0] : ctx->g_mid[ring0];
   if (!ge) {
     const int cap = ctx->cap.max_points_per_scan;
     WinArg wa = make_winarg(P, 0);
@@ -744,9 +778,13 @@ static int stage_insert_recut(vg_ctx* ctx) {
     hipStream_t s = ctx->stream;
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     ctx->capturing = true;
+    ctx->in_ph = sg;
     int nf = 0;
     int r = map_insert(ctx, P->mpd, slot, cap, P->epoch, c.thread_num, &P->push, nullptr, ctx->ds.hflags + 1);
+    ctx->in_ph = false;
     if (r == VG_OK) r = map_recut(ctx, P->mpd, wa, c.thread_num, &nf, false, 1);
+    if (r == VG_OK && sg) r = ba_capture_scan_lm(ctx, P->mp.data());
+    if (r == VG_OK && sg) r = map_margi_tail_capture(ctx, P->mpd, P->tail_wa);
     ctx->capturing = false;
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(s, &g);
@@ -758,6 +796,16 @@ static int stage_insert_recut(vg_ctx* ctx) {
   prof_begin(ctx, kProfInsert);
   VG_HIP(hipGraphLaunch(ge, ctx->stream));
   prof_end(ctx, kProfInsert);
+  if (sg) {  // nothing to record: the prefix and the next downsample order themselves on the flags
+    ctx->ins_ev_pending = false;
+    ctx->tail_a_valid = true;  // the next IEKF waits for this graph's tail (device flags)
+    P->wp_n[slot] = P->n_raw;
+    P->ins_slot = slot;
+    P->cur.ins_slot = slot;
+    P->ins_n = -1;
+    P->rc_seq = ++ctx->rc_pub;
+    return VG_OK;
+  }
   // ev_ds_free (the insert has read the ds buffers) and ev_recut_done (the
   // margi prefix starts from here): recorded by their first waiter's flush,
   // the LM's right behind k_ba_init (a record right behind the graph leaves
@@ -821,6 +869,9 @@ int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows) {
     return VG_E_STATE;
   }
   VG_TRY(resolve_lm(ctx, P));  // (resolved by the IEKF's enqueue already)
+  const bool pre = P->scan_g;  // the scan graph holds k_ba_init, two iterations and the gated tail
+  P->scan_g = false;
+  ctx->ba_no_defer = false;
   int iters = 0;
   prof_begin(ctx, kProfBA);
   // margi's BA-independent part goes onto the second stream once the first LM
@@ -833,11 +884,17 @@ int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows) {
     if (P->rc_seq > 0) {
       VG_TRY(pub_wait(ctx, &ctx->h_pub->seq_rc, P->rc_seq, "k_fac_sort"));
       rc_status = __atomic_load_n(&ctx->h_pub->rc_status, __ATOMIC_ACQUIRE);
-      if (rc_status) return VG_OK;
+      if (rc_status) {
+        ctx->ba_no_defer = true;  // the scan graph's LM skipped: the host completes the recut below
+        return VG_OK;
+      }
       P->n_factors = __atomic_load_n(&ctx->h_pub->rc_nf, __ATOMIC_ACQUIRE);
       P->cur.st.n_factors = P->n_factors;
     }
-    VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], ctx->cfg.thread_num, P->jour));
+    // after a scan graph whose recut completed on the device, the prefix and the
+    // graph's tail meet on device flags (the host-completed recut records events)
+    VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], ctx->cfg.thread_num, P->jour,
+                            pre && !rc_status ? P->sg_flags : nullptr));
     P->prefix = true;
     return VG_OK;
   };
@@ -858,9 +915,9 @@ int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows) {
   const bool defer = spec_ok && ctx->lm_defer && ctx->flag_sync && !ctx->serial_kernels && ctx->overlap_iekf &&
                      ctx->want_ds_stream;
   bool pending = false;
-  VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), &iters, prefix, spec_ok ? spec : std::function<int(bool*)>(), &tail_ok,
-                defer ? &pending : nullptr));
-  P->tail_queued = tail_ok;
+  VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), &iters, prefix,
+                spec_ok && !pre ? spec : std::function<int(bool*)>(), &tail_ok, defer ? &pending : nullptr, pre ? 2 : 0));
+  P->tail_queued = tail_ok && !rc_status;  // (a skipped LM left the graph's tail shut)
   if (pending) {
     P->lmp.active = true;
     P->lmp.seq1 = P->tail_seq1;

@@ -75,8 +75,25 @@ __global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict
 // ascending column order over F's non-zeros (the host's sandwich()). The
 // round-4 first form (the chain on one lane, per-lane index arrays for F's
 // rows) took 54 us: 11 us chain, 37 us covariance (scripts/probe_prop.py).
+// Hand-offs inside the kernel (the split IEKF stream, pipeline.cpp): the
+// per-sample rotations need only the biases, final since the previous scan's
+// IEKF, so they run before the margi head's flag (head_flag >= head_target:
+// x_curr.R/p <- x_buf.back() stored); the kernel then waits for the margi
+// leaves' plane updates (leaf_flag >= leaf_target) before it ends, so the
+// IEKF behind it needs no polling kernel and no launch gap of its own. A wait
+// that times out (~1 s) sets error bit 64 and closes the IEKF (st->done).
+__device__ __forceinline__ bool flag_wait(const unsigned* flag, unsigned target) {
+  for (long it = 0; (int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0; it++) {
+    __builtin_amdgcn_s_sleep(2);
+    if (it > (1l << 24)) return false;
+  }
+  return true;
+}
 __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restrict__ st, const float* x, const float* y,
-                                                   const float* z, int n, int set_scan) {
+                                                   const float* z, int n, int set_scan,
+                                                   const unsigned* __restrict__ head_flag, unsigned head_target,
+                                                   const unsigned* __restrict__ leaf_flag, unsigned leaf_target,
+                                                   int* __restrict__ err) {
   // the arguments once into LDS, by all lanes (the kernel-argument block is
   // host memory: the serial chain below would pay a round trip per sample)
   __shared__ PropArg a;
@@ -120,6 +137,19 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
     }
     sDt[tid] = dt;
     sOk[tid] = ok ? 1 : 0;
+  }
+  if (head_flag) {  // x_curr.R/p of the previous scan's margi head
+    __shared__ int s_late;
+    if (tid == 0) s_late = flag_wait(head_flag, head_target) ? 0 : 1;
+    __syncthreads();
+    if (s_late) {
+      if (tid == 0) {
+        atomicOr(err, 64);
+        st->done = 1;
+      }
+      return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
   VG_PROBE_MARK(2);
@@ -311,6 +341,10 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
 #ifdef VG_PROBE
   if (tid == 0) atomicAdd(&g_probe[63], 1ull);
 #endif
+  if (leaf_flag && tid == 0 && !flag_wait(leaf_flag, leaf_target)) {  // the margi leaves' plane updates
+    atomicOr(err, 64);
+    st->done = 1;
+  }
 }
 
 // ---- cross-stream hand-offs on the critical path (vg_ctx::flag_sync)
@@ -341,6 +375,25 @@ __global__ void k_sync_wait(const unsigned* __restrict__ flag, unsigned target, 
       return;
     }
   }
+}
+// the same poll with the target read from the device (a replayed graph's
+// per-scan value) and a gate (the margi tail's: the LM finished)
+__global__ void k_sync_wait_dev(const unsigned* __restrict__ flag, const int* __restrict__ target,
+                                const int* __restrict__ gate, int* __restrict__ err) {
+  if (threadIdx.x != 0 || (gate && !*gate)) return;
+  const unsigned t = (unsigned)*target;
+  for (long it = 0; (int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - t) < 0; it++) {
+    __builtin_amdgcn_s_sleep(4);
+    if (it > (1l << 24)) {
+      atomicOr(err, 64);
+      return;
+    }
+  }
+}
+int sync_wait_dev(vg_ctx* ctx, hipStream_t s, int k, const int* target, const int* gate) {
+  k_sync_wait_dev<<<1, 64, 0, s>>>(ctx->d_sync + k, target, gate, ctx->map.counters + kCntErr);
+  VG_HIP(hipGetLastError());
+  return VG_OK;
 }
 int sync_set(vg_ctx* ctx, hipStream_t s, int k, unsigned value, const int* gate) {
   k_sync_set<<<1, 64, 0, s>>>(ctx->d_sync + k, gate, value);
@@ -574,9 +627,11 @@ int state_alloc(vg_ctx* ctx) {
 }
 
 int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x, const float* y, const float* z, int n,
-                     hipStream_t s, const PropArg* prop) {
+                     hipStream_t s, const PropArg* prop, const unsigned* head_flag, unsigned head_target,
+                     const unsigned* leaf_flag, unsigned leaf_target) {
   if (prop) {
-    k_scan_prop<<<1, 256, 0, s ? s : ctx->stream>>>(*prop, ctx->st, x, y, z, n, x != nullptr ? 1 : 0);
+    k_scan_prop<<<1, 256, 0, s ? s : ctx->stream>>>(*prop, ctx->st, x, y, z, n, x != nullptr ? 1 : 0, head_flag,
+                                                    head_target, leaf_flag, leaf_target, ctx->map.counters + kCntErr);
     VG_HIP(hipGetLastError());
     return VG_OK;
   }

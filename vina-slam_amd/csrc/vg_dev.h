@@ -411,21 +411,42 @@ __device__ __forceinline__ void pub_flag(int* dst, int v) {
   __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// P1: x_curr, the post-IEKF pose, window states, IEKF / BA summary
+// P1: x_curr, the post-IEKF pose, window states, IEKF / BA summary.
+// head_flag: x_curr is final (the caller stored R/p): the next scan's device
+// propagation may start (vg_ctx::d_sync[2]) — raised once what it overwrites
+// (x_curr, the IEKF summary) is read, before the slow host-memory stores
 __device__ __forceinline__ void publish_state_block(const DState* __restrict__ st, int win_count, int ba_iters_valid,
                                                     const int* __restrict__ ba_iters, const int* __restrict__ ba_hess,
-                                                    Pub* __restrict__ pub, int seq) {
+                                                    Pub* __restrict__ pub, int seq, unsigned* head_flag = nullptr,
+                                                    unsigned head_value = 0) {
   const int t = threadIdx.x;
-  for (int e = t; e < kXC; e += blockDim.x) pub_store(&pub->xc[e], st->xc[e]);
+  __shared__ double s_xc[kXC];
+  __shared__ int s_sum[9];
+  for (int e = t; e < kXC; e += blockDim.x) s_xc[e] = st->xc[e];
+  if (t == 0) {
+    s_sum[0] = st->iters;
+    for (int k = 0; k < 4; k++) {
+      s_sum[1 + k] = st->matches[k];
+      s_sum[5 + k] = st->planes[k];
+    }
+  }
+  __syncthreads();
+  if (head_flag) {
+    __threadfence();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(head_flag, head_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (seq <= 0) return;
+  for (int e = t; e < kXC; e += blockDim.x) pub_store(&pub->xc[e], s_xc[e]);
   for (int e = t; e < 12; e += blockDim.x) pub_store(&pub->traj[e], st->traj[e]);
   for (int e = t; e < 6; e += blockDim.x) pub_store(&pub->nnt[e], st->nnt[e]);
   for (int e = t; e < win_count * kXS; e += blockDim.x) pub_store(&pub->xs[e], st->xs[e]);
   if (t == 0) {
-    pub_store(&pub->iekf_iters, st->iters);
-    for (int k = 0; k < 4; k++) pub_store(&pub->matches[k], st->matches[k]);
+    pub_store(&pub->iekf_iters, s_sum[0]);
+    for (int k = 0; k < 4; k++) pub_store(&pub->matches[k], s_sum[1 + k]);
     pub_store(&pub->ba_iters1, ba_iters_valid ? *ba_iters : 0);
     pub_store(&pub->ba_hess1, ba_iters_valid ? *ba_hess : 0);
-    for (int k = 0; k < 4; k++) pub_store(&pub->planes[k], st->planes[k]);
+    for (int k = 0; k < 4; k++) pub_store(&pub->planes[k], s_sum[5 + k]);
   }
   pub_drain();
   __syncthreads();

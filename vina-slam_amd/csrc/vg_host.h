@@ -180,6 +180,8 @@ struct HostPipe {
     WinArg wa;
   } lmp;
   int rc_seq = 0;          // > 0: this scan's recut ran asynchronously (status with Pub::seq_rc == rc_seq)
+  bool scan_g = false;     // this scan's insert + recut + LM + tail went in as the scan graph (stage_insert_recut)
+  unsigned sg_flags[2] = {0, 0};  // its hand-off values: recut done (d_sync[3]), margi prefix done (d_sync[4])
   std::deque<Pend> pend;   // enqueued scans awaiting absorption (oldest first)
   int sticky = VG_OK;      // deferred device error
   // device work deferred to the next launch that can carry it (one launch

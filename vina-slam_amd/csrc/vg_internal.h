@@ -267,7 +267,11 @@ struct DState {
   // IMU_PRE records of the window factors (preintegrated deltas, bias
   // Jacobians, cov_inv; constant once pushed): a ring, factor k at slot
   // (imu_head + k) % kMaxWin, so the slide is one index step
-  int imu_head, margi_seq, pad_h[2];  // margi_seq: the last margi head's publication number (k_margi_copy signals it)
+  int imu_head, margi_seq;  // margi_seq: the last margi head's publication number (k_margi_copy signals it)
+  // the scan graph's per-scan numbers (HostIn::ph, copied by k_ins_prep's block 0):
+  // [0] the LM's first flag number, [1] / [2] the margi tail's publication
+  // numbers, [3] the recut-done flag value, [4] the margi prefix's flag value
+  int ph[6];
   double imurec[kMaxWin * kBaImuRec];
   KClock clk;
 };
@@ -289,9 +293,12 @@ struct PropArg {
   double imu[kPropMax * 7];                      // t, gyr[3], acc[3] per sample
 };
 // per-scan inputs of the replayed graphs, in host-mapped memory: the host
-// writes them before the launch, the kernels read them in place
+// writes them before the launch, the kernels read them in place. One per ring
+// position (the steady state's graphs are per ring position, so a slot is
+// rewritten W scans after the graph that read it)
 struct HostIn {
   PushArg push;
+  int ph[6];  // DState::ph
 };
 // Spatial-tile sharding of one sequence over `world` contexts (one per GPU):
 // every context keeps the root voxels of the tiles it owns (tile_owner) and
@@ -384,8 +391,17 @@ struct vg_ctx {
   // kernels do not run concurrently (AMD_SERIALIZE_KERNEL, or VG_SERIAL_KERNELS=1 as rocprofv3 --pmc
   // runs set): no device-flag hand-offs (a polling kernel would wait for a producer queued behind it)
   bool serial_kernels = false;
-  vg::HostIn* h_in = nullptr;  // host-mapped per-scan inputs of replayed graphs (host address)
+  vg::HostIn* h_in = nullptr;  // host-mapped per-scan inputs of replayed graphs, kMaxWin slots (host address)
   vg::HostIn* d_in = nullptr;  // its device address
+  int in_sel = 0;              // the slot map_insert uses (the ring position of a scan graph)
+  bool in_ph = false;          // map_insert copies the slot's per-scan numbers into DState::ph (scan graph capture)
+  // the scan graph (pipeline.cpp stage_insert_recut): insert + recut + k_ba_init
+  // + two LM iterations + the gated margi tail, one per ring position
+  hipGraphExec_t g_scan[vg::kMaxWin] = {};
+  bool scan_graph = true;   // vgx_debug 27: 0 = separate insert+recut graph, LM graph, margi tail
+  int ba_seq0_pre = 0;      // the LM flag numbers a scan graph's k_ba_init uses (ba_run pre > 0)
+  bool ba_no_defer = false; // set by stage_ba's prefix step when the recut needs the host (no deferral)
+  unsigned rc_flag_ctr = 0, pre_flag_ctr = 0;  // d_sync[3] / d_sync[4] values (scan graph hand-offs)
   bool pool_zeroed = false;
   bool ins_ev_pending = false;  // ev_ds_free / ev_recut_done of the last insert+recut graph not recorded yet  // map_reset has cleared the node records once (then only the used ids)
   bool use_graphs = true;  // margi prefix on the second stream
@@ -449,7 +465,8 @@ struct vg_ctx {
   bool ba_fuse_ctl = true;    // vgx_debug 19: the LM bookkeeping in k_ba_resid's IMU workgroup (A/Bs r04e 0, r04g/h +0.8-0.9 %)
   bool ba_graph = true;      // LM iterations replay one captured graph each (vgx_debug 15: 0 = direct launches)
   bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)
-  unsigned* d_sync = nullptr;  // hand-off flags: [0] margi leaf -> next IEKF, [1] IEKF -> insert, [2] margi head -> propagation
+  unsigned* d_sync = nullptr;  // hand-off flags: [0] margi leaf -> next IEKF, [1] IEKF -> insert, [2] margi head -> propagation,
+                               // [3] recut done -> margi prefix, [4] margi prefix -> tail (scan graph)
   bool sync_tail_armed = false;  // the last margi's leaf pass stores sync_tail_value into d_sync[0]
   unsigned sync_tail_value = 0, sync_iekf_value = 0;
   bool dev_prop = false;     // host_step propagates on the device (k_scan_prop; vgx_debug 13: 1 = on the device)
@@ -651,16 +668,26 @@ int map_memo_probe(vg_ctx* ctx, const MP& mp, int* out);  // test-only (vgx_memo
 int iekf_grid(vg_ctx* ctx);  // k_iekf's workgroups (map.hip iekf_blocks)
 int sync_set(vg_ctx* ctx, hipStream_t s, int k, unsigned value, const int* gate = nullptr);  // state.hip: cross-stream flags
 int sync_wait(vg_ctx* ctx, hipStream_t s, int k, unsigned target);
+int sync_wait_dev(vg_ctx* ctx, hipStream_t s, int k, const int* target, const int* gate);  // target / gate on the device
 // multi_margi + the device-state slide; publishes the state (pub_seq, before
 // the margi kernels) and the end-of-scan counters (pub_seq2)
-int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, double jour);
+// flags (the scan graph): {recut-done value of d_sync[3] to wait for, value to
+// store into d_sync[4] at the end}; nullptr: event waits
+int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, double jour,
+                     const unsigned* flags = nullptr);
 int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, int pub_seq, int pub_seq2,
               const int* gate);
+int map_margi_tail_capture(vg_ctx* ctx, const MP& mp, const WinArg& wa);  // the scan graph's gated margi tail
 // state.hip
 int state_alloc(vg_ctx* ctx);
 // x_curr / x_prop / IEKF flags; with x != nullptr also the scan the IEKF reads
+// prop: propagate on the device (k_scan_prop), optionally waiting inside for
+// the margi head's flag (before the rotation chain) and the leaves' flag (at
+// its end); see state.hip
 int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x = nullptr, const float* y = nullptr,
-                     const float* z = nullptr, int n = 0, hipStream_t s = nullptr, const PropArg* prop = nullptr);
+                     const float* z = nullptr, int n = 0, hipStream_t s = nullptr, const PropArg* prop = nullptr,
+                     const unsigned* head_flag = nullptr, unsigned head_target = 0,
+                     const unsigned* leaf_flag = nullptr, unsigned leaf_target = 0);
 int state_set_scan(vg_ctx* ctx, const float* x, const float* y, const float* z, int n, hipStream_t s = nullptr);
 int state_push(vg_ctx* ctx, int ord, int new_imu, const double* imurec);  // imurec: kBaImuRec doubles (new_imu >= 0)
 int state_publish(vg_ctx* ctx, int win_count, const int* ba_iters_dev, int seq, const int* gate = nullptr);
@@ -689,9 +716,15 @@ int ba_alloc(vg_ctx* ctx);
 // ba_gate_dev; *tail_ok tells whether that copy is the one that runs
 // pending != nullptr: the run may return once the speculative tail is queued
 // (*pending = true, *iters = -1); ba_resolve then continues it
+// pre > 0: the scan graph already holds k_ba_init, the first `pre`
+// iterations and the gated margi tail (flag numbers from ctx->ba_seq0_pre)
 int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters,
            const std::function<int()>& before_first_wait = nullptr,
-           const std::function<int(bool*)>& spec_tail = nullptr, bool* tail_ok = nullptr, bool* pending = nullptr);
+           const std::function<int(bool*)>& spec_tail = nullptr, bool* tail_ok = nullptr, bool* pending = nullptr,
+           int pre = 0);
+// the scan graph's LM part, captured on the context stream (k_ba_init with its
+// numbers from DState::ph, iterations 0 and 1)
+int ba_capture_scan_lm(vg_ctx* ctx, const int* mp_ring);
 // the rest of a deferred run (ctx->ba_loop): waits for the iteration flags and
 // enqueues further iterations as ba_run would have. block = false: returns
 // with *finished = false as soon as a flag it needs is not published yet.

@@ -129,7 +129,8 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
   {
     const char* a = getenv("AMD_SERIALIZE_KERNEL");
     const char* v = getenv("VG_SERIAL_KERNELS");
-    if ((a && atoi(a) != 0) || (v && atoi(v) != 0)) {
+    const char* p = getenv("ROCPROF_COUNTER_COLLECTION");  // rocprofv3 --pmc sets it for its target
+    if ((a && atoi(a) != 0) || (v && atoi(v) != 0) || (p && atoi(p) != 0)) {
       ctx->serial_kernels = true;
       ctx->flag_sync = false;
     }
@@ -230,13 +231,13 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     return fail(VG_E_HIP);
   }
   memset(ctx->h_pub, 0, sizeof(Pub));
-  if ((e = hipHostMalloc((void**)&ctx->h_in, sizeof(HostIn), hipHostMallocMapped | hipHostMallocCoherent)) !=
+  if ((e = hipHostMalloc((void**)&ctx->h_in, kMaxWin * sizeof(HostIn), hipHostMallocMapped | hipHostMallocCoherent)) !=
           hipSuccess ||
       (e = hipHostGetDevicePointer((void**)&ctx->d_in, ctx->h_in, 0)) != hipSuccess) {
     ctx->err = std::string("hipHostMalloc (mapped inputs): ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
   }
-  memset(ctx->h_in, 0, sizeof(HostIn));
+  memset(ctx->h_in, 0, kMaxWin * sizeof(HostIn));
   if ((e = hipEventCreateWithFlags(&ctx->sync_ev, hipEventDisableTiming)) != hipSuccess) {
     ctx->err = std::string("hipEventCreate: ") + hipGetErrorString(e);
     return fail(VG_E_HIP);
@@ -279,6 +280,8 @@ int vg_destroy(vg_ctx* ctx) {
   if (ctx->g_ba2) (void)hipGraphExecDestroy(ctx->g_ba2);
   if (ctx->g_ds) (void)hipGraphExecDestroy(ctx->g_ds);
   for (auto& g : ctx->g_mid)
+    if (g) (void)hipGraphExecDestroy(g);
+  for (auto& g : ctx->g_scan)
     if (g) (void)hipGraphExecDestroy(g);
   if (ctx->h_in) (void)hipHostFree(ctx->h_in);
   if (ctx->stream_ds && ctx->stream_ds != ctx->stream) (void)hipStreamSynchronize(ctx->stream_ds);
@@ -860,6 +863,10 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
   }
   if (key == 14) {  // 0: event waits for the margi leaf -> IEKF and IEKF -> insert hand-offs
     ctx->flag_sync = value != 0;
+    return VG_OK;
+  }
+  if (key == 27) {  // 0: no scan graph (separate insert+recut graph, LM launches, margi tail)
+    ctx->scan_graph = value != 0;
     return VG_OK;
   }
   if (key == 26) {  // 0: a fused step waits for its LM's outcome (no deferral to the next step)
