@@ -35,7 +35,8 @@ METRIC = "scans/sec (downsample+kNN+LM solve), 64-line LiDAR, 1/2/4/8 MI355X; AT
 # reference's fp64 record (PlaneRec, 224 B), so the byte model uses that
 PLANE_B = 224.0
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E (MI355X_MICROARCH.md)
-FP64_MFMA_TFLOPS = 78.6  # MI355X dense fp64 matrix peak
+FP64_MFMA_TFLOPS = 78.6  # MI355X dense fp64 matrix peak (AMD spec)
+FP64_TFLOPS = 78.6       # MI355X fp64 vector peak (AMD spec; k_ba_hess is mostly VALU)
 
 
 def parse():
@@ -258,8 +259,13 @@ def main():
     ctx.close()
     host_ms = {k[5:]: round(v["ms"] / args.steps, 4) for k, v in prof.items() if k.startswith("host_")}
 
+    # P_k of the timed scans themselves, from the committed PMC pass over the
+    # same scans (scripts/pmc_run.py: same workload, sequence and warm-up; the
+    # pipeline is deterministic, so a scan's P_k is the same in every run)
+    pmc = pmc_traffic()
+    pk_scans = pmc_pk(pmc, "synthetic-%s@%s.yaml" % (args.lidar, args.config), seq_id, warmup, total, stats)
     # ---- headline roofline: the whole scan against HBM -------
-    roof = scan_roofline(stats, stage_stats, W, dt / args.steps)
+    roof = scan_roofline(stats, stage_stats, W, dt / args.steps, pk_scans)
     # ---- per-kernel rooflines ----------------------------------------------
     # Kernel-only launch times from the in-kernel clocks (vg_profile bit 2:
     # the device's constant-rate wall clock read inside the kernel, executed
@@ -279,14 +285,19 @@ def main():
                   "timing": "in-kernel clock (wall_clock64), executed launches of the timed region"}
     # k_iekf (hot loop #1, HBM-bound gather): 16 B per raw point (fp32 xyz +
     # cached leaf) + PLANE_B per distinct plane record (P_k) per launch. The
-    # timed scans' own point counts and iteration counts; P_k (distinct plane
-    # records per executed iteration) from the per-stage pass, as its mean
+    # timed scans' own point counts, iteration counts and P_k (from the PMC
+    # pass over the same scans; else the per-stage pass's mean)
     iek = prof["k_iekf_clock"]
     n_launch = iek["launches"]
     it_n = sum(s["iekf_iters"] for s in stage_stats)
     p_mean = sum(sum(s["iekf_planes"][: s["iekf_iters"]]) for s in stage_stats) / it_n if it_n else 0.0
     it_t = sum(s["iekf_iters"] for s in stats)
-    bytes_tot = sum(s["iekf_iters"] * 16.0 * s["n_raw"] for s in stats) + PLANE_B * p_mean * it_t
+    if pk_scans:
+        bytes_tot = sum(s["iekf_iters"] * 16.0 * s["n_raw"] + PLANE_B * sum(pk[: s["iekf_iters"]])
+                        for s, pk in zip(stats, pk_scans))
+        p_mean = sum(sum(pk[: s["iekf_iters"]]) for s, pk in zip(stats, pk_scans)) / max(it_t, 1)
+    else:
+        bytes_tot = sum(s["iekf_iters"] * 16.0 * s["n_raw"] for s in stats) + PLANE_B * p_mean * it_t
     avg_s = iek["ms"] * 1e-3 / max(n_launch, 1)
     bpl = bytes_tot / max(it_t, 1)
     achieved = bpl / avg_s / 1e9 if avg_s > 0 else 0.0
@@ -297,29 +308,58 @@ def main():
                  "bytes_per_launch": int(bpl), "P_k_mean": round(p_mean, 1),
                  "timing": "in-kernel clock (wall_clock64: first workgroup start -> last workgroup end), executed "
                            "launches of the timed region",
+                 "P_k_source": "PMC pass over the same scans (%s)" % pmc.get("_file") if pk_scans else
+                               "per-stage pass mean",
                  "event_interval_us": round(ev["ms"] * 1e3 / ev["launches"], 3) if ev["launches"] else None}
-    pmc = pmc_traffic()
-    for r in (roof_solve, roof_iekf):
-        if r["kernel"] in pmc:
-            r["traffic"] = pmc[r["kernel"]]["traffic_bytes"]
-            r["traffic_source"] = pmc["_file"]
-    # FETCH_SIZE calibrated per access shape (scripts/micro/fetch_cal.hip ->
-    # profiles/<round>/fetch_calibration.json): the counter k_iekf's
-    # algorithmic bytes would produce (its 4 B/lane SoA planes + leaf cache at
-    # the SoA ratio, its 224 B plane-record gathers at the record ratio) beside
-    # the measured counter; their quotient is the traffic ratio the x2
-    # correction cannot give for these shapes
-    cal = fetch_calibration()
-    if cal and "k_iekf" in pmc and "fetch_raw_bytes" in pmc["k_iekf"]:
-        it_n = max(it_t, 1)
-        n_mean = sum(s["iekf_iters"] * s["n_raw"] for s in stats) / it_n
-        exp_fetch = cal["k_soa4"] * 16.0 * n_mean + cal["k_rec224"] * PLANE_B * p_mean
-        roof_iekf["fetch_calibrated"] = {
-            "measured_fetch_raw": pmc["k_iekf"]["fetch_raw_bytes"], "expected_fetch_raw": int(exp_fetch),
-            "ratio": round(pmc["k_iekf"]["fetch_raw_bytes"] / exp_fetch, 3) if exp_fetch else None,
-            "shape_ratios": {"soa4": cal["k_soa4"], "rec224": cal["k_rec224"]}, "source": cal["_file"],
-            "note": "measured FETCH_SIZE bytes (no x2) / the FETCH the algorithmic bytes produce at the calibrated "
-                    "per-shape ratios (same workload, PMC pass of the same build)"}
+    # the recut's level kernels (k_rc_level0 + max_layer x k_rc_level), one
+    # span per scan: SURVEY 8(d)'s recut bytes V_slide (80 W + 80) per scan
+    rck = prof["k_rc_clock"]
+    rc_s = rck["ms"] * 1e-3 / max(rck["launches"], 1)
+    rc_b = sum(s["n_slide"] * (80.0 * W + 80.0) for s in stats) / max(len(stats), 1)
+    rc_a = rc_b / rc_s / 1e9 if rc_s > 0 else 0.0
+    roof_rc = {"kernel": "k_rc_level0 + %d x k_rc_level (the recut's levels, one span per scan)" % p["LocalBA"]["max_layer"],
+               "bound": "hbm", "achieved": round(rc_a, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+               "frac": round(rc_a / HBM_PEAK_GBPS, 6), "traffic": None, "avg_span_us": round(rc_s * 1e6, 3),
+               "spans": rck["launches"], "bytes_per_scan": int(rc_b),
+               "timing": "in-kernel clock: k_rc_level0's first workgroup start -> the last level kernel's last "
+                         "workgroup end, timed scans"}
+    # k_ba_hess (the LM's LiDAR + IMU Hessian pass): SURVEY 8(d)'s BA bytes
+    # F (80 W + 176) per pass; fp64 flops per pass from the kernel's operations
+    # (hess_flops: counted per (factor, frame) lane, off-diagonal X^T S X,
+    # the ordered reduction and the IMU factor blocks)
+    hk = prof["k_ba_hess_clock"]
+    h_s = hk["ms"] * 1e-3 / max(hk["launches"], 1)
+    nh = sum(s["ba_hess"] for s in stats)
+    h_b = sum(s["ba_hess"] * s["n_factors"] * (80.0 * W + 176.0) for s in stats) / max(nh, 1)
+    h_f = sum(s["ba_hess"] * hess_flops(W, s["n_factors"]) for s in stats) / max(nh, 1)
+    h_a = h_b / h_s / 1e9 if h_s > 0 else 0.0
+    h_t = h_f / h_s / 1e12 if h_s > 0 else 0.0
+    roof_hess = {"kernel": "k_ba_hess", "bound": "hbm", "achieved": round(h_a, 2), "peak": HBM_PEAK_GBPS,
+                 "unit": "GB/s", "frac": round(h_a / HBM_PEAK_GBPS, 6), "traffic": None,
+                 "avg_launch_us": round(h_s * 1e6, 3), "launches": hk["launches"], "bytes_per_launch": int(h_b),
+                 "fp64": {"flops_per_launch": int(h_f), "achieved_tflops": round(h_t, 4), "peak_tflops": FP64_TFLOPS,
+                          "frac": round(h_t / FP64_TFLOPS, 6)},
+                 "timing": "in-kernel clock (first workgroup start -> last workgroup end), executed launches of the "
+                           "timed region"}
+    # traffic: FETCH x2 + WRITE per unit (MI355X_MICROARCH.md), and its ratio
+    # to the algorithmic bytes, both over the same launches of the PMC pass
+    # (scripts/pmc_summary.py; a fixed set of scans, so the same whatever
+    # --steps this run times)
+    for r, key in ((roof_solve, "k_ba_solve"), (roof_iekf, "k_iekf"), (roof_rc, "recut_levels"),
+                   (roof_hess, "k_ba_hess")):
+        e = pmc.get(key)
+        if not e:
+            continue
+        r["traffic"] = e["traffic_bytes"]
+        r["traffic_source"] = pmc["_file"]
+        if e.get("traffic_ratio") is not None:
+            r["traffic_ratio"] = e["traffic_ratio"]
+            r["traffic_unit"] = e["unit"]
+            r["traffic_alg_bytes"] = e["alg_bytes"]
+        if "fetch_calibrated" in e:
+            r["fetch_calibrated"] = dict(e["fetch_calibrated"], note="measured FETCH_SIZE bytes (no x2) / the FETCH "
+                                         "the algorithmic bytes produce at the calibrated per-shape ratios, same "
+                                         "launches of the PMC pass")
     roof["stage_ms_per_scan"] = stage_ms
 
     h2d = None
@@ -364,8 +404,12 @@ def main():
                        "nodes_used_end": int(stats[-1]["nodes_used"]), "fix_used_end": int(stats[-1]["fix_used"]),
                        "factors_per_scan": int(np.mean([s["n_factors"] for s in stats])),
                        "lm_iters_per_scan": round(float(np.mean([s["ba_iters"] for s in stats])), 2),
-                       "parallelism": ("tile-sharded x%d" if tile else "replica x%d") % world},
+                       "parallelism": ("tile-sharded x%d" if tile else "replica x%d") % world,
+                       "vnc_prep": "skipped on the GPU: matchVoxelMap always returns 0, so the scan-plane prep "
+                                   "(voxel_map.cpp:169-200, octree.cpp:628-684, odometry.cpp:22-61) never changes "
+                                   "the output (SURVEY A8); the CPU baseline pays it"},
             "roofline": roof, "roofline_k_ba_solve": roof_solve, "roofline_k_iekf": roof_iekf,
+            "roofline_k_rc_level": roof_rc, "roofline_k_ba_hess": roof_hess,
             "host_ms_per_scan": host_ms, "host_input": h2d, "cpu_baseline": cpu, "ate_vs_cpu": ate_cpu,
             "target_128line": targets or None, "multi_sequence": multi_roofline(multi, roof),
             "multi_sequence_1M": multi_1m, "env": {"GPU_MAX_HW_QUEUES": hwq, "VG_BENCH_DEBUG": dbg or None},
@@ -375,7 +419,7 @@ def main():
         dist.destroy_process_group()
 
 
-def scan_roofline(stats, stage_stats, W, t_scan):
+def scan_roofline(stats, stage_stats, W, t_scan, pk_scans=None):
     """Whole-scan algorithmic bytes per timed scan / its wall time:
     B = 16 N_raw + 16 N_ds + sum_k (12 N_raw + 4 N_raw + PLANE_B P_k) + 12 N_ds
         + 2 V_ins 440 + V_slide (80 W + 80) + (I_H + I_R) F (80 W + 176).
@@ -385,10 +429,16 @@ def scan_roofline(stats, stage_stats, W, t_scan):
     per executed iteration."""
     it_n = sum(s["iekf_iters"] for s in stage_stats)
     p_mean = sum(sum(s["iekf_planes"][: s["iekf_iters"]]) for s in stage_stats) / it_n if it_n else 0.0
+    if pk_scans:  # the timed scans' own P_k (PMC pass over the same scans)
+        it_t = sum(s["iekf_iters"] for s in stats)
+        p_mean = sum(sum(pk[: s["iekf_iters"]]) for s, pk in zip(stats, pk_scans)) / max(it_t, 1)
     b = 0.0
-    for s in stats:
+    for q, s in enumerate(stats):
         b += 16.0 * s["n_raw"] + 16.0 * s["n_ds"]
-        b += s["iekf_iters"] * (16.0 * s["n_raw"] + PLANE_B * p_mean)
+        if pk_scans:
+            b += s["iekf_iters"] * 16.0 * s["n_raw"] + PLANE_B * sum(pk_scans[q][: s["iekf_iters"]])
+        else:
+            b += s["iekf_iters"] * (16.0 * s["n_raw"] + PLANE_B * p_mean)
         b += 12.0 * s["n_ds"] + 2.0 * s["v_ins"] * 440.0
         b += s["n_slide"] * (W * 80.0 + 80.0)
         b += (s["ba_hess"] + s["ba_iters"]) * s["n_factors"] * (W * 80.0 + 176.0)
@@ -402,7 +452,9 @@ def scan_roofline(stats, stage_stats, W, t_scan):
                               "P_k": round(p_mean, 1), "V_ins": mean("v_ins"), "V_slide": mean("n_slide"),
                               "F": mean("n_factors"), "I_H": mean("ba_hess"), "I_R": mean("ba_iters")},
             "note": "SURVEY 8(d) algorithmic bytes per scan / ms_per_step, plane records at %d B (fp64, as the "
-                    "gate reads them; SURVEY prices 112 B fp32); P_k from the per-stage pass" % PLANE_B}
+                    "gate reads them; SURVEY prices 112 B fp32); P_k %s" % (
+                        PLANE_B, "of each timed scan (PMC pass over the same scans)" if pk_scans else
+                        "from the per-stage pass")}
 
 
 def multi_roofline(multi, roof):
@@ -668,28 +720,45 @@ def target_workload(args, cfg, host, warm, dev, lidar="128line"):
 
 
 def pmc_traffic():
-    """HBM bytes per launch from the newest committed PMC summary
+    """HBM bytes per unit from the newest committed PMC summary
     (profiles/<round>/pmc_traffic.json, scripts/pmc_summary.py): rocprofv3
-    FETCH_SIZE (x2 on gfx950) + WRITE_SIZE, separate passes."""
+    FETCH_SIZE (x2 on gfx950) + WRITE_SIZE, separate passes, paired with the
+    algorithmic bytes of the same launches."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_traffic.json")))
     if not files:
         return {}
-    d = json.load(open(files[-1]))["kernels"]
+    f = json.load(open(files[-1]))
+    d = dict(f["kernels"])
     d["_file"] = os.path.relpath(files[-1], REPO)
+    d["_meta"] = {k: f.get(k) for k in ("workload", "seq", "per_scan")}
     return d
 
 
-def fetch_calibration():
-    """FETCH_SIZE bytes / algorithmic bytes per access shape, newest
-    profiles/<round>/fetch_calibration.json (scripts/gpu_fetch_cal.sh)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "fetch_calibration.json")))
-    if not files:
-        return {}
-    d = {k: v["fetch_ratio"] for k, v in json.load(open(files[-1]))["shapes"].items() if "fetch_ratio" in v}
-    d["_file"] = os.path.relpath(files[-1], REPO)
-    return d
+def pmc_pk(pmc, workload, seq_id, first, end, stats):
+    """The per-iteration P_k of scans [first, end) of this workload from the
+    PMC pass's log, when that pass ran the same workload and sequence and its
+    point counts agree with this run's (the same scans); else None."""
+    m = pmc.get("_meta") or {}
+    ps = m.get("per_scan")
+    if not ps or m.get("workload") != workload or m.get("seq") != seq_id or len(ps["P_k"]) < end:
+        return None
+    if [s["n_raw"] for s in stats] != ps["n_raw"][first:end]:
+        return None
+    return ps["P_k"][first:end]
+
+
+def hess_flops(W, F):
+    """fp64 flops of one k_ba_hess pass over F factors, counted from the
+    kernel's operations: per (factor, frame) lane
+    factor_frame's ~972 (A_uk, the diagonal block A^T umumT A + corrections,
+    the gradient, the three rank-1 rows) + 54 accumulating it; per factor the
+    lower off-diagonal blocks as three rank-1 terms, 3 (18 W^2 - 18 W) x 2,
+    plus their S scaling 18 W and the ordered row reduction 27 W; per IMU
+    factor J^T C (450 x 29), J^T C J (900 x 29), J^T C r and r^T C r."""
+    per_factor = W * 1026 + 6 * (18 * W * W - 18 * W) + 18 * W + 27 * W
+    imu = (W - 1) * (450 * 29 + 900 * 29 + 30 * 29 + 15 * 29 + 29)
+    return F * per_factor + imu
 
 
 def aggregate(dt, steps, world, dev):

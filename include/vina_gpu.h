@@ -330,8 +330,9 @@ int vg_shard_host(vg_ctx* ctx, int rank, int world, vg_host_allreduce_fn fn, voi
  * (n > 1) time k_ba_solve on every n-th BA run only; bit 2 (4): in-kernel
  * clocks of k_iekf and k_ba_solve (the device's constant-rate wall clock read
  * inside the kernels: kernel-only time of the executed launches, graph replays
- * included, no events in the stream), read as stages 16 (k_iekf) and 17
- * (k_ba_solve).
+ * included, no events in the stream), read as stages 16 (k_iekf), 17
+ * (k_ba_solve), 18 (the recut's level kernels k_rc_level0 + k_rc_level, one
+ * span per scan) and 19 (k_ba_hess), over the last <= 64 scans.
  * vg_profile resets the accumulators; vg_profile_read returns total ms and the
  * number of intervals. */
 int vg_profile(vg_ctx* ctx, int on);

@@ -177,22 +177,39 @@ __device__ __forceinline__ void factor_frame(const double* e, const Clu& pa, con
       A(r, 3 + c) = A2(r, c) / NN;
     }
   V6 jjt = mul(tr(A), uk);
-  M3 HRt = scl(outer3(viRiTuk, uk), 2.0 / NN * (1.0 - ni / NN));
-  M6 Hb = mul(mul(tr(A), umumT), A);
-  M3 c00 = sub(sub(scl(mul(sub(combo1, mul(RiTukhat, Pi)), RiTukhat), 2.0 / NN),
-                   scl(outer3(viRiTuk, viRiTuk), 2.0 / NN / NN)),
-               scl(hat(v3(jjt[0], jjt[1], jjt[2])), 0.5));
-  M3 c11 = scl(ukukT, 2.0 / NN * (ni - ni * ni / NN));
-  for (int r = 0; r < 3; r++)
-    for (int c = 0; c < 3; c++) {
-      Hb(r, c) += c00(r, c);
-      Hb(r, 3 + c) += HRt(r, c);
-      Hb(3 + r, c) += HRt(c, r);
-      Hb(3 + r, 3 + c) += c11(r, c);
-    }
+  // Hb = (A^T umumT) A + the corrections, only the lower triangle the output
+  // keeps: every entry formed exactly as the full products form it (same
+  // terms, same order), the upper 15 entries and their registers skipped
+  // (the full 6x6 pushed k_ba_hess past 256 VGPRs: 50 spilled)
+  M<6, 3> AtU = mul(tr(A), umumT);
+  const double s2n = 2.0 / NN * (1.0 - ni / NN);  // HRt's scale
+  const double c00s = 2.0 / NN, c00v = 2.0 / NN / NN;
+  const double c11s = 2.0 / NN * (ni - ni * ni / NN);
+  M3 L1;  // combo1 - RiTukhat Pi (c00's left factor, full: its rows meet RiTukhat's columns)
+  {
+    const M3 RP = mul(RiTukhat, Pi);
+    for (int t = 0; t < 9; t++) L1[t] = combo1[t] - RP[t];
+  }
   int q = 0;
   for (int r = 0; r < 6; r++)
-    for (int c = 0; c <= r; c++) hb[q++] = Hb(r, c);
+    for (int c = 0; c <= r; c++) {
+      double v = AtU(r, 0) * A(0, c);
+      v += AtU(r, 1) * A(1, c);
+      v += AtU(r, 2) * A(2, c);
+      if (r < 3) {  // c00 = ((L1 RiTukhat) * 2/NN - (viRiTuk viRiTuk^T) * 2/NN/NN) - hat(jjt[0..3]) * 0.5
+        double m = L1(r, 0) * RiTukhat(0, c);
+        m += L1(r, 1) * RiTukhat(1, c);
+        m += L1(r, 2) * RiTukhat(2, c);
+        const V3 jt = v3(jjt[0], jjt[1], jjt[2]);
+        const double hj = r == c ? 0.0 : (r == 1 ? (c == 0 ? jt[2] : 0.0) : (c == 0 ? -jt[1] : jt[0]));
+        v += (m * c00s - (viRiTuk[r] * viRiTuk[c]) * c00v) - hj * 0.5;
+      } else if (c < 3) {  // HRt(c, r - 3) (the lower off-diagonal block)
+        v += (viRiTuk[c] * uk[r - 3]) * s2n;
+      } else {
+        v += ukukT(r - 3, c - 3) * c11s;
+      }
+      hb[q++] = v;
+    }
   for (int k = 0; k < 6; k++) jjt_o[k] = jjt[k];
   const V3 u1 = v3(e[3 + 0 * 3 + 1], e[3 + 1 * 3 + 1], e[3 + 2 * 3 + 1]);
   const V3 u2 = v3(e[3 + 0 * 3 + 2], e[3 + 1 * 3 + 2], e[3 + 2 * 3 + 2]);
@@ -239,23 +256,24 @@ __device__ __forceinline__ void hess_chunk_eval(int ch, int nf, int W, const int
   const bool active = f < FS;
   const int a_begin = ch * hess_chunk(W);
   const int a_end = min(nf, a_begin + hess_chunk(W));
-  double hb[21], jj[6], res = 0.0;
-  for (int k = 0; k < 21; k++) hb[k] = 0.0;
-  for (int k = 0; k < 6; k++) jj[k] = 0.0;
   const int ntl = NT * (NT + 1) / 2;
-  v4d acc[4];  // <= 15 lower tiles (W <= 11) over the 8 waves (<= 2 per wave; 4 slots)
-  for (int s = 0; s < 4; s++) acc[s] = v4d{0.0, 0.0, 0.0, 0.0};
-  for (int sub = a_begin; sub < a_end; sub += FS) {
-    for (int t = tid; t < KS * XS; t += kHessThreads) X[t] = 0.0;
-    for (int t = tid; t < KS; t += kHessThreads) S[t] = 0.0;
-    __syncthreads();
-    const int a = sub + f;
+  // A chunk is one sub-chunk (hess_chunk == hess_fs): the lane's factor_frame
+  // writes its diagonal block and gradient straight into hb / jj (0 + coe x,
+  // the accumulation's value), so no second copy is live beside the call
+  // (it was: 256 VGPRs and ~50 spilled, scratch traffic ~5x the kernel's bytes)
+  for (int t = tid; t < KS * XS; t += kHessThreads) X[t] = 0.0;
+  for (int t = tid; t < KS; t += kHessThreads) S[t] = 0.0;
+  __syncthreads();
+  double hb[21], jj[6], res = 0.0;
+  {
+    const int a = a_begin + f;
+    bool got = false;
     if (active && a < a_end) {
       const double* e = &fac_eig[(size_t)a * 12];
       const Clu pa = fac_pcr[a];
       const double coe = 1.0;  // octree.cpp:507
       if (i == 0) {
-        res += coe * e[0];
+        res = 0.0 + coe * e[0];
         const double NN = (double)pa.N;
         S[3 * f + 0] = coe * (2.0 / (e[0] - e[1]));
         S[3 * f + 1] = coe * (2.0 / (e[0] - e[2]));
@@ -263,35 +281,41 @@ __device__ __forceinline__ void hess_chunk_eval(int ch, int nf, int W, const int
       }
       const Clu sc = pcrs[(size_t)fac_node[a] * W + mpring[i]];
       if (sc.N != 0) {
-        double hbi[21], jji[6], g1[6], g2[6], h[6];
-        factor_frame(e, pa, sc, &xs[(size_t)i * kX], hbi, jji, g1, g2, h);
-        for (int k = 0; k < 21; k++) hb[k] += coe * hbi[k];
-        for (int k = 0; k < 6; k++) jj[k] += coe * jji[k];
+        double g1[6], g2[6], h[6];
+        factor_frame(e, pa, sc, &xs[(size_t)i * kX], hb, jj, g1, g2, h);
+        for (int k = 0; k < 21; k++) hb[k] = 0.0 + coe * hb[k];
+        for (int k = 0; k < 6; k++) jj[k] = 0.0 + coe * jj[k];
         double* x0 = &X[(size_t)(3 * f) * XS + 6 * i];
         for (int k = 0; k < 6; k++) {
           x0[k] = g1[k];
           x0[XS + k] = g2[k];
           x0[2 * XS + k] = h[k];
         }
+        got = true;
       }
     }
-    __syncthreads();
-    for (int q = wave, slot = 0; q < ntl; q += kHessThreads / 64, slot++) {
-      int TI = 0;
-      while ((TI + 1) * (TI + 2) / 2 <= q) TI++;
-      const int TJ = q - TI * (TI + 1) / 2;
-      const int cc = lane & 15, rq = lane >> 4;
-      v4d c = acc[slot];
-      for (int k0 = 0; k0 < KS; k0 += 4) {
-        const int k = k0 + rq;
-        const double av = S[k] * X[(size_t)k * XS + 16 * TI + cc];
-        const double bv = X[(size_t)k * XS + 16 * TJ + cc];
-        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c, 0, 0, 0);
-      }
-      acc[slot] = c;
+    if (!got) {
+      for (int k = 0; k < 21; k++) hb[k] = 0.0;
+      for (int k = 0; k < 6; k++) jj[k] = 0.0;
     }
-    __syncthreads();
   }
+  __syncthreads();
+  v4d acc[4];  // <= 15 lower tiles (W <= 11) over the 8 waves (<= 2 per wave; 4 slots)
+  for (int q = wave, slot = 0; q < ntl; q += kHessThreads / 64, slot++) {
+    int TI = 0;
+    while ((TI + 1) * (TI + 2) / 2 <= q) TI++;
+    const int TJ = q - TI * (TI + 1) / 2;
+    const int cc = lane & 15, rq = lane >> 4;
+    v4d c = v4d{0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < KS; k0 += 4) {
+      const int k = k0 + rq;
+      const double av = S[k] * X[(size_t)k * XS + 16 * TI + cc];
+      const double bv = X[(size_t)k * XS + 16 * TJ + cc];
+      c = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, c, 0, 0, 0);
+    }
+    acc[slot] = c;
+  }
+  __syncthreads();
   double* out = &part[(size_t)ch * nout];
   // off-diagonal blocks from the MFMA tiles (diagonal 6x6 blocks come from Hb)
   for (int q = wave, slot = 0; q < ntl; q += kHessThreads / 64, slot++) {
@@ -335,6 +359,13 @@ __device__ __forceinline__ void hess_chunk_eval(int ch, int nf, int W, const int
 
 // The factor count is read on the device (*nfp): workgroups [0, G) loop over
 // the chunks (chunk c -> partial c, whatever G), G + k evaluates IMU factor k.
+__device__ __forceinline__ void hess_body(const int* __restrict__ nfp, int W, const int* __restrict__ fac_node,
+                                          const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
+                                          const Clu* __restrict__ pcrs, const int* __restrict__ mpring,
+                                          const double* __restrict__ xs, double* __restrict__ part,
+                                          const BaState* __restrict__ st, int G, int nimu,
+                                          const double* __restrict__ imurec, const int* __restrict__ imu_head,
+                                          const double* __restrict__ bias, double* __restrict__ imuout);
 __global__ void __launch_bounds__(kHessThreads) k_ba_hess(const int* __restrict__ nfp, int W,
                                                           const int* __restrict__ fac_node,
                                                           const double* __restrict__ fac_eig,
@@ -343,8 +374,30 @@ __global__ void __launch_bounds__(kHessThreads) k_ba_hess(const int* __restrict_
                                                           double* __restrict__ part, const BaState* __restrict__ st,
                                                           int G, int nimu, const double* __restrict__ imurec,
                                                           const int* __restrict__ imu_head,
-                                                          const double* __restrict__ bias, double* __restrict__ imuout) {
+                                                          const double* __restrict__ bias, double* __restrict__ imuout,
+                                                          KClock* __restrict__ clk) {
   if (st->done || !st->calc_hess) return;
+  // in-kernel clock (vg_profile bit 2): slot (scan, LM iteration), start by
+  // workgroup 0, every workgroup's end (KClock h_*)
+  const bool clk_on = clk && clk->on;
+  const int clk_slot = clk_on ? (clk->scan * 8 + (st->iters < 7 ? st->iters : 7)) & (kClkHRing - 1) : 0;
+  if (clk_on && blockIdx.x == 0 && threadIdx.x == 0) {
+    clk->h_t0[clk_slot] = (unsigned long long)wall_clock64();
+    clk->h_exec[clk_slot] = 1;
+  }
+  hess_body(nfp, W, fac_node, fac_eig, fac_pcr, pcrs, mpring, xs, part, st, G, nimu, imurec, imu_head, bias, imuout);
+  if (clk_on && blockIdx.x < kClkHBlocks) {
+    __syncthreads();
+    if (threadIdx.x == 0) clk->h_tend[clk_slot][blockIdx.x] = (unsigned long long)wall_clock64();
+  }
+}
+__device__ __forceinline__ void hess_body(const int* __restrict__ nfp, int W, const int* __restrict__ fac_node,
+                                          const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
+                                          const Clu* __restrict__ pcrs, const int* __restrict__ mpring,
+                                          const double* __restrict__ xs, double* __restrict__ part,
+                                          const BaState* __restrict__ st, int G, int nimu,
+                                          const double* __restrict__ imurec, const int* __restrict__ imu_head,
+                                          const double* __restrict__ bias, double* __restrict__ imuout) {
   if ((int)blockIdx.x >= G) {  // IMU factors ride in the same launch (give_evaluate, jac_enable)
     const int k = blockIdx.x - G;
     if (k < nimu) imu_factor_block(k, imurec, *imu_head, bias, xs, imuout);
@@ -1303,7 +1356,7 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr) {
   if (!sharded && ctx->ba_fuse_ctl) ctl_fused.err = ctx->map.counters + kCntErr;
   k_ba_hess<<<G + nimu, kHessThreads, hess_lds, s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
                                                     ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, nimu, d.imurec, &ctx->st->imu_head,
-                                                    d.bias, d.imuout);
+                                                    d.bias, d.imuout, &ctx->st->clk);
   k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, sharded ? hl_part : d.hl,
                                                        d.st);
   // sharded: every shard's factors -> one LiDAR Hessian / gradient / residual
@@ -1570,7 +1623,7 @@ int ba_lidar_pass(vg_ctx* ctx, bool hessian, const double* poses, const int* mp_
     const int G = std::min(kHessGridMax, ctx->ba.cap_f / hess_chunk(W) + 1);
     k_ba_hess<<<G, kHessThreads, hess_lds_bytes(W), s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
                                                         ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, 0, d.imurec,
-                                                        &ctx->st->imu_head, d.bias, d.imuout);
+                                                        &ctx->st->imu_head, d.bias, d.imuout, nullptr);
     k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, d.hl, d.st);
     VG_HIP(hipGetLastError());
     VG_HIP(hipMemcpyAsync(h, d.hl, nout * sizeof(double), hipMemcpyDeviceToHost, s));

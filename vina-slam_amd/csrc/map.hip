@@ -2175,13 +2175,41 @@ __device__ __forceinline__ void rc_visit_chunk(int L, const int* __restrict__ wo
 }
 
 constexpr int kRcFusedWaves = 4;
+// in-kernel clock of the recut's level kernels (KClock rc_*, vg_profile bit 2)
+__device__ __forceinline__ void rc_clock_start(KClock* clk) {
+  if (clk && clk->on && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int slot = clk->scan & (kClkRcScans - 1);
+    clk->rc_t0[slot] = (unsigned long long)wall_clock64();
+    clk->rc_exec[slot] = 1;
+  }
+}
+__device__ __forceinline__ void rc_clock_end(KClock* clk) {
+  if (clk && clk->on && blockIdx.x < kClkRcBlocks) {
+    __syncthreads();
+    if (threadIdx.x == 0) clk->rc_tend[clk->scan & (kClkRcScans - 1)][blockIdx.x] = (unsigned long long)wall_clock64();
+  }
+}
+__device__ __forceinline__ void rc_level0_body(int thread_num, const MP& mp, DevMap& m, int* __restrict__ next,
+                                               int* __restrict__ sub, int* __restrict__ cand, int* __restrict__ rc,
+                                               uint32_t* __restrict__ cand_bits, const WinD* __restrict__ win,
+                                               uint64_t* __restrict__ ev, int* __restrict__ rcinfo, int cap);
+// clk_end: this launch ends the scan's recut levels (max_layer 0)
 __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level0(int thread_num, MP mp, DevMap m,
                                                                   int* __restrict__ next, int* __restrict__ sub,
                                                                   int* __restrict__ cand, int* __restrict__ rc,
                                                                   uint32_t* __restrict__ cand_bits,
                                                                   const WinD* __restrict__ win,
                                                                   uint64_t* __restrict__ ev,
-                                                                  int* __restrict__ rcinfo, int cap) {
+                                                                  int* __restrict__ rcinfo, int cap, KClock* clk,
+                                                                  int clk_end) {
+  rc_clock_start(clk);
+  rc_level0_body(thread_num, mp, m, next, sub, cand, rc, cand_bits, win, ev, rcinfo, cap);
+  if (clk_end) rc_clock_end(clk);
+}
+__device__ __forceinline__ void rc_level0_body(int thread_num, const MP& mp, DevMap& m, int* __restrict__ next,
+                                               int* __restrict__ sub, int* __restrict__ cand, int* __restrict__ rc,
+                                               uint32_t* __restrict__ cand_bits, const WinD* __restrict__ win,
+                                               uint64_t* __restrict__ ev, int* __restrict__ rcinfo, int cap) {
   if (blockIdx.x == 0 && threadIdx.x == 0) rc[kRcNode0] = m.counters[kCntNodes];  // k_rc_level(0)'s id base
   if (rc[kRcAbort]) return;
   if (g_slide(m) < thread_num) return;  // local_mapping.cpp:150-154 (global count)
@@ -2196,8 +2224,23 @@ __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level0(int thread_num
     rc_visit_chunk(0, m.slide, nw, j, mp, m, next, sub, cand, rc, cand_bits, do_win, win, ev, rcinfo, cap);
 }
 
+__device__ __forceinline__ void rc_level_body(
+    int L, int sub_cap, const MP& mp, DevMap& m, const int* __restrict__ sub_in, const int* __restrict__ info_in,
+    const uint64_t* __restrict__ ev_in, int* __restrict__ next, int* __restrict__ next2, int* __restrict__ sub_out,
+    int* __restrict__ cand, int* __restrict__ rc, uint32_t* __restrict__ cand_bits, const WinD* __restrict__ win,
+    uint64_t* __restrict__ ev_out, int* __restrict__ info_out, int cap);
+// clk_end: the scan's last level kernel (its workgroups stamp the recut's end)
 __global__ void __launch_bounds__(64 * kRcFusedWaves) k_rc_level(
     int L, int sub_cap, MP mp, DevMap m, const int* __restrict__ sub_in, const int* __restrict__ info_in,
+    const uint64_t* __restrict__ ev_in, int* __restrict__ next, int* __restrict__ next2, int* __restrict__ sub_out,
+    int* __restrict__ cand, int* __restrict__ rc, uint32_t* __restrict__ cand_bits, const WinD* __restrict__ win,
+    uint64_t* __restrict__ ev_out, int* __restrict__ info_out, int cap, KClock* clk, int clk_end) {
+  rc_level_body(L, sub_cap, mp, m, sub_in, info_in, ev_in, next, next2, sub_out, cand, rc, cand_bits, win, ev_out,
+                info_out, cap);
+  if (clk_end) rc_clock_end(clk);
+}
+__device__ __forceinline__ void rc_level_body(
+    int L, int sub_cap, const MP& mp, DevMap& m, const int* __restrict__ sub_in, const int* __restrict__ info_in,
     const uint64_t* __restrict__ ev_in, int* __restrict__ next, int* __restrict__ next2, int* __restrict__ sub_out,
     int* __restrict__ cand, int* __restrict__ rc, uint32_t* __restrict__ cand_bits, const WinD* __restrict__ win,
     uint64_t* __restrict__ ev_out, int* __restrict__ info_out, int cap) {
@@ -2667,16 +2710,20 @@ static int map_recut_impl(vg_ctx* ctx, const MP& mp, const WinArg& wa, int threa
   }
   const int nlev = mp.max_layer + 1;  // children sit one layer down; leaves at max_layer do not subdivide
   auto list_of = [&](int L) { return (L % 2 == 1) ? w.list0 : w.list1; };  // worklist of level L >= 1
-  const int gv = 256, gw = grid_for(total > 0 ? total : 1, kBlock, 2048);  // grid-stride over the device total
+  constexpr int gv = 256;
+  const int gw = grid_for(total > 0 ? total : 1, kBlock, 2048);  // grid-stride over the device total
   const int sub_cap = (ctx->dbg_apply_cap >= 0 && ctx->dbg_apply_cap < kApplySub) ? ctx->dbg_apply_cap : kApplySub;
   uint32_t* bits = pub_seq > 0 ? w.cand_bits : nullptr;
   if (ctx->rc_fused) {  // one launch per level boundary (k_rc_level0, k_rc_level)
+    static_assert(gv <= kClkRcBlocks, "recut clock slots");
     k_rc_level0<<<gv, 64 * kRcFusedWaves, 0, s>>>(thread_num, mp, m, list_of(1), sub_of(w, 0), w.cand, w.rc, bits,
-                                                 dwin, ev_of(w, 0), info_of(w, 0), w.cap);
+                                                 dwin, ev_of(w, 0), info_of(w, 0), w.cap, &ctx->st->clk,
+                                                 mp.max_layer == 0 ? 1 : 0);
     for (int L = 0; L < mp.max_layer; L++)
       k_rc_level<<<gv, 64 * kRcFusedWaves, 0, s>>>(L, sub_cap, mp, m, sub_of(w, L), info_of(w, L), ev_of(w, L),
                                                   list_of(L + 1), list_of(L + 2), sub_of(w, L + 1), w.cand, w.rc,
-                                                  bits, dwin, ev_of(w, L + 1), info_of(w, L + 1), w.cap);
+                                                  bits, dwin, ev_of(w, L + 1), info_of(w, L + 1), w.cap, &ctx->st->clk,
+                                                  L == mp.max_layer - 1 ? 1 : 0);
   } else {
     for (int L = 0; L < nlev; L++) {
       k_rc_visit<<<gv * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(L, thread_num, L > 0 ? list_of(L) : nullptr, mp, m,
@@ -2856,8 +2903,33 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
                                                     const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
                                                     int* __restrict__ plan, const int* __restrict__ gate,
                                                     unsigned* __restrict__ head_flag, int batch,
-                                                    const int* __restrict__ dseq) {
+                                                    const int* __restrict__ dseq, const unsigned* __restrict__ pre_flag) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
+  if (pre_flag && blockIdx.x > 0) {  // the scan graph: the leaves read the margi prefix's lists (d_sync[4] >= ph[4])
+    // Normally the prefix ended long before (it runs under the LM): its
+    // writes were released at its end and this kernel's start acquired them,
+    // so no fence. Only a workgroup that had to wait acquires after the wait
+    // (an agent-scope acquire per workgroup invalidates the XCD's L2: with
+    // ~2k workgroups that cost the kernel 14 us when every one did it)
+    __shared__ int s_state;  // 0 ready at once, 1 waited, 2 timed out
+    if (threadIdx.x == 0) {
+      const unsigned t = (unsigned)st->ph[4];
+      int state = 0;
+      for (long it = 0; (int)(__hip_atomic_load(pre_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - t) < 0; it++) {
+        state = 1;
+        __builtin_amdgcn_s_sleep(4);
+        if (it > (1l << 24)) {
+          state = 2;
+          atomicOr(&m.counters[kCntErr], 64);
+          break;
+        }
+      }
+      s_state = state;
+    }
+    __syncthreads();
+    if (s_state == 2) return;
+    if (s_state == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
   if (blockIdx.x == 0) {  // the margi head: x_curr <- x_buf.back(), the window view, the state publication
     if (dseq) {  // the scan graph: this scan's publication numbers from the device state (DState::ph)
       seq = dseq[0];
@@ -3335,7 +3407,7 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   k_margi_leaf<<<1 + 512 * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(
       m.counters + kCntLeaves, w.list0, mp, wa2, ctx->st, dwin, dn, dn + 32, bi != nullptr, bi,
       bi ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, pub_seq, m, ctx->ba.fac_eig, ctx->ba.fac_pcr, w.plan, gate,
-      flags ? ctx->d_sync + 2 : nullptr, ctx->margi_batch ? 1 : 0, nullptr);
+      flags ? ctx->d_sync + 2 : nullptr, ctx->margi_batch ? 1 : 0, nullptr, nullptr);
   VG_HIP(hipEventRecord(ctx->ev_tail_a, s));
   // the margi's publication number into the IEKF hand-off flag: by the margi
   // graph's first kernel (k_margi_copy) — or k_sync_set when the local map
@@ -3382,7 +3454,8 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
 // The margi tail inside the scan graph (pipeline.cpp stage_insert_recut),
 // captured on the context stream behind the first two LM iterations: gated on
 // the LM's `fin` like a speculative tail; the margi prefix (second stream) is
-// waited for on a device flag (d_sync[4] >= DState::ph[4]); the publication
+// waited for on a device flag (d_sync[4] >= DState::ph[4], by k_margi_leaf's
+// leaf workgroups: no polling kernel in front); the publication
 // numbers come from DState::ph; the ring (wa) is the graph's own.
 int map_margi_tail_capture(vg_ctx* ctx, const MP& mp, const WinArg& wa) {
   DevMap& m = ctx->map;
@@ -3393,11 +3466,10 @@ int map_margi_tail_capture(vg_ctx* ctx, const MP& mp, const WinArg& wa) {
   int* dn = (int*)((char*)ctx->ba.xs + sizeof(WinD));
   const int* gate = ba_gate_dev(ctx);
   const int thread_num = ctx->cfg.thread_num;
-  VG_TRY(sync_wait_dev(ctx, s, 4, &ctx->st->ph[4], gate));
   k_margi_leaf<<<1 + 512 * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(
       m.counters + kCntLeaves, w.list0, mp, wa, ctx->st, dwin, dn, dn + 32, 1, ba_iters_dev(ctx), ba_hess_dev(ctx),
       ctx->d_pub, 0, m, ctx->ba.fac_eig, ctx->ba.fac_pcr, w.plan, gate, ctx->d_sync + 2, ctx->margi_batch ? 1 : 0,
-      &ctx->st->ph[1]);
+      &ctx->st->ph[1], ctx->d_sync + 4);
   k_margi_copy<<<256, 64 * kCopyWaves, 0, s>>>(m.counters + kCntLeaves, w.plan, dwin, m, gate, w.list0,
                                                 ctx->margi_fused ? 1 : 0, ctx->d_sync, ctx->st);
   if (ctx->margi_fused) {

@@ -69,12 +69,14 @@ __global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict
 // host's propagate() in pipeline.cpp, same expression trees) from the device's
 // x_curr, then the scan opening (k_scan_begin). One workgroup: the per-sample
 // rotations (Exp, the sin / cos) in parallel, the rotation / velocity /
-// position chain on wave 0 (one lane per matrix / vector entry, rows by
-// shuffle), the F / noise blocks of each sample in parallel, then
-// cov <- F cov F^T + Q sample by sample, one lane per entry, each sum in
-// ascending column order over F's non-zeros (the host's sandwich()). The
-// round-4 first form (the chain on one lane, per-lane index arrays for F's
-// rows) took 54 us: 11 us chain, 37 us covariance (scripts/probe_prop.py).
+// position chain on one lane in registers (inputs loaded a step ahead), the F
+// / noise blocks of each sample in parallel, then cov <- F cov F^T + Q sample
+// by sample, one lane per entry, each sum in ascending column order over F's
+// non-zeros (the host's sandwich()), one wave per row (column) group so that
+// every wave runs one row shape. Round 4's forms: the chain on one lane with
+// per-lane index arrays for F's rows 54 us (11 chain, 37 covariance); the chain
+// on wave 0 by shuffles and 256 lanes of mixed shapes 32 us (8.3 chain, 16.4
+// covariance, scripts/probe_prop.py).
 // Hand-offs inside the kernel (the split IEKF stream, pipeline.cpp): the
 // per-sample rotations need only the biases, final since the previous scan's
 // IEKF, so they run before the margi head's flag (head_flag >= head_target:
@@ -89,11 +91,12 @@ __device__ __forceinline__ bool flag_wait(const unsigned* flag, unsigned target)
   }
   return true;
 }
-__global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restrict__ st, const float* x, const float* y,
-                                                   const float* z, int n, int set_scan,
-                                                   const unsigned* __restrict__ head_flag, unsigned head_target,
-                                                   const unsigned* __restrict__ leaf_flag, unsigned leaf_target,
-                                                   int* __restrict__ err) {
+constexpr int kPropThreads = 320;  // five waves: one 3-row (3-column) group of the covariance each
+__global__ void __launch_bounds__(kPropThreads) k_scan_prop(PropArg arg, DState* __restrict__ st, const float* x,
+                                                            const float* y, const float* z, int n, int set_scan,
+                                                            const unsigned* __restrict__ head_flag, unsigned head_target,
+                                                            const unsigned* __restrict__ leaf_flag, unsigned leaf_target,
+                                                            int* __restrict__ err) {
   // the arguments once into LDS, by all lanes (the kernel-argument block is
   // host memory: the serial chain below would pay a round trip per sample)
   __shared__ PropArg a;
@@ -108,6 +111,7 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
   VG_PROBE_MARK(1);
   __shared__ double sExp[kPropMax][9], sF00[kPropMax][9], sRi[kPropMax][9], sAsk[kPropMax][9];
   __shared__ double sF60[kPropMax][9], sF612[kPropMax][9], sCw[kPropMax][9], sDt[kPropMax];
+  __shared__ double sAa[kPropMax][3], sAng[kPropMax][3];
   __shared__ int sOk[kPropMax];
   __shared__ double C[225], A[225];
   const int tid = threadIdx.x;
@@ -135,6 +139,10 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
       sF00[tid][q] = f[q];
       sAsk[tid][q] = k[q];
     }
+    for (int q = 0; q < 3; q++) {
+      sAa[tid][q] = acc_avr[q];
+      sAng[tid][q] = angvel[q];
+    }
     sDt[tid] = dt;
     sOk[tid] = ok ? 1 : 0;
   }
@@ -153,70 +161,81 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
   }
   __syncthreads();
   VG_PROBE_MARK(2);
-  // 2. the rotation / velocity / position chain on wave 0: lane 3r+c holds
-  // R_imu(r, c), lanes 9-11 the position, 12-14 the velocity; each lane forms
-  // the acceleration component it needs from its row (the host's mul() tree)
-  __shared__ double sTail[24];
-  if (tid < 64) {
-    const int l = tid;
-    const bool isR = l < 9;
-    const int rr = isR ? l / 3 : 0, cc = l % 3;
-    const int ci = l < 9 ? rr : (l < 12 ? l - 9 : (l < 15 ? l - 12 : 0));  // its component of acc_imu / angvel
-    double Rv = isR ? xc[l] : 0.0;
-    double pv = (l >= 9 && l < 12) ? xc[9 + l - 9] : 0.0;
-    double vv = (l >= 12 && l < 15) ? xc[12 + l - 12] : 0.0;
-    const double gci = xc[21 + ci], bgc = bg[ci];
-    double acc_last = 0.0, ang_last = 0.0;
-    for (int k = 0; k < ns; k++) {
-      if (!sOk[k]) continue;  // uniform
-      const double* h = &a.imu[7 * k];
-      const double* t = &a.imu[7 * (k + 1)];
-      double aa[3];
-      for (int j2 = 0; j2 < 3; j2++) aa[j2] = 0.5 * (h[4 + j2] + t[4 + j2]) * a.sg - ba[j2];
-      const double r0 = __shfl(Rv, 3 * ci, 64), r1 = __shfl(Rv, 3 * ci + 1, 64), r2 = __shfl(Rv, 3 * ci + 2, 64);
-      double s = r0 * aa[0];
-      s += r1 * aa[1];
-      s += r2 * aa[2];
-      const double acc = s + gci;  // acc_imu[ci] = (R_imu acc_avr)[ci] + g[ci]
-      if (isR) sRi[k][l] = Rv;
-      const double dt = sDt[k];
-      const double velc = __shfl(vv, 12 + ci, 64);  // vel[ci] before this pair's update
-      if (l >= 9 && l < 12) pv = (pv + velc * dt) + acc * (0.5 * dt * dt);
-      if (l >= 12 && l < 15) vv = vv + acc * dt;
-      const double q0 = __shfl(Rv, 3 * rr, 64), q1 = __shfl(Rv, 3 * rr + 1, 64), q2 = __shfl(Rv, 3 * rr + 2, 64);
-      if (isR) {  // R_imu <- R_imu Exp(angvel, dt)
-        double s2 = q0 * sExp[k][cc];
-        s2 += q1 * sExp[k][3 + cc];
-        s2 += q2 * sExp[k][6 + cc];
-        Rv = s2;
+  // 2. the rotation / velocity / position chain on one lane, everything in
+  // registers, the next pair's inputs loaded one step ahead (the host's mul /
+  // add / scl trees term for term; the wave-0 form with one entry per lane
+  // paid a shuffle round trip per dependent step: 8.3 us)
+  if (tid < 225) C[tid] = xc[kXS + tid];  // (cov: final since the previous scan's IEKF)
+  if (tid == 0) {
+    double R[9], p[3], v[3], g[3];
+    for (int q = 0; q < 9; q++) R[q] = xc[q];
+    for (int j = 0; j < 3; j++) {
+      p[j] = xc[9 + j];
+      v[j] = xc[12 + j];
+      g[j] = xc[21 + j];
+    }
+    double acc[3] = {0.0, 0.0, 0.0}, ang[3] = {0.0, 0.0, 0.0};
+    double nE[9], nA[3], nG[3], ndt = 0.0;
+    int nok = 0;
+    auto load = [&](int k) {
+      for (int q = 0; q < 9; q++) nE[q] = sExp[k][q];
+      for (int q = 0; q < 3; q++) {
+        nA[q] = sAa[k][q];
+        nG[q] = sAng[k][q];
       }
-      ang_last = 0.5 * (h[1 + ci] + t[1 + ci]) - bgc;
-      acc_last = acc;
+      ndt = sDt[k];
+      nok = sOk[k];
+    };
+    if (ns > 0) load(0);
+    for (int k = 0; k < ns; k++) {
+      double E[9], aa[3], an[3];
+      for (int q = 0; q < 9; q++) E[q] = nE[q];
+      for (int q = 0; q < 3; q++) {
+        aa[q] = nA[q];
+        an[q] = nG[q];
+      }
+      const double dt = ndt;
+      const int ok = nok;
+      if (k + 1 < ns) load(k + 1);
+      if (!ok) continue;
+      for (int i = 0; i < 3; i++) {  // acc_imu = R_imu acc_avr + g
+        double t = R[3 * i] * aa[0];
+        t += R[3 * i + 1] * aa[1];
+        t += R[3 * i + 2] * aa[2];
+        acc[i] = t + g[i];
+      }
+      for (int q = 0; q < 9; q++) sRi[k][q] = R[q];
+      const double hdt2 = 0.5 * dt * dt;
+      for (int j = 0; j < 3; j++) {
+        p[j] = (p[j] + v[j] * dt) + acc[j] * hdt2;
+        v[j] = v[j] + acc[j] * dt;
+        ang[j] = an[j];
+      }
+      double Rn[9];
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+          double t = R[3 * i] * E[j];
+          t += R[3 * i + 1] * E[3 + j];
+          t += R[3 * i + 2] * E[6 + j];
+          Rn[3 * i + j] = t;
+        }
+      for (int q = 0; q < 9; q++) R[q] = Rn[q];
     }
-    if (isR) sTail[l] = Rv;
-    if (l >= 9 && l < 12) sTail[l] = pv;
-    if (l >= 12 && l < 15) sTail[l] = vv;
-    if (l < 3) {
-      sTail[15 + l] = acc_last;
-      sTail[18 + l] = ang_last;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (l == 0 && a.n > 0) {  // imu_ekf.cpp:81-86
-      const M3 R_imu = ld_m3(sTail);
-      const V3 pos = v3(sTail[9], sTail[10], sTail[11]), vel = v3(sTail[12], sTail[13], sTail[14]);
-      const V3 acc_imu = v3(sTail[15], sTail[16], sTail[17]), angvel = v3(sTail[18], sTail[19], sTail[20]);
+    if (a.n > 0) {  // imu_ekf.cpp:81-86
+      M3 R_imu;
+      for (int q = 0; q < 9; q++) R_imu[q] = R[q];
+      const V3 pos = v3(p[0], p[1], p[2]), vel = v3(v[0], v[1], v[2]);
+      const V3 acc_imu = v3(acc[0], acc[1], acc[2]), angvel = v3(ang[0], ang[1], ang[2]);
       const double tb = a.imu[7 * (a.n - 1)];
       const double note = a.end > tb ? 1.0 : -1.0;
       const double dt = note * (a.end - tb);
-      const V3 v = add(vel, scl(acc_imu, note * dt));
-      const M3 R = mul(R_imu, Exp(scl(angvel, note), dt));
-      const V3 p = add(add(pos, scl(vel, note * dt)), scl(acc_imu, note * 0.5 * dt * dt));
-      for (int q = 0; q < 9; q++) st->xc[q] = R[q];
+      const V3 vv = add(vel, scl(acc_imu, note * dt));
+      const M3 Rr = mul(R_imu, Exp(scl(angvel, note), dt));
+      const V3 pp = add(add(pos, scl(vel, note * dt)), scl(acc_imu, note * 0.5 * dt * dt));
+      for (int q = 0; q < 9; q++) st->xc[q] = Rr[q];
       for (int j2 = 0; j2 < 3; j2++) {
-        st->xc[9 + j2] = p[j2];
-        st->xc[12 + j2] = v[j2];
+        st->xc[9 + j2] = pp[j2];
+        st->xc[12 + j2] = vv[j2];
       }
     }
   }
@@ -236,12 +255,16 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
       sCw[tid][q] = cw[q];
     }
   }
-  const int r = tid / 15, c = tid % 15;
-  if (tid < 225) C[tid] = xc[kXS + tid];
   __syncthreads();
   VG_PROBE_MARK(4);
   // 4. cov = F cov F^T + Q per pair, F's non-zero columns ascending (sandwich()),
-  // the four row shapes of F written out (no per-lane index arrays)
+  // F's four row shapes written out. Wave w takes rows 3w..3w+2 of F C, then
+  // columns 3w..3w+2 of (F C) F^T: every lane of a wave runs the same shape
+  // (the 256-lane form mixed all four shapes in each wave: 16.4 us)
+  const int wv = tid >> 6, ln = tid & 63;
+  const bool act = ln < 45;
+  const int ai = 3 * wv + ln / 15, aj = ln % 15;  // phase A entry (row group wv)
+  const int bi = ln % 15, bj = 3 * wv + ln / 15;  // phase B entry (column group wv)
   auto a_ent = [&](int k, int i, int j) -> double {  // (F C)(i, j)
     const double dt = sDt[k];
     if (i < 3) {
@@ -300,15 +323,11 @@ __global__ void __launch_bounds__(256) k_scan_prop(PropArg arg, DState* __restri
     else if (i == j && i >= 12) q = a.rdw_acc * dt * dt;
     return s + q;
   };
-  // one lane per entry, two workgroup barriers per sample (15.7 us for ~18
-  // samples, r04e probe); the same chain on wave 0 alone, four entries per
-  // lane meeting at wave barriers, took 56.8 us (r04g: the lanes of one wave
-  // then take different row shapes and every shape's code runs for all)
   for (int k = 0; k < ns; k++) {
     if (!sOk[k]) continue;  // uniform
-    if (tid < 225) A[tid] = a_ent(k, r, c);
+    if (act) A[ai * 15 + aj] = a_ent(k, ai, aj);
     __syncthreads();
-    if (tid < 225) C[tid] = o_ent(k, r, c);
+    if (act) C[bi * 15 + bj] = o_ent(k, bi, bj);
     __syncthreads();
   }
   VG_PROBE_MARK(5);
@@ -630,7 +649,7 @@ int state_scan_begin(vg_ctx* ctx, const double* xc249, const float* x, const flo
                      hipStream_t s, const PropArg* prop, const unsigned* head_flag, unsigned head_target,
                      const unsigned* leaf_flag, unsigned leaf_target) {
   if (prop) {
-    k_scan_prop<<<1, 256, 0, s ? s : ctx->stream>>>(*prop, ctx->st, x, y, z, n, x != nullptr ? 1 : 0, head_flag,
+    k_scan_prop<<<1, kPropThreads, 0, s ? s : ctx->stream>>>(*prop, ctx->st, x, y, z, n, x != nullptr ? 1 : 0, head_flag,
                                                     head_target, leaf_flag, leaf_target, ctx->map.counters + kCntErr);
     VG_HIP(hipGetLastError());
     return VG_OK;

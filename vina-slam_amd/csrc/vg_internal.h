@@ -242,12 +242,26 @@ constexpr int kBaImuRec = 64 + 225;  // IMU_PRE record (doubles): deltas, bias J
 // thread 0.
 constexpr int kClkRing = 256;    // k_iekf launch slots: the last 64 scans x 4 iterations
 constexpr int kClkBlocks = 512;  // >= the IEKF grid (iekf_blocks)
+// The recut's level kernels (k_rc_level0 + max_layer x k_rc_level), one span
+// per scan: k_rc_level0's workgroup 0 stamps the start, every workgroup of the
+// last level kernel its end. k_ba_hess: executed launches like k_iekf, slot
+// (scan, LM iteration).
+constexpr int kClkRcScans = 64;   // recut spans of the last 64 scans
+constexpr int kClkRcBlocks = 256; // the level kernels' grid
+constexpr int kClkHRing = 512;    // k_ba_hess slots: 64 scans x 8 LM iterations
+constexpr int kClkHBlocks = 272;  // >= k_ba_hess's grid (chunk workgroups + IMU workgroups)
 struct KClock {
   unsigned long long solve_ticks, solve_n;  // executed k_ba_solve launches
   int on, scan;                             // scans opened since vg_profile (k_scan_begin / k_scan_prop)
   int exec[kClkRing];                       // the slot's k_iekf ran (not a no-op after convergence)
   unsigned long long t0[kClkRing];
   unsigned long long tend[kClkRing][kClkBlocks];
+  int rc_exec[kClkRcScans];
+  unsigned long long rc_t0[kClkRcScans];
+  unsigned long long rc_tend[kClkRcScans][kClkRcBlocks];
+  int h_exec[kClkHRing];
+  unsigned long long h_t0[kClkHRing];
+  unsigned long long h_tend[kClkHRing][kClkHBlocks];
 };
 
 struct DState {

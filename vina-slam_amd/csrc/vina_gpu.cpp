@@ -768,8 +768,10 @@ int vg_profile(vg_ctx* ctx, int on) {
 }
 
 int vg_profile_read(vg_ctx* ctx, int stage, double* total_ms, int* count) {
-  if (!ctx || stage < 0 || stage >= vg::kProfAll + 2 || !total_ms || !count) return VG_E_ARG;
-  if (stage >= vg::kProfAll) {  // 16 k_iekf, 17 k_ba_solve: kernel-only time from the in-kernel clocks
+  if (!ctx || stage < 0 || stage >= vg::kProfAll + 4 || !total_ms || !count) return VG_E_ARG;
+  // 16 k_iekf, 17 k_ba_solve, 18 the recut level kernels (per scan), 19 k_ba_hess:
+  // kernel-only time from the in-kernel clocks
+  if (stage >= vg::kProfAll) {
     VG_TRY(host_sync(ctx));
     std::vector<vg::KClock> kv(1);
     vg::KClock& k = kv[0];
@@ -777,11 +779,41 @@ int vg_profile_read(vg_ctx* ctx, int stage, double* total_ms, int* count) {
     int khz = 0;
     VG_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
     unsigned long long t = k.solve_ticks, nl = k.solve_n;
+    const int s1 = k.scan, s0 = k.scan - 63 > 1 ? k.scan - 63 : 1;  // the last <= 64 scans
+    if (stage == vg::kProfAll + 2) {  // recut level kernels: one span per scan
+      t = 0;
+      nl = 0;
+      for (int sc = s0; sc <= s1; sc++) {
+        const int slot = sc & (vg::kClkRcScans - 1);
+        if (!k.rc_exec[slot]) continue;
+        unsigned long long e = 0;
+        for (int b = 0; b < vg::kClkRcBlocks; b++) e = k.rc_tend[slot][b] > e ? k.rc_tend[slot][b] : e;
+        if (e > k.rc_t0[slot]) {
+          t += e - k.rc_t0[slot];
+          nl++;
+        }
+      }
+    }
+    if (stage == vg::kProfAll + 3) {  // k_ba_hess: the executed launches
+      t = 0;
+      nl = 0;
+      for (int sc = s0; sc <= s1; sc++)
+        for (int it = 0; it < 8; it++) {
+          const int slot = (sc * 8 + it) & (vg::kClkHRing - 1);
+          if (!k.h_exec[slot]) continue;
+          unsigned long long e = 0;
+          for (int b = 0; b < vg::kClkHBlocks; b++) e = k.h_tend[slot][b] > e ? k.h_tend[slot][b] : e;
+          if (e > k.h_t0[slot]) {
+            t += e - k.h_t0[slot];
+            nl++;
+          }
+        }
+    }
     if (stage == vg::kProfAll) {  // k_iekf: the executed launches of the last <= 64 scans
       t = 0;
       nl = 0;
       const int nb = vg::iekf_grid(ctx) < vg::kClkBlocks ? vg::iekf_grid(ctx) : vg::kClkBlocks;
-      const int s1 = k.scan, s0 = k.scan - vg::kClkRing / 4 + 1 > 1 ? k.scan - vg::kClkRing / 4 + 1 : 1;
+      // (s0, s1: kClkRing / 4 = 64 scans)
       for (int sc = s0; sc <= s1; sc++)
         for (int it = 0; it < 4; it++) {
           const int slot = (sc * 4 + it) & (vg::kClkRing - 1);

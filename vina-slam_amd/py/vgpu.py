@@ -421,7 +421,7 @@ class Context:
 
     PROFILE_STAGES = ["downsample", "iekf", "insert", "recut", "ba", "margi", "iekf_total", "ba_solve",
                       "host_propagate", "host_downsample", "host_iekf", "host_push", "host_insert", "host_recut",
-                      "host_ba", "host_margi", "k_iekf_clock", "k_ba_solve_clock"]
+                      "host_ba", "host_margi", "k_iekf_clock", "k_ba_solve_clock", "k_rc_clock", "k_ba_hess_clock"]
 
     def profile(self, on=True, stages=False, every=1, clock=False):
         """on: k_iekf / k_ba_solve launch events (the solve's on every `every`-th
