@@ -14,8 +14,9 @@ import synth  # noqa: E402
 import vgconfig  # noqa: E402
 import vgpu  # noqa: E402
 
-PHASES = {1: "arguments -> LDS", 2: "per-pair Exp / F00", 3: "rotation chain (lane 0)", 4: "F60/F612/noise + cov load",
-          5: "cov sandwich chain", 6: "opening (x_prop, flags)"}
+PHASES = {1: "arguments -> LDS", 2: "per-pair Exp / F00", 7: "wait for the margi head's flag",
+          3: "rotation chain (lane 0)", 4: "F60/F612/noise + cov load", 5: "cov sandwich chain",
+          6: "opening (x_prop, flags)"}
 
 
 def main(nscan=30):

@@ -146,6 +146,7 @@ __global__ void __launch_bounds__(kPropThreads) k_scan_prop(PropArg arg, DState*
     sDt[tid] = dt;
     sOk[tid] = ok ? 1 : 0;
   }
+  VG_PROBE_MARK(2);
   if (head_flag) {  // x_curr.R/p of the previous scan's margi head
     __shared__ int s_late;
     if (tid == 0) s_late = flag_wait(head_flag, head_target) ? 0 : 1;
@@ -160,7 +161,7 @@ __global__ void __launch_bounds__(kPropThreads) k_scan_prop(PropArg arg, DState*
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
-  VG_PROBE_MARK(2);
+  VG_PROBE_MARK(7);
   // 2. the rotation / velocity / position chain on one lane, everything in
   // registers, the next pair's inputs loaded one step ahead (the host's mul /
   // add / scl trees term for term; the wave-0 form with one entry per lane
