@@ -72,6 +72,10 @@ typedef struct vg_config {
    * Mid-360; imu_ekf.cpp:182-185, node.cpp:309). vg_imu_init derives it the
    * same way. 0 is read as 1. */
   double scale_gravity;
+  /* Journey release distance in metres (local_mapping.cpp:324: roots whose
+   * jour stamp is >= 700 behind are erased, vg_release_far); 0 is read as 700. */
+  int release_dis;
+  int pad_r;
 } vg_config;
 
 /* Capacities of the device-resident map (HBM). Zero fields take defaults. */
@@ -231,6 +235,22 @@ int vg_get_stats(vg_ctx* ctx, vg_stats* out);
 /* Per-scan counters of every completed scan since vg_create / vg_reset, in
  * order: copies min(n, cap) records, *n = total (out may be NULL to query). */
 int vg_stats_log(vg_ctx* ctx, vg_stats* out, int cap, int* n);
+/* The map's lifetime — the idle branch of thd_odometry_localmapping
+ * (local_mapping.cpp:317-344), which the caller runs when it has no package
+ * (sync_packages false): once jour has advanced (release_flag, :510-518),
+ * every root voxel whose jour stamp is >= vg_config::release_dis (700 m)
+ * behind is erased with its subtree (OctoTree::tras_ptr, octree.cpp:597-608).
+ * The device then reclaims: erased nodes, point_fix blocks abandoned by
+ * growth and the blocks of leaves past max_points (octree.cpp:467-468) are
+ * compacted out of the node pool and the point_fix arena (order-preserving;
+ * results are unchanged). flags bit 0: compact even without a release. The
+ * pool is also compacted when over half the arena is abandoned blocks.
+ * Completes outstanding work first; between scans only. out (6): [0] roots
+ * erased (-1: no release was pending), [1] nodes erased, [2] roots, [3] nodes
+ * in the map after it, [4] point_fix points held, [5] point_fix arena used.
+ * A root still in surf_map_slide is never erased (the reference would keep a
+ * dangling pointer in it; unreachable at 700 m). */
+int vg_release_far(vg_ctx* ctx, int flags, long long* out);
 /* Window states x_buf (win_count x 250 doubles); returns win_count via *n. */
 int vg_window_states(vg_ctx* ctx, double* out, int* n);
 

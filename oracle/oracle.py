@@ -62,6 +62,9 @@ def lib():
         L.orc_get_state.argtypes = [P, dp]
         L.orc_step.argtypes = [P, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int, dp]
         L.orc_get_stats.argtypes = [P, ctypes.POINTER(Stats)]
+        L.orc_release_far.argtypes = [P, ctypes.POINTER(ctypes.c_longlong)]
+        L.orc_jour.argtypes = [P]
+        L.orc_jour.restype = ctypes.c_double
         L.orc_shard.argtypes = [P, ctypes.c_int, ctypes.c_int, ALLREDUCE, P]
         L.orc_step_deskew.argtypes = [P, fp, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int,
                                       dp]
@@ -279,6 +282,16 @@ class Pipeline:
         s = Stats()
         lib().orc_get_stats(self.h, ctypes.byref(s))
         return {k: (list(getattr(s, k)) if k == "iekf_matches" else getattr(s, k)) for k, _ in Stats._fields_}
+
+    def release_far(self):
+        """The idle branch's journey release (local_mapping.cpp:317-344): [roots erased (-1: none pending),
+        nodes erased, roots, nodes, point_fix points after it]."""
+        out = (ctypes.c_longlong * 5)()
+        lib().orc_release_far(self.h, out)
+        return list(out)
+
+    def jour(self):
+        return lib().orc_jour(self.h)
 
     def trajectory(self):
         """save_pose_tum rows (steady-state scans): t, R(9), p(3)."""

@@ -31,6 +31,7 @@ struct Pipeline {
   LidarFactor voxhess;
   int win_count = 0, win_base = 0;
   double jour = 0;
+  bool release_flag = false;  // local_mapping.cpp:272: set when jour advanced (:510-518)
   V3 last_pos;
   double last_pcl_end_time = 0;
   bool first = true;
@@ -491,6 +492,60 @@ struct Pipeline {
     }
   }
 
+  // The idle branch's journey release (local_mapping.cpp:317-344), taken when
+  // the caller has no package (sync_packages false): once jour has advanced
+  // (release_flag), every root voxel whose jour stamp is >= release_dis (700,
+  // :324) behind is erased with its subtree (OctoTree::tras_ptr,
+  // octree.cpp:597-608; the deletes run at once here). The reference's int
+  // truncation of jour - root.jour is kept. A root still in surf_map_slide is
+  // kept: the reference would leave a dangling pointer there (unreachable at
+  // 700 m: slide roots are stamped at every margi). out: [0] roots erased
+  // (-1: no release pending), [1] nodes erased, then the census after it:
+  // [2] roots, [3] nodes, [4] point_fix points held.
+  static long long subtree_nodes(OctoTree* o) {
+    std::vector<OctoTree*> v;
+    o->tras_ptr(v);
+    return 1 + (long long)v.size();
+  }
+  void census(long long* out) {
+    long long nodes = 0, fix = 0;
+    for (auto& kv : surf_map) {
+      std::vector<OctoTree*> v;
+      kv.second->tras_ptr(v);
+      v.push_back(kv.second);
+      nodes += (long long)v.size();
+      for (OctoTree* o : v) fix += (long long)o->point_fix.size();
+    }
+    out[2] = (long long)surf_map.size();
+    out[3] = nodes;
+    out[4] = fix;
+  }
+  void release_far(long long* out) {
+    out[0] = -1;
+    out[1] = 0;
+    if (release_flag) {
+      release_flag = false;
+      const int thr = cfg.release_dis > 0 ? cfg.release_dis : 700;
+      out[0] = 0;
+      for (auto it = surf_map.begin(); it != surf_map.end();) {
+        const int dis = jour - it->second->jour;
+        if (dis < thr || surf_map_slide.find(it->first) != surf_map_slide.end()) {
+          ++it;
+          continue;
+        }
+        std::vector<OctoTree*> octos;
+        it->second->tras_ptr(octos);
+        octos.push_back(it->second);
+        out[0]++;
+        out[1] += (long long)octos.size();
+        it->second->clear_slwd(sws[0]);
+        for (OctoTree* o : octos) delete o;
+        it = surf_map.erase(it);
+      }
+    }
+    census(out);
+  }
+
   // local_mapping.cpp:489-546: with a full window, LI_BA damping_iter, x_curr.R/p
   // from the window's last frame, multi_margi, jour, the mp ring and the slide
   template <class TP>
@@ -518,6 +573,7 @@ struct Pipeline {
       if (spat > 0.5) {
         jour += spat;
         last_pos = x_curr.p;
+        release_flag = true;  // local_mapping.cpp:517
       }
     }
     for (int i = 0; i < cfg.win_size; i++) {
@@ -852,6 +908,8 @@ int orc_deskew_only(void* h, float* xyz, const float* times, int n, double beg, 
   return (int)P->imu_poses.size();
 }
 void orc_get_stats(void* h, orc_stats* s) { *s = ((Pipeline*)h)->st; }
+void orc_release_far(void* h, long long* out) { ((Pipeline*)h)->release_far(out); }
+double orc_jour(void* h) { return ((Pipeline*)h)->jour; }
 // one lio_state_estimation_kdtree call on the scan downsampled at
 // max(down_size, 0.5) (raw LiDAR frame; var_init applies the extrinsic),
 // with the context's x_curr (orc_seed / orc_get_state) as the state

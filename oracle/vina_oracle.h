@@ -35,6 +35,8 @@ typedef struct orc_config {
                                      SURVEY row f2) instead of a seeded state */
   double scale_gravity;           /* IMUEKF::scale_gravity = imupre_scale_gravity (imu_ekf.cpp:51,
                                      imu_preintegration.cpp:51); 0 is read as 1 */
+  int release_dis;                /* journey release distance (local_mapping.cpp:324, 700 m); 0 is read as 700 */
+  int pad_r;
 } orc_config;
 
 typedef struct orc_stats {
@@ -65,6 +67,11 @@ void orc_get_state(void* h, double* state);
 int orc_step(void* h, const float* xyz, const float* inten, int n, double beg, double end, const double* imu, int m,
              double* timing);
 void orc_get_stats(void* h, orc_stats* s);
+/* The idle branch's journey release (local_mapping.cpp:317-344): out[0] roots
+ * erased (-1: jour has not advanced since the last call), [1] nodes erased,
+ * [2] roots, [3] nodes, [4] point_fix points after it. orc_jour: jour. */
+void orc_release_far(void* h, long long* out);
+double orc_jour(void* h);
 /* orc_step with IMUEKF::motion_blur's per-point deskew first (imu_ekf.cpp:114-144);
  * times: per-point offset from beg in seconds (the reference's curvature), ascending. */
 int orc_step_deskew(void* h, const float* xyz, const float* inten, const float* times, int n, double beg, double end,

@@ -138,6 +138,9 @@ def test_fused_launches_equal_separate(ka, kb, exact):
     a = vgpu.Context(vgconfig.to_c(p), **CAP)
     b = vgpu.Context(vgconfig.to_c(p), **CAP)
     for c, kv in ((a, ka), (b, kb)):
+        # two live contexts on the device turn the flag hand-offs off (dev_ctx_count) unless forced:
+        # this test drains each context before stepping the other
+        kv = {14: 2, **kv}
         for key, val in kv.items():
             assert vgpu.lib().vgx_debug(c.h, key, val) == 0
     a.seed(seq.gt_state(0))

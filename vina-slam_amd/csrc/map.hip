@@ -2934,6 +2934,7 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
     if (dseq) {  // the scan graph: this scan's publication numbers from the device state (DState::ph)
       seq = dseq[0];
       wa.seq2 = dseq[1];
+      wa.jour_check = dseq[4];
     }
     make_win_block(st, wa, m.wpn, win, nper, slot_of);
     __syncthreads();  // x_curr (set_xc), seen by the whole block
@@ -3244,6 +3245,16 @@ __global__ void __launch_bounds__(256) k_margi_erase_all(int nlev, int thread_nu
 __global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m, DState* __restrict__ st, int wc,
                                                         int nimu, Pub* __restrict__ pub, int seq2, const int* __restrict__ gate) {
   if (gate && !*gate) return;  // a speculative tail the LM did not reach (ba_run)
+  if (threadIdx.x == 0 && st->jour_check && wc > 0) {  // local_mapping.cpp:510-518, x_curr.p = x_buf.back().p
+    const double* xb = st->xs + (size_t)(wc - 1) * kXS + 9;  // (read before the slide below)
+    const V3 p = v3(xb[0], xb[1], xb[2]);
+    const double spat = norm3(sub(p, v3(st->last_pos[0], st->last_pos[1], st->last_pos[2])));
+    if (spat > 0.5) {
+      st->jour += spat;
+      for (int j = 0; j < 3; j++) st->last_pos[j] = p[j];
+    }
+    st->jour_check = 0;
+  }
   __shared__ int base;
   __shared__ int sc[1024];
   __shared__ int s_w[17];
@@ -3309,8 +3320,8 @@ __global__ void __launch_bounds__(1024) k_slide_compact(int thread_num, DevMap m
     if (t == 0) pub_flag(&pub->seq2, seq2);
   }
 }
-__global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, double j, int* __restrict__ rc,
-                                                  int n_oldest) {
+__global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, const double* __restrict__ jour,
+                                                  int* __restrict__ rc, int n_oldest) {
   if (blockIdx.x == 0) {  // margi level counts and the leaf count start at zero
     // kRcStatus is the recut's (k_ba_init may read it concurrently on the main stream)
     for (int i = threadIdx.x; i < kRcN; i += blockDim.x)
@@ -3319,6 +3330,7 @@ __global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, doub
   }
   const int n = m.counters[kCntSlide];
   if (g_slide(m) < thread_num) return;
+  const double j = *jour;  // the device's jour (DState::jour, the previous margi's update)
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) m.jour[m.slide[q]] = j;
 }
 
@@ -3328,8 +3340,7 @@ __global__ void __launch_bounds__(256) k_set_jour(int thread_num, DevMap m, doub
 // The part of multi_margi that does not depend on the BA (jour stamps, the
 // slide-tree levels, the oldest slot's points grouped by leaf), enqueued right
 // after the recut on the second stream so it runs under the LM iterations.
-int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, double jour,
-                     const unsigned* flags) {
+int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, const unsigned* flags) {
   DevMap& m = ctx->map;
   Work& w = ctx->wk;
   hipStream_t s = ctx->stream_ds;
@@ -3341,7 +3352,7 @@ int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thr
     VG_HIP(hipStreamWaitEvent(s, ctx->ev_recut_done, 0));  // recorded at the recut's end (map_recut)
   }
   const int gl = 64;  // grid-stride over device-side counts
-  k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, jour, w.rc, n_oldest);
+  k_set_jour<<<gl, kBlock, 0, s>>>(thread_num, m, &ctx->st->jour, w.rc, n_oldest);
   for (int L = 0; L < nlev; L++) k_collect_level<<<gl * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(L, thread_num, m, w.list1, w.list0, w.rc);
   (void)slot0;  // the oldest slot's points per leaf are the leaves' runs (DevMap::lseg): no sort here
   (void)n_oldest;

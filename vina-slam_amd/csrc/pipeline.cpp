@@ -159,6 +159,7 @@ static int absorb_p1(vg_ctx* ctx, HostPipe* P, Pend& q) {
     if (spat > 0.5) {
       P->jour += spat;
       P->last_pos = xc.p;
+      P->release_flag = true;
     }
   }
   q.seq1 = 0;
@@ -464,6 +465,7 @@ static WinArg make_winarg(const HostPipe* P, int set_xc) {
   for (int i = 0; i < P->win_count && i < 32; i++) w.nper[i] = P->wp_n[P->mp[i]];
   w.win_count = P->win_count;
   w.set_xc = set_xc;
+  w.jour_check = ((P->win_base + P->win_count) % 10 == 0) ? 1 : 0;  // local_mapping.cpp:510 (stage_margi_slide)
   return w;
 }
 
@@ -490,6 +492,10 @@ int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double en
   if (init_active(P)) {
     ctx->err = "vg_propagate: cold-start initialisation in progress (use vg_step* until init_phase 3)";
     return VG_E_STATE;
+  }
+  if (ctx->flag_sync && !ctx->flag_force && dev_ctx_count(ctx->device) > 1) {  // another context on the device: event waits from here
+    VG_TRY(host_sync(ctx));
+    ctx->flag_sync = false;
   }
   // device propagation (k_scan_prop): from the device's x_curr, so the host
   // does not wait for the previous scan's state here (the window push absorbs
@@ -767,7 +773,8 @@ static int stage_insert_recut(vg_ctx* ctx) {
     P->tail_wa = make_winarg(P, 1);
     P->sg_flags[0] = ++ctx->rc_flag_ctr;
     P->sg_flags[1] = ++ctx->pre_flag_ctr;
-    const int ph[6] = {seq0, P->tail_seq1, P->tail_seq2, (int)P->sg_flags[0], (int)P->sg_flags[1], 0};
+    const int ph[6] = {seq0, P->tail_seq1, P->tail_seq2, (int)P->sg_flags[0], (int)P->sg_flags[1],
+                       P->tail_wa.jour_check};
     memcpy(hin.ph, ph, sizeof(ph));
   }
   hipGraphExec_t& ge = sg ? ctx->g_scan[ring0] : ctx->g_mid[ring0];
@@ -893,7 +900,7 @@ int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows) {
     }
     // after a scan graph whose recut completed on the device, the prefix and the
     // graph's tail meet on device flags (the host-completed recut records events)
-    VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], ctx->cfg.thread_num, P->jour,
+    VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], ctx->cfg.thread_num,
                             pre && !rc_status ? P->sg_flags : nullptr));
     P->prefix = true;
     return VG_OK;
@@ -959,7 +966,7 @@ static int margi_enqueue(vg_ctx* ctx, HostPipe* P, const int* gate, int* seq1, i
   *seq1 = ++ctx->pub_seq;
   *seq2 = ++ctx->pub_seq;
   if (!P->prefix) {
-    VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], c.thread_num, P->jour));
+    VG_TRY(map_margi_prefix(ctx, P->mpd, P->mp[0], P->wp_n[P->mp[0]], c.thread_num));
     P->prefix = true;
   }
   return map_margi(ctx, P->mpd, wa, P->wp_n[P->mp[0]], c.thread_num, *seq1, *seq2, gate);
@@ -1034,6 +1041,33 @@ int stage_finish(vg_ctx* ctx) {
 }
 
 int host_win_count(vg_ctx* ctx) { return hp(ctx)->win_count; }
+
+// The idle branch's journey release (local_mapping.cpp:317-344) after
+// host_sync: pending once jour has advanced (release_flag, :510-518); the
+// device erases the far roots and compacts (lifetime.hip map_release). The
+// device keeps its own jour (DState::jour, for the margi stamps): it must be
+// the host's, bit for bit.
+int host_release_far(vg_ctx* ctx, int flags, long long* out) {
+  HostPipe* P = hp(ctx);
+  if (P->in_scan) {
+    ctx->err = "vg_release_far inside a scan";
+    return VG_E_STATE;
+  }
+  if (init_active(P)) {
+    ctx->err = "vg_release_far: cold-start initialisation in progress";
+    return VG_E_STATE;
+  }
+  double dj = 0;
+  VG_HIP(hipMemcpy(&dj, &ctx->st->jour, sizeof(double), hipMemcpyDeviceToHost));
+  if (memcmp(&dj, &P->jour, sizeof(double)) != 0) {
+    ctx->err = "vg_release_far: device jour " + std::to_string(dj) + " != host jour " + std::to_string(P->jour);
+    return VG_E_STATE;
+  }
+  const bool release = P->release_flag;
+  P->release_flag = false;
+  const int thr = ctx->cfg.release_dis > 0 ? ctx->cfg.release_dis : 700;
+  return map_release(ctx, release, thr, P->jour, flags & 1, out);
+}
 int host_memo_probe(vg_ctx* ctx, int* out) { return map_memo_probe(ctx, hp(ctx)->mpd, out); }
 
 // IMUEKF::motion_blur's per-point deskew (imu_ekf.cpp:114-144), SURVEY row

@@ -482,6 +482,7 @@ __device__ __forceinline__ void make_win_block(DState* __restrict__ st, const Wi
     win->win_count = wc;
     win->pad = 0;
     st->seq2 = wa.seq2;
+    if (wa.set_xc) st->jour_check = wa.jour_check;  // the margi head (k_slide_compact reads it)
   }
 }
 }  // namespace vg

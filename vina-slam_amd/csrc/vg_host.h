@@ -149,6 +149,7 @@ struct HostPipe {
   std::vector<int> mp;
   int win_count = 0, win_base = 0, epoch = 0;
   double jour = 0, last_pcl_end_time = 0;
+  bool release_flag = false;  // local_mapping.cpp:272, 517: jour advanced since the last release (vg_release_far)
   V3 last_pos = V3::Z();
   bool first = true;
   int wp_n[32] = {0};

@@ -284,8 +284,14 @@ struct DState {
   int imu_head, margi_seq;  // margi_seq: the last margi head's publication number (k_margi_copy signals it)
   // the scan graph's per-scan numbers (HostIn::ph, copied by k_ins_prep's block 0):
   // [0] the LM's first flag number, [1] / [2] the margi tail's publication
-  // numbers, [3] the recut-done flag value, [4] the margi prefix's flag value
+  // numbers, [3] the recut-done flag value, [4] the margi prefix's flag value,
+  // [5] the tail's jour_check (WinArg::jour_check)
   int ph[6];
+  // jour (local_mapping.cpp:510-518) on the device, so the margi prefix's
+  // stamps (k_set_jour) never wait for the host: jour_check is set by the margi
+  // head, the update runs in k_slide_compact (x_buf.back().p before the slide)
+  int jour_check, pad_j;
+  double jour, last_pos[3];
   double imurec[kMaxWin * kBaImuRec];
   KClock clk;
 };
@@ -361,7 +367,7 @@ struct WinArg {
   int win_count;
   int set_xc;           // x_curr.R/p <- x_buf.back() first (local_mapping.cpp:501-502)
   int seq2;             // end-of-scan publication number (stored in DState::seq2)
-  int pad;
+  int jour_check;       // (win_base + win_count) % 10 == 0: the jour update follows the margi (local_mapping.cpp:510)
 };
 
 }  // namespace vg
@@ -405,6 +411,8 @@ struct vg_ctx {
   // kernels do not run concurrently (AMD_SERIALIZE_KERNEL, or VG_SERIAL_KERNELS=1 as rocprofv3 --pmc
   // runs set): no device-flag hand-offs (a polling kernel would wait for a producer queued behind it)
   bool serial_kernels = false;
+  bool counted = false;          // in the per-device live-context count (dev_ctx_count)
+  bool flag_force = false;       // flag hand-offs even beside other contexts (vgx_debug 14 = 2: the caller drains between them)
   vg::HostIn* h_in = nullptr;  // host-mapped per-scan inputs of replayed graphs, kMaxWin slots (host address)
   vg::HostIn* d_in = nullptr;  // its device address
   int in_sel = 0;              // the slot map_insert uses (the ring position of a scan graph)
@@ -687,7 +695,7 @@ int sync_wait_dev(vg_ctx* ctx, hipStream_t s, int k, const int* target, const in
 // the margi kernels) and the end-of-scan counters (pub_seq2)
 // flags (the scan graph): {recut-done value of d_sync[3] to wait for, value to
 // store into d_sync[4] at the end}; nullptr: event waits
-int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num, double jour,
+int map_margi_prefix(vg_ctx* ctx, const MP& mp, int slot0, int n_oldest, int thread_num,
                      const unsigned* flags = nullptr);
 int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thread_num, int pub_seq, int pub_seq2,
               const int* gate);
@@ -773,6 +781,14 @@ int shard_alloc(vg_ctx* ctx);
 void shard_free(vg_ctx* ctx);
 int shard_allreduce(vg_ctx* ctx, const void* send, void* recv, int count, int dtype, int site);
 int host_sync(vg_ctx* ctx);
+// live contexts on a HIP device in this process (vina_gpu.cpp): with more than
+// one, each context's three streams share the device's hardware queues
+// (GPU_MAX_HW_QUEUES, 4 by default) with another's, and a polling hand-off
+// kernel could wait on a producer queued behind it: the flag hand-offs are off
+int dev_ctx_count(int device);
+int host_release_far(vg_ctx* ctx, int flags, long long* out);
+// lifetime.hip: the journey release + the node pool / point_fix arena compaction
+int map_release(vg_ctx* ctx, bool release, int thr, double jour, int compact, long long* out);
 int host_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* valid, int* iters);
 int decode_scan(vg_ctx* ctx, const void* records, int n, const vg_lidar_format* fmt, float* xyz, float* inten,
                 float* time, int* n_out);  // decode.hip

@@ -102,6 +102,11 @@ static void pinned_copy(vg_ctx* ctx, const std::vector<CopyPool::Job>& pieces) {
 }
 
 
+static std::atomic<int> g_dev_ctx[64];
+namespace vg {
+int dev_ctx_count(int device) { return (device >= 0 && device < 64) ? g_dev_ctx[device].load() : 1; }
+}  // namespace vg
+
 static void fill_capacity(vg_capacity& c) {
   if (c.max_points_per_scan <= 0) c.max_points_per_scan = 2000000;
   if (c.max_nodes <= 0) c.max_nodes = 4000000;
@@ -243,6 +248,10 @@ int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx**
     return fail(VG_E_HIP);
   }
   host_init(ctx);
+  if (device >= 0 && device < 64) {
+    ctx->counted = true;
+    if (g_dev_ctx[device].fetch_add(1) > 0) ctx->flag_sync = false;  // (stage_propagate: the others follow)
+  }
   *out = ctx;
   return VG_OK;
 }
@@ -255,6 +264,7 @@ int vg_destroy(vg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->stream_ds && ctx->stream_ds != ctx->stream) (void)hipStreamSynchronize(ctx->stream_ds);
   if (ctx->stream_iekf) (void)hipStreamSynchronize(ctx->stream_iekf);
+  if (ctx->counted) g_dev_ctx[ctx->device].fetch_sub(1);
   if (ctx->arena.base) (void)hipFree(ctx->arena.base);
   if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
   if (ctx->dbg_cap_buf) (void)hipFree(ctx->dbg_cap_buf);
@@ -319,6 +329,8 @@ int vg_reset(vg_ctx* ctx) {
   if (ctx->stream_iekf) VG_HIP(hipStreamSynchronize(ctx->stream_iekf));
   ctx->ba_loop.active = false;  // the HostPipe's record of it goes with host_reset
   VG_TRY(map_reset(ctx));
+  // the device's jour with the host's (host_reset: 0)
+  VG_HIP(hipMemset(&ctx->st->jour_check, 0, offsetof(DState, imurec) - offsetof(DState, jour_check)));
   VG_TRY(kd_reset(ctx));
   host_reset(ctx);
   return VG_OK;
@@ -574,6 +586,12 @@ int vg_scan_points(vg_ctx* ctx, float* xyz, int cap, int* n) {
     }
   }
   return VG_OK;
+}
+
+int vg_release_far(vg_ctx* ctx, int flags, long long* out) {
+  if (!ctx || !out || (flags & ~1)) return VG_E_ARG;
+  VG_TRY(host_sync(ctx));
+  return host_release_far(ctx, flags, out);
 }
 
 int vg_get_stats(vg_ctx* ctx, vg_stats* out) {
@@ -893,8 +911,11 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     ctx->ba_graph = value != 0;
     return VG_OK;
   }
-  if (key == 14) {  // 0: event waits for the margi leaf -> IEKF and IEKF -> insert hand-offs
+  if (key == 14) {  // 0: event waits for the margi leaf -> IEKF and IEKF -> insert hand-offs;
+                    // 2: the flag hand-offs even beside other contexts on the device (a caller that
+                    // drains each context before stepping another, as the A/B tests do)
     ctx->flag_sync = value != 0;
+    ctx->flag_force = value == 2;
     return VG_OK;
   }
   if (key == 27) {  // 0: no scan graph (separate insert+recut graph, LM launches, margi tail)

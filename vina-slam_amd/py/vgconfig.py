@@ -37,6 +37,7 @@ class CConfig(ctypes.Structure):
         ("max_layer", ctypes.c_int), ("max_points", ctypes.c_int), ("win_size", ctypes.c_int),
         ("thread_num", ctypes.c_int), ("if_BA", ctypes.c_int), ("use_threads", ctypes.c_int),
         ("vnc_prep", ctypes.c_int), ("cold_start", ctypes.c_int), ("scale_gravity", ctypes.c_double),
+        ("release_dis", ctypes.c_int), ("pad_r", ctypes.c_int),
     ]
 
 
@@ -53,7 +54,7 @@ def load(name_or_path):
     return out
 
 
-def to_c(p, use_threads=1, vnc_prep=1, scale_gravity=1.0, cold_start=0):
+def to_c(p, use_threads=1, vnc_prep=1, scale_gravity=1.0, cold_start=0, release_dis=0):
     g, o, b = p["General"], p["Odometry"], p["LocalBA"]
     c = CConfig()
     c.voxel_size = o["voxel_size"]
@@ -79,4 +80,5 @@ def to_c(p, use_threads=1, vnc_prep=1, scale_gravity=1.0, cold_start=0):
     c.vnc_prep = vnc_prep
     c.scale_gravity = scale_gravity
     c.cold_start = cold_start
+    c.release_dis = release_dis  # 0: the reference's 700 (local_mapping.cpp:324)
     return c

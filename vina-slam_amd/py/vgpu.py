@@ -131,6 +131,7 @@ def lib():
         L.vg_get_state.argtypes = [P, dp]
         L.vg_get_stats.argtypes = [P, ctypes.POINTER(Stats)]
         L.vg_stats_log.argtypes = [P, ctypes.POINTER(Stats), ctypes.c_int, ip]
+        L.vg_release_far.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_longlong)]
         L.vg_window_states.argtypes = [P, dp, ip]
         L.vg_trajectory.argtypes = [P, dp, ctypes.c_int, ip]
         L.vg_path.argtypes = [P, dp, ctypes.c_int, ip]
@@ -337,6 +338,13 @@ class Context:
         arr = (Stats * max(n.value, 1))()
         self._chk(lib().vg_stats_log(self.h, arr, n.value, ctypes.byref(n)), "vg_stats_log")
         return [_stats_dict(s) for s in arr[: n.value]]
+
+    def release_far(self, compact=False):
+        """The idle branch's journey release + pool compaction (vg_release_far): [roots erased (-1: none
+        pending), nodes erased, roots, nodes, point_fix points held, point_fix arena used]."""
+        out = (ctypes.c_longlong * 6)()
+        self._chk(lib().vg_release_far(self.h, 1 if compact else 0, out), "vg_release_far")
+        return list(out)
 
     def window_states(self):
         out = np.zeros((64, STATE_LEN))
