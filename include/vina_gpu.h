@@ -243,11 +243,15 @@ int vg_stats_log(vg_ctx* ctx, vg_stats* out, int cap, int* n);
  * The device then reclaims: erased nodes, point_fix blocks abandoned by
  * growth and the blocks of leaves past max_points (octree.cpp:467-468) are
  * compacted out of the node pool and the point_fix arena (order-preserving;
- * results are unchanged). flags bit 0: compact even without a release. The
- * pool is also compacted when over half the arena is abandoned blocks.
- * Completes outstanding work first; between scans only. out (6): [0] roots
- * erased (-1: no release was pending), [1] nodes erased, [2] roots, [3] nodes
- * in the map after it, [4] point_fix points held, [5] point_fix arena used.
+ * results are unchanged). flags bit 0: compact even without a release; bit
+ * 1: report the census (out[2..5]) even without one. The pool is also
+ * compacted when over half the arena is abandoned blocks. With flags 0 and no
+ * release pending among the scans already published it returns at once (no
+ * wait; out[] = -1), so a caller may call it whenever sync_packages comes back
+ * empty; otherwise it completes outstanding work first. Between scans only.
+ * out (6): [0] roots erased (-1: no release was pending), [1] nodes erased,
+ * [2] roots, [3] nodes in the map after it, [4] point_fix points held,
+ * [5] point_fix arena used.
  * A root still in surf_map_slide is never erased (the reference would keep a
  * dangling pointer in it; unreachable at 700 m). */
 int vg_release_far(vg_ctx* ctx, int flags, long long* out);

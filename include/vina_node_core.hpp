@@ -118,7 +118,11 @@ class NodeCore {
       int id = -1, m = 0, ready = 0;
       double beg = 0, end = 0;
       check(vg_sync_pop(sync_, &id, &beg, &end, imu.data(), kImuCap, &m, &ready), "vg_sync_pop");
-      if (ready == 0) break;
+      if (ready == 0) {  // sync_packages came back empty: the idle branch (local_mapping.cpp:303-356)
+        long long rel[6];
+        check(vg_release_far(lio_.raw(), 0, rel), "vg_release_far");  // returns at once unless jour advanced
+        break;
+      }
       auto it = scans_.find(id);
       if (ready < 0) {  // too few IMU samples: the reference drops the scan
         if (it != scans_.end()) scans_.erase(it);

@@ -1047,6 +1047,7 @@ int host_win_count(vg_ctx* ctx) { return hp(ctx)->win_count; }
 // device erases the far roots and compacts (lifetime.hip map_release). The
 // device keeps its own jour (DState::jour, for the margi stamps): it must be
 // the host's, bit for bit.
+bool host_release_pending(vg_ctx* ctx) { return hp(ctx)->release_flag; }
 int host_release_far(vg_ctx* ctx, int flags, long long* out) {
   HostPipe* P = hp(ctx);
   if (P->in_scan) {

@@ -787,6 +787,7 @@ int host_sync(vg_ctx* ctx);
 // kernel could wait on a producer queued behind it: the flag hand-offs are off
 int dev_ctx_count(int device);
 int host_release_far(vg_ctx* ctx, int flags, long long* out);
+bool host_release_pending(vg_ctx* ctx);  // jour advanced in an absorbed scan since the last release
 // lifetime.hip: the journey release + the node pool / point_fix arena compaction
 int map_release(vg_ctx* ctx, bool release, int thr, double jour, int compact, long long* out);
 int host_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* valid, int* iters);

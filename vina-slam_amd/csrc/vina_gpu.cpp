@@ -589,7 +589,14 @@ int vg_scan_points(vg_ctx* ctx, float* xyz, int cap, int* n) {
 }
 
 int vg_release_far(vg_ctx* ctx, int flags, long long* out) {
-  if (!ctx || !out || (flags & ~1)) return VG_E_ARG;
+  if (!ctx || !out || (flags & ~3)) return VG_E_ARG;
+  if (!(flags & 3)) {  // nothing asked but the release: no wait unless one is pending
+    VG_TRY(host_poll(ctx));
+    if (!host_release_pending(ctx)) {
+      for (int i = 0; i < 6; i++) out[i] = -1;
+      return VG_OK;
+    }
+  }
   VG_TRY(host_sync(ctx));
   return host_release_far(ctx, flags, out);
 }

@@ -339,11 +339,12 @@ class Context:
         self._chk(lib().vg_stats_log(self.h, arr, n.value, ctypes.byref(n)), "vg_stats_log")
         return [_stats_dict(s) for s in arr[: n.value]]
 
-    def release_far(self, compact=False):
+    def release_far(self, compact=False, census=True):
         """The idle branch's journey release + pool compaction (vg_release_far): [roots erased (-1: none
-        pending), nodes erased, roots, nodes, point_fix points held, point_fix arena used]."""
+        pending), nodes erased, roots, nodes, point_fix points held, point_fix arena used]; census=False:
+        the caller's idle-branch call (returns at once with -1s when no release is pending)."""
         out = (ctypes.c_longlong * 6)()
-        self._chk(lib().vg_release_far(self.h, 1 if compact else 0, out), "vg_release_far")
+        self._chk(lib().vg_release_far(self.h, (1 if compact else 0) | (2 if census else 0), out), "vg_release_far")
         return list(out)
 
     def window_states(self):
