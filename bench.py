@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--workers", type=int, default=0,
                     help="scan-generation processes (0: min(16, cpus); 1 under a profiler)")
     ap.add_argument("--no-h2d", action="store_true", help="skip the host-input (vg_step) rate")
+    ap.add_argument("--no-tile1", action="store_true", help="skip the one-GPU sharded-path leg")
     ap.add_argument("--max-nodes", type=int, default=0, help="context capacity: octree nodes (0: product default)")
     ap.add_argument("--max-fix", type=int, default=0, help="context capacity: point_fix points (0: default)")
     ap.add_argument("--hash-log2", type=int, default=0, help="context capacity: root hash slots, log2 (0: default)")
@@ -366,6 +367,10 @@ def main():
     if world == 1 and not args.no_h2d:
         beat("host-input leg")
         h2d = host_input_rate(p, seq, host_scans, imus, warmup, args.steps, dev)
+    tile1 = None
+    if world == 1 and not args.no_tile1:
+        beat("sharded-path leg on one GPU")
+        tile1 = tile_path_rate(p, seq, scans, imus, warmup, args.steps, dev, value)
     cpu, ate_cpu = None, None
     if cpu_on:
         beat("CPU baseline: %d + %d scans, 5 threads then 1" % (args.cpu_warmup, args.cpu_scans))
@@ -410,7 +415,8 @@ def main():
                                    "the output (SURVEY A8); the CPU baseline pays it"},
             "roofline": roof, "roofline_k_ba_solve": roof_solve, "roofline_k_iekf": roof_iekf,
             "roofline_k_rc_level": roof_rc, "roofline_k_ba_hess": roof_hess,
-            "host_ms_per_scan": host_ms, "host_input": h2d, "cpu_baseline": cpu, "ate_vs_cpu": ate_cpu,
+            "host_ms_per_scan": host_ms, "host_input": h2d, "tile_path_1gpu": tile1, "cpu_baseline": cpu,
+            "ate_vs_cpu": ate_cpu,
             "target_128line": targets or None, "multi_sequence": multi_roofline(multi, roof),
             "multi_sequence_1M": multi_1m, "env": {"GPU_MAX_HW_QUEUES": hwq, "VG_BENCH_DEBUG": dbg or None},
         }
@@ -630,6 +636,44 @@ def multi_child(args, p, g, warmup, total):
     for c in ctxs:
         c.close()
     return 0
+
+
+def tile_path_rate(p, seq, scans, imus, warmup, steps, dev, unsharded):
+    """The spatial-tile sharded code path (BASELINE config 4) on ONE GPU: a
+    one-rank RCCL communicator (vgx_debug 30), so every exchange point runs its
+    collective (ncclAllReduce on the context stream, the guarded frames) and
+    the scan takes the sharded launches (no scan graph, no IEKF/margi overlap).
+    Against the unsharded metric leg on the same scans: the sharded path's own
+    cost per scan, no peer traffic (RCCL over xGMI is unmeasured here)."""
+    import torch
+
+    import vgconfig
+    import vgpu
+    n = min(warmup + steps, len(scans))
+    ctx = vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=max(s[1] for s in scans) + 16, **CAP)
+    ctx.debug(30, 1)
+    ctx.shard_rccl(0, 1, vgpu.rccl_unique_id())
+    ctx.seed(seq.gt_state(0))
+    prepped = [ctx.prep_step_dev(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), m, b, e, imus[k])
+               for k, (t, m, b, e) in enumerate(scans[:n])]
+    for k in range(warmup):
+        ctx.step_prepped(prepped[k])
+    ctx.stats_log()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(warmup, n):
+        ctx.step_prepped(prepped[k])
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    ctx.stats_log()
+    ctx.close()
+    k = n - warmup
+    v = k / dt
+    return {"value": round(v, 3), "unit": "scans/s", "ms_per_step": round(dt * 1e3 / k, 4), "steps": k,
+            "overhead_ms_per_scan": round(dt * 1e3 / k - 1e3 / unsharded, 4),
+            "note": "the tile-sharded path (config 4) with a one-rank RCCL communicator (vgx_debug 30): every "
+                    "exchange runs ncclAllReduce on the stream, direct launches, no peer traffic; overhead vs the "
+                    "unsharded metric leg on the same scans"}
 
 
 def host_input_rate(p, seq, host_scans, imus, warmup, steps, dev):

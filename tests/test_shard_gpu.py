@@ -156,3 +156,33 @@ def test_desynchronised_rank_gets_an_error():
         pr.join(timeout=60)
     for r in (0, 1):
         assert "out of step" in res[r] and "(-5)" in res[r], res[r]
+
+
+def test_one_rank_rccl_sharded_path_matches_unsharded():
+    """The sharded code path on one GPU (vgx_debug 30: a one-rank RCCL
+    communicator, the bench's `tile_path_1gpu` leg): every exchange point runs
+    ncclAllReduce in its guarded frame, the scans take the sharded launches;
+    every counter equals the unsharded run's and the trajectory is within the
+    sharded tolerance (the sharded sums are ordered per shard)."""
+    p = vgconfig.load("mid360")
+    g = p["General"]
+    seq = synth.Sequence("16line", 2, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
+    out = []
+    for force in (False, True):
+        ctx = vgpu.Context(vgconfig.to_c(p), **CAP["16line"])
+        if force:
+            ctx.debug(30, 1)
+            ctx.shard_rccl(0, 1, vgpu.rccl_unique_id())
+        ctx.seed(seq.gt_state(0))
+        for k in range(16):
+            xyz, it, b, e = seq.scan(k)
+            ctx.step(xyz, it, b, e, seq.imu(k))
+        out.append((ctx.trajectory(), ctx.stats_log()))
+        ctx.close()
+    (t0, s0), (t1, s1) = out
+    keys = ("n_raw", "n_ds", "iekf_iters", "iekf_matches", "roots_new", "n_slide", "n_factors", "ba_iters",
+            "plane_updates", "fix_full")
+    for k, (a, b) in enumerate(zip(s0, s1)):
+        for key in keys:
+            assert a[key] == b[key], (k, key, a[key], b[key])
+    assert np.abs(t0[:, 10:13] - t1[:, 10:13]).max() < TIGHT_M and np.abs(t0[:, 1:10] - t1[:, 1:10]).max() < TIGHT_M

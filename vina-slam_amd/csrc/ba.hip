@@ -1339,7 +1339,7 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr) {
   BaDev d = carve(ctx);
   const int nimu = W - 1;
   const int L = 6 * W, nl = L * (L + 1) / 2, nout = nl + L + 1;
-  const bool sharded = ctx->shard.world > 1;
+  const bool shard_on = sharded(ctx);
   double* hl_part = ctx->ba.hout_part;  // this shard's LiDAR Hessian (sharded mode)
   double* rsum = ctx->shard.d_buf + 256;  // [0]: this shard's residual, [1]: all-reduced
   // factor count on the device (the recut's kCntFactors): fixed grids, so an
@@ -1350,18 +1350,18 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr) {
   const size_t hess_lds = hess_lds_bytes(W);
   const size_t solve_lds = solve_lds_bytes(W);
   const int NBt = (15 * W - 15 + kTile - 1) / kTile, ntile = NBt * (NBt + 1) / 2;
-  CtlArg ctl{W, nimu, sharded ? 1 : nrb, nl + L, ctx->cfg.imu_coef, d.hl, d.imuout, d.imures,
-             sharded ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st, ctx->d_pub, nullptr};
+  CtlArg ctl{W, nimu, shard_on ? 1 : nrb, nl + L, ctx->cfg.imu_coef, d.hl, d.imuout, d.imures,
+             shard_on ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st, ctx->d_pub, nullptr};
   CtlArg ctl_fused = ctl;  // unsharded: the bookkeeping rides in k_ba_resid's IMU workgroup
-  if (!sharded && ctx->ba_fuse_ctl) ctl_fused.err = ctx->map.counters + kCntErr;
+  if (!shard_on && ctx->ba_fuse_ctl) ctl_fused.err = ctx->map.counters + kCntErr;
   k_ba_hess<<<G + nimu, kHessThreads, hess_lds, s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
                                                     ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, nimu, d.imurec, &ctx->st->imu_head,
                                                     d.bias, d.imuout, &ctx->st->clk);
-  k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, sharded ? hl_part : d.hl,
+  k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, shard_on ? hl_part : d.hl,
                                                        d.st);
   // sharded: every shard's factors -> one LiDAR Hessian / gradient / residual
   // (out of place: a rejected step re-reduces the unchanged partial)
-  if (sharded && xerr == VG_OK) xerr = shard_allreduce(ctx, hl_part, d.hl, nout, 0, 3);
+  if (shard_on && xerr == VG_OK) xerr = shard_allreduce(ctx, hl_part, d.hl, nout, 0, 3);
   if (k == 0 && ctx->dbg_capture == 1 && ctx->dbg_cap_buf) {  // test knob (vgx_debug 5): the first pass
     (void)hipMemcpyAsync(ctx->dbg_cap_buf, d.hl, nout * sizeof(double), hipMemcpyDeviceToDevice, s);
     (void)hipMemcpyAsync(ctx->dbg_cap_buf + nout, d.imuout, (size_t)nimu * 931 * sizeof(double),
@@ -1378,7 +1378,7 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr) {
   k_ba_resid<<<nrb + 1, 256, 0, s>>>(nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
                                      ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, nimu, d.imurec, &ctx->st->imu_head, d.bias,
                                      d.imures, ctl_fused);
-  if (sharded) {  // the residual over every shard's factors
+  if (shard_on) {  // the residual over every shard's factors
     k_ba_rsum<<<1, 64, 0, s>>>(nrb, d.rpart, rsum, d.st);
     if (xerr == VG_OK) xerr = shard_allreduce(ctx, rsum, rsum + 1, 1, 0, 4);
   }
@@ -1426,7 +1426,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   }
   hipStream_t s = ctx->stream;
   (void)nf;
-  const bool sharded = ctx->shard.world > 1;
+  const bool shard_on = sharded(ctx);
   int seq0;
   if (pre > 0) {
     seq0 = ctx->ba_seq0_pre;
@@ -1442,7 +1442,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   const bool solve_ev = pre == 0 && ctx->prof_on && !ctx->prof_clock &&
                         (ctx->prof_every <= 1 || ctx->prof_runs++ % ctx->prof_every == 0);
   auto enqueue = [&](int k) { ba_iter_kernels(ctx, k, solve_ev, xerr); };
-  const bool graph = ctx->use_graphs && ctx->ba_graph && !sharded && !solve_ev && ctx->dbg_capture != 1;
+  const bool graph = ctx->use_graphs && ctx->ba_graph && !shard_on && !solve_ev && ctx->dbg_capture != 1;
   if (graph && !ctx->g_ba) {
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     enqueue(0);

@@ -513,7 +513,7 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
   kern<<<nb, 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials, tag ? w.pk_leaf : nullptr);
   if (ev1) VG_HIP(hipEventRecord(ev1, s));
   if (tag) k_iekf_planes<<<nb, 256, 0, s>>>(ctx->st, ctx->map, w.pk_leaf, tag, &ctx->st->planes[it]);
-  if (ctx->shard.world > 1) {  // this shard's sums, all-reduced, then the (replicated) update
+  if (sharded(ctx)) {  // this shard's sums, all-reduced, then the (replicated) update
     double* sums = ctx->shard.d_buf;
     k_iekf_reduce<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, sums);
     VG_TRY(shard_allreduce(ctx, sums, sums + 64, kIekfVals, 0, 0));
@@ -538,10 +538,10 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
   if (begin_xc || begin_prop)  // the scan opens here (pipeline.cpp)
     VG_TRY(state_scan_begin(ctx, begin_xc, x, y, z, n, s, begin_prop));
   else if (!opened) VG_TRY(state_set_scan(ctx, x, y, z, n, s));
-  const bool graph = ctx->use_graphs && ctx->shard.world <= 1 && !ctx->prof_stages;
+  const bool graph = ctx->use_graphs && !sharded(ctx) && !ctx->prof_stages;
   const bool ev = ctx->prof_on && !graph;
   // the last update signals the hand-off itself (k_iekf_update; not when sharded)
-  const bool self_signal = signal && ctx->shard.world <= 1;
+  const bool self_signal = signal && !sharded(ctx);
   unsigned* flag = self_signal ? ctx->d_sync + 1 : nullptr;
   auto enqueue = [&]() -> int {
     for (int it = 0; it < 4; it++)
@@ -1539,7 +1539,7 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread
     k_ins_flags<<<ntile, kBlock, 0, s>>>(n, nd, w.u0, m, w.v1, (int*)w.ac_cnt);
     k_ins_roots_alloc<<<ntile, kBlock, 0, s>>>(n, nd, ntile, w.u0, w.v1, (const int*)w.ac_cnt, mp, m);
   }
-  if (m.shard_world > 1) {  // the thread_num quirk counts distinct roots over all shards
+  if (sharded(ctx)) {  // the thread_num quirk counts distinct roots over all shards
     k_copy_int<<<1, 64, 0, s>>>(m.counters + kCntTouched, m.counters + kCntGTouched);
     VG_TRY(shard_allreduce(ctx, m.counters + kCntGTouched, m.counters + kCntGTouched, 1, 1, 1));
   }
@@ -2702,7 +2702,7 @@ static int map_recut_impl(vg_ctx* ctx, const MP& mp, const WinArg& wa, int threa
   ctx->rc_total = total;
   ctx->rc_thread_num = thread_num;
   k_make_win_recut_begin<<<1, 256, 0, s>>>(ctx->st, wa, ctx->map.wpn, dwin, dn, dslot, m, w.rc, thread_num);
-  if (m.shard_world > 1) {
+  if (sharded(ctx)) {
     if (!replay) {  // the global slide count (a replay re-uses it: the insert replay does not change it)
       VG_TRY(shard_allreduce(ctx, m.counters + kCntGSlide, ctx->shard.d_buf + 512, 1, 1, 2));
     }
@@ -3414,7 +3414,7 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   // the hand-off flags to the next scan's IEKF stream: the margi head's
   // x_curr (d_sync[2], the device propagation starts from it) and the leaves'
   // plane updates (d_sync[0], the IEKF reads them)
-  const bool flags = ctx->flag_sync && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages && ctx->shard.world == 1;
+  const bool flags = ctx->flag_sync && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages && !sharded(ctx);
   k_margi_leaf<<<1 + 512 * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(
       m.counters + kCntLeaves, w.list0, mp, wa2, ctx->st, dwin, dn, dn + 32, bi != nullptr, bi,
       bi ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, pub_seq, m, ctx->ba.fac_eig, ctx->ba.fac_pcr, w.plan, gate,

@@ -401,7 +401,7 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   // scan k+1 is being enqueued
   ctx->iekf_ring_base = ctx->iekf_ring_base == 0 ? 8 : 0;
   P->cur.ev_base = ctx->iekf_ring_base;
-  P->cur.ev_n = (ctx->prof_on && (ctx->prof_stages || !ctx->use_graphs || ctx->shard.world > 1)) ? 4 : 0;
+  P->cur.ev_n = (ctx->prof_on && (ctx->prof_stages || !ctx->use_graphs || sharded(ctx))) ? 4 : 0;
   VG_TRY(flush_deferred_push(ctx, P));
   const bool begin = P->begin_pending;
   P->begin_pending = false;
@@ -409,7 +409,7 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   // remainder on the main stream runs under this IEKF, and the main stream
   // then waits for the IEKF. The opening (k_scan_begin) goes with it.
   const bool split = ctx->tail_a_valid && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages &&
-                     ctx->shard.world == 1;
+                     !sharded(ctx);
   ctx->tail_a_valid = false;
   const double* bxc = begin && !P->begin_prop ? P->begin_xc : nullptr;
   const PropArg* bprop = begin && P->begin_prop ? &P->prop : nullptr;
@@ -726,7 +726,7 @@ static int insert_replay(vg_ctx* ctx, HostPipe* P) {
 // factor extraction is the asynchronous one), no debug capacity overrides.
 static bool mid_graph_ok(vg_ctx* ctx, const HostPipe* P) {
   const vg_config& c = ctx->cfg;
-  return ctx->use_graphs && !ctx->prof_stages && ctx->shard.world == 1 && c.if_BA == 1 &&
+  return ctx->use_graphs && !ctx->prof_stages && !sharded(ctx) && c.if_BA == 1 &&
          P->win_count == c.win_size && P->push_pending && P->push.ord == c.win_size - 1 && !P->begin_pending &&
          ctx->dbg_apply_cap < 0 && ctx->dbg_ins_cap < 0 && ctx->dbg_fac_max < 0 && P->ds_seq != 0;
 }
@@ -841,7 +841,7 @@ int stage_recut(vg_ctx* ctx, int* nf_out) {
   int nf = 0;
   prof_begin(ctx, kProfRecut);
   P->rc_seq = 0;
-  if (!nf_out && P->win_count >= c.win_size && c.if_BA == 1 && ctx->shard.world == 1) {
+  if (!nf_out && P->win_count >= c.win_size && c.if_BA == 1 && !sharded(ctx)) {
     // the LM follows: its kernels read the factor count on the device, and the
     // host learns the recut's outcome only once the LM is enqueued (stage_ba)
     P->rc_seq = ++ctx->rc_pub;  // the device counts its asynchronous recuts the same way (k_fac_sort)
@@ -907,7 +907,7 @@ int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows) {
   };
   // the margi tail behind the LM (see ba_run): fused step, plain graph path
   const bool spec_ok = margi_follows && ctx->spec_tail && ctx->use_graphs && !ctx->prof_stages &&
-                       ctx->shard.world == 1;
+                       !sharded(ctx);
   std::function<int(bool*)> spec = [&](bool* queued) -> int {
     if (rc_status || !P->prefix) return VG_OK;
     VG_TRY(margi_enqueue(ctx, P, ba_gate_dev(ctx), &P->tail_seq1, &P->tail_seq2));
@@ -999,7 +999,7 @@ int stage_margi_slide(vg_ctx* ctx) {
   // the margi that stands (the speculative tail or the one just enqueued) stores seq1 into the
   // IEKF hand-off flag (map_margi), which the next scan's IEKF stream polls (lio_state_estimation)
   ctx->sync_tail_armed = ctx->flag_sync && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages &&
-                         ctx->shard.world == 1;
+                         !sharded(ctx);
   ctx->sync_tail_value = (unsigned)seq1;
   P->cur.seq1 = seq1;
   P->cur.seq2 = seq2;

@@ -7,17 +7,20 @@
 //         gloo); the library synchronises the stream, stages through pinned
 //         memory and copies the sum back. For tests and CPU-mediated transports.
 //
-// Exchange guard. Every all-reduce of a context carries the same fixed frame
-// (Shard::frame_n doubles: the payload, ints as doubles, zeros, then the
-// guard pair (x, x^2) with x = (seq mod 2^16) * 16 + site; seq is the
+// Exchange guard. Every all-reduce carries a frame of its call site's class
+// (kShardSmall = 64 doubles for the IEKF's normal equations and the counts,
+// Shard::frame_n for the LM's Hessian: the payload, ints as doubles, zeros,
+// then the guard pair (x, x^2) with x = (seq mod 2^16) * 16 + site; seq is the
 // device's count of this context's exchanges, site the call site). The summed
 // pair equals (world x, world x^2) exactly when every rank sent the same x
 // (sum over ranks of (x_r - x)^2 = 0; all terms < 2^44, exact in fp64), i.e.
 // the ranks are at the same exchange of the same call site. A rank that
 // enqueued a different exchange sequence gets VG_E_STATE ("sharded exchange
-// out of step") instead of a collective that pairs messages of different
-// sizes and hangs; with one frame size the out-of-step collectives still
-// complete, so every rank reaches the error.
+// out of step"), and the consumers of that exchange read zeros; within a
+// frame class the out-of-step collectives still complete, so every rank
+// reaches the error (ranks drifting across classes would pair frames of
+// different sizes: the cost of not sending the 15 KB Hessian frame for every
+// 34-value IEKF exchange).
 #include <rccl/rccl.h>
 #include <cstring>
 #include "vg_internal.h"
@@ -43,8 +46,12 @@ __global__ void k_xchg_unpack(const double* __restrict__ frame, void* __restrict
                               int world, int* __restrict__ err) {
   const double x = frame[n];
   const bool ok = frame[n - 2] == world * x && frame[n - 1] == world * (x * x);
-  if (!ok) {
+  if (!ok) {  // the consumers read zeros, not another exchange's (or a stale) sum
     if (threadIdx.x == 0) atomicOr(err, 32);
+    for (int i = threadIdx.x; i < count; i += blockDim.x) {
+      if (dtype == 0) static_cast<double*>(recv)[i] = 0.0;
+      else static_cast<int*>(recv)[i] = 0;
+    }
     return;
   }
   for (int i = threadIdx.x; i < count; i += blockDim.x) {
@@ -81,8 +88,12 @@ void shard_free(vg_ctx* ctx) {
 // equal recv
 int shard_allreduce(vg_ctx* ctx, const void* send, void* recv, int count, int dtype, int site) {
   Shard& sh = ctx->shard;
-  if (sh.world <= 1 || count <= 0) return VG_OK;
-  const int n = sh.frame_n;
+  if (sh.mode == 0 || count <= 0) return VG_OK;
+  // the frame of the call site's class: the IEKF's normal equations and the
+  // counts (<= 62 values) travel in a 64-double frame, the LM's Hessian in the
+  // largest; a site always sends the same count, so ranks at the same exchange
+  // agree on the size (the guard catches a rank at another exchange of the class)
+  const int n = count <= kShardSmall - 2 ? kShardSmall : sh.frame_n;
   if (count > n - 2) {
     ctx->err = "shard_allreduce: message larger than the exchange frame";
     return VG_E_ARG;
@@ -127,7 +138,7 @@ static int shard_common(vg_ctx* ctx, int rank, int world) {
     ctx->err = "vg_shard: rank/world out of range";
     return VG_E_ARG;
   }
-  if (host_win_count(ctx) != 0 || ctx->shard.world > 1) {
+  if (host_win_count(ctx) != 0 || ctx->shard.mode != 0) {
     ctx->err = "vg_shard: call once, before the first scan";
     return VG_E_STATE;
   }
@@ -155,7 +166,7 @@ int vg_rccl_unique_id(void* id128) {
 int vg_shard_rccl(vg_ctx* ctx, int rank, int world, const void* id128) {
   if (!ctx || !id128) return VG_E_ARG;
   VG_TRY(shard_common(ctx, rank, world));
-  if (world == 1) return VG_OK;
+  if (world == 1 && !ctx->shard_force) return VG_OK;  // (vgx_debug 30: the sharded path on one GPU)
   ncclUniqueId id;
   memcpy(&id, id128, sizeof(id));
   ncclComm_t comm;

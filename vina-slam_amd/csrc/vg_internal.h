@@ -325,6 +325,7 @@ struct HostIn {
 // sums only its own points / factors; the normal equations are all-reduced
 // (RCCL on the context stream, or a host callback for CPU-mediated tests).
 constexpr int kShardBuf = 4096;  // doubles of exchange scratch / staging
+constexpr int kShardSmall = 64;   // doubles of a small exchange frame (payload + guard pair)
 struct Shard {
   int rank = 0, world = 1;
   int mode = 0;              // 0 none, 1 RCCL, 2 host callback
@@ -412,6 +413,7 @@ struct vg_ctx {
   // runs set): no device-flag hand-offs (a polling kernel would wait for a producer queued behind it)
   bool serial_kernels = false;
   bool counted = false;          // in the per-device live-context count (dev_ctx_count)
+  bool shard_force = false;       // vg_shard_rccl at world 1 still sets up the sharded path (vgx_debug 30)
   bool flag_force = false;       // flag hand-offs even beside other contexts (vgx_debug 14 = 2: the caller drains between them)
   vg::HostIn* h_in = nullptr;  // host-mapped per-scan inputs of replayed graphs, kMaxWin slots (host address)
   vg::HostIn* d_in = nullptr;  // its device address
@@ -781,6 +783,10 @@ int shard_alloc(vg_ctx* ctx);
 void shard_free(vg_ctx* ctx);
 int shard_allreduce(vg_ctx* ctx, const void* send, void* recv, int count, int dtype, int site);
 int host_sync(vg_ctx* ctx);
+// the sharded path (collectives at the exchange points, direct launches): a
+// shard transport is set (vg_shard_rccl / vg_shard_host with world > 1, or
+// world 1 with vgx_debug 30: the sharded path's own cost on one GPU)
+inline bool sharded(const vg_ctx* c) { return c->shard.mode != 0; }
 // live contexts on a HIP device in this process (vina_gpu.cpp): with more than
 // one, each context's three streams share the device's hardware queues
 // (GPU_MAX_HW_QUEUES, 4 by default) with another's, and a polling hand-off

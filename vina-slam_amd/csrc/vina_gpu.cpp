@@ -918,6 +918,10 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     ctx->ba_graph = value != 0;
     return VG_OK;
   }
+  if (key == 30) {  // 1: vg_shard_rccl(ctx, 0, 1, id) sets up the sharded path on one GPU (RCCL, one rank)
+    ctx->shard_force = value != 0;
+    return VG_OK;
+  }
   if (key == 14) {  // 0: event waits for the margi leaf -> IEKF and IEKF -> insert hand-offs;
                     // 2: the flag hand-offs even beside other contexts on the device (a caller that
                     // drains each context before stepping another, as the A/B tests do)
