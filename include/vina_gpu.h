@@ -18,6 +18,15 @@
  *      [19..21] ba, [22..24] g, [25..249] cov 15x15 row-major.
  *  - IMU samples: m rows of 7 doubles [t, gx, gy, gz, ax, ay, az]
  *    (sensor_msgs::Imu subset, m/s^2 and rad/s).
+ *  - A context runs on three HIP streams and hands work between them through
+ *    device flags that kernels poll, which needs kernels of different streams
+ *    to run concurrently. Where they may not, the context uses event waits
+ *    instead: serialised-kernel runs (AMD_SERIALIZE_KERNEL, VG_SERIAL_KERNELS=1,
+ *    or rocprofv3 --pmc, detected at vg_create), and several live contexts on
+ *    one device in one process (their streams would share the device's
+ *    hardware queues; use vg_multi_* for several sequences). A hand-off that
+ *    still times out (~1 s) fails the scan with VG_E_STATE; device errors are
+ *    sticky: every later call returns them until vg_reset.
  */
 #ifndef VINA_GPU_H
 #define VINA_GPU_H

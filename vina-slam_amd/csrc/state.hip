@@ -386,12 +386,16 @@ __global__ void k_sync_set(unsigned* __restrict__ flag, const int* __restrict__ 
   if (threadIdx.x != 0 || (gate && !*gate)) return;
   __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__global__ void k_sync_wait(const unsigned* __restrict__ flag, unsigned target, int* __restrict__ err) {
+// close: the consumer is the IEKF — a wait that timed out also closes it
+// (st->done: its iterations exit), so it never runs on a half-updated map
+__global__ void k_sync_wait(const unsigned* __restrict__ flag, unsigned target, int* __restrict__ err,
+                            DState* __restrict__ close) {
   if (threadIdx.x != 0) return;
   for (long it = 0; (int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0; it++) {
     __builtin_amdgcn_s_sleep(4);
     if (it > (1l << 24)) {
       atomicOr(err, 64);
+      if (close) close->done = 1;
       return;
     }
   }
@@ -421,7 +425,7 @@ int sync_set(vg_ctx* ctx, hipStream_t s, int k, unsigned value, const int* gate)
   return VG_OK;
 }
 int sync_wait(vg_ctx* ctx, hipStream_t s, int k, unsigned target) {
-  k_sync_wait<<<1, 64, 0, s>>>(ctx->d_sync + k, target, ctx->map.counters + kCntErr);
+  k_sync_wait<<<1, 64, 0, s>>>(ctx->d_sync + k, target, ctx->map.counters + kCntErr, k == 0 ? ctx->st : nullptr);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }
