@@ -516,7 +516,7 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
                                                  double* __restrict__ Jcalc, double* __restrict__ timg,
                                                  double* __restrict__ bvec, double* __restrict__ dvec,
                                                  double* __restrict__ jvec, int* __restrict__ ipg,
-                                                 const BaState* __restrict__ st) {
+                                                 const BaState* __restrict__ st, int structural) {
   if (st->done) return;
   constexpr int kN = kMaxNB * kTile;
   __shared__ double Dv[kN], Jg[kN];
@@ -528,7 +528,13 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
   for (int t = tid; t < n; t += blockDim.x)
     Dv[t] = t < 15 ? 1.0 : (calc ? asm_entry(t, t, nimu, imu_coef, hl, imuout, L) : Hcalc[lo(t, t)]);
   __syncthreads();
-  for (int i = 15 + tid; i < n; i += blockDim.x) {  // rank of |D + u D| descending, index ascending on ties
+  for (int i = 15 + tid; i < n; i += blockDim.x) {
+    if (structural) {  // v / bg / ba of frames 1..W-1 first (frame order), then their poses
+      const int j = i / 15, v = i - 15 * j;
+      ip[v >= 6 ? 9 * (j - 1) + (v - 6) : 9 * (W - 1) + 6 * (j - 1) + v] = i;
+      continue;
+    }
+    // Eigen's order: rank of |D + u D| descending, index ascending on ties
     const unsigned long long ki = (unsigned long long)__double_as_longlong(fabs(Dv[i] + u * Dv[i]));
     int c = 0;
     for (int j = 15; j < n; j++) {
@@ -781,6 +787,13 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
 #pragma unroll
     for (int g = 0; g < 4; g++) t[tel(rq + 4 * g, cc)] = a[g];
   };
+  // an all-zero tile (wave-uniform): its updates are exact no-ops and are
+  // skipped. In the structural order (k_ba_prep) the v/bg/ba tiles far from the
+  // diagonal are zero and stay zero (the IMU factors couple adjacent frames only)
+  auto zero_tile = [&](const v4d& o) __attribute__((always_inline)) {
+    const bool nz = o[0] != 0.0 || o[1] != 0.0 || o[2] != 0.0 || o[3] != 0.0;
+    return __ballot(nz) == 0;
+  };
 
   // wave 0 takes tile (0, 0) straight from the image and inverts it while the
   // other waves fill the tile store and the vectors
@@ -853,11 +866,15 @@ __global__ void __launch_bounds__(1024) k_ba_solve(int W, int nimu, const double
       for (int I = K + 2; I < NB; I++)
         for (int J0 = K + 1; J0 <= I; J0 += 4) {
           if (q++ % nwk != wk) continue;
-          const v4d gt = mk_gt(tv, ld_ops(&T[tix(I, K) * 256]));
+          const v4d sik = ld_ops(&T[tix(I, K) * 256]);
+          if (zero_tile(sik)) continue;  // L_IK = 0: no update, no y update, the tile stays 0 (= -L_IK^T)
+          const v4d gt = mk_gt(tv, sik);
           const int J1 = J0 + 4 < I + 1 ? J0 + 4 : I + 1;
           for (int J = J0; J < J1; J++) {
+            const v4d sjk = ld_ops(&T[tix(J, K) * 256]);
+            if (zero_tile(sjk)) continue;
             double* Tij = &T[tix(I, J) * 256];
-            st_tile(Tij, tile_upd(ld_tile(Tij), gt, ld_ops(&T[tix(J, K) * 256])));
+            st_tile(Tij, tile_upd(ld_tile(Tij), gt, sjk));
           }
           if (J0 == K + 1) {
             y_upd(gt, K, I);
@@ -1370,7 +1387,7 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr) {
     ctx->dbg_capture = 2;
   }
   k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
-                                  d.dvec, d.jvec, d.ipg, d.st);
+                                  d.dvec, d.jvec, d.ipg, d.st, ctx->ba_structural ? 1 : 0);
   if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][0], s);
   k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
                                        d.st, &ctx->st->clk);

@@ -486,6 +486,7 @@ struct vg_ctx {
   bool margi_batch = true;    // vgx_debug 24: k_margi_leaf reads a leaf's frame clusters four at a time (r04k +0.4 %)
   bool margi_fused = true;    // margi isexist bottom-up in k_margi_copy, erase in one launch (vgx_debug 21: 0 = per-level launches)
   bool iekf_prefetch = true;  // vgx_debug 23: k_iekf touches a cached match's plane record beside its header (r04i A/B +0.9 %)
+  bool ba_structural = true;  // vgx_debug 31: k_ba_prep's structural elimination order (0: Eigen's |diag| order)
   bool ba_fuse_ctl = true;    // vgx_debug 19: the LM bookkeeping in k_ba_resid's IMU workgroup (A/Bs r04e 0, r04g/h +0.8-0.9 %)
   bool ba_graph = true;      // LM iterations replay one captured graph each (vgx_debug 15: 0 = direct launches)
   bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)

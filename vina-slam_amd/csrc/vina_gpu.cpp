@@ -918,6 +918,10 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     ctx->ba_graph = value != 0;
     return VG_OK;
   }
+  if (key == 31) {  // 0: the LM system in Eigen's pivot order (descending |diag|) instead of the structural one
+    ctx->ba_structural = value != 0;
+    return VG_OK;
+  }
   if (key == 30) {  // 1: vg_shard_rccl(ctx, 0, 1, id) sets up the sharded path on one GPU (RCCL, one rank)
     ctx->shard_force = value != 0;
     return VG_OK;
