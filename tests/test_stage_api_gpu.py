@@ -112,11 +112,13 @@ def test_recut_replay_path_equals_fast_path(knob):
 @pytest.mark.parametrize("ka,kb,exact", [({19: 0}, {}, True), ({21: 0}, {}, True), ({}, {13: 1}, True),
                                          ({23: 0}, {}, True), ({24: 0}, {}, True), ({11: 0}, {}, True),
                                          ({16: 0}, {}, True), ({17: 0}, {}, True), ({14: 0}, {}, True),
-                                         ({26: 0}, {}, True), ({27: 0}, {}, True)],
+                                         ({26: 0}, {}, True), ({27: 0}, {}, True), ({32: 0}, {}, True),
+                                         ({31: 0}, {}, False)],
                          ids=["lm-bookkeeping-in-resid", "margi-exist-up", "device-propagation",
                               "iekf-plane-prefetch", "margi-batched-cluster-loads", "recut-fused-levels",
                               "root-registration-lookback", "lm-two-iteration-graph", "flag-hand-offs",
-                              "lm-outcome-deferred", "scan-graph"])
+                              "lm-outcome-deferred", "scan-graph", "factor-bookkeeping-in-ba-init",
+                              "lm-structural-order"])
 def test_fused_launches_equal_separate(ka, kb, exact):
     """Every default-on launch fusion or hand-off of the scan chain against its
     separate-launch form (vgx_debug knobs), bit for bit: k_ba_control inside
@@ -130,9 +132,12 @@ def test_fused_launches_equal_separate(ka, kb, exact):
     hand-offs against event waits (14) and a step that returns before its
     LM's outcome (26: the next step enqueues its IEKF first, then resolves it;
     the first window-full scans need more LM iterations than predicted, so
-    the real margi tail replaces a speculative one there) and the scan graph
+    the real margi tail replaces a speculative one there), the scan graph
     (27: insert + recut + LM + margi tail as one replayed graph per ring
-    position, hand-offs on device flags)."""
+    position, hand-offs on device flags) and tras_opt's factor bookkeeping
+    inside k_ba_init (32); the LM system's structural elimination order
+    against Eigen's |diag| order (31) agrees within rounding (counters exact,
+    poses within 1e-12 m)."""
     p = vgconfig.load("mid360")
     seq = _seq(p, seq_id=7)
     a = vgpu.Context(vgconfig.to_c(p), **CAP)

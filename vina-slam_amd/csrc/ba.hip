@@ -1188,17 +1188,34 @@ struct MpRing {
 // from host-mapped memory into DState::ph — the LM's first flag number
 // replaces seq0, and the recut-done flag the margi prefix waits for
 // (vg_ctx::d_sync[3]) is raised here (the recut's kernels have ended)
+// fin (an asynchronous recut, map_recut): tras_opt's factor bookkeeping
+// (k_factor_finish_dev's work: opt_state = factor index, the factors' eigen
+// and cluster copies) over the whole grid, beside the LM state in workgroup 0 —
+// one launch fewer on the chain
 __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict__ hl, double* __restrict__ hl_part,
                                                  int nout, MpRing ring, int* __restrict__ mpring, int W,
                                                  const int* __restrict__ rc_status, int seq0, double* __restrict__ rpart,
-                                                 int nrb, const int* __restrict__ ph, unsigned* __restrict__ rc_flag) {
-  for (int b = threadIdx.x; b < nrb; b += blockDim.x)  // empty residual slots (resid_bookkeeping)
+                                                 int nrb, const int* __restrict__ ph, unsigned* __restrict__ rc_flag,
+                                                 int fin, DevMap m, const int* __restrict__ fac_node,
+                                                 double* __restrict__ fac_eig, Clu* __restrict__ fac_pcr) {
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x, gn = gridDim.x * blockDim.x;
+  if (fin && !(rc_status && *rc_status)) {
+    const int nf = m.counters[kCntFactors];
+    for (int a = gt; a < nf; a += gn) {
+      const int node = fac_node[a];
+      m.hdr[node].opt_state = a;
+      for (int j = 0; j < 12; j++) fac_eig[(size_t)a * 12 + j] = m.eig[(size_t)node * 12 + j];
+      fac_pcr[a] = m.pcr_add[node];
+    }
+  }
+  for (int b = gt; b < nrb; b += gn)  // empty residual slots (resid_bookkeeping)
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(rpart + b), kRpartEmpty, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-  for (int t = threadIdx.x; t < nout; t += blockDim.x) {
+  for (int t = gt; t < nout; t += gn) {
     hl[t] = 0.0;
     hl_part[t] = 0.0;
   }
+  if (blockIdx.x != 0) return;
   if ((int)threadIdx.x < W) mpring[threadIdx.x] = ring.mp[threadIdx.x];
   if (threadIdx.x == 0) {
     const int skip = (rc_status && *rc_status) ? 1 : 0;  // an asynchronous recut that needs the host: skip
@@ -1411,8 +1428,12 @@ static void ba_init_kernel(vg_ctx* ctx, const int* mp_ring, int seq0) {
   // the IMU records are in DState's ring (k_push_state), the mp ring rides in k_ba_init's arguments
   MpRing ring;
   for (int i = 0; i < kMaxW; i++) ring.mp[i] = i < W ? mp_ring[i] : 0;
-  k_ba_init<<<1, 256, 0, ctx->stream>>>(d.st, d.hl, ctx->ba.hout_part, nout, ring, d.mpring, W, map_rc_status(ctx),
-                                        seq0, d.rpart, kResidBlocks, seq0 > 0 ? nullptr : ctx->st->ph, ctx->d_sync + 3);
+  const bool fin = ctx->rc_finish_in_init;  // the asynchronous recut left tras_opt's bookkeeping to this launch
+  ctx->rc_finish_in_init = false;
+  k_ba_init<<<fin ? 64 : 1, 256, 0, ctx->stream>>>(d.st, d.hl, ctx->ba.hout_part, nout, ring, d.mpring, W,
+                                                    map_rc_status(ctx), seq0, d.rpart, kResidBlocks,
+                                                    seq0 > 0 ? nullptr : ctx->st->ph, ctx->d_sync + 3, fin ? 1 : 0,
+                                                    ctx->map, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr);
 }
 
 // the scan graph's LM part (pipeline.cpp stage_insert_recut), captured on the

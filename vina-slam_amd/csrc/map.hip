@@ -2575,6 +2575,15 @@ __global__ void __launch_bounds__(256) k_factor_finish_dev(const int* __restrict
   }
 }
 const int* map_rc_status(vg_ctx* ctx) { return ctx->wk.rc + kRcStatus; }
+// the factor bookkeeping an asynchronous recut left to a k_ba_init that did not come
+int map_factor_finish(vg_ctx* ctx) {
+  if (!ctx->rc_finish_in_init) return VG_OK;
+  ctx->rc_finish_in_init = false;
+  k_factor_finish_dev<<<64, 256, 0, ctx->stream>>>(ctx->wk.rc, ctx->map, ctx->ba.fac_node, ctx->ba.fac_eig,
+                                                   ctx->ba.fac_pcr);
+  VG_HIP(hipGetLastError());
+  return VG_OK;
+}
 
 // Test-only (vgx_memo_probe): the IEKF memo at centre planes. For every
 // internal node, points exactly on its centre plane along each axis (the
@@ -2743,7 +2752,11 @@ static int map_recut_impl(vg_ctx* ctx, const MP& mp, const WinArg& wa, int threa
     const int max_fac = (ctx->dbg_fac_max >= 0 && ctx->dbg_fac_max < kFacMax) ? ctx->dbg_fac_max : kFacMax;
     k_fac_sort<<<1, 1024, 0, s>>>(m, w.rc, w.cand_bits, ctx->ba.fac_node, ctx->ba.cap_f, ctx->d_pub,
                                   &ctx->st->rc_ctr, max_fac);
-    k_factor_finish_dev<<<64, 256, 0, s>>>(w.rc, m, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr);
+    if (ctx->rc_init_finish) {  // the LM's k_ba_init (next on the stream) does tras_opt's bookkeeping
+      ctx->rc_finish_in_init = true;
+    } else {
+      k_factor_finish_dev<<<64, 256, 0, s>>>(w.rc, m, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr);
+    }
     VG_HIP(hipGetLastError());
     *n_factors = -1;
     return VG_OK;

@@ -803,6 +803,9 @@ static int stage_insert_recut(vg_ctx* ctx) {
   prof_begin(ctx, kProfInsert);
   VG_HIP(hipGraphLaunch(ge, ctx->stream));
   prof_end(ctx, kProfInsert);
+  // the insert + recut graph's asynchronous recut leaves tras_opt's factor
+  // bookkeeping to the LM's k_ba_init (the scan graph holds that k_ba_init)
+  if (!sg) ctx->rc_finish_in_init = ctx->rc_init_finish;
   if (sg) {  // nothing to record: the prefix and the next downsample order themselves on the flags
     ctx->ins_ev_pending = false;
     ctx->tail_a_valid = true;  // the next IEKF waits for this graph's tail (device flags)
@@ -963,6 +966,7 @@ static int margi_enqueue(vg_ctx* ctx, HostPipe* P, const int* gate, int* seq1, i
   const vg_config& c = ctx->cfg;
   const WinArg wa = make_winarg(P, 1);
   P->tail_wa = wa;
+  VG_TRY(map_factor_finish(ctx));  // an asynchronous recut no k_ba_init followed (stage API without the LM)
   *seq1 = ++ctx->pub_seq;
   *seq2 = ++ctx->pub_seq;
   if (!P->prefix) {
@@ -1145,6 +1149,7 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   // and this scan's IEKF instead of behind the IEKF's enqueue. The IEKF then
   // opens the main stream's critical path.
   HostPipe* P = hp(ctx);
+  host_delay(5);
   const bool early = ctx->ds_early && ctx->want_ds_stream && !P->in_scan && P->sticky == VG_OK && !ctx->prof_stages;
   if (early) {
     HostTimer ht_(ctx, kHostDownsample);

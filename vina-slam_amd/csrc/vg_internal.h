@@ -486,7 +486,9 @@ struct vg_ctx {
   bool margi_batch = true;    // vgx_debug 24: k_margi_leaf reads a leaf's frame clusters four at a time (r04k +0.4 %)
   bool margi_fused = true;    // margi isexist bottom-up in k_margi_copy, erase in one launch (vgx_debug 21: 0 = per-level launches)
   bool iekf_prefetch = true;  // vgx_debug 23: k_iekf touches a cached match's plane record beside its header (r04i A/B +0.9 %)
-  bool ba_structural = true;  // vgx_debug 31: k_ba_prep's structural elimination order (0: Eigen's |diag| order)
+  bool ba_structural = true;
+  bool rc_init_finish = true;     // vgx_debug 32: the asynchronous recut's factor bookkeeping inside k_ba_init (0: k_factor_finish_dev)
+  bool rc_finish_in_init = false; // set by map_recut for the next k_ba_init  // vgx_debug 31: k_ba_prep's structural elimination order (0: Eigen's |diag| order)
   bool ba_fuse_ctl = true;    // vgx_debug 19: the LM bookkeeping in k_ba_resid's IMU workgroup (A/Bs r04e 0, r04g/h +0.8-0.9 %)
   bool ba_graph = true;      // LM iterations replay one captured graph each (vgx_debug 15: 0 = direct launches)
   bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)
@@ -688,7 +690,8 @@ int map_recut(vg_ctx* ctx, const MP& mp, const WinArg& wa, int thread_num, int* 
               int pub_seq = 0);
 int map_recut_resume(vg_ctx* ctx, const MP& mp, int* n_factors);
 int map_set_attrs(vg_ctx* ctx);
-const int* map_rc_status(vg_ctx* ctx);  // the asynchronous recut's status word (k_fac_sort)
+const int* map_rc_status(vg_ctx* ctx);
+int map_factor_finish(vg_ctx* ctx);  // k_factor_finish_dev when no k_ba_init took it (map.hip)  // the asynchronous recut's status word (k_fac_sort)
 int map_memo_probe(vg_ctx* ctx, const MP& mp, int* out);  // test-only (vgx_memo_probe)
 int iekf_grid(vg_ctx* ctx);  // k_iekf's workgroups (map.hip iekf_blocks)
 int sync_set(vg_ctx* ctx, hipStream_t s, int k, unsigned value, const int* gate = nullptr);  // state.hip: cross-stream flags
