@@ -113,12 +113,12 @@ def test_recut_replay_path_equals_fast_path(knob):
                                          ({23: 0}, {}, True), ({24: 0}, {}, True), ({11: 0}, {}, True),
                                          ({16: 0}, {}, True), ({17: 0}, {}, True), ({14: 0}, {}, True),
                                          ({26: 0}, {}, True), ({27: 0}, {}, True), ({32: 0}, {}, True),
-                                         ({31: 0}, {}, False)],
+                                         ({33: 0}, {}, True), ({31: 0}, {}, False)],
                          ids=["lm-bookkeeping-in-resid", "margi-exist-up", "device-propagation",
                               "iekf-plane-prefetch", "margi-batched-cluster-loads", "recut-fused-levels",
                               "root-registration-lookback", "lm-two-iteration-graph", "flag-hand-offs",
                               "lm-outcome-deferred", "scan-graph", "factor-bookkeeping-in-ba-init",
-                              "lm-structural-order"])
+                              "recut-head-in-push-window", "lm-structural-order"])
 def test_fused_launches_equal_separate(ka, kb, exact):
     """Every default-on launch fusion or hand-off of the scan chain against its
     separate-launch form (vgx_debug knobs), bit for bit: k_ba_control inside
@@ -134,8 +134,9 @@ def test_fused_launches_equal_separate(ka, kb, exact):
     the first window-full scans need more LM iterations than predicted, so
     the real margi tail replaces a speculative one there), the scan graph
     (27: insert + recut + LM + margi tail as one replayed graph per ring
-    position, hand-offs on device flags) and tras_opt's factor bookkeeping
-    inside k_ba_init (32); the LM system's structural elimination order
+    position, hand-offs on device flags), tras_opt's factor bookkeeping
+    inside k_ba_init (32) and the recut's head inside the insert's
+    k_push_window (33); the LM system's structural elimination order
     against Eigen's |diag| order (31) agrees within rounding (counters exact,
     poses within 1e-12 m)."""
     p = vgconfig.load("mid360")

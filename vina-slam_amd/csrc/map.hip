@@ -1148,18 +1148,40 @@ constexpr int kPwBits = 1 << 16;  // point indices per bitmap window of k_push_w
 constexpr int kPwWords = kPwBits / 32;
 constexpr int kPwRankMax = 256;  // longest segment ordered by ranking (the bitmap's cost is its index range)
 static_assert(kPwWords * 4 <= 64 * kErec * 8, "the ordering bitmap lives in the wave's record buffer");
+// the recut's head (k_make_win_recut_begin's work) riding in the insert's
+// last launch as one extra workgroup: the window view and the level counters
+// need only the insert's counts, and the recut's first level starts one launch
+// boundary earlier (the insert + recut graph, map_insert's rb)
+struct RcBeginArg {
+  WinArg wa;
+  DState* st;
+  const int* wpn;
+  WinD* win;
+  int* nper;
+  int* slot_of;
+  int* rc;
+};
+__device__ __forceinline__ void recut_begin_block(DevMap& m, int* __restrict__ rc, int thread_num);
 __global__ void __launch_bounds__(64 * kPushWaves, 4) k_push_window(const int* __restrict__ seg_leaf,
                                                                  const int* __restrict__ seg_off,
                                                                  const int* __restrict__ order,
                                                                  int* __restrict__ order2, MP mp, int slot, DevMap m,
-                                                                 const double* __restrict__ pw, int thread_num) {
+                                                                 const double* __restrict__ pw, int thread_num,
+                                                                 RcBeginArg rb, int has_rb) {
   __shared__ double E[kPushWaves][64][kErec];
+  if (has_rb && blockIdx.x == gridDim.x - 1) {
+    make_win_block(rb.st, rb.wa, rb.wpn, rb.win, rb.nper, rb.slot_of);
+    __syncthreads();
+    recut_begin_block(m, rb.rc, thread_num);
+    return;
+  }
   if (ins_skip(m, thread_num)) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int role = lane < 63 ? lane : -1;
   RoleIdx ri = role < 9 ? role_clu(role < 0 ? 0 : role, kEq) : role < 18 ? role_clu(role - 9, kEp) : role_cov(role - 18);
   const int nseg = m.counters[kCntSeg];
-  for (int sg = blockIdx.x * kPushWaves + wv; sg < nseg; sg += gridDim.x * kPushWaves) {
+  const int gsz = (int)gridDim.x - (has_rb ? 1 : 0);
+  for (int sg = blockIdx.x * kPushWaves + wv; sg < nseg; sg += gsz * kPushWaves) {
     const int j0 = seg_off[sg], L = seg_off[sg + 1] - j0;
     const int leaf = seg_leaf[sg];
     // the leaf's points in index order (the reference's push order): up to 64
@@ -1492,8 +1514,24 @@ static int insert_tail(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_nu
   k_ins_resolve<<<g * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(n, nd, thread_num, w.pw, m, w.leaf, seg_leaf);
   k_seg_offsets<<<1, 1024, 0, s>>>(thread_num, m, seg_leaf, seg_off);
   k_ins_scatter<<<g * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(n, nd, thread_num, m, w.leaf, seg_off, order);
-  // ~one wave per leaf segment (the count stays on the device)
-  k_push_window<<<gseg, 64 * kPushWaves, 0, s>>>(seg_leaf, seg_off, order, order2, mp, slot, m, w.pw, thread_num);
+  // ~one wave per leaf segment (the count stays on the device); plus the
+  // recut's head when the recut follows in the same graph (ctx->rc_begin_wa)
+  RcBeginArg rb;
+  memset(&rb, 0, sizeof(rb));
+  const bool has_rb = ctx->rc_begin_wa != nullptr;
+  if (has_rb) {
+    rb.wa = *ctx->rc_begin_wa;
+    rb.st = ctx->st;
+    rb.wpn = m.wpn;
+    rb.win = (WinD*)ctx->ba.xs;
+    rb.nper = (int*)((char*)ctx->ba.xs + sizeof(WinD));
+    rb.slot_of = rb.nper + 32;  // (map_recut's dslot)
+    rb.rc = w.rc;
+    ctx->rc_begin_wa = nullptr;
+    ctx->rc_begun = true;
+  }
+  k_push_window<<<gseg + (has_rb ? 1 : 0), 64 * kPushWaves, 0, s>>>(seg_leaf, seg_off, order, order2, mp, slot, m, w.pw,
+                                                                     thread_num, rb, has_rb ? 1 : 0);
   VG_HIP(hipGetLastError());
   return VG_OK;
 }
@@ -2710,7 +2748,11 @@ static int map_recut_impl(vg_ctx* ctx, const MP& mp, const WinArg& wa, int threa
   for (int i = 0; i < wa.win_count; i++) total += wa.nper[i];
   ctx->rc_total = total;
   ctx->rc_thread_num = thread_num;
-  k_make_win_recut_begin<<<1, 256, 0, s>>>(ctx->st, wa, ctx->map.wpn, dwin, dn, dslot, m, w.rc, thread_num);
+  if (ctx->rc_begun) {  // done by the insert's k_push_window (the same graph)
+    ctx->rc_begun = false;
+  } else {
+    k_make_win_recut_begin<<<1, 256, 0, s>>>(ctx->st, wa, ctx->map.wpn, dwin, dn, dslot, m, w.rc, thread_num);
+  }
   if (sharded(ctx)) {
     if (!replay) {  // the global slide count (a replay re-uses it: the insert replay does not change it)
       VG_TRY(shard_allreduce(ctx, m.counters + kCntGSlide, ctx->shard.d_buf + 512, 1, 1, 2));

@@ -786,8 +786,10 @@ static int stage_insert_recut(vg_ctx* ctx) {
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     ctx->capturing = true;
     ctx->in_ph = sg;
+    ctx->rc_begin_wa = ctx->rc_begin_fold ? &wa : nullptr;  // the recut's head rides in the insert's last launch
     int nf = 0;
     int r = map_insert(ctx, P->mpd, slot, cap, P->epoch, c.thread_num, &P->push, nullptr, ctx->ds.hflags + 1);
+    ctx->rc_begin_wa = nullptr;
     ctx->in_ph = false;
     if (r == VG_OK) r = map_recut(ctx, P->mpd, wa, c.thread_num, &nf, false, 1);
     if (r == VG_OK && sg) r = ba_capture_scan_lm(ctx, P->mp.data());

@@ -488,7 +488,10 @@ struct vg_ctx {
   bool iekf_prefetch = true;  // vgx_debug 23: k_iekf touches a cached match's plane record beside its header (r04i A/B +0.9 %)
   bool ba_structural = true;
   bool rc_init_finish = true;     // vgx_debug 32: the asynchronous recut's factor bookkeeping inside k_ba_init (0: k_factor_finish_dev)
-  bool rc_finish_in_init = false; // set by map_recut for the next k_ba_init  // vgx_debug 31: k_ba_prep's structural elimination order (0: Eigen's |diag| order)
+  bool rc_finish_in_init = false; // set by map_recut for the next k_ba_init
+  bool rc_begin_fold = true;      // vgx_debug 33: the recut's head in the insert's k_push_window (insert + recut graph)
+  const vg::WinArg* rc_begin_wa = nullptr;  // set for one map_insert: its k_push_window runs the recut's head
+  bool rc_begun = false;          // ... and the map_recut after it skips k_make_win_recut_begin  // vgx_debug 31: k_ba_prep's structural elimination order (0: Eigen's |diag| order)
   bool ba_fuse_ctl = true;    // vgx_debug 19: the LM bookkeeping in k_ba_resid's IMU workgroup (A/Bs r04e 0, r04g/h +0.8-0.9 %)
   bool ba_graph = true;      // LM iterations replay one captured graph each (vgx_debug 15: 0 = direct launches)
   bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)

@@ -918,6 +918,10 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     ctx->ba_graph = value != 0;
     return VG_OK;
   }
+  if (key == 33) {  // 0: k_make_win_recut_begin as its own launch in the insert + recut graph
+    ctx->rc_begin_fold = value != 0;
+    return VG_OK;
+  }
   if (key == 32) {  // 0: k_factor_finish_dev after k_fac_sort instead of inside k_ba_init
     ctx->rc_init_finish = value != 0;
     return VG_OK;
