@@ -1199,7 +1199,8 @@ __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict
                                                  int fin, DevMap m, const int* __restrict__ fac_node,
                                                  double* __restrict__ fac_eig, Clu* __restrict__ fac_pcr) {
   const int gt = blockIdx.x * blockDim.x + threadIdx.x, gn = gridDim.x * blockDim.x;
-  if (fin && !(rc_status && *rc_status)) {
+  const int status = rc_status ? *rc_status : 0;
+  if (fin && !status) {
     const int nf = m.counters[kCntFactors];
     for (int a = gt; a < nf; a += gn) {
       const int node = fac_node[a];
@@ -1218,7 +1219,7 @@ __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict
   if (blockIdx.x != 0) return;
   if ((int)threadIdx.x < W) mpring[threadIdx.x] = ring.mp[threadIdx.x];
   if (threadIdx.x == 0) {
-    const int skip = (rc_status && *rc_status) ? 1 : 0;  // an asynchronous recut that needs the host: skip
+    const int skip = status ? 1 : 0;  // an asynchronous recut that needs the host: skip
     st->u = 0.01;
     st->v = 2;
     st->res1 = st->res2 = st->q1 = 0.0;

@@ -1083,7 +1083,6 @@ __global__ void __launch_bounds__(256) k_ins_resolve(int n_arg, const int* __res
   }
 }
 
-__device__ __forceinline__ int block_excl_scan(int v, int* s_wsum, int* total);
 // one workgroup: segment offsets = prefix over the segments' point counts;
 // the counts return to zero (k_ins_scatter counts the fill again)
 __global__ void __launch_bounds__(1024) k_seg_offsets(int thread_num, DevMap m, const int* __restrict__ seg_leaf,
@@ -1332,33 +1331,6 @@ __device__ __forceinline__ void alloc_parent(DevMap& m, int p, int id0, int* nex
     if (next) next[next_pos + k - 1] = id;
   }
   m.nscr[(size_t)p * 4 + 1] = -1;
-}
-
-// exclusive prefix over one value per thread of a 1024-lane workgroup
-__device__ __forceinline__ int block_excl_scan(int v, int* s_wsum, int* total) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    int y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
-  if (lane == 63) s_wsum[wv] = x;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int acc = 0;
-    for (int k = 0; k < (int)(blockDim.x >> 6); k++) {
-      int t = s_wsum[k];
-      s_wsum[k] = acc;
-      acc += t;
-    }
-    s_wsum[16] = acc;
-  }
-  __syncthreads();
-  const int r = s_wsum[wv] + x - v;
-  *total = s_wsum[16];
-  __syncthreads();
-  return r;
 }
 
 // ascending bitonic sort of n (power of two) keys in LDS by the whole workgroup
@@ -1610,8 +1582,6 @@ int map_insert_replay(vg_ctx* ctx, const MP& mp, int slot, int n, int thread_num
 // k_rc_apply sets rc[kRcAbort]; the host then replays the rest of the recut
 // with the host-sized path (recut_slow_apply), which only happens while the
 // map is first built.
-enum { kRcLvl = 0, kRcSub = 16, kRcWin = 32, kRcAbort = 48, kRcCh = 64, kRcChBase = 80, kRcNch = 96, kRcTot = 104,
-       kRcNode0 = 112, kRcStatus = 126, kRcNOld = 127, kRcN = 128 };
 constexpr int kApplyThreads = 1024;
 constexpr int kApplySub = kApplyThreads;  // subdividing leaves per level (one lane each)
 
@@ -2563,42 +2533,10 @@ __global__ void k_make_win_recut_begin(DState* __restrict__ st, WinArg wa, const
 // leaves the status in rc[kRcStatus], where k_ba_init reads it: a recut that
 // needs the host-sized path (insert replay, level overflow, more factors than
 // max_fac) makes the LM skip, and the host completes the recut and reruns it.
-constexpr int kFacMax = 1 << 20;
-constexpr int kRcBig = 200;
 __global__ void __launch_bounds__(1024) k_fac_sort(DevMap m, int* __restrict__ rc, uint32_t* __restrict__ bits,
                                                    int* __restrict__ fac_node, int cap_f, Pub* __restrict__ pub,
                                                    int* __restrict__ seq_ctr, int max_fac) {
-  __shared__ int s_w[17];
-  const int nf = m.counters[kCntFactors];
-  int status = rc[kRcAbort];
-  if (status == 0 && (nf > cap_f || nf > max_fac)) status = kRcBig;
-  const int words = (m.counters[kCntNodes] + 31) >> 5;
-  const int per = (words + (int)blockDim.x - 1) / (int)blockDim.x;
-  const int w0 = threadIdx.x * per, w1 = min(words, w0 + per);
-  int cnt = 0;
-  for (int w = w0; w < w1; w++) cnt += __popc(bits[w]);
-  int total;
-  int pos = block_excl_scan(cnt, s_w, &total);
-  if (status == 0 && total != nf) status = kRcBig;  // the two counts disagree: let the host path decide
-  for (int w = w0; w < w1; w++) {
-    uint32_t b = bits[w];
-    if (b == 0) continue;
-    bits[w] = 0;
-    if (status == 0)
-      while (b) {
-        const int k = __ffs(b) - 1;
-        b &= b - 1;
-        fac_node[pos++] = (w << 5) + k;
-      }
-  }
-  if (threadIdx.x == 0) {
-    const int seq = *seq_ctr + 1;  // the device's count of asynchronous recuts (the host mirrors it)
-    *seq_ctr = seq;
-    rc[kRcStatus] = status;
-    pub_store(&pub->rc_status, status);
-    pub_store(&pub->rc_nf, nf);
-    pub_flag(&pub->seq_rc, seq);
-  }
+  fac_sort_block(m, rc, bits, fac_node, cap_f, pub, seq_ctr, max_fac);
 }
 __global__ void __launch_bounds__(256) k_factor_finish_dev(const int* __restrict__ rc, DevMap m,
                                                            const int* __restrict__ fac_node,

@@ -485,4 +485,78 @@ __device__ __forceinline__ void make_win_block(DState* __restrict__ st, const Wi
     if (wa.set_xc) st->jour_check = wa.jour_check;  // the margi head (k_slide_compact reads it)
   }
 }
+// exclusive prefix over one value per thread of a 1024-lane workgroup
+__device__ __forceinline__ int block_excl_scan(int v, int* s_wsum, int* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_wsum[wv] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); k++) {
+      int t = s_wsum[k];
+      s_wsum[k] = acc;
+      acc += t;
+    }
+    s_wsum[16] = acc;
+  }
+  __syncthreads();
+  const int r = s_wsum[wv] + x - v;
+  *total = s_wsum[16];
+  __syncthreads();
+  return r;
+}
+
+
+// the recut / margi device-side counts (Work::rc)
+enum { kRcLvl = 0, kRcSub = 16, kRcWin = 32, kRcAbort = 48, kRcCh = 64, kRcChBase = 80, kRcNch = 96, kRcTot = 104,
+       kRcNode0 = 112, kRcStatus = 126, kRcNOld = 127, kRcN = 128 };
+
+// tras_opt's factor list (octree.cpp:491-516): the candidate bitmap over node
+// ids -> the id-ascending factor list, cleared as it is read; the recut status
+// (kRcBig: more factors than the device list holds) and the factor count
+// published. One workgroup (k_fac_sort)
+constexpr int kFacMax = 1 << 20;
+constexpr int kRcBig = 200;
+__device__ __forceinline__ void fac_sort_block(DevMap& m, int* __restrict__ rc, uint32_t* __restrict__ bits,
+                                               int* __restrict__ fac_node, int cap_f, Pub* __restrict__ pub,
+                                               int* __restrict__ seq_ctr, int max_fac) {
+  __shared__ int s_w[17];
+  const int nf = m.counters[kCntFactors];
+  int status = rc[kRcAbort];
+  if (status == 0 && (nf > cap_f || nf > max_fac)) status = kRcBig;
+  const int words = (m.counters[kCntNodes] + 31) >> 5;
+  const int per = (words + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int w0 = threadIdx.x * per, w1 = min(words, w0 + per);
+  int cnt = 0;
+  for (int w = w0; w < w1; w++) cnt += __popc(bits[w]);
+  int total;
+  int pos = block_excl_scan(cnt, s_w, &total);
+  if (status == 0 && total != nf) status = kRcBig;  // the two counts disagree: let the host path decide
+  for (int w = w0; w < w1; w++) {
+    uint32_t b = bits[w];
+    if (b == 0) continue;
+    bits[w] = 0;
+    if (status == 0)
+      while (b) {
+        const int k = __ffs(b) - 1;
+        b &= b - 1;
+        fac_node[pos++] = (w << 5) + k;
+      }
+  }
+  if (threadIdx.x == 0) {
+    const int seq = *seq_ctr + 1;  // the device's count of asynchronous recuts (the host mirrors it)
+    *seq_ctr = seq;
+    rc[kRcStatus] = status;
+    pub_store(&pub->rc_status, status);
+    pub_store(&pub->rc_nf, nf);
+    pub_flag(&pub->seq_rc, seq);
+  }
+}
+
 }  // namespace vg
