@@ -15,8 +15,8 @@ scan (and IEKF / LM iteration) they belong to:
     records, fp64 PlaneRec as the gate reads them);
   * the recut's level kernels (k_rc_level0 + max_layer x k_rc_level), per scan:
     V_slide (80 W + 80);
-  * k_ba_hess, executed launches (its Hessian passes, ba_hess per scan):
-    F (80 W + 176);
+  * k_ba_hess, executed launches (Hessian passes; the second LM iteration's
+    rides in k_ba_resid_hess): F (80 W + 176);
   * k_ba_solve, executed launches (no byte model: the LM step's flops).
 Counters are KiB per dispatch. `traffic` follows MI355X_MICROARCH.md: FETCH x2
 (on gfx950 FETCH_SIZE reports half the bytes of a 16 B/lane streaming read)
@@ -27,6 +27,7 @@ reported beside it as `fetch_calibrated`. Only scans >= first_scan (default
 and do not depend on how many the bench times. The per-scan P_k of those
 scans is kept (`per_scan`): the bench prices its own timed scans with them.
 """
+import bisect
 import csv
 import glob
 import json
@@ -47,7 +48,7 @@ def load(path):
         rows[short(r["Kernel_Name"])].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     for k in rows:
         rows[k].sort()
-    return {k: [v for _, v in rows[k]] for k in rows}
+    return {k: [v for _, v in rows[k]] for k in rows}, {k: [i for i, _ in rows[k]] for k in rows}
 
 
 def calibration(repo):
@@ -61,14 +62,14 @@ def calibration(repo):
 
 def summarise(pass_dir, counter):
     scans = json.load(open(os.path.join(pass_dir, "scans.json")))
-    rows = load(glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True)[0])
-    return scans, rows
+    rows, ids = load(glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True)[0])
+    return scans, rows, ids
 
 
 def main(src, dst, first):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    meta, fetch = summarise(os.path.join(src, "fetch"), "FETCH_SIZE")
-    meta_w, write = summarise(os.path.join(src, "write"), "WRITE_SIZE")
+    meta, fetch, fid = summarise(os.path.join(src, "fetch"), "FETCH_SIZE")
+    meta_w, write, _ = summarise(os.path.join(src, "write"), "WRITE_SIZE")
     S = meta["scans"]
     for other in (meta_w["scans"], json.load(open(os.path.join(src, "scans_pk.json")))["scans"]):
         assert [(s["n_raw"], s["n_ds"], s["iekf_iters"], s["n_factors"], s["ba_iters"]) for s in S] == \
@@ -127,18 +128,20 @@ def main(src, dst, first):
         pairs.append((fs, ws, S[s]["n_slide"] * (80.0 * W + 80.0)))
     out["kernels"]["recut_levels"] = entry("scan (k_rc_level0 + %d x k_rc_level)" % L, pairs,
                                            "V_slide (80 W + 80) per scan")
-    # k_ba_hess: executed launches in dispatch order, ba_hess of them per scan
+    # k_ba_hess: executed launches, each paired with its scan by dispatch order
+    # (a scan's launches follow its four k_iekf dispatches). A scan has at most
+    # ba_hess of them: the second LM iteration's pass rides in k_ba_resid_hess
     fh, wh = fetch.get("k_ba_hess", []), write.get("k_ba_hess", [])
+    starts = fid["k_iekf"][0::4]
     ex = [i for i, v in enumerate(fh) if v > 64.0]  # an early exit fetches a few KiB
-    need = sum(s["ba_hess"] for s in S)
-    assert len(ex) == need, ("k_ba_hess executed launches", len(ex), need)
-    pairs, q = [], 0
-    for s in range(ns):
-        for _ in range(S[s]["ba_hess"]):
-            d = ex[q]
-            q += 1
-            if s >= first:
-                pairs.append((fh[d], wh[d], S[s]["n_factors"] * (80.0 * W + 176.0)))
+    per = [0] * ns
+    pairs = []
+    for d in ex:
+        s = bisect.bisect_right(starts, fid["k_ba_hess"][d]) - 1
+        per[s] += 1
+        if s >= first:
+            pairs.append((fh[d], wh[d], S[s]["n_factors"] * (80.0 * W + 176.0)))
+    assert all(0 <= s and per[s] <= S[s]["ba_hess"] for s in range(ns)), ("k_ba_hess launches per scan", per)
     out["kernels"]["k_ba_hess"] = entry("launch (executed Hessian pass)", pairs, "F (80 W + 176) per pass")
     # k_ba_solve: executed launches (traffic only)
     fs_, ws_ = fetch.get("k_ba_solve", []), write.get("k_ba_solve", [])

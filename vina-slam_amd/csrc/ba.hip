@@ -230,7 +230,15 @@ __device__ __forceinline__ int lower_idx(int r, int c) { return r * (r + 1) / 2 
 constexpr int kHessThreads = 512;  // 8 waves: a chunk's (factor, frame) lanes in one pass
 constexpr int kHessGridMax = 256;  // k_ba_hess chunk workgroups (more chunks loop)
 constexpr int kResidBlocks = 512;  // k_ba_resid workgroups (more chunks loop)
-__host__ __device__ constexpr int hess_fs(int W) { return kHessThreads / W < 64 ? kHessThreads / W : 64; }  // factors per sub-chunk
+constexpr int kResidThreads = 256;  // k_ba_resid's workgroup (its chunking and residual order)
+// factors per sub-chunk: two of k_ba_resid's chunks (256 / W factors) where
+// that fits the lanes and the 64-row cap (W >= 8), so a Hessian chunk holds
+// whole residual chunks (k_ba_resid_hess); else min(512 / W, 64)
+__host__ __device__ constexpr int hess_fs(int W) {
+  return 2 * (256 / W) <= 64 && 2 * (256 / W) <= kHessThreads / W ? 2 * (256 / W)
+                                                                    : (kHessThreads / W < 64 ? kHessThreads / W : 64);
+}
+__host__ __device__ constexpr bool resid_hess_ok(int W) { return hess_fs(W) == 2 * (256 / W) && 256 / W <= 64; }
 __host__ __device__ constexpr int hess_ks(int W) { return (3 * hess_fs(W) + 3) / 4 * 4; }  // GEMM K per sub-chunk
 __host__ __device__ constexpr int hess_nt(int W) { return (6 * W + 15) / 16; }           // 16-wide output tiles
 __host__ __device__ constexpr int hess_xs(int W) { return hess_nt(W) * 16 + 16; }        // X row stride (+16: rows k, k+1 in opposite LDS halves)
@@ -242,10 +250,24 @@ __host__ __device__ constexpr int hess_chunk(int W) { return hess_fs(W); }      
 // X (LDS); the off-diagonal blocks are then X^T S X on v_mfma_f64_16x16x4
 // (one wave per lower 16x16 output tile, accumulators live across
 // sub-chunks). Chunk partials go to `part` (summed by k_ba_hfinal).
+// kSpec (k_ba_resid_hess): the pass at the LM's trial state, `xs` = the trial
+// states. The chunk first does k_ba_resid's work for its factors —
+// evaluate_only_residual: frame clusters moved to the trial poses, merged onto
+// pcr_fix in frame order, 3x3 eigen, fac_eig / fac_pcr written — with
+// k_ba_resid's operations, then evaluates the Hessian from those values (LDS)
+// instead of fac_eig / fac_pcr. ev0[0] / ev0[1] take each lane's smallest
+// eigenvalues for the two residual chunks the Hessian chunk holds.
+template <bool kSpec = false>
 __device__ __forceinline__ void hess_chunk_eval(int ch, int nf, int W, const int* __restrict__ fac_node,
                                                 const double* __restrict__ fac_eig, const Clu* __restrict__ fac_pcr,
                                                 const Clu* __restrict__ pcrs, const int* __restrict__ mpring,
-                                                const double* __restrict__ xs, double* __restrict__ part) {
+                                                const double* __restrict__ xs, double* __restrict__ part,
+                                                const Clu* __restrict__ pcr_fix = nullptr,
+                                                double* __restrict__ eig_out = nullptr,
+                                                Clu* __restrict__ pcr_out = nullptr, double* ev0 = nullptr,
+                                                const double* __restrict__ eig_src = nullptr,
+                                                const Clu* __restrict__ pcr_src = nullptr,
+                                                NodeHdr* __restrict__ hdr = nullptr) {
   __syncthreads();  // the previous chunk's reduction has read the LDS
   extern __shared__ __attribute__((aligned(16))) double X[];
   __shared__ double S[kHessThreads];
@@ -257,6 +279,44 @@ __device__ __forceinline__ void hess_chunk_eval(int ch, int nf, int W, const int
   const int a_begin = ch * hess_chunk(W);
   const int a_end = min(nf, a_begin + hess_chunk(W));
   const int ntl = NT * (NT + 1) / 2;
+  __shared__ double s_e[kSpec ? 64 : 1][12];  // kSpec: the chunk's eigen systems and merged clusters at the trial
+  __shared__ Clu s_pa[kSpec ? 64 : 1];
+  if constexpr (kSpec) {
+    Clu* s_t = reinterpret_cast<Clu*>(X);  // the moved frame clusters (X is filled below)
+    {
+      const int a = a_begin + f;
+      if (active && a < a_end) {
+        const Clu src = pcrs[(size_t)fac_node[a] * W + mpring[i]];
+        Clu t;
+        if (src.N != 0) {
+          t = clu_transform(src, ld_m3(&xs[(size_t)i * kX]), ld_v3(&xs[(size_t)i * kX + 9]));
+        } else {
+          clu_zero(t);
+          t.N = 0;
+        }
+        s_t[tid] = t;
+      }
+    }
+    __syncthreads();
+    const int a2 = a_begin + tid;
+    if (tid < FS && a2 < a_end) {
+      Clu sig = pcr_fix[fac_node[a2]];
+      for (int k = 0; k < W; k++) {
+        const Clu& t = s_t[tid * W + k];
+        if (t.N != 0) clu_add(sig, t);
+      }
+      V3 ev;
+      M3 U;
+      eig3(clu_cov(sig), ev, U);
+      double* e = &eig_out[(size_t)a2 * 12];
+      for (int j = 0; j < 3; j++) e[j] = s_e[tid][j] = ev[j];
+      for (int j = 0; j < 9; j++) e[3 + j] = s_e[tid][3 + j] = U[j];
+      pcr_out[a2] = sig;
+      s_pa[tid] = sig;
+      ev0[tid < FS / 2 ? 0 : 1] += 1.0 * ev[0];  // k_ba_resid's acc (lane tid mod FS/2 of its chunk)
+    }
+    __syncthreads();  // s_t is read: X may be cleared
+  }
   // A chunk is one sub-chunk (hess_chunk == hess_fs): the lane's factor_frame
   // writes its diagonal block and gradient straight into hb / jj (0 + coe x,
   // the accumulation's value), so no second copy is live beside the call
@@ -269,8 +329,16 @@ __device__ __forceinline__ void hess_chunk_eval(int ch, int nf, int W, const int
     const int a = a_begin + f;
     bool got = false;
     if (active && a < a_end) {
-      const double* e = &fac_eig[(size_t)a * 12];
-      const Clu pa = fac_pcr[a];
+      const int node = fac_node[a];
+      // eig_src (k_ba_init_hess): tras_opt's bookkeeping in this pass, the
+      // factor's eigen system and cluster read from the map and copied out
+      const double* e = kSpec ? s_e[f] : (eig_src ? &eig_src[(size_t)node * 12] : &fac_eig[(size_t)a * 12]);
+      const Clu pa = kSpec ? s_pa[f] : (eig_src ? pcr_src[node] : fac_pcr[a]);
+      if (!kSpec && eig_src && i == 0) {
+        for (int j = 0; j < 12; j++) eig_out[(size_t)a * 12 + j] = e[j];
+        pcr_out[a] = pa;
+        hdr[node].opt_state = a;
+      }
       const double coe = 1.0;  // octree.cpp:507
       if (i == 0) {
         res = 0.0 + coe * e[0];
@@ -279,7 +347,7 @@ __device__ __forceinline__ void hess_chunk_eval(int ch, int nf, int W, const int
         S[3 * f + 1] = coe * (2.0 / (e[0] - e[2]));
         S[3 * f + 2] = -coe * (2.0 / NN / NN);
       }
-      const Clu sc = pcrs[(size_t)fac_node[a] * W + mpring[i]];
+      const Clu sc = pcrs[(size_t)node * W + mpring[i]];
       if (sc.N != 0) {
         double g1[6], g2[6], h[6];
         factor_frame(e, pa, sc, &xs[(size_t)i * kX], hb, jj, g1, g2, h);
@@ -516,7 +584,7 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
                                                  double* __restrict__ Jcalc, double* __restrict__ timg,
                                                  double* __restrict__ bvec, double* __restrict__ dvec,
                                                  double* __restrict__ jvec, int* __restrict__ ipg,
-                                                 const BaState* __restrict__ st, int structural) {
+                                                 BaState* __restrict__ st, int structural) {
   if (st->done) return;
   constexpr int kN = kMaxNB * kTile;
   __shared__ double Dv[kN], Jg[kN];
@@ -525,6 +593,13 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
   const int tid = threadIdx.x, q = blockIdx.x;
   const bool calc = st->calc_hess != 0;
   const double u = st->u;
+  if (calc && q == 0 && tid == 0) {  // residual1 of divide_thread at the current state (optimizers.cpp:454)
+    double r = 0.0;
+    for (int k = 0; k < nimu; k++) r += imuout[(size_t)k * 931 + 930];
+    r *= imu_coef * 0.5;
+    r += hl[L * (L + 1) / 2 + L];
+    st->res1 = r;
+  }
   for (int t = tid; t < n; t += blockDim.x)
     Dv[t] = t < 15 ? 1.0 : (calc ? asm_entry(t, t, nimu, imu_coef, hl, imuout, L) : Hcalc[lo(t, t)]);
   __syncthreads();
@@ -988,18 +1063,21 @@ struct CtlArg {
   Pub* pub;
   int* err;   // k_ba_resid runs the bookkeeping (nullptr: k_ba_control follows); error bit 64 on a stalled hand-off
 };
-// `pre`: the lane's strided sum of the residual partials, already formed (k_ba_resid)
+// `pre`: the lane's strided sum of the residual partials, already formed (k_ba_resid).
+// The sums run over the first kResidThreads lanes whatever the workgroup size
+// (k_ba_resid_hess's is 512), so the residual's order is k_ba_resid's.
 __device__ __forceinline__ void ba_control_body(const CtlArg& c, const double* pre = nullptr) {
   __shared__ int accept;
-  __shared__ double s_r[256];
+  __shared__ double s_r[kResidThreads];
+  const int nt = kResidThreads;
   {  // residual partials: lane-strided sums, then a fixed tree (deterministic)
     double part = 0.0;
     if (pre) part = *pre;
     else if (!c.st->done)
-      for (int b = threadIdx.x; b < c.nrb; b += blockDim.x) part += c.rpart[b];
-    s_r[threadIdx.x] = part;
+      for (int b = threadIdx.x; b < c.nrb; b += nt) part += c.rpart[b];
+    if ((int)threadIdx.x < nt) s_r[threadIdx.x] = part;
     __syncthreads();
-    for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
+    for (int w = nt >> 1; w > 0; w >>= 1) {
       if ((int)threadIdx.x < w) s_r[threadIdx.x] += s_r[threadIdx.x + w];
       __syncthreads();
     }
@@ -1007,14 +1085,8 @@ __device__ __forceinline__ void ba_control_body(const CtlArg& c, const double* p
   if (threadIdx.x == 0) {
     accept = -1;
     if (!c.st->done) {
+      // (residual1 of divide_thread at the current state: k_ba_prep, on the Hessian iterations)
       if (c.st->calc_hess) c.st->nhess += 1;
-      if (c.st->calc_hess) {  // residual1 of divide_thread at the current state
-        double r = 0.0;
-        for (int k = 0; k < c.nimu; k++) r += c.imuout[(size_t)k * 931 + 930];
-        r *= c.imu_coef * 0.5;
-        r += c.hl[c.nl];
-        c.st->res1 = r;
-      }
       double r1 = 0.0;
       for (int k = 0; k < c.nimu; k++) r1 += c.imures[k];
       r1 *= c.imu_coef * 0.5;
@@ -1077,7 +1149,7 @@ __device__ __forceinline__ void resid_bookkeeping(const CtlArg& c) {
   if (threadIdx.x == 0) s_late = 0;
   __syncthreads();
   double part = 0.0;  // k_ba_control's lane-strided order: slots t, t + 256, ...
-  for (int b = threadIdx.x; b < c.nrb; b += blockDim.x) {
+  for (int b = threadIdx.x; b < c.nrb && (int)threadIdx.x < kResidThreads; b += kResidThreads) {
     unsigned long long* p = reinterpret_cast<unsigned long long*>(const_cast<double*>(c.rpart) + b);
     unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int spin = 0; v == kRpartEmpty; spin++) {
@@ -1169,6 +1241,76 @@ __global__ void __launch_bounds__(256, 2) k_ba_resid(const int* __restrict__ nfp
   if (threadIdx.x == 0) rpart_put(&rpart[blockIdx.x], ((red[0] + red[1]) + red[2]) + red[3]);
 }
 
+// The first LM iteration's residual pass and, speculatively, the second
+// iteration's Hessian pass at the same trial state, as one launch
+// (vg_ctx::ba_resid_hess). An accepted step makes the trial the state
+// (optimizers.cpp:480-492), so the second iteration's Hessian is the one of
+// the trial poses: every chunk workgroup does k_ba_resid's work for its
+// factors (hess_chunk_eval<true>) and goes straight on to their Hessian, so
+// the second iteration needs no k_ba_hess launch. A rejected step leaves the
+// Hessian unused (calc_hess = 0: k_ba_hfinal / k_ba_prep take the stored
+// system). Layout: workgroups [0, kResidBlocks / 2) the Hessian chunks c, c +
+// kResidBlocks / 2, ... (hess_fs = 2 x k_ba_resid's chunk: chunk c holds
+// residual chunks 2c and 2c + 1, and this workgroup stores their residual
+// partials exactly as k_ba_resid's workgroups 2c and 2c + 1 would); then the
+// IMU residuals + the LM bookkeeping (resid_bookkeeping); then one workgroup
+// per IMU factor's Hessian block (imu_factor_block at the trial). Results are
+// bit-identical to k_ba_resid followed by k_ba_hess.
+constexpr int kRhChunkWg = kResidBlocks / 2;
+__global__ void __launch_bounds__(kHessThreads) k_ba_resid_hess(const int* __restrict__ nfp, int W,
+                                                                const int* __restrict__ fac_node,
+                                                                const Clu* __restrict__ pcr_fix,
+                                                                const Clu* __restrict__ pcrs,
+                                                                const int* __restrict__ mpring,
+                                                                const double* __restrict__ xt,
+                                                                double* __restrict__ fac_eig, Clu* __restrict__ fac_pcr,
+                                                                double* __restrict__ part, double* __restrict__ rpart,
+                                                                const BaState* st, int nimu,
+                                                                const double* __restrict__ imurec,
+                                                                const int* __restrict__ imu_head,
+                                                                const double* __restrict__ bias,
+                                                                double* __restrict__ imures, double* __restrict__ imuout,
+                                                                CtlArg ctl) {
+  const int G = kRhChunkWg;
+  if (st->done) {  // converged: the bookkeeping still publishes the flags
+    if ((int)blockIdx.x == G) ba_control_body(ctl);
+    return;
+  }
+  if ((int)blockIdx.x == G) {  // IMU residuals at the trial state, then the bookkeeping (k_ba_resid's)
+    if ((int)threadIdx.x < nimu) imu_residual_lane(threadIdx.x, imurec, *imu_head, bias, xt, imures);
+    __syncthreads();
+    resid_bookkeeping(ctl);
+    return;
+  }
+  if ((int)blockIdx.x > G) {  // the IMU factors' Hessian blocks at the trial (k_ba_hess's IMU workgroups)
+    const int k = blockIdx.x - G - 1;
+    if (k < nimu) imu_factor_block(k, imurec, *imu_head, bias, xt, imuout);
+    return;
+  }
+  const int nf = *nfp;
+  const int nchunk = (nf + hess_chunk(W) - 1) / hess_chunk(W);
+  double ev0[2] = {0.0, 0.0};
+  for (int ch = blockIdx.x; ch < nchunk; ch += G)
+    hess_chunk_eval<true>(ch, nf, W, fac_node, nullptr, nullptr, pcrs, mpring, xt, part, pcr_fix, fac_eig, fac_pcr,
+                          ev0);
+  // the residual partials of chunks 2c and 2c + 1 in k_ba_resid's form: lane l
+  // of its wave 0 holds the chunk's factor l, the other waves hold zeros
+  if (threadIdx.x < 64) {
+    const int fr = 256 / W, lane = threadIdx.x;
+    double r0 = ev0[0];
+    double r1 = __shfl_down(ev0[1], fr, 64);
+    if (lane >= fr) r1 = 0.0;
+    for (int off = 32; off > 0; off >>= 1) r0 += __shfl_down(r0, off, 64);
+    for (int off = 32; off > 0; off >>= 1) r1 += __shfl_down(r1, off, 64);
+    double z = 0.0;  // waves 1-3 of k_ba_resid: an all-zero tree
+    for (int off = 32; off > 0; off >>= 1) z += __shfl_down(z, off, 64);
+    if (lane == 0) {
+      rpart_put(&rpart[2 * blockIdx.x], ((r0 + z) + z) + z);
+      rpart_put(&rpart[2 * blockIdx.x + 1], ((r1 + z) + z) + z);
+    }
+  }
+}
+
 // sharded mode: this shard's factor residual (ordered sum of the block partials)
 __global__ void k_ba_rsum(int nrb, const double* __restrict__ rpart, double* __restrict__ out,
                           const BaState* __restrict__ st) {
@@ -1192,6 +1334,11 @@ struct MpRing {
 // (k_factor_finish_dev's work: opt_state = factor index, the factors' eigen
 // and cluster copies) over the whole grid, beside the LM state in workgroup 0 —
 // one launch fewer on the chain
+__device__ __forceinline__ void ba_init_common(int gt, int gn, bool wg0, BaState* st, double* __restrict__ hl,
+                                               double* __restrict__ hl_part, int nout, const MpRing& ring,
+                                               int* __restrict__ mpring, int W, int status, int seq0,
+                                               double* __restrict__ rpart, int nrb, const int* __restrict__ ph,
+                                               unsigned* __restrict__ rc_flag);
 __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict__ hl, double* __restrict__ hl_part,
                                                  int nout, MpRing ring, int* __restrict__ mpring, int W,
                                                  const int* __restrict__ rc_status, int seq0, double* __restrict__ rpart,
@@ -1209,6 +1356,17 @@ __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict
       fac_pcr[a] = m.pcr_add[node];
     }
   }
+  ba_init_common(gt, gn, blockIdx.x == 0, st, hl, hl_part, nout, ring, mpring, W, status, seq0, rpart, nrb, ph,
+                 rc_flag);
+}
+// k_ba_init's part after the factor bookkeeping: the residual slots armed, the
+// Hessian accumulators cleared (grid-stride gt / gn), then (wg0) the ring and
+// the LM state
+__device__ __forceinline__ void ba_init_common(int gt, int gn, bool wg0, BaState* st, double* __restrict__ hl,
+                                               double* __restrict__ hl_part, int nout, const MpRing& ring,
+                                               int* __restrict__ mpring, int W, int status, int seq0,
+                                               double* __restrict__ rpart, int nrb, const int* __restrict__ ph,
+                                               unsigned* __restrict__ rc_flag) {
   for (int b = gt; b < nrb; b += gn)  // empty residual slots (resid_bookkeeping)
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(rpart + b), kRpartEmpty, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -1216,7 +1374,7 @@ __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict
     hl[t] = 0.0;
     hl_part[t] = 0.0;
   }
-  if (blockIdx.x != 0) return;
+  if (!wg0) return;
   if ((int)threadIdx.x < W) mpring[threadIdx.x] = ring.mp[threadIdx.x];
   if (threadIdx.x == 0) {
     const int skip = status ? 1 : 0;  // an asynchronous recut that needs the host: skip
@@ -1231,6 +1389,54 @@ __global__ void __launch_bounds__(256) k_ba_init(BaState* st, double* __restrict
     st->seq = ph ? ph[0] : seq0;
     st->fin = 0;
     if (ph) __hip_atomic_store(rc_flag, (unsigned)ph[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// k_ba_init + the first LM iteration's k_ba_hess as one launch (the scan
+// graph, vg_ctx::ba_init_hess): workgroups [0, G) the Hessian chunks, which
+// also do tras_opt's bookkeeping for their own factors when `fin` (each
+// factor's eigen system and cluster read from the map, copied to fac_eig /
+// fac_pcr, opt_state = factor index: k_ba_init's loop), with the ring from
+// the arguments; then the IMU factors' blocks; the last workgroup does the
+// rest of k_ba_init (ba_init_common). Nothing in the launch reads the LM state
+// the last workgroup writes: the chunks decide on the recut status, the same
+// test k_ba_init's skip is.
+__global__ void __launch_bounds__(kHessThreads) k_ba_init_hess(
+    const int* __restrict__ nfp, int W, const int* __restrict__ fac_node, double* __restrict__ fac_eig,
+    Clu* __restrict__ fac_pcr, const Clu* __restrict__ pcrs, const double* __restrict__ xs, double* __restrict__ part,
+    int G, int nimu, const double* __restrict__ imurec, const int* __restrict__ imu_head,
+    const double* __restrict__ bias, double* __restrict__ imuout, KClock* __restrict__ clk, BaState* st,
+    double* __restrict__ hl, double* __restrict__ hl_part, int nout, MpRing ring, int* __restrict__ mpring,
+    const int* __restrict__ rc_status, double* __restrict__ rpart, int nrb, const int* __restrict__ ph,
+    unsigned* __restrict__ rc_flag, int fin, DevMap m) {
+  const int status = rc_status ? *rc_status : 0;
+  if ((int)blockIdx.x == G + nimu) {
+    ba_init_common(threadIdx.x, blockDim.x, true, st, hl, hl_part, nout, ring, mpring, W, status, 0, rpart, nrb, ph,
+                   rc_flag);
+    return;
+  }
+  if (status) return;  // the recut needs the host: the LM is skipped (k_ba_init's skip)
+  if ((int)blockIdx.x >= G) {  // IMU factors (give_evaluate, jac_enable)
+    imu_factor_block(blockIdx.x - G, imurec, *imu_head, bias, xs, imuout);
+    return;
+  }
+  __shared__ int s_mp[kMaxW];
+  if ((int)threadIdx.x < kMaxW) s_mp[threadIdx.x] = ring.mp[threadIdx.x];
+  const bool clk_on = clk && clk->on;  // in-kernel clock (vg_profile bit 2): the LM's iteration 0 slot
+  const int clk_slot = clk_on ? (clk->scan * 8) & (kClkHRing - 1) : 0;
+  if (clk_on && blockIdx.x == 0 && threadIdx.x == 0) {
+    clk->h_t0[clk_slot] = (unsigned long long)wall_clock64();
+    clk->h_exec[clk_slot] = 1;
+  }
+  __syncthreads();  // s_mp
+  const int nf = *nfp;
+  const int nchunk = (nf + hess_chunk(W) - 1) / hess_chunk(W);
+  for (int ch = blockIdx.x; ch < nchunk; ch += G)
+    hess_chunk_eval<false>(ch, nf, W, fac_node, fac_eig, fac_pcr, pcrs, s_mp, xs, part, nullptr, fac_eig, fac_pcr,
+                           nullptr, fin ? m.eig : nullptr, fin ? m.pcr_add : nullptr, fin ? m.hdr : nullptr);
+  if (clk_on && blockIdx.x < kClkHBlocks) {
+    __syncthreads();
+    if (threadIdx.x == 0) clk->h_tend[clk_slot][blockIdx.x] = (unsigned long long)wall_clock64();
   }
 }
 
@@ -1310,6 +1516,10 @@ int ba_alloc(vg_ctx* ctx) {
                              (int)solve_lds_bytes(W)));
   VG_HIP(hipFuncSetAttribute((const void*)k_ba_hess, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)hess_lds_bytes(W)));
+  VG_HIP(hipFuncSetAttribute((const void*)k_ba_resid_hess, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)hess_lds_bytes(W)));
+  VG_HIP(hipFuncSetAttribute((const void*)k_ba_init_hess, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)hess_lds_bytes(W)));
   return VG_OK;
 }
 
@@ -1368,7 +1578,16 @@ const int* ba_gate_dev(vg_ctx* ctx) { return &carve(ctx).st->fin; }
 // factor count, the flags and the publication number live on the device), so
 // an unsharded run replays one captured graph per iteration; the sampled
 // solve-timing runs launch directly (events around k_ba_solve).
-static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr) {
+// rh: 1 this iteration's residual pass is k_ba_resid_hess (it also forms the
+// next iteration's Hessian at the trial), 2 this iteration's Hessian came
+// from the previous iteration's k_ba_resid_hess (no k_ba_hess launch)
+// ih (the scan graph, k == 0): k_ba_init_hess replaces k_ba_init + k_ba_hess
+struct InitHessArg {
+  MpRing ring;
+  int fin;
+};
+static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr, int rh = 0,
+                            const InitHessArg* ih = nullptr) {
   const int W = ctx->cfg.win_size;
   hipStream_t s = ctx->stream;
   BaDev d = carve(ctx);
@@ -1389,9 +1608,15 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr) {
              shard_on ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st, ctx->d_pub, nullptr};
   CtlArg ctl_fused = ctl;  // unsharded: the bookkeeping rides in k_ba_resid's IMU workgroup
   if (!shard_on && ctx->ba_fuse_ctl) ctl_fused.err = ctx->map.counters + kCntErr;
-  k_ba_hess<<<G + nimu, kHessThreads, hess_lds, s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
-                                                    ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, nimu, d.imurec, &ctx->st->imu_head,
-                                                    d.bias, d.imuout, &ctx->st->clk);
+  if (ih)
+    k_ba_init_hess<<<G + nimu + 1, kHessThreads, hess_lds, s>>>(
+        nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr, ctx->map.pcrs, d.xs, d.part, G, nimu, d.imurec,
+        &ctx->st->imu_head, d.bias, d.imuout, &ctx->st->clk, d.st, d.hl, ctx->ba.hout_part, nout, ih->ring, d.mpring,
+        map_rc_status(ctx), d.rpart, kResidBlocks, ctx->st->ph, ctx->d_sync + 3, ih->fin, ctx->map);
+  else if (rh != 2)
+    k_ba_hess<<<G + nimu, kHessThreads, hess_lds, s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
+                                                      ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, nimu, d.imurec,
+                                                      &ctx->st->imu_head, d.bias, d.imuout, &ctx->st->clk);
   k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, shard_on ? hl_part : d.hl,
                                                        d.st);
   // sharded: every shard's factors -> one LiDAR Hessian / gradient / residual
@@ -1410,9 +1635,14 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr) {
   k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
                                        d.st, &ctx->st->clk);
   if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][1], s);
-  k_ba_resid<<<nrb + 1, 256, 0, s>>>(nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt,
-                                     ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, nimu, d.imurec, &ctx->st->imu_head, d.bias,
-                                     d.imures, ctl_fused);
+  if (rh == 1)
+    k_ba_resid_hess<<<kRhChunkWg + 1 + nimu, kHessThreads, hess_lds, s>>>(
+        nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring, d.xt, ctx->ba.fac_eig, ctx->ba.fac_pcr,
+        d.part, d.rpart, d.st, nimu, d.imurec, &ctx->st->imu_head, d.bias, d.imures, d.imuout, ctl_fused);
+  else
+    k_ba_resid<<<nrb + 1, kResidThreads, 0, s>>>(nfp, W, ctx->ba.fac_node, ctx->map.pcr_fix, ctx->map.pcrs, d.mpring,
+                                                 d.xt, ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, nimu,
+                                                 d.imurec, &ctx->st->imu_head, d.bias, d.imures, ctl_fused);
   if (shard_on) {  // the residual over every shard's factors
     k_ba_rsum<<<1, 64, 0, s>>>(nrb, d.rpart, rsum, d.st);
     if (xerr == VG_OK) xerr = shard_allreduce(ctx, rsum, rsum + 1, 1, 0, 4);
@@ -1437,14 +1667,29 @@ static void ba_init_kernel(vg_ctx* ctx, const int* mp_ring, int seq0) {
                                                     ctx->map, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr);
 }
 
+// the two-iteration LM graphs take k_ba_resid_hess (unsharded, bookkeeping
+// fused, hess_fs(W) two residual chunks)
+static bool ba_rh_on(vg_ctx* ctx) {
+  return ctx->ba_resid_hess && ctx->ba_fuse_ctl && !sharded(ctx) && resid_hess_ok(ctx->cfg.win_size);
+}
+
 // the scan graph's LM part (pipeline.cpp stage_insert_recut), captured on the
 // context stream: k_ba_init reading its per-scan numbers from the device,
 // then the first two iterations
 int ba_capture_scan_lm(vg_ctx* ctx, const int* mp_ring) {
-  ba_init_kernel(ctx, mp_ring, 0);
   int xerr = VG_OK;
-  ba_iter_kernels(ctx, 0, false, xerr);
-  ba_iter_kernels(ctx, 1, false, xerr);
+  const bool rh = ba_rh_on(ctx);
+  if (ctx->ba_init_hess && !sharded(ctx)) {  // k_ba_init inside the first Hessian pass
+    InitHessArg ih;
+    for (int i = 0; i < kMaxW; i++) ih.ring.mp[i] = i < ctx->cfg.win_size ? mp_ring[i] : 0;
+    ih.fin = ctx->rc_finish_in_init ? 1 : 0;
+    ctx->rc_finish_in_init = false;
+    ba_iter_kernels(ctx, 0, false, xerr, rh ? 1 : 0, &ih);
+  } else {
+    ba_init_kernel(ctx, mp_ring, 0);
+    ba_iter_kernels(ctx, 0, false, xerr, rh ? 1 : 0);
+  }
+  ba_iter_kernels(ctx, 1, false, xerr, rh ? 2 : 0);
   VG_HIP(hipGetLastError());
   return xerr;
 }
@@ -1496,8 +1741,9 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   const bool graph2 = pre == 0 && graph && ctx->ba_graph2 && ctx->ba_last_iters >= 2;
   if (graph2 && !ctx->g_ba2) {
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    enqueue(0);
-    enqueue(1);
+    const bool rh = ba_rh_on(ctx);
+    ba_iter_kernels(ctx, 0, solve_ev, xerr, rh ? 1 : 0);
+    ba_iter_kernels(ctx, 1, solve_ev, xerr, rh ? 2 : 0);
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(s, &g);
     VG_HIP(e);

@@ -486,12 +486,14 @@ struct vg_ctx {
   bool margi_batch = true;    // vgx_debug 24: k_margi_leaf reads a leaf's frame clusters four at a time (r04k +0.4 %)
   bool margi_fused = true;    // margi isexist bottom-up in k_margi_copy, erase in one launch (vgx_debug 21: 0 = per-level launches)
   bool iekf_prefetch = true;  // vgx_debug 23: k_iekf touches a cached match's plane record beside its header (r04i A/B +0.9 %)
-  bool ba_structural = true;
+  bool ba_structural = true;      // vgx_debug 31: k_ba_prep's structural elimination order (0: Eigen's |diag| order)
+  bool ba_resid_hess = true;      // vgx_debug 34: k_ba_resid_hess in the two-iteration LM graphs (0: k_ba_resid + k_ba_hess)
+  bool ba_init_hess = true;       // vgx_debug 35: k_ba_init inside the scan graph's first Hessian pass (0: its own launch)
   bool rc_init_finish = true;     // vgx_debug 32: the asynchronous recut's factor bookkeeping inside k_ba_init (0: k_factor_finish_dev)
   bool rc_finish_in_init = false; // set by map_recut for the next k_ba_init
   bool rc_begin_fold = true;      // vgx_debug 33: the recut's head in the insert's k_push_window (insert + recut graph)
   const vg::WinArg* rc_begin_wa = nullptr;  // set for one map_insert: its k_push_window runs the recut's head
-  bool rc_begun = false;          // ... and the map_recut after it skips k_make_win_recut_begin  // vgx_debug 31: k_ba_prep's structural elimination order (0: Eigen's |diag| order)
+  bool rc_begun = false;          // ... and the map_recut after it skips k_make_win_recut_begin
   bool ba_fuse_ctl = true;    // vgx_debug 19: the LM bookkeeping in k_ba_resid's IMU workgroup (A/Bs r04e 0, r04g/h +0.8-0.9 %)
   bool ba_graph = true;      // LM iterations replay one captured graph each (vgx_debug 15: 0 = direct launches)
   bool flag_sync = true;     // counter hand-offs instead of event waits on the critical path (vgx_debug 14)

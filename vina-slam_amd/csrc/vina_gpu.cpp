@@ -918,6 +918,14 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     ctx->ba_graph = value != 0;
     return VG_OK;
   }
+  if (key == 35) {  // 0: k_ba_init as its own launch ahead of the scan graph's first k_ba_hess
+    ctx->ba_init_hess = value != 0;
+    return VG_OK;
+  }
+  if (key == 34) {  // 0: the second LM iteration's Hessian by its own k_ba_hess, not inside the first's residual pass
+    ctx->ba_resid_hess = value != 0;
+    return VG_OK;
+  }
   if (key == 33) {  // 0: k_make_win_recut_begin as its own launch in the insert + recut graph
     ctx->rc_begin_fold = value != 0;
     return VG_OK;
