@@ -593,13 +593,6 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
   const int tid = threadIdx.x, q = blockIdx.x;
   const bool calc = st->calc_hess != 0;
   const double u = st->u;
-  if (calc && q == 0 && tid == 0) {  // residual1 of divide_thread at the current state (optimizers.cpp:454)
-    double r = 0.0;
-    for (int k = 0; k < nimu; k++) r += imuout[(size_t)k * 931 + 930];
-    r *= imu_coef * 0.5;
-    r += hl[L * (L + 1) / 2 + L];
-    st->res1 = r;
-  }
   for (int t = tid; t < n; t += blockDim.x)
     Dv[t] = t < 15 ? 1.0 : (calc ? asm_entry(t, t, nimu, imu_coef, hl, imuout, L) : Hcalc[lo(t, t)]);
   __syncthreads();
@@ -636,6 +629,15 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
     timg[(size_t)q * 256 + tel(r, c)] = v;
   }
   if (q == 0) {
+    // residual1 of divide_thread at the current state (optimizers.cpp:454), on
+    // a lane the gradient loop below leaves idle (n < 256)
+    if (calc && tid == (int)blockDim.x - 1) {
+      double r = 0.0;
+      for (int k = 0; k < nimu; k++) r += imuout[(size_t)k * 931 + 930];
+      r *= imu_coef * 0.5;
+      r += hl[L * (L + 1) / 2 + L];
+      st->res1 = r;
+    }
     for (int t = tid; t < n; t += blockDim.x) {
       const double raw = calc ? asm_grad(t, nimu, imu_coef, hl, imuout, L) : Jcalc[t];
       if (calc) Jcalc[t] = raw;

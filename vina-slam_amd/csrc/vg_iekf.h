@@ -22,7 +22,6 @@ constexpr int kIekfGroups = 60;  // row groups of the partial sums (1024-lane up
 struct IekfLds {
   double red[kIekfGroups][kIekfVals];
   double o[kIekfVals], K6[15][6], G6[15][6], vec[15], sol[15], IG[15][15];
-  double xcc[kXS + 225];  // x_curr (kXS) and its covariance (225), loaded with the ordered sum's partials
   int fin;
 };
 
@@ -37,16 +36,11 @@ struct IekfLds {
 // (nact: the workgroups whose chunk holds points, iekf_chunk below; the
 // others' rows are +0 and skipped — the same sums)
 __device__ __forceinline__ int iekf_chunk(int b, int nb);
-// side (optional): x_curr + covariance (kXS + 225 doubles) copied into L.xcc,
-// one value per lane, its load issued with the lane's partial loads (no extra
-// memory round trip for the update's later reads)
 __device__ __forceinline__ void iekf_reduce_block(int nb, const double* __restrict__ partials, IekfLds& L,
-                                                  int nact, const double* __restrict__ side = nullptr) {
+                                                  int nact) {
   const int tid = threadIdx.x;
   const int G = (int)blockDim.x / 17 < kIekfGroups ? (int)blockDim.x / 17 : kIekfGroups;
   const int g = tid / 17, j2 = 2 * (tid % 17);
-  const bool sd = side && tid < kXS + 225;
-  const double sv = sd ? side[tid] : 0.0;
   if (g < G) {
     // the group's first kRows rows loaded at once (one memory round trip, not
     // one per row), then summed in the same row order
@@ -75,7 +69,6 @@ __device__ __forceinline__ void iekf_reduce_block(int nb, const double* __restri
     L.red[g][j2] = a0;
     L.red[g][j2 + 1] = a1;
   }
-  if (sd) L.xcc[tid] = sv;
   __syncthreads();
   if (tid < kIekfVals) {
     double s = L.red[0][tid];
@@ -117,17 +110,16 @@ __device__ void iekf_update_block(int nb, const double* __restrict__ partials, D
   const int tid = threadIdx.x;
   VG_PROBE_BEGIN();
   // x_curr does not change before the update's end: vec on a lane the
-  // ordered sum leaves idle (17 x 60 = 1020 of 1024), beside the sum, and the
-  // update's x_curr / covariance reads from the copy the sum's lanes load
-  // (L.xcc) instead of dependent global round trips after it
+  // ordered sum leaves idle (17 x 60 = 1020 of 1024), beside the sum. (Copies
+  // of x_curr and its covariance loaded with the partials, read from LDS after
+  // the sum, measured -0.8 %: profiles/r05/ab_iekf_state_copy_r05p.txt.)
   const bool vec_early = (int)blockDim.x > 17 * kIekfGroups;
   if (vec_early && tid == (int)blockDim.x - 1) iekf_vec(st, L);
   if (nb >= 0) {
     const int n = st->sn;
-    iekf_reduce_block(nb, partials, L, n < nb * 256 ? (n + 255) / 256 : nb, vec_early ? st->xc : nullptr);
+    iekf_reduce_block(nb, partials, L, n < nb * 256 ? (n + 255) / 256 : nb);
   } else {  // sharded mode: `partials` holds the all-reduced sums
     if (tid < kIekfVals) L.o[tid] = partials[tid];
-    if (vec_early && tid < kXS + 225) L.xcc[tid] = st->xc[tid];
     __syncthreads();
   }
   VG_PROBE_MARK(23);  // the ordered sum of the block partials
@@ -150,7 +142,7 @@ __device__ __forceinline__ void iekf_update_tail(DState* __restrict__ st, int it
   VG_PROBE_MARK(24);
   if (tid < 64) {  // K6 = cov(:, 0:6) M^-1, M = I + HTH cov66: solve M^T X = cov(:, 0:6)^T, K6 = X^T
     const int lane = tid;
-    const double* cov = vec_done ? L.xcc + kXS : st->xc + kXS;  // (iekf_update_block's copy)
+    const double* cov = st->xc + kXS;
     double col[6];
     if (lane < 6) {  // column `lane` of M^T = row `lane` of M
       for (int r = 0; r < 6; r++) {
@@ -220,17 +212,16 @@ __device__ __forceinline__ void iekf_update_tail(DState* __restrict__ st, int it
   VG_PROBE_MARK(26);
   if (tid == 0) {  // x_curr ⊞= sol (types.hpp:67-78); convergence / rematch (odometry.cpp:205-227)
     double* xc = st->xc;
-    const double* x0 = vec_done ? L.xcc : xc;  // x_curr before the update (iekf_update_block's copy)
     const double* sol = L.sol;
-    const M3 Rn = mul(ld_m3(x0), Exp(v3(sol[0], sol[1], sol[2])));
+    const M3 Rn = mul(ld_m3(xc), Exp(v3(sol[0], sol[1], sol[2])));
     for (int k = 0; k < 9; k++) xc[k] = Rn[k];
     double pn[3];
     for (int k = 0; k < 3; k++) {
-      pn[k] = x0[9 + k] + sol[3 + k];
+      pn[k] = xc[9 + k] + sol[3 + k];
       xc[9 + k] = pn[k];
-      xc[12 + k] = x0[12 + k] + sol[6 + k];
-      xc[15 + k] = x0[15 + k] + sol[9 + k];
-      xc[18 + k] = x0[18 + k] + sol[12 + k];
+      xc[12 + k] += sol[6 + k];
+      xc[15 + k] += sol[9 + k];
+      xc[18 + k] += sol[12 + k];
     }
     const double rot_add = norm3(v3(sol[0], sol[1], sol[2])), tra_add = norm3(v3(sol[3], sol[4], sol[5]));
     const bool conv = (rot_add * 57.3 < 0.01) && (tra_add * 100 < 0.015);
@@ -258,7 +249,7 @@ __device__ __forceinline__ void iekf_update_tail(DState* __restrict__ st, int it
   double cv = 0.0;
   if (tid < 225) {
     const int r = tid / 15, c = tid % 15;
-    const double* cov = vec_done ? L.xcc + kXS : st->xc + kXS;
+    const double* cov = st->xc + kXS;
     double s = L.IG[r][0] * cov[c];
     for (int k = 1; k < 15; k++) s += L.IG[r][k] * cov[k * 15 + c];
     cv = s;
