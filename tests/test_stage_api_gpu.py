@@ -114,13 +114,13 @@ def test_recut_replay_path_equals_fast_path(knob):
                                          ({16: 0}, {}, True), ({17: 0}, {}, True), ({14: 0}, {}, True),
                                          ({26: 0}, {}, True), ({27: 0}, {}, True), ({32: 0}, {}, True),
                                          ({33: 0}, {}, True), ({34: 0}, {}, True), ({35: 0}, {}, True),
-                                         ({31: 0}, {}, False)],
+                                         ({37: 0}, {}, True), ({31: 0}, {}, False)],
                          ids=["lm-bookkeeping-in-resid", "margi-exist-up", "device-propagation",
                               "iekf-plane-prefetch", "margi-batched-cluster-loads", "recut-fused-levels",
                               "root-registration-lookback", "lm-two-iteration-graph", "flag-hand-offs",
                               "lm-outcome-deferred", "scan-graph", "factor-bookkeeping-in-ba-init",
                               "recut-head-in-push-window", "lm-resid-hess", "lm-init-in-first-hessian",
-                              "lm-structural-order"])
+                              "downsample-after-iekf-enqueue", "lm-structural-order"])
 def test_fused_launches_equal_separate(ka, kb, exact):
     """Every default-on launch fusion or hand-off of the scan chain against its
     separate-launch form (vgx_debug knobs), bit for bit: k_ba_control inside
@@ -139,8 +139,9 @@ def test_fused_launches_equal_separate(ka, kb, exact):
     position, hand-offs on device flags), tras_opt's factor bookkeeping
     inside k_ba_init (32), the recut's head inside the insert's
     k_push_window (33), the second LM iteration's Hessian inside the
-    first iteration's residual pass (34, k_ba_resid_hess) and k_ba_init
-    inside the scan graph's first Hessian pass (35); the LM system's
+    first iteration's residual pass (34, k_ba_resid_hess), k_ba_init
+    inside the scan graph's first Hessian pass (35) and the early downsample
+    enqueued behind the IEKF's launches (37); the LM system's
     structural elimination order against Eigen's |diag| order (31) agrees
     within rounding (counters exact, poses within 1e-12 m)."""
     p = vgconfig.load("mid360")

@@ -413,10 +413,21 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   ctx->tail_a_valid = false;
   const double* bxc = begin && !P->begin_prop ? P->begin_xc : nullptr;
   const PropArg* bprop = begin && P->begin_prop ? &P->prop : nullptr;
+  // host_step's early downsample: enqueued behind this IEKF's launches when
+  // those go out without a host wait (below), else first
+  auto ds_hook = [&]() -> int {
+    if (!P->ds_hook) return VG_OK;
+    const std::function<int()> h = std::move(P->ds_hook);
+    P->ds_hook = nullptr;
+    return h();
+  };
   // a pending LM is resolved before this IEKF is enqueued unless the IEKF
   // stream waits for the margi on device flags (the numbers the real tail
   // stores as well) and starts from the device's state
-  if (!(split && ctx->flag_sync && ctx->sync_tail_armed && bprop)) VG_TRY(resolve_lm(ctx, P));
+  if (!(split && ctx->flag_sync && ctx->sync_tail_armed && bprop)) {
+    VG_TRY(ds_hook());
+    VG_TRY(resolve_lm(ctx, P));
+  }
   if (!split) return iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, bxc, nullptr, bprop);
   // created on first use: a context of the multi-sequence mode never makes
   // it (vg_multi_create), as a third stream per sequence makes sequences
@@ -441,6 +452,11 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
     else VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->ev_tail_a, 0));
     if (ctx->in_ev) VG_HIP(hipStreamWaitEvent(ctx->stream_iekf, ctx->in_ev, 0));  // a host-input scan's unpack
   }
+  // the early downsample between the device propagation's launch and the
+  // IEKF's: k_scan_prop (queued) waits on the device for the margi while the
+  // host enqueues the downsample, which still runs under the previous LM, and
+  // the IEKF's graph goes in before k_scan_prop ends
+  VG_TRY(ds_hook());
   bool signalled = false;  // k_iekf_all advanced the flag itself (no k_sync_set launch)
   VG_TRY(iekf_run(ctx, P->mpd, x, y, z, n, ctx->iekf_ring_base, bxc, ctx->stream_iekf, bprop, flags, &signalled,
                   opened));
@@ -480,6 +496,12 @@ static int need_open(vg_ctx* ctx, HostPipe* P, const char* what) {
   return VG_OK;
 }
 
+// the scan propagates on the device (k_scan_prop) rather than on the host
+// after a wait for the previous scan's state
+static bool prop_on_device(vg_ctx* ctx, const HostPipe* P, int m, bool dev) {
+  return dev && (ctx->dev_prop || P->lmp.active) && !P->first && m <= kPropMax && P->sticky == VG_OK;
+}
+
 // odom_ekf.process -> motion_blur state/covariance part (local_mapping.cpp:389);
 // opens the scan on the device (x_curr, x_prop, cov_inv)
 int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double end, bool dev) {
@@ -502,7 +524,7 @@ int stage_propagate(vg_ctx* ctx, const double* imu, int m, double beg, double en
   // it, behind the IEKF's enqueue); the first scan has nothing to propagate
   // A pending LM (the previous fused step returned before its outcome):
   // only the device has that scan's state, so it propagates there
-  P->begin_prop = dev && (ctx->dev_prop || P->lmp.active) && !P->first && m <= kPropMax && P->sticky == VG_OK;
+  P->begin_prop = prop_on_device(ctx, P, m, dev);
   if (P->begin_prop) {
     PropArg& a = P->prop;
     const vg_config& c = ctx->cfg;
@@ -1154,12 +1176,24 @@ int host_step(vg_ctx* ctx, const float* dx, const float* dy, const float* dz, co
   host_delay(5);
   const bool early = ctx->ds_early && ctx->want_ds_stream && !P->in_scan && P->sticky == VG_OK && !ctx->prof_stages;
   if (early) {
-    HostTimer ht_(ctx, kHostDownsample);
-    VG_TRY(ds_enqueue_scan(ctx, dx, dy, dz, di, n, 0));
+    // ds_after_iekf: behind the device propagation's launch (lio_state_estimation
+    // runs the hook), so k_scan_prop is queued before the host enqueues it
+    auto enq = [=]() -> int {
+      HostTimer ht_(ctx, kHostDownsample);
+      return ds_enqueue_scan(ctx, dx, dy, dz, di, n, 0);
+    };
+    if (ctx->ds_after_iekf && prop_on_device(ctx, P, m, true)) P->ds_hook = enq;  // (no host wait before it)
+    else VG_TRY(enq());
   }
   VG_TRY(stage_propagate(ctx, imu, m, beg, end, true));
   host_delay(0);
-  VG_TRY(stage_iekf(ctx, dx, dy, dz, n, nullptr));
+  const int r_iekf = stage_iekf(ctx, dx, dy, dz, n, nullptr);
+  if (P->ds_hook) {  // not run inside (an error, or a path without the IEKF's enqueue)
+    const std::function<int()> h = std::move(P->ds_hook);
+    P->ds_hook = nullptr;
+    if (r_iekf == VG_OK) VG_TRY(h());
+  }
+  VG_TRY(r_iekf);
   host_delay(4);
   if (early) {
     ds_adopt(P, dx, dy, dz, di, n);

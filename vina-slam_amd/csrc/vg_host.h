@@ -4,6 +4,7 @@
 // pending-publication queue.
 #pragma once
 #include <deque>
+#include <functional>
 #include <vector>
 #include "vg_internal.h"
 
@@ -143,6 +144,7 @@ struct Pend {          // a scan whose device results the host has not absorbed 
 struct InitState;  // init.cpp
 
 struct HostPipe {
+  std::function<int()> ds_hook;  // host_step: the early downsample's enqueue, run inside lio_state_estimation
   HX x_curr;
   std::vector<HX> x_buf;
   std::deque<HImuPre> imu_pre;

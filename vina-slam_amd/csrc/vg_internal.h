@@ -434,6 +434,7 @@ struct vg_ctx {
   float4* d_cmap = nullptr;  // the last /map_cmap cloud (x, y, z, intensity) and its size
   int* d_cmap_n = nullptr;
   bool ds_early = true;      // a fused step's downsample enqueued before the host waits for the previous state (host_step)
+  bool ds_after_iekf = true; // vgx_debug 37: ... behind the device propagation's launch (0: ahead of it)
   bool spec_tail = true;     // the margi tail behind the predicted LM iterations (stage_ba)
   std::string err;
   vg::Arena arena;

@@ -918,6 +918,10 @@ extern "C" int vgx_debug(vg_ctx* ctx, int key, int value) {
     ctx->ba_graph = value != 0;
     return VG_OK;
   }
+  if (key == 37) {  // 0: host_step enqueues the early downsample ahead of the propagation / IEKF launches
+    ctx->ds_after_iekf = value != 0;
+    return VG_OK;
+  }
   if (key == 35) {  // 0: k_ba_init as its own launch ahead of the scan graph's first k_ba_hess
     ctx->ba_init_hess = value != 0;
     return VG_OK;
