@@ -2946,6 +2946,20 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
   const bool pwork = (int)((blockIdx.x - 1) * blockDim.x) < nl;
 #endif
   int n_pu = 0, n_full = 0;  // plane_update calls / leaves past max_points (per-scan counters)
+#ifdef VG_PROBE
+  // per leaf thread, summed over the live leaves (scripts/probe_margi.py): 51 header + run + own
+  // cluster, 52 frame clusters + merge + eigen, 54 plane update, 55 point_fix carve + stores;
+  // 56 live leaves, 57 the longest leaf, 58 factor leaves
+  unsigned long long pq0 = wall_clock64(), pa = 0, pb2 = 0, pc = 0, pd = 0, ptot = 0, nlive = 0, nfac = 0;
+#define PMG(v)                                   \
+  do {                                           \
+    const unsigned long long n_ = wall_clock64(); \
+    v += n_ - pq0;                               \
+    pq0 = n_;                                    \
+  } while (0)
+#else
+#define PMG(v) (void)0
+#endif
   // whole waves per round: the point_fix blocks that grow are carved with one
   // atomic per wave (wave_append) instead of one per leaf on the shared counter
   for (int base = (blockIdx.x - 1) * blockDim.x; base < nl; base += (gridDim.x - 1) * blockDim.x) {
@@ -2959,6 +2973,10 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
     const bool live = node >= 0 && m.hdr[node].isexist && m.hdr[node].has_sw;
     const int W = mp.W;
     const int s0 = wa.mp[0];
+#ifdef VG_PROBE
+    const unsigned long long pstart = wall_clock64();
+    pq0 = pstart;
+#endif
     int seg = -1, segn = 0;  // the leaf's run of the oldest slot: its sw->points[mp[0]] in push order
     Clu w0, add_, fix_;
     int grow = 0;  // size of a new point_fix block (the live one is full)
@@ -2972,6 +2990,10 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
       clu_zero(w0);
       if (loc[s0].N != 0) w0 = clu_transform(loc[s0], R0, p0);
       double* e = &m.eig[(size_t)node * 12];
+      PMG(pa);
+#ifdef VG_PROBE
+      if (h.opt_state >= 0) nfac++;
+#endif
       if (h.opt_state >= 0) {
         add_ = fac_pcr[h.opt_state];
         for (int j = 0; j < 12; j++) e[j] = fac_eig[(size_t)h.opt_state * 12 + j];
@@ -3011,12 +3033,14 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
         }
       }
       fix_ = m.pcr_fix[node];
+      PMG(pb2);
       if (fix_.N < mp.max_points && h.is_plane)
         if (add_.N - h.last_num >= 5 || h.last_num <= 10) {
           plane_update_dev(m, node, add_, e);
           h.last_num = add_.N;
           n_pu++;
         }
+      PMG(pc);
       if (fix_.N >= mp.max_points) n_full++;
       if (fix_.N < mp.max_points) {
         if (w0.N != 0) {
@@ -3062,8 +3086,34 @@ __global__ void __launch_bounds__(256) k_margi_leaf(const int* __restrict__ nlea
         m.pcr_add[node] = add_;
         h.isexist = (fix_.N >= add_.N) ? 0 : 1;
       }
+#ifdef VG_PROBE
+      PMG(pd);
+      const unsigned long long tl = wall_clock64() - pstart;
+      ptot = tl > ptot ? tl : ptot;
+      nlive++;
+#endif
     }
   }
+#undef PMG
+#ifdef VG_PROBE
+  {
+    unsigned long long v[7] = {pa, pb2, pc, pd, nlive, nfac, ptot};
+    for (int off = 32; off > 0; off >>= 1)
+      for (int k = 0; k < 7; k++) {
+        const unsigned long long o = __shfl_xor(v[k], off, 64);
+        v[k] = k == 6 ? (o > v[k] ? o : v[k]) : v[k] + o;
+      }
+    if ((threadIdx.x & 63) == 0 && blockIdx.x > 0 && v[4] > 0) {  // working waves only (few atomics)
+      atomicAdd(&g_probe[51], v[0]);
+      atomicAdd(&g_probe[52], v[1]);
+      atomicAdd(&g_probe[54], v[2]);
+      atomicAdd(&g_probe[55], v[3]);
+      atomicAdd(&g_probe[56], v[4]);
+      atomicAdd(&g_probe[58], v[5]);
+      atomicMax(&g_probe[57], v[6]);
+    }
+  }
+#endif
   wave_append(&m.counters[kCntPlaneUpd], n_pu);
   wave_append(&m.counters[kCntFixFull], n_full);
 #ifdef VG_PROBE
