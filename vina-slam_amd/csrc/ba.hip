@@ -1128,8 +1128,11 @@ __device__ __forceinline__ void ba_control_body(const CtlArg& c, const double* p
     c.st->fin = ((c.st->done || c.st->iters >= 10) && !c.st->skip) ? 1 : 0;
     const int seq = c.st->seq;  // one publication per launch, numbered on the device (graph replays)
     c.st->seq = seq + 1;
-    pub_store(&c.pub->ba_done, c.st->done);
-    pub_store(&c.pub->ba_iters, c.st->iters);
+    // done and the iteration count in one word: the host reads them as one
+    // (a queued-ahead iteration publishing between two separate reads could
+    // pair one iteration's count with the next one's done, and sharded ranks
+    // would then enqueue different iteration counts)
+    pub_store(&c.pub->ba_word, c.st->iters * 2 + (c.st->done ? 1 : 0));
     pub_flag(&c.pub->seq_ba, seq);
   }
 }
@@ -1815,8 +1818,9 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
     // before it (the device stops counting once done) — so the number of
     // iterations enqueued never depends on timing (sharded mode: every
     // enqueue is an exchange, all ranks must enqueue alike)
-    done_iters = __atomic_load_n(&ctx->h_pub->ba_iters, __ATOMIC_ACQUIRE);
-    if (__atomic_load_n(&ctx->h_pub->ba_done, __ATOMIC_ACQUIRE) && done_iters <= k + 1) break;
+    const int bw = __atomic_load_n(&ctx->h_pub->ba_word, __ATOMIC_ACQUIRE);
+    done_iters = bw >> 1;
+    if ((bw & 1) && done_iters <= k + 1) break;
     done_iters = k + 1;
     if (enq == k + 1 && enq < 10) iteration(enq++);  // not queued ahead: now
   }
@@ -1866,8 +1870,9 @@ int ba_resolve(vg_ctx* ctx, bool block, bool* finished, int* iters, bool* tail_o
       L.active = false;
       return r;
     }
-    done_iters = __atomic_load_n(&ctx->h_pub->ba_iters, __ATOMIC_ACQUIRE);
-    if (__atomic_load_n(&ctx->h_pub->ba_done, __ATOMIC_ACQUIRE) && done_iters <= k + 1) break;
+    const int bw = __atomic_load_n(&ctx->h_pub->ba_word, __ATOMIC_ACQUIRE);
+    done_iters = bw >> 1;
+    if ((bw & 1) && done_iters <= k + 1) break;
     done_iters = k + 1;
     if (L.enq == k + 1 && L.enq < 10) VG_TRY(launch());  // not queued ahead: now
   }

@@ -343,7 +343,7 @@ struct Shard {
 // stores, each part closed by a sequence flag the host spins on).
 struct Pub {
   int seq_ds, n_ds, ds_err, pad0;          // downsample (after k_ds_*)
-  int seq_ba, ba_done, ba_iters, pad1;     // LM iteration flags (k_ba_control)
+  int seq_ba, ba_word, pad1, pad1b;  // LM iteration flags (k_ba_control): iterations * 2 + done, one word (no torn pair)
   int seq_rc, rc_status, rc_nf, pad5;      // asynchronous recut status (k_fac_sort)
   int seq1, iekf_iters, degenerate, matches[4], ba_iters1, ba_hess1, planes[4], pad2[3];  // P1: state after IEKF/BA
   int seq2, pad3[3];
