@@ -49,6 +49,9 @@ def main(nscan=40):
     for k, name in ((48, "parent lookup + child init"), (49, "push"), (51, "visit + append"),
                     (52, "window split (rc_win_leaf)")):
         print("  %-32s %8.2f us/child" % (name, buf[k] / n / 100.0))
+    n = max(buf[18], 1)
+    print("window splits (rc_win_leaf, every wave): %d, %.1f us each, longest %.2f us; points %.1f each, "
+          "most %d" % (buf[18], buf[17] / n / 100.0, buf[16] / 100.0, buf[20] / n, buf[19]))
     ctx.close()
 
 

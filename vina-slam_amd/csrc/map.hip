@@ -1654,29 +1654,8 @@ __global__ void __launch_bounds__(256) k_rc_visit(int L, int thread_num, const i
 // block's start, then per octant its offset and count, then the mask of
 // non-empty octants; nscr[leaf*4+0] = q.
 constexpr int kRcWinWaves = 4;
+constexpr int kRcWalkB = 4;  // rc_win_leaf: 64-point chunks per round of loads
 constexpr int kRcInfo = 18;  // event base, 8 octant offsets, 8 octant counts, octant mask
-// point e of the leaf's walk (fixed points, then the window's runs in
-// order), its phase located among the wave's per-phase run starts (lane ph
-// holds phase ph's exclusive start ex, run start st and slot)
-__device__ __forceinline__ int rc_walk_octant(const NodeHdr& h, int e, int wc, int ex, int st, int slot,
-                                              const WinD* win, const DevMap& m, int& ph, int& idx) {
-  ph = 0;
-#pragma unroll
-  for (int step = 32; step >= 1; step >>= 1) {
-    const int cand = ph + step;
-    const int v = __shfl(ex, cand <= wc ? cand : wc, 64);
-    if (cand <= wc && v <= e) ph = cand;
-  }
-  const int loc = e - __shfl(ex, ph, 64);
-  const int pst = __shfl(st, ph, 64), psl = __shfl(slot, ph, 64);
-  if (ph == 0) {
-    idx = loc;
-    return octant(ld_v3(&m.fix_pnt[((size_t)h.fix_off + loc) * 3]), h.center);
-  }
-  idx = m.wp_ord[(size_t)psl * m.ord_stride + pst + loc];
-  const V3 pw = rigid(ld_m3(win->R[ph - 1]), ld_v3(&m.wp_pnt[((size_t)psl * m.cap_wp + idx) * 3]), ld_v3(win->p[ph - 1]));
-  return octant(pw, h.center);
-}
 // one wave per subdividing leaf: the leaf's points are flattened across the
 // phases so each 64-point chunk costs one round of loads whatever the runs'
 // lengths; pass 1 counts the octants, pass 2 writes each octant's events
@@ -1687,6 +1666,9 @@ __device__ __forceinline__ void rc_win_leaf(int L, int leaf, int q, const WinD* 
                                             uint64_t* __restrict__ ev, int* __restrict__ rcinfo, int cap,
                                             int info_cap, int* __restrict__ rc) {
   const int lane = threadIdx.x & 63;
+#ifdef VG_PROBE
+  const unsigned long long wl_t0 = wall_clock64();  // scripts/probe_recut.py: 16-20 split time / points
+#endif
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int wc = win->win_count;
   const int my_slot = (lane >= 1 && lane <= wc) ? win->mp[lane - 1] : 0;
@@ -1712,15 +1694,51 @@ __device__ __forceinline__ void rc_win_leaf(int L, int leaf, int q, const WinD* 
     }
     return;
   }
-  int cnt8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int e0 = 0; e0 < total; e0 += 64) {
-    const int e = e0 + lane;
-    int ph, idx;
-    int o = rc_walk_octant(h, e < total ? e : total - 1, wc, ex, st, my_slot, win, m, ph, idx);
-    if (e < total) m.cfirst[(size_t)leaf * 8 + o] = -5;
-    else o = -1;
+  // kRcWalkB chunks of 64 walk points per round of loads (the index loads of
+  // all of them, then all their point loads): a split costs two memory round
+  // trips per batch instead of two per chunk; a leaf of at most one batch
+  // keeps it in registers for pass 2
+  constexpr int kB = kRcWalkB;
+  int bph[kB], bix[kB], boc[kB];
+  auto walk_batch = [&](int c0) __attribute__((always_inline)) {
+    int loc[kB], pst[kB], psl[kB];
 #pragma unroll
-    for (int k = 0; k < 8; k++) cnt8[k] += __popcll(__ballot(o == k));
+    for (int b = 0; b < kB; b++) {
+      const int e = min((c0 + b) * 64 + lane, total - 1);
+      int ph = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const int cand = ph + step;
+        const int v = __shfl(ex, cand <= wc ? cand : wc, 64);
+        if (cand <= wc && v <= e) ph = cand;
+      }
+      bph[b] = ph;
+      loc[b] = e - __shfl(ex, ph, 64);
+      pst[b] = __shfl(st, ph, 64);
+      psl[b] = __shfl(my_slot, ph, 64);
+      bix[b] = ph == 0 ? loc[b] : m.wp_ord[(size_t)psl[b] * m.ord_stride + pst[b] + loc[b]];
+    }
+#pragma unroll
+    for (int b = 0; b < kB; b++) {
+      const int ph = bph[b];
+      const V3 pw = ph == 0 ? ld_v3(&m.fix_pnt[((size_t)h.fix_off + loc[b]) * 3])
+                            : rigid(ld_m3(win->R[ph - 1]), ld_v3(&m.wp_pnt[((size_t)psl[b] * m.cap_wp + bix[b]) * 3]),
+                                    ld_v3(win->p[ph - 1]));
+      boc[b] = octant(pw, h.center);
+    }
+  };
+  int cnt8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int c0 = 0; c0 * 64 < total; c0 += kB) {
+    walk_batch(c0);
+#pragma unroll
+    for (int b = 0; b < kB; b++) {
+      const int e = (c0 + b) * 64 + lane;
+      int o = boc[b];
+      if (e < total) m.cfirst[(size_t)leaf * 8 + o] = -5;
+      else o = -1;
+#pragma unroll
+      for (int k = 0; k < 8; k++) cnt8[k] += __popcll(__ballot(o == k));
+    }
   }
   int off8[8], run = 0, mask = 0;
 #pragma unroll
@@ -1740,20 +1758,33 @@ __device__ __forceinline__ void rc_win_leaf(int L, int leaf, int q, const WinD* 
     m.nscr[(size_t)leaf * 4 + 0] = q;
     atomicAdd(&rc[kRcNch + L], __popc(mask));
   }
-  for (int e0 = 0; e0 < total; e0 += 64) {
-    const int e = e0 + lane;
-    int ph, idx;
-    int o = rc_walk_octant(h, e < total ? e : total - 1, wc, ex, st, my_slot, win, m, ph, idx);
-    if (e >= total) o = -1;
-    int pos = 0;
+  const bool kept = total <= 64 * kB;  // pass 1's only batch is still in registers
+  for (int c0 = 0; c0 * 64 < total; c0 += kB) {
+    if (!kept) walk_batch(c0);
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint64_t bk = __ballot(o == k);
-      if (o == k) pos = base + off8[k] + __popcll(bk & below);
-      off8[k] += __popcll(bk);
+    for (int b = 0; b < kB; b++) {
+      const int e = (c0 + b) * 64 + lane;
+      const int o = e < total ? boc[b] : -1;
+      int pos = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint64_t bk = __ballot(o == k);
+        if (o == k) pos = base + off8[k] + __popcll(bk & below);
+        off8[k] += __popcll(bk);
+      }
+      if (o >= 0) ev[pos] = ((uint64_t)bph[b] << 21) | (uint64_t)bix[b];
     }
-    if (o >= 0) ev[pos] = ((uint64_t)ph << 21) | (uint64_t)idx;
   }
+#ifdef VG_PROBE
+  if (lane == 0) {
+    const unsigned long long d = wall_clock64() - wl_t0;
+    atomicMax(&g_probe[16], d);
+    atomicAdd(&g_probe[17], d);
+    atomicAdd(&g_probe[18], 1ull);
+    atomicMax(&g_probe[19], (unsigned long long)total);
+    atomicAdd(&g_probe[20], (unsigned long long)total);
+  }
+#endif
 }
 __global__ void __launch_bounds__(64 * kRcWinWaves) k_rc_win(int L, const int* __restrict__ sub,
                                                              const WinD* __restrict__ win, DevMap m,
