@@ -39,6 +39,21 @@ FP64_MFMA_TFLOPS = 78.6  # MI355X dense fp64 matrix peak (AMD spec)
 FP64_TFLOPS = 78.6       # MI355X fp64 vector peak (AMD spec; k_ba_hess is mostly VALU)
 
 
+class _StdoutToStderr:
+    """fd 1 -> stderr for a block: RCCL prints its version banner on stdout when
+    it initialises, which must not precede the bench's one JSON line"""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *a):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -174,7 +189,9 @@ def main():
     import vgpu
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        with _StdoutToStderr():  # (RCCL's banner)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.barrier()
     dev = torch.device("cuda", local)
     seq = synth.Sequence(args.lidar, seq_id, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
 
@@ -193,9 +210,10 @@ def main():
         k, v = kv.split("=")
         ctx.debug(int(k), int(v))
     if tile:  # one RCCL communicator inside the library, id from rank 0
-        obj = [vgpu.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        ctx.shard_rccl(rank, world, obj[0])
+        with _StdoutToStderr():
+            obj = [vgpu.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            ctx.shard_rccl(rank, world, obj[0])
     ctx.seed(seq.gt_state(0))
     torch.cuda.synchronize(dev)
 
@@ -652,7 +670,11 @@ def tile_path_rate(p, seq, scans, imus, warmup, steps, dev, unsharded):
     n = min(warmup + steps, len(scans))
     ctx = vgpu.Context(vgconfig.to_c(p), device=dev.index or 0, max_points=max(s[1] for s in scans) + 16, **CAP)
     ctx.debug(30, 1)
-    ctx.shard_rccl(0, 1, vgpu.rccl_unique_id())
+    for kv in filter(None, os.environ.get("VG_TILE_DEBUG", "").split(",")):  # same-build A/Bs of this leg only
+        k_, v_ = kv.split("=")
+        ctx.debug(int(k_), int(v_))
+    with _StdoutToStderr():  # (RCCL's banner)
+        ctx.shard_rccl(0, 1, vgpu.rccl_unique_id())
     ctx.seed(seq.gt_state(0))
     prepped = [ctx.prep_step_dev(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(), t[3].data_ptr(), m, b, e, imus[k])
                for k, (t, m, b, e) in enumerate(scans[:n])]
@@ -673,7 +695,8 @@ def tile_path_rate(p, seq, scans, imus, warmup, steps, dev, unsharded):
             "overhead_ms_per_scan": round(dt * 1e3 / k - 1e3 / unsharded, 4),
             "note": "the tile-sharded path (config 4) with a one-rank RCCL communicator (vgx_debug 30): every "
                     "exchange runs ncclAllReduce on the stream, direct launches, no peer traffic; overhead vs the "
-                    "unsharded metric leg on the same scans"}
+                    "unsharded metric leg on the same scans",
+            "debug": os.environ.get("VG_TILE_DEBUG") or None}
 
 
 def host_input_rate(p, seq, host_scans, imus, warmup, steps, dev):
