@@ -478,9 +478,11 @@ __device__ __forceinline__ void hess_body(const int* __restrict__ nfp, int W, co
 
 // ordered sum of the chunk partials: 8 lanes per output split the chunks
 // (stride 8), then a fixed 3-step shuffle tree (deterministic)
+// xa.frame (sharded): `out` is the exchange frame, closed here (nout = its payload)
 __global__ void __launch_bounds__(256) k_ba_hfinal(const int* __restrict__ nfp, int chunk, int nout,
                                                    const double* __restrict__ part, double* __restrict__ out,
-                                                   const BaState* __restrict__ st) {
+                                                   const BaState* __restrict__ st, XchgArg xa) {
+  if (xa.frame && blockIdx.x == 0 && threadIdx.x == 0) xchg_close(xa.frame, xa.n, 3, xa.seq);
   if (st->done || !st->calc_hess) return;
   const int nchunk = (*nfp + chunk - 1) / chunk;
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
@@ -584,8 +586,18 @@ __global__ void __launch_bounds__(256) k_ba_prep(int W, int nimu, double imu_coe
                                                  double* __restrict__ Jcalc, double* __restrict__ timg,
                                                  double* __restrict__ bvec, double* __restrict__ dvec,
                                                  double* __restrict__ jvec, int* __restrict__ ipg,
-                                                 BaState* __restrict__ st, int structural) {
+                                                 BaState* __restrict__ st, int structural, int xworld,
+                                                 int* __restrict__ xerr) {
   if (st->done) return;
+  // sharded: `hl` is the all-reduced exchange frame; a guard mismatch ends the
+  // LM (error bit 32: the scan fails with VG_E_STATE)
+  if (xworld > 0 && !xchg_ok(hl, 3 * W * (6 * W + 1) + 6 * W + 1 + 2, xworld)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      atomicOr(xerr, 32);
+      st->done = 1;
+    }
+    return;
+  }
   constexpr int kN = kMaxNB * kTile;
   __shared__ double Dv[kN], Jg[kN];
   __shared__ int ip[kN];
@@ -1064,6 +1076,8 @@ struct CtlArg {
   BaState* st;
   Pub* pub;
   int* err;   // k_ba_resid runs the bookkeeping (nullptr: k_ba_control follows); error bit 64 on a stalled hand-off
+  int xworld;  // sharded: rpart is the all-reduced exchange frame, its guard checked here (mismatch: bit 32 in xerr)
+  int* xerr;
 };
 // `pre`: the lane's strided sum of the residual partials, already formed (k_ba_resid).
 // The sums run over the first kResidThreads lanes whatever the workgroup size
@@ -1074,8 +1088,10 @@ __device__ __forceinline__ void ba_control_body(const CtlArg& c, const double* p
   const int nt = kResidThreads;
   {  // residual partials: lane-strided sums, then a fixed tree (deterministic)
     double part = 0.0;
+    const bool ok = c.xworld <= 0 || xchg_ok(c.rpart, kShardSmall, c.xworld);  // (the frame's consumers read zeros)
+    if (!ok && threadIdx.x == 0) atomicOr(c.xerr, 32);
     if (pre) part = *pre;
-    else if (!c.st->done)
+    else if (!c.st->done && ok)
       for (int b = threadIdx.x; b < c.nrb; b += nt) part += c.rpart[b];
     if ((int)threadIdx.x < nt) s_r[threadIdx.x] = part;
     __syncthreads();
@@ -1316,14 +1332,16 @@ __global__ void __launch_bounds__(kHessThreads) k_ba_resid_hess(const int* __res
   }
 }
 
-// sharded mode: this shard's factor residual (ordered sum of the block partials)
-__global__ void k_ba_rsum(int nrb, const double* __restrict__ rpart, double* __restrict__ out,
-                          const BaState* __restrict__ st) {
+// sharded mode: this shard's factor residual (ordered sum of the block
+// partials) packed into the exchange frame (k_ba_control checks its guard)
+__global__ void k_ba_rsum(int nrb, const double* __restrict__ rpart, const BaState* __restrict__ st, XchgArg xa) {
+  for (int i = threadIdx.x + 1; i < xa.n - 2; i += blockDim.x) xa.frame[i] = 0.0;
   if (threadIdx.x == 0) {
     double r = 0.0;
     if (!st->done)
       for (int b = 0; b < nrb; b++) r += rpart[b];
-    out[0] = r;
+    xa.frame[0] = r;
+    xchg_close(xa.frame, xa.n, 4, xa.seq);
   }
 }
 
@@ -1599,8 +1617,6 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr, int rh
   const int nimu = W - 1;
   const int L = 6 * W, nl = L * (L + 1) / 2, nout = nl + L + 1;
   const bool shard_on = sharded(ctx);
-  double* hl_part = ctx->ba.hout_part;  // this shard's LiDAR Hessian (sharded mode)
-  double* rsum = ctx->shard.d_buf + 256;  // [0]: this shard's residual, [1]: all-reduced
   // factor count on the device (the recut's kCntFactors): fixed grids, so an
   // asynchronous recut needs no host round trip before the LM
   const int* nfp = ctx->map.counters + kCntFactors;
@@ -1609,8 +1625,14 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr, int rh
   const size_t hess_lds = hess_lds_bytes(W);
   const size_t solve_lds = solve_lds_bytes(W);
   const int NBt = (15 * W - 15 + kTile - 1) / kTile, ntile = NBt * (NBt + 1) / 2;
-  CtlArg ctl{W, nimu, shard_on ? 1 : nrb, nl + L, ctx->cfg.imu_coef, d.hl, d.imuout, d.imures,
-             shard_on ? rsum + 1 : d.rpart, d.xs, d.xt, d.bias, d.st, ctx->d_pub, nullptr};
+  Shard& sh = ctx->shard;
+  // sharded: the Hessian / gradient / residual frame and the trial residual's
+  // frame are packed by k_ba_hfinal / k_ba_rsum and checked by k_ba_prep /
+  // k_ba_control (no pack / unpack launches)
+  const double* hlx = shard_on ? sh.d_frame : d.hl;  // the LiDAR system the assembly reads
+  CtlArg ctl{W, nimu, shard_on ? 1 : nrb, nl + L, ctx->cfg.imu_coef, hlx, d.imuout, d.imures,
+             shard_on ? sh.d_frame : d.rpart, d.xs, d.xt, d.bias, d.st, ctx->d_pub, nullptr,
+             shard_on ? sh.world : 0, ctx->map.counters + kCntErr};
   CtlArg ctl_fused = ctl;  // unsharded: the bookkeeping rides in k_ba_resid's IMU workgroup
   if (!shard_on && ctx->ba_fuse_ctl) ctl_fused.err = ctx->map.counters + kCntErr;
   if (ih)
@@ -1622,11 +1644,11 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr, int rh
     k_ba_hess<<<G + nimu, kHessThreads, hess_lds, s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
                                                       ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, nimu, d.imurec,
                                                       &ctx->st->imu_head, d.bias, d.imuout, &ctx->st->clk);
-  k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, shard_on ? hl_part : d.hl,
-                                                       d.st);
+  const XchgArg xh{shard_on ? sh.d_frame : nullptr, sh.d_seq, ctx->map.counters + kCntErr, sh.frame_n, sh.world};
+  k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, shard_on ? sh.d_frame : d.hl,
+                                                       d.st, xh);
   // sharded: every shard's factors -> one LiDAR Hessian / gradient / residual
-  // (out of place: a rejected step re-reduces the unchanged partial)
-  if (shard_on && xerr == VG_OK) xerr = shard_allreduce(ctx, hl_part, d.hl, nout, 0, 3);
+  if (shard_on && xerr == VG_OK) xerr = shard_exchange(ctx, sh.frame_n);
   if (k == 0 && ctx->dbg_capture == 1 && ctx->dbg_cap_buf) {  // test knob (vgx_debug 5): the first pass
     (void)hipMemcpyAsync(ctx->dbg_cap_buf, d.hl, nout * sizeof(double), hipMemcpyDeviceToDevice, s);
     (void)hipMemcpyAsync(ctx->dbg_cap_buf + nout, d.imuout, (size_t)nimu * 931 * sizeof(double),
@@ -1634,8 +1656,9 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr, int rh
     ctx->dbg_cap_n = nout + nimu * 931;
     ctx->dbg_capture = 2;
   }
-  k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, d.hl, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
-                                  d.dvec, d.jvec, d.ipg, d.st, ctx->ba_structural ? 1 : 0);
+  k_ba_prep<<<ntile, 256, 0, s>>>(W, nimu, ctx->cfg.imu_coef, hlx, d.imuout, d.Hcalc, d.Jcalc, d.timg, d.bvec,
+                                  d.dvec, d.jvec, d.ipg, d.st, ctx->ba_structural ? 1 : 0, shard_on ? sh.world : 0,
+                                  ctx->map.counters + kCntErr);
   if (solve_ev) (void)hipEventRecord(ctx->solve_ev[k][0], s);
   k_ba_solve<<<1, 1024, solve_lds, s>>>(W, nimu, d.timg, d.bvec, d.dvec, d.jvec, d.ipg, d.xs, d.xt, d.bias, d.dxi,
                                        d.st, &ctx->st->clk);
@@ -1649,8 +1672,9 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr, int rh
                                                  d.xt, ctx->ba.fac_eig, ctx->ba.fac_pcr, d.rpart, d.st, nrb, nimu,
                                                  d.imurec, &ctx->st->imu_head, d.bias, d.imures, ctl_fused);
   if (shard_on) {  // the residual over every shard's factors
-    k_ba_rsum<<<1, 64, 0, s>>>(nrb, d.rpart, rsum, d.st);
-    if (xerr == VG_OK) xerr = shard_allreduce(ctx, rsum, rsum + 1, 1, 0, 4);
+    k_ba_rsum<<<1, 64, 0, s>>>(nrb, d.rpart, d.st,
+                               XchgArg{sh.d_frame, sh.d_seq, ctx->map.counters + kCntErr, kShardSmall, sh.world});
+    if (xerr == VG_OK) xerr = shard_exchange(ctx, kShardSmall);
   }
   if (!ctl_fused.err) k_ba_control<<<1, 256, 0, s>>>(ctl);
 }
@@ -1916,7 +1940,7 @@ int ba_lidar_pass(vg_ctx* ctx, bool hessian, const double* poses, const int* mp_
     k_ba_hess<<<G, kHessThreads, hess_lds_bytes(W), s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
                                                         ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, 0, d.imurec,
                                                         &ctx->st->imu_head, d.bias, d.imuout, nullptr);
-    k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, d.hl, d.st);
+    k_ba_hfinal<<<(nout * 8 + 255) / 256, 256, 0, s>>>(nfp, hess_chunk(W), nout, d.part, d.hl, d.st, XchgArg{});
     VG_HIP(hipGetLastError());
     VG_HIP(hipMemcpyAsync(h, d.hl, nout * sizeof(double), hipMemcpyDeviceToHost, s));
     VG_HIP(hipStreamSynchronize(s));

@@ -474,20 +474,27 @@ __global__ void __launch_bounds__(256) k_iekf_planes(const DState* __restrict__ 
 // insert hand-off flag (one workgroup: one release), so no k_sync_set launch
 // follows the IEKF graph
 __global__ void __launch_bounds__(1024) k_iekf_update(int nb, const double* __restrict__ partials,
-                                                     DState* __restrict__ st, int it, unsigned* done_flag) {
+                                                     DState* __restrict__ st, int it, unsigned* done_flag,
+                                                     int xworld, int* xerr) {
   __shared__ IekfLds L;
   if (st->done) return;
-  iekf_update_block(nb, partials, st, it, L);
+  iekf_update_block(nb, partials, st, it, L, xworld, xerr);
   if (done_flag && L.fin) iekf_signal_done(done_flag);
 }
 // sharded mode: this shard's 34 sums (the update then runs on the all-reduced ones)
+// sharded mode: this shard's 34 sums, packed into the exchange frame (the
+// update runs on the all-reduced frame, k_iekf_update checks its guard); an
+// iteration after convergence still closes the frame (the exchange runs)
 __global__ void __launch_bounds__(256) k_iekf_reduce(int nb, const double* __restrict__ partials,
-                                                     const DState* __restrict__ st, double* __restrict__ out) {
+                                                     const DState* __restrict__ st, XchgArg xa) {
   __shared__ IekfLds L;
-  if (st->done) return;
-  const int n = st->sn;
-  iekf_reduce_block(nb, partials, L, n < nb * 256 ? (n + 255) / 256 : nb);
-  if (threadIdx.x < kIekfVals) out[threadIdx.x] = L.o[threadIdx.x];
+  const bool done = st->done;
+  if (!done) {
+    const int n = st->sn;
+    iekf_reduce_block(nb, partials, L, n < nb * 256 ? (n + 255) / 256 : nb);
+  }
+  for (int i = threadIdx.x; i < xa.n - 2; i += blockDim.x) xa.frame[i] = (!done && i < kIekfVals) ? L.o[i] : 0.0;
+  if (threadIdx.x == 0) xchg_close(xa.frame, xa.n, 0, xa.seq);
 }
 
 // grid of the IEKF point loop: sized by the context's capacity (the kernels
@@ -513,13 +520,14 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
   kern<<<nb, 256, 0, s>>>(mp, ctx->st, it, ctx->map, w.iekf_cache, w.partials, tag ? w.pk_leaf : nullptr);
   if (ev1) VG_HIP(hipEventRecord(ev1, s));
   if (tag) k_iekf_planes<<<nb, 256, 0, s>>>(ctx->st, ctx->map, w.pk_leaf, tag, &ctx->st->planes[it]);
-  if (sharded(ctx)) {  // this shard's sums, all-reduced, then the (replicated) update
-    double* sums = ctx->shard.d_buf;
-    k_iekf_reduce<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, sums);
-    VG_TRY(shard_allreduce(ctx, sums, sums + 64, kIekfVals, 0, 0));
-    k_iekf_update<<<1, 1024, 0, s>>>(-1, sums + 64, ctx->st, it, nullptr);
+  if (sharded(ctx)) {  // this shard's sums packed into the frame, all-reduced, then the (replicated) update
+    Shard& sh = ctx->shard;
+    const XchgArg xa{sh.d_frame, sh.d_seq, ctx->map.counters + kCntErr, kShardSmall, sh.world};
+    k_iekf_reduce<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, xa);
+    VG_TRY(shard_exchange(ctx, kShardSmall));
+    k_iekf_update<<<1, 1024, 0, s>>>(-1, sh.d_frame, ctx->st, it, nullptr, sh.world, ctx->map.counters + kCntErr);
   } else {
-    k_iekf_update<<<1, 1024, 0, s>>>(nb, w.partials, ctx->st, it, done_flag);
+    k_iekf_update<<<1, 1024, 0, s>>>(nb, w.partials, ctx->st, it, done_flag, 0, nullptr);
   }
   VG_HIP(hipGetLastError());
   return VG_OK;

@@ -133,6 +133,38 @@ int shard_allreduce(vg_ctx* ctx, const void* send, void* recv, int count, int dt
   return VG_OK;
 }
 
+// the all-reduce of a frame its producer kernel packed (xchg_close) and its
+// consumer kernel checks (xchg_ok): RCCL on the stream, or the host transport
+// (which checks the guard itself as well, to fail at once)
+int shard_exchange(vg_ctx* ctx, int n) {
+  Shard& sh = ctx->shard;
+  if (sh.mode == 1) {
+    const ncclResult_t r =
+        ncclAllReduce(sh.d_frame, sh.d_frame, (size_t)n, ncclFloat64, ncclSum, (ncclComm_t)sh.comm, ctx->stream);
+    if (r != ncclSuccess) {
+      ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
+      return VG_E_HIP;
+    }
+    return VG_OK;
+  }
+  VG_HIP(hipMemcpyAsync(sh.h_buf, sh.d_frame, (size_t)(n + 1) * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  VG_HIP(stream_wait(ctx));
+  const double x = sh.h_buf[n];
+  if (sh.host_fn(sh.h_buf, n, 0, sh.user) != 0) {
+    ctx->err = "host all-reduce callback failed";
+    return VG_E_HIP;
+  }
+  if (!(sh.h_buf[n - 2] == sh.world * x && sh.h_buf[n - 1] == sh.world * (x * x))) {
+    ctx->err = "sharded exchange out of step: the ranks' exchange sequences differ (site " +
+               std::to_string((int)x & 15) + ", exchange " + std::to_string((int)x >> 4) + " mod 2^16)";
+    return VG_E_STATE;
+  }
+  sh.h_buf[n] = x;
+  VG_HIP(hipMemcpyAsync(sh.d_frame, sh.h_buf, (size_t)(n + 1) * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  VG_HIP(stream_wait(ctx));  // the staging buffer is reused by the next exchange
+  return VG_OK;
+}
+
 static int shard_common(vg_ctx* ctx, int rank, int world) {
   if (world < 1 || rank < 0 || rank >= world) {
     ctx->err = "vg_shard: rank/world out of range";

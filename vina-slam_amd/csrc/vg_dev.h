@@ -559,4 +559,28 @@ __device__ __forceinline__ void fac_sort_block(DevMap& m, int* __restrict__ rc, 
   }
 }
 
+// ---- sharded exchange frames packed / checked inside their producer and
+// consumer kernels (shard.hip's guard; shard_exchange): one thread closes the
+// frame after its payload [0, n - 2) is stored (zeros past the payload are the
+// producer's), the consumer tests the summed guard pair against its own x
+__device__ __forceinline__ void xchg_close(double* __restrict__ frame, int n, int site, unsigned* __restrict__ seq) {
+  const unsigned s = *seq;
+  *seq = s + 1;
+  const double x = (double)((s & 0xffffu) * 16u + (unsigned)site);
+  frame[n - 2] = x;
+  frame[n - 1] = x * x;
+  frame[n] = x;  // this rank's own x (not exchanged)
+}
+__device__ __forceinline__ bool xchg_ok(const double* __restrict__ frame, int n, int world) {
+  const double x = frame[n];
+  return frame[n - 2] == world * x && frame[n - 1] == world * (x * x);
+}
+// a producer's frame: its consumer checks it (world), reports a mismatch (err, bit 32)
+struct XchgArg {
+  double* frame;
+  unsigned* seq;
+  int* err;
+  int n, world;
+};
+
 }  // namespace vg

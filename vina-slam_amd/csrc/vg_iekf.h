@@ -105,8 +105,11 @@ __device__ __forceinline__ void iekf_vec(const DState* __restrict__ st, IekfLds&
     L.vec[12 + k] = xp[18 + k] - xc[18 + k];
   }
 }
+// nb < 0 (sharded): `partials` is the all-reduced exchange frame; xworld > 0:
+// its guard is checked here (a mismatch sets error bit 32 and the update runs
+// on zeros, as a separately unpacked frame's consumers did)
 __device__ void iekf_update_block(int nb, const double* __restrict__ partials, DState* __restrict__ st, int it,
-                                  IekfLds& L) {
+                                  IekfLds& L, int xworld = 0, int* xerr = nullptr) {
   const int tid = threadIdx.x;
   VG_PROBE_BEGIN();
   // x_curr does not change before the update's end: vec on a lane the
@@ -119,7 +122,9 @@ __device__ void iekf_update_block(int nb, const double* __restrict__ partials, D
     const int n = st->sn;
     iekf_reduce_block(nb, partials, L, n < nb * 256 ? (n + 255) / 256 : nb);
   } else {  // sharded mode: `partials` holds the all-reduced sums
-    if (tid < kIekfVals) L.o[tid] = partials[tid];
+    const bool ok = xworld <= 0 || xchg_ok(partials, kShardSmall, xworld);
+    if (!ok && tid == 0) atomicOr(xerr, 32);
+    if (tid < kIekfVals) L.o[tid] = ok ? partials[tid] : 0.0;
     __syncthreads();
   }
   VG_PROBE_MARK(23);  // the ordered sum of the block partials

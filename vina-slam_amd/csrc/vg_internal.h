@@ -326,6 +326,10 @@ struct HostIn {
 // (RCCL on the context stream, or a host callback for CPU-mediated tests).
 constexpr int kShardBuf = 4096;  // doubles of exchange scratch / staging
 constexpr int kShardSmall = 64;   // doubles of a small exchange frame (payload + guard pair)
+// a frame its producer kernel packed and its consumer kernel checks (the IEKF
+// sums, the LM's Hessian and residual): the all-reduce alone, no pack / unpack
+// launches (shard.hip)
+int shard_exchange(vg_ctx* ctx, int n);
 struct Shard {
   int rank = 0, world = 1;
   int mode = 0;              // 0 none, 1 RCCL, 2 host callback
