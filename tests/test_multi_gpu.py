@@ -30,8 +30,10 @@ def _ctx(p, seq):
     return c
 
 
-@pytest.mark.parametrize("lidar,B", [("16line", 3), ("64line", 2)])
-def test_multi_sequences_match_lone_runs(lidar, B):
+@pytest.mark.parametrize("lidar,B,cap", [("16line", 3, 0), ("64line", 2, 0), ("16line", 8, 0), ("16line", 8, 4)])
+def test_multi_sequences_match_lone_runs(lidar, B, cap):
+    """B = 8 with cap 4 is the bench's form past four sequences (slots shared
+    by two sequences each, vg_multi_set_active)."""
     import torch
     dev = torch.device("cuda", 0)
     p = vgconfig.load("mid360")
@@ -49,6 +51,8 @@ def test_multi_sequences_match_lone_runs(lidar, B):
         c.close()
     ctxs = [_ctx(p, s) for s in seqs]
     mv = vgpu.Multi(ctxs)
+    if cap:
+        mv.set_active(cap)
     for k in range(nscan):
         scans = []
         for d in data:
