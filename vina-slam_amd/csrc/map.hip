@@ -1679,7 +1679,8 @@ __device__ __forceinline__ void rc_win_leaf(int L, int leaf, int q, const WinD* 
 #endif
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int wc = win->win_count;
-  const int my_slot = (lane >= 1 && lane <= wc) ? win->mp[lane - 1] : 0;
+  const int mp_l = win->mp[lane >= 1 && lane <= 32 ? lane - 1 : 0];  // in the same round of loads as wc
+  const int my_slot = (lane >= 1 && lane <= wc) ? mp_l : 0;
   const NodeHdr& h = m.hdr[leaf];
   int len = 0, st = 0;
   if (lane == 0) len = h.fix_cnt;
@@ -1949,7 +1950,8 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
   // the prologue's other loads go out with the keys' (one round): each
   // lane's window slot and its epoch, the frame clusters (s_pre, stored
   // below) and the accumulators' starting values
-  const int my_slot = lane < win->win_count ? win->mp[lane] : 0;  // listed or not (the batches read it)
+  const int mp_l = win->mp[lane < 32 ? lane : 0];  // in the same round of loads as win_count
+  const int my_slot = lane < win->win_count ? mp_l : 0;  // listed or not (the batches read it)
   const int my_epoch = lane < wc ? m.slot_epoch[my_slot] : 0;
   double pv[kPreV];
 #pragma unroll
@@ -2018,44 +2020,51 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
   }
   // the point_fix block and the slots' runs are allocated in one round (an
   // overflow of either fails the scan with VG_E_CAPACITY, so a run taken
-  // beside a point_fix overflow is never used)
+  // beside a point_fix overflow is never used); the returning atomics are
+  // consumed after the first batch's loads (settle), so their round trip
+  // overlaps those loads
   int off = 0, run_st = 0;
   if (lane == 0 && nfix > 0 && listed) off = atomicAdd(&m.counters[kCntFix], nfix);
   if (lane < wc && run_n > 0) run_st = atomicAdd(&m.arena[my_slot], run_n);
   int fix_off = 0;
-  if (nfix > 0 && listed) {
-    if (lane == 0) {
-      if (off + nfix > m.cap_fix) {
-        atomicOr(&m.counters[kCntErr], 8);
-        off = -1;
+  bool settled = false;
+  auto settle = [&]() __attribute__((always_inline)) {  // false: point_fix overflow (wave-uniform)
+    settled = true;
+    if (nfix > 0 && listed) {
+      if (lane == 0) {
+        if (off + nfix > m.cap_fix) {
+          atomicOr(&m.counters[kCntErr], 8);
+          off = -1;
+        } else {
+          h.fix_off = off;
+          h.fix_cap = nfix;
+          h.fix_cnt = nfix;
+        }
+      }
+      fix_off = __shfl(off, 0, 64);
+      if (fix_off < 0) return false;
+    }
+    // lane p < win_count holds phase p + 1's run in the slot's arena
+    if (lane < wc && run_n > 0) {
+      if (run_st + run_n > m.ord_stride) {
+        atomicOr(&m.counters[kCntErr], 16);
+        run_st = 0;
       } else {
-        h.fix_off = off;
-        h.fix_cap = nfix;
-        h.fix_cnt = nfix;
+        m.lseg[(size_t)child * mp.W + my_slot] = lseg_pack(run_st, run_n, my_epoch);
       }
     }
-    fix_off = __shfl(off, 0, 64);
-    if (fix_off < 0) return;
-  }
-  // lane p < win_count holds phase p + 1's run in the slot's arena
-  if (lane < wc && run_n > 0) {
-    if (run_st + run_n > m.ord_stride) {
-      atomicOr(&m.counters[kCntErr], 16);
-      run_st = 0;
-    } else {
-      m.lseg[(size_t)child * mp.W + my_slot] = lseg_pack(run_st, run_n, my_epoch);
-    }
-  }
-  // every slot's frame cluster, loaded above in one round (a slot's run is
-  // contiguous, so each is read once, before this wave writes it): a cluster
-  // switch then costs an LDS read, not a dependent HBM load; their point
-  // counts sit at s_pre[kPreN + slot], so the count update at a switch is a
-  // plain store
+    // every slot's frame cluster, loaded above in one round (a slot's run is
+    // contiguous, so each is read once, before this wave writes it): a
+    // cluster switch then costs an LDS read, not a dependent HBM load; their
+    // point counts sit at s_pre[kPreN + slot], so the count update at a
+    // switch is a plain store
 #pragma unroll
-  for (int i = 0; i < kPreV; i++) {
-    const int t = lane + 64 * i;
-    if (t < mp.W * 10) s_pre[t < mp.W * 9 ? t : kPreN + t - mp.W * 9] = pv[i];
-  }
+    for (int i = 0; i < kPreV; i++) {
+      const int t = lane + 64 * i;
+      if (t < mp.W * 10) s_pre[t < mp.W * 9 ? t : kPreN + t - mp.W * 9] = pv[i];
+    }
+    return true;
+  };
   int cur_slot = -1, loc_n = 0, nwin = 0;
   PUSH_MARK(42);
   for (int b0 = j0; b0 < j1; b0 += 64) {
@@ -2064,18 +2073,15 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
                                  : (bi == 0 ? kv[0] : bi == 1 ? kv[1] : bi == 2 ? kv[2] : kv[3]);
     const int phase = (int)((k >> 21) & 63), idx = (int)(k & ((1u << 21) - 1));
     const int slot_e = __shfl(my_slot, phase > 0 ? phase - 1 : 0, 64);  // win->mp[phase - 1]
+    V3 pt;
+    M3 var;
     if (e < j1) {
       if (phase == 0) {
         const size_t f = (size_t)ph.fix_off + idx;
-        const V3 pt = ld_v3(&m.fix_pnt[f * 3]);
-        const M3 var = ld_m3(&m.fix_var[f * 9]);
+        pt = ld_v3(&m.fix_pnt[f * 3]);
+        var = ld_m3(&m.fix_var[f * 9]);
         fill_record(E[lane], pt, pt, var);
         s_slot[lane] = -1;
-        if (listed) {
-          const size_t d = (size_t)fix_off + (e - j0);
-          for (int t = 0; t < 3; t++) m.fix_pnt[d * 3 + t] = pt[t];
-          for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = var[t];
-        }
       } else {
         const int ord = phase - 1, slot = slot_e;
         const size_t bb = (size_t)slot * m.cap_wp + idx;
@@ -2085,6 +2091,12 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
         s_slot[lane] = slot;
         m.wp_leaf[bb] = listed ? child : -1;
       }
+    }
+    if (!settled && !settle()) return;
+    if (e < j1 && phase == 0 && listed) {  // the point_fix copy into the child's block
+      const size_t d = (size_t)fix_off + (e - j0);
+      for (int t = 0; t < 3; t++) m.fix_pnt[d * 3 + t] = pt[t];
+      for (int t = 0; t < 9; t++) m.fix_var[d * 9 + t] = var[t];
     }
     if (listed) {  // the point into the child's run (ds_bpermute of the run's lane; uniform call)
       const int ph = e < j1 ? phase : 0;
@@ -2126,6 +2138,7 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
     PUSH_MARK(44);
   }
 #undef PUSH_MARK
+  if (!settled && !settle()) return;  // no events
   if (r0 < 63) *acc_ptr(r0, 0) = a0;
   if (cur_slot >= 0) {
     if (r0 >= 63) *acc_ptr(r0, cur_slot) = a0;
