@@ -488,17 +488,17 @@ __global__ void __launch_bounds__(256) k_ba_hfinal(const int* __restrict__ nfp, 
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = gt >> 3, sub = gt & 7;
   double s = 0.0;
-  if (e < nout) {  // chunks sub, sub + 8, ... in order; 16 loads issued per batch, then added
-    constexpr int kB = 16;
-    int b = sub;
-    for (; b + 8 * (kB - 1) < nchunk; b += 8 * kB) {
+  if (e < nout) {  // chunks sub, sub + 8, ... in order; up to 32 loads issued per batch (one batch up to
+                   // 256 chunks: one memory round trip), then added
+    constexpr int kB = 32;
+    for (int b = sub; b < nchunk; b += 8 * kB) {
       double v[kB];
 #pragma unroll
-      for (int k = 0; k < kB; k++) v[k] = part[(size_t)(b + 8 * k) * nout + e];
+      for (int k = 0; k < kB; k++) v[k] = b + 8 * k < nchunk ? part[(size_t)(b + 8 * k) * nout + e] : 0.0;
 #pragma unroll
-      for (int k = 0; k < kB; k++) s += v[k];
+      for (int k = 0; k < kB; k++)
+        if (b + 8 * k < nchunk) s += v[k];
     }
-    for (; b < nchunk; b += 8) s += part[(size_t)b * nout + e];
   }
   s += __shfl_down(s, 4, 8);
   s += __shfl_down(s, 2, 8);
