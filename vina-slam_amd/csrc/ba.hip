@@ -1091,8 +1091,17 @@ __device__ __forceinline__ void ba_control_body(const CtlArg& c, const double* p
     const bool ok = c.xworld <= 0 || xchg_ok(c.rpart, kShardSmall, c.xworld);  // (the frame's consumers read zeros)
     if (!ok && threadIdx.x == 0) atomicOr(c.xerr, 32);
     if (pre) part = *pre;
-    else if (!c.st->done && ok)
-      for (int b = threadIdx.x; b < c.nrb; b += nt) part += c.rpart[b];
+    else if (!c.st->done && ok) {  // a lane's loads in one batch, summed in the same order
+      constexpr int kU = 4;
+      for (int b0 = threadIdx.x; b0 < c.nrb; b0 += kU * nt) {
+        double v[kU];
+#pragma unroll
+        for (int k = 0; k < kU; k++) v[k] = b0 + k * nt < c.nrb ? c.rpart[b0 + k * nt] : 0.0;
+#pragma unroll
+        for (int k = 0; k < kU; k++)
+          if (b0 + k * nt < c.nrb) part += v[k];
+      }
+    }
     if ((int)threadIdx.x < nt) s_r[threadIdx.x] = part;
     __syncthreads();
     for (int w = nt >> 1; w > 0; w >>= 1) {
@@ -1334,11 +1343,32 @@ __global__ void __launch_bounds__(kHessThreads) k_ba_resid_hess(const int* __res
 
 // sharded mode: this shard's factor residual (ordered sum of the block
 // partials) packed into the exchange frame (k_ba_control checks its guard)
+// (the partials staged in LDS by every lane in one round of loads, then the
+// same sequential sum on one lane)
 __global__ void k_ba_rsum(int nrb, const double* __restrict__ rpart, const BaState* __restrict__ st, XchgArg xa) {
+  __shared__ double sp[kResidBlocks];
   for (int i = threadIdx.x + 1; i < xa.n - 2; i += blockDim.x) xa.frame[i] = 0.0;
+  const bool run = !st->done && nrb <= kResidBlocks;
+  if (run) {
+    constexpr int kU = kResidBlocks / 64;
+    double v[kU];
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const int b = threadIdx.x + 64 * k;
+      v[k] = b < nrb ? rpart[b] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const int b = threadIdx.x + 64 * k;
+      if (b < nrb) sp[b] = v[k];
+    }
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     double r = 0.0;
-    if (!st->done)
+    if (run)
+      for (int b = 0; b < nrb; b++) r += sp[b];
+    else if (!st->done)
       for (int b = 0; b < nrb; b++) r += rpart[b];
     xa.frame[0] = r;
     xchg_close(xa.frame, xa.n, 4, xa.seq);
