@@ -485,7 +485,7 @@ __global__ void __launch_bounds__(1024) k_iekf_update(int nb, const double* __re
 // sharded mode: this shard's 34 sums, packed into the exchange frame (the
 // update runs on the all-reduced frame, k_iekf_update checks its guard); an
 // iteration after convergence still closes the frame (the exchange runs)
-__global__ void __launch_bounds__(256) k_iekf_reduce(int nb, const double* __restrict__ partials,
+__global__ void __launch_bounds__(1024) k_iekf_reduce(int nb, const double* __restrict__ partials,
                                                      const DState* __restrict__ st, XchgArg xa) {
   __shared__ IekfLds L;
   const bool done = st->done;
@@ -523,7 +523,7 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
   if (sharded(ctx)) {  // this shard's sums packed into the frame, all-reduced, then the (replicated) update
     Shard& sh = ctx->shard;
     const XchgArg xa{sh.d_frame, sh.d_seq, ctx->map.counters + kCntErr, kShardSmall, sh.world};
-    k_iekf_reduce<<<1, 256, 0, s>>>(nb, w.partials, ctx->st, xa);
+    k_iekf_reduce<<<1, 1024, 0, s>>>(nb, w.partials, ctx->st, xa);  // (the unsharded update's 60 row groups)
     VG_TRY(shard_exchange(ctx, kShardSmall));
     k_iekf_update<<<1, 1024, 0, s>>>(-1, sh.d_frame, ctx->st, it, nullptr, sh.world, ctx->map.counters + kCntErr);
   } else {
