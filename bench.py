@@ -547,51 +547,60 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=Non
             out["wait_policy"] = "spin %s us, then sleep %s us" % tuple(wait.split(","))
         grp = args.multi_group
         for B in Bs:
-            beat("multi-sequence %s: B = %d" % (lidar, B))
-            # the child warms up, reports READY and waits; the parent then
-            # releases it and times the job from GO to its end.
-            # B > grp: ONE process whose B streams share grp hardware queues
-            # (GPU_MAX_HW_QUEUES = grp): past ~4 hardware queues the GPU
-            # time-slices them (profiles/r04/multi_pmc_r04g.json: same L2 hit
-            # rates, a ~47 us floor per kernel at B = 8), and B = 8 / 16 over
-            # 4 shared queues ran 2,839 / 3,140 scans/s against 2,565 / ~2,250
-            # over private queues (profiles/r04/multi_hwq_r04.json)
-            P = 1
-            benv = dict(env, GPU_MAX_HW_QUEUES=str(grp)) if B > grp else env
-            out.setdefault("hw_queues_by_B", {})[str(B)] = int(benv["GPU_MAX_HW_QUEUES"])
-            sizes = [B // P + (1 if q < B % P else 0) for q in range(P)]
-            runs, first_seq = [], 0
-            for q in range(P):
-                cmd = [sys.executable, os.path.abspath(__file__), "--multi-child", str(sizes[q]),
-                       "--multi-scans", ",".join(paths[first_seq:first_seq + sizes[q]]),
-                       "--multi-max-points", str(npmax + 16),
-                       "--lidar", lidar, "--config", args.config, "--steps", str(steps), "--warmup", str(args.warmup),
-                       "--max-nodes", str(args.max_nodes), "--max-fix", str(args.max_fix),
-                       "--hash-log2", str(args.hash_log2), "--multi-active", str(args.multi_active)]
-                first_seq += sizes[q]
-                runs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=benv))
-            for r in runs:  # every child warmed up and idle
-                line = r.stdout.readline()
-                if line.strip() != "READY":
-                    for x in runs:
-                        x.kill()
-                    raise RuntimeError("multi-sequence child B=%d: %r" % (B, line[-500:]))
-            t0 = time.perf_counter()
-            for r in runs:
-                r.stdin.write("GO\n")
-                r.stdin.flush()
-            res = []
-            for r in runs:
-                res.append(json.loads(r.stdout.readline()))
-            wall = time.perf_counter() - t0
-            for r in runs:
-                r.stdin.close()
-                r.wait(timeout=60)
-                if r.returncode != 0:
-                    raise RuntimeError("multi-sequence child B=%d failed (%d)" % (B, r.returncode))
-            out["by_B"][str(B)] = round(B * steps / wall, 1)
-            out.setdefault("processes_by_B", {})[str(B)] = P
-            out.setdefault("points_per_scan", res[0]["points_per_scan"])
+            # a child that fails (or crashes) costs this B its number, not the line
+            runs = []
+            try:
+                beat("multi-sequence %s: B = %d" % (lidar, B))
+                # the child warms up, reports READY and waits; the parent then
+                # releases it and times the job from GO to its end.
+                # B > grp: ONE process whose B streams share grp hardware queues
+                # (GPU_MAX_HW_QUEUES = grp): past ~4 hardware queues the GPU
+                # time-slices them (profiles/r04/multi_pmc_r04g.json: same L2 hit
+                # rates, a ~47 us floor per kernel at B = 8), and B = 8 / 16 over
+                # 4 shared queues ran 2,839 / 3,140 scans/s against 2,565 / ~2,250
+                # over private queues (profiles/r04/multi_hwq_r04.json)
+                P = 1
+                benv = dict(env, GPU_MAX_HW_QUEUES=str(grp)) if B > grp else env
+                out.setdefault("hw_queues_by_B", {})[str(B)] = int(benv["GPU_MAX_HW_QUEUES"])
+                sizes = [B // P + (1 if q < B % P else 0) for q in range(P)]
+                runs, first_seq = [], 0
+                for q in range(P):
+                    cmd = [sys.executable, os.path.abspath(__file__), "--multi-child", str(sizes[q]),
+                           "--multi-scans", ",".join(paths[first_seq:first_seq + sizes[q]]),
+                           "--multi-max-points", str(npmax + 16),
+                           "--lidar", lidar, "--config", args.config, "--steps", str(steps), "--warmup", str(args.warmup),
+                           "--max-nodes", str(args.max_nodes), "--max-fix", str(args.max_fix),
+                           "--hash-log2", str(args.hash_log2), "--multi-active", str(args.multi_active)]
+                    first_seq += sizes[q]
+                    runs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=benv))
+                for r in runs:  # every child warmed up and idle
+                    line = r.stdout.readline()
+                    if line.strip() != "READY":
+                        for x in runs:
+                            x.kill()
+                        raise RuntimeError("multi-sequence child B=%d: %r" % (B, line[-500:]))
+                t0 = time.perf_counter()
+                for r in runs:
+                    r.stdin.write("GO\n")
+                    r.stdin.flush()
+                res = []
+                for r in runs:
+                    res.append(json.loads(r.stdout.readline()))
+                wall = time.perf_counter() - t0
+                for r in runs:
+                    r.stdin.close()
+                    r.wait(timeout=60)
+                    if r.returncode != 0:
+                        raise RuntimeError("multi-sequence child B=%d failed (%d)" % (B, r.returncode))
+                out["by_B"][str(B)] = round(B * steps / wall, 1)
+                out.setdefault("processes_by_B", {})[str(B)] = P
+                out.setdefault("points_per_scan", res[0]["points_per_scan"])
+            except Exception as ex:  # noqa: BLE001
+                for r in runs:
+                    if r.poll() is None:
+                        r.kill()
+                out.setdefault("failed_by_B", {})[str(B)] = str(ex)[-300:]
+                beat("multi-sequence %s: B = %d failed: %s" % (lidar, B, str(ex)[-200:]))
     finally:
         for path in paths:
             os.unlink(path)
