@@ -65,6 +65,7 @@ def lib():
         L.orc_release_far.argtypes = [P, ctypes.POINTER(ctypes.c_longlong)]
         L.orc_jour.argtypes = [P]
         L.orc_jour.restype = ctypes.c_double
+        L.orc_roots.argtypes = [P, ctypes.POINTER(ctypes.c_longlong), dp, ip, ip, ip, ctypes.c_int]
         L.orc_shard.argtypes = [P, ctypes.c_int, ctypes.c_int, ALLREDUCE, P]
         L.orc_step_deskew.argtypes = [P, fp, fp, fp, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, ctypes.c_int,
                                       dp]
@@ -216,6 +217,20 @@ def ldlt_solve(A, b):
     return x
 
 
+def _roots_call(fn):
+    """fn(key, jour, flags, nodes, nfix, cap) -> root count (orc_roots / vgx_roots shape)."""
+    n = fn(None, None, None, None, None, 0)
+    n = max(int(n), 0)
+    key = np.zeros((max(n, 1), 3), dtype=np.int64)
+    jour = np.zeros(max(n, 1))
+    arr = [np.zeros(max(n, 1), dtype=np.int32) for _ in range(3)]
+    ip = ctypes.POINTER(ctypes.c_int)
+    m = fn(key.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), _d(jour), *[a.ctypes.data_as(ip) for a in arr], n)
+    assert m == n, (m, n)
+    return {tuple(int(v) for v in key[i]): (float(jour[i]), int(arr[0][i]), int(arr[1][i]), int(arr[2][i]))
+            for i in range(n)}
+
+
 class Pipeline:
     """The reference's per-scan steady-state loop (CPU restatement)."""
 
@@ -292,6 +307,10 @@ class Pipeline:
 
     def jour(self):
         return lib().orc_jour(self.h)
+
+    def roots(self):
+        """Every root voxel: {(x, y, z): (jour stamp, flags 1 in slide | 2 isexist, subtree nodes, point_fix)}."""
+        return _roots_call(lambda *a: lib().orc_roots(self.h, *a))
 
     def trajectory(self):
         """save_pose_tum rows (steady-state scans): t, R(9), p(3)."""

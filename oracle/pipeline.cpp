@@ -909,6 +909,32 @@ int orc_deskew_only(void* h, float* xyz, const float* times, int n, double beg, 
 }
 void orc_get_stats(void* h, orc_stats* s) { *s = ((Pipeline*)h)->st; }
 void orc_release_far(void* h, long long* out) { ((Pipeline*)h)->release_far(out); }
+// test hook: every root voxel of surf_map (any order) — key x/y/z, its jour
+// stamp, flags (1: in surf_map_slide, 2: isexist), subtree nodes and
+// point_fix points; returns the root count (rows past cap are not written)
+int orc_roots(void* h, long long* key, double* jour, int* flags, int* nodes, int* nfix, int cap) {
+  Pipeline* P = (Pipeline*)h;
+  int n = 0;
+  for (auto& kv : P->surf_map) {
+    if (n < cap) {
+      std::vector<OctoTree*> v;
+      kv.second->tras_ptr(v);
+      v.push_back(kv.second);
+      long long f = 0;
+      for (OctoTree* o : v) f += (long long)o->point_fix.size();
+      key[3 * n] = kv.first.x;
+      key[3 * n + 1] = kv.first.y;
+      key[3 * n + 2] = kv.first.z;
+      jour[n] = kv.second->jour;
+      flags[n] = (P->surf_map_slide.find(kv.first) != P->surf_map_slide.end() ? 1 : 0) |
+                 (kv.second->isexist ? 2 : 0);
+      nodes[n] = (int)v.size();
+      nfix[n] = (int)f;
+    }
+    n++;
+  }
+  return n;
+}
 double orc_jour(void* h) { return ((Pipeline*)h)->jour; }
 // one lio_state_estimation_kdtree call on the scan downsampled at
 // max(down_size, 0.5) (raw LiDAR frame; var_init applies the extrinsic),

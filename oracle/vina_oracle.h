@@ -72,6 +72,9 @@ void orc_get_stats(void* h, orc_stats* s);
  * [2] roots, [3] nodes, [4] point_fix points after it. orc_jour: jour. */
 void orc_release_far(void* h, long long* out);
 double orc_jour(void* h);
+/* test hook: every root voxel (key x/y/z, jour stamp, flags 1: in the slide map |
+ * 2: isexist, subtree nodes, point_fix points); returns the root count */
+int orc_roots(void* h, long long* key, double* jour, int* flags, int* nodes, int* nfix, int cap);
 /* orc_step with IMUEKF::motion_blur's per-point deskew first (imu_ekf.cpp:114-144);
  * times: per-point offset from beg in seconds (the reference's curvature), ascending. */
 int orc_step_deskew(void* h, const float* xyz, const float* inten, const float* times, int n, double beg, double end,

@@ -30,11 +30,18 @@ def _ctx(p, seq):
     return c
 
 
-@pytest.mark.parametrize("lidar,B,cap", [("16line", 3, 0), ("64line", 2, 0), ("16line", 8, 0), ("16line", 8, 4)])
-def test_multi_sequences_match_lone_runs(lidar, B, cap):
+@pytest.mark.parametrize("lidar,B,cap,serial", [("16line", 3, 0, 0), ("64line", 2, 0, 0), ("16line", 8, 0, 0),
+                                                ("16line", 8, 4, 0), ("16line", 16, 0, 1)])
+def test_multi_sequences_match_lone_runs(lidar, B, cap, serial, monkeypatch):
     """B = 8 with cap 4 is the bench's form past four sequences (slots shared
-    by two sequences each, vg_multi_set_active)."""
+    by two sequences each, vg_multi_set_active). B = 16 with
+    VG_SERIAL_KERNELS=1: sixteen worker threads in the library's event-wait
+    mode, the mode of round 5's B = 16 crash under the profiler (sixteen
+    threads capturing and instantiating graphs at once; vg::capture_mutex
+    serialises that now)."""
     import torch
+    if serial:
+        monkeypatch.setenv("VG_SERIAL_KERNELS", "1")
     dev = torch.device("cuda", 0)
     p = vgconfig.load("mid360")
     g = p["General"]

@@ -1787,6 +1787,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   auto enqueue = [&](int k) { ba_iter_kernels(ctx, k, solve_ev, xerr); };
   const bool graph = ctx->use_graphs && ctx->ba_graph && !shard_on && !solve_ev && ctx->dbg_capture != 1;
   if (graph && !ctx->g_ba) {
+    std::lock_guard<std::recursive_mutex> cap_lk_(capture_mutex());  // (vg_internal.h)
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     enqueue(0);
     hipGraph_t g = nullptr;
@@ -1799,6 +1800,7 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   // between them: each boundary left the stream idle ~9 us)
   const bool graph2 = pre == 0 && graph && ctx->ba_graph2 && ctx->ba_last_iters >= 2;
   if (graph2 && !ctx->g_ba2) {
+    std::lock_guard<std::recursive_mutex> cap_lk_(capture_mutex());  // (vg_internal.h)
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     const bool rh = ba_rh_on(ctx);
     ba_iter_kernels(ctx, 0, solve_ev, xerr, rh ? 1 : 0);

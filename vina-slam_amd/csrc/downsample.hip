@@ -848,6 +848,7 @@ int ds_enqueue_hashed(vg_ctx* ctx, hipStream_t s, const float* x, const float* y
     };
     const bool use_graph = ctx->use_graphs && fallback && voxel == ctx->cfg.down_size;
     if (use_graph && !ctx->g_ds) {
+      std::lock_guard<std::recursive_mutex> cap_lk_(capture_mutex());  // (vg_internal.h)
       VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
       chain(s);
       hipGraph_t gr = nullptr;

@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(256) k_rel_live(DevMap m, int n, const int* __
                                                   int* __restrict__ fblk, unsigned long long* __restrict__ cnt) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int r = i;
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < 8; k++) {  // depth <= max_layer + 1 <= 4 (vg_create rejects max_layer > 3)
       const int p = m.hdr[r].parent;
       if (p < 0) break;
       r = p;
@@ -67,31 +67,58 @@ __global__ void __launch_bounds__(256) k_rel_live(DevMap m, int n, const int* __
   }
 }
 
-// the kept roots' (key, new id) pairs, then the table is cleared and refilled
+// The root hash rebuilt from the kept roots with a layout that is a function
+// of the kept (key, new id) set alone, not of scheduling: each kept root's key
+// is filed under its new id (ids are unique, no atomics), the table is
+// cleared, then linear probing runs in rounds — every unplaced root bids for
+// its current probe slot with atomicMin of its id (in hfirst, which must end
+// cleared anyway), the lowest id takes the slot, the others move one slot on.
+// A winner never moves again, so every slot between a root's home and its
+// final slot is occupied: hash_find's probe sequence stays valid.
 __global__ void __launch_bounds__(256) k_rel_hash_collect(DevMap m, int n, const int* __restrict__ live,
-                                                          const int* __restrict__ nid, uint64_t* __restrict__ keys,
-                                                          int* __restrict__ ids, unsigned long long* __restrict__ cnt) {
+                                                          const int* __restrict__ nid, uint64_t* __restrict__ rkey,
+                                                          int* __restrict__ pos) {
   const int hs = m.hash_mask + 1;
   for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < hs; s += gridDim.x * blockDim.x) {
     const uint64_t key = m.hkey[s];
     if (key == kKeyEmpty) continue;
     const int r = m.hval[s];
     if (r < 0 || r >= n || !live[r]) continue;
-    const int q = (int)atomicAdd(&cnt[kRelKeys], 1ull);
-    keys[q] = key;
-    ids[q] = nid[r];
+    const int q = nid[r];
+    rkey[q] = key;
+    pos[q] = (int)hash_slot(key, m.hash_mask);  // its home slot; -1 (memset) for every other id
   }
 }
-__global__ void __launch_bounds__(256) k_rel_hash_fill(DevMap m, int nk, const uint64_t* __restrict__ keys,
-                                                       const int* __restrict__ ids, int* __restrict__ err) {
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nk; q += gridDim.x * blockDim.x) {
-    bool fresh = false;
-    const int s = hash_insert(m.hkey, m.hash_mask, keys[q], fresh);
-    if (s < 0 || !fresh) {
-      atomicOr(err, 1);
+// one probing round: bids (phase 0), then the outcome (phase 1); cnt: roots
+// still unplaced after the round (each counted once: moved on in phase 0 or
+// outbid in phase 1)
+constexpr int kBid = 1 << 30;  // pos[q] flag: q bid for that slot in this round's phase 0
+__global__ void __launch_bounds__(256) k_rel_hash_round(DevMap m, int nl, const uint64_t* __restrict__ rkey,
+                                                        int* __restrict__ pos, int phase, int* __restrict__ cnt) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nl; q += gridDim.x * blockDim.x) {
+    int p = pos[q];
+    if (p < 0) continue;  // not a kept root, or placed
+    if (phase == 0) {
+      if (m.hkey[p] != kKeyEmpty) {  // a winner of an earlier round: probe on (bid next round)
+        pos[q] = (p + 1) & m.hash_mask;
+        atomicAdd(cnt, 1);
+      } else {
+        atomicMin(&m.hfirst[p], q);
+        pos[q] = p | kBid;
+      }
       continue;
     }
-    m.hval[s] = ids[q];
+    if (!(p & kBid)) continue;
+    p &= ~kBid;
+    if (m.hfirst[p] == q) {  // won: the lowest id bidding for the slot
+      m.hkey[p] = rkey[q];
+      m.hval[p] = q;
+      pos[q] = -1;
+      m.hfirst[p] = 0x7f7f7f7f;  // an outbid lane reading it after this still sees != its id
+    } else {
+      pos[q] = (p + 1) & m.hash_mask;
+      atomicAdd(cnt, 1);
+    }
   }
 }
 
@@ -156,6 +183,40 @@ __global__ void k_rel_counts(DevMap m, int n_live, int fix_used) {
   }
 }
 
+// test hook (vgx_roots): per node, its subtree's root gets the node and its point_fix points
+__global__ void __launch_bounds__(256) k_roots_count(DevMap m, int n, int* __restrict__ nodes, int* __restrict__ nfix) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    int r = i;
+    for (int k = 0; k < 16 && m.hdr[r].parent >= 0; k++) r = m.hdr[r].parent;
+    if (m.hdr[r].parent >= 0) continue;
+    atomicAdd(&nodes[r], 1);
+    const int f = m.hdr[i].fix_cnt;
+    if (f > 0) atomicAdd(&nfix[r], f);
+  }
+}
+// one row per hashed root: key x/y/z, jour stamp, flags (1 in the slide map, 2 isexist), subtree counts
+__global__ void __launch_bounds__(256) k_roots_rows(DevMap m, int n, const int* __restrict__ nodes,
+                                                    const int* __restrict__ nfix, int* __restrict__ cnt,
+                                                    long long* __restrict__ key, double* __restrict__ jour,
+                                                    int* __restrict__ flags, int* __restrict__ onodes,
+                                                    int* __restrict__ ofix) {
+  const int hs = m.hash_mask + 1;
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < hs; s += gridDim.x * blockDim.x) {
+    const uint64_t k = m.hkey[s];
+    if (k == kKeyEmpty) continue;
+    const int r = m.hval[s];
+    if (r < 0 || r >= n) continue;
+    const int q = atomicAdd(cnt, 1);
+    key[3 * q] = unpack_axis(k, 42);
+    key[3 * q + 1] = unpack_axis(k, 21);
+    key[3 * q + 2] = unpack_axis(k, 0);
+    jour[q] = m.jour[r];
+    flags[q] = (m.in_slide[r] ? 1 : 0) | (m.hdr[r].isexist ? 2 : 0);
+    onodes[q] = nodes[r];
+    ofix[q] = nfix[r];
+  }
+}
+
 template <class F>
 int with_scratch(vg_ctx* ctx, size_t bytes, void** p, F&& body) {
   const hipError_t e = hipMalloc(p, bytes > 0 ? bytes : 64);
@@ -178,6 +239,11 @@ int with_scratch(vg_ctx* ctx, size_t bytes, void** p, F&& body) {
 int map_release(vg_ctx* ctx, bool release, int thr, double jour, int compact, long long* out) {
   DevMap& m = ctx->map;
   hipStream_t s = ctx->stream;
+  // every stream of the context is idle before the map is rewritten in place
+  // (host_sync drains the main stream, which waits for the others' work of
+  // the pipeline; the downsample and IEKF streams are drained here as well)
+  VG_HIP(hipStreamSynchronize(ctx->stream_ds));
+  if (ctx->stream_iekf) VG_HIP(hipStreamSynchronize(ctx->stream_iekf));
   int hc[kCntN];
   VG_HIP(hipMemcpyAsync(hc, m.counters, sizeof(hc), hipMemcpyDeviceToHost, s));
   VG_HIP(hipStreamSynchronize(s));
@@ -230,23 +296,40 @@ int map_release(vg_ctx* ctx, bool release, int thr, double jour, int compact, lo
     const size_t rec_max = std::max({sizeof(NodeHdr), sizeof(PlaneRec), (size_t)kCovN * 8, (size_t)W * sizeof(Clu),
                                      (size_t)W * sizeof(uint64_t)});
     const size_t gbytes = std::max({(size_t)n_live * rec_max, (size_t)fix_new * 9 * sizeof(double),
-                                    (size_t)(hcnt[kRelRootsLive] + 1) * 16});
+                                    (size_t)n_live * 12 + 64});
     void* gp = nullptr;
     return with_scratch(ctx, gbytes, &gp, [&]() -> int {
-      // the root hash, rebuilt from the kept roots under their new ids
-      auto* keys = (uint64_t*)gp;
-      int* ids = (int*)(keys + hcnt[kRelRootsLive] + 1);
+      // the root hash, rebuilt from the kept roots under their new ids, its
+      // layout a function of the kept set (k_rel_hash_collect)
+      auto* rkey = (uint64_t*)gp;
+      int* pos = (int*)(rkey + n_live);
       const int gh = grid_for((long)m.hash_mask + 1);
-      VG_HIP(hipMemsetAsync(&cnt[kRelKeys], 0, sizeof(unsigned long long), s));
-      k_rel_hash_collect<<<gh, kBlock, 0, s>>>(m, n, live, nid, keys, ids, cnt);
+      VG_HIP(hipMemsetAsync(pos, 0xff, (size_t)n_live * sizeof(int), s));
+      k_rel_hash_collect<<<gh, kBlock, 0, s>>>(m, n, live, nid, rkey, pos);
       const size_t hs = (size_t)m.hash_mask + 1;
       VG_HIP(hipMemsetAsync(m.hkey, 0xff, hs * sizeof(uint64_t), s));
       VG_HIP(hipMemsetAsync(m.hval, 0xff, hs * sizeof(int), s));
       VG_HIP(hipMemsetAsync(m.hfirst, 0x7f, hs * sizeof(int), s));
-      int* herr = (int*)&cnt[kRelN - 1];
-      VG_HIP(hipMemsetAsync(herr, 0, sizeof(int), s));
-      const int nk = (int)hcnt[kRelRootsLive];
-      if (nk > 0) k_rel_hash_fill<<<grid_for(nk), kBlock, 0, s>>>(m, nk, keys, ids, herr);
+      int* rcnt = (int*)(cnt + 16);  // the rounds' unplaced counts (in the scratch's 256-byte counter block)
+      int herr_h = hcnt[kRelRootsLive] > (unsigned long long)m.hash_mask ? 1 : 0;
+      constexpr int kRounds = 8;
+      for (long done = 0; !herr_h && n_live > 0;) {
+        VG_HIP(hipMemsetAsync(rcnt, 0, kRounds * sizeof(int), s));
+        for (int t = 0; t < kRounds; t++) {
+          k_rel_hash_round<<<grid_for(n_live), kBlock, 0, s>>>(m, n_live, rkey, pos, 0, rcnt + t);
+          k_rel_hash_round<<<grid_for(n_live), kBlock, 0, s>>>(m, n_live, rkey, pos, 1, rcnt + t);
+        }
+        int left = 0;
+        VG_HIP(hipMemcpyAsync(&left, rcnt + kRounds - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+        VG_HIP(hipStreamSynchronize(s));
+        if (left == 0) break;
+        done += kRounds;
+        if (done > (long)m.hash_mask + 1) herr_h = 1;  // (never: each round places the lowest bidder)
+      }
+      if (herr_h) {
+        ctx->err = "vg_release_far: root hash rebuild failed";
+        return VG_E_STATE;
+      }
       // the point_fix arena: the kept blocks packed in node order (read with
       // the old records' offsets, so before the records are rewritten)
       const int gn = grid_for((long)n * 64);
@@ -286,13 +369,6 @@ int map_release(vg_ctx* ctx, bool release, int thr, double jour, int compact, lo
       if (n > n_live) VG_HIP(hipMemsetAsync(m.in_slide + n_live, 0, (size_t)(n - n_live), s));
       VG_HIP(hipMemsetAsync(ctx->wk.cand_bits, 0, (ctx->cap.max_nodes / 32 + 1) * sizeof(uint32_t), s));
       k_rel_counts<<<1, 64, 0, s>>>(m, n_live, fix_new);
-      int herr_h = 0;
-      VG_HIP(hipMemcpyAsync(&herr_h, herr, sizeof(int), hipMemcpyDeviceToHost, s));
-      VG_HIP(hipStreamSynchronize(s));
-      if (herr_h) {
-        ctx->err = "vg_release_far: root hash rebuild failed";
-        return VG_E_STATE;
-      }
       VG_HIP(hipGetLastError());
       return VG_OK;
     });
@@ -305,6 +381,49 @@ int map_release(vg_ctx* ctx, bool release, int thr, double jour, int compact, lo
   out[3] = n_live;
   out[4] = (long long)hcnt[kRelFixHeld];
   out[5] = did ? fix_new : nfix_used;
+  return VG_OK;
+}
+
+// test hook (vgx_roots): every hashed root's key, jour stamp, flags and
+// subtree counts, in hash-slot order; *count = the roots (rows past cap unwritten)
+int map_roots(vg_ctx* ctx, long long* key, double* jour, int* flags, int* nodes, int* nfix, int cap, int* count) {
+  DevMap& m = ctx->map;
+  hipStream_t s = ctx->stream;
+  int hc[kCntN];
+  VG_HIP(hipMemcpyAsync(hc, m.counters, sizeof(hc), hipMemcpyDeviceToHost, s));
+  VG_HIP(hipStreamSynchronize(s));
+  const int n = hc[kCntNodes] < m.cap_nodes ? hc[kCntNodes] : m.cap_nodes;
+  const size_t un = (size_t)(n > 0 ? n : 1);
+  // scratch: the row count, per node (subtree nodes, point_fix), then the rows
+  const size_t o_cnt = 0, o_nodes = 256, o_fix = o_nodes + un * 4, o_key = ((o_fix + un * 4 + 255) / 256) * 256,
+               o_jour = o_key + un * 24, o_flags = o_jour + un * 8, o_on = o_flags + un * 4, o_of = o_on + un * 4,
+               total = o_of + un * 4;
+  void* sp = nullptr;
+  int nr = 0;
+  const int r = with_scratch(ctx, total, &sp, [&]() -> int {
+    char* b = (char*)sp;
+    VG_HIP(hipMemsetAsync(b, 0, o_key, s));
+    if (n > 0) {
+      k_roots_count<<<grid_for(n), kBlock, 0, s>>>(m, n, (int*)(b + o_nodes), (int*)(b + o_fix));
+      k_roots_rows<<<grid_for((long)m.hash_mask + 1), kBlock, 0, s>>>(
+          m, n, (int*)(b + o_nodes), (int*)(b + o_fix), (int*)(b + o_cnt), (long long*)(b + o_key),
+          (double*)(b + o_jour), (int*)(b + o_flags), (int*)(b + o_on), (int*)(b + o_of));
+    }
+    VG_HIP(hipGetLastError());
+    VG_HIP(hipMemcpyAsync(&nr, b + o_cnt, sizeof(int), hipMemcpyDeviceToHost, s));
+    VG_HIP(hipStreamSynchronize(s));
+    const int k = nr < cap ? nr : cap;
+    if (k > 0 && key) {
+      VG_HIP(hipMemcpyAsync(key, b + o_key, (size_t)k * 24, hipMemcpyDeviceToHost, s));
+      VG_HIP(hipMemcpyAsync(jour, b + o_jour, (size_t)k * 8, hipMemcpyDeviceToHost, s));
+      VG_HIP(hipMemcpyAsync(flags, b + o_flags, (size_t)k * 4, hipMemcpyDeviceToHost, s));
+      VG_HIP(hipMemcpyAsync(nodes, b + o_on, (size_t)k * 4, hipMemcpyDeviceToHost, s));
+      VG_HIP(hipMemcpyAsync(nfix, b + o_of, (size_t)k * 4, hipMemcpyDeviceToHost, s));
+    }
+    return VG_OK;
+  });
+  if (r != VG_OK) return r;
+  *count = nr;
   return VG_OK;
 }
 

@@ -565,6 +565,7 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
   }
   hipGraphExec_t& ge = ctx->g_iekf[self_signal ? 3 : 0];
   if (!ge) {
+    std::lock_guard<std::recursive_mutex> cap_lk_(capture_mutex());  // (vg_internal.h)
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     const int r = enqueue();
     hipGraph_t g = nullptr;
@@ -3544,6 +3545,7 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   if (!ctx->use_graphs || ctx->prof_stages) return body();
   hipGraphExec_t& ge = ctx->g_margi[(gate ? 1 : 0) + (copy_signals ? 2 : 0)];
   if (!ge) {
+    std::lock_guard<std::recursive_mutex> cap_lk_(capture_mutex());  // (vg_internal.h)
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     const int r = body();
     hipGraph_t g = nullptr;

@@ -805,6 +805,7 @@ static int stage_insert_recut(vg_ctx* ctx) {
     WinArg wa = make_winarg(P, 0);
     for (int i = 0; i < W; i++) wa.nper[i] = cap;  // grid bounds only: the kernels read the device counts
     hipStream_t s = ctx->stream;
+    std::lock_guard<std::recursive_mutex> cap_lk_(capture_mutex());  // (vg_internal.h)
     VG_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     ctx->capturing = true;
     ctx->in_ph = sg;
@@ -1093,9 +1094,10 @@ int host_release_far(vg_ctx* ctx, int flags, long long* out) {
     return VG_E_STATE;
   }
   const bool release = P->release_flag;
-  P->release_flag = false;
   const int thr = ctx->cfg.release_dis > 0 ? ctx->cfg.release_dis : 700;
-  return map_release(ctx, release, thr, P->jour, flags & 1, out);
+  const int r = map_release(ctx, release, thr, P->jour, flags & 1, out);
+  if (r == VG_OK) P->release_flag = false;  // a failed release (e.g. its scratch allocation) stays pending
+  return r;
 }
 int host_memo_probe(vg_ctx* ctx, int* out) { return map_memo_probe(ctx, hp(ctx)->mpd, out); }
 

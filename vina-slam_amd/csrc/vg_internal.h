@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <functional>
+#include <mutex>
 #include <cstdint>
 #include <string>
 #include <thread>
@@ -806,10 +807,15 @@ inline bool sharded(const vg_ctx* c) { return c->shard.mode != 0; }
 // (GPU_MAX_HW_QUEUES, 4 by default) with another's, and a polling hand-off
 // kernel could wait on a producer queued behind it: the flag hand-offs are off
 int dev_ctx_count(int device);
+// Graph capture and instantiation are serialised across the process's
+// contexts (one-time work per context): the multi-sequence mode's worker
+// threads otherwise capture concurrently (B = 16: sixteen threads at once).
+std::recursive_mutex& capture_mutex();
 int host_release_far(vg_ctx* ctx, int flags, long long* out);
 bool host_release_pending(vg_ctx* ctx);  // jour advanced in an absorbed scan since the last release
 // lifetime.hip: the journey release + the node pool / point_fix arena compaction
 int map_release(vg_ctx* ctx, bool release, int thr, double jour, int compact, long long* out);
+int map_roots(vg_ctx* ctx, long long* key, double* jour, int* flags, int* nodes, int* nfix, int cap, int* count);
 int host_lio_kdtree(vg_ctx* ctx, const float* xyz, int n, double* state, int* valid, int* iters);
 int decode_scan(vg_ctx* ctx, const void* records, int n, const vg_lidar_format* fmt, float* xyz, float* inten,
                 float* time, int* n_out);  // decode.hip

@@ -2,7 +2,10 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <csignal>
 #include <cstdio>
+#include <execinfo.h>
+#include <unistd.h>
 #include <cstdlib>
 #include <mutex>
 #include <cstring>
@@ -105,7 +108,34 @@ static void pinned_copy(vg_ctx* ctx, const std::vector<CopyPool::Job>& pieces) {
 static std::atomic<int> g_dev_ctx[64];
 namespace vg {
 int dev_ctx_count(int device) { return (device >= 0 && device < 64) ? g_dev_ctx[device].load() : 1; }
+std::recursive_mutex& capture_mutex() {
+  static std::recursive_mutex mu;
+  return mu;
+}
 }  // namespace vg
+
+// VG_SEGV_TRACE=1: a fatal signal prints the native stack (the frames of this
+// library and of the HIP runtime) to stderr before the default action, so a
+// crash inside a worker thread of the multi-sequence mode names its call site.
+static void segv_trace(int sig) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  const char msg[] = "vina_gpu: fatal signal, native stack:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+static void segv_trace_install() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char* e = getenv("VG_SEGV_TRACE");
+    if (!e || atoi(e) == 0) return;
+    signal(SIGSEGV, segv_trace);
+    signal(SIGBUS, segv_trace);
+    signal(SIGABRT, segv_trace);
+  });
+}
 
 static void fill_capacity(vg_capacity& c) {
   if (c.max_points_per_scan <= 0) c.max_points_per_scan = 2000000;
@@ -119,6 +149,7 @@ extern "C" {
 int vg_create(const vg_config* cfg, const vg_capacity* cap, int device, vg_ctx** out) {
   if (!cfg || !out) return VG_E_ARG;
   *out = nullptr;
+  segv_trace_install();
   vg_ctx* ctx = new (std::nothrow) vg_ctx();
   if (!ctx) return VG_E_CAPACITY;
   ctx->cfg = *cfg;
@@ -998,6 +1029,17 @@ extern "C" int vgx_memo_probe(vg_ctx* ctx, int* out) {
   if (!ctx || !out) return VG_E_ARG;
   VG_TRY(host_sync(ctx));
   return host_memo_probe(ctx, out);
+}
+
+// Test-only: every root voxel of the device map (lifetime.hip map_roots) —
+// key x/y/z, jour stamp, flags (1: in the slide map, 2: isexist), subtree
+// nodes and point_fix points — for a per-root comparison with the oracle's
+// surf_map (orc_roots). *n = the root count; rows past cap are not written.
+extern "C" int vgx_roots(vg_ctx* ctx, long long* key, double* jour, int* flags, int* nodes, int* nfix, int cap,
+                         int* n) {
+  if (!ctx || !n || cap < 0 || (cap > 0 && (!key || !jour || !flags || !nodes || !nfix))) return VG_E_ARG;
+  VG_TRY(host_sync(ctx));
+  return map_roots(ctx, key, jour, flags, nodes, nfix, cap, n);
 }
 
 // Test-only: the per-scan pipeline's hashed downsample (ds_enqueue_hashed,

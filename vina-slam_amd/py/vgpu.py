@@ -172,6 +172,8 @@ def lib():
             L.vgx_ba_solve.argtypes = [P, dp, dp, dp]
         if hasattr(L, "vgx_memo_probe"):
             L.vgx_memo_probe.argtypes = [P, ip]
+        if hasattr(L, "vgx_roots"):
+            L.vgx_roots.argtypes = [P, ctypes.POINTER(ctypes.c_longlong), dp, ip, ip, ip, ctypes.c_int, ip]
         _lib = L
     return _lib
 
@@ -483,6 +485,24 @@ class Context:
         out = np.zeros(4, np.int32)
         self._chk(lib().vgx_memo_probe(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int))), "vgx_memo_probe")
         return [int(v) for v in out]
+
+    def roots(self):
+        """Every root voxel of the device map (vgx_roots): {(x, y, z): (jour stamp,
+        flags 1 in slide | 2 isexist, subtree nodes, point_fix points)} — the
+        shape of the oracle's Pipeline.roots()."""
+        def call(key, jour, flags, nodes, nfix, cap):
+            n = ctypes.c_int(0)
+            self._chk(lib().vgx_roots(self.h, key, jour, flags, nodes, nfix, cap, ctypes.byref(n)), "vgx_roots")
+            return n.value
+        n = call(None, None, None, None, None, 0)
+        key = np.zeros((max(n, 1), 3), dtype=np.int64)
+        jour = np.zeros(max(n, 1))
+        arr = [np.zeros(max(n, 1), dtype=np.int32) for _ in range(3)]
+        ip = ctypes.POINTER(ctypes.c_int)
+        m = call(key.ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)), _d(jour), *[a.ctypes.data_as(ip) for a in arr], n)
+        assert m == n, (m, n)
+        return {tuple(int(v) for v in key[i]): (float(jour[i]), int(arr[0][i]), int(arr[1][i]), int(arr[2][i]))
+                for i in range(n)}
 
     def capture_arm(self):
         """Capture the next LM run's first Hessian pass (vgx_debug 5)."""
