@@ -114,6 +114,9 @@ typedef struct vg_stats {
    * failed (system_reset); motion_init rounds run on this scan; the kd-tree
    * LIO's valid correspondences (-1: the scan seeded the map) */
   int init_phase, init_rounds, init_valid;
+  /* points the IEKF point loop processed, summed over the executed iterations
+   * (sharded mode, world > 1: this rank's kept points, map.hip k_keep_*) */
+  int iekf_points;
 } vg_stats;
 
 typedef struct vg_ctx vg_ctx;

@@ -100,6 +100,21 @@ def test_two_shards_match_one(cfgname, lidar, nscan):
         assert a["ba_iters"] == b["ba_iters"] == c["ba_iters"], k
         # the match count is part of the all-reduced normal equations: global on every rank
         assert a["iekf_matches"] == b["iekf_matches"] == c["iekf_matches"], k
+    # per-rank work: each rank's IEKF transforms and matches only the points of
+    # its tiles plus a 0.1 m band, not the whole scan (map.hip k_keep_*). The
+    # synthetic box's floor lies on the z = 0 tile face, so its points (a third
+    # of the scan, +-2 cm of range noise) are near-boundary for both ranks:
+    # observed 0.82 + 0.55 (mid360, 8 m tiles) and 0.64 + 0.57 (1 m voxels,
+    # 16 m tiles) of the unsharded count
+    for k, (a, b, c) in enumerate(zip(sa, sb, s1)):
+        print(k, "IEKF points per iteration / n_raw: %.3f %.3f (iterations %d)"
+              % (a["iekf_points"] / a["iekf_iters"] / c["n_raw"], b["iekf_points"] / b["iekf_iters"] / c["n_raw"],
+                 c["iekf_iters"]))
+    pa, pb, pc = (sum(s["iekf_points"] for s in x) for x in (sa, sb, s1))
+    print("IEKF points over %d scans: rank 0 %d (%.2f), rank 1 %d (%.2f), unsharded %d"
+          % (nscan, pa, pa / pc, pb, pb / pc, pc))
+    assert pc == sum(s["n_raw"] * s["iekf_iters"] for s in s1)
+    assert pa < 0.9 * pc and pb < 0.9 * pc and pa + pb < 1.45 * pc
     assert np.array_equal(ta, tb), "the ranks' trajectories must agree bit for bit"
     err = synth.ate(t1, ta)
     dpos = np.linalg.norm(t1[:, 10:13] - ta[:, 10:13], axis=1).max()

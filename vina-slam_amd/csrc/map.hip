@@ -278,13 +278,15 @@ __device__ __forceinline__ void iekf_points(const MP& mp, const DState* __restri
                                             int* __restrict__ cache, int* __restrict__ pk, int it, int nb, int vb,
                                             const M3& R, const V3& p, const M3& rot_var, const M3& tsl_var,
                                             double (&acc)[kIekfVals]) {
-  const int n = st->sn;
+  const int* __restrict__ keep = iekf_keep(st);
+  const int n = keep ? st->snk : st->sn;
   const float* __restrict__ x = st->sx;
   const float* __restrict__ y = st->sy;
   const float* __restrict__ z = st->sz;
   const M3 Rt = tr(R);
   for (int j = 0; j < kIekfVals; j++) acc[j] = 0.0;
-  for (int i = vb * blockDim.x + threadIdx.x; i < n; i += nb * blockDim.x) {
+  for (int q = vb * blockDim.x + threadIdx.x; q < n; q += nb * blockDim.x) {
+    const int i = keep ? keep[q] : q;  // the raw index (the memo and the profiling pass are per raw point)
     V3 pnt;
     M3 var;
     var_init_pt(mp, x[i], y[i], z[i], pnt, var);
@@ -427,6 +429,7 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
   const int vb = iekf_chunk(blockIdx.x, nb);
   double acc[kIekfVals];
   iekf_points<kPf>(mp, st, m, cache, pk, it, nb, vb, R, p, rot_var, tsl_var, acc);
+  if (blockIdx.x == 0 && threadIdx.x == 0) st->iekf_pts += iekf_n(st);  // (vg_stats::iekf_points)
   if (blockIdx.x == 0) VG_PROBE_MARK(30);  // the point loop (thread 0 of block 0)
   __shared__ double red[4][kIekfVals];
   const double v = iekf_wg_sum(acc, red);
@@ -456,10 +459,11 @@ __device__ __forceinline__ void iekf_signal_done(unsigned* flag) {
 __global__ void __launch_bounds__(256) k_iekf_planes(const DState* __restrict__ st, DevMap m,
                                                      const int* __restrict__ pk, int tag, int* __restrict__ out) {
   if (st->done) return;
-  const int n = st->sn;
+  const int* keep = iekf_keep(st);
+  const int n = iekf_n(st);
   int cnt = 0;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const int leaf = pk[i];
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    const int leaf = pk[keep ? keep[q] : q];
     if (leaf >= 0 && m.stamp[leaf] != tag && atomicExch(&m.stamp[leaf], tag) != tag) cnt++;
   }
   wave_append(out, cnt);
@@ -490,7 +494,7 @@ __global__ void __launch_bounds__(1024) k_iekf_reduce(int nb, const double* __re
   __shared__ IekfLds L;
   const bool done = st->done;
   if (!done) {
-    const int n = st->sn;
+    const int n = iekf_n(st);
     iekf_reduce_block(nb, partials, L, n < nb * 256 ? (n + 255) / 256 : nb);
   }
   for (int i = threadIdx.x; i < xa.n - 2; i += blockDim.x) xa.frame[i] = (!done && i < kIekfVals) ? L.o[i] : 0.0;
@@ -533,6 +537,83 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
   return VG_OK;
 }
 
+// ---- sharded mode (world > 1): the scan's points this rank can match ----
+// A point is matched only in its own root voxel (A7, voxel_map.cpp:241-266),
+// and only the owner of the voxel's tile holds it. At the
+// scan's opening pose each raw point's world position w is taken with a box of
+// kKeepM metres around it; the key rule is monotone in each coordinate, so
+// the voxel keys of the box are those between the keys of w - kKeepM and
+// w + kKeepM, and the point is kept when a tile of those keys is this rank's:
+// one pass and a prefix sum per scan, and the IEKF's four iterations then
+// transform and test only those (DState::skeep). The list holds while every
+// point moved less than kmargin = kKeepM since the opening (iekf_keep, checked
+// per iteration on the device), else the iteration takes every point. owns()
+// still decides per point and iteration, so the matches are the unsharded
+// path's either way; only the order of the fp sums within a rank follows the
+// list.
+constexpr double kKeepM = 0.1;
+__global__ void __launch_bounds__(256) k_keep_flags(MP mp, const DState* __restrict__ st, DevMap m,
+                                                    int* __restrict__ flag, unsigned* __restrict__ rmax_bits) {
+  const int n = st->sn;
+  const float* __restrict__ x = st->sx;
+  const float* __restrict__ y = st->sy;
+  const float* __restrict__ z = st->sz;
+  M3 R;
+  for (int q = 0; q < 9; q++) R[q] = st->xc[q];
+  const V3 p = v3(st->xc[9], st->xc[10], st->xc[11]);
+  const M3 eR = ld_m3(mp.extR);
+  const V3 et = ld_v3(mp.extt);
+  float rmax = 0.0f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const V3 pnt = rigid(eR, v3(x[i], y[i], z[i]), et);
+    const V3 w = rigid(R, pnt, p);
+    rmax = fmaxf(rmax, (float)norm3(pnt));
+    int64_t lo[3], hi[3];
+    bool in = true;
+    for (int j = 0; j < 3; j++) {
+      const int64_t k0 = key_axis_d(w[j] - kKeepM, mp.vs) + kKeyOff, k1 = key_axis_d(w[j] + kKeepM, mp.vs) + kKeyOff;
+      lo[j] = (k0 > 0 ? k0 : 0) >> 4;  // (keys outside the packed range are never matched)
+      hi[j] = (k1 < 2 * kKeyOff - 1 ? k1 : 2 * kKeyOff - 1) >> 4;
+      in &= k1 >= 0 && k0 < 2 * kKeyOff;
+    }
+    int keep = 0;
+    if (in)
+      for (int64_t tx = lo[0]; tx <= hi[0] && !keep; tx++)
+        for (int64_t ty = lo[1]; ty <= hi[1] && !keep; ty++)
+          for (int64_t tz = lo[2]; tz <= hi[2] && !keep; tz++)
+            keep = tile_owner_t((uint64_t)tx, (uint64_t)ty, (uint64_t)tz, m.shard_world) == m.shard_rank;
+    flag[i] = keep;
+  }
+  for (int off = 32; off > 0; off >>= 1) rmax = fmaxf(rmax, __shfl_down(rmax, off, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(rmax_bits, __float_as_uint(rmax));  // (non-negative: ordered as bits)
+}
+__global__ void __launch_bounds__(256) k_keep_scatter(MP mp, DState* __restrict__ st, const int* __restrict__ flag,
+                                                      const int* __restrict__ pos, int* __restrict__ list,
+                                                      const unsigned* __restrict__ rmax_bits) {
+  const int n = st->sn;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    if (flag[i]) list[pos[i]] = i;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->snk = n > 0 ? pos[n - 1] + flag[n - 1] : 0;
+    st->skeep = list;
+    for (int t = 0; t < 12; t++) st->kpose[t] = st->xc[t];
+    st->krmax = (double)__uint_as_float(*rmax_bits) * (1.0 + 1e-6) + 1e-6;  // (the float max rounded up)
+    st->kmargin = kKeepM;
+  }
+}
+static int keep_list(vg_ctx* ctx, const MP& mp, int n, hipStream_t s) {
+  Shard& sh = ctx->shard;
+  if (n <= 0) n = 1;  // (an empty scan: the kernels read the count from the state)
+  VG_HIP(hipMemsetAsync(sh.keep_rmax, 0, sizeof(unsigned), s));
+  const int g = grid_for(n);
+  k_keep_flags<<<g, kBlock, 0, s>>>(mp, ctx->st, ctx->map, sh.keep_flag, sh.keep_rmax);
+  size_t tb = sh.keep_tmp_bytes;
+  VG_HIP(hipcub::DeviceScan::ExclusiveSum(sh.keep_tmp, tb, sh.keep_flag, sh.keep_pos, n, s));
+  k_keep_scatter<<<g, kBlock, 0, s>>>(mp, ctx->st, sh.keep_flag, sh.keep_pos, sh.keep_list, sh.keep_rmax);
+  VG_HIP(hipGetLastError());
+  return VG_OK;
+}
+
 // the four IEKF iterations (odometry.cpp:68). The launches do not change from
 // scan to scan, so an unsharded context captures them once and replays the
 // graph: one host call instead of eight launches, and the device starts each
@@ -546,6 +627,7 @@ int iekf_run(vg_ctx* ctx, const MP& mp, const float* x, const float* y, const fl
   if (begin_xc || begin_prop)  // the scan opens here (pipeline.cpp)
     VG_TRY(state_scan_begin(ctx, begin_xc, x, y, z, n, s, begin_prop));
   else if (!opened) VG_TRY(state_set_scan(ctx, x, y, z, n, s));
+  if (sharded(ctx) && ctx->shard.world > 1) VG_TRY(keep_list(ctx, mp, n, s));  // at the opening pose
   const bool graph = ctx->use_graphs && !sharded(ctx) && !ctx->prof_stages;
   const bool ev = ctx->prof_on && !graph;
   // the last update signals the hand-off itself (k_iekf_update; not when sharded)
@@ -2588,8 +2670,20 @@ __global__ void k_make_win_recut_begin(DState* __restrict__ st, WinArg wa, const
 // max_fac) makes the LM skip, and the host completes the recut and reruns it.
 __global__ void __launch_bounds__(1024) k_fac_sort(DevMap m, int* __restrict__ rc, uint32_t* __restrict__ bits,
                                                    int* __restrict__ fac_node, int cap_f, Pub* __restrict__ pub,
-                                                   int* __restrict__ seq_ctr, int max_fac) {
-  fac_sort_block(m, rc, bits, fac_node, cap_f, pub, seq_ctr, max_fac);
+                                                   int* __restrict__ seq_ctr, int max_fac, int publish) {
+  fac_sort_block(m, rc, bits, fac_node, cap_f, pub, seq_ctr, max_fac, publish != 0);
+}
+// sharded mode: the recut status all-reduced over the ranks (rc[kRcStatus]),
+// so every rank's k_ba_init skips alike and every host takes the same
+// host-sized completion and LM rerun — the ranks' exchange sequences stay in
+// step. The factor count published is this rank's own.
+__global__ void k_pub_rc(const DevMap m, const int* __restrict__ rc, Pub* __restrict__ pub,
+                         const int* __restrict__ seq_ctr) {
+  if (threadIdx.x == 0) {
+    pub_store(&pub->rc_status, rc[kRcStatus]);
+    pub_store(&pub->rc_nf, m.counters[kCntFactors]);
+    pub_flag(&pub->seq_rc, *seq_ctr);
+  }
 }
 __global__ void __launch_bounds__(256) k_factor_finish_dev(const int* __restrict__ rc, DevMap m,
                                                            const int* __restrict__ fac_node,
@@ -2783,8 +2877,13 @@ static int map_recut_impl(vg_ctx* ctx, const MP& mp, const WinArg& wa, int threa
   VG_HIP(hipGetLastError());
   if (pub_seq > 0) {
     const int max_fac = (ctx->dbg_fac_max >= 0 && ctx->dbg_fac_max < kFacMax) ? ctx->dbg_fac_max : kFacMax;
+    const bool shard_on = sharded(ctx);
     k_fac_sort<<<1, 1024, 0, s>>>(m, w.rc, w.cand_bits, ctx->ba.fac_node, ctx->ba.cap_f, ctx->d_pub,
-                                  &ctx->st->rc_ctr, max_fac);
+                                  &ctx->st->rc_ctr, max_fac, shard_on ? 0 : 1);
+    if (shard_on) {
+      VG_TRY(shard_allreduce(ctx, w.rc + kRcStatus, w.rc + kRcStatus, 1, 1, 5));
+      k_pub_rc<<<1, 64, 0, s>>>(m, w.rc, ctx->d_pub, &ctx->st->rc_ctr);
+    }
     if (ctx->rc_init_finish) {  // the LM's k_ba_init (next on the stream) does tras_opt's bookkeeping
       ctx->rc_finish_in_init = true;
     } else {

@@ -142,6 +142,7 @@ static int absorb_p1(vg_ctx* ctx, HostPipe* P, Pend& q) {
     P->path.push_back(P->jour);
     q.st.iekf_iters = pb.iekf_iters;
     for (int i = 0; i < 4; i++) q.st.iekf_matches[i] = pb.matches[i];
+    q.st.iekf_points = pb.iekf_pts;
     q.st.degenerate = degenerate_of(pb.nnt);
   }
   q.st.ba_iters = pb.ba_iters1;
@@ -869,9 +870,11 @@ int stage_recut(vg_ctx* ctx, int* nf_out) {
   int nf = 0;
   prof_begin(ctx, kProfRecut);
   P->rc_seq = 0;
-  if (!nf_out && P->win_count >= c.win_size && c.if_BA == 1 && !sharded(ctx)) {
+  if (!nf_out && P->win_count >= c.win_size && c.if_BA == 1) {
     // the LM follows: its kernels read the factor count on the device, and the
-    // host learns the recut's outcome only once the LM is enqueued (stage_ba)
+    // host learns the recut's outcome only once the LM is enqueued (stage_ba);
+    // sharded, the status is all-reduced first (map.hip k_pub_rc), so every
+    // rank takes the same host-sized completion and LM rerun
     P->rc_seq = ++ctx->rc_pub;  // the device counts its asynchronous recuts the same way (k_fac_sort)
     VG_TRY(map_recut(ctx, P->mpd, wa, c.thread_num, &nf, false, 1));
     prof_end(ctx, kProfRecut);

@@ -21,6 +21,7 @@
 // reaches the error (ranks drifting across classes would pair frames of
 // different sizes: the cost of not sending the 15 KB Hessian frame for every
 // 34-value IEKF exchange).
+#include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 #include <cstring>
 #include "vg_internal.h"
@@ -69,7 +70,17 @@ int shard_alloc(vg_ctx* ctx) {
   if (ctx->shard.frame_n < 64 + 2) ctx->shard.frame_n = 64 + 2;
   ctx->shard.d_frame = ctx->arena.take<double>((size_t)ctx->shard.frame_n + 2);
   ctx->shard.d_seq = ctx->arena.take<unsigned>(4);
-  if (!ctx->shard.d_buf || !ctx->shard.d_frame || !ctx->shard.d_seq) {
+  const size_t cap = (size_t)ctx->cap.max_points_per_scan;
+  Shard& sh = ctx->shard;
+  sh.keep_flag = ctx->arena.take<int>(cap);
+  sh.keep_pos = ctx->arena.take<int>(cap);
+  sh.keep_list = ctx->arena.take<int>(cap);
+  sh.keep_rmax = ctx->arena.take<unsigned>(4);
+  sh.keep_tmp_bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sh.keep_tmp_bytes, (int*)nullptr, (int*)nullptr, (int)cap);
+  sh.keep_tmp = ctx->arena.take<char>(sh.keep_tmp_bytes + 256);
+  if (!ctx->shard.d_buf || !ctx->shard.d_frame || !ctx->shard.d_seq || !sh.keep_flag || !sh.keep_pos ||
+      !sh.keep_list || !sh.keep_rmax || !sh.keep_tmp) {
     ctx->err = "arena exhausted (shard)";
     return VG_E_CAPACITY;
   }

@@ -57,6 +57,7 @@ __global__ void __launch_bounds__(256) k_scan_begin(XcArg xa, DState* __restrict
     st->ticket = 0;
     for (int k = 0; k < 4; k++) st->matches[k] = 0;
     for (int k = 0; k < 4; k++) st->planes[k] = 0;
+    st->iekf_pts = 0;
     if (st->clk.on) {  // this scan's k_iekf clock slots (KClock)
       const int sc = st->clk.scan + 1;
       st->clk.scan = sc;
@@ -351,6 +352,7 @@ __global__ void __launch_bounds__(kPropThreads) k_scan_prop(PropArg arg, DState*
     st->ticket = 0;
     for (int k = 0; k < 4; k++) st->matches[k] = 0;
     for (int k = 0; k < 4; k++) st->planes[k] = 0;
+    st->iekf_pts = 0;
     if (st->clk.on) {  // this scan's k_iekf clock slots (KClock)
       const int sc = st->clk.scan + 1;
       st->clk.scan = sc;

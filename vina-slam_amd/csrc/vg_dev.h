@@ -67,16 +67,41 @@ __device__ __forceinline__ int hash_insert(uint64_t* hkey, int mask, uint64_t ke
   return -1;
 }
 
-// owner rank of the 16^3-root-voxel tile holding a packed root key
-// (shard.cpp tile_owner_host is the same function)
-__host__ __device__ __forceinline__ int tile_owner(uint64_t key, int world) {
-  const uint64_t tx = (key >> 46) & 0x1ffff, ty = (key >> 25) & 0x1ffff, tz = (key >> 4) & 0x1ffff;
+// owner rank of a 16^3-root-voxel tile given by its coordinates (the offset
+// voxel key >> 4 per axis)
+__host__ __device__ __forceinline__ int tile_owner_t(uint64_t tx, uint64_t ty, uint64_t tz, int world) {
   uint64_t h = (tx * 0x9E3779B97F4A7C15ull) ^ (ty * 0xC2B2AE3D27D4EB4Full) ^ (tz * 0x165667B19E3779F9ull);
   h ^= h >> 31;
   h *= 0xBF58476D1CE4E5B9ull;
   h ^= h >> 29;
   return (int)(h % (uint64_t)world);
 }
+// of the tile holding a packed root key (oracle/map.hpp tile_owner is the same function)
+__host__ __device__ __forceinline__ int tile_owner(uint64_t key, int world) {
+  return tile_owner_t((key >> 46) & 0x1ffff, (key >> 25) & 0x1ffff, (key >> 4) & 0x1ffff, world);
+}
+// Sharded mode's keep list (DState::skeep, map.hip k_keep_*): usable while the
+// current pose x_curr moved every point by less than kmargin from the pose the
+// list was made at — |dR|_2 r_max + |dp| bounds |R q + p - (R0 q + p0)| for
+// |q| <= r_max, and for two rotations |R - R0|_2 = |R - R0|_F / sqrt(2) (the
+// singular values of R0 (Q - I) are 2 sin(a/2) twice and 0; 1.4 leaves room for
+// rounding). Every lane of every IEKF kernel evaluates it on the same state.
+__device__ __forceinline__ const int* iekf_keep(const DState* __restrict__ st) {
+  const int* k = st->skeep;
+  if (!k) return nullptr;
+  double dr = 0.0, dp = 0.0;
+  for (int t = 0; t < 9; t++) {
+    const double d = st->xc[t] - st->kpose[t];
+    dr += d * d;
+  }
+  for (int t = 9; t < 12; t++) {
+    const double d = st->xc[t] - st->kpose[t];
+    dp += d * d;
+  }
+  return sqrt(dr) * (1.0 / 1.4) * st->krmax + sqrt(dp) < st->kmargin ? k : nullptr;
+}
+// the points the IEKF point loop takes this iteration
+__device__ __forceinline__ int iekf_n(const DState* __restrict__ st) { return iekf_keep(st) ? st->snk : st->sn; }
 __device__ __forceinline__ bool owns(const DevMap& m, uint64_t key) {
   return m.shard_world <= 1 || tile_owner(key, m.shard_world) == m.shard_rank;
 }
@@ -421,10 +446,11 @@ __device__ __forceinline__ void publish_state_block(const DState* __restrict__ s
                                                     unsigned head_value = 0) {
   const int t = threadIdx.x;
   __shared__ double s_xc[kXC];
-  __shared__ int s_sum[9];
+  __shared__ int s_sum[10];
   for (int e = t; e < kXC; e += blockDim.x) s_xc[e] = st->xc[e];
   if (t == 0) {
     s_sum[0] = st->iters;
+    s_sum[9] = st->iekf_pts;
     for (int k = 0; k < 4; k++) {
       s_sum[1 + k] = st->matches[k];
       s_sum[5 + k] = st->planes[k];
@@ -447,6 +473,7 @@ __device__ __forceinline__ void publish_state_block(const DState* __restrict__ s
     pub_store(&pub->ba_iters1, ba_iters_valid ? *ba_iters : 0);
     pub_store(&pub->ba_hess1, ba_iters_valid ? *ba_hess : 0);
     for (int k = 0; k < 4; k++) pub_store(&pub->planes[k], s_sum[5 + k]);
+    pub_store(&pub->iekf_pts, s_sum[9]);
   }
   pub_drain();
   __syncthreads();
@@ -525,7 +552,7 @@ constexpr int kFacMax = 1 << 20;
 constexpr int kRcBig = 200;
 __device__ __forceinline__ void fac_sort_block(DevMap& m, int* __restrict__ rc, uint32_t* __restrict__ bits,
                                                int* __restrict__ fac_node, int cap_f, Pub* __restrict__ pub,
-                                               int* __restrict__ seq_ctr, int max_fac) {
+                                               int* __restrict__ seq_ctr, int max_fac, bool publish = true) {
   __shared__ int s_w[17];
   const int nf = m.counters[kCntFactors];
   int status = rc[kRcAbort];
@@ -553,9 +580,11 @@ __device__ __forceinline__ void fac_sort_block(DevMap& m, int* __restrict__ rc, 
     const int seq = *seq_ctr + 1;  // the device's count of asynchronous recuts (the host mirrors it)
     *seq_ctr = seq;
     rc[kRcStatus] = status;
-    pub_store(&pub->rc_status, status);
-    pub_store(&pub->rc_nf, nf);
-    pub_flag(&pub->seq_rc, seq);
+    if (publish) {
+      pub_store(&pub->rc_status, status);
+      pub_store(&pub->rc_nf, nf);
+      pub_flag(&pub->seq_rc, seq);
+    }
   }
 }
 

@@ -119,7 +119,7 @@ __device__ void iekf_update_block(int nb, const double* __restrict__ partials, D
   const bool vec_early = (int)blockDim.x > 17 * kIekfGroups;
   if (vec_early && tid == (int)blockDim.x - 1) iekf_vec(st, L);
   if (nb >= 0) {
-    const int n = st->sn;
+    const int n = iekf_n(st);
     iekf_reduce_block(nb, partials, L, n < nb * 256 ? (n + 255) / 256 : nb);
   } else {  // sharded mode: `partials` holds the all-reduced sums
     const bool ok = xworld <= 0 || xchg_ok(partials, kShardSmall, xworld);

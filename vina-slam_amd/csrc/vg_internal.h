@@ -295,6 +295,13 @@ struct DState {
   double jour, last_pos[3];
   double imurec[kMaxWin * kBaImuRec];
   KClock clk;
+  // sharded mode (world > 1): the scan's points this rank can match, made
+  // once per scan at the opening pose (map.hip k_keep_*): raw indices,
+  // ascending; null: every point. The IEKF uses the list while the pose
+  // stays within kmargin of kpose for every point (|dR|_F krmax + |dp|).
+  const int* skeep;
+  int snk, iekf_pts;  // kept points; points the point loop processed this scan (vg_stats::iekf_points)
+  double kpose[12], krmax, kmargin;
 };
 // x_buf.push_back(x_curr) + a new IMU_PRE record, as kernel arguments (k_push_state,
 // or folded into the insert's first launch, map_insert)
@@ -342,6 +349,12 @@ struct Shard {
   int frame_n = 0;           // doubles per exchange (shard.hip: payload + guard pair)
   double* d_frame = nullptr; // the exchange frame (+ this rank's guard value)
   unsigned* d_seq = nullptr; // the device's count of exchanges (the guard's sequence number)
+  // the scan's kept points (world > 1, map.hip k_keep_*): per raw point its
+  // flag and exclusive prefix, the kept list, max |pnt| (float bits), scan scratch
+  int *keep_flag = nullptr, *keep_pos = nullptr, *keep_list = nullptr;
+  unsigned* keep_rmax = nullptr;
+  void* keep_tmp = nullptr;
+  size_t keep_tmp_bytes = 0;
 };
 
 // Host-mapped publication block (written by the device with system-scope
@@ -350,7 +363,7 @@ struct Pub {
   int seq_ds, n_ds, ds_err, pad0;          // downsample (after k_ds_*)
   int seq_ba, ba_word, pad1, pad1b;  // LM iteration flags (k_ba_control): iterations * 2 + done, one word (no torn pair)
   int seq_rc, rc_status, rc_nf, pad5;      // asynchronous recut status (k_fac_sort)
-  int seq1, iekf_iters, degenerate, matches[4], ba_iters1, ba_hess1, planes[4], pad2[3];  // P1: state after IEKF/BA
+  int seq1, iekf_iters, degenerate, matches[4], ba_iters1, ba_hess1, planes[4], iekf_pts, pad2[2];  // P1: state after IEKF/BA
   int seq2, pad3[3];
   int counters[kCntN];                      // P2: map counters at the end of the scan
   double xc[256];

@@ -48,7 +48,7 @@ class Stats(ctypes.Structure):
                 ("nodes_used", ctypes.c_int), ("fix_used", ctypes.c_int), ("plane_updates", ctypes.c_int),
                 ("fix_full", ctypes.c_int), ("iekf_planes", ctypes.c_int * 4), ("v_ins", ctypes.c_int),
                 ("ba_hess", ctypes.c_int), ("init_phase", ctypes.c_int), ("init_rounds", ctypes.c_int),
-                ("init_valid", ctypes.c_int)]
+                ("init_valid", ctypes.c_int), ("iekf_points", ctypes.c_int)]
 
 
 def _stats_dict(s):
