@@ -2152,8 +2152,14 @@ __device__ __forceinline__ void rc_push_child(int child, int parent, int layer, 
   PUSH_MARK(42);
   for (int b0 = j0; b0 < j1; b0 += 64) {
     const int e = b0 + lane, bi = (b0 - j0) >> 6;
-    const uint64_t k = !short_ev ? (e < j1 ? keys[e] : 0ull)
-                                 : (bi == 0 ? kv[0] : bi == 1 ? kv[1] : bi == 2 ? kv[2] : kv[3]);
+    uint64_t k = 0ull;
+    if (!short_ev) {
+      k = e < j1 ? keys[e] : 0ull;
+    } else {
+#pragma unroll
+      for (int b = 0; b < kPushScan; b++)  // (a register select: kv stays in VGPRs)
+        if (bi == b) k = kv[b];
+    }
     const int phase = (int)((k >> 21) & 63), idx = (int)(k & ((1u << 21) - 1));
     const int slot_e = __shfl(my_slot, phase > 0 ? phase - 1 : 0, 64);  // win->mp[phase - 1]
     V3 pt;
