@@ -528,7 +528,7 @@ int iekf_iteration(vg_ctx* ctx, const MP& mp, const float* x, const float* y, co
     Shard& sh = ctx->shard;
     const XchgArg xa{sh.d_frame, sh.d_seq, ctx->map.counters + kCntErr, kShardSmall, sh.world};
     k_iekf_reduce<<<1, 1024, 0, s>>>(nb, w.partials, ctx->st, xa);  // (the unsharded update's 60 row groups)
-    VG_TRY(shard_exchange(ctx, kShardSmall));
+    VG_TRY(shard_exchange(ctx, kShardSmall, s));
     k_iekf_update<<<1, 1024, 0, s>>>(-1, sh.d_frame, ctx->st, it, nullptr, sh.world, ctx->map.counters + kCntErr);
   } else {
     k_iekf_update<<<1, 1024, 0, s>>>(nb, w.partials, ctx->st, it, done_flag, 0, nullptr);
@@ -1641,8 +1641,7 @@ int map_insert(vg_ctx* ctx, const MP& mp, int slot, int n, int epoch, int thread
     k_ins_roots_alloc<<<ntile, kBlock, 0, s>>>(n, nd, ntile, w.u0, w.v1, (const int*)w.ac_cnt, mp, m);
   }
   if (sharded(ctx)) {  // the thread_num quirk counts distinct roots over all shards
-    k_copy_int<<<1, 64, 0, s>>>(m.counters + kCntTouched, m.counters + kCntGTouched);
-    VG_TRY(shard_allreduce(ctx, m.counters + kCntGTouched, m.counters + kCntGTouched, 1, 1, 1));
+    VG_TRY(shard_allreduce(ctx, m.counters + kCntTouched, m.counters + kCntGTouched, 1, 1, 1));
   }
   k_ins_descend<<<g * (kBlock / kSpreadBlock), kSpreadBlock, 0, s>>>(n, nd, thread_num, w.pw, m, w.u0, w.leaf, w.list2);
   const int ins_cap = (ctx->dbg_ins_cap >= 0 && ctx->dbg_ins_cap < kInsAllocCap) ? ctx->dbg_ins_cap : kInsAllocCap;
@@ -3615,7 +3614,9 @@ int map_margi(vg_ctx* ctx, const MP& mp, const WinArg& wa, int n_oldest, int thr
   // the hand-off flags to the next scan's IEKF stream: the margi head's
   // x_curr (d_sync[2], the device propagation starts from it) and the leaves'
   // plane updates (d_sync[0], the IEKF reads them)
-  const bool flags = ctx->flag_sync && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages && !sharded(ctx);
+  // (sharded as well: the hand-offs are device-side only, and no exchange sits
+  // between a flag's producer and its consumer)
+  const bool flags = ctx->flag_sync && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages;
   k_margi_leaf<<<1 + 512 * kBlock / kSpreadBlock, kSpreadBlock, 0, s>>>(
       m.counters + kCntLeaves, w.list0, mp, wa2, ctx->st, dwin, dn, dn + 32, bi != nullptr, bi,
       bi ? ba_hess_dev(ctx) : nullptr, ctx->d_pub, pub_seq, m, ctx->ba.fac_eig, ctx->ba.fac_pcr, w.plan, gate,

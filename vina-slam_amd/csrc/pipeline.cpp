@@ -409,8 +409,9 @@ static int lio_state_estimation(vg_ctx* ctx, HostPipe* P, const float* x, const 
   // behind the previous margi's plane updates only (map_margi): its
   // remainder on the main stream runs under this IEKF, and the main stream
   // then waits for the IEKF. The opening (k_scan_begin) goes with it.
-  const bool split = ctx->tail_a_valid && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages &&
-                     !sharded(ctx);
+  // (sharded: the IEKF's exchanges go on the IEKF stream, shard_exchange; the
+  // hand-offs are events, sync_tail_armed being off)
+  const bool split = ctx->tail_a_valid && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages;
   ctx->tail_a_valid = false;
   const double* bxc = begin && !P->begin_prop ? P->begin_xc : nullptr;
   const PropArg* bprop = begin && P->begin_prop ? &P->prop : nullptr;
@@ -937,8 +938,9 @@ int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows) {
     return VG_OK;
   };
   // the margi tail behind the LM (see ba_run): fused step, plain graph path
-  const bool spec_ok = margi_follows && ctx->spec_tail && ctx->use_graphs && !ctx->prof_stages &&
-                       !sharded(ctx);
+  // (sharded: the gated tail holds no exchange, and the LM's iteration count —
+  // the only thing it depends on — is the same on every rank)
+  const bool spec_ok = margi_follows && ctx->spec_tail && ctx->use_graphs && !ctx->prof_stages;
   std::function<int(bool*)> spec = [&](bool* queued) -> int {
     if (rc_status || !P->prefix) return VG_OK;
     VG_TRY(margi_enqueue(ctx, P, ba_gate_dev(ctx), &P->tail_seq1, &P->tail_seq2));
@@ -951,7 +953,7 @@ int stage_ba(vg_ctx* ctx, int* iters_out, bool margi_follows) {
   // and IEKF first — all behind the margi on device flags — and reads it then
   // (resolve_lm). Needs the flag hand-offs and the IEKF stream.
   const bool defer = spec_ok && ctx->lm_defer && ctx->flag_sync && !ctx->serial_kernels && ctx->overlap_iekf &&
-                     ctx->want_ds_stream;
+                     ctx->want_ds_stream && !sharded(ctx);
   bool pending = false;
   VG_TRY(ba_run(ctx, P->n_factors, P->mp.data(), &iters, prefix,
                 spec_ok && !pre ? spec : std::function<int(bool*)>(), &tail_ok, defer ? &pending : nullptr, pre ? 2 : 0));
@@ -1030,8 +1032,7 @@ int stage_margi_slide(vg_ctx* ctx) {
   P->tail_queued = false;
   // the margi that stands (the speculative tail or the one just enqueued) stores seq1 into the
   // IEKF hand-off flag (map_margi), which the next scan's IEKF stream polls (lio_state_estimation)
-  ctx->sync_tail_armed = ctx->flag_sync && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages &&
-                         !sharded(ctx);
+  ctx->sync_tail_armed = ctx->flag_sync && ctx->overlap_iekf && ctx->use_graphs && !ctx->prof_stages;
   ctx->sync_tail_value = (unsigned)seq1;
   P->cur.seq1 = seq1;
   P->cur.seq2 = seq2;

@@ -147,19 +147,20 @@ int shard_allreduce(vg_ctx* ctx, const void* send, void* recv, int count, int dt
 // the all-reduce of a frame its producer kernel packed (xchg_close) and its
 // consumer kernel checks (xchg_ok): RCCL on the stream, or the host transport
 // (which checks the guard itself as well, to fail at once)
-int shard_exchange(vg_ctx* ctx, int n) {
+int shard_exchange(vg_ctx* ctx, int n, hipStream_t s) {
   Shard& sh = ctx->shard;
+  if (!s) s = ctx->stream;
   if (sh.mode == 1) {
     const ncclResult_t r =
-        ncclAllReduce(sh.d_frame, sh.d_frame, (size_t)n, ncclFloat64, ncclSum, (ncclComm_t)sh.comm, ctx->stream);
+        ncclAllReduce(sh.d_frame, sh.d_frame, (size_t)n, ncclFloat64, ncclSum, (ncclComm_t)sh.comm, s);
     if (r != ncclSuccess) {
       ctx->err = std::string("ncclAllReduce: ") + ncclGetErrorString(r);
       return VG_E_HIP;
     }
     return VG_OK;
   }
-  VG_HIP(hipMemcpyAsync(sh.h_buf, sh.d_frame, (size_t)(n + 1) * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-  VG_HIP(stream_wait(ctx));
+  VG_HIP(hipMemcpyAsync(sh.h_buf, sh.d_frame, (size_t)(n + 1) * sizeof(double), hipMemcpyDeviceToHost, s));
+  VG_HIP(stream_wait(ctx, s));
   const double x = sh.h_buf[n];
   if (sh.host_fn(sh.h_buf, n, 0, sh.user) != 0) {
     ctx->err = "host all-reduce callback failed";
@@ -171,8 +172,8 @@ int shard_exchange(vg_ctx* ctx, int n) {
     return VG_E_STATE;
   }
   sh.h_buf[n] = x;
-  VG_HIP(hipMemcpyAsync(sh.d_frame, sh.h_buf, (size_t)(n + 1) * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-  VG_HIP(stream_wait(ctx));  // the staging buffer is reused by the next exchange
+  VG_HIP(hipMemcpyAsync(sh.d_frame, sh.h_buf, (size_t)(n + 1) * sizeof(double), hipMemcpyHostToDevice, s));
+  VG_HIP(stream_wait(ctx, s));  // the staging buffer is reused by the next exchange
   return VG_OK;
 }
 

@@ -337,7 +337,7 @@ constexpr int kShardSmall = 64;   // doubles of a small exchange frame (payload 
 // a frame its producer kernel packed and its consumer kernel checks (the IEKF
 // sums, the LM's Hessian and residual): the all-reduce alone, no pack / unpack
 // launches (shard.hip)
-int shard_exchange(vg_ctx* ctx, int n);
+int shard_exchange(vg_ctx* ctx, int n, hipStream_t s = nullptr);  // s: the producer's stream (default ctx->stream)
 struct Shard {
   int rank = 0, world = 1;
   int mode = 0;              // 0 none, 1 RCCL, 2 host callback
@@ -600,8 +600,8 @@ inline void prof_end(vg_ctx* c, int id, hipStream_t s = nullptr) {
 // Wait for the context stream by spinning on an event: a blocking
 // hipStreamSynchronize may sleep and costs up to ~100+ us of wake-up latency
 // per round trip, and the map stages make several per scan.
-inline hipError_t stream_wait(vg_ctx* c) {
-  hipError_t e = hipEventRecord(c->sync_ev, c->stream);
+inline hipError_t stream_wait(vg_ctx* c, hipStream_t s = nullptr) {
+  hipError_t e = hipEventRecord(c->sync_ev, s ? s : c->stream);
   if (e != hipSuccess) return e;
   const auto t0 = std::chrono::steady_clock::now();
   for (long spin = 0; (e = hipEventQuery(c->sync_ev)) == hipErrorNotReady; spin++) wait_pause(c, spin, t0);
