@@ -1303,13 +1303,15 @@ __global__ void __launch_bounds__(kHessThreads) k_ba_resid_hess(const int* __res
                                                                 CtlArg ctl) {
   const int G = kRhChunkWg;
   if (st->done) {  // converged: the bookkeeping still publishes the flags
-    if ((int)blockIdx.x == G) ba_control_body(ctl);
+    if (ctl.err && (int)blockIdx.x == G) ba_control_body(ctl);
     return;
   }
   if ((int)blockIdx.x == G) {  // IMU residuals at the trial state, then the bookkeeping (k_ba_resid's)
     if ((int)threadIdx.x < nimu) imu_residual_lane(threadIdx.x, imurec, *imu_head, bias, xt, imures);
-    __syncthreads();
-    resid_bookkeeping(ctl);
+    if (ctl.err) {  // (sharded: k_ba_rsum, the exchange and k_ba_control follow)
+      __syncthreads();
+      resid_bookkeeping(ctl);
+    }
     return;
   }
   if ((int)blockIdx.x > G) {  // the IMU factors' Hessian blocks at the trial (k_ba_hess's IMU workgroups)
@@ -1461,10 +1463,10 @@ __global__ void __launch_bounds__(kHessThreads) k_ba_init_hess(
     const double* __restrict__ bias, double* __restrict__ imuout, KClock* __restrict__ clk, BaState* st,
     double* __restrict__ hl, double* __restrict__ hl_part, int nout, MpRing ring, int* __restrict__ mpring,
     const int* __restrict__ rc_status, double* __restrict__ rpart, int nrb, const int* __restrict__ ph,
-    unsigned* __restrict__ rc_flag, int fin, DevMap m) {
+    unsigned* __restrict__ rc_flag, int fin, DevMap m, int seq0) {
   const int status = rc_status ? *rc_status : 0;
   if ((int)blockIdx.x == G + nimu) {
-    ba_init_common(threadIdx.x, blockDim.x, true, st, hl, hl_part, nout, ring, mpring, W, status, 0, rpart, nrb, ph,
+    ba_init_common(threadIdx.x, blockDim.x, true, st, hl, hl_part, nout, ring, mpring, W, status, seq0, rpart, nrb, ph,
                    rc_flag);
     return;
   }
@@ -1638,6 +1640,7 @@ const int* ba_gate_dev(vg_ctx* ctx) { return &carve(ctx).st->fin; }
 struct InitHessArg {
   MpRing ring;
   int fin;
+  int seq0;  // > 0: the LM's first flag number (a direct launch); 0: DState::ph (the scan graph)
 };
 static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr, int rh = 0,
                             const InitHessArg* ih = nullptr) {
@@ -1669,7 +1672,8 @@ static void ba_iter_kernels(vg_ctx* ctx, int k, bool solve_ev, int& xerr, int rh
     k_ba_init_hess<<<G + nimu + 1, kHessThreads, hess_lds, s>>>(
         nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr, ctx->map.pcrs, d.xs, d.part, G, nimu, d.imurec,
         &ctx->st->imu_head, d.bias, d.imuout, &ctx->st->clk, d.st, d.hl, ctx->ba.hout_part, nout, ih->ring, d.mpring,
-        map_rc_status(ctx), d.rpart, kResidBlocks, ctx->st->ph, ctx->d_sync + 3, ih->fin, ctx->map);
+        map_rc_status(ctx), d.rpart, kResidBlocks, ih->seq0 > 0 ? nullptr : ctx->st->ph,
+        ih->seq0 > 0 ? nullptr : ctx->d_sync + 3, ih->fin, ctx->map, ih->seq0);
   else if (rh != 2)
     k_ba_hess<<<G + nimu, kHessThreads, hess_lds, s>>>(nfp, W, ctx->ba.fac_node, ctx->ba.fac_eig, ctx->ba.fac_pcr,
                                                       ctx->map.pcrs, d.mpring, d.xs, d.part, d.st, G, nimu, d.imurec,
@@ -1742,6 +1746,7 @@ int ba_capture_scan_lm(vg_ctx* ctx, const int* mp_ring) {
     InitHessArg ih;
     for (int i = 0; i < kMaxW; i++) ih.ring.mp[i] = i < ctx->cfg.win_size ? mp_ring[i] : 0;
     ih.fin = ctx->rc_finish_in_init ? 1 : 0;
+    ih.seq0 = 0;
     ctx->rc_finish_in_init = false;
     ba_iter_kernels(ctx, 0, false, xerr, rh ? 1 : 0, &ih);
   } else {
@@ -1771,12 +1776,25 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   (void)nf;
   const bool shard_on = sharded(ctx);
   int seq0;
+  // sharded (direct launches, exchanges between): k_ba_init inside the first
+  // Hessian pass and the first residual pass forming the second iteration's
+  // Hessian, as the unsharded graphs do; the residual's bookkeeping stays in
+  // k_ba_control, behind the residual exchange
+  const bool shard_fused = shard_on && ctx->ba_init_hess && ctx->ba_resid_hess && resid_hess_ok(W);
+  InitHessArg ih;
   if (pre > 0) {
     seq0 = ctx->ba_seq0_pre;
   } else {
     seq0 = ctx->pub_seq + 1;
     ctx->pub_seq += 10;
-    ba_init_kernel(ctx, mp_ring, seq0);
+    if (shard_fused) {
+      for (int i = 0; i < kMaxW; i++) ih.ring.mp[i] = i < W ? mp_ring[i] : 0;
+      ih.fin = ctx->rc_finish_in_init ? 1 : 0;
+      ctx->rc_finish_in_init = false;
+      ih.seq0 = seq0;
+    } else {
+      ba_init_kernel(ctx, mp_ring, seq0);
+    }
     VG_HIP(flush_insert_events(ctx));
   }
   int xerr = VG_OK;  // exchange errors (sharded mode)
@@ -1784,7 +1802,10 @@ int ba_run(vg_ctx* ctx, int nf, const int* mp_ring, int* iters, const std::funct
   // that timing a long run costs the stream little (each record is a gap)
   const bool solve_ev = pre == 0 && ctx->prof_on && !ctx->prof_clock &&
                         (ctx->prof_every <= 1 || ctx->prof_runs++ % ctx->prof_every == 0);
-  auto enqueue = [&](int k) { ba_iter_kernels(ctx, k, solve_ev, xerr); };
+  auto enqueue = [&](int k) {
+    if (shard_fused && pre == 0 && k < 2) ba_iter_kernels(ctx, k, solve_ev, xerr, k + 1, k == 0 ? &ih : nullptr);
+    else ba_iter_kernels(ctx, k, solve_ev, xerr);
+  };
   const bool graph = ctx->use_graphs && ctx->ba_graph && !shard_on && !solve_ev && ctx->dbg_capture != 1;
   if (graph && !ctx->g_ba) {
     std::lock_guard<std::recursive_mutex> cap_lk_(capture_mutex());  // (vg_internal.h)

@@ -2673,19 +2673,33 @@ __global__ void k_make_win_recut_begin(DState* __restrict__ st, WinArg wa, const
 // leaves the status in rc[kRcStatus], where k_ba_init reads it: a recut that
 // needs the host-sized path (insert replay, level overflow, more factors than
 // max_fac) makes the LM skip, and the host completes the recut and reruns it.
+// xa.frame (sharded): the status goes out in the exchange frame (site 5),
+// closed here; k_pub_rc takes the sum
 __global__ void __launch_bounds__(1024) k_fac_sort(DevMap m, int* __restrict__ rc, uint32_t* __restrict__ bits,
                                                    int* __restrict__ fac_node, int cap_f, Pub* __restrict__ pub,
-                                                   int* __restrict__ seq_ctr, int max_fac, int publish) {
-  fac_sort_block(m, rc, bits, fac_node, cap_f, pub, seq_ctr, max_fac, publish != 0);
+                                                   int* __restrict__ seq_ctr, int max_fac, XchgArg xa) {
+  fac_sort_block(m, rc, bits, fac_node, cap_f, pub, seq_ctr, max_fac, xa.frame == nullptr);
+  if (xa.frame) {
+    for (int i = threadIdx.x + 1; i < xa.n - 2; i += blockDim.x) xa.frame[i] = 0.0;
+    if (threadIdx.x == 0) {  // (fac_sort_block's thread 0 wrote rc[kRcStatus])
+      xa.frame[0] = (double)rc[kRcStatus];
+      xchg_close(xa.frame, xa.n, 5, xa.seq);
+    }
+  }
 }
-// sharded mode: the recut status all-reduced over the ranks (rc[kRcStatus]),
-// so every rank's k_ba_init skips alike and every host takes the same
-// host-sized completion and LM rerun — the ranks' exchange sequences stay in
-// step. The factor count published is this rank's own.
-__global__ void k_pub_rc(const DevMap m, const int* __restrict__ rc, Pub* __restrict__ pub,
-                         const int* __restrict__ seq_ctr) {
+// sharded mode: the recut status summed over the ranks into rc[kRcStatus], so
+// every rank's k_ba_init skips alike and every host takes the same host-sized
+// completion and LM rerun — the ranks' exchange sequences stay in step (a
+// guard mismatch: error bit 32, VG_E_STATE with the scan's counters). The
+// factor count published is this rank's own.
+__global__ void k_pub_rc(const DevMap m, int* __restrict__ rc, Pub* __restrict__ pub, const int* __restrict__ seq_ctr,
+                         XchgArg xa) {
   if (threadIdx.x == 0) {
-    pub_store(&pub->rc_status, rc[kRcStatus]);
+    const bool ok = xchg_ok(xa.frame, xa.n, xa.world);
+    if (!ok) atomicOr(xa.err, 32);
+    const int status = ok ? (int)llrint(xa.frame[0]) : 0;
+    rc[kRcStatus] = status;
+    pub_store(&pub->rc_status, status);
     pub_store(&pub->rc_nf, m.counters[kCntFactors]);
     pub_flag(&pub->seq_rc, *seq_ctr);
   }
@@ -2883,11 +2897,13 @@ static int map_recut_impl(vg_ctx* ctx, const MP& mp, const WinArg& wa, int threa
   if (pub_seq > 0) {
     const int max_fac = (ctx->dbg_fac_max >= 0 && ctx->dbg_fac_max < kFacMax) ? ctx->dbg_fac_max : kFacMax;
     const bool shard_on = sharded(ctx);
+    Shard& sh = ctx->shard;
+    const XchgArg xa{shard_on ? sh.d_frame : nullptr, sh.d_seq, m.counters + kCntErr, kShardSmall, sh.world};
     k_fac_sort<<<1, 1024, 0, s>>>(m, w.rc, w.cand_bits, ctx->ba.fac_node, ctx->ba.cap_f, ctx->d_pub,
-                                  &ctx->st->rc_ctr, max_fac, shard_on ? 0 : 1);
+                                  &ctx->st->rc_ctr, max_fac, xa);
     if (shard_on) {
-      VG_TRY(shard_allreduce(ctx, w.rc + kRcStatus, w.rc + kRcStatus, 1, 1, 5));
-      k_pub_rc<<<1, 64, 0, s>>>(m, w.rc, ctx->d_pub, &ctx->st->rc_ctr);
+      VG_TRY(shard_exchange(ctx, kShardSmall));
+      k_pub_rc<<<1, 64, 0, s>>>(m, w.rc, ctx->d_pub, &ctx->st->rc_ctr, xa);
     }
     if (ctx->rc_init_finish) {  // the LM's k_ba_init (next on the stream) does tras_opt's bookkeeping
       ctx->rc_finish_in_init = true;
