@@ -10,6 +10,13 @@
 //   hdr96     one 96 B NodeHdr per lane, random permutation (the descent)
 //   gather8   one double per lane, random permutation over the whole array
 //   store16 / store8 / store4  coalesced stores of 16 / 8 / 4 B per lane
+//   fachess   k_ba_hess's reads: lane (f, i) of ten lanes per factor reads
+//             frame cluster i (80 B) of factor f's ten-cluster block (blocks in
+//             a random order, as factor nodes are) plus factor f's 96 B eigen
+//             record (all ten lanes the same address, records contiguous)
+//   storerun  k_ba_hess's old partial stores: runs of 16 doubles (128 B) at
+//             offsets 8 B past a 128 B boundary, four runs per wave, runs in a
+//             random order
 // Run under rocprofv3 --pmc FETCH_SIZE (then WRITE_SIZE) --kernel-trace;
 // scripts/fetch_cal.py divides the counters by the byte counts printed here.
 #include <hip/hip_runtime.h>
@@ -84,6 +91,26 @@ __global__ void k_gather8(const double* __restrict__ a, unsigned mask, float* __
     s += a[perm(i, mask)];
   if (s == 1234.5) sink[0] = (float)s;
 }
+struct Clu80 {
+  double v[10];
+};
+__global__ void k_fachess(const Clu80* __restrict__ clu, const double* __restrict__ eig, unsigned nf,
+                          unsigned gmask, float* __restrict__ sink) {
+  double s = 0.0;
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < nf * 10; t += gridDim.x * blockDim.x) {
+    const unsigned f = t / 10, i = t % 10;
+    const Clu80& c = clu[(size_t)perm(f, gmask) * 10 + i];
+    for (int k = 0; k < 10; k++) s += c.v[k];
+    for (int k = 0; k < 12; k++) s += eig[(size_t)f * 12 + k];
+  }
+  if (s == 1234.5) sink[0] = (float)s;
+}
+__global__ void k_storerun(double* __restrict__ a, unsigned rmask) {
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < (rmask + 1) * 16; t += gridDim.x * blockDim.x) {
+    const unsigned run = perm(t >> 4, rmask);
+    a[1 + (size_t)run * 16 + (t & 15)] = 0.0;
+  }
+}
 #define STORE_KERNEL(name, T)                                                                              \
   __global__ void name(T* __restrict__ a, size_t n) {                                                      \
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) \
@@ -129,6 +156,14 @@ int main() {
     flush();
     k_gather8<<<grid, blk>>>((const double*)A, nG - 1, sink);
     if (rep == 0) printf("k_gather8,%zu,0\n", (size_t)nG * 8);
+    const unsigned nF = 1u << 18;  // 256 k factors x (800 B clusters + 96 B eigen record) = 224 MiB
+    flush();
+    k_fachess<<<grid, blk>>>((const Clu80*)A, (const double*)(A + (size_t)nF * 800), nF, nF - 1, sink);
+    if (rep == 0) printf("k_fachess,%zu,0\n", (size_t)nF * 896);
+    const unsigned nRun = 1u << 20;  // 1 M runs x 128 B = 128 MiB (+8 B)
+    flush();
+    k_storerun<<<grid, blk>>>((double*)A, nRun - 1);
+    if (rep == 0) printf("k_storerun,0,%zu\n", (size_t)nRun * 128);
     flush();
     k_store16<<<grid, blk>>>((float4*)A, 256 * MB / 16);
     if (rep == 0) printf("k_store16,0,%zu\n", 256 * MB);

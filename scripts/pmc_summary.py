@@ -31,11 +31,17 @@ import bisect
 import csv
 import glob
 import json
+import math
 import os
 import sys
 from collections import defaultdict
 
 PLANE_B = 224.0
+
+
+def hess_chunk(W):
+    """factors per k_ba_hess chunk (ba.hip hess_fs, kHessThreads = 512)"""
+    return 2 * (256 // W) if 2 * (256 // W) <= 64 and 2 * (256 // W) <= 512 // W else min(512 // W, 64)
 
 
 def short(name):
@@ -142,7 +148,22 @@ def main(src, dst, first):
         if s >= first:
             pairs.append((fh[d], wh[d], S[s]["n_factors"] * (80.0 * W + 176.0)))
     assert all(0 <= s and per[s] <= S[s]["ba_hess"] for s in range(ns)), ("k_ba_hess launches per scan", per)
-    out["kernels"]["k_ba_hess"] = entry("launch (executed Hessian pass)", pairs, "F (80 W + 176) per pass")
+    e = entry("launch (executed Hessian pass)", pairs, "F (80 W + 176) per pass")
+    if cal and "k_fachess" in cal:  # the pass's own read shape (scripts/micro/fetch_cal.hip k_fachess)
+        exp = cal["k_fachess"] * e["alg_bytes"]
+        e["fetch_calibrated"] = {"expected_fetch_raw": round(exp), "measured_fetch_raw": e["fetch_raw_bytes"],
+                                 "ratio": round(e["fetch_raw_bytes"] / exp, 4),
+                                 "shape_ratios": {"fachess": cal["k_fachess"]}, "source": cal["_file"]}
+    # its own stores: the chunk partials (1,891 packed entries at W = 10) + the
+    # IMU blocks (931 doubles each); WRITE_SIZE also counts the write-back of
+    # earlier kernels' dirty lines evicted under the pass (the PMC run is
+    # serialised: k_ba_init's factor copies and the recut's records)
+    nl = 6 * W * (6 * W + 1) // 2 + 6 * W + 1
+    own = [math.ceil(S[s]["n_factors"] / hess_chunk(W)) * nl * 8.0 + (W - 1) * 931 * 8.0
+           for s in range(first, ns) for _ in range(per[s])]
+    if own:
+        e["own_store_bytes"] = round(sum(own) / len(own))
+    out["kernels"]["k_ba_hess"] = e
     # k_ba_solve: executed launches (traffic only)
     fs_, ws_ = fetch.get("k_ba_solve", []), write.get("k_ba_solve", [])
     ex = [i for i, v in enumerate(fs_) if v > 16.0]
