@@ -379,6 +379,8 @@ def main():
             r["fetch_calibrated"] = dict(e["fetch_calibrated"], note="measured FETCH_SIZE bytes (no x2) / the FETCH "
                                          "the algorithmic bytes produce at the calibrated per-shape ratios, same "
                                          "launches of the PMC pass")
+        if "own_store_bytes" in e:  # k_ba_hess: its own stores; WRITE_SIZE adds evicted dirty lines
+            r["own_store_bytes"] = e["own_store_bytes"]
     roof["stage_ms_per_scan"] = stage_ms
 
     h2d = None
