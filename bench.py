@@ -440,7 +440,14 @@ def main():
             "target_128line": targets or None, "multi_sequence": multi_roofline(multi, roof),
             "multi_sequence_1M": multi_1m, "env": {"GPU_MAX_HW_QUEUES": hwq, "VG_BENCH_DEBUG": dbg or None},
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
+        # a multi-sequence child that crashed is a defect, not a data point: the
+        # line above keeps what was measured (failed_by_B names the B), the exit
+        # status reports the failure
+        failed = {k: v.get("failed_by_B") for k, v in (("64line", multi), ("1M", multi_1m)) if v and v.get("failed_by_B")}
+        if failed:
+            print("bench: multi-sequence children failed: %s" % json.dumps(failed), file=sys.stderr, flush=True)
+            sys.exit(3)
     if world > 1:
         dist.destroy_process_group()
 
