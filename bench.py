@@ -83,16 +83,14 @@ def parse():
     ap.add_argument("--hash-log2", type=int, default=0, help="context capacity: root hash slots, log2 (0: default)")
     ap.add_argument("--multi", default="2,4,8,16",
                     help="multi-sequence mode (vg_multi_*): B values to time at N=1 (empty: skip); each B runs "
-                         "in ceil(B / --multi-group) child processes started before this one touches the GPU and "
-                         "released together; B distinct sequences")
+                         "in one child process started before this one touches the GPU, warmed up, then released; "
+                         "B distinct sequences")
     ap.add_argument("--multi-1m", default="1,2,4,8",
                     help="BASELINE config 5 (synthetic 1M-ray scans, batched): B values of the multi-sequence "
                          "mode on the 1M workload at N=1 (empty: skip)")
     ap.add_argument("--multi-1m-steps", type=int, default=10, help="timed scans per sequence of the 1M leg")
-    ap.add_argument("--multi-group", type=int, default=4, help="sequences per process in the multi-sequence legs")
     ap.add_argument("--multi-active", type=int, default=0,
-                    help="at most this many sequences on the device at once (vg_multi_set_active; 0: no cap); "
-                         "with a cap, every B runs in ONE process")
+                    help="at most this many sequences on the device at once (vg_multi_set_active; 0: no cap)")
     ap.add_argument("--multi-child", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--multi-scans", default="", help=argparse.SUPPRESS)
     ap.add_argument("--multi-max-points", type=int, default=0, help=argparse.SUPPRESS)
@@ -507,9 +505,9 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=Non
     sequences need, sequences end up sharing queues (measured: the same B = 4
     run at 1,100 or 3,300 scans/s depending on the streams created before it).
     Every context runs a distinct synthetic sequence (seed args.seq + b; no two
-    contexts read the same scan). GPU_MAX_HW_QUEUES (children only): 16 for
-    B <= --multi-group (a hardware queue per sequence stream), --multi-group
-    for larger B (the streams share that many queues: more busy queues are
+    contexts read the same scan). GPU_MAX_HW_QUEUES (children only): 16, a
+    hardware queue per stream. Past four sequences the library runs them on
+    four shared streams (vg_multi_create; more busy hardware queues are
     time-sliced by the GPU).
     """
     import subprocess
@@ -521,12 +519,12 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=Non
     total = warmup + steps
     paths = []
     out = {"lidar": lidar, "unit": "scans/s", "steps": steps, "warmup": warmup,
-           "workers": "one native thread + one stream per sequence", "inputs": "B distinct sequences",
+           "workers": "B <= 4: one native thread + one stream per sequence; B > 4: four streams, one thread "
+                      "each, stepping its sequences (b % 4) one scan each in turn (vg_multi_create)",
+           "inputs": "B distinct sequences",
            "wait_policy": "spin",
-           "process": "one process per B, released after its warm-up; B > %d: the B streams share %d hardware "
-                      "queues (GPU_MAX_HW_QUEUES)%s; rate = B x steps / (release -> end)"
-                      % (args.multi_group, args.multi_group,
-                         ", at most %d sequences on the device at once (vg_multi_set_active)" % args.multi_active
+           "process": "one process per B, released after its warm-up%s; rate = B x steps / (release -> end)"
+                      % (", at most %d sequences on the device at once (vg_multi_set_active)" % args.multi_active
                          if args.multi_active > 0 else ""),
            "env": {"GPU_MAX_HW_QUEUES": "16"},
            "by_B": {}}
@@ -554,7 +552,6 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=Non
         wait = os.environ.get("VG_MULTI_WAIT", "")  # experiments: "spin_us,sleep_us" (the line records it)
         if wait:
             out["wait_policy"] = "spin %s us, then sleep %s us" % tuple(wait.split(","))
-        grp = args.multi_group
         for B in Bs:
             # a child that fails (or crashes) costs this B its number, not the line
             runs = []
@@ -562,15 +559,18 @@ def multi_children(args, lidar, Bs, warmup, steps, workers, first=None, keep=Non
                 beat("multi-sequence %s: B = %d" % (lidar, B))
                 # the child warms up, reports READY and waits; the parent then
                 # releases it and times the job from GO to its end.
-                # B > grp: ONE process whose B streams share grp hardware queues
-                # (GPU_MAX_HW_QUEUES = grp): past ~4 hardware queues the GPU
+                # ONE process per B. Past ~4 busy hardware queues the GPU
                 # time-slices them (profiles/r04/multi_pmc_r04g.json: same L2 hit
-                # rates, a ~47 us floor per kernel at B = 8), and B = 8 / 16 over
-                # 4 shared queues ran 2,839 / 3,140 scans/s against 2,565 / ~2,250
-                # over private queues (profiles/r04/multi_hwq_r04.json)
+                # rates, a ~47 us floor per kernel at B = 8); past four
+                # sequences the library therefore shares four streams among
+                # them (B = 8: 3,837 scans/s against 2,970 over eight streams
+                # sharing four hardware queues, profiles/r06/multi_streams_r06.txt)
                 P = 1
-                benv = dict(env, GPU_MAX_HW_QUEUES=str(grp)) if B > grp else env
+                benv = env
                 out.setdefault("hw_queues_by_B", {})[str(B)] = int(benv["GPU_MAX_HW_QUEUES"])
+                ms = os.environ.get("VG_MULTI_STREAMS")
+                G = int(ms) if ms is not None else (4 if B > 4 else 0)
+                out.setdefault("streams_by_B", {})[str(B)] = G if 0 < G < B else B
                 sizes = [B // P + (1 if q < B % P else 0) for q in range(P)]
                 runs, first_seq = [], 0
                 for q in range(P):

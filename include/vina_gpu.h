@@ -394,8 +394,13 @@ int vg_set_wait_policy(vg_ctx* ctx, int spin_us, int sleep_us);
  * scans or none: after a worker's error it returns that status without
  * queuing (call vg_multi_sync before reading vg_last_error of the contexts).
  * With B > 1 the contexts run on one stream each while the multi object
- * exists; vg_multi_destroy gives each back its own downsample stream and the
- * IEKF / margi overlap. */
+ * exists; vg_multi_destroy gives each back its own stream, downsample stream
+ * and the IEKF / margi overlap. Past four sequences they share four streams
+ * (sequence b on stream b % 4, one worker thread per stream stepping its
+ * sequences one scan each in turn): MI355X time-slices more than about four
+ * busy hardware queues, and four shared streams keep B = 8 / 16 at B = 4's
+ * rate. The environment variable VG_MULTI_STREAMS = G overrides
+ * the count (G <= 0 or G >= B: one stream and one worker per sequence). */
 typedef struct vg_scan_dev {
   const float *d_x, *d_y, *d_z, *d_intensity, *d_time;
   int n;

@@ -30,18 +30,27 @@ def _ctx(p, seq):
     return c
 
 
-@pytest.mark.parametrize("lidar,B,cap,serial", [("16line", 3, 0, 0), ("64line", 2, 0, 0), ("16line", 8, 0, 0),
-                                                ("16line", 8, 4, 0), ("16line", 16, 0, 1)])
-def test_multi_sequences_match_lone_runs(lidar, B, cap, serial, monkeypatch):
+@pytest.mark.parametrize("lidar,B,cap,serial,streams", [("16line", 3, 0, 0, None), ("64line", 2, 0, 0, None),
+                                                        ("16line", 8, 0, 0, None), ("16line", 8, 0, 0, 0),
+                                                        ("16line", 8, 4, 0, None), ("16line", 16, 0, 1, None),
+                                                        ("16line", 16, 0, 1, 0), ("64line", 5, 0, 0, 2)])
+def test_multi_sequences_match_lone_runs(lidar, B, cap, serial, streams, monkeypatch):
     """B = 8 with cap 4 is the bench's form past four sequences (slots shared
     by two sequences each, vg_multi_set_active). B = 16 with
     VG_SERIAL_KERNELS=1: sixteen worker threads in the library's event-wait
     mode, the mode of round 5's B = 16 crash under the profiler (sixteen
     threads capturing and instantiating graphs at once; vg::capture_mutex
-    serialises that now)."""
+    serialises that now). streams (VG_MULTI_STREAMS): None = the library's
+    default (past four sequences they share four streams, one worker per
+    stream stepping its sequences in turn), 0 = one stream and one worker per
+    sequence, 2 = B = 5 over two streams (groups of three and two)."""
     import torch
     if serial:
         monkeypatch.setenv("VG_SERIAL_KERNELS", "1")
+    if streams is not None:
+        monkeypatch.setenv("VG_MULTI_STREAMS", str(streams))
+    else:
+        monkeypatch.delenv("VG_MULTI_STREAMS", raising=False)
     dev = torch.device("cuda", 0)
     p = vgconfig.load("mid360")
     g = p["General"]

@@ -1,10 +1,13 @@
-// multi.cpp — multi-sequence mode: B independent sequences on one GPU, each
-// context driven by its own native worker thread (BASELINE config 5, SURVEY §7
-// "Hard parts"). vg_multi_step_dev queues one scan per sequence and returns;
-// every worker runs its context's scans in order, free-running (no lock-step
-// between sequences), so the contexts' own streams (two each) overlap on the
-// device. Each worker runs exactly the single-sequence path (host_step), so
-// every sequence's results are those of a lone context, bit for bit.
+// multi.cpp — multi-sequence mode: B independent sequences on one GPU
+// (BASELINE config 5, SURVEY §7 "Hard parts"). Up to four sequences: each
+// context on its own stream, driven by its own native worker thread; past
+// four, the sequences share four streams, one worker per stream stepping its
+// sequences one scan each in turn (a graph capture then never meets another
+// thread's work on its stream). vg_multi_step_dev queues one scan per sequence
+// and returns; the workers run free (no lock-step between streams), so the
+// streams overlap on the device. Each worker runs exactly the single-sequence
+// path (host_step), so every sequence's results are those of a lone context,
+// bit for bit.
 //
 // Why threads and not one launch for B sequences: the per-scan path is ~90
 // small dependent kernels whose cost is dispatch + cross-XCD memory latency,
@@ -21,6 +24,7 @@
 #include "vg_host.h"
 
 namespace {
+constexpr int kMultiStreams = 4;  // default shared streams past this many sequences
 struct Job {
   vg_scan_dev sc;
   std::vector<double> imu;  // the scan's IMU samples (the caller's buffer may be reused)
@@ -54,53 +58,72 @@ struct vg_multi {
   std::vector<char> slot_busy;  // sequence b runs in slot b % cap (its stream shares a hardware queue with
                                 // the other sequences of that slot when GPU_MAX_HW_QUEUES = cap)
   std::condition_variable cv_slot;
+  // Shared streams (VG_MULTI_STREAMS = G < B): sequence b runs on stream
+  // b % G, driven by worker b % G, which steps its sequences one scan each in
+  // turn. G busy hardware queues instead of B time-sliced ones; one thread per
+  // stream, so a graph capture never sees another thread's work on it.
+  int groups = 0;                 // 0: one stream + one worker per sequence
+  std::vector<hipStream_t> own;   // each context's own stream (restored on destroy)
 };
 
-static void worker(vg_multi* M, int b) {
-  for (;;) {
-    Job j;
-    {
-      std::unique_lock<std::mutex> lk(M->mu);
-      M->cv_job.wait(lk, [&] { return M->quit || !M->wk[b].q.empty(); });
-      if (M->wk[b].q.empty()) return;  // quit with nothing left
-      j = std::move(M->wk[b].q.front());
-      M->wk[b].q.pop_front();
-      M->busy++;
-    }
-    M->cv_room.notify_all();
-    vg_ctx* c = M->ctx[b];
-    const vg_scan_dev& sc = j.sc;
-    const double* imu = j.imu.empty() ? nullptr : j.imu.data();
-    const bool capped = M->cap > 0;
-    const int slot = capped ? b % M->cap : 0;
-    if (capped) {
-      std::unique_lock<std::mutex> lk(M->mu);
-      M->cv_slot.wait(lk, [&] { return !M->slot_busy[slot]; });
-      M->slot_busy[slot] = 1;
-      M->active++;
-    }
-    int r;
-    if (sc.d_time)
-      r = vg_step_deskew_dev(c, sc.d_x, sc.d_y, sc.d_z, sc.d_intensity, sc.d_time, sc.n, sc.pcl_beg_time,
-                             sc.pcl_end_time, imu, sc.m);
-    else
-      r = vg_step_dev(c, sc.d_x, sc.d_y, sc.d_z, sc.d_intensity, sc.n, sc.pcl_beg_time, sc.pcl_end_time, imu, sc.m);
-    if (capped) {  // the scan's device work done before the slot goes to another sequence
-      const int r2 = vg::host_sync(c);
-      if (r == VG_OK) r = r2;
-      {
-        std::lock_guard<std::mutex> lk(M->mu);
-        M->slot_busy[slot] = 0;
-        M->active--;
-      }
-      M->cv_slot.notify_all();
-    }
+// one queued scan of sequence b (busy already counted)
+static void run_job(vg_multi* M, int b, Job& j) {
+  vg_ctx* c = M->ctx[b];
+  const vg_scan_dev& sc = j.sc;
+  const double* imu = j.imu.empty() ? nullptr : j.imu.data();
+  const bool capped = M->cap > 0;
+  const int slot = capped ? b % M->cap : 0;
+  if (capped) {
+    std::unique_lock<std::mutex> lk(M->mu);
+    M->cv_slot.wait(lk, [&] { return !M->slot_busy[slot]; });
+    M->slot_busy[slot] = 1;
+    M->active++;
+  }
+  int r;
+  if (sc.d_time)
+    r = vg_step_deskew_dev(c, sc.d_x, sc.d_y, sc.d_z, sc.d_intensity, sc.d_time, sc.n, sc.pcl_beg_time,
+                           sc.pcl_end_time, imu, sc.m);
+  else
+    r = vg_step_dev(c, sc.d_x, sc.d_y, sc.d_z, sc.d_intensity, sc.n, sc.pcl_beg_time, sc.pcl_end_time, imu, sc.m);
+  if (capped) {  // the scan's device work done before the slot goes to another sequence
+    const int r2 = vg::host_sync(c);
+    if (r == VG_OK) r = r2;
     {
       std::lock_guard<std::mutex> lk(M->mu);
-      if (r != VG_OK && M->wk[b].rc == VG_OK) M->wk[b].rc = r;
-      M->busy--;
+      M->slot_busy[slot] = 0;
+      M->active--;
     }
-    M->cv_room.notify_all();
+    M->cv_slot.notify_all();
+  }
+  {
+    std::lock_guard<std::mutex> lk(M->mu);
+    if (r != VG_OK && M->wk[b].rc == VG_OK) M->wk[b].rc = r;
+    M->busy--;
+  }
+  M->cv_room.notify_all();
+}
+
+// worker g: sequences g, g + G, ... (G = groups, or one sequence when 0), one
+// scan each in turn; returns on quit once its queues are empty
+static void worker(vg_multi* M, int g) {
+  const int B = (int)M->ctx.size(), G = M->groups > 0 ? M->groups : B;
+  for (;;) {
+    bool any = false;
+    for (int b = g; b < B; b += G) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(M->mu);
+        M->cv_job.wait(lk, [&] { return M->quit || !M->wk[b].q.empty(); });
+        if (M->wk[b].q.empty()) continue;  // quit with nothing left for this sequence
+        j = std::move(M->wk[b].q.front());
+        M->wk[b].q.pop_front();
+        M->busy++;
+      }
+      any = true;
+      M->cv_room.notify_all();
+      run_job(M, b, j);
+    }
+    if (!any) return;
   }
 }
 
@@ -131,7 +154,27 @@ vg_multi* vg_multi_create(vg_ctx** ctxs, int B, int spin_us, int sleep_us) {
       }
     }
   }
-  for (int b = 0; b < B; b++) M->th.emplace_back(worker, M, b);
+  // shared streams past four sequences (vina_gpu.h; measured in
+  // profiles/r06/multi_streams_r06.txt: B = 8 3,837 scans/s on four shared
+  // streams against 2,970 on eight, B = 4 3,824)
+  const char* gs = getenv("VG_MULTI_STREAMS");
+  const int G = gs ? atoi(gs) : (B > kMultiStreams ? kMultiStreams : 0);
+  if (B > 1 && G > 0 && G < B) {  // sequence b on sequence (b % G)'s stream
+    M->groups = G;
+    M->own.resize(B);
+    for (int b = 0; b < B; b++) {
+      vg_ctx* c = ctxs[b];
+      (void)hipStreamSynchronize(c->stream);  // (its seed / setup work)
+      M->own[b] = c->stream;
+    }
+    for (int b = G; b < B; b++) {
+      vg_ctx* c = ctxs[b];
+      c->stream = M->own[b % G];
+      c->stream_ds = c->stream;
+    }
+  }
+  const int nw = M->groups > 0 ? M->groups : B;
+  for (int g = 0; g < nw; g++) M->th.emplace_back(worker, M, g);
   return M;
 }
 
@@ -205,6 +248,10 @@ void vg_multi_destroy(vg_multi* M) {
   for (size_t b = 0; b < M->ctx.size(); b++) {
     vg_ctx* c = M->ctx[b];
     (void)hipStreamSynchronize(c->stream);
+    if (!M->own.empty()) {  // back on its own stream
+      c->stream = M->own[b];
+      c->stream_ds = c->stream;
+    }
     if (M->split[b] & 2) c->want_ds_stream = true;  // made again on the next scan (stage_downsample)
     if (M->split[b] & 1) c->overlap_iekf = true;
   }
