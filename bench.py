@@ -381,32 +381,51 @@ def main():
             r["own_store_bytes"] = e["own_store_bytes"]
     roof["stage_ms_per_scan"] = stage_ms
 
+    # the legs after the metric's: a leg that fails records its error in the
+    # line (which still prints, with the metric) and the exit status reports it
+    leg_errors = {}
+
+    def leg(name, fn):
+        try:
+            return fn()
+        except Exception as ex:  # noqa: BLE001
+            leg_errors[name] = "%s: %s" % (type(ex).__name__, str(ex)[-300:])
+            beat("%s failed: %s" % (name, leg_errors[name]))
+            return {"error": leg_errors[name]}
+
     h2d = None
     if world == 1 and not args.no_h2d:
         beat("host-input leg")
-        h2d = host_input_rate(p, seq, host_scans, imus, warmup, args.steps, dev)
+        h2d = leg("host_input", lambda: host_input_rate(p, seq, host_scans, imus, warmup, args.steps, dev))
     tile1 = None
     if world == 1 and not args.no_tile1:
         beat("sharded-path leg on one GPU")
-        tile1 = tile_path_rate(p, seq, scans, imus, warmup, args.steps, dev, value)
+        tile1 = leg("tile_path_1gpu", lambda: tile_path_rate(p, seq, scans, imus, warmup, args.steps, dev, value))
     cpu, ate_cpu = None, None
     if cpu_on:
         beat("CPU baseline: %d + %d scans, 5 threads then 1" % (args.cpu_warmup, args.cpu_scans))
-        cpu, traj_cpu = cpu_baseline(args, p, seq, host_scans)
-        lo, hi = args.cpu_warmup, min(traj_cpu.shape[0], traj_gpu.shape[0])
-        if hi > lo:
-            d = np.linalg.norm(traj_cpu[lo:hi, 10:13] - traj_gpu[lo:hi, 10:13], axis=1)
-            ate_cpu = {"ate_m": float("%.3e" % np.sqrt(np.mean(d ** 2))), "max_m": float("%.3e" % d.max()),
-                       "scans": hi - lo, "first_scan": lo,
-                       "reference": "CPU restatement, 5 threads, the CPU baseline's own scans",
-                       "tolerance_m": 0.01}
+        res = leg("cpu_baseline", lambda: cpu_baseline(args, p, seq, host_scans))
+        if isinstance(res, dict):
+            cpu = res
+        else:
+            cpu, traj_cpu = res
+            lo, hi = args.cpu_warmup, min(traj_cpu.shape[0], traj_gpu.shape[0])
+            if hi > lo:
+                d = np.linalg.norm(traj_cpu[lo:hi, 10:13] - traj_gpu[lo:hi, 10:13], axis=1)
+                ate_cpu = {"ate_m": float("%.3e" % np.sqrt(np.mean(d ** 2))), "max_m": float("%.3e" % d.max()),
+                           "scans": hi - lo, "first_scan": lo,
+                           "reference": "CPU restatement, 5 threads, the CPU baseline's own scans",
+                           "tolerance_m": 0.01}
     targets = {}
     for cfg, sc in tgt_scans.items():
         beat("128-line target workload (%s)" % cfg)
-        targets[cfg] = target_workload(args, cfg, sc, warmup, dev)
+        targets[cfg] = leg("target_128line." + cfg, lambda: target_workload(args, cfg, sc, warmup, dev))
+    w1 = None
     if multi_1m and scans_1m:
         beat("1M workload: single-context roofline")
-        w1 = target_workload(args, args.config, scans_1m, warmup, dev, lidar="1M")
+        w1 = leg("multi_sequence_1M.single_context",
+                 lambda: target_workload(args, args.config, scans_1m, warmup, dev, lidar="1M"))
+    if w1 and "error" not in w1:
         multi_1m["bytes_per_scan"] = w1["bytes_per_scan"]
         multi_1m["counters_mean"] = w1["counters_mean"]
         multi_1m["single_context"] = {k: w1[k] for k in ("value", "ms_per_step", "steps", "achieved", "frac")}
@@ -445,6 +464,9 @@ def main():
         failed = {k: v.get("failed_by_B") for k, v in (("64line", multi), ("1M", multi_1m)) if v and v.get("failed_by_B")}
         if failed:
             print("bench: multi-sequence children failed: %s" % json.dumps(failed), file=sys.stderr, flush=True)
+        if leg_errors:
+            print("bench: legs failed: %s" % json.dumps(leg_errors), file=sys.stderr, flush=True)
+        if failed or leg_errors:
             sys.exit(3)
     if world > 1:
         dist.destroy_process_group()
