@@ -408,6 +408,9 @@ __global__ void __launch_bounds__(256) k_iekf(MP mp, DState* __restrict__ st, in
                                               int* __restrict__ cache, double* __restrict__ partials,
                                               int* __restrict__ pk) {
   if (st->done) return;
+  // the scan's critical chain: its waves issue ahead of co-resident waves of
+  // the previous scan's margi remainder (k_margi_copy) on a shared SIMD
+  __builtin_amdgcn_s_setprio(2);
   const bool clk_on = st->clk.on != 0;
   const int clk_slot = (st->clk.scan * 4 + it) & (kClkRing - 1);
   if (clk_on && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -482,6 +485,7 @@ __global__ void __launch_bounds__(1024) k_iekf_update(int nb, const double* __re
                                                      int xworld, int* xerr) {
   __shared__ IekfLds L;
   if (st->done) return;
+  __builtin_amdgcn_s_setprio(2);  // (k_iekf)
   iekf_update_block(nb, partials, st, it, L, xworld, xerr);
   if (done_flag && L.fin) iekf_signal_done(done_flag);
 }
