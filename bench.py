@@ -185,10 +185,20 @@ def main():
     import torch.distributed as dist
 
     import vgpu
+    # VG_BENCH_REHEARSE=1 (replica mode only): the N > 1 flow on a box with
+    # fewer GPUs than ranks — every rank on GPU local % count, gloo instead of
+    # RCCL for the barriers and the max over ranks (scripts/gpu_rehearse.sh);
+    # never part of a reported line
+    rehearse = world > 1 and os.environ.get("VG_BENCH_REHEARSE") == "1" and not tile
+    if rehearse:
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
         with _StdoutToStderr():  # (RCCL's banner)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            if rehearse:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
             dist.barrier()
     dev = torch.device("cuda", local)
     seq = synth.Sequence(args.lidar, seq_id, blind=g["blind"], ext_R=g["extrinsic_rota"], ext_t=g["extrinsic_tran"])
@@ -456,6 +466,8 @@ def main():
             "ate_vs_cpu": ate_cpu,
             "target_128line": targets or None, "multi_sequence": multi_roofline(multi, roof),
             "multi_sequence_1M": multi_1m, "env": {"GPU_MAX_HW_QUEUES": hwq, "VG_BENCH_DEBUG": dbg or None},
+            **({"rehearsal": "VG_BENCH_REHEARSE: %d ranks on %d GPU(s) over gloo, not a measurement"
+                % (world, torch.cuda.device_count())} if rehearse else {}),
         }
         print(json.dumps(line), flush=True)
         # a multi-sequence child that crashed is a defect, not a data point: the
@@ -874,7 +886,8 @@ def aggregate(dt, steps, world, dev):
     if world > 1:
         import torch
         import torch.distributed as dist
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        on_cpu = dist.get_backend() == "gloo"  # (the rehearsal)
+        tt = torch.tensor([dt], device="cpu" if on_cpu else dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     return world * steps / dt, dt
