@@ -191,52 +191,61 @@ __device__ __forceinline__ void iekf_update_tail(DState* __restrict__ st, int it
       for (int r = 0; r < 6; r++)
         if (r != c && pc[r] != 0.0) col[r] -= pc[r] * cv;
     }
-    if (lane >= 6 && lane < 21)
-      for (int r = 0; r < 6; r++) L.K6[lane - 6][r] = col[r];
-  }
-  __syncthreads();
-  VG_PROBE_MARK(25);
-  // G6 = K6 * HTH
-  if (tid < 90) {
-    const int r = tid / 6, c = tid % 6;
-    double s = L.K6[r][0] * hth(0, c);
-    for (int k = 1; k < 6; k++) s += L.K6[r][k] * hth(k, c);
-    L.G6[r][c] = s;
-    st->G6[r * 6 + c] = s;
-  }
-  if (tid == 128 && !vec_done) iekf_vec(st, L);  // (iekf_update_block: computed beside the sum)
-  __syncthreads();
-  if (tid < 15) {  // sol = (K6 HTz + vec) - G6 v6
-    double s1 = L.K6[tid][0] * o[21];
-    for (int k = 1; k < 6; k++) s1 += L.K6[tid][k] * o[21 + k];
-    double s2 = L.G6[tid][0] * L.vec[0];
-    for (int k = 1; k < 6; k++) s2 += L.G6[tid][k] * L.vec[k];
-    L.sol[tid] = (s1 + L.vec[tid]) - s2;
-  }
-  __syncthreads();
-  VG_PROBE_MARK(26);
-  if (tid == 0) {  // x_curr ⊞= sol (types.hpp:67-78); convergence / rematch (odometry.cpp:205-227)
-    double* xc = st->xc;
-    const double* sol = L.sol;
-    const M3 Rn = mul(ld_m3(xc), Exp(v3(sol[0], sol[1], sol[2])));
-    for (int k = 0; k < 9; k++) xc[k] = Rn[k];
-    double pn[3];
-    for (int k = 0; k < 3; k++) {
-      pn[k] = xc[9 + k] + sol[3 + k];
-      xc[9 + k] = pn[k];
-      xc[12 + k] += sol[6 + k];
-      xc[15 + k] += sol[9 + k];
-      xc[18 + k] += sol[12 + k];
+    if (!vec_done) {  // (iekf_update_block computes it beside the sum)
+      if (lane == 63) iekf_vec(st, L);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    const double rot_add = norm3(v3(sol[0], sol[1], sol[2])), tra_add = norm3(v3(sol[3], sol[4], sol[5]));
-    const bool conv = (rot_add * 57.3 < 0.01) && (tra_add * 100 < 0.015);
-    int rm = st->rematch;
-    if (conv || ((rm == 0) && (it == 4 - 2))) rm++;
-    st->rematch = rm;
-    L.fin = (rm >= 2 || it == 4 - 1) ? 1 : 0;
-    if (L.fin) {  // the trajectory row (the pose the IEKF ends at), from registers
-      for (int k = 0; k < 9; k++) st->traj[k] = Rn[k];
-      for (int k = 0; k < 3; k++) st->traj[9 + k] = pn[k];
+    // G6 = K6 HTH and sol = (K6 HTz + vec) - G6 v6 on the lanes that hold K6's
+    // rows (lane 6 + r: row r), in the same operation order as a separate
+    // pass would take them from LDS, so no workgroup barrier sits between
+    // the 6 x 6 solve and the state update
+    if (lane >= 6 && lane < 21) {
+      const int r = lane - 6;
+      double g[6];
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        double sv = col[0] * hth(0, c);
+        for (int k = 1; k < 6; k++) sv += col[k] * hth(k, c);
+        g[c] = sv;
+        L.G6[r][c] = sv;
+        st->G6[r * 6 + c] = sv;
+      }
+      double s1 = col[0] * o[21];
+      for (int k = 1; k < 6; k++) s1 += col[k] * o[21 + k];
+      double s2 = g[0] * L.vec[0];
+      for (int k = 1; k < 6; k++) s2 += g[k] * L.vec[k];
+      L.sol[r] = (s1 + L.vec[r]) - s2;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // lane 0 reads every row's sol
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    VG_PROBE_MARK(25);
+    VG_PROBE_MARK(26);
+    if (lane == 0) {  // x_curr ⊞= sol (types.hpp:67-78); convergence / rematch (odometry.cpp:205-227)
+      double* xc = st->xc;
+      const double* sol = L.sol;
+      const M3 Rn = mul(ld_m3(xc), Exp(v3(sol[0], sol[1], sol[2])));
+      for (int k = 0; k < 9; k++) xc[k] = Rn[k];
+      double pn[3];
+      for (int k = 0; k < 3; k++) {
+        pn[k] = xc[9 + k] + sol[3 + k];
+        xc[9 + k] = pn[k];
+        xc[12 + k] += sol[6 + k];
+        xc[15 + k] += sol[9 + k];
+        xc[18 + k] += sol[12 + k];
+      }
+      const double rot_add = norm3(v3(sol[0], sol[1], sol[2])), tra_add = norm3(v3(sol[3], sol[4], sol[5]));
+      const bool conv = (rot_add * 57.3 < 0.01) && (tra_add * 100 < 0.015);
+      int rm = st->rematch;
+      if (conv || ((rm == 0) && (it == 4 - 2))) rm++;
+      st->rematch = rm;
+      L.fin = (rm >= 2 || it == 4 - 1) ? 1 : 0;
+      if (L.fin) {  // the trajectory row (the pose the IEKF ends at), from registers
+        for (int k = 0; k < 9; k++) st->traj[k] = Rn[k];
+        for (int k = 0; k < 3; k++) st->traj[9 + k] = pn[k];
+      }
     }
   }
   __syncthreads();
